@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Benchmark: GiB/s of CRC-32 over device-resident blocks on MI355X (BASELINE.json metric).
+
+Workload per GPU (N=1 line = BASELINE configs[1]): 1 M x 4 KiB blocks = 4 GiB of
+synthetic data (splitmix64 generator, seed 1) resident in HBM; one step = one launch of the batch
+CRC kernel over the whole batch (every block checksummed, results written to HBM). With
+--gpus N (torch.distributed.run, one rank per GPU) every rank checksums its own 1 M blocks
+(global block ids rank*1M ...): weak scaling, no collective on the data path; the only collectives
+are the timing barrier and the max-over-ranks reduction.
+
+Prints one JSON line (rank 0). Extra fields: roofline (dominant kernel: algorithmic bytes per
+launch / HIP-event launch time vs 8 TB/s HBM peak), cpu_baseline (the reference's own crc32.cpp
+compiled from /root/reference into oracle/_ref, or the oracle port, on host cores over the same
+buffers), bit_exact (this run's CRCs vs the oracle / golden aggregates).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (nblocks, block_len, description) — BASELINE.json configs
+    "cfg2": (1 << 20, 4096, "1 M x 4 KiB WAL-record-sized blocks, device-resident"),
+    "cfg3": (1 << 18, 65536, "256 K x 64 KiB SSTable data blocks, device-resident"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def load_oracle():
+    o = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+    o.oracle_crc_synthetic.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_void_p]
+    return o
+
+
+def cpu_baseline(host, nblocks, blen, seconds_target=8.0):
+    """Time the reference crc32 (oracle/_ref, else the oracle port) on host cores over a bounded
+    contiguous sample of the batch's own bytes; contiguous per-thread block ranges."""
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libref_crc32.so")
+    if os.path.exists(ref_path):
+        lib = ctypes.CDLL(ref_path)
+        fn = lib.ref_crc32_blocks
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
+        kind = "reference"
+    else:
+        lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+        fn = None
+        kind = "port"
+
+    def run(lo, hi, out):
+        if fn is not None:
+            fn(host.ctypes.data + lo * blen, blen, blen, hi - lo, out.ctypes.data + lo * 4)
+        else:
+            lib.oracle_crc_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p]
+            offs = (np.arange(lo, hi, dtype=np.uint64) * blen)
+            lens = np.full(hi - lo, blen, np.uint32)
+            lib.oracle_crc_batch(host.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, hi - lo,
+                                 out.ctypes.data + lo * 4)
+
+    cores = max(1, min(len(os.sched_getaffinity(0)), 16))  # the GPU box's CPU share is 16
+    out = np.zeros(nblocks, np.uint32)
+    # calibrate on 1 thread, then size the all-core sample to ~seconds_target of wall time
+    t0 = time.perf_counter()
+    cal = min(nblocks, 4096)
+    run(0, cal, out)
+    per_block = (time.perf_counter() - t0) / cal
+    one_core_gibs = cal * blen / (1 << 30) / max(per_block * cal, 1e-9)
+    sample = int(min(nblocks, max(cores * 1024, seconds_target * cores / max(per_block, 1e-12))))
+    step = (sample + cores - 1) // cores
+    ths = [threading.Thread(target=run, args=(i * step, min(sample, (i + 1) * step), out)) for i in range(cores)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dt = time.perf_counter() - t0
+    return {"value": round(sample * blen / (1 << 30) / dt, 4), "unit": "GiB/s", "cores": cores, "kind": kind,
+            "sample": f"first {sample} of the {nblocks} x {blen} B blocks (same bytes as the GPU run), "
+                      f"{cores} threads, contiguous block ranges, {dt:.2f} s wall",
+            "one_core_gibs": round(one_core_gibs, 4)}, out[:sample]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-csv", default=None,
+                    help="rocprofv3 --pmc counter_collection.csv (FETCH_SIZE) of this command, for roofline.traffic")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import tinykvpp_amd as tk
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    tk.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    nblocks, blen, desc = CONFIGS[args.config]
+    first = rank * nblocks  # weak scaling: every rank owns its own nblocks blocks
+    data = torch.empty(nblocks * blen, dtype=torch.uint8, device=dev)
+    out = torch.empty(nblocks, dtype=torch.int32, device=dev)
+    tk.fill_synthetic_uniform(data, blen, nblocks, first_block=first)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        tk.crc32_batch_uniform(data, blen, nblocks, out=out)
+    torch.cuda.synchronize()
+
+    # correctness of this exact buffer (checked outside the timed region)
+    crcs = out.cpu().numpy().view(np.uint32).copy()
+    ora = load_oracle()
+    probe = np.zeros(64, np.uint32)
+    ora.oracle_crc_synthetic(1, first, 64, blen, probe.ctypes.data)
+    bit_exact = bool(np.array_equal(crcs[:64], probe))
+    if rank == 0 and world == 1:
+        with open(os.path.join(ROOT, "tests", "golden", "synthetic.json")) as f:
+            g = json.load(f)[args.config]
+        bit_exact = bit_exact and int(np.bitwise_xor.reduce(crcs)) == g["xor"]
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        tk.crc32_batch_uniform(data, blen, nblocks, out=out, stream=stream)
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+        ok = torch.tensor([1 if bit_exact else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        bit_exact = bool(ok.item())
+
+    bytes_per_step = nblocks * blen
+    total_bytes = bytes_per_step * args.steps * world
+    value = total_bytes / (1 << 30) / elapsed
+    achieved = bytes_per_step / (kernel_ms * 1e-3) / 1e9
+
+    traffic = None
+    if args.traffic_csv and os.path.exists(args.traffic_csv):
+        import csv
+        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(args.traffic_csv))
+                if r.get("Counter_Name") == "FETCH_SIZE" and "crc_rows" in r.get("Kernel_Name", "")]
+        if vals:  # FETCH_SIZE is KiB and reads 1/2 of a wide streaming read on gfx950 (MI355X_MICROARCH §HBM)
+            traffic = float(np.median(vals)) * 1024 * 2
+
+    line = {
+        "metric": "GiB/s CRC32 over device-resident blocks (4 KiB & 64 KiB) on 1 MI355X",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (SURVEY §8d splitmix64 generator, seed 1), generated in HBM",
+        "config": {"workload": f"{args.config}: {desc}", "blocks_per_gpu": nblocks, "block_bytes": blen,
+                   "bytes_per_gpu_per_step": bytes_per_step, "parallelism": f"batch split x{world}, no collective"},
+        "bit_exact": bit_exact,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
+                     "algorithmic_bytes_per_launch": bytes_per_step},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        host = data.cpu().numpy()
+        cb, cpu_crcs = cpu_baseline(host, nblocks, blen)
+        cb["agrees_with_gpu"] = bool(np.array_equal(cpu_crcs, crcs[:cpu_crcs.size]))
+        line["cpu_baseline"] = cb
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

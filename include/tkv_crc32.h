@@ -1,0 +1,127 @@
+/*
+ * tkv_crc32.h — C ABI of the MI355X CRC-32 block-checksum engine (libtkv_crc32.so).
+ *
+ * Drop-in boundary for tinykvpp's integrity hot path: the CRC-32/ISO-HDLC routine
+ * frankie::core::crc32 (/root/reference/src/core/crc32.hpp:32-49, crc32.cpp:9-22) and the call
+ * sites that stamp/verify WAL records (/root/reference/src/engine/wal.cpp:54-58, 89-96).
+ * Plain C: pointers, sizes and integer status codes only. Every checksum is computed by the HIP
+ * kernels for gfx950; the library has no CPU implementation of the CRC and reports an error when
+ * no GPU is usable.
+ *
+ * State conventions (match crc32.hpp:37-46):
+ *   "raw" register  = the value crc32::crc_ holds (init 0xFFFFFFFF, no xorout applied);
+ *   "final" value   = crc32::finalize() = raw ^ 0xFFFFFFFF.
+ *
+ * Stream arguments are hipStream_t passed as void* (NULL = the legacy default stream).
+ */
+#ifndef TKV_CRC32_H
+#define TKV_CRC32_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes mirror frankie::core::status_code (/root/reference/src/core/status.hpp:11-20). */
+enum tkv_status {
+  TKV_OK = 0,
+  TKV_NOT_FOUND = 1,
+  TKV_IO_ERROR = 2,          /* HIP runtime failure (no device, launch or copy error) */
+  TKV_INVALID_ARGUMENT = 3,
+  TKV_CORRUPTED = 4,         /* a verified checksum did not match (wal.cpp:93-96) */
+  TKV_EOF = 5,
+  TKV_OUT_OF_MEMORY = 6,
+  TKV_BUFFER_OVERFLOW = 7
+};
+
+#define TKV_CRC32_DEFAULT_RAW 0xFFFFFFFFu /* crc32.hpp:9 kCRC32DefaultValue */
+#define TKV_CRC32_POLYNOMIAL 0xEDB88320u  /* crc32.hpp:11 kCRC32Polynomial */
+
+/* ---- library / device management -------------------------------------------------------------- */
+
+/* Number of usable GPUs (0 when the HIP runtime finds none). */
+int tkv_device_count(void);
+
+/* Bind the calling thread to `device` and create that device's context (tables, scratch) if needed.
+ * Every other entry point uses the calling thread's current device. */
+int tkv_set_device(int device);
+
+/* Human-readable text of the last error on this thread ("" if none). */
+const char *tkv_last_error(void);
+
+/* ---- crc32::update replacement ---------------------------------------------------------------- */
+
+/* Continue raw register `raw_state` over `len` bytes of HOST memory; writes the new raw register.
+ * Replaces crc32::update (crc32.hpp:37, crc32.cpp:9-16); finalize is raw ^ 0xFFFFFFFF
+ * (crc32.cpp:19) and reset is raw = 0xFFFFFFFF (crc32.cpp:22). Synchronous (stages through the
+ * GPU; the right tool for one span is the batch API). */
+int tkv_crc32_update(uint32_t raw_state, const void *data, size_t len, uint32_t *out_raw);
+
+/* Same over DEVICE memory, asynchronous on `stream`; *d_out_raw is written on the device. */
+int tkv_crc32_update_device(uint32_t raw_state, const void *d_data, size_t len, uint32_t *d_out_raw,
+                            void *stream);
+
+/* ---- batch APIs (new: the reference has only per-record calls, wal.cpp:54-57,89-92) ------------ */
+
+/* Irregular batch in device memory: block i is [d_base + d_offsets[i], + d_lengths[i]) (any
+ * alignment, any length, blocks may overlap). d_out_final[i] = finalize() of the block continued
+ * from d_init_raw[i] (NULL: every block starts from 0xFFFFFFFF). Asynchronous on `stream`; d_* must
+ * stay valid until the stream has completed. */
+int tkv_crc32_batch_device(const uint8_t *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths,
+                           const uint32_t *d_init_raw, uint32_t *d_out_final, uint64_t n, void *stream);
+
+/* Uniform batch in device memory: block i is [d_base + i*stride, + len). Fast path for fixed-size
+ * WAL/SSTable blocks (no prepass; 16-byte aligned blocks take the aligned kernel). */
+int tkv_crc32_batch_uniform_device(const uint8_t *d_base, uint64_t stride, uint64_t len,
+                                   const uint32_t *d_init_raw, uint32_t *d_out_final, uint64_t n,
+                                   void *stream);
+
+/* Irregular batch in HOST memory on the current device: blocks are streamed through pinned
+ * staging buffers with H2D copy / kernel / D2H copy overlapped on two streams. Synchronous.
+ * h_base may be pageable or pinned (pinned avoids one host memcpy). */
+int tkv_crc32_batch_host(const uint8_t *h_base, const uint64_t *h_offsets, const uint32_t *h_lengths,
+                         const uint32_t *h_init_raw, uint32_t *h_out_final, uint64_t n);
+
+/* Same, split across `ndev` devices by bytes (one host thread and stream pair per device, no
+ * collective). */
+int tkv_crc32_batch_host_multi(const int *devices, int ndev, const uint8_t *h_base, const uint64_t *h_offsets,
+                               const uint32_t *h_lengths, const uint32_t *h_init_raw, uint32_t *h_out_final,
+                               uint64_t n);
+
+/* ---- WAL record verification (wal_entry::decode's CRC check, wal.cpp:63-96) ------------------- */
+
+/* Verify every record of a slurped WAL image (host memory, wal_reader::open, wal.cpp:204-240):
+ * walks the record_len chain on the host, checks all CRCs in one batch on the GPU, and reports the
+ * number of leading good records in *n_good and the byte offset where decoding stopped in
+ * *stop_offset. Returns TKV_OK when the whole image verified (clean EOF), TKV_CORRUPTED at the
+ * first record whose length or CRC is bad (wal.cpp:68-96 order: header size, length, CRC). */
+int tkv_wal_verify(const uint8_t *h_wal, uint64_t size, uint64_t *n_good, uint64_t *stop_offset);
+
+/* Stamp n records in place (host memory): for record i at h_buf + h_offsets[i] of total size
+ * h_sizes[i] (>= 8), write crc32 of bytes [8, size) LE at offset 4 (wal.cpp:54-58). */
+int tkv_wal_stamp(uint8_t *h_buf, const uint64_t *h_offsets, const uint32_t *h_sizes, uint64_t n);
+
+/* ---- synthetic data (SURVEY.md §8d generator; bench/test inputs) ------------------------------- */
+
+int tkv_fill_synthetic_uniform(uint8_t *d_dst, uint64_t stride, uint64_t len, uint64_t first_block,
+                               uint64_t nblocks, uint64_t seed, void *stream);
+int tkv_fill_synthetic_blocks(uint8_t *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths,
+                              uint64_t first_block, uint64_t nblocks, uint64_t seed, void *stream);
+
+/* ---- introspection for tests (no GPU needed) --------------------------------------------------- */
+
+/* Copy the constant tables the kernels use (layout of tkv::DeviceTables) into `out`; returns the
+ * byte size needed (call with out = NULL to query). */
+size_t tkv_debug_tables(void *out, size_t cap);
+
+/* Host GF(2) helpers the decomposition rests on: a*b mod P and x^(8n) mod P, reflected. */
+uint32_t tkv_debug_multmodp(uint32_t a, uint32_t b);
+uint32_t tkv_debug_x8nmodp(uint64_t nbytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TKV_CRC32_H */

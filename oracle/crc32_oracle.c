@@ -1,0 +1,127 @@
+/*
+ * oracle/crc32_oracle.c -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * Plain-C restatement of lnikon/tinykvpp's CRC-32 (frankie::core::crc32), used by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg to check and time the HIP path.
+ * Nothing in tinykvpp_amd/ links or calls this file; the product fails loudly without its
+ * HIP library instead of falling back here.
+ *
+ * Parity pinning: tests/test_oracle.py checks every function below against
+ *   - the known answers of /root/reference/test/crc32_test.cpp:81-124,
+ *   - the WAL records of test/wal_test.cpp (fixtures in tests/golden/),
+ *   - outputs of the reference's own src/core/crc32.cpp compiled into oracle/_ref/ (when built),
+ *   - Python's zlib.crc32 (an independent CRC-32/ISO-HDLC implementation).
+ *
+ * Algorithm (follows /root/reference/src/core/crc32.hpp:9-30 and crc32.cpp:9-22):
+ *   reflected polynomial 0xEDB88320, init 0xFFFFFFFF, xorout 0xFFFFFFFF,
+ *   byte-at-a-time Sarwate table: crc = (crc >> 8) ^ T[(byte ^ crc) & 0xFF].
+ *
+ * Synthetic data generator: byte j of block b is LE byte (j % 8) of
+ * splitmix64((b << 24) ^ (j >> 3) ^ (seed << 56)).  Zipf lengths for cfg4 as in §8d.
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+#define ORACLE_POLY 0xEDB88320u   /* crc32.hpp:11 kCRC32Polynomial */
+#define ORACLE_INIT 0xFFFFFFFFu   /* crc32.hpp:9  kCRC32DefaultValue */
+
+static uint32_t g_table[256];
+static int g_table_ready = 0;
+
+/* crc32.hpp:16-30 generate_crc32_table(): 8 shift/xor rounds per entry. */
+void oracle_table(uint32_t out[256]) {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int bit = 0; bit < 8; ++bit) c = (c & 1u) ? (c >> 1) ^ ORACLE_POLY : (c >> 1);
+    out[i] = c;
+  }
+}
+
+static void ensure_table(void) {
+  if (!g_table_ready) {
+    oracle_table(g_table);
+    g_table_ready = 1;
+  }
+}
+
+/* crc32.cpp:9-16 crc32::update — continues from raw (pre-xorout) state, no pre/post XOR. */
+uint32_t oracle_update(uint32_t raw, const uint8_t *p, size_t n) {
+  ensure_table();
+  for (size_t i = 0; i < n; ++i) raw = (raw >> 8) ^ g_table[(p[i] ^ raw) & 0xFFu];
+  return raw;
+}
+
+/* crc32{}.update(span).finalize() — crc32.hpp:48 default state, crc32.cpp:19 finalize. */
+uint32_t oracle_crc32(const uint8_t *p, size_t n) { return oracle_update(ORACLE_INIT, p, n) ^ ORACLE_INIT; }
+
+/* ---- synthetic generator ---- */
+uint64_t oracle_splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* Bytes [off, off+n) of synthetic block b (one splitmix64 per aligned 8-byte group). */
+void oracle_fill(uint64_t seed, uint64_t b, uint64_t off, uint8_t *out, size_t n) {
+  size_t i = 0;
+  while (i < n) {
+    uint64_t j = off + i;
+    uint64_t w = oracle_splitmix64((b << 24) ^ (j >> 3) ^ (seed << 56));
+    for (unsigned k = (unsigned)(j & 7); k < 8 && i < n; ++k, ++i) out[i] = (uint8_t)(w >> (8 * k));
+  }
+}
+
+/* Sarwate CRC (init/xorout per crc32.hpp) of synthetic blocks [first, first+count) of length len
+ * each; out[i] = finalize() value.  Generates the bytes in 64 KiB slabs. */
+void oracle_crc_synthetic(uint64_t seed, uint64_t first, uint64_t count, uint64_t len, uint32_t *out) {
+  uint8_t buf[65536];
+  for (uint64_t i = 0; i < count; ++i) {
+    uint64_t b = first + i;
+    uint32_t raw = ORACLE_INIT;
+    for (uint64_t off = 0; off < len; off += sizeof(buf)) {
+      size_t n = (size_t)((len - off) < sizeof(buf) ? (len - off) : sizeof(buf));
+      oracle_fill(seed, b, off, buf, n);
+      raw = oracle_update(raw, buf, n);
+    }
+    out[i] = raw ^ ORACLE_INIT;
+  }
+}
+
+/* Zipf block length for cfg4: class k in [0,12], S = 256 * 2^k, P(k) ∝ 1/(k+1),
+ * r = splitmix64((seed<<56) ^ (1<<55) ^ b), u = (r & 0xFFFFFFFF) / 2^32 against the CDF,
+ * len = max(256, S - ((r >> 32) mod (S/2))). */
+uint64_t oracle_zipf_len(uint64_t seed, uint64_t b) {
+  double w[13], tot = 0.0, cdf = 0.0;
+  for (int k = 0; k < 13; ++k) { w[k] = 1.0 / (double)(k + 1); tot += w[k]; }
+  uint64_t r = oracle_splitmix64((seed << 56) ^ (1ull << 55) ^ b);
+  double u = (double)(r & 0xFFFFFFFFull) / 4294967296.0;
+  int k = 12;
+  for (int i = 0; i < 13; ++i) {
+    cdf += w[i] / tot;
+    if (u < cdf) { k = i; break; }
+  }
+  uint64_t S = 256ull << k;
+  uint64_t len = S - ((r >> 32) % (S / 2));
+  return len < 256 ? 256 : len;
+}
+
+void oracle_zipf_lengths(uint64_t seed, uint64_t first, uint64_t count, uint64_t *out) {
+  for (uint64_t i = 0; i < count; ++i) out[i] = oracle_zipf_len(seed, first + i);
+}
+
+/* CRC of synthetic blocks with per-block lengths (cfg4). */
+void oracle_crc_synthetic_lens(uint64_t seed, uint64_t first, uint64_t count, const uint64_t *lens,
+                               uint32_t *out) {
+  for (uint64_t i = 0; i < count; ++i) oracle_crc_synthetic(seed, first + i, 1, lens[i], out + i);
+}
+
+/* Batch over caller-provided host buffers: out[i] = finalize(update(init_i, base+off[i], len[i])). */
+void oracle_crc_batch(const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths,
+                      const uint32_t *init_raw, uint64_t n, uint32_t *out) {
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t s = init_raw ? init_raw[i] : ORACLE_INIT;
+    out[i] = oracle_update(s, base + offsets[i], lengths[i]) ^ ORACLE_INIT;
+  }
+}

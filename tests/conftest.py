@@ -1,0 +1,118 @@
+"""Shared fixtures. `-m "not gpu"` runs everywhere (oracle, golden vectors, host logic, ABI
+symbols); `-m gpu` needs an MI355X and calls the HIP kernels through the C ABI."""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a GPU (MI355X); calls the HIP path through the C ABI")
+
+
+def golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+class Oracle:
+    """ctypes view of oracle/liboracle.so (TEST INFRASTRUCTURE: the checker, never the product)."""
+
+    def __init__(self, path):
+        o = ctypes.CDLL(path)
+        o.oracle_update.restype = ctypes.c_uint32
+        o.oracle_update.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+        o.oracle_crc32.restype = ctypes.c_uint32
+        o.oracle_crc32.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        o.oracle_table.argtypes = [ctypes.c_void_p]
+        o.oracle_splitmix64.restype = ctypes.c_uint64
+        o.oracle_splitmix64.argtypes = [ctypes.c_uint64]
+        o.oracle_fill.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p, ctypes.c_size_t]
+        o.oracle_crc_synthetic.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_void_p]
+        o.oracle_zipf_lengths.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p]
+        o.oracle_crc_synthetic_lens.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
+        o.oracle_crc_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p]
+        self.lib = o
+
+    def crc(self, data: bytes) -> int:
+        a = np.frombuffer(bytes(data), np.uint8)
+        return self.lib.oracle_crc32(a.ctypes.data if a.size else None, a.size)
+
+    def update(self, raw: int, data: bytes) -> int:
+        a = np.frombuffer(bytes(data), np.uint8)
+        return self.lib.oracle_update(raw, a.ctypes.data if a.size else None, a.size)
+
+    def fill(self, seed, block, off, n):
+        out = np.zeros(n, np.uint8)
+        self.lib.oracle_fill(seed, block, off, out.ctypes.data, n)
+        return out
+
+    def synthetic(self, seed, first, count, length):
+        out = np.zeros(count, np.uint32)
+        self.lib.oracle_crc_synthetic(seed, first, count, length, out.ctypes.data)
+        return out
+
+    def zipf_lengths(self, seed, first, count):
+        out = np.zeros(count, np.uint64)
+        self.lib.oracle_zipf_lengths(seed, first, count, out.ctypes.data)
+        return out
+
+    def synthetic_lens(self, seed, first, lens):
+        lens = np.ascontiguousarray(lens, np.uint64)
+        out = np.zeros(lens.size, np.uint32)
+        self.lib.oracle_crc_synthetic_lens(seed, first, lens.size, lens.ctypes.data, out.ctypes.data)
+        return out
+
+    def batch(self, base: np.ndarray, offsets, lengths, init=None):
+        off = np.ascontiguousarray(offsets, np.uint64)
+        ln = np.ascontiguousarray(lengths, np.uint32)
+        ini = None if init is None else np.ascontiguousarray(init, np.uint32)
+        out = np.zeros(off.size, np.uint32)
+        self.lib.oracle_crc_batch(base.ctypes.data, off.ctypes.data, ln.ctypes.data,
+                                  None if ini is None else ini.ctypes.data, off.size, out.ctypes.data)
+        return out
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    path = os.path.join(ROOT, "oracle", "liboracle.so")
+    if not os.path.exists(path):
+        import subprocess
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "all"], check=True)
+    return Oracle(path)
+
+
+@pytest.fixture(scope="session")
+def ref_lib():
+    """The reference's own crc32.cpp compiled by oracle/Makefile (absent on the GPU box unless built)."""
+    path = os.path.join(ROOT, "oracle", "_ref", "libref_crc32.so")
+    if not os.path.exists(path):
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    r = ctypes.CDLL(path)
+    r.ref_crc32.restype = ctypes.c_uint32
+    r.ref_crc32.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    return r
+
+
+@pytest.fixture(scope="session")
+def lib():
+    import tinykvpp_amd
+    return tinykvpp_amd.load_library()
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import torch
+    import tinykvpp_amd as tk
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but torch sees no GPU")
+    torch.cuda.set_device(0)
+    tk.set_device(0)
+    return torch.device("cuda:0")

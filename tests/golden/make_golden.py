@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ (TEST INFRASTRUCTURE).
+
+Run in the build container, where /root/reference exists:
+    make -C oracle all ref && python tests/golden/make_golden.py [--aggregates]
+
+Every value is computed by the reference's OWN crc32 (src/core/crc32.cpp compiled from
+/root/reference into oracle/_ref/libref_crc32.so by oracle/Makefile) and cross-checked against
+our C restatement (oracle/liboracle.so) and Python's zlib.crc32; the script aborts on any
+disagreement.  Only data (inputs and expected outputs) is written -- no reference source.
+
+Sources of the vectors:
+  kat.json        test/crc32_test.cpp:81-124 (table, empty, "123456789", fox, incremental)
+  wal.json        records laid out as src/engine/wal.cpp:14-61 encodes them (CRC over
+                  [8, end) stored LE at offset 4), for the entries used in test/wal_test.cpp
+  odd.json        prefixes of synthetic block 7 (SURVEY.md §8c "Odd lengths")
+  synthetic.json  per-block CRCs of the §8d generator, first blocks of cfg2/cfg3/cfg4 plus the
+                  full-size aggregates (XOR and SUM32 over every block) with --aggregates
+"""
+import argparse
+import ctypes
+import json
+import os
+import struct
+import sys
+import threading
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+ORA = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+REF = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref_crc32.so"))
+
+ORA.oracle_crc32.restype = ctypes.c_uint32
+ORA.oracle_crc32.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+REF.ref_crc32.restype = ctypes.c_uint32
+REF.ref_crc32.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+REF.ref_crc32_chunked.restype = ctypes.c_uint32
+REF.ref_crc32_chunked.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t]
+REF.ref_table.argtypes = [ctypes.c_void_p]
+ORA.oracle_fill.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p, ctypes.c_size_t]
+ORA.oracle_crc_synthetic.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_void_p]
+ORA.oracle_zipf_lengths.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p]
+ORA.oracle_crc_synthetic_lens.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
+
+SEED = 1
+
+
+def crc_all(data: bytes) -> int:
+    a, b, c = REF.ref_crc32(data, len(data)), ORA.oracle_crc32(data, len(data)), zlib.crc32(data)
+    if not (a == b == c):
+        sys.exit(f"oracle disagreement on {len(data)} bytes: ref={a:08x} port={b:08x} zlib={c:08x}")
+    return a
+
+
+def wal_encode(op: int, seq: int, key: bytes, value: bytes, tomb: int) -> bytes:
+    """Record layout of src/engine/wal.cpp:14-18 / wal.hpp:21-27 (LE, packed, 26 B header)."""
+    body = struct.pack("<BQBII", op, seq, tomb, len(key), len(value)) + key + value
+    record_len = len(body)  # everything after record_len(u32) + crc32(u32)
+    crc = crc_all(body)     # wal.cpp:54-57 CRC over [8, end)
+    return struct.pack("<II", record_len, crc) + body
+
+
+def kat():
+    t = np.zeros(256, np.uint32)
+    REF.ref_table(t.ctypes.data)
+    s = b"Hello, World!"
+    cuts = np.array([5, 7], np.uint64)  # "Hello" | ", " | "World!"
+    inc = REF.ref_crc32_chunked(s, cuts.ctypes.data, 2, len(s))
+    return {
+        "source": "test/crc32_test.cpp:81-124",
+        "table": [int(x) for x in t],
+        "table_checks": {"0": 0x00000000, "1": 0x77073096, "2": 0xEE0E612C, "255": 0x2D02EF8D},
+        "strings": [
+            {"text": "", "crc": crc_all(b"")},
+            {"text": "123456789", "crc": crc_all(b"123456789")},
+            {"text": "The quick brown fox jumps over the lazy dog",
+             "crc": crc_all(b"The quick brown fox jumps over the lazy dog")},
+            {"text": "Hello, World!", "crc": crc_all(s)},
+        ],
+        "incremental": {"text": "Hello, World!", "cuts": [5, 7], "crc": inc},
+    }
+
+
+def wal():
+    entries = [  # (op, seq, key, value, tombstone) as in test/wal_test.cpp
+        (0, 42, b"hello", b"world", 0),
+        (1, 100, b"removed", b"", 1),
+        (0, 1, b"k", b"v", 0),
+        (0, 0, b"", b"", 0),
+        (0, 7, b"test", b"data", 0),
+        (0, 1, b"a", b"b", 0),
+        (0, 2, b"c", b"d", 0),
+    ]
+    out = []
+    for op, seq, k, v, tomb in entries:
+        rec = wal_encode(op, seq, k, v, tomb)
+        out.append({"op": op, "seq": seq, "key": k.decode(), "value": v.decode(), "tombstone": tomb,
+                    "hex": rec.hex(), "crc": struct.unpack_from("<I", rec, 4)[0]})
+    return {"source": "src/engine/wal.cpp:19-61 layout; entries from test/wal_test.cpp", "records": out}
+
+
+def odd():
+    buf = np.zeros(1 << 20, np.uint8)
+    ORA.oracle_fill(SEED, 7, 0, buf.ctypes.data, 1 << 20)
+    lens = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 31, 63, 64, 65, 255, 256, 1023, 4095, 4096, 4097,
+            65535, 65536, 1048576]
+    return {"source": "prefixes of synthetic block 7 (seed 1), SURVEY.md §8c",
+            "block": 7, "seed": SEED,
+            "prefixes": [{"len": n, "crc": crc_all(buf[:n].tobytes())} for n in lens]}
+
+
+def _parallel(fn, n, nthreads=8):
+    """Run fn(lo, hi) over [0, n) in contiguous ranges on threads (ctypes drops the GIL)."""
+    step = (n + nthreads - 1) // nthreads
+    ths = [threading.Thread(target=fn, args=(i * step, min(n, (i + 1) * step))) for i in range(nthreads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+
+
+def synth_uniform(nblocks, blen, full):
+    first = 64
+    crcs = np.zeros(first, np.uint32)
+    ORA.oracle_crc_synthetic(SEED, 0, first, blen, crcs.ctypes.data)
+    # cross-check the first blocks against the reference binary itself
+    buf = np.zeros(blen, np.uint8)
+    for b in range(4):
+        ORA.oracle_fill(SEED, b, 0, buf.ctypes.data, blen)
+        assert crc_all(buf.tobytes()) == int(crcs[b])
+    ORA.oracle_fill(SEED, nblocks - 1, 0, buf.ctypes.data, blen)
+    last = crc_all(buf.tobytes())
+    d = {"nblocks": nblocks, "len": blen, "first": [int(x) for x in crcs], "last": last}
+    if full:
+        allc = np.zeros(nblocks, np.uint32)
+        _parallel(lambda lo, hi: ORA.oracle_crc_synthetic(SEED, lo, hi - lo, blen, allc[lo:].ctypes.data),
+                  nblocks)
+        d["xor"] = int(np.bitwise_xor.reduce(allc))
+        d["sum32"] = int(allc.astype(np.uint64).sum() & 0xFFFFFFFF)
+    return d
+
+
+def synth_zipf(nblocks, full):
+    lens = np.zeros(nblocks, np.uint64)
+    ORA.oracle_zipf_lengths(SEED, 0, nblocks, lens.ctypes.data)
+    first = 256
+    crcs = np.zeros(first, np.uint32)
+    ORA.oracle_crc_synthetic_lens(SEED, 0, first, lens.ctypes.data, crcs.ctypes.data)
+    for b in range(4):
+        buf = np.zeros(int(lens[b]), np.uint8)
+        ORA.oracle_fill(SEED, b, 0, buf.ctypes.data, int(lens[b]))
+        assert crc_all(buf.tobytes()) == int(crcs[b])
+    d = {"nblocks": nblocks, "total_bytes": int(lens.sum()), "first_lens": [int(x) for x in lens[:first]],
+         "first": [int(x) for x in crcs]}
+    if full:
+        allc = np.zeros(nblocks, np.uint32)
+        _parallel(lambda lo, hi: ORA.oracle_crc_synthetic_lens(SEED, lo, hi - lo, lens[lo:].ctypes.data,
+                                                               allc[lo:].ctypes.data), nblocks)
+        d["xor"] = int(np.bitwise_xor.reduce(allc))
+        d["sum32"] = int(allc.astype(np.uint64).sum() & 0xFFFFFFFF)
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--aggregates", action="store_true", help="also compute full-size cfg2/3/4 aggregates")
+    a = ap.parse_args()
+    w = lambda name, obj: json.dump(obj, open(os.path.join(HERE, name), "w"), indent=1)
+    w("kat.json", kat())
+    w("wal.json", wal())
+    w("odd.json", odd())
+    syn = {"generator": "SURVEY.md §8d splitmix64, seed 1",
+           "cfg2": synth_uniform(1 << 20, 4096, a.aggregates),
+           "cfg3": synth_uniform(1 << 18, 65536, a.aggregates),
+           "cfg4": synth_zipf(1 << 17, a.aggregates),
+           # cfg5 (4 M x 64 KiB, 256 GiB) is too large to recompute here; the survey's value,
+           # computed with the reference crc32 over the same generator, is recorded as-is.
+           "cfg5": {"nblocks": 1 << 22, "len": 65536, "xor": 0x5A7EAA3B, "sum32": 0x9D26EBFD,
+                    "provenance": "SURVEY.md §8c (reference crc32, survey session)"}}
+    if a.aggregates:
+        survey = {"cfg2": (0x90E1CC31, 0xB9691C49), "cfg3": (0xEF4407CE, 0x8185ADF2),
+                  "cfg4": (0x3B2B6926, 0x02C0ECA2)}
+        for k, (x, s) in survey.items():
+            if (syn[k]["xor"], syn[k]["sum32"]) != (x, s):
+                sys.exit(f"{k}: aggregate {syn[k]['xor']:08x}/{syn[k]['sum32']:08x} != survey {x:08x}/{s:08x}")
+    w("synthetic.json", syn)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

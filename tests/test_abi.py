@@ -1,0 +1,222 @@
+"""C-ABI library checks that need no GPU: exported symbols, constant tables, and a numpy model of
+the exact kernel decomposition (rows, lanes, slicing-by-4, lane shifts, Horner, init injection,
+seam fix-up, wave partition) checked against the oracle."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import tinykvpp_amd as tk
+from tinykvpp_amd._lib import SIGNATURES
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROW, SEG = 4096, 64
+POLY = 0xEDB88320
+
+
+def header_symbols():
+    text = open(os.path.join(ROOT, "include", "tkv_crc32.h")).read()
+    return sorted(set(re.findall(r"\b(tkv_\w+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol(lib):
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), f"libtkv_crc32.so does not export {s}"
+    assert sorted(SIGNATURES) == syms, "ctypes signatures out of sync with include/tkv_crc32.h"
+
+
+def test_no_gpu_is_an_error_not_a_fallback(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    assert lib.tkv_device_count() == 0
+    with pytest.raises(tk.TkvError) as e:
+        tk.crc32().update(b"123456789")
+    assert e.value.code == 2  # io_error: no device, and no CPU path to fall back to
+
+
+def load_tables(lib):
+    n = lib.tkv_debug_tables(None, 0)
+    buf = np.zeros(n // 4, np.uint32)
+    lib.tkv_debug_tables(buf.ctypes.data, n)
+    o = 0
+    slice_ = buf[o:o + 1024].reshape(4, 256); o += 1024
+    lane = buf[o:o + 8 * 16 * 64].reshape(8, 16, 64); o += 8 * 16 * 64
+    horner = buf[o:o + 64]; o += 64
+    row_pow = buf[o:o + 64]; o += 64
+    head = buf[o:o + (ROW + 1) * 32].reshape(ROW + 1, 32); o += (ROW + 1) * 32
+    assert o * 4 == n
+    return slice_, lane, horner, row_pow, head
+
+
+@pytest.fixture(scope="module")
+def tables(lib):
+    return load_tables(lib)
+
+
+def shift_zeros(oracle, reg, n):
+    """Shift_n(reg) computed the slow way: feed n zero bytes to the reference algorithm."""
+    return oracle.update(reg, b"\0" * n)
+
+
+def test_slice_tables(tables, oracle):
+    from conftest import golden
+    s = tables[0]
+    assert [int(x) for x in s[0]] == golden("kat.json")["table"]
+    for k in range(1, 4):  # Tk[i] = register after feeding k zero bytes from T0[i]
+        for i in (0, 1, 77, 255):
+            assert int(s[k][i]) == shift_zeros(oracle, int(s[0][i]), k)
+
+
+def test_gf2_helpers(lib, oracle):
+    rng = np.random.default_rng(3)
+    for n in [0, 1, 3, 4, 64, 4032, 4096, 100000]:
+        z = lib.tkv_debug_x8nmodp(n)
+        for v in rng.integers(0, 2**32, 4, dtype=np.uint64):
+            assert lib.tkv_debug_multmodp(z, int(v)) == shift_zeros(oracle, int(v), n)
+
+
+def test_lane_shift_horner_head_tables(tables, oracle):
+    _, lane, horner, row_pow, head = tables
+    for l in (0, 1, 31, 62, 63):
+        for j in (0, 3, 7):
+            for v in (1, 9, 15):
+                assert int(lane[j][v][l]) == shift_zeros(oracle, v << (4 * j), (63 - l) * SEG)
+    for i in (0, 5, 31):
+        assert int(horner[i]) == shift_zeros(oracle, 1 << i, ROW)
+    assert all(int(x) == 0 for x in horner[32:])
+    for h in (0, 1, 3, 4, 100, 4095, 4096):
+        for i in (0, 17, 31):
+            assert int(head[h][i]) == shift_zeros(oracle, 1 << i, h)
+
+
+# ---- numpy model of the kernel ------------------------------------------------------------------
+
+def rows_for_len(n):
+    return 1 if n == 0 else (n - 1) // ROW + 1
+
+
+def head_len(n):
+    return n - (rows_for_len(n) - 1) * ROW
+
+
+def bits_dot(sel, consts):
+    """XOR of consts[i] over the set bits i of sel (the lane-parallel GF(2) product)."""
+    out = 0
+    for i in range(32):
+        if (sel >> i) & 1:
+            out ^= int(consts[i])
+    return out
+
+
+class Model:
+    def __init__(self, tables):
+        self.s, self.lane, self.horner, self.row_pow, self.head = tables
+
+    def slice_lanes(self, row):
+        """16 slicing-by-4 steps per lane over a (64, 64)-byte row image; returns (64,) partials."""
+        dw = row.reshape(64, 16, 4).astype(np.uint32)
+        dw = dw[..., 0] | (dw[..., 1] << 8) | (dw[..., 2] << 16) | (dw[..., 3] << 24)
+        p = np.zeros(64, np.uint32)
+        T = self.s
+        for k in range(16):
+            x = p ^ dw[:, k]
+            p = T[3][x & 0xFF] ^ T[2][(x >> 8) & 0xFF] ^ T[1][(x >> 16) & 0xFF] ^ T[0][x >> 24]
+        return p
+
+    def row_value(self, row, B, init, head_row, h):
+        p = self.slice_lanes(row)
+        v = np.zeros(64, np.uint32)
+        for j in range(8):
+            v ^= self.lane[j][(p >> (4 * j)) & 15, np.arange(64)]
+        acc = int(np.bitwise_xor.reduce(v))
+        acc ^= bits_dot(B, self.horner[:32])
+        if head_row:
+            acc ^= bits_dot(init, self.head[h])
+        return acc
+
+    def row_image(self, data, n, r):
+        R = rows_for_len(n)
+        start = n - (R - r) * ROW
+        img = np.zeros(ROW, np.uint8)
+        lo = max(0, start)
+        img[lo - start:] = data[lo:start + ROW]
+        return img
+
+    def block_pieces(self, data, init, cuts):
+        """Partials of the row pieces [cuts[i], cuts[i+1]) of one block (seam emulation)."""
+        n = len(data)
+        h = head_len(n)
+        out = []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            B = 0
+            for r in range(a, b):
+                B = self.row_value(self.row_image(data, n, r), B, init, r == 0, h)
+            out.append((B, rows_for_len(n) - b))
+        return out
+
+    def crc(self, data, init=0xFFFFFFFF, cuts=None):
+        R = rows_for_len(len(data))
+        cuts = cuts or [0, R]
+        acc = 0
+        for partial, after in self.block_pieces(np.asarray(data, np.uint8), init, cuts):
+            z = 0x80000000
+            for k in range(64):
+                if (after >> k) & 1:
+                    z = tk.load_library().tkv_debug_multmodp(z, int(self.row_pow[k]))
+            acc ^= tk.load_library().tkv_debug_multmodp(z, partial)
+        return acc ^ 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def model(tables):
+    return Model(tables)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 5, 15, 16, 17, 63, 64, 65, 255, 1000, 4095, 4096, 4097,
+                               8191, 8192, 12289])
+def test_model_matches_oracle(model, oracle, n):
+    rng = np.random.default_rng(n + 1)
+    d = rng.integers(0, 256, n, dtype=np.uint8)
+    for init in (0xFFFFFFFF, 0x0BADF00D):
+        want = oracle.update(init, d.tobytes()) ^ 0xFFFFFFFF
+        assert model.crc(d, init) == want
+
+
+def test_model_seams(model, oracle):
+    rng = np.random.default_rng(5)
+    n = 5 * ROW + 123
+    d = rng.integers(0, 256, n, dtype=np.uint8)
+    want = oracle.crc(d.tobytes())
+    for cuts in ([0, 1, 6], [0, 2, 3, 6], [0, 5, 6], [0, 1, 2, 3, 4, 5, 6]):
+        assert model.crc(d, cuts=cuts) == want
+
+
+def wave_partition(lengths, W):
+    """Row partition of crc_rows + wave_start of rows_finish (irregular path), in Python."""
+    rows = [rows_for_len(n) for n in lengths]
+    rs = np.concatenate([[0], np.cumsum(rows)]).astype(np.int64)
+    TR = int(rs[-1])
+    starts = {}
+    for b in range(len(lengths)):
+        lo, hi = int(rs[b]), int(rs[b + 1])
+        for w in range((lo * W + TR - 1) // TR, min(W, (hi * W + TR - 1) // TR)):
+            starts[w] = b
+    return rs, TR, starts
+
+
+@pytest.mark.parametrize("W", [1, 16, 64, 4096])
+def test_wave_start_partition(W):
+    rng = np.random.default_rng(W)
+    for trial in range(5):
+        lengths = rng.integers(0, 40000, rng.integers(1, 200)).tolist()
+        rs, TR, starts = wave_partition(lengths, W)
+        for w in range(W):
+            g0, g1 = w * TR // W, (w + 1) * TR // W
+            if g0 < g1:
+                b = starts[w]
+                assert rs[b] <= g0 < rs[b + 1]

@@ -1,0 +1,284 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the reference's golden vectors.
+
+Bit-exact on every block. Small sizes are compared block by block with the oracle; the BASELINE
+configs at full size are compared through their golden aggregates (XOR and SUM32 of all block
+CRCs), plus properties (incremental == single, corruption always detected).
+"""
+import struct
+
+import numpy as np
+import pytest
+
+import tinykvpp_amd as tk
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def dev_bytes(b, device):
+    a = np.frombuffer(bytes(b), np.uint8)
+    return torch.from_numpy(a.copy()).to(device) if a.size else torch.empty(0, dtype=torch.uint8, device=device)
+
+
+# ---- crc32_test.cpp:81-124 through the reference-shaped class ------------------------------------
+
+def test_known_answers(gpu):
+    k = golden("kat.json")
+    assert tk.crc32().finalize() == 0  # EmptyInput
+    for s in k["strings"]:
+        assert tk.crc32().update(s["text"].encode()).finalize() == s["crc"]
+    assert tk.crc32().update(b"123456789").finalize() == 0xCBF43926
+    assert tk.crc32().update(b"The quick brown fox jumps over the lazy dog").finalize() == 0x414FA339
+
+
+def test_incremental_equals_single(gpu):
+    data = b"Hello, World!"
+    single = tk.crc32().update(data).finalize()
+    c = tk.crc32()
+    c.update(data[:5]).update(data[5:7]).update(data[7:])
+    assert c.finalize() == single == golden("kat.json")["incremental"]["crc"]
+    c.reset()
+    assert c.finalize() == 0
+
+
+def test_update_device_tensor(gpu, oracle):
+    rng = np.random.default_rng(1)
+    for n in (0, 1, 3, 4, 5, 64, 4095, 4096, 4097, 100003, 3 << 20):
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+        t = torch.from_numpy(d).to(gpu)
+        assert tk.crc32().update(t).finalize() == oracle.crc(d.tobytes()), n
+
+
+def test_update_chaining_raw_state(gpu, oracle):
+    rng = np.random.default_rng(2)
+    d = rng.integers(0, 256, 50000, dtype=np.uint8).tobytes()
+    c = tk.crc32()
+    for a, b in ((0, 1), (1, 3), (3, 4100), (4100, 4101), (4101, 50000)):
+        c.update(d[a:b])
+    assert c.finalize() == oracle.crc(d)
+
+
+def test_odd_prefixes(gpu, oracle):
+    g = golden("odd.json")
+    buf = oracle.fill(g["seed"], g["block"], 0, 1 << 20)
+    t = torch.from_numpy(buf).to(gpu)
+    lens = [p["len"] for p in g["prefixes"]]
+    offs = torch.zeros(len(lens), dtype=torch.int64, device=gpu)
+    ln = torch.tensor(lens, dtype=torch.int32, device=gpu)
+    got = u32(tk.crc32_batch(t, offs, ln))
+    assert [int(x) for x in got] == [p["crc"] for p in g["prefixes"]]
+    for p in g["prefixes"]:
+        assert tk.crc32().update(buf[:p["len"]].tobytes()).finalize() == p["crc"]
+
+
+# ---- WAL call sites (wal.cpp:54-58, 89-96; wal_test.cpp, engine_test.cpp:437-459) ----------------
+
+def test_wal_records_stamped_identically(gpu):
+    recs = golden("wal.json")["records"]
+    unstamped = [tk.wal.encode_unstamped(r["op"], r["seq"], r["key"].encode(), r["value"].encode(),
+                                         r["tombstone"]) for r in recs]
+    stamped = tk.wal.stamp(unstamped)
+    for r, s in zip(recs, stamped):
+        assert s.hex() == r["hex"]
+        assert struct.unpack_from("<I", s, 4)[0] == r["crc"]
+
+
+def test_wal_verify_and_first_corruption(gpu):
+    recs = [bytes.fromhex(r["hex"]) for r in golden("wal.json")["records"]]
+    image = b"".join(recs)
+    assert tk.wal.verify(image) == ("ok", len(recs), len(image))
+    assert tk.wal.verify(b"") == ("ok", 0, 0)
+    # flip the CRC byte of record 1 (wal_test.cpp:809-850): record 0 good, parked at record 1
+    bad = bytearray(image)
+    bad[len(recs[0]) + 4] ^= 0xFF
+    assert tk.wal.verify(bytes(bad)) == ("corrupted", 1, len(recs[0]))
+    # payload corruption of record 0 (wal_test.cpp:245-263)
+    bad = bytearray(image)
+    bad[10] ^= 0xFF
+    assert tk.wal.verify(bytes(bad)) == ("corrupted", 0, 0)
+    # truncated tail (wal.cpp:68-70 / 82-87)
+    st, good, stop = tk.wal.verify(image[:-3])
+    assert st == "corrupted" and good == len(recs) - 1
+
+
+def test_wal_key_value_overflow_detected_after_crc(gpu):
+    rec = bytearray(bytes.fromhex(golden("wal.json")["records"][2]["hex"]))  # {put,1,"k","v"}
+    struct.pack_into("<I", rec, 18, 9999)  # wal_test.cpp:265-294: bogus key_len, CRC recomputed
+    rec[4:8] = struct.pack("<I", tk.crc32().update(bytes(rec[8:])).finalize())
+    assert tk.wal.verify(bytes(rec)) == ("corrupted", 0, 0)
+
+
+def test_wal_many_records(gpu, oracle):
+    rng = np.random.default_rng(9)
+    recs = []
+    for i in range(3000):
+        k = rng.integers(0, 256, rng.integers(0, 40), dtype=np.uint8).tobytes()
+        v = rng.integers(0, 256, rng.integers(0, 300), dtype=np.uint8).tobytes()
+        recs.append(tk.wal.encode_unstamped(i % 2, i, k, v, i % 2))
+    stamped = tk.wal.stamp(recs)
+    for s in stamped[:200]:
+        assert struct.unpack_from("<I", s, 4)[0] == oracle.crc(s[8:])
+    image = b"".join(stamped)
+    assert tk.wal.verify(image) == ("ok", 3000, len(image))
+
+
+# ---- uniform batches ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("blen,n", [(4096, 5000), (65536, 300), (4096, 7), (16, 100000), (1000, 9000),
+                                    (4100, 4097), (12288, 513), (1, 4096), (0, 10), (3, 20000)])
+def test_uniform_vs_oracle(gpu, oracle, blen, n):
+    stride = max(blen, 8) + (8 - max(blen, 8) % 8) % 8
+    data = torch.empty(n * stride + 16, dtype=torch.uint8, device=gpu)
+    if blen % 8 == 0 and blen:
+        tk.fill_synthetic_uniform(data, blen, n, first_block=3, stride=stride)
+        want = oracle.synthetic(1, 3, n, blen)
+        got = u32(tk.crc32_batch_uniform(data, blen, n, stride=stride))
+        assert np.array_equal(got, want)
+    host = np.random.default_rng(blen).integers(0, 256, n * stride + 16, dtype=np.uint8)
+    data.copy_(torch.from_numpy(host))
+    want = oracle.batch(host, np.arange(n) * stride, np.full(n, blen))
+    got = u32(tk.crc32_batch_uniform(data, blen, n, stride=stride))
+    assert np.array_equal(got, want)
+    # same blocks at an odd (unaligned) base address
+    got = u32(tk.crc32_batch_uniform(data, blen, n, stride=stride, offset=5)) if (n - 1) * stride + blen + 5 <= data.numel() else None
+    if got is not None:
+        want = oracle.batch(host, np.arange(n) * stride + 5, np.full(n, blen))
+        assert np.array_equal(got, want)
+
+
+def test_uniform_per_block_init(gpu, oracle):
+    n, blen = 2000, 4096
+    host = np.random.default_rng(4).integers(0, 256, n * blen, dtype=np.uint8)
+    init = np.random.default_rng(5).integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    got = u32(tk.crc32_batch_uniform(torch.from_numpy(host).to(gpu), blen, n,
+                                     init_raw=torch.from_numpy(init.view(np.int32)).to(gpu)))
+    want = oracle.batch(host, np.arange(n) * blen, np.full(n, blen), init)
+    assert np.array_equal(got, want)
+
+
+def test_single_huge_block_split_across_waves(gpu, oracle):
+    n = (64 << 20) + 77  # one block, rows spread over every wave, joined by crc_fixup
+    host = np.random.default_rng(6).integers(0, 256, n, dtype=np.uint8)
+    got = u32(tk.crc32_batch_uniform(torch.from_numpy(host).to(gpu), n, 1))
+    assert int(got[0]) == oracle.crc(host.tobytes())
+
+
+# ---- irregular batches ---------------------------------------------------------------------------
+
+def irregular_case(rng, nblocks, maxlen, packed=True, overlap=False):
+    lens = rng.integers(0, maxlen + 1, nblocks)
+    lens[rng.integers(0, nblocks, max(1, nblocks // 50))] = rng.integers(0, 4, max(1, nblocks // 50))
+    if packed:
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])]) + 3
+    else:
+        offs = rng.integers(0, int(lens.sum()) + 1, nblocks)
+    size = int((offs + lens).max()) + 32
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    return host, offs.astype(np.int64), lens.astype(np.int32)
+
+
+@pytest.mark.parametrize("nblocks,maxlen,packed", [(1, 100, True), (10, 5000, True), (5000, 300, True),
+                                                   (3000, 20000, False), (200, 300000, True),
+                                                   (70000, 64, True)])
+def test_irregular_vs_oracle(gpu, oracle, nblocks, maxlen, packed):
+    rng = np.random.default_rng(nblocks + maxlen)
+    host, offs, lens = irregular_case(rng, nblocks, maxlen, packed)
+    init = rng.integers(0, 2**32, nblocks, dtype=np.uint64).astype(np.uint32)
+    d = torch.from_numpy(host).to(gpu)
+    o = torch.from_numpy(offs).to(gpu)
+    ln = torch.from_numpy(lens).to(gpu)
+    got = u32(tk.crc32_batch(d, o, ln))
+    assert np.array_equal(got, oracle.batch(host, offs, lens))
+    got = u32(tk.crc32_batch(d, o, ln, init_raw=torch.from_numpy(init.view(np.int32)).to(gpu)))
+    assert np.array_equal(got, oracle.batch(host, offs, lens, init))
+
+
+def test_irregular_zipf_sample(gpu, oracle):
+    """First 4096 blocks of cfg4 (Zipf 256 B - 1 MiB), packed back to back, unaligned starts."""
+    c = golden("synthetic.json")["cfg4"]
+    lens = oracle.zipf_lengths(1, 0, 4096)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+    d = torch.empty(int(lens.sum()) + 64, dtype=torch.uint8, device=gpu)
+    o = torch.from_numpy(offs).to(gpu)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    tk.fill_synthetic_blocks(d, o, ln, first_block=0)
+    got = u32(tk.crc32_batch(d, o, ln))
+    assert [int(x) for x in got[:256]] == c["first"]
+    assert np.array_equal(got, oracle.synthetic_lens(1, 0, lens))
+
+
+def test_corruption_always_detected(gpu):
+    n, blen = 1024, 4096
+    host = np.random.default_rng(8).integers(0, 256, n * blen, dtype=np.uint8)
+    d = torch.from_numpy(host).to(gpu)
+    clean = u32(tk.crc32_batch_uniform(d, blen, n))
+    rng = np.random.default_rng(9)
+    pos = rng.integers(0, n * blen, 256)
+    bits = rng.integers(0, 8, 256)
+    for p, b in zip(pos, bits):
+        host[p] ^= np.uint8(1 << int(b))
+    d2 = torch.from_numpy(host).to(gpu)
+    dirty = u32(tk.crc32_batch_uniform(d2, blen, n))
+    hit = np.zeros(n, bool)
+    hit[np.unique(pos // blen)] = True
+    assert np.array_equal(clean != dirty, hit)  # every single-bit-flipped block differs, no others
+
+
+# ---- host pipeline and multi-device host API ----------------------------------------------------
+
+def test_host_batch(gpu, oracle):
+    rng = np.random.default_rng(12)
+    host, offs, lens = irregular_case(rng, 20000, 20000, packed=False)
+    got = tk.crc32_batch_host(host, offs, lens)
+    assert np.array_equal(got, oracle.batch(host, offs, lens))
+    got = tk.crc32_batch_host(host, offs, lens, devices=[0])
+    assert np.array_equal(got, oracle.batch(host, offs, lens))
+
+
+def test_host_batch_block_larger_than_slab(gpu, oracle):
+    n = (300 << 20) + 5
+    host = np.random.default_rng(13).integers(0, 256, n, dtype=np.uint8)
+    got = tk.crc32_batch_host(host, [0, 7, 1 << 20], [n, 100, 4096])
+    want = [oracle.crc(host.tobytes()), oracle.crc(host[7:107].tobytes()), oracle.crc(host[1 << 20:(1 << 20) + 4096].tobytes())]
+    assert [int(x) for x in got] == want
+
+
+# ---- full-size BASELINE configs through golden aggregates ----------------------------------------
+
+def aggregates(crcs):
+    return int(np.bitwise_xor.reduce(crcs)), int(crcs.astype(np.uint64).sum() & 0xFFFFFFFF)
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
+def test_full_size_uniform_configs(gpu, cfg):
+    c = golden("synthetic.json")[cfg]
+    n, blen = c["nblocks"], c["len"]
+    got = np.zeros(n, np.uint32)
+    chunk = min(n, (4 << 30) // blen)  # 4 GiB of device data at a time
+    data = torch.empty(chunk * blen, dtype=torch.uint8, device=gpu)
+    for first in range(0, n, chunk):
+        m = min(chunk, n - first)
+        tk.fill_synthetic_uniform(data, blen, m, first_block=first)
+        got[first:first + m] = u32(tk.crc32_batch_uniform(data, blen, m))
+    assert [int(x) for x in got[:len(c["first"])]] == c["first"]
+    assert int(got[-1]) == c["last"]
+    assert aggregates(got) == (c["xor"], c["sum32"])
+
+
+def test_full_size_zipf_config(gpu, oracle):
+    c = golden("synthetic.json")["cfg4"]
+    lens = oracle.zipf_lengths(1, 0, c["nblocks"])
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+    d = torch.empty(int(lens.sum()) + 64, dtype=torch.uint8, device=gpu)
+    o = torch.from_numpy(offs).to(gpu)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    tk.fill_synthetic_blocks(d, o, ln, first_block=0)
+    got = u32(tk.crc32_batch(d, o, ln))
+    assert [int(x) for x in got[:256]] == c["first"]
+    assert aggregates(got) == (c["xor"], c["sum32"])

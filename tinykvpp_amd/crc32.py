@@ -1,0 +1,189 @@
+"""Python mirror of frankie::core::crc32 and the batch engine behind it.
+
+Reference interface (/root/reference/src/core/crc32.hpp:9-49, crc32.cpp:9-22):
+
+    constexpr kCRC32DefaultValue = 0xFFFFFFFF, kCRC32Bits = 8, kCRC32Polynomial = 0xEDB88320
+    generate_crc32_table() -> std::array<uint32_t, 256>
+    class crc32 { update(span<const byte>) -> crc32&; finalize() -> uint32_t; reset(); }
+
+Same names, argument meaning and semantics here: ``crc32().update(b"...").finalize()``. Every
+``update`` runs on the GPU through the C ABI (include/tkv_crc32.h); there is no CPU fallback.
+The batch functions take torch tensors already resident on the GPU (or numpy arrays for the host
+pipeline) and return ``finalize()`` values per block.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import check, load_library
+
+kCRC32DefaultValue = 0xFFFFFFFF  # crc32.hpp:9
+kCRC32Bits = 8                   # crc32.hpp:10
+kCRC32Polynomial = 0xEDB88320    # crc32.hpp:11
+kCRC32TableSize = 256            # crc32.hpp:13
+
+
+def generate_crc32_table():
+    """The 256-entry Sarwate table (crc32.hpp:16-30); kept for API parity, not used to compute."""
+    table = []
+    for i in range(kCRC32TableSize):
+        c = i
+        for _ in range(kCRC32Bits):
+            c = (c >> 1) ^ (kCRC32Polynomial if c & 1 else 0)
+        table.append(c)
+    return table
+
+
+def _stream_ptr(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _host_view(data):
+    """(pointer, nbytes, keepalive) for a bytes-like or numpy host buffer."""
+    if isinstance(data, np.ndarray):
+        arr = np.ascontiguousarray(data)
+        return arr.ctypes.data, arr.nbytes, arr
+    mv = memoryview(data).cast("B")
+    if mv.readonly:
+        buf = ctypes.create_string_buffer(mv.tobytes(), len(mv))
+        return ctypes.addressof(buf), len(mv), buf
+    arr = np.frombuffer(mv, dtype=np.uint8)
+    return arr.ctypes.data, arr.nbytes, arr
+
+
+class crc32:  # noqa: N801 - reference class name (crc32.hpp:32)
+    """CRC-32/ISO-HDLC accumulator; raw register starts at 0xFFFFFFFF (crc32.hpp:48)."""
+
+    __slots__ = ("_crc",)
+
+    def __init__(self):
+        self._crc = kCRC32DefaultValue
+
+    def update(self, data, stream=None):
+        """Continue the register over ``data`` (crc32.cpp:9-16) and return self (chainable).
+
+        ``data``: bytes-like / numpy (host memory) or a torch uint8 tensor (device memory; the
+        device path is asynchronous on ``stream`` but this call waits for the 4-byte result).
+        """
+        lib = load_library()
+        try:
+            import torch
+            is_dev = isinstance(data, torch.Tensor) and data.is_cuda
+        except ImportError:  # pragma: no cover - torch is part of the image
+            is_dev = False
+        if is_dev:
+            t = data.contiguous().view(torch.uint8)
+            out = torch.empty(1, dtype=torch.int32, device=t.device)
+            check(lib.tkv_crc32_update_device(self._crc, ctypes.c_void_p(t.data_ptr()), t.numel(),
+                                              ctypes.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+            self._crc = int(out.cpu().numpy().view(np.uint32)[0])
+        else:
+            ptr, n, keep = _host_view(data)
+            res = ctypes.c_uint32(0)
+            check(lib.tkv_crc32_update(self._crc, ctypes.c_void_p(ptr), n, ctypes.byref(res)))
+            del keep
+            self._crc = res.value
+        return self
+
+    def finalize(self):
+        """Register XOR 0xFFFFFFFF (crc32.cpp:19)."""
+        return self._crc ^ kCRC32DefaultValue
+
+    def reset(self):
+        """Back to 0xFFFFFFFF (crc32.cpp:22)."""
+        self._crc = kCRC32DefaultValue
+
+    @property
+    def raw(self):
+        return self._crc
+
+
+# ---- batch engine -------------------------------------------------------------------------------
+
+def _u32_view(t):
+    import torch
+    return t.view(torch.int32) if t.dtype != torch.int32 else t
+
+
+def crc32_batch(data, offsets, lengths, init_raw=None, out=None, stream=None):
+    """Irregular batch on the GPU: block i = data[offsets[i] : offsets[i] + lengths[i]].
+
+    data: uint8 CUDA tensor; offsets: int64 CUDA tensor; lengths: int32 CUDA tensor (< 2^32 bytes
+    each); init_raw: optional int32 CUDA tensor of raw registers (crc32::crc_). Returns an int32
+    tensor of finalize() bit patterns (``.cpu().numpy().view(np.uint32)`` for unsigned values).
+    """
+    import torch
+    n = offsets.numel()
+    if lengths.numel() != n:
+        raise ValueError("offsets and lengths differ in length")
+    for name, t, dt in (("offsets", offsets, torch.int64), ("lengths", lengths, torch.int32)):
+        if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous CUDA {dt} tensor")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=data.device)
+    initp = ctypes.c_void_p(init_raw.data_ptr()) if init_raw is not None else None
+    check(load_library().tkv_crc32_batch_device(
+        ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
+        ctypes.c_void_p(lengths.data_ptr()), initp, ctypes.c_void_p(out.data_ptr()), n,
+        _stream_ptr(stream)))
+    return out
+
+
+def crc32_batch_uniform(data, length, n, stride=None, init_raw=None, out=None, stream=None, offset=0):
+    """Uniform batch on the GPU: block i = data[offset + i*stride : + length] (stride = length)."""
+    import torch
+    stride = length if stride is None else stride
+    if n and offset + (n - 1) * stride + length > data.numel():
+        raise ValueError("batch exceeds the data tensor")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=data.device)
+    initp = ctypes.c_void_p(init_raw.data_ptr()) if init_raw is not None else None
+    check(load_library().tkv_crc32_batch_uniform_device(
+        ctypes.c_void_p(data.data_ptr() + offset), stride, length, initp,
+        ctypes.c_void_p(out.data_ptr()), n, _stream_ptr(stream)))
+    return out
+
+
+def crc32_batch_host(data, offsets, lengths, init_raw=None, devices=None):
+    """Host-memory batch (numpy): pinned staging, H2D / kernel / D2H overlapped. Returns uint32."""
+    lib = load_library()
+    buf = np.ascontiguousarray(data).view(np.uint8)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    ini = None if init_raw is None else np.ascontiguousarray(init_raw, dtype=np.uint32)
+    out = np.zeros(off.size, np.uint32)
+    initp = None if ini is None else ctypes.c_void_p(ini.ctypes.data)
+    if devices is None:
+        check(lib.tkv_crc32_batch_host(ctypes.c_void_p(buf.ctypes.data), ctypes.c_void_p(off.ctypes.data),
+                                       ctypes.c_void_p(ln.ctypes.data), initp,
+                                       ctypes.c_void_p(out.ctypes.data), off.size))
+    else:
+        devs = (ctypes.c_int * len(devices))(*devices)
+        check(lib.tkv_crc32_batch_host_multi(devs, len(devices), ctypes.c_void_p(buf.ctypes.data),
+                                             ctypes.c_void_p(off.ctypes.data), ctypes.c_void_p(ln.ctypes.data),
+                                             initp, ctypes.c_void_p(out.ctypes.data), off.size))
+    return out
+
+
+def fill_synthetic_uniform(data, length, n, first_block=0, seed=1, stride=None, stream=None):
+    """Write the SURVEY §8d generator's blocks [first_block, first_block+n) into ``data`` (GPU)."""
+    stride = length if stride is None else stride
+    check(load_library().tkv_fill_synthetic_uniform(ctypes.c_void_p(data.data_ptr()), stride, length,
+                                                    first_block, n, seed, _stream_ptr(stream)))
+
+
+def fill_synthetic_blocks(data, offsets, lengths, first_block=0, seed=1, stream=None):
+    check(load_library().tkv_fill_synthetic_blocks(ctypes.c_void_p(data.data_ptr()),
+                                                   ctypes.c_void_p(offsets.data_ptr()),
+                                                   ctypes.c_void_p(lengths.data_ptr()), first_block,
+                                                   offsets.numel(), seed, _stream_ptr(stream)))
+
+
+def device_count():
+    return load_library().tkv_device_count()
+
+
+def set_device(device):
+    check(load_library().tkv_set_device(device))

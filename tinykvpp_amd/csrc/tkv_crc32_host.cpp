@@ -1,0 +1,642 @@
+// Host runtime of the MI355X CRC-32 engine: per-device contexts, the C ABI of include/tkv_crc32.h,
+// the pinned-staging host pipeline, multi-GPU batch split and the WAL verify/stamp helpers.
+// All checksum arithmetic runs in tkv_crc32_kernels.hip; this file only plans and launches it
+// (the GF(2) helpers here build the constant tables and are exported for tests).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "tkv_crc32.h"
+#include "tkv_crc32_internal.h"
+
+namespace tkv {
+
+// ---- launchers (tkv_crc32_kernels.hip) ---------------------------------------------------------
+hipError_t launch_rows(const RowsArgs& a, bool aligned, bool uniform, unsigned grid, hipStream_t st);
+hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
+hipError_t launch_prepass(const std::uint32_t* lengths, std::uint32_t n, std::uint32_t* row_scan,
+                          std::uint32_t* tile_sums, std::uint32_t* wave_start, std::uint32_t W, hipStream_t st);
+std::uint32_t prepass_tiles(std::uint32_t n);
+hipError_t launch_fill_uniform(std::uint8_t* dst, std::uint64_t stride, std::uint64_t len, std::uint64_t first,
+                               std::uint64_t nblocks, std::uint64_t seed, hipStream_t st);
+hipError_t launch_fill_blocks(std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
+                              std::uint64_t first, std::uint64_t nblocks, std::uint64_t seed, hipStream_t st);
+
+// ---- GF(2) arithmetic in the reflected representation (x^0 = 0x80000000) -------------------------
+std::uint32_t multmodp(std::uint32_t a, std::uint32_t b) {
+  std::uint32_t p = 0;
+  for (int i = 31; i >= 0; --i) {
+    if (a & (1u << i)) p ^= b;
+    b = (b & 1u) ? (b >> 1) ^ kPoly : (b >> 1);
+  }
+  return p;
+}
+
+std::uint32_t x8nmodp(std::uint64_t nbytes) {
+  // x^(8n) = product over set bits k of n of x^(8*2^k); x^(8*2^k) by repeated squaring of x^8.
+  std::uint32_t result = 0x80000000u;  // x^0
+  std::uint32_t sq = 0x00800000u;      // x^8
+  while (nbytes) {
+    if (nbytes & 1u) result = multmodp(result, sq);
+    sq = multmodp(sq, sq);
+    nbytes >>= 1;
+  }
+  return result;
+}
+
+std::uint32_t shift_bytes(std::uint32_t reg, std::uint64_t nbytes) { return multmodp(x8nmodp(nbytes), reg); }
+
+void build_tables(DeviceTables* t) {
+  // T0: the Sarwate table of crc32.hpp:16-30; Tk[i] = T0[T(k-1)[i] & 0xFF] ^ (T(k-1)[i] >> 8).
+  for (std::uint32_t i = 0; i < 256; ++i) {
+    std::uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? kPoly : 0u);
+    t->slice[0][i] = c;
+  }
+  for (int k = 1; k < 4; ++k)
+    for (std::uint32_t i = 0; i < 256; ++i)
+      t->slice[k][i] = t->slice[0][t->slice[k - 1][i] & 0xFFu] ^ (t->slice[k - 1][i] >> 8);
+  for (int l = 0; l < 64; ++l) {
+    const std::uint32_t m = x8nmodp(static_cast<std::uint64_t>(63 - l) * kSeg);
+    for (int j = 0; j < 8; ++j)
+      for (std::uint32_t v = 0; v < 16; ++v) t->lane_shift[j][v][l] = multmodp(m, v << (4 * j));
+  }
+  const std::uint32_t mrow = x8nmodp(kRow);
+  for (int l = 0; l < 64; ++l) t->horner[l] = l < 32 ? multmodp(mrow, 1u << l) : 0u;
+  std::uint32_t p = mrow;
+  for (int k = 0; k < 64; ++k) {
+    t->row_pow[k] = p;
+    p = multmodp(p, p);
+  }
+  std::uint32_t z = 0x80000000u;  // x^(8h), h = 0..kRow
+  for (int h = 0; h <= kRow; ++h) {
+    for (int i = 0; i < 32; ++i) t->head_shift[h][i] = multmodp(z, 1u << i);
+    z = multmodp(z, 0x00800000u);
+  }
+}
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(TKV_IO_ERROR, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define TKV_HIP(call)                                   \
+  do {                                                  \
+    hipError_t e_ = (call);                             \
+    if (e_ != hipSuccess) return hip_fail(e_, #call);   \
+  } while (0)
+
+// Scratch used by one in-flight batch on one stream (the prepass arrays and seam records are
+// written and read by kernels of that stream only).
+struct StreamScratch {
+  Seam* seams = nullptr;
+  std::uint32_t* row_scan = nullptr;
+  std::uint32_t* tiles = nullptr;
+  std::uint32_t* wave_start = nullptr;
+  std::uint64_t cap_blocks = 0;
+};
+
+struct DevCtx {
+  int dev = -1;
+  int ncu = 0;
+  std::uint32_t W = 0;  // waves of a full launch (one 16-wave workgroup per CU)
+  DeviceTables* d_tabs = nullptr;
+  std::uint8_t* d_dummy = nullptr;
+  std::mutex mu;
+  std::map<void*, std::unique_ptr<StreamScratch>> scratch;
+  // synchronous update() staging (guarded by upd_mu)
+  std::mutex upd_mu;
+  hipStream_t st = nullptr;
+  std::uint8_t* h_stage = nullptr;
+  std::uint8_t* d_stage = nullptr;
+  std::uint32_t* d_io = nullptr;
+  std::uint32_t* h_io = nullptr;
+  std::size_t stage_cap = 0;
+};
+
+std::mutex g_mu;
+DevCtx* g_ctx[64] = {};
+
+int get_ctx(DevCtx** out) {
+  int dev = 0;
+  TKV_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return fail(TKV_INVALID_ARGUMENT, "device index out of range");
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_ctx[dev]) {
+    auto* c = new DevCtx();
+    c->dev = dev;
+    hipDeviceProp_t prop;
+    TKV_HIP(hipGetDeviceProperties(&prop, dev));
+    c->ncu = prop.multiProcessorCount;
+    c->W = static_cast<std::uint32_t>(c->ncu) * kWavesPerWG;
+    std::unique_ptr<DeviceTables> h(new DeviceTables);
+    build_tables(h.get());
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&c->d_tabs), sizeof(DeviceTables)));
+    TKV_HIP(hipMemcpy(c->d_tabs, h.get(), sizeof(DeviceTables), hipMemcpyHostToDevice));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&c->d_dummy), 256));
+    TKV_HIP(hipMemset(c->d_dummy, 0, 256));
+    g_ctx[dev] = c;
+  }
+  *out = g_ctx[dev];
+  return TKV_OK;
+}
+
+int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** out) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  auto& slot = c->scratch[stream];
+  if (!slot) {
+    slot.reset(new StreamScratch());
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->seams), sizeof(Seam) * 2 * c->W));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->wave_start), sizeof(std::uint32_t) * c->W));
+  }
+  StreamScratch* s = slot.get();
+  if (nblocks > s->cap_blocks) {
+    std::uint64_t cap = std::max<std::uint64_t>(nblocks, 2 * s->cap_blocks);
+    if (s->row_scan) {
+      // Freed blocks may still be in use by earlier work on this stream.
+      TKV_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+      TKV_HIP(hipFree(s->row_scan));
+      TKV_HIP(hipFree(s->tiles));
+    }
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&s->row_scan), sizeof(std::uint32_t) * (cap + 1)));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&s->tiles),
+                      sizeof(std::uint32_t) * (prepass_tiles(static_cast<std::uint32_t>(cap)) + 1)));
+    s->cap_blocks = cap;
+  }
+  *out = s;
+  return TKV_OK;
+}
+
+bool ptr_ok(const void* p) { return p != nullptr; }
+
+RowsArgs base_args(DevCtx* c, StreamScratch* s) {
+  RowsArgs a{};
+  a.tabs = c->d_tabs;
+  a.dummy = c->d_dummy;
+  a.seams = s->seams;
+  a.init_default = kInit;
+  a.out_xor = kInit;
+  a.nwaves = c->W;
+  return a;
+}
+
+// Uniform-length batch (also used for single spans).
+int run_uniform(DevCtx* c, const std::uint8_t* d_base, std::uint64_t stride, std::uint64_t len,
+                const std::uint32_t* d_init, std::uint32_t init_default, std::uint32_t out_xor, std::uint32_t* d_out,
+                std::uint64_t n, hipStream_t st) {
+  if (n == 0) return TKV_OK;
+  if (len > 0xFFFFFFFFull || n > 0xFFFFFFFFull) return fail(TKV_INVALID_ARGUMENT, "block length or count >= 2^32");
+  const std::uint64_t R = rows_for_len(static_cast<std::uint32_t>(len));
+  if (n * R > 0xFFFFFFFFull) return fail(TKV_INVALID_ARGUMENT, "batch larger than 2^32 rows (16 TiB)");
+  StreamScratch* s = nullptr;
+  if (int rc = get_scratch(c, st, 0, &s)) return rc;
+  RowsArgs a = base_args(c, s);
+  a.base = d_base;
+  a.stride = stride;
+  a.len = static_cast<std::uint32_t>(len);
+  a.head_z = x8nmodp(head_len(a.len));
+  a.init_raw = d_init;
+  a.init_default = init_default;
+  a.out_xor = out_xor;
+  a.out = d_out;
+  a.nblocks = static_cast<std::uint32_t>(n);
+  a.total_rows = static_cast<std::uint32_t>(n * R);
+  // Launch only as many workgroups as there are rows to give them (small batches).
+  std::uint64_t grid = std::min<std::uint64_t>(c->ncu, (a.total_rows + kWavesPerWG - 1) / kWavesPerWG);
+  if (grid == 0) grid = 1;
+  a.nwaves = static_cast<std::uint32_t>(grid * kWavesPerWG);
+  a.snap_blocks = n >= a.nwaves ? 1u : 0u;
+  const bool aligned = (reinterpret_cast<std::uintptr_t>(d_base) % 16 == 0) && (stride % 16 == 0) && (len % 16 == 0);
+  TKV_HIP(launch_rows(a, aligned, true, static_cast<unsigned>(grid), st));
+  if (!a.snap_blocks) TKV_HIP(launch_fixup(a, st));
+  return TKV_OK;
+}
+
+int run_irregular(DevCtx* c, const std::uint8_t* d_base, const std::uint64_t* d_off, const std::uint32_t* d_len,
+                  const std::uint32_t* d_init, std::uint32_t* d_out, std::uint64_t n, hipStream_t st) {
+  if (n == 0) return TKV_OK;
+  if (n >= 0xFFFFFFFFull) return fail(TKV_INVALID_ARGUMENT, "batch of 2^32 or more blocks");
+  StreamScratch* s = nullptr;
+  if (int rc = get_scratch(c, st, n, &s)) return rc;
+  RowsArgs a = base_args(c, s);
+  a.base = d_base;
+  a.offsets = d_off;
+  a.lengths = d_len;
+  a.row_scan = s->row_scan;
+  a.wave_start = s->wave_start;
+  a.init_raw = d_init;
+  a.out = d_out;
+  a.nblocks = static_cast<std::uint32_t>(n);
+  TKV_HIP(launch_prepass(d_len, a.nblocks, s->row_scan, s->tiles, s->wave_start, a.nwaves, st));
+  TKV_HIP(launch_rows(a, false, false, static_cast<unsigned>(c->ncu), st));
+  TKV_HIP(launch_fixup(a, st));
+  return TKV_OK;
+}
+
+bool is_pinned_or_device(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost || attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+// ---- host-memory pipeline ---------------------------------------------------------------------------
+constexpr std::size_t kSlab = std::size_t(256) << 20;  // bytes of block data per pipeline stage
+
+struct HostPipe {
+  hipStream_t st[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  std::uint8_t* h_data[2] = {nullptr, nullptr};
+  std::uint8_t* d_data[2] = {nullptr, nullptr};
+  std::uint64_t* h_off[2] = {nullptr, nullptr};
+  std::uint32_t* h_len[2] = {nullptr, nullptr};
+  std::uint32_t* h_init[2] = {nullptr, nullptr};
+  std::uint32_t* h_out[2] = {nullptr, nullptr};
+  std::uint64_t* d_off[2] = {nullptr, nullptr};
+  std::uint32_t* d_len[2] = {nullptr, nullptr};
+  std::uint32_t* d_init[2] = {nullptr, nullptr};
+  std::uint32_t* d_out[2] = {nullptr, nullptr};
+  std::size_t cap_blocks = 0;
+  ~HostPipe() {
+    for (int i = 0; i < 2; ++i) {
+      if (st[i]) (void)hipStreamSynchronize(st[i]);
+      if (done[i]) (void)hipEventDestroy(done[i]);
+      if (st[i]) (void)hipStreamDestroy(st[i]);
+      (void)hipHostFree(h_data[i]);
+      (void)hipFree(d_data[i]);
+      (void)hipHostFree(h_off[i]);
+      (void)hipHostFree(h_len[i]);
+      (void)hipHostFree(h_init[i]);
+      (void)hipHostFree(h_out[i]);
+      (void)hipFree(d_off[i]);
+      (void)hipFree(d_len[i]);
+      (void)hipFree(d_init[i]);
+      (void)hipFree(d_out[i]);
+    }
+  }
+};
+
+int pipe_init(HostPipe& p, std::size_t max_blocks) {
+  p.cap_blocks = max_blocks;
+  for (int i = 0; i < 2; ++i) {
+    TKV_HIP(hipStreamCreateWithFlags(&p.st[i], hipStreamNonBlocking));
+    TKV_HIP(hipEventCreateWithFlags(&p.done[i], hipEventDisableTiming));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_data[i]), kSlab, hipHostMallocDefault));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&p.d_data[i]), kSlab));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_off[i]), max_blocks * 8, hipHostMallocDefault));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_len[i]), max_blocks * 4, hipHostMallocDefault));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_init[i]), max_blocks * 4, hipHostMallocDefault));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_out[i]), max_blocks * 4, hipHostMallocDefault));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&p.d_off[i]), max_blocks * 8));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&p.d_len[i]), max_blocks * 4));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&p.d_init[i]), max_blocks * 4));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&p.d_out[i]), max_blocks * 4));
+  }
+  return TKV_OK;
+}
+
+// Blocks in [lo, hi) of a host batch, processed slab by slab. Blocks larger than a slab are
+// chained through update_device in slab-sized pieces on stream 0.
+int host_batch(DevCtx* c, const std::uint8_t* h_base, const std::uint64_t* off, const std::uint32_t* len,
+               const std::uint32_t* init, std::uint32_t* out, std::uint64_t lo, std::uint64_t hi) {
+  if (hi <= lo) return TKV_OK;
+  // Largest number of blocks a slab can hold (all >= 1 byte... zero-length blocks count too).
+  std::size_t max_blocks = 1;
+  {
+    std::uint64_t b = lo;
+    while (b < hi) {
+      std::size_t cnt = 0, bytes = 0;
+      while (b < hi && len[b] <= kSlab && bytes + len[b] <= kSlab && cnt < (std::size_t(1) << 22)) {
+        bytes += len[b];
+        ++cnt;
+        ++b;
+      }
+      if (cnt == 0) ++b;
+      max_blocks = std::max(max_blocks, cnt);
+    }
+  }
+  HostPipe p;
+  if (int rc = pipe_init(p, max_blocks)) return rc;
+  struct Pending {
+    std::uint64_t lo = 0, cnt = 0;
+    bool active = false;
+  } pend[2];
+  auto retire = [&](int k) -> int {
+    if (!pend[k].active) return TKV_OK;
+    TKV_HIP(hipEventSynchronize(p.done[k]));
+    std::memcpy(out + pend[k].lo, p.h_out[k], pend[k].cnt * 4);
+    pend[k].active = false;
+    return TKV_OK;
+  };
+  std::uint64_t b = lo;
+  int k = 0;
+  while (b < hi) {
+    if (len[b] > kSlab) {
+      // Huge block: chain raw registers through slab-sized device updates.
+      for (int i = 0; i < 2; ++i)
+        if (int rc = retire(i)) return rc;
+      std::uint32_t raw = init ? init[b] : kInit;
+      const std::uint8_t* src = h_base + off[b];
+      std::uint64_t rem = len[b];
+      while (rem) {
+        const std::size_t m = static_cast<std::size_t>(std::min<std::uint64_t>(rem, kSlab));
+        std::memcpy(p.h_data[0], src, m);
+        p.h_init[0][0] = raw;
+        TKV_HIP(hipMemcpyAsync(p.d_data[0], p.h_data[0], m, hipMemcpyHostToDevice, p.st[0]));
+        TKV_HIP(hipMemcpyAsync(p.d_init[0], p.h_init[0], 4, hipMemcpyHostToDevice, p.st[0]));
+        if (int rc = run_uniform(c, p.d_data[0], m, m, p.d_init[0], kInit, 0u, p.d_out[0], 1, p.st[0])) return rc;
+        TKV_HIP(hipMemcpyAsync(p.h_out[0], p.d_out[0], 4, hipMemcpyDeviceToHost, p.st[0]));
+        TKV_HIP(hipStreamSynchronize(p.st[0]));
+        raw = p.h_out[0][0];
+        src += m;
+        rem -= m;
+      }
+      out[b] = raw ^ kInit;
+      ++b;
+      continue;
+    }
+    // Gather the next slab of blocks.
+    if (int rc = retire(k)) return rc;
+    std::size_t cnt = 0, bytes = 0;
+    const std::uint64_t b0 = b;
+    while (b < hi && len[b] <= kSlab && bytes + len[b] <= kSlab && cnt < p.cap_blocks) {
+      std::memcpy(p.h_data[k] + bytes, h_base + off[b], len[b]);
+      p.h_off[k][cnt] = bytes;
+      p.h_len[k][cnt] = len[b];
+      p.h_init[k][cnt] = init ? init[b] : kInit;
+      bytes += len[b];
+      ++cnt;
+      ++b;
+    }
+    TKV_HIP(hipMemcpyAsync(p.d_data[k], p.h_data[k], bytes, hipMemcpyHostToDevice, p.st[k]));
+    TKV_HIP(hipMemcpyAsync(p.d_off[k], p.h_off[k], cnt * 8, hipMemcpyHostToDevice, p.st[k]));
+    TKV_HIP(hipMemcpyAsync(p.d_len[k], p.h_len[k], cnt * 4, hipMemcpyHostToDevice, p.st[k]));
+    TKV_HIP(hipMemcpyAsync(p.d_init[k], p.h_init[k], cnt * 4, hipMemcpyHostToDevice, p.st[k]));
+    if (int rc = run_irregular(c, p.d_data[k], p.d_off[k], p.d_len[k], p.d_init[k], p.d_out[k], cnt, p.st[k]))
+      return rc;
+    TKV_HIP(hipMemcpyAsync(p.h_out[k], p.d_out[k], cnt * 4, hipMemcpyDeviceToHost, p.st[k]));
+    TKV_HIP(hipEventRecord(p.done[k], p.st[k]));
+    pend[k] = {b0, cnt, true};
+    k ^= 1;
+  }
+  for (int i = 0; i < 2; ++i)
+    if (int rc = retire(i)) return rc;
+  return TKV_OK;
+}
+
+}  // namespace
+}  // namespace tkv
+
+using namespace tkv;
+
+extern "C" {
+
+int tkv_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+int tkv_set_device(int device) {
+  int n = tkv_device_count();
+  if (device < 0 || device >= n) return fail(TKV_INVALID_ARGUMENT, "no such device");
+  TKV_HIP(hipSetDevice(device));
+  DevCtx* c = nullptr;
+  return get_ctx(&c);
+}
+
+const char* tkv_last_error(void) { return g_err.c_str(); }
+
+int tkv_crc32_update_device(uint32_t raw_state, const void* d_data, size_t len, uint32_t* d_out_raw, void* stream) {
+  if (!ptr_ok(d_out_raw) || (len && !ptr_ok(d_data))) return fail(TKV_INVALID_ARGUMENT, "null pointer");
+  DevCtx* c = nullptr;
+  if (int rc = get_ctx(&c)) return rc;
+  // One block of `len` bytes continued from raw_state; raw register out (no xorout).
+  const auto* base = static_cast<const std::uint8_t*>(d_data ? d_data : c->d_dummy);
+  return run_uniform(c, base, len, len, nullptr, raw_state, 0u, d_out_raw, 1, static_cast<hipStream_t>(stream));
+}
+
+int tkv_crc32_update(uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
+  if (!ptr_ok(out_raw) || (len && !ptr_ok(data))) return fail(TKV_INVALID_ARGUMENT, "null pointer");
+  DevCtx* c = nullptr;
+  if (int rc = get_ctx(&c)) return rc;
+  std::lock_guard<std::mutex> lk(c->upd_mu);
+  if (!c->st) {
+    TKV_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_io), 16, hipHostMallocDefault));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&c->d_io), 16));
+  }
+  const std::size_t want = std::min<std::size_t>(std::max<std::size_t>(len, 1 << 16), kSlab);
+  if (want > c->stage_cap) {
+    (void)hipHostFree(c->h_stage);
+    (void)hipFree(c->d_stage);
+    c->h_stage = nullptr;
+    c->d_stage = nullptr;
+    c->stage_cap = 0;
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), want, hipHostMallocDefault));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&c->d_stage), want));
+    c->stage_cap = want;
+  }
+  std::uint32_t raw = raw_state;
+  const auto* src = static_cast<const std::uint8_t*>(data);
+  std::size_t rem = len;
+  do {
+    const std::size_t m = std::min(rem, c->stage_cap);
+    if (m) {
+      std::memcpy(c->h_stage, src, m);
+      TKV_HIP(hipMemcpyAsync(c->d_stage, c->h_stage, m, hipMemcpyHostToDevice, c->st));
+    }
+    if (int rc = run_uniform(c, c->d_stage, m, m, nullptr, raw, 0u, c->d_io, 1, c->st)) return rc;
+    TKV_HIP(hipMemcpyAsync(c->h_io, c->d_io, 4, hipMemcpyDeviceToHost, c->st));
+    TKV_HIP(hipStreamSynchronize(c->st));
+    raw = c->h_io[0];
+    src += m;
+    rem -= m;
+  } while (rem);
+  *out_raw = raw;
+  return TKV_OK;
+}
+
+int tkv_crc32_batch_device(const uint8_t* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
+                           const uint32_t* d_init_raw, uint32_t* d_out_final, uint64_t n, void* stream) {
+  if (n == 0) return TKV_OK;
+  if (!ptr_ok(d_base) || !ptr_ok(d_offsets) || !ptr_ok(d_lengths) || !ptr_ok(d_out_final))
+    return fail(TKV_INVALID_ARGUMENT, "null pointer");
+  DevCtx* c = nullptr;
+  if (int rc = get_ctx(&c)) return rc;
+  return run_irregular(c, d_base, d_offsets, d_lengths, d_init_raw, d_out_final, n, static_cast<hipStream_t>(stream));
+}
+
+int tkv_crc32_batch_uniform_device(const uint8_t* d_base, uint64_t stride, uint64_t len, const uint32_t* d_init_raw,
+                                   uint32_t* d_out_final, uint64_t n, void* stream) {
+  if (n == 0) return TKV_OK;
+  if ((len && !ptr_ok(d_base)) || !ptr_ok(d_out_final)) return fail(TKV_INVALID_ARGUMENT, "null pointer");
+  DevCtx* c = nullptr;
+  if (int rc = get_ctx(&c)) return rc;
+  const auto* base = d_base ? d_base : c->d_dummy;
+  return run_uniform(c, base, stride, len, d_init_raw, kInit, kInit, d_out_final, n, static_cast<hipStream_t>(stream));
+}
+
+int tkv_crc32_batch_host(const uint8_t* h_base, const uint64_t* h_offsets, const uint32_t* h_lengths,
+                         const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
+  if (n == 0) return TKV_OK;
+  if (!ptr_ok(h_base) || !ptr_ok(h_offsets) || !ptr_ok(h_lengths) || !ptr_ok(h_out_final))
+    return fail(TKV_INVALID_ARGUMENT, "null pointer");
+  DevCtx* c = nullptr;
+  if (int rc = get_ctx(&c)) return rc;
+  return host_batch(c, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, 0, n);
+}
+
+int tkv_crc32_batch_host_multi(const int* devices, int ndev, const uint8_t* h_base, const uint64_t* h_offsets,
+                               const uint32_t* h_lengths, const uint32_t* h_init_raw, uint32_t* h_out_final,
+                               uint64_t n) {
+  if (ndev <= 0 || !ptr_ok(devices)) return fail(TKV_INVALID_ARGUMENT, "no devices");
+  if (n == 0) return TKV_OK;
+  if (!ptr_ok(h_base) || !ptr_ok(h_offsets) || !ptr_ok(h_lengths) || !ptr_ok(h_out_final))
+    return fail(TKV_INVALID_ARGUMENT, "null pointer");
+  // Byte-balanced contiguous split of the block list.
+  std::uint64_t total = 0;
+  for (std::uint64_t i = 0; i < n; ++i) total += h_lengths[i];
+  std::vector<std::uint64_t> cut(ndev + 1, n);
+  cut[0] = 0;
+  {
+    std::uint64_t acc = 0, i = 0;
+    for (int d = 1; d < ndev; ++d) {
+      const std::uint64_t target = total * d / ndev;
+      while (i < n && acc + h_lengths[i] <= target) acc += h_lengths[i++];
+      cut[d] = i;
+    }
+  }
+  std::vector<int> rcs(ndev, TKV_OK);
+  std::vector<std::string> errs(ndev);
+  std::vector<std::thread> th;
+  for (int d = 0; d < ndev; ++d) {
+    th.emplace_back([&, d] {
+      if (int rc = tkv_set_device(devices[d])) {
+        rcs[d] = rc;
+        errs[d] = g_err;
+        return;
+      }
+      DevCtx* c = nullptr;
+      rcs[d] = get_ctx(&c);
+      if (rcs[d] == TKV_OK) rcs[d] = host_batch(c, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, cut[d], cut[d + 1]);
+      errs[d] = g_err;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int d = 0; d < ndev; ++d)
+    if (rcs[d]) return fail(rcs[d], "device " + std::to_string(devices[d]) + ": " + errs[d]);
+  return TKV_OK;
+}
+
+int tkv_wal_verify(const uint8_t* h_wal, uint64_t size, uint64_t* n_good, uint64_t* stop_offset) {
+  if ((size && !ptr_ok(h_wal)) || !ptr_ok(n_good) || !ptr_ok(stop_offset))
+    return fail(TKV_INVALID_ARGUMENT, "null pointer");
+  // Walk the record_len chain (wal.cpp:63-87): each record is [u32 record_len][u32 crc][payload].
+  constexpr std::uint64_t kMeta = 26;  // wal.hpp:21-27 kMetadataSize
+  std::vector<std::uint64_t> off;
+  std::vector<std::uint32_t> len, stored;
+  std::uint64_t pos = 0;
+  bool structural_error = false;
+  while (pos < size) {
+    const std::uint64_t left = size - pos;
+    if (left < kMeta) {
+      structural_error = true;  // wal.cpp:68-70
+      break;
+    }
+    std::uint32_t rlen, crc;
+    std::memcpy(&rlen, h_wal + pos, 4);
+    std::memcpy(&crc, h_wal + pos + 4, 4);
+    if (static_cast<std::uint64_t>(rlen) + 8 > left) {
+      structural_error = true;  // wal.cpp:82-87
+      break;
+    }
+    off.push_back(pos + 8);
+    len.push_back(rlen);
+    stored.push_back(crc);
+    pos += 8 + static_cast<std::uint64_t>(rlen);
+  }
+  std::vector<std::uint32_t> got(off.size());
+  if (!off.empty()) {
+    if (int rc = tkv_crc32_batch_host(h_wal, off.data(), len.data(), nullptr, got.data(), off.size())) return rc;
+  }
+  std::uint64_t good = 0, stop = 0;
+  for (; good < off.size(); ++good) {
+    if (got[good] != stored[good]) break;  // wal.cpp:93-96
+    // key/value bounds inside the payload (wal.cpp:118-121)
+    const std::uint8_t* rec = h_wal + off[good] - 8;
+    std::uint32_t klen, vlen;
+    std::memcpy(&klen, rec + 18, 4);
+    std::memcpy(&vlen, rec + 22, 4);
+    if (kMeta + static_cast<std::uint64_t>(klen) + vlen > 8 + static_cast<std::uint64_t>(len[good])) break;
+  }
+  stop = good < off.size() ? off[good] - 8 : pos;
+  *n_good = good;
+  *stop_offset = stop;
+  if (good < off.size() || structural_error) return fail(TKV_CORRUPTED, "corrupted WAL record");
+  return TKV_OK;
+}
+
+int tkv_wal_stamp(uint8_t* h_buf, const uint64_t* h_offsets, const uint32_t* h_sizes, uint64_t n) {
+  if (n == 0) return TKV_OK;
+  if (!ptr_ok(h_buf) || !ptr_ok(h_offsets) || !ptr_ok(h_sizes)) return fail(TKV_INVALID_ARGUMENT, "null pointer");
+  std::vector<std::uint64_t> off(n);
+  std::vector<std::uint32_t> len(n), crc(n);
+  for (std::uint64_t i = 0; i < n; ++i) {
+    if (h_sizes[i] < 8) return fail(TKV_INVALID_ARGUMENT, "WAL record shorter than its 8-byte prefix");
+    off[i] = h_offsets[i] + 8;  // wal.cpp:54-57: CRC over [8, size)
+    len[i] = h_sizes[i] - 8;
+  }
+  if (int rc = tkv_crc32_batch_host(h_buf, off.data(), len.data(), nullptr, crc.data(), n)) return rc;
+  for (std::uint64_t i = 0; i < n; ++i) std::memcpy(h_buf + h_offsets[i] + 4, &crc[i], 4);  // wal.cpp:58
+  return TKV_OK;
+}
+
+int tkv_fill_synthetic_uniform(uint8_t* d_dst, uint64_t stride, uint64_t len, uint64_t first_block, uint64_t nblocks,
+                               uint64_t seed, void* stream) {
+  if (len % 8 || stride % 8 || reinterpret_cast<std::uintptr_t>(d_dst) % 8)
+    return fail(TKV_INVALID_ARGUMENT, "uniform fill needs 8-byte aligned blocks");
+  DevCtx* c = nullptr;
+  if (int rc = get_ctx(&c)) return rc;
+  TKV_HIP(launch_fill_uniform(d_dst, stride, len, first_block, nblocks, seed, static_cast<hipStream_t>(stream)));
+  return TKV_OK;
+}
+
+int tkv_fill_synthetic_blocks(uint8_t* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
+                              uint64_t first_block, uint64_t nblocks, uint64_t seed, void* stream) {
+  DevCtx* c = nullptr;
+  if (int rc = get_ctx(&c)) return rc;
+  TKV_HIP(launch_fill_blocks(d_base, d_offsets, d_lengths, first_block, nblocks, seed, static_cast<hipStream_t>(stream)));
+  return TKV_OK;
+}
+
+size_t tkv_debug_tables(void* out, size_t cap) {
+  if (out && cap >= sizeof(DeviceTables)) build_tables(static_cast<DeviceTables*>(out));
+  return sizeof(DeviceTables);
+}
+
+uint32_t tkv_debug_multmodp(uint32_t a, uint32_t b) { return multmodp(a, b); }
+uint32_t tkv_debug_x8nmodp(uint64_t nbytes) { return x8nmodp(nbytes); }
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// Internal definitions shared by the CRC-32 kernels (tkv_crc32_kernels.hip) and the host runtime
+// (tkv_crc32_host.cpp). Not part of the public C ABI (include/tkv_crc32.h).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define TKV_HD __host__ __device__
+#else
+#define TKV_HD
+#endif
+
+namespace tkv {
+
+// CRC-32/ISO-HDLC parameters of frankie::core::crc32 (/root/reference/src/core/crc32.hpp:9-11).
+constexpr std::uint32_t kPoly = 0xEDB88320u;  // reflected polynomial
+constexpr std::uint32_t kInit = 0xFFFFFFFFu;  // init and xorout
+
+// Work decomposition of the row kernel.
+constexpr int kSeg = 64;                 // contiguous bytes one lane folds per row
+constexpr int kRow = 64 * kSeg;          // bytes one wave folds per row (4 KiB)
+constexpr int kWavesPerWG = 16;          // 1024-thread workgroups, one per CU (LDS-bound)
+constexpr int kThreads = 64 * kWavesPerWG;
+
+// LDS image (160 KiB, one workgroup per CU):
+//   words [0, 32768): slicing-by-4 tables T0..T3, each entry replicated 32x so lane c of every
+//                     32-lane half reads bank c: byte address = pair*64K + e*256 + t*128 + c*4,
+//                     table index = 2*pair + t.
+//   words [32768, 40960): lane-shift nibble tables LS[j][v][lane] (j nibble, v value).
+constexpr int kLdsSliceWords = 4 * 256 * 32;
+constexpr int kLdsLaneWords = 8 * 16 * 64;
+constexpr int kLdsWords = kLdsSliceWords + kLdsLaneWords;
+constexpr std::uint32_t kLdsLaneBase = kLdsSliceWords * 4u;  // byte offset of LS in LDS
+
+// Constant tables uploaded once per device (global memory, read by every workgroup prologue).
+struct DeviceTables {
+  std::uint32_t slice[4][256];          // slicing-by-4: T0 = Sarwate table, Tk[i] = Shift_1 o T(k-1)
+  std::uint32_t lane_shift[8][16][64];  // LS[j][v][l] = Shift_{(63-l)*kSeg}(v << 4j)
+  std::uint32_t horner[64];             // lanes 0..31: Shift_{kRow}(1 << l); lanes 32..63: 0
+  std::uint32_t row_pow[64];            // x^(8*kRow*2^k) mod P (reflected), k = 0..63
+  std::uint32_t head_shift[kRow + 1][32];  // [h][i] = Shift_h(1 << i): init injection at a head row
+};
+
+// One partial result of a block that was split between waves (irregular / huge-block path).
+struct Seam {
+  std::uint64_t block;
+  std::uint32_t partial;     // pure (init-0) CRC register of this wave's rows of the block
+  std::uint32_t rows_after;  // rows of the block that follow this piece
+  std::uint32_t flags;       // bit0 valid, bit1 piece contains row 0 (the block's head)
+  std::uint32_t pad[3];
+};
+constexpr std::uint32_t kSeamValid = 1u;
+constexpr std::uint32_t kSeamHasRow0 = 2u;
+
+struct RowsArgs {
+  const std::uint8_t* base;          // batch base pointer (device)
+  const std::uint64_t* offsets;      // irregular: byte offset of block b from base
+  const std::uint32_t* lengths;      // irregular: byte length of block b
+  const std::uint32_t* row_scan;     // irregular: exclusive scan of rows(b); [nblocks] = total
+  const std::uint32_t* wave_start;   // irregular: first block of wave w
+  std::uint64_t stride;              // uniform: block b at base + b*stride
+  std::uint32_t len;                 // uniform: every block's length
+  std::uint32_t head_z;              // uniform: x^(8h) mod P, h = head-row length of every block
+  const std::uint32_t* init_raw;     // nullable: per-block raw initial register
+  std::uint32_t init_default;        // initial register when init_raw == nullptr (kInit)
+  std::uint32_t out_xor;             // kInit: write finalize() values; 0: write raw registers
+  std::uint32_t* out;                // per-block result
+  Seam* seams;                       // 2 per wave
+  const DeviceTables* tabs;
+  const std::uint8_t* dummy;         // 256 zero bytes, target of loads outside any block
+  std::uint32_t nblocks;
+  std::uint32_t total_rows;          // uniform only (irregular reads row_scan[nblocks])
+  std::uint32_t nwaves;
+  std::uint32_t snap_blocks;         // uniform: partition by whole blocks (no seams)
+};
+
+// rows(b): wave-rows a block of n bytes occupies (every block, even n = 0, owns >= 1 row), and
+// h(b): bytes of its head row (row 0), in [0, kRow].
+TKV_HD inline std::uint32_t rows_for_len(std::uint32_t n) { return n == 0 ? 1u : (n - 1u) / kRow + 1u; }
+TKV_HD inline std::uint32_t head_len(std::uint32_t n) { return n - (rows_for_len(n) - 1u) * kRow; }
+
+// Host-side math shared with tests (tkv_crc32_host.cpp).
+std::uint32_t multmodp(std::uint32_t a, std::uint32_t b);   // a*b mod P, reflected
+std::uint32_t x8nmodp(std::uint64_t nbytes);                // x^(8n) mod P, reflected
+std::uint32_t shift_bytes(std::uint32_t reg, std::uint64_t nbytes);
+void build_tables(DeviceTables* t);
+
+}  // namespace tkv

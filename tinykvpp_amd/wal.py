@@ -1,0 +1,71 @@
+"""WAL record stamping and batched verification on the GPU CRC engine.
+
+Mirrors the CRC call sites of frankie::engine::wal_entry (/root/reference/src/engine/wal.cpp):
+  * encode (wal.cpp:19-61): record = u32 record_len | u32 crc32 | u8 op | u64 seq | u8 tombstone |
+    u32 key_len | u32 value_len | key | value (LE, packed, 26-byte header, wal.hpp:21-27);
+    record_len = size - 8; crc32 = crc32{}.update([8, size)).finalize() stored LE at offset 4.
+  * decode (wal.cpp:63-130): eof on empty input; corrupted when fewer than 26 bytes remain, when
+    record_len + 8 exceeds the input, on a CRC mismatch, or when key/value overflow the record.
+
+Here a whole slurped WAL (wal_reader::open, wal.cpp:204-240) is verified in ONE GPU batch after a
+host walk of the record_len chain (tkv_wal_verify), and many records are stamped in one batch
+(tkv_wal_stamp) — the recovery loop of engine::create (engine.cpp:31-53) and group commit.
+"""
+import ctypes
+import struct
+
+import numpy as np
+
+from ._lib import CORRUPTED, OK, check, load_library
+
+kMetadataSize = 26  # wal.hpp:21-27
+PUT, DEL = 0, 1     # wal_operation (wal.hpp:14-17)
+
+
+def encode_unstamped(op, seq, key, value, tombstone):
+    """Record bytes laid out as wal.cpp:30-52 with the CRC field left zero (wal.cpp:28 memset)."""
+    body = struct.pack("<BQBII", op, seq, int(bool(tombstone)), len(key), len(value)) + key + value
+    return struct.pack("<II", len(body), 0) + body
+
+
+def stamp(records):
+    """Stamp a list of unstamped records (bytes) in one batch; returns the stamped bytes list."""
+    if not records:
+        return []
+    sizes = np.array([len(r) for r in records], np.uint32)
+    offs = np.zeros(len(records), np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(records), np.uint8).copy()
+    check(load_library().tkv_wal_stamp(ctypes.c_void_p(buf.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                                       ctypes.c_void_p(sizes.ctypes.data), len(records)))
+    raw = buf.tobytes()
+    return [raw[int(o):int(o) + int(s)] for o, s in zip(offs, sizes)]
+
+
+def encode(op, seq, key, value, tombstone):
+    """wal_entry::encode: one stamped record (uses the batch path with n = 1)."""
+    return stamp([encode_unstamped(op, seq, key, value, tombstone)])[0]
+
+
+def verify(wal_bytes):
+    """Verify a slurped WAL image. Returns (status, n_good_records, stop_offset).
+
+    status is "ok" (every record verified, clean eof) or "corrupted" (first bad record at
+    stop_offset, the position wal_entry::decode leaves the view parked on, wal_test.cpp:809-850).
+    """
+    buf = np.frombuffer(bytes(wal_bytes), np.uint8)
+    good, stop = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    rc = load_library().tkv_wal_verify(ctypes.c_void_p(buf.ctypes.data) if buf.size else None, buf.size,
+                                       ctypes.byref(good), ctypes.byref(stop))
+    if rc not in (OK, CORRUPTED):
+        check(rc)
+    return ("ok" if rc == OK else "corrupted"), good.value, stop.value
+
+
+def decode_fields(rec):
+    """Header fields of one record (no checking): (record_len, crc, op, seq, tomb, key, value)."""
+    record_len, crc = struct.unpack_from("<II", rec, 0)
+    op, seq, tomb, klen, vlen = struct.unpack_from("<BQBII", rec, 8)
+    key = rec[kMetadataSize:kMetadataSize + klen]
+    value = rec[kMetadataSize + klen:kMetadataSize + klen + vlen]
+    return record_len, crc, op, seq, tomb, key, value
