@@ -1,0 +1,436 @@
+// Device-side building blocks of the CRC-32 row kernel (gfx950). Included by the product kernels
+// (tkv_crc32_kernels.hip) and by the variant explorer (tools/explore.hip).
+//
+// Notation: Shift_n(v) = CRC register after n zero bytes from v (= v * x^(8n) mod P, reflected);
+// crc_s(D) = Shift_|D|(s) ^ crc_0(D) — the register is affine in its initial value s.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "tkv_crc32_internal.h"
+
+namespace tkv {
+namespace dev {
+
+// Global (VMEM) and constant (SMEM) address-space views.
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef const v4u __attribute__((address_space(1))) g_v4u;
+typedef const std::uint32_t __attribute__((address_space(1))) g_u32;
+typedef const std::uint32_t __attribute__((address_space(4))) c_u32;
+typedef const std::uint64_t __attribute__((address_space(4))) c_u64;
+
+__device__ __forceinline__ uint4 gload16(std::uintptr_t p) {
+  const v4u v = *reinterpret_cast<g_v4u*>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ std::uint32_t sload32(const std::uint32_t* p, std::uint32_t i) {
+  return reinterpret_cast<c_u32*>(reinterpret_cast<std::uintptr_t>(p))[i];
+}
+__device__ __forceinline__ std::uint64_t sload64(const std::uint64_t* p, std::uint32_t i) {
+  return reinterpret_cast<c_u64*>(reinterpret_cast<std::uintptr_t>(p))[i];
+}
+__device__ __forceinline__ std::uint32_t lds_at(const std::uint32_t* lds, std::uint32_t byte_addr) {
+  return *reinterpret_cast<const std::uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
+}
+
+// Per-lane constants of the LDS table image (see kLds* in tkv_crc32_internal.h).
+struct LaneConst {
+  std::uint32_t L0, L1, L2, L3;  // slicing tables T0..T3: {byte0 = t*128 + c*4, byte2 = pair}
+  std::uint32_t lsbase;          // byte address of LS[0][0][lane]
+};
+
+__device__ __forceinline__ LaneConst lane_const(std::uint32_t lane) {
+  const std::uint32_t c4 = (lane & 31u) << 2;
+  return {c4, 128u + c4, 0x10000u + c4, 0x10080u + c4, kLdsLaneBase + lane * 4u};
+}
+
+// One slicing-by-4 step over a little-endian dword: crc ^= w; crc = T3[b0]^T2[b1]^T1[b2]^T0[b3].
+// v_perm_b32 drops byte j of x into byte1 of Lk (entry*256), giving the LDS byte address directly.
+__device__ __forceinline__ std::uint32_t slice4(const std::uint32_t* lds, std::uint32_t crc, std::uint32_t w,
+                                                const LaneConst& k) {
+  const std::uint32_t x = crc ^ w;
+  const std::uint32_t a0 = __builtin_amdgcn_perm(x, k.L3, 0x0C020400u);
+  const std::uint32_t a1 = __builtin_amdgcn_perm(x, k.L2, 0x0C020500u);
+  const std::uint32_t a2 = __builtin_amdgcn_perm(x, k.L1, 0x0C020600u);
+  const std::uint32_t a3 = __builtin_amdgcn_perm(x, k.L0, 0x0C020700u);
+  return (lds_at(lds, a0) ^ lds_at(lds, a1)) ^ (lds_at(lds, a2) ^ lds_at(lds, a3));
+}
+
+// Shift_{(63-lane)*64}(p): 8 lookups into this lane's nibble tables.
+__device__ __forceinline__ std::uint32_t lane_shift(const std::uint32_t* lds, std::uint32_t p, const LaneConst& k) {
+  std::uint32_t v = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v ^= lds_at(lds, k.lsbase + 4096u * j + (((p >> (4 * j)) & 15u) << 8));
+  return v;
+}
+
+// XOR of v over the 64 lanes, complete in lane 63 (DPP: within rows of 16, then row broadcasts).
+__device__ __forceinline__ std::uint32_t wave_xor_to_lane63(std::uint32_t v) {
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, false);  // row_mirror
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1,3
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2,3
+  return v;
+}
+
+// a*b mod P in the reflected representation (x^0 = 0x80000000).
+__device__ __forceinline__ std::uint32_t multmodp(std::uint32_t a, std::uint32_t b) {
+  std::uint32_t p = 0;
+  for (int i = 31; i >= 0; --i) {
+    if (a & (1u << i)) p ^= b;
+    b = (b & 1u) ? (b >> 1) ^ kPoly : (b >> 1);
+  }
+  return p;
+}
+
+// reg * x^(8*kRow*k) mod P.
+__device__ __forceinline__ std::uint32_t shift_rows(const DeviceTables* t, std::uint32_t reg, std::uint32_t k) {
+  std::uint32_t m = 0x80000000u;  // x^0
+  for (int i = 0; k != 0; ++i, k >>= 1)
+    if (k & 1u) m = multmodp(m, t->row_pow[i]);
+  return multmodp(m, reg);
+}
+
+struct Cursor {
+  std::uint32_t b;          // block index
+  std::uint32_t r;          // row within the block
+  std::uint32_t R;          // rows of the block
+  std::uint32_t n;          // bytes of the block
+  const std::uint8_t* blk;  // block start
+};
+
+template <bool UNIFORM>
+__device__ __forceinline__ void load_desc(const RowsArgs& a, Cursor& c) {
+  const std::uint32_t b = c.b < a.nblocks ? c.b : a.nblocks - 1;
+  if constexpr (UNIFORM) {
+    c.blk = a.base + static_cast<std::uint64_t>(b) * a.stride;
+    c.n = a.len;
+  } else {
+    c.blk = a.base + sload64(a.offsets, b);
+    c.n = sload32(a.lengths, b);
+  }
+  c.R = rows_for_len(c.n);
+}
+
+template <bool UNIFORM>
+__device__ __forceinline__ void advance(const RowsArgs& a, Cursor& c) {
+  if (++c.r == c.R) {
+    c.r = 0;
+    ++c.b;
+    load_desc<UNIFORM>(a, c);
+  }
+}
+
+// Loads of one row for this lane: NP aligned 16-byte pieces covering its 64-byte segment, and (for
+// irregular batches) its Shift_h constant when the row is a head row. Pieces outside the block and
+// rows past the wave's range read the zero `dummy` buffer.
+template <int NP>
+struct RowBuf {
+  uint4 q[NP];
+  std::uint32_t hs;
+};
+
+template <int NP, bool UNIFORM>
+__device__ __forceinline__ void issue_row(const RowsArgs& a, const Cursor& c, bool live, std::uint32_t lane,
+                                          RowBuf<NP>& rb) {
+  const std::int64_t rowstart =
+      static_cast<std::int64_t>(c.n) - static_cast<std::int64_t>(c.R - c.r) * kRow;
+  const std::uintptr_t blo = reinterpret_cast<std::uintptr_t>(c.blk);
+  const std::uintptr_t bhi = blo + c.n;
+  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
+  const std::uintptr_t seg = static_cast<std::uintptr_t>(static_cast<std::int64_t>(blo) + rowstart) + lane * kSeg;
+  const std::uintptr_t al = seg & ~static_cast<std::uintptr_t>(15);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const std::uintptr_t p = al + 16u * i;
+    const bool ok = live && (p + 16 > blo) && (p < bhi);
+    rb.q[i] = gload16(ok ? p : dmy);
+  }
+  if constexpr (!UNIFORM) {
+    const std::uintptr_t hp = reinterpret_cast<std::uintptr_t>(&a.tabs->head_shift[head_len(c.n)][lane & 31u]);
+    rb.hs = *reinterpret_cast<g_u32*>((live && c.r == 0) ? hp : dmy);
+  } else {
+    rb.hs = 0;
+  }
+}
+
+// The 16 little-endian dwords of this lane's 64-byte segment (realigned; head-row bytes in front of
+// the block zeroed — whole pieces in front of it were already loaded from `dummy`).
+template <bool ALIGNED, int NP>
+__device__ __forceinline__ void segment_dwords(const Cursor& c, const RowBuf<NP>& rb, std::uint32_t lane,
+                                               std::uint32_t (&dw)[16]) {
+  if constexpr (ALIGNED) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dw[4 * i + 0] = rb.q[i].x;
+      dw[4 * i + 1] = rb.q[i].y;
+      dw[4 * i + 2] = rb.q[i].z;
+      dw[4 * i + 3] = rb.q[i].w;
+    }
+  } else {
+    std::uint32_t raw[20];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      raw[4 * i + 0] = rb.q[i].x;
+      raw[4 * i + 1] = rb.q[i].y;
+      raw[4 * i + 2] = rb.q[i].z;
+      raw[4 * i + 3] = rb.q[i].w;
+    }
+    // Every segment of a block has the same misalignment (segments start at end - k*64).
+    const std::uint32_t s = static_cast<std::uint32_t>((reinterpret_cast<std::uintptr_t>(c.blk) + c.n) & 15u);
+    const std::uint32_t t = s & 3u;
+    if (s & 8u) {
+#pragma unroll
+      for (int i = 0; i < 18; ++i) raw[i] = raw[i + 2];
+    }
+    if (s & 4u) {
+#pragma unroll
+      for (int i = 0; i < 19; ++i) raw[i] = raw[i + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dw[k] = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], t);
+    const std::int32_t rowstart = static_cast<std::int32_t>(c.n - c.R * static_cast<std::uint32_t>(kRow));
+    if (c.r == 0 && rowstart < 0) {
+      const std::int32_t off0 = rowstart + static_cast<std::int32_t>(lane * kSeg);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const std::int32_t before = -(off0 + 4 * k);  // bytes of this dword in front of the block
+        const std::uint32_t sh = static_cast<std::uint32_t>(before < 0 ? 0 : (before > 4 ? 4 : before)) * 8u;
+        dw[k] &= static_cast<std::uint32_t>(0xFFFFFFFFull << sh);
+      }
+    }
+  }
+}
+
+// Per-wave state of the piece of a block the wave is folding.
+struct WaveState {
+  std::uint32_t B;          // running register of the current piece (Horner over rows)
+  bool piece_has_row0;      // the current piece started at the block's head row
+  bool first_piece;         // the current piece is the wave's first
+  std::uint32_t s_block[2], s_part[2], s_after[2], s_flags[2];
+};
+
+// Horner step + init injection + DPP reduction for one row whose lane contributions are v; emits
+// the block's result (or a seam record) when the row ends the block or the wave's range.
+template <bool UNIFORM>
+__device__ __forceinline__ void finish_row(const RowsArgs& a, const Cursor& c, std::uint32_t v, std::uint32_t hs,
+                                           std::uint32_t hcon, std::uint32_t lane, bool last_of_range,
+                                           WaveState& st) {
+  const bool lo_half = lane < 32u;
+  std::uint32_t init = 0;
+  if (c.r == 0) init = a.init_raw ? sload32(a.init_raw, c.b) : a.init_default;
+  std::uint32_t hk = hcon;
+  if constexpr (!UNIFORM) hk = lo_half ? hcon : hs;
+  // lanes 0..31: bit l of B times Shift_4096(1<<l); lanes 32..63 on a head row: bit l-32 of init
+  // times Shift_h(1<<(l-32)).
+  const std::uint32_t sel = lo_half ? st.B : init;
+  v ^= static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(sel), lane & 31u, 1)) & hk;
+  const std::uint32_t Bn = __builtin_amdgcn_readlane(wave_xor_to_lane63(v), 63);
+  if (c.r + 1 == c.R || last_of_range) {
+    if (st.piece_has_row0 && c.r + 1 == c.R) {
+      if (lane == 0) a.out[c.b] = Bn ^ a.out_xor;
+    } else {
+      // (explicit slots: a runtime index into these arrays would put them in scratch memory)
+      const std::uint32_t flags = kSeamValid | (st.piece_has_row0 ? kSeamHasRow0 : 0u);
+      if (st.first_piece) {
+        st.s_block[0] = c.b;
+        st.s_part[0] = Bn;
+        st.s_after[0] = c.R - 1 - c.r;
+        st.s_flags[0] = flags;
+      } else {
+        st.s_block[1] = c.b;
+        st.s_part[1] = Bn;
+        st.s_after[1] = c.R - 1 - c.r;
+        st.s_flags[1] = flags;
+      }
+    }
+    st.first_piece = false;
+    st.piece_has_row0 = true;
+    st.B = 0;
+  } else {
+    st.B = Bn;
+  }
+}
+
+// Fill the 160 KiB LDS table image (slicing tables replicated 32x, lane-shift nibble tables).
+__device__ __forceinline__ void fill_lds(const DeviceTables* tabs, std::uint32_t* lds) {
+  for (std::uint32_t i = threadIdx.x; i < kLdsSliceWords; i += blockDim.x) {
+    const std::uint32_t pair = i >> 14, e = (i >> 6) & 255u, t = (i >> 5) & 1u;
+    lds[i] = tabs->slice[2 * pair + t][e];
+  }
+  const std::uint32_t* ls = &tabs->lane_shift[0][0][0];
+  for (std::uint32_t i = threadIdx.x; i < kLdsLaneWords; i += blockDim.x) lds[kLdsSliceWords + i] = ls[i];
+}
+
+// MODE 0: CRC. MODE 1 (explorer only): same loads, XOR of the data instead of the CRC (memory
+// ceiling of this access pattern).
+template <bool ALIGNED, bool UNIFORM, int DEPTH, int ILP, int MODE>
+__device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
+  constexpr int NP = ALIGNED ? 4 : 5;
+  if constexpr (MODE == 0) fill_lds(a.tabs, lds);
+
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const LaneConst kc = lane_const(lane);
+  std::uint32_t hcon = a.tabs->horner[lane];
+  if constexpr (UNIFORM) {
+    if (lane >= 32u) hcon = multmodp(a.head_z, 1u << (lane - 32u));  // Shift_h(1 << (l-32))
+  }
+  __syncthreads();
+
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves;
+
+  // This wave's contiguous range of rows [g0, g1).
+  std::uint32_t g0, g1;
+  Cursor cur;
+  if constexpr (UNIFORM) {
+    const std::uint32_t R = rows_for_len(a.len);
+    if (a.snap_blocks) {
+      g0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W) * R;
+      g1 = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W) * R;
+    } else {
+      g0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.total_rows) / W);
+      g1 = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.total_rows) / W);
+    }
+    cur.b = g0 / R;
+    cur.r = g0 - cur.b * R;
+  } else {
+    const std::uint64_t TR = sload32(a.row_scan, a.nblocks);
+    g0 = static_cast<std::uint32_t>(wave * TR / W);
+    g1 = static_cast<std::uint32_t>((wave + 1) * TR / W);
+    cur.b = g0 < g1 ? sload32(a.wave_start, wave) : 0u;
+    cur.r = g0 < g1 ? g0 - sload32(a.row_scan, cur.b) : 0u;
+  }
+
+  WaveState st;
+  st.B = 0;
+  st.first_piece = true;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) st.s_block[s] = st.s_part[s] = st.s_after[s] = st.s_flags[s] = 0;
+
+  if (g0 < g1) {
+    load_desc<UNIFORM>(a, cur);
+    st.piece_has_row0 = cur.r == 0;
+
+    // Lane contribution of one row before the Horner step: Shift_{(63-l)*64}(crc_0(segment)).
+    auto lane_value = [&](const Cursor& c, const RowBuf<NP>& rb) -> std::uint32_t {
+      std::uint32_t dw[16];
+      segment_dwords<ALIGNED, NP>(c, rb, lane, dw);
+      if constexpr (MODE == 1) {
+        std::uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x ^= dw[k];
+        return x;
+      } else {
+        std::uint32_t p = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) p = slice4(lds, p, dw[k], kc);
+        return lane_shift(lds, p, kc);
+      }
+    };
+    // Two rows with their slicing chains interleaved (independent until the Horner step).
+    auto lane_value2 = [&](const Cursor& c0, const RowBuf<NP>& r0, const Cursor& c1, const RowBuf<NP>& r1,
+                           std::uint32_t& v0, std::uint32_t& v1) {
+      std::uint32_t d0[16], d1[16];
+      segment_dwords<ALIGNED, NP>(c0, r0, lane, d0);
+      segment_dwords<ALIGNED, NP>(c1, r1, lane, d1);
+      if constexpr (MODE == 1) {
+        v0 = v1 = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          v0 ^= d0[k];
+          v1 ^= d1[k];
+        }
+      } else {
+        std::uint32_t p0 = 0, p1 = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          p0 = slice4(lds, p0, d0[k], kc);
+          p1 = slice4(lds, p1, d1[k], kc);
+        }
+        v0 = lane_shift(lds, p0, kc);
+        v1 = lane_shift(lds, p1, kc);
+      }
+    };
+
+    RowBuf<NP> buf[DEPTH];
+    Cursor cq[DEPTH];
+    Cursor lc = cur;  // cursor of the next row to load
+    std::uint32_t gl = g0;
+#pragma unroll
+    for (int s = 0; s < DEPTH - ILP; ++s) {
+      cq[s] = lc;
+      issue_row<NP, UNIFORM>(a, lc, gl < g1, lane, buf[s]);
+      advance<UNIFORM>(a, lc);
+      ++gl;
+    }
+    for (std::uint32_t g = g0; g < g1; g += DEPTH) {
+#pragma unroll
+      for (int k = 0; k < DEPTH; k += ILP) {
+        // refill the slots freed by the previous step
+#pragma unroll
+        for (int j = 0; j < ILP; ++j) {
+          const int s = (k + DEPTH - ILP + j) % DEPTH;
+          cq[s] = lc;
+          issue_row<NP, UNIFORM>(a, lc, gl < g1, lane, buf[s]);
+          advance<UNIFORM>(a, lc);
+          ++gl;
+        }
+        const std::uint32_t gk = g + k;
+        if (gk >= g1) break;
+        if constexpr (ILP == 2) {
+          if (gk + 1 < g1) {
+            std::uint32_t v0, v1;
+            lane_value2(cq[k], buf[k], cq[k + 1], buf[k + 1], v0, v1);
+            finish_row<UNIFORM>(a, cq[k], v0, buf[k].hs, hcon, lane, false, st);
+            finish_row<UNIFORM>(a, cq[k + 1], v1, buf[k + 1].hs, hcon, lane, gk + 2 == g1, st);
+          } else {
+            const std::uint32_t v0 = lane_value(cq[k], buf[k]);
+            finish_row<UNIFORM>(a, cq[k], v0, buf[k].hs, hcon, lane, true, st);
+          }
+        } else {
+          const std::uint32_t v0 = lane_value(cq[k], buf[k]);
+          finish_row<UNIFORM>(a, cq[k], v0, buf[k].hs, hcon, lane, gk + 1 == g1, st);
+        }
+      }
+    }
+  }
+
+  if (lane == 0) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      Seam rec;
+      rec.block = st.s_block[s];
+      rec.partial = st.s_part[s];
+      rec.rows_after = st.s_after[s];
+      rec.flags = st.s_flags[s];
+      a.seams[2 * static_cast<std::uint64_t>(wave) + s] = rec;
+    }
+  }
+}
+
+// Combine the partials of blocks that were split between waves. One thread per wave; the thread
+// whose wave holds a block's head row walks the following waves' first pieces.
+__device__ __forceinline__ void crc_fixup_body(const RowsArgs& a) {
+  const std::uint64_t w = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+  if (w >= a.nwaves) return;
+  for (int slot = 0; slot < 2; ++slot) {
+    const Seam s = a.seams[2 * w + slot];
+    if ((s.flags & kSeamValid) == 0 || (s.flags & kSeamHasRow0) == 0) continue;
+    std::uint32_t acc = shift_rows(a.tabs, s.partial, s.rows_after);
+    std::uint32_t after = s.rows_after;
+    for (std::uint64_t ww = w + 1; after != 0 && ww < a.nwaves; ++ww) {
+      const Seam t = a.seams[2 * ww];
+      if ((t.flags & kSeamValid) == 0) continue;  // wave with an empty row range
+      acc ^= shift_rows(a.tabs, t.partial, t.rows_after);
+      after = t.rows_after;
+    }
+    a.out[s.block] = acc ^ a.out_xor;
+  }
+}
+
+}  // namespace dev
+}  // namespace tkv
