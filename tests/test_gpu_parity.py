@@ -162,6 +162,18 @@ def test_uniform_per_block_init(gpu, oracle):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("blen,n", [(4096, 4096), (8192, 4500), (12288, 9000), (65536, 4097)])
+def test_packed_fast_path(gpu, oracle, blen, n):
+    """len % 4 KiB == 0, stride == len, aligned, n >= waves: the crc_packed kernel."""
+    host = np.random.default_rng(blen + n).integers(0, 256, n * blen, dtype=np.uint8)
+    d = torch.from_numpy(host).to(gpu)
+    want = oracle.batch(host, np.arange(n) * blen, np.full(n, blen))
+    assert np.array_equal(u32(tk.crc32_batch_uniform(d, blen, n)), want)
+    init = np.random.default_rng(n).integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    got = u32(tk.crc32_batch_uniform(d, blen, n, init_raw=torch.from_numpy(init.view(np.int32)).to(gpu)))
+    assert np.array_equal(got, oracle.batch(host, np.arange(n) * blen, np.full(n, blen), init))
+
+
 def test_single_huge_block_split_across_waves(gpu, oracle):
     n = (64 << 20) + 77  # one block, rows spread over every wave, joined by crc_fixup
     host = np.random.default_rng(6).integers(0, 256, n, dtype=np.uint8)

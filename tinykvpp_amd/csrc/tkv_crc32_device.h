@@ -44,24 +44,34 @@ __device__ __forceinline__ LaneConst lane_const(std::uint32_t lane) {
   return {c4, 128u + c4, 0x10000u + c4, 0x10080u + c4, kLdsLaneBase + lane * 4u};
 }
 
+__device__ __forceinline__ std::uint32_t xor3(std::uint32_t a, std::uint32_t b, std::uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32 truth table 0x96 = a ^ b ^ c
+}
+
 // One slicing-by-4 step over a little-endian dword: crc ^= w; crc = T3[b0]^T2[b1]^T1[b2]^T0[b3].
 // v_perm_b32 drops byte j of x into byte1 of Lk (entry*256), giving the LDS byte address directly.
-__device__ __forceinline__ std::uint32_t slice4(const std::uint32_t* lds, std::uint32_t crc, std::uint32_t w,
-                                                const LaneConst& k) {
-  const std::uint32_t x = crc ^ w;
+// The register is carried split as crc = t ^ u so each step costs 2 v_bitop3 + 4 v_perm.
+struct Reg {
+  std::uint32_t t, u;
+  __device__ __forceinline__ std::uint32_t value() const { return t ^ u; }
+};
+
+__device__ __forceinline__ void slice4(const std::uint32_t* lds, Reg& r, std::uint32_t w, const LaneConst& k) {
+  const std::uint32_t x = xor3(r.t, r.u, w);
   const std::uint32_t a0 = __builtin_amdgcn_perm(x, k.L3, 0x0C020400u);
   const std::uint32_t a1 = __builtin_amdgcn_perm(x, k.L2, 0x0C020500u);
   const std::uint32_t a2 = __builtin_amdgcn_perm(x, k.L1, 0x0C020600u);
   const std::uint32_t a3 = __builtin_amdgcn_perm(x, k.L0, 0x0C020700u);
-  return (lds_at(lds, a0) ^ lds_at(lds, a1)) ^ (lds_at(lds, a2) ^ lds_at(lds, a3));
+  r.t = xor3(lds_at(lds, a0), lds_at(lds, a1), lds_at(lds, a2));
+  r.u = lds_at(lds, a3);
 }
 
 // Shift_{(63-lane)*64}(p): 8 lookups into this lane's nibble tables.
 __device__ __forceinline__ std::uint32_t lane_shift(const std::uint32_t* lds, std::uint32_t p, const LaneConst& k) {
-  std::uint32_t v = 0;
+  std::uint32_t l[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v ^= lds_at(lds, k.lsbase + 4096u * j + (((p >> (4 * j)) & 15u) << 8));
-  return v;
+  for (int j = 0; j < 8; ++j) l[j] = lds_at(lds, k.lsbase + 4096u * j + (((p >> (4 * j)) & 15u) << 8));
+  return xor3(xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5]), l[6] ^ l[7]);
 }
 
 // XOR of v over the 64 lanes, complete in lane 63 (DPP: within rows of 16, then row broadcasts).
@@ -325,10 +335,10 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
         for (int k = 0; k < 16; ++k) x ^= dw[k];
         return x;
       } else {
-        std::uint32_t p = 0;
+        Reg p{0, 0};
 #pragma unroll
-        for (int k = 0; k < 16; ++k) p = slice4(lds, p, dw[k], kc);
-        return lane_shift(lds, p, kc);
+        for (int k = 0; k < 16; ++k) slice4(lds, p, dw[k], kc);
+        return lane_shift(lds, p.value(), kc);
       }
     };
     // Two rows with their slicing chains interleaved (independent until the Horner step).
@@ -345,14 +355,14 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
           v1 ^= d1[k];
         }
       } else {
-        std::uint32_t p0 = 0, p1 = 0;
+        Reg p0{0, 0}, p1{0, 0};
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-          p0 = slice4(lds, p0, d0[k], kc);
-          p1 = slice4(lds, p1, d1[k], kc);
+          slice4(lds, p0, d0[k], kc);
+          slice4(lds, p1, d1[k], kc);
         }
-        v0 = lane_shift(lds, p0, kc);
-        v1 = lane_shift(lds, p1, kc);
+        v0 = lane_shift(lds, p0.value(), kc);
+        v1 = lane_shift(lds, p1.value(), kc);
       }
     };
 
@@ -408,6 +418,128 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
       rec.rows_after = st.s_after[s];
       rec.flags = st.s_flags[s];
       a.seams[2 * static_cast<std::uint64_t>(wave) + s] = rec;
+    }
+  }
+}
+
+// Packed uniform fast path: block b = [base + b*len, +len) with len a multiple of kRow (4 KiB) and
+// 16-byte aligned base, so every row is full, row g of the batch sits at base + g*kRow, and the
+// head length is kRow (init injection constants = the Horner constants). Each wave owns whole
+// blocks [b0, b1) (no seams), keeps ILP rows' slicing chains interleaved, DEPTH-ILP rows in flight,
+// and stores its results 64 at a time (lane k holds the k-th block's value).
+template <int DEPTH, int ILP>
+__device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
+  fill_lds(a.tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const LaneConst kc = lane_const(lane);
+  const std::uint32_t hcon = a.tabs->horner[lane & 31u];  // Shift_4096(1 << (l & 31))
+  const bool lo_half = lane < 32u;
+  // Init injection term for blocks without a per-block init: bit (l-32) of init * Shift_4096(...)
+  const std::uint32_t inj_const =
+      lo_half ? 0u
+              : static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(a.init_default),
+                                                                lane & 31u, 1)) & hcon;
+  __syncthreads();
+
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves;
+  const std::uint32_t R = a.len / kRow;
+  const std::uint32_t b0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W);
+  const std::uint32_t b1 = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W);
+  if (b0 >= b1) return;
+  const std::uint32_t g0 = b0 * R, g1 = b1 * R;
+  const std::uintptr_t lane_base = reinterpret_cast<std::uintptr_t>(a.base) + lane * kSeg;
+
+  uint4 buf[DEPTH][4];
+  auto issue = [&](std::uint32_t g, uint4 (&q)[4]) {
+    const std::uint32_t gc = g < g1 ? g : g1 - 1;  // rows past the range reload the last one
+    const std::uintptr_t p = lane_base + static_cast<std::uint64_t>(gc) * kRow;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i);
+  };
+  auto dwords = [&](const uint4 (&q)[4], std::uint32_t (&dw)[16]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dw[4 * i + 0] = q[i].x;
+      dw[4 * i + 1] = q[i].y;
+      dw[4 * i + 2] = q[i].z;
+      dw[4 * i + 3] = q[i].w;
+    }
+  };
+
+  std::uint32_t B = 0;     // running register of the current block (Horner over its rows)
+  std::uint32_t r = 0;     // row within the current block
+  std::uint32_t b = b0;    // current block
+  std::uint32_t keep = 0;  // lane k: result of block (b & ~63) + k
+  auto finish = [&](std::uint32_t v) {
+    std::uint32_t term;
+    if (r == 0) {
+      term = inj_const;
+      if (a.init_raw) {
+        const std::uint32_t init = sload32(a.init_raw, b);
+        term = lo_half ? 0u : static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init),
+                                                                                lane & 31u, 1)) & hcon;
+      }
+    } else {
+      term = lo_half ? static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(B), lane, 1)) & hcon
+                     : 0u;
+    }
+    const std::uint32_t Bn = __builtin_amdgcn_readlane(wave_xor_to_lane63(v ^ term), 63);
+    if (++r == R) {
+      const std::uint32_t k = (b - b0) & 63u;
+      if (lane == k) keep = Bn ^ a.out_xor;
+      if (k == 63u || b + 1 == b1) {
+        const std::uint32_t first = b - k;  // b - ((b - b0) & 63)
+        if (lane <= k) a.out[first + lane] = keep;
+      }
+      r = 0;
+      ++b;
+      B = 0;
+    } else {
+      B = Bn;
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < DEPTH - ILP; ++s) issue(g0 + s, buf[s]);
+  for (std::uint32_t g = g0; g < g1; g += DEPTH) {
+#pragma unroll
+    for (int k = 0; k < DEPTH; k += ILP) {
+#pragma unroll
+      for (int j = 0; j < ILP; ++j) issue(g + k + DEPTH - ILP + j, buf[(k + DEPTH - ILP + j) % DEPTH]);
+      const std::uint32_t gk = g + k;
+      if (gk >= g1) break;
+      if (gk + ILP <= g1) {
+        std::uint32_t dw[ILP][16];
+        Reg p[ILP];
+#pragma unroll
+        for (int j = 0; j < ILP; ++j) {
+          dwords(buf[k + j], dw[j]);
+          p[j] = Reg{0, 0};
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+#pragma unroll
+          for (int j = 0; j < ILP; ++j) slice4(lds, p[j], dw[j][i], kc);
+        std::uint32_t v[ILP];
+#pragma unroll
+        for (int j = 0; j < ILP; ++j) v[j] = lane_shift(lds, p[j].value(), kc);
+#pragma unroll
+        for (int j = 0; j < ILP; ++j) finish(v[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < ILP; ++j) {  // tail: fewer than ILP rows left
+          if (gk + j < g1) {
+            std::uint32_t dw[16];
+            dwords(buf[k + j], dw);
+            Reg p{0, 0};
+#pragma unroll
+            for (int i = 0; i < 16; ++i) slice4(lds, p, dw[i], kc);
+            finish(lane_shift(lds, p.value(), kc));
+          }
+        }
+      }
     }
   }
 }

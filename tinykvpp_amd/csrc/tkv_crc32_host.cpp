@@ -22,6 +22,7 @@ namespace tkv {
 // ---- launchers (tkv_crc32_kernels.hip) ---------------------------------------------------------
 hipError_t launch_rows(const RowsArgs& a, bool aligned, bool uniform, unsigned grid, hipStream_t st);
 hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
+hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st);
 hipError_t launch_prepass(const std::uint32_t* lengths, std::uint32_t n, std::uint32_t* row_scan,
                           std::uint32_t* tile_sums, std::uint32_t* wave_start, std::uint32_t W, hipStream_t st);
 std::uint32_t prepass_tiles(std::uint32_t n);
@@ -223,6 +224,10 @@ int run_uniform(DevCtx* c, const std::uint8_t* d_base, std::uint64_t stride, std
   a.nwaves = static_cast<std::uint32_t>(grid * kWavesPerWG);
   a.snap_blocks = n >= a.nwaves ? 1u : 0u;
   const bool aligned = (reinterpret_cast<std::uintptr_t>(d_base) % 16 == 0) && (stride % 16 == 0) && (len % 16 == 0);
+  if (aligned && a.snap_blocks && len != 0 && len % kRow == 0 && stride == len) {
+    TKV_HIP(launch_packed(a, static_cast<unsigned>(grid), st));  // whole blocks per wave, no seams
+    return TKV_OK;
+  }
   TKV_HIP(launch_rows(a, aligned, true, static_cast<unsigned>(grid), st));
   if (!a.snap_blocks) TKV_HIP(launch_fixup(a, st));
   return TKV_OK;

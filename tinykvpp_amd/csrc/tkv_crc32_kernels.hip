@@ -42,6 +42,15 @@ __global__ __launch_bounds__(kThreads) void crc_rows(RowsArgs a) {
   dev::crc_rows_body<ALIGNED, UNIFORM, Shape<ALIGNED>::kDepth, Shape<ALIGNED>::kIlp, 0>(a, lds);
 }
 
+// Packed uniform batches (len % 4 KiB == 0, stride == len, 16-byte aligned): DESIGN.md §4.
+constexpr int kPackedDepth = 4;
+constexpr int kPackedIlp = 2;
+
+__global__ __launch_bounds__(kThreads) void crc_packed(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  dev::crc_packed_body<kPackedDepth, kPackedIlp>(a, lds);
+}
+
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 
 }  // namespace
@@ -159,6 +168,11 @@ hipError_t launch_rows(const RowsArgs& a, bool aligned, bool uniform, unsigned g
   } else {
     hipLaunchKernelGGL((crc_rows<false, false>), dim3(grid), dim3(kThreads), 0, st, a);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st) {
+  hipLaunchKernelGGL(crc_packed, dim3(grid), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 

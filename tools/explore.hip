@@ -26,6 +26,65 @@ __global__ __launch_bounds__(256) void k_stream(const uint4* p, std::uint64_t n1
   if (x == 0x12345678u) out[0] = x;  // keep the loads alive
 }
 
+
+// Memory-pattern probe: uniform aligned batch, each wave owns a contiguous range of 4 KiB rows
+// (same partition as crc_rows), DEPTH rows of 4 x 16-byte loads in flight per lane.
+// PAT 0: lane l reads bytes [64l, 64l+64) of the row (the production segment layout)
+// PAT 1: fully coalesced, load i reads [1024i + 16l, +16)
+// PAT 2: lane l reads [2048(i/2) + 32l + 16(i%2), +16) (32-byte lane segments)
+// FIN 0: XOR into a register, one store per wave; FIN 1: per-row DPP reduce + lane-0 store per row;
+// FIN 2: per-row reduce, results kept in lane (row % 64) and stored 64 at a time (coalesced).
+template <int PAT, int DEPTH, int FIN>
+__global__ __launch_bounds__(1024) void k_pat(const std::uint8_t* base, std::uint32_t nrows, std::uint32_t W,
+                                              std::uint32_t* out) {
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint32_t wave = blockIdx.x * 16 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t g0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(nrows) / W);
+  const std::uint32_t g1 = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(nrows) / W);
+  auto addr = [&](std::uint32_t g, int i) -> std::uintptr_t {
+    const std::uintptr_t rb = reinterpret_cast<std::uintptr_t>(base) + static_cast<std::uint64_t>(g < g1 ? g : g0) * 4096u;
+    if constexpr (PAT == 0) return rb + 64u * lane + 16u * i;
+    else if constexpr (PAT == 1) return rb + 1024u * i + 16u * lane;
+    else return rb + 2048u * (i / 2) + 32u * lane + 16u * (i % 2);
+  };
+  uint4 buf[DEPTH][4];
+  std::uint32_t acc = 0, keep = 0;
+#pragma unroll
+  for (int s = 0; s < DEPTH - 1; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) buf[s][i] = dev::gload16(addr(g0 + s, i));
+  for (std::uint32_t g = g0; g < g1; g += DEPTH) {
+#pragma unroll
+    for (int k = 0; k < DEPTH; ++k) {
+      const int s = (k + DEPTH - 1) % DEPTH;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) buf[s][i] = dev::gload16(addr(g + k + DEPTH - 1, i));
+      if (g + k >= g1) break;
+      std::uint32_t x = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x ^= buf[k][i].x ^ buf[k][i].y ^ buf[k][i].z ^ buf[k][i].w;
+      if constexpr (FIN == 0) {
+        acc ^= x;
+      } else {
+        const std::uint32_t r = __builtin_amdgcn_readlane(dev::wave_xor_to_lane63(x), 63);
+        if constexpr (FIN == 1) {
+          if (lane == 0) out[g + k] = r;
+        } else {
+          const std::uint32_t gi = g + k;
+          if (lane == (gi & 63u)) keep = r;
+          if ((gi & 63u) == 63u || gi + 1 == g1) {
+            const std::uint32_t first = gi & ~63u;
+            if (first + lane >= g0 && first + lane <= gi) out[first + lane] = keep;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (FIN == 0) {
+    if (acc == 0x9E3779B9u) out[0] = acc;
+  }
+}
+
 namespace {
 DeviceTables* g_tabs = nullptr;
 std::uint8_t* g_dummy = nullptr;
@@ -42,11 +101,33 @@ void L(RowsArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_rows<D, I, M>), dim3(g_ncu), dim3(kThreads), 0, s, a);
 }
 
+template <int PAT, int D, int F>
+void P(RowsArgs a, hipStream_t s) {
+  hipLaunchKernelGGL((k_pat<PAT, D, F>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows, a.nwaves, a.out);
+}
+
+template <int D, int I>
+__global__ __launch_bounds__(kThreads) void k_packed(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  dev::crc_packed_body<D, I>(a, lds);
+}
+
+template <int D, int I>
+void PK(RowsArgs a, hipStream_t s) {
+  hipLaunchKernelGGL((k_packed<D, I>), dim3(g_ncu), dim3(kThreads), 0, s, a);
+}
+
 const V kVariants[] = {
+    {"packed D2 I1", PK<2, 1>}, {"packed D3 I1", PK<3, 1>}, {"packed D4 I2", PK<4, 2>}, {"packed D6 I2", PK<6, 2>},
+    {"packed D6 I3", PK<6, 3>}, {"packed D8 I4", PK<8, 4>}, {"packed D4 I1", PK<4, 1>},
     {"crc D2 I1", L<2, 1, 0>}, {"crc D3 I1", L<3, 1, 0>}, {"crc D4 I1", L<4, 1, 0>},
-    {"crc D4 I2", L<4, 2, 0>}, {"crc D6 I2", L<6, 2, 0>}, {"crc D6 I3", L<6, 3, 0>},
+    {"crc D4 I2", L<4, 2, 0>}, {"crc D6 I2", L<6, 2, 0>},
     {"mem D2 I1", L<2, 1, 1>}, {"mem D4 I1", L<4, 1, 1>}, {"mem D4 I2", L<4, 2, 1>},
     {"mem D8 I1", L<8, 1, 1>},
+    {"pat seg64 D2 fin0", P<0, 2, 0>}, {"pat seg64 D4 fin0", P<0, 4, 0>}, {"pat seg64 D4 fin1", P<0, 4, 1>},
+    {"pat seg64 D4 fin2", P<0, 4, 2>}, {"pat coal D2 fin0", P<1, 2, 0>}, {"pat coal D4 fin0", P<1, 4, 0>},
+    {"pat coal D4 fin1", P<1, 4, 1>}, {"pat coal D4 fin2", P<1, 4, 2>}, {"pat seg32 D4 fin0", P<2, 4, 0>},
+    {"pat seg32 D4 fin2", P<2, 4, 2>}, {"pat coal D6 fin0", P<1, 6, 0>}, {"pat seg64 D6 fin0", P<0, 6, 0>},
 };
 constexpr int kNV = sizeof(kVariants) / sizeof(kVariants[0]);
 }  // namespace
