@@ -34,6 +34,21 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
+def rank_shard(rank, nblocks):
+    """Weak scaling: rank r checksums global synthetic blocks [r*nblocks, (r+1)*nblocks)."""
+    return rank * nblocks, nblocks
+
+
+def reduce_timing(elapsed, kernel_ms, bit_exact, dist, dev=None):
+    """Max over ranks of wall time and per-launch time; AND of the ranks' bit-exact checks."""
+    import torch
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ok = torch.tensor([1 if bit_exact else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return float(t[0]), float(t[1]), bool(ok.item())
+
+
 def load_oracle():
     o = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
     o.oracle_crc_synthetic.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_void_p]
@@ -114,7 +129,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     nblocks, blen, desc = CONFIGS[args.config]
-    first = rank * nblocks  # weak scaling: every rank owns its own nblocks blocks
+    first, nblocks = rank_shard(rank, nblocks)
     data = torch.empty(nblocks * blen, dtype=torch.uint8, device=dev)
     out = torch.empty(nblocks, dtype=torch.int32, device=dev)
     tk.fill_synthetic_uniform(data, blen, nblocks, first_block=first)
@@ -152,12 +167,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
-        ok = torch.tensor([1 if bit_exact else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        bit_exact = bool(ok.item())
+        elapsed, kernel_ms, bit_exact = reduce_timing(elapsed, kernel_ms, bit_exact, dist, dev)
 
     bytes_per_step = nblocks * blen
     total_bytes = bytes_per_step * args.steps * world

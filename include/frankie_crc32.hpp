@@ -1,0 +1,74 @@
+// frankie_crc32.hpp — drop-in replacement for tinykvpp's src/core/crc32.hpp (+ crc32.cpp).
+//
+// Keeps the reference's C++ surface exactly (/root/reference/src/core/crc32.hpp:9-49): namespace
+// frankie::core, the kCRC32* constants, crc32_table, the constexpr generate_crc32_table(), and
+// class crc32 with constexpr default ctor, [[nodiscard]] crc32& update(span<const byte>) noexcept,
+// [[nodiscard]] uint32_t finalize() const noexcept and void reset() noexcept — so wal.cpp's
+// `core::crc32{}.update({...}).finalize()` (wal.cpp:54-57, 89-92) and test/crc32_test.cpp compile
+// unchanged. update() forwards to the C ABI (tkv_crc32_update, include/tkv_crc32.h), which runs the
+// gfx950 HIP kernel; there is no CPU implementation behind it. The reference's update is noexcept
+// with no error path, so a device failure is reported on stderr and aborts (a wrong checksum would
+// be worse than a crash for an integrity routine).
+//
+// Build: add include/ to the include path and link libtkv_crc32.so.
+#pragma once
+
+#include <array>
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <span>
+
+#include "tkv_crc32.h"
+
+namespace frankie::core {
+
+constexpr std::uint32_t kCRC32DefaultValue{TKV_CRC32_DEFAULT_RAW};  // crc32.hpp:9
+constexpr std::uint32_t kCRC32Bits{8};                               // crc32.hpp:10
+constexpr std::uint32_t kCRC32Polynomial = TKV_CRC32_POLYNOMIAL;     // crc32.hpp:11
+
+constexpr std::size_t kCRC32TableSize{256};                        // crc32.hpp:13
+using crc32_table = std::array<std::uint32_t, kCRC32TableSize>;     // crc32.hpp:14
+
+// Byte-at-a-time table of the reflected polynomial, usable in constant expressions
+// (crc32_test.cpp:83 evaluates it with constexpr).
+constexpr auto generate_crc32_table() noexcept -> crc32_table {
+  crc32_table t{};
+  for (std::size_t e = 0; e < t.size(); ++e) {
+    std::uint32_t v = static_cast<std::uint32_t>(e);
+    for (std::uint32_t k = 0; k < kCRC32Bits; ++k) v = (v >> 1) ^ ((v & 1u) != 0 ? kCRC32Polynomial : 0u);
+    t[e] = v;
+  }
+  return t;
+}
+
+class crc32 final {
+ public:
+  constexpr crc32() = default;
+
+  // Continues the stored register over `data` without XORing with 0xFFFFFFFF (crc32.cpp:9-16).
+  [[nodiscard]] crc32 &update(std::span<const std::byte> data) noexcept {
+    std::uint32_t next = crc_;
+    const int rc = tkv_crc32_update(crc_, data.data(), data.size(), &next);
+    if (rc != TKV_OK) {
+      std::fprintf(stderr, "frankie::core::crc32::update: GPU CRC failed (status %d): %s\n", rc, tkv_last_error());
+      std::abort();
+    }
+    crc_ = next;
+    return *this;
+  }
+
+  // Stored register XOR 0xFFFFFFFF (crc32.cpp:19).
+  [[nodiscard]] std::uint32_t finalize() const noexcept { return crc_ ^ kCRC32DefaultValue; }
+
+  // Register back to 0xFFFFFFFF (crc32.cpp:22).
+  void reset() noexcept { crc_ = kCRC32DefaultValue; }
+
+ private:
+  static constexpr const auto TABLE{generate_crc32_table()};  // crc32.hpp:46 (kept for layout parity)
+
+  std::uint32_t crc_{kCRC32DefaultValue};
+};
+
+}  // namespace frankie::core

@@ -23,6 +23,11 @@ __device__ __forceinline__ uint4 gload16(std::uintptr_t p) {
   const v4u v = *reinterpret_cast<g_v4u*>(p);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// Non-temporal variant (global_load_dwordx4 ... nt): streamed bytes are read exactly once.
+__device__ __forceinline__ uint4 gload16_nt(std::uintptr_t p) {
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<g_v4u*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ std::uint32_t sload32(const std::uint32_t* p, std::uint32_t i) {
   return reinterpret_cast<c_u32*>(reinterpret_cast<std::uintptr_t>(p))[i];
 }
@@ -423,11 +428,11 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
 }
 
 // Packed uniform fast path: block b = [base + b*len, +len) with len a multiple of kRow (4 KiB) and
-// 16-byte aligned base, so every row is full, row g of the batch sits at base + g*kRow, and the
-// head length is kRow (init injection constants = the Horner constants). Each wave owns whole
-// blocks [b0, b1) (no seams), keeps ILP rows' slicing chains interleaved, DEPTH-ILP rows in flight,
-// and stores its results 64 at a time (lane k holds the k-th block's value).
-template <int DEPTH, int ILP>
+// 16-byte aligned base, so every row is full and the head length is kRow (init injection constants
+// = the Horner constants). Each wave owns whole blocks (no seams): a contiguous range [b0, b1), or
+// with STRIDED the blocks w, w+W, w+2W, ...; it keeps ILP rows' slicing chains interleaved and
+// DEPTH-ILP rows in flight, and stores its results 64 at a time (lane k holds its k-th block).
+template <int DEPTH, int ILP, bool NT, bool STRIDED>
 __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
   fill_lds(a.tabs, lds);
@@ -443,20 +448,30 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
   __syncthreads();
 
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const std::uint64_t W = a.nwaves;
+  const std::uint32_t W = a.nwaves;
   const std::uint32_t R = a.len / kRow;
-  const std::uint32_t b0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W);
-  const std::uint32_t b1 = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W);
-  if (b0 >= b1) return;
-  const std::uint32_t g0 = b0 * R, g1 = b1 * R;
+  std::uint32_t b0, nb;  // first block, number of blocks of this wave
+  if constexpr (STRIDED) {
+    b0 = wave;
+    nb = wave < a.nblocks ? (a.nblocks - 1 - wave) / W + 1 : 0u;
+  } else {
+    b0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W);
+    nb = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W) - b0;
+  }
+  if (nb == 0) return;
+  const std::uint32_t nrows = nb * R;  // wave-local rows j = 0 .. nrows-1
   const std::uintptr_t lane_base = reinterpret_cast<std::uintptr_t>(a.base) + lane * kSeg;
+  const std::uint64_t bstride = STRIDED ? static_cast<std::uint64_t>(W) * a.len : a.len;
+  auto blk_of = [&](std::uint32_t k) -> std::uint32_t { return STRIDED ? b0 + k * W : b0 + k; };
 
   uint4 buf[DEPTH][4];
-  auto issue = [&](std::uint32_t g, uint4 (&q)[4]) {
-    const std::uint32_t gc = g < g1 ? g : g1 - 1;  // rows past the range reload the last one
-    const std::uintptr_t p = lane_base + static_cast<std::uint64_t>(gc) * kRow;
+  auto issue = [&](std::uint32_t j, uint4 (&q)[4]) {
+    const std::uint32_t jc = j < nrows ? j : nrows - 1;  // rows past the range reload the last one
+    const std::uint32_t k = jc / R, r = jc - k * R;
+    const std::uintptr_t p = lane_base + static_cast<std::uint64_t>(b0) * a.len + k * bstride +
+                             static_cast<std::uint64_t>(r) * kRow;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i);
+    for (int i = 0; i < 4; ++i) q[i] = NT ? gload16_nt(p + 16u * i) : gload16(p + 16u * i);
   };
   auto dwords = [&](const uint4 (&q)[4], std::uint32_t (&dw)[16]) {
 #pragma unroll
@@ -470,14 +485,14 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
 
   std::uint32_t B = 0;     // running register of the current block (Horner over its rows)
   std::uint32_t r = 0;     // row within the current block
-  std::uint32_t b = b0;    // current block
-  std::uint32_t keep = 0;  // lane k: result of block (b & ~63) + k
+  std::uint32_t k = 0;     // wave-local index of the current block
+  std::uint32_t keep = 0;  // lane i: result of wave-local block (k & ~63) + i
   auto finish = [&](std::uint32_t v) {
     std::uint32_t term;
     if (r == 0) {
       term = inj_const;
       if (a.init_raw) {
-        const std::uint32_t init = sload32(a.init_raw, b);
+        const std::uint32_t init = sload32(a.init_raw, blk_of(k));
         term = lo_half ? 0u : static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init),
                                                                                 lane & 31u, 1)) & hcon;
       }
@@ -487,14 +502,14 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
     }
     const std::uint32_t Bn = __builtin_amdgcn_readlane(wave_xor_to_lane63(v ^ term), 63);
     if (++r == R) {
-      const std::uint32_t k = (b - b0) & 63u;
-      if (lane == k) keep = Bn ^ a.out_xor;
-      if (k == 63u || b + 1 == b1) {
-        const std::uint32_t first = b - k;  // b - ((b - b0) & 63)
-        if (lane <= k) a.out[first + lane] = keep;
+      const std::uint32_t slot = k & 63u;
+      if (lane == slot) keep = Bn ^ a.out_xor;
+      if (slot == 63u || k + 1 == nb) {
+        const std::uint32_t first = k - slot;
+        if (lane <= slot) a.out[blk_of(first + lane)] = keep;
       }
       r = 0;
-      ++b;
+      ++k;
       B = 0;
     } else {
       B = Bn;
@@ -502,40 +517,40 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
   };
 
 #pragma unroll
-  for (int s = 0; s < DEPTH - ILP; ++s) issue(g0 + s, buf[s]);
-  for (std::uint32_t g = g0; g < g1; g += DEPTH) {
+  for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
+  for (std::uint32_t j = 0; j < nrows; j += DEPTH) {
 #pragma unroll
-    for (int k = 0; k < DEPTH; k += ILP) {
+    for (int q = 0; q < DEPTH; q += ILP) {
 #pragma unroll
-      for (int j = 0; j < ILP; ++j) issue(g + k + DEPTH - ILP + j, buf[(k + DEPTH - ILP + j) % DEPTH]);
-      const std::uint32_t gk = g + k;
-      if (gk >= g1) break;
-      if (gk + ILP <= g1) {
+      for (int i = 0; i < ILP; ++i) issue(j + q + DEPTH - ILP + i, buf[(q + DEPTH - ILP + i) % DEPTH]);
+      const std::uint32_t jq = j + q;
+      if (jq >= nrows) break;
+      if (jq + ILP <= nrows) {
         std::uint32_t dw[ILP][16];
         Reg p[ILP];
 #pragma unroll
-        for (int j = 0; j < ILP; ++j) {
-          dwords(buf[k + j], dw[j]);
-          p[j] = Reg{0, 0};
+        for (int i = 0; i < ILP; ++i) {
+          dwords(buf[q + i], dw[i]);
+          p[i] = Reg{0, 0};
         }
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
+        for (int t = 0; t < 16; ++t)
 #pragma unroll
-          for (int j = 0; j < ILP; ++j) slice4(lds, p[j], dw[j][i], kc);
+          for (int i = 0; i < ILP; ++i) slice4(lds, p[i], dw[i][t], kc);
         std::uint32_t v[ILP];
 #pragma unroll
-        for (int j = 0; j < ILP; ++j) v[j] = lane_shift(lds, p[j].value(), kc);
+        for (int i = 0; i < ILP; ++i) v[i] = lane_shift(lds, p[i].value(), kc);
 #pragma unroll
-        for (int j = 0; j < ILP; ++j) finish(v[j]);
+        for (int i = 0; i < ILP; ++i) finish(v[i]);
       } else {
 #pragma unroll
-        for (int j = 0; j < ILP; ++j) {  // tail: fewer than ILP rows left
-          if (gk + j < g1) {
+        for (int i = 0; i < ILP; ++i) {  // tail: fewer than ILP rows left
+          if (jq + i < nrows) {
             std::uint32_t dw[16];
-            dwords(buf[k + j], dw);
+            dwords(buf[q + i], dw);
             Reg p{0, 0};
 #pragma unroll
-            for (int i = 0; i < 16; ++i) slice4(lds, p, dw[i], kc);
+            for (int t = 0; t < 16; ++t) slice4(lds, p, dw[t], kc);
             finish(lane_shift(lds, p.value(), kc));
           }
         }

@@ -48,7 +48,7 @@ constexpr int kPackedIlp = 2;
 
 __global__ __launch_bounds__(kThreads) void crc_packed(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<kPackedDepth, kPackedIlp>(a, lds);
+  dev::crc_packed_body<kPackedDepth, kPackedIlp, false, false>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }

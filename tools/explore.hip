@@ -106,20 +106,25 @@ void P(RowsArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_pat<PAT, D, F>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows, a.nwaves, a.out);
 }
 
-template <int D, int I>
-__global__ __launch_bounds__(kThreads) void k_packed(RowsArgs a) {
+template <int D, int I, bool NT, bool ST, int T>
+__global__ __launch_bounds__(T) void k_packed(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<D, I>(a, lds);
+  dev::crc_packed_body<D, I, NT, ST>(a, lds);
 }
 
-template <int D, int I>
+template <int D, int I, bool NT = false, bool ST = false, int T = 1024>
 void PK(RowsArgs a, hipStream_t s) {
-  hipLaunchKernelGGL((k_packed<D, I>), dim3(g_ncu), dim3(kThreads), 0, s, a);
+  a.nwaves = g_ncu * (T / 64);
+  hipLaunchKernelGGL((k_packed<D, I, NT, ST, T>), dim3(g_ncu), dim3(T), 0, s, a);
 }
 
 const V kVariants[] = {
-    {"packed D2 I1", PK<2, 1>}, {"packed D3 I1", PK<3, 1>}, {"packed D4 I2", PK<4, 2>}, {"packed D6 I2", PK<6, 2>},
-    {"packed D6 I3", PK<6, 3>}, {"packed D8 I4", PK<8, 4>}, {"packed D4 I1", PK<4, 1>},
+    {"packed D4 I2", PK<4, 2>}, {"packed D4 I1", PK<4, 1>}, {"packed D3 I1", PK<3, 1>},
+    {"packed D4 I2 nt", PK<4, 2, true>}, {"packed D4 I1 nt", PK<4, 1, true>},
+    {"packed D4 I2 strided", PK<4, 2, false, true>}, {"packed D4 I2 nt strided", PK<4, 2, true, true>},
+    {"packed T512 D8 I4", PK<8, 4, false, false, 512>}, {"packed T512 D6 I3", PK<6, 3, false, false, 512>},
+    {"packed T512 D6 I2", PK<6, 2, false, false, 512>}, {"packed T512 D8 I4 nt", PK<8, 4, true, false, 512>},
+    {"packed T768 D6 I2", PK<6, 2, false, false, 768>},
     {"crc D2 I1", L<2, 1, 0>}, {"crc D3 I1", L<3, 1, 0>}, {"crc D4 I1", L<4, 1, 0>},
     {"crc D4 I2", L<4, 2, 0>}, {"crc D6 I2", L<6, 2, 0>},
     {"mem D2 I1", L<2, 1, 1>}, {"mem D4 I1", L<4, 1, 1>}, {"mem D4 I2", L<4, 2, 1>},
