@@ -27,9 +27,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
-    # name: (nblocks, block_len, description) — BASELINE.json configs
+    # name: (nblocks, block_len, description) — BASELINE.json configs; cfg4's lengths are Zipf
     "cfg2": (1 << 20, 4096, "1 M x 4 KiB WAL-record-sized blocks, device-resident"),
     "cfg3": (1 << 18, 65536, "256 K x 64 KiB SSTable data blocks, device-resident"),
+    "cfg4": (1 << 17, None, "131072 blocks, Zipf sizes 256 B - 1 MiB packed back to back (unaligned), "
+                            "device-resident, irregular-length path"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
@@ -130,21 +132,43 @@ def main():
 
     nblocks, blen, desc = CONFIGS[args.config]
     first, nblocks = rank_shard(rank, nblocks)
-    data = torch.empty(nblocks * blen, dtype=torch.uint8, device=dev)
+    ora = load_oracle()
+    stream = torch.cuda.current_stream()
     out = torch.empty(nblocks, dtype=torch.int32, device=dev)
-    tk.fill_synthetic_uniform(data, blen, nblocks, first_block=first)
+    if blen is None:  # cfg4: Zipf lengths computed on the host, packed, unaligned
+        lens = np.zeros(nblocks, np.uint64)
+        ora.oracle_zipf_lengths.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p]
+        ora.oracle_zipf_lengths(1, first, nblocks, lens.ctypes.data)
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+        total = int(lens.sum())
+        data = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+        d_off = torch.from_numpy(offs).to(dev)
+        d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+        tk.fill_synthetic_blocks(data, d_off, d_len, first_block=first)
+
+        def step(strm=None):
+            tk.crc32_batch(data, d_off, d_len, out=out, stream=strm)
+    else:
+        total = nblocks * blen
+        data = torch.empty(total, dtype=torch.uint8, device=dev)
+        tk.fill_synthetic_uniform(data, blen, nblocks, first_block=first)
+
+        def step(strm=None):
+            tk.crc32_batch_uniform(data, blen, nblocks, out=out, stream=strm)
     torch.cuda.synchronize()
 
-    stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
-        tk.crc32_batch_uniform(data, blen, nblocks, out=out)
+        step()
     torch.cuda.synchronize()
 
     # correctness of this exact buffer (checked outside the timed region)
     crcs = out.cpu().numpy().view(np.uint32).copy()
-    ora = load_oracle()
     probe = np.zeros(64, np.uint32)
-    ora.oracle_crc_synthetic(1, first, 64, blen, probe.ctypes.data)
+    if blen is None:
+        ora.oracle_crc_synthetic_lens.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
+        ora.oracle_crc_synthetic_lens(1, first, 64, lens.ctypes.data, probe.ctypes.data)
+    else:
+        ora.oracle_crc_synthetic(1, first, 64, blen, probe.ctypes.data)
     bit_exact = bool(np.array_equal(crcs[:64], probe))
     if rank == 0 and world == 1:
         with open(os.path.join(ROOT, "tests", "golden", "synthetic.json")) as f:
@@ -159,7 +183,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         starts[i].record(stream)
-        tk.crc32_batch_uniform(data, blen, nblocks, out=out, stream=stream)
+        step(stream)
         ends[i].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -169,7 +193,7 @@ def main():
     if world > 1:
         elapsed, kernel_ms, bit_exact = reduce_timing(elapsed, kernel_ms, bit_exact, dist, dev)
 
-    bytes_per_step = nblocks * blen
+    bytes_per_step = total
     total_bytes = bytes_per_step * args.steps * world
     value = total_bytes / (1 << 30) / elapsed
     achieved = bytes_per_step / (kernel_ms * 1e-3) / 1e9
@@ -195,7 +219,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (SURVEY §8d splitmix64 generator, seed 1), generated in HBM",
-        "config": {"workload": f"{args.config}: {desc}", "blocks_per_gpu": nblocks, "block_bytes": blen,
+        "config": {"workload": f"{args.config}: {desc}", "blocks_per_gpu": nblocks, "block_bytes": blen or "zipf",
                    "bytes_per_gpu_per_step": bytes_per_step, "parallelism": f"batch split x{world}, no collective"},
         "bit_exact": bit_exact,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -204,7 +228,7 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_step},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and blen is not None:
         host = data.cpu().numpy()
         cb, cpu_crcs = cpu_baseline(host, nblocks, blen)
         cb["agrees_with_gpu"] = bool(np.array_equal(cpu_crcs, crcs[:cpu_crcs.size]))

@@ -318,6 +318,24 @@ int pipe_init(HostPipe& p, std::size_t max_blocks) {
   return TKV_OK;
 }
 
+// Copy blocks [b0, b0+cnt) into dst at the slab offsets so_[i]; large slabs use several threads.
+void gather(std::uint8_t* dst, const std::uint8_t* src, const std::uint64_t* off, const std::uint32_t* len,
+            std::uint64_t b0, std::size_t cnt, const std::uint64_t* so_) {
+  const std::uint64_t bytes = so_[cnt - 1] + len[b0 + cnt - 1];
+  const unsigned nt = bytes >= (std::uint64_t(32) << 20) ? 8u : 1u;
+  auto part = [&](unsigned t) {
+    for (std::size_t i = cnt * t / nt; i < cnt * (t + 1) / nt; ++i)
+      std::memcpy(dst + so_[i], src + off[b0 + i], len[b0 + i]);
+  };
+  if (nt == 1) {
+    part(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back(part, t);
+  for (auto& t : th) t.join();
+}
+
 // Blocks in [lo, hi) of a host batch, processed slab by slab. Blocks larger than a slab are
 // chained through update_device in slab-sized pieces on stream 0.
 int host_batch(DevCtx* c, const std::uint8_t* h_base, const std::uint64_t* off, const std::uint32_t* len,
@@ -340,6 +358,7 @@ int host_batch(DevCtx* c, const std::uint8_t* h_base, const std::uint64_t* off, 
   }
   HostPipe p;
   if (int rc = pipe_init(p, max_blocks)) return rc;
+  const bool src_pinned = is_pinned_or_device(h_base);
   struct Pending {
     std::uint64_t lo = 0, cnt = 0;
     bool active = false;
@@ -378,12 +397,16 @@ int host_batch(DevCtx* c, const std::uint8_t* h_base, const std::uint64_t* off, 
       ++b;
       continue;
     }
-    // Gather the next slab of blocks.
+    // Next slab: the longest run of blocks that fits kSlab bytes.
     if (int rc = retire(k)) return rc;
     std::size_t cnt = 0, bytes = 0;
     const std::uint64_t b0 = b;
+    bool contiguous = true, uniform = true;
     while (b < hi && len[b] <= kSlab && bytes + len[b] <= kSlab && cnt < p.cap_blocks) {
-      std::memcpy(p.h_data[k] + bytes, h_base + off[b], len[b]);
+      if (cnt) {
+        contiguous = contiguous && off[b] == off[b - 1] + len[b - 1];
+        uniform = uniform && len[b] == len[b0];
+      }
       p.h_off[k][cnt] = bytes;
       p.h_len[k][cnt] = len[b];
       p.h_init[k][cnt] = init ? init[b] : kInit;
@@ -391,12 +414,25 @@ int host_batch(DevCtx* c, const std::uint8_t* h_base, const std::uint64_t* off, 
       ++cnt;
       ++b;
     }
-    TKV_HIP(hipMemcpyAsync(p.d_data[k], p.h_data[k], bytes, hipMemcpyHostToDevice, p.st[k]));
-    TKV_HIP(hipMemcpyAsync(p.d_off[k], p.h_off[k], cnt * 8, hipMemcpyHostToDevice, p.st[k]));
-    TKV_HIP(hipMemcpyAsync(p.d_len[k], p.h_len[k], cnt * 4, hipMemcpyHostToDevice, p.st[k]));
+    // Contiguous blocks from pinned memory go straight to the device; anything else is gathered
+    // into the pinned staging slab (several host threads for large slabs).
+    if (contiguous && src_pinned) {
+      TKV_HIP(hipMemcpyAsync(p.d_data[k], h_base + off[b0], bytes, hipMemcpyHostToDevice, p.st[k]));
+    } else {
+      gather(p.h_data[k], h_base, off, len, b0, cnt, p.h_off[k]);
+      TKV_HIP(hipMemcpyAsync(p.d_data[k], p.h_data[k], bytes, hipMemcpyHostToDevice, p.st[k]));
+    }
     TKV_HIP(hipMemcpyAsync(p.d_init[k], p.h_init[k], cnt * 4, hipMemcpyHostToDevice, p.st[k]));
-    if (int rc = run_irregular(c, p.d_data[k], p.d_off[k], p.d_len[k], p.d_init[k], p.d_out[k], cnt, p.st[k]))
-      return rc;
+    if (uniform) {
+      // equal lengths, packed back to back in the slab: the uniform (packed) kernels, no prepass
+      if (int rc = run_uniform(c, p.d_data[k], len[b0], len[b0], p.d_init[k], kInit, kInit, p.d_out[k], cnt, p.st[k]))
+        return rc;
+    } else {
+      TKV_HIP(hipMemcpyAsync(p.d_off[k], p.h_off[k], cnt * 8, hipMemcpyHostToDevice, p.st[k]));
+      TKV_HIP(hipMemcpyAsync(p.d_len[k], p.h_len[k], cnt * 4, hipMemcpyHostToDevice, p.st[k]));
+      if (int rc = run_irregular(c, p.d_data[k], p.d_off[k], p.d_len[k], p.d_init[k], p.d_out[k], cnt, p.st[k]))
+        return rc;
+    }
     TKV_HIP(hipMemcpyAsync(p.h_out[k], p.d_out[k], cnt * 4, hipMemcpyDeviceToHost, p.st[k]));
     TKV_HIP(hipEventRecord(p.done[k], p.st[k]));
     pend[k] = {b0, cnt, true};
