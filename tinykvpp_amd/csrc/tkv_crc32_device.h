@@ -7,6 +7,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "tkv_crc32_internal.h"
 
 namespace tkv {
@@ -156,12 +158,23 @@ __device__ __forceinline__ void issue_row(const RowsArgs& a, const Cursor& c, bo
   const std::uintptr_t bhi = blo + c.n;
   const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
   const std::uintptr_t seg = static_cast<std::uintptr_t>(static_cast<std::int64_t>(blo) + rowstart) + lane * kSeg;
-  const std::uintptr_t al = seg & ~static_cast<std::uintptr_t>(15);
+  if (NP == 4 || c.r == 0 || !live) {
+    // 16-byte aligned pieces; pieces outside the block (head padding, dead rows) read `dummy`.
+    const std::uintptr_t al = seg & ~static_cast<std::uintptr_t>(15);
 #pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const std::uintptr_t p = al + 16u * i;
-    const bool ok = live && (p + 16 > blo) && (p < bhi);
-    rb.q[i] = gload16(ok ? p : dmy);
+    for (int i = 0; i < NP; ++i) {
+      const std::uintptr_t p = al + 16u * i;
+      const bool ok = live && (p + 16 > blo) && (p < bhi);
+      rb.q[i] = gload16(ok ? p : dmy);
+    }
+  } else {
+    // Interior row of an unaligned block: the segment lies inside the block, so four dword-aligned
+    // 16-byte loads (as fast as aligned ones on gfx950; byte-misaligned ones are 27 % slower) plus
+    // one dword cover it; bytes read outside the block share an aligned dword with block bytes.
+    const std::uintptr_t a4 = seg & ~static_cast<std::uintptr_t>(3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rb.q[i] = gload16(a4 + 16u * i);
+    rb.q[NP - 1].x = *reinterpret_cast<g_u32*>((seg & 3u) ? a4 + 64u : dmy);
   }
   if constexpr (!UNIFORM) {
     const std::uintptr_t hp = reinterpret_cast<std::uintptr_t>(&a.tabs->head_shift[head_len(c.n)][lane & 31u]);
@@ -184,6 +197,20 @@ __device__ __forceinline__ void segment_dwords(const Cursor& c, const RowBuf<NP>
       dw[4 * i + 2] = rb.q[i].z;
       dw[4 * i + 3] = rb.q[i].w;
     }
+  } else if (c.r != 0) {
+    // interior row: dword-aligned loads (issue_row), only the byte shift t remains
+    std::uint32_t raw[17];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      raw[4 * i + 0] = rb.q[i].x;
+      raw[4 * i + 1] = rb.q[i].y;
+      raw[4 * i + 2] = rb.q[i].z;
+      raw[4 * i + 3] = rb.q[i].w;
+    }
+    raw[16] = rb.q[NP - 1].x;
+    const std::uint32_t t = static_cast<std::uint32_t>((reinterpret_cast<std::uintptr_t>(c.blk) + c.n) & 3u);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dw[k] = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], t);
   } else {
     std::uint32_t raw[20];
 #pragma unroll
@@ -330,44 +357,30 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
     load_desc<UNIFORM>(a, cur);
     st.piece_has_row0 = cur.r == 0;
 
-    // Lane contribution of one row before the Horner step: Shift_{(63-l)*64}(crc_0(segment)).
-    auto lane_value = [&](const Cursor& c, const RowBuf<NP>& rb) -> std::uint32_t {
-      std::uint32_t dw[16];
-      segment_dwords<ALIGNED, NP>(c, rb, lane, dw);
+    // Lane contributions of n rows before the Horner step, Shift_{(63-l)*64}(crc_0(segment)), with
+    // the rows' slicing chains interleaved (independent until the Horner step).
+    auto lane_values = [&](auto n_const, const Cursor* cs, const RowBuf<NP>* rbs, std::uint32_t* v) {
+      constexpr int n = decltype(n_const)::value;
+      std::uint32_t d[n][16];
+#pragma unroll
+      for (int i = 0; i < n; ++i) segment_dwords<ALIGNED, NP>(cs[i], rbs[i], lane, d[i]);
       if constexpr (MODE == 1) {
-        std::uint32_t x = 0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) x ^= dw[k];
-        return x;
-      } else {
-        Reg p{0, 0};
+        for (int i = 0; i < n; ++i) {
+          v[i] = 0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) slice4(lds, p, dw[k], kc);
-        return lane_shift(lds, p.value(), kc);
-      }
-    };
-    // Two rows with their slicing chains interleaved (independent until the Horner step).
-    auto lane_value2 = [&](const Cursor& c0, const RowBuf<NP>& r0, const Cursor& c1, const RowBuf<NP>& r1,
-                           std::uint32_t& v0, std::uint32_t& v1) {
-      std::uint32_t d0[16], d1[16];
-      segment_dwords<ALIGNED, NP>(c0, r0, lane, d0);
-      segment_dwords<ALIGNED, NP>(c1, r1, lane, d1);
-      if constexpr (MODE == 1) {
-        v0 = v1 = 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          v0 ^= d0[k];
-          v1 ^= d1[k];
+          for (int t = 0; t < 16; ++t) v[i] ^= d[i][t];
         }
       } else {
-        Reg p0{0, 0}, p1{0, 0};
+        Reg p[n];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          slice4(lds, p0, d0[k], kc);
-          slice4(lds, p1, d1[k], kc);
-        }
-        v0 = lane_shift(lds, p0.value(), kc);
-        v1 = lane_shift(lds, p1.value(), kc);
+        for (int i = 0; i < n; ++i) p[i] = Reg{0, 0};
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+#pragma unroll
+          for (int i = 0; i < n; ++i) slice4(lds, p[i], d[i][t], kc);
+#pragma unroll
+        for (int i = 0; i < n; ++i) v[i] = lane_shift(lds, p[i].value(), kc);
       }
     };
 
@@ -396,19 +409,21 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
         }
         const std::uint32_t gk = g + k;
         if (gk >= g1) break;
-        if constexpr (ILP == 2) {
-          if (gk + 1 < g1) {
-            std::uint32_t v0, v1;
-            lane_value2(cq[k], buf[k], cq[k + 1], buf[k + 1], v0, v1);
-            finish_row<UNIFORM>(a, cq[k], v0, buf[k].hs, hcon, lane, false, st);
-            finish_row<UNIFORM>(a, cq[k + 1], v1, buf[k + 1].hs, hcon, lane, gk + 2 == g1, st);
-          } else {
-            const std::uint32_t v0 = lane_value(cq[k], buf[k]);
-            finish_row<UNIFORM>(a, cq[k], v0, buf[k].hs, hcon, lane, true, st);
-          }
+        if (gk + ILP <= g1) {
+          std::uint32_t v[ILP];
+          lane_values(std::integral_constant<int, ILP>{}, &cq[k], &buf[k], v);
+#pragma unroll
+          for (int i = 0; i < ILP; ++i)
+            finish_row<UNIFORM>(a, cq[k + i], v[i], buf[k + i].hs, hcon, lane, gk + i + 1 == g1, st);
         } else {
-          const std::uint32_t v0 = lane_value(cq[k], buf[k]);
-          finish_row<UNIFORM>(a, cq[k], v0, buf[k].hs, hcon, lane, gk + 1 == g1, st);
+#pragma unroll
+          for (int i = 0; i < ILP; ++i) {  // tail: fewer than ILP rows left
+            if (gk + i < g1) {
+              std::uint32_t v[1];
+              lane_values(std::integral_constant<int, 1>{}, &cq[k + i], &buf[k + i], v);
+              finish_row<UNIFORM>(a, cq[k + i], v[0], buf[k + i].hs, hcon, lane, gk + i + 1 == g1, st);
+            }
+          }
         }
       }
     }

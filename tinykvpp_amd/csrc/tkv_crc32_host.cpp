@@ -218,16 +218,19 @@ int run_uniform(DevCtx* c, const std::uint8_t* d_base, std::uint64_t stride, std
   a.out = d_out;
   a.nblocks = static_cast<std::uint32_t>(n);
   a.total_rows = static_cast<std::uint32_t>(n * R);
-  // Launch only as many workgroups as there are rows to give them (small batches).
-  std::uint64_t grid = std::min<std::uint64_t>(c->ncu, (a.total_rows + kWavesPerWG - 1) / kWavesPerWG);
-  if (grid == 0) grid = 1;
-  a.nwaves = static_cast<std::uint32_t>(grid * kWavesPerWG);
-  a.snap_blocks = n >= a.nwaves ? 1u : 0u;
   const bool aligned = (reinterpret_cast<std::uintptr_t>(d_base) % 16 == 0) && (stride % 16 == 0) && (len % 16 == 0);
-  if (aligned && a.snap_blocks && len != 0 && len % kRow == 0 && stride == len) {
-    TKV_HIP(launch_packed(a, static_cast<unsigned>(grid), st));  // whole blocks per wave, no seams
+  const std::uint64_t packed_waves = static_cast<std::uint64_t>(c->ncu) * kWavesPerWG;
+  if (aligned && n >= packed_waves && len != 0 && len % kRow == 0 && stride == len) {
+    a.nwaves = static_cast<std::uint32_t>(packed_waves);
+    a.snap_blocks = 1;
+    TKV_HIP(launch_packed(a, static_cast<unsigned>(c->ncu), st));  // whole blocks per wave, no seams
     return TKV_OK;
   }
+  // Launch only as many workgroups as there are rows to give them (small batches).
+  std::uint64_t grid = std::min<std::uint64_t>(c->ncu, (a.total_rows + kRowsWavesPerWG - 1) / kRowsWavesPerWG);
+  if (grid == 0) grid = 1;
+  a.nwaves = static_cast<std::uint32_t>(grid * kRowsWavesPerWG);
+  a.snap_blocks = n >= a.nwaves ? 1u : 0u;
   TKV_HIP(launch_rows(a, aligned, true, static_cast<unsigned>(grid), st));
   if (!a.snap_blocks) TKV_HIP(launch_fixup(a, st));
   return TKV_OK;
@@ -248,6 +251,7 @@ int run_irregular(DevCtx* c, const std::uint8_t* d_base, const std::uint64_t* d_
   a.init_raw = d_init;
   a.out = d_out;
   a.nblocks = static_cast<std::uint32_t>(n);
+  a.nwaves = static_cast<std::uint32_t>(c->ncu) * kRowsWavesPerWG;
   TKV_HIP(launch_prepass(d_len, a.nblocks, s->row_scan, s->tiles, s->wave_start, a.nwaves, st));
   TKV_HIP(launch_rows(a, false, false, static_cast<unsigned>(c->ncu), st));
   TKV_HIP(launch_fixup(a, st));

@@ -21,8 +21,10 @@ constexpr std::uint32_t kInit = 0xFFFFFFFFu;  // init and xorout
 // Work decomposition of the row kernel.
 constexpr int kSeg = 64;                 // contiguous bytes one lane folds per row
 constexpr int kRow = 64 * kSeg;          // bytes one wave folds per row (4 KiB)
-constexpr int kWavesPerWG = 16;          // 1024-thread workgroups, one per CU (LDS-bound)
+constexpr int kWavesPerWG = 16;          // packed kernel: 1024-thread workgroups, one per CU (LDS-bound)
 constexpr int kThreads = 64 * kWavesPerWG;
+constexpr int kRowsWavesPerWG = 12;      // generic row kernels: 768 threads (162 VGPRs at ILP 2)
+constexpr int kRowsThreads = 64 * kRowsWavesPerWG;
 
 // LDS image (160 KiB, one workgroup per CU):
 //   words [0, 32768): slicing-by-4 tables T0..T3, each entry replicated 32x so lane c of every

@@ -30,14 +30,16 @@ namespace {
 // Pipeline shape per variant: DEPTH row buffers per wave (DEPTH-ILP rows in flight
 // while ILP rows are folded with interleaved chains). The unaligned variants carry a fifth 16-byte
 // piece per row, so they keep fewer rows in registers.
+// 768-thread workgroups (12 waves/CU, <= 168 VGPRs) with 2 rows folded together and 2 in flight
+// measured best on cfg4 (tools/explore.py --irregular, profiles/r1/explore_irregular.txt).
 template <bool ALIGNED>
 struct Shape {
-  static constexpr int kDepth = ALIGNED ? 4 : 3;
-  static constexpr int kIlp = ALIGNED ? 2 : 1;
+  static constexpr int kDepth = 4;
+  static constexpr int kIlp = 2;
 };
 
 template <bool ALIGNED, bool UNIFORM>
-__global__ __launch_bounds__(kThreads) void crc_rows(RowsArgs a) {
+__global__ __launch_bounds__(kRowsThreads) void crc_rows(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   dev::crc_rows_body<ALIGNED, UNIFORM, Shape<ALIGNED>::kDepth, Shape<ALIGNED>::kIlp, 0>(a, lds);
 }
@@ -163,10 +165,10 @@ __global__ void fill_blocks(std::uint8_t* base, const std::uint64_t* offsets, co
 // ---- launchers (called from tkv_crc32_host.cpp) ----------------------------------------------------
 hipError_t launch_rows(const RowsArgs& a, bool aligned, bool uniform, unsigned grid, hipStream_t st) {
   if (uniform) {
-    if (aligned) hipLaunchKernelGGL((crc_rows<true, true>), dim3(grid), dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((crc_rows<false, true>), dim3(grid), dim3(kThreads), 0, st, a);
+    if (aligned) hipLaunchKernelGGL((crc_rows<true, true>), dim3(grid), dim3(kRowsThreads), 0, st, a);
+    else hipLaunchKernelGGL((crc_rows<false, true>), dim3(grid), dim3(kRowsThreads), 0, st, a);
   } else {
-    hipLaunchKernelGGL((crc_rows<false, false>), dim3(grid), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((crc_rows<false, false>), dim3(grid), dim3(kRowsThreads), 0, st, a);
   }
   return hipGetLastError();
 }

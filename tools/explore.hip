@@ -34,9 +34,10 @@ __global__ __launch_bounds__(256) void k_stream(const uint4* p, std::uint64_t n1
 // PAT 2: lane l reads [2048(i/2) + 32l + 16(i%2), +16) (32-byte lane segments)
 // FIN 0: XOR into a register, one store per wave; FIN 1: per-row DPP reduce + lane-0 store per row;
 // FIN 2: per-row reduce, results kept in lane (row % 64) and stored 64 at a time (coalesced).
-template <int PAT, int DEPTH, int FIN>
+template <int PAT, int DEPTH, int FIN, int MIS = 0>
 __global__ __launch_bounds__(1024) void k_pat(const std::uint8_t* base, std::uint32_t nrows, std::uint32_t W,
                                               std::uint32_t* out) {
+  base += MIS;  // byte misalignment of every load (unaligned global_load_dwordx4)
   const std::uint32_t lane = threadIdx.x & 63u;
   const std::uint32_t wave = blockIdx.x * 16 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint32_t g0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(nrows) / W);
@@ -101,9 +102,10 @@ void L(RowsArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_rows<D, I, M>), dim3(g_ncu), dim3(kThreads), 0, s, a);
 }
 
-template <int PAT, int D, int F>
+template <int PAT, int D, int F, int MIS = 0>
 void P(RowsArgs a, hipStream_t s) {
-  hipLaunchKernelGGL((k_pat<PAT, D, F>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows, a.nwaves, a.out);
+  hipLaunchKernelGGL((k_pat<PAT, D, F, MIS>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows - 1, a.nwaves,
+                     a.out);
 }
 
 template <int D, int I, bool NT, bool ST, int T>
@@ -129,17 +131,51 @@ const V kVariants[] = {
     {"crc D4 I2", L<4, 2, 0>}, {"crc D6 I2", L<6, 2, 0>},
     {"mem D2 I1", L<2, 1, 1>}, {"mem D4 I1", L<4, 1, 1>}, {"mem D4 I2", L<4, 2, 1>},
     {"mem D8 I1", L<8, 1, 1>},
+    {"pat seg64 D4 fin2 mis0", P<0, 4, 2, 0>}, {"pat seg64 D4 fin2 mis4", P<0, 4, 2, 4>},
+    {"pat seg64 D4 fin2 mis5", P<0, 4, 2, 5>}, {"pat seg64 D4 fin2 mis8", P<0, 4, 2, 8>},
     {"pat seg64 D2 fin0", P<0, 2, 0>}, {"pat seg64 D4 fin0", P<0, 4, 0>}, {"pat seg64 D4 fin1", P<0, 4, 1>},
     {"pat seg64 D4 fin2", P<0, 4, 2>}, {"pat coal D2 fin0", P<1, 2, 0>}, {"pat coal D4 fin0", P<1, 4, 0>},
     {"pat coal D4 fin1", P<1, 4, 1>}, {"pat coal D4 fin2", P<1, 4, 2>}, {"pat seg32 D4 fin0", P<2, 4, 0>},
     {"pat seg32 D4 fin2", P<2, 4, 2>}, {"pat coal D6 fin0", P<1, 6, 0>}, {"pat seg64 D6 fin0", P<0, 6, 0>},
 };
 constexpr int kNV = sizeof(kVariants) / sizeof(kVariants[0]);
+
+template <int D, int I, int T>
+__global__ __launch_bounds__(T) void k_irr(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  dev::crc_rows_body<false, false, D, I, 0>(a, lds);
+}
+
+struct IV {
+  const char* name;
+  int threads;
+  void (*launch)(RowsArgs, hipStream_t);
+};
+
+template <int D, int I, int T>
+void LI(RowsArgs a, hipStream_t s) {
+  hipLaunchKernelGGL((k_irr<D, I, T>), dim3(g_ncu), dim3(T), 0, s, a);
+}
+
+const IV kIrr[] = {
+    {"irr T1024 D3 I1", 1024, LI<3, 1, 1024>}, {"irr T1024 D2 I1", 1024, LI<2, 1, 1024>},
+    {"irr T1024 D4 I2", 1024, LI<4, 2, 1024>}, {"irr T512 D4 I2", 512, LI<4, 2, 512>},
+    {"irr T512 D6 I2", 512, LI<6, 2, 512>}, {"irr T512 D6 I3", 512, LI<6, 3, 512>},
+    {"irr T768 D4 I2", 768, LI<4, 2, 768>}, {"irr T512 D8 I4", 512, LI<8, 4, 512>},
+};
+constexpr int kNIrr = sizeof(kIrr) / sizeof(kIrr[0]);
+std::uint32_t* g_scan = nullptr;
+std::uint32_t* g_tiles = nullptr;
+std::uint32_t* g_wstart = nullptr;
+std::uint64_t g_cap = 0;
 }  // namespace
 
 namespace tkv {
 void build_tables(DeviceTables* t);
 std::uint32_t x8nmodp(std::uint64_t nbytes);
+hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
+hipError_t launch_prepass(const std::uint32_t* lengths, std::uint32_t n, std::uint32_t* row_scan,
+                          std::uint32_t* tile_sums, std::uint32_t* wave_start, std::uint32_t W, hipStream_t st);
 }  // namespace tkv
 
 extern "C" int explore_count() { return kNV + 1; }
@@ -182,5 +218,45 @@ extern "C" int explore_run(int v, const std::uint8_t* base, std::uint64_t n, std
   a.nwaves = g_ncu * kWavesPerWG;
   a.snap_blocks = 1;
   kVariants[v].launch(a, st);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int explore_irr_count() { return kNIrr; }
+extern "C" const char* explore_irr_name(int v) { return kIrr[v].name; }
+
+extern "C" int explore_run_irr(int v, const std::uint8_t* base, const std::uint64_t* off, const std::uint32_t* len,
+                               std::uint64_t n, std::uint32_t* out, void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!g_tabs) {
+    std::uint32_t dummy_out;
+    (void)dummy_out;
+    if (explore_run(kNV, base, 0, 16, out, stream)) return 1;  // one-time init of tables etc.
+  }
+  if (n > g_cap) {
+    hipFree(g_scan);
+    hipFree(g_tiles);
+    hipFree(g_wstart);
+    hipMalloc(&g_scan, 4 * (n + 1));
+    hipMalloc(&g_tiles, 4 * (n / 4096 + 2));
+    hipMalloc(&g_wstart, 4 * g_ncu * 16);
+    g_cap = n;
+  }
+  RowsArgs a{};
+  a.base = base;
+  a.offsets = off;
+  a.lengths = len;
+  a.row_scan = g_scan;
+  a.wave_start = g_wstart;
+  a.init_default = 0xFFFFFFFFu;
+  a.out_xor = 0xFFFFFFFFu;
+  a.out = out;
+  a.seams = g_seams;
+  a.tabs = g_tabs;
+  a.dummy = g_dummy;
+  a.nblocks = static_cast<std::uint32_t>(n);
+  a.nwaves = g_ncu * (kIrr[v].threads / 64);
+  launch_prepass(len, a.nblocks, g_scan, g_tiles, g_wstart, a.nwaves, st);
+  kIrr[v].launch(a, st);
+  launch_fixup(a, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
