@@ -49,8 +49,9 @@ def load_tables(lib):
     horner = buf[o:o + 64]; o += 64
     row_pow = buf[o:o + 64]; o += 64
     head = buf[o:o + (ROW + 1) * 32].reshape(ROW + 1, 32); o += (ROW + 1) * 32
+    shift32 = buf[o:o + 128].reshape(8, 16); o += 128
     assert o * 4 == n
-    return slice_, lane, horner, row_pow, head
+    return slice_, lane, horner, row_pow, head, shift32
 
 
 @pytest.fixture(scope="module")
@@ -81,7 +82,7 @@ def test_gf2_helpers(lib, oracle):
 
 
 def test_lane_shift_horner_head_tables(tables, oracle):
-    _, lane, horner, row_pow, head = tables
+    _, lane, horner, row_pow, head, shift32 = tables
     for l in (0, 1, 31, 62, 63):
         for j in (0, 3, 7):
             for v in (1, 9, 15):
@@ -92,6 +93,9 @@ def test_lane_shift_horner_head_tables(tables, oracle):
     for h in (0, 1, 3, 4, 100, 4095, 4096):
         for i in (0, 17, 31):
             assert int(head[h][i]) == shift_zeros(oracle, 1 << i, h)
+    for j in (0, 4, 7):
+        for v in (1, 6, 15):
+            assert int(shift32[j][v]) == shift_zeros(oracle, v << (4 * j), 32)
 
 
 # ---- numpy model of the kernel ------------------------------------------------------------------
@@ -115,7 +119,7 @@ def bits_dot(sel, consts):
 
 class Model:
     def __init__(self, tables):
-        self.s, self.lane, self.horner, self.row_pow, self.head = tables
+        self.s, self.lane, self.horner, self.row_pow, self.head, _ = tables
 
     def slice_lanes(self, row):
         """16 slicing-by-4 steps per lane over a (64, 64)-byte row image; returns (64,) partials."""

@@ -81,6 +81,19 @@ __device__ __forceinline__ std::uint32_t lane_shift(const std::uint32_t* lds, st
   return xor3(xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5]), l[6] ^ l[7]);
 }
 
+// Shift_32(p) from a 128-entry nibble table held in two VGPRs (lane i of s32[h] = entry 64h + i),
+// read with ds_bpermute (LDS crossbar, no LDS memory): joins a lane's two 32-byte half chains.
+__device__ __forceinline__ std::uint32_t shift32_bperm(std::uint32_t p, std::uint32_t s32lo, std::uint32_t s32hi) {
+  std::uint32_t l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const std::uint32_t addr = (static_cast<std::uint32_t>((j & 3) * 16) + ((p >> (4 * j)) & 15u)) << 2;
+    l[j] = static_cast<std::uint32_t>(
+        __builtin_amdgcn_ds_bpermute(static_cast<int>(addr), static_cast<int>(j < 4 ? s32lo : s32hi)));
+  }
+  return xor3(xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5]), l[6] ^ l[7]);
+}
+
 // XOR of v over the 64 lanes, complete in lane 63 (DPP: within rows of 16, then row broadcasts).
 __device__ __forceinline__ std::uint32_t wave_xor_to_lane63(std::uint32_t v) {
   v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
@@ -443,11 +456,14 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
 }
 
 // Packed uniform fast path: block b = [base + b*len, +len) with len a multiple of kRow (4 KiB) and
-// 16-byte aligned base, so every row is full and the head length is kRow (init injection constants
-// = the Horner constants). Each wave owns whole blocks (no seams): a contiguous range [b0, b1), or
-// with STRIDED the blocks w, w+W, w+2W, ...; it keeps ILP rows' slicing chains interleaved and
-// DEPTH-ILP rows in flight, and stores its results 64 at a time (lane k holds its k-th block).
-template <int DEPTH, int ILP, bool NT, bool STRIDED>
+// 16-byte aligned base, so every row is full, row g of the batch sits at base + g*kRow, and the head
+// length is kRow (init injection constants = the Horner constants). Each wave owns the contiguous
+// blocks [b0, b1) (no seams), keeps ILP rows' slicing chains interleaved and DEPTH-ILP rows in
+// flight, and stores its results 64 at a time (lane k holds its k-th block). R1: one row per block
+// (4 KiB blocks), so no Horner state at all. The SIMDs are issue-bound here (PMC: every SIMD issues
+// ~96 % of cycles), so the loop is written for instruction count: incremental row addressing, no
+// divisions, selects instead of divergent branches.
+template <int DEPTH, int ILP, bool R1, bool SPLIT = false>
 __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
   fill_lds(a.tabs, lds);
@@ -460,42 +476,29 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
       lo_half ? 0u
               : static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(a.init_default),
                                                                 lane & 31u, 1)) & hcon;
+  std::uint32_t s32lo = 0, s32hi = 0;
+  if constexpr (SPLIT) {
+    s32lo = (&a.tabs->shift32[0][0])[lane];
+    s32hi = (&a.tabs->shift32[0][0])[64 + lane];
+  }
   __syncthreads();
 
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const std::uint32_t W = a.nwaves;
-  const std::uint32_t R = a.len / kRow;
-  std::uint32_t b0, nb;  // first block, number of blocks of this wave
-  if constexpr (STRIDED) {
-    b0 = wave;
-    nb = wave < a.nblocks ? (a.nblocks - 1 - wave) / W + 1 : 0u;
-  } else {
-    b0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W);
-    nb = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W) - b0;
-  }
+  const std::uint64_t W = a.nwaves;
+  const std::uint32_t R = R1 ? 1u : a.len / kRow;
+  const std::uint32_t b0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W);
+  const std::uint32_t nb = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W) - b0;
   if (nb == 0) return;
-  const std::uint32_t nrows = nb * R;  // wave-local rows j = 0 .. nrows-1
-  const std::uintptr_t lane_base = reinterpret_cast<std::uintptr_t>(a.base) + lane * kSeg;
-  const std::uint64_t bstride = STRIDED ? static_cast<std::uint64_t>(W) * a.len : a.len;
-  auto blk_of = [&](std::uint32_t k) -> std::uint32_t { return STRIDED ? b0 + k * W : b0 + k; };
+  const std::uint32_t nrows = nb * R;  // wave-local rows j = 0 .. nrows-1, contiguous in memory
+  const std::uintptr_t lane_base =
+      reinterpret_cast<std::uintptr_t>(a.base) + static_cast<std::uint64_t>(b0) * R * kRow + lane * kSeg;
 
   uint4 buf[DEPTH][4];
   auto issue = [&](std::uint32_t j, uint4 (&q)[4]) {
     const std::uint32_t jc = j < nrows ? j : nrows - 1;  // rows past the range reload the last one
-    const std::uint32_t k = jc / R, r = jc - k * R;
-    const std::uintptr_t p = lane_base + static_cast<std::uint64_t>(b0) * a.len + k * bstride +
-                             static_cast<std::uint64_t>(r) * kRow;
+    const std::uintptr_t p = lane_base + static_cast<std::uint64_t>(jc) * kRow;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = NT ? gload16_nt(p + 16u * i) : gload16(p + 16u * i);
-  };
-  auto dwords = [&](const uint4 (&q)[4], std::uint32_t (&dw)[16]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      dw[4 * i + 0] = q[i].x;
-      dw[4 * i + 1] = q[i].y;
-      dw[4 * i + 2] = q[i].z;
-      dw[4 * i + 3] = q[i].w;
-    }
+    for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i);
   };
 
   std::uint32_t B = 0;     // running register of the current block (Horner over its rows)
@@ -504,10 +507,11 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
   std::uint32_t keep = 0;  // lane i: result of wave-local block (k & ~63) + i
   auto finish = [&](std::uint32_t v) {
     std::uint32_t term;
-    if (r == 0) {
+    const bool head = R1 || r == 0;
+    if (head) {
       term = inj_const;
       if (a.init_raw) {
-        const std::uint32_t init = sload32(a.init_raw, blk_of(k));
+        const std::uint32_t init = sload32(a.init_raw, b0 + k);
         term = lo_half ? 0u : static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init),
                                                                                 lane & 31u, 1)) & hcon;
       }
@@ -516,12 +520,12 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
                      : 0u;
     }
     const std::uint32_t Bn = __builtin_amdgcn_readlane(wave_xor_to_lane63(v ^ term), 63);
-    if (++r == R) {
+    const bool last = R1 || ++r == R;
+    if (last) {
       const std::uint32_t slot = k & 63u;
-      if (lane == slot) keep = Bn ^ a.out_xor;
+      keep = lane == slot ? (Bn ^ a.out_xor) : keep;
       if (slot == 63u || k + 1 == nb) {
-        const std::uint32_t first = k - slot;
-        if (lane <= slot) a.out[blk_of(first + lane)] = keep;
+        if (lane <= slot) a.out[b0 + k - slot + lane] = keep;
       }
       r = 0;
       ++k;
@@ -541,31 +545,70 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
       const std::uint32_t jq = j + q;
       if (jq >= nrows) break;
       if (jq + ILP <= nrows) {
-        std::uint32_t dw[ILP][16];
-        Reg p[ILP];
-#pragma unroll
-        for (int i = 0; i < ILP; ++i) {
-          dwords(buf[q + i], dw[i]);
-          p[i] = Reg{0, 0};
-        }
-#pragma unroll
-        for (int t = 0; t < 16; ++t)
-#pragma unroll
-          for (int i = 0; i < ILP; ++i) slice4(lds, p[i], dw[i][t], kc);
         std::uint32_t v[ILP];
+        if constexpr (SPLIT) {
+          // two independent 32-byte chains per row: p = Shift_32(crc_0(dw 0..7)) ^ crc_0(dw 8..15)
+          Reg pa[ILP], pb[ILP];
 #pragma unroll
-        for (int i = 0; i < ILP; ++i) v[i] = lane_shift(lds, p[i].value(), kc);
+          for (int i = 0; i < ILP; ++i) pa[i] = pb[i] = Reg{0, 0};
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int i = 0; i < ILP; ++i) {
+              slice4(lds, pa[i], buf[q + i][t].x, kc);
+              slice4(lds, pb[i], buf[q + i][t + 2].x, kc);
+            }
+#pragma unroll
+            for (int i = 0; i < ILP; ++i) {
+              slice4(lds, pa[i], buf[q + i][t].y, kc);
+              slice4(lds, pb[i], buf[q + i][t + 2].y, kc);
+            }
+#pragma unroll
+            for (int i = 0; i < ILP; ++i) {
+              slice4(lds, pa[i], buf[q + i][t].z, kc);
+              slice4(lds, pb[i], buf[q + i][t + 2].z, kc);
+            }
+#pragma unroll
+            for (int i = 0; i < ILP; ++i) {
+              slice4(lds, pa[i], buf[q + i][t].w, kc);
+              slice4(lds, pb[i], buf[q + i][t + 2].w, kc);
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < ILP; ++i)
+            v[i] = lane_shift(lds, shift32_bperm(pa[i].value(), s32lo, s32hi) ^ pb[i].value(), kc);
+        } else {
+          Reg p[ILP];
+#pragma unroll
+          for (int i = 0; i < ILP; ++i) p[i] = Reg{0, 0};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+#pragma unroll
+            for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].x, kc);
+#pragma unroll
+            for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].y, kc);
+#pragma unroll
+            for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].z, kc);
+#pragma unroll
+            for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].w, kc);
+          }
+#pragma unroll
+          for (int i = 0; i < ILP; ++i) v[i] = lane_shift(lds, p[i].value(), kc);
+        }
 #pragma unroll
         for (int i = 0; i < ILP; ++i) finish(v[i]);
       } else {
 #pragma unroll
         for (int i = 0; i < ILP; ++i) {  // tail: fewer than ILP rows left
           if (jq + i < nrows) {
-            std::uint32_t dw[16];
-            dwords(buf[q + i], dw);
             Reg p{0, 0};
 #pragma unroll
-            for (int t = 0; t < 16; ++t) slice4(lds, p, dw[t], kc);
+            for (int t = 0; t < 4; ++t) {
+              slice4(lds, p, buf[q + i][t].x, kc);
+              slice4(lds, p, buf[q + i][t].y, kc);
+              slice4(lds, p, buf[q + i][t].z, kc);
+              slice4(lds, p, buf[q + i][t].w, kc);
+            }
             finish(lane_shift(lds, p.value(), kc));
           }
         }

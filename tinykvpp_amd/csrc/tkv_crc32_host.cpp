@@ -77,6 +77,9 @@ void build_tables(DeviceTables* t) {
     t->row_pow[k] = p;
     p = multmodp(p, p);
   }
+  const std::uint32_t z32 = x8nmodp(32);
+  for (int j = 0; j < 8; ++j)
+    for (std::uint32_t v = 0; v < 16; ++v) t->shift32[j][v] = multmodp(z32, v << (4 * j));
   std::uint32_t z = 0x80000000u;  // x^(8h), h = 0..kRow
   for (int h = 0; h <= kRow; ++h) {
     for (int i = 0; i < 32; ++i) t->head_shift[h][i] = multmodp(z, 1u << i);

@@ -43,6 +43,7 @@ struct DeviceTables {
   std::uint32_t horner[64];             // lanes 0..31: Shift_{kRow}(1 << l); lanes 32..63: 0
   std::uint32_t row_pow[64];            // x^(8*kRow*2^k) mod P (reflected), k = 0..63
   std::uint32_t head_shift[kRow + 1][32];  // [h][i] = Shift_h(1 << i): init injection at a head row
+  std::uint32_t shift32[8][16];         // [j][v] = Shift_32(v << 4j): joins two 32-byte half chains
 };
 
 // One partial result of a block that was split between waves (irregular / huge-block path).

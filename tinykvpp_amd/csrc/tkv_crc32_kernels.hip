@@ -48,9 +48,10 @@ __global__ __launch_bounds__(kRowsThreads) void crc_rows(RowsArgs a) {
 constexpr int kPackedDepth = 4;
 constexpr int kPackedIlp = 2;
 
+template <bool R1>
 __global__ __launch_bounds__(kThreads) void crc_packed(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<kPackedDepth, kPackedIlp, false, false>(a, lds);
+  dev::crc_packed_body<kPackedDepth, kPackedIlp, R1>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
@@ -174,7 +175,8 @@ hipError_t launch_rows(const RowsArgs& a, bool aligned, bool uniform, unsigned g
 }
 
 hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st) {
-  hipLaunchKernelGGL(crc_packed, dim3(grid), dim3(kThreads), 0, st, a);
+  if (a.len == kRow) hipLaunchKernelGGL(crc_packed<true>, dim3(grid), dim3(kThreads), 0, st, a);
+  else hipLaunchKernelGGL(crc_packed<false>, dim3(grid), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 

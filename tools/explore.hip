@@ -86,6 +86,62 @@ __global__ __launch_bounds__(1024) void k_pat(const std::uint8_t* base, std::uin
   }
 }
 
+
+// Interference probe: the packed kernel's loads and pipeline (D4, seg64, batched stores), plus
+// per row NLDS conflict-free ds_read_b32 in 4-wide dependent steps and/or NVALU dependent VALU
+// ops, to see which pipe's activity slows the memory stream.
+template <int NLDS, int NVALU>
+__global__ __launch_bounds__(1024) void k_interf(const std::uint8_t* base, std::uint32_t nrows, std::uint32_t W,
+                                                 std::uint32_t* out) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  for (std::uint32_t i = threadIdx.x; i < kLdsWords; i += 1024) lds[i] = i * 2654435761u;
+  __syncthreads();
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint32_t wave = blockIdx.x * 16 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t g0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(nrows) / W);
+  const std::uint32_t g1 = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(nrows) / W);
+  constexpr int DEPTH = 4;
+  auto addr = [&](std::uint32_t g, int i) -> std::uintptr_t {
+    return reinterpret_cast<std::uintptr_t>(base) + static_cast<std::uint64_t>(g < g1 ? g : g0) * 4096u +
+           64u * lane + 16u * i;
+  };
+  uint4 buf[DEPTH][4];
+  std::uint32_t keep = 0;
+#pragma unroll
+  for (int s = 0; s < DEPTH - 1; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) buf[s][i] = dev::gload16(addr(g0 + s, i));
+  for (std::uint32_t g = g0; g < g1; g += DEPTH) {
+#pragma unroll
+    for (int k = 0; k < DEPTH; ++k) {
+      const int s = (k + DEPTH - 1) % DEPTH;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) buf[s][i] = dev::gload16(addr(g + k + DEPTH - 1, i));
+      if (g + k >= g1) break;
+      std::uint32_t x = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x ^= buf[k][i].x ^ buf[k][i].y ^ buf[k][i].z ^ buf[k][i].w;
+      std::uint32_t y = x;
+#pragma unroll
+      for (int j = 0; j < NLDS / 4; ++j) {
+        const std::uint32_t a0 = ((y & 0xFFu) << 8) | (lane & 31u) << 2;
+        y = dev::xor3(dev::lds_at(lds, a0), dev::lds_at(lds, a0 + 0x10000u), dev::lds_at(lds, a0 + 0x10080u)) ^
+            dev::lds_at(lds, a0 + 128u);
+      }
+#pragma unroll
+      for (int j = 0; j < NVALU / 2; ++j) y = __builtin_amdgcn_perm(y, y * 3u + j, 0x0C020500u) ^ x;
+      const std::uint32_t r = __builtin_amdgcn_readlane(dev::wave_xor_to_lane63(y), 63);
+      const std::uint32_t gi = g + k;
+      if (lane == (gi & 63u)) keep = r;
+      if ((gi & 63u) == 63u || gi + 1 == g1) {
+        const std::uint32_t first = gi & ~63u;
+        if (first + lane >= g0 && first + lane <= gi) out[first + lane] = keep;
+      }
+    }
+  }
+}
+
+
 namespace {
 DeviceTables* g_tabs = nullptr;
 std::uint8_t* g_dummy = nullptr;
@@ -108,25 +164,34 @@ void P(RowsArgs a, hipStream_t s) {
                      a.out);
 }
 
-template <int D, int I, bool NT, bool ST, int T>
+template <int D, int I, bool R1, int T, bool SP>
 __global__ __launch_bounds__(T) void k_packed(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<D, I, NT, ST>(a, lds);
+  dev::crc_packed_body<D, I, R1, SP>(a, lds);
 }
 
-template <int D, int I, bool NT = false, bool ST = false, int T = 1024>
+template <int D, int I, int T = 1024, bool SP = false>
 void PK(RowsArgs a, hipStream_t s) {
   a.nwaves = g_ncu * (T / 64);
-  hipLaunchKernelGGL((k_packed<D, I, NT, ST, T>), dim3(g_ncu), dim3(T), 0, s, a);
+  if (a.len == kRow) hipLaunchKernelGGL((k_packed<D, I, true, T, SP>), dim3(g_ncu), dim3(T), 0, s, a);
+  else hipLaunchKernelGGL((k_packed<D, I, false, T, SP>), dim3(g_ncu), dim3(T), 0, s, a);
+}
+
+template <int NL, int NV>
+void IF(RowsArgs a, hipStream_t s) {
+  hipLaunchKernelGGL((k_interf<NL, NV>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows, a.nwaves, a.out);
 }
 
 const V kVariants[] = {
+    {"interf L0 V0", IF<0, 0>}, {"interf L72 V0", IF<72, 0>}, {"interf L0 V128", IF<0, 128>},
+    {"interf L72 V128", IF<72, 128>}, {"interf L36 V0", IF<36, 0>}, {"interf L144 V0", IF<144, 0>},
+    {"interf L0 V256", IF<0, 256>},
     {"packed D4 I2", PK<4, 2>}, {"packed D4 I1", PK<4, 1>}, {"packed D3 I1", PK<3, 1>},
-    {"packed D4 I2 nt", PK<4, 2, true>}, {"packed D4 I1 nt", PK<4, 1, true>},
-    {"packed D4 I2 strided", PK<4, 2, false, true>}, {"packed D4 I2 nt strided", PK<4, 2, true, true>},
-    {"packed T512 D8 I4", PK<8, 4, false, false, 512>}, {"packed T512 D6 I3", PK<6, 3, false, false, 512>},
-    {"packed T512 D6 I2", PK<6, 2, false, false, 512>}, {"packed T512 D8 I4 nt", PK<8, 4, true, false, 512>},
-    {"packed T768 D6 I2", PK<6, 2, false, false, 768>},
+    {"packed T512 D8 I4", PK<8, 4, 512>}, {"packed T512 D6 I3", PK<6, 3, 512>},
+    {"packed T768 D6 I2", PK<6, 2, 768>}, {"packed T768 D6 I3", PK<6, 3, 768>},
+    {"packed T512 D6 I2", PK<6, 2, 512>}, {"packed D4 I2 split", PK<4, 2, 1024, true>},
+    {"packed D4 I1 split", PK<4, 1, 1024, true>}, {"packed D3 I1 split", PK<3, 1, 1024, true>},
+    {"packed T512 D8 I4 split", PK<8, 4, 512, true>}, {"packed T768 D6 I2 split", PK<6, 2, 768, true>},
     {"crc D2 I1", L<2, 1, 0>}, {"crc D3 I1", L<3, 1, 0>}, {"crc D4 I1", L<4, 1, 0>},
     {"crc D4 I2", L<4, 2, 0>}, {"crc D6 I2", L<6, 2, 0>},
     {"mem D2 I1", L<2, 1, 1>}, {"mem D4 I1", L<4, 1, 1>}, {"mem D4 I2", L<4, 2, 1>},
