@@ -142,6 +142,20 @@ __global__ __launch_bounds__(1024) void k_interf(const std::uint8_t* base, std::
 }
 
 
+
+// Diagnostic: per-wave start/end s_memrealtime (100 MHz) of the production packed body.
+__global__ __launch_bounds__(1024) void k_packed_stamped(RowsArgs a, unsigned long long* stamps) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  const std::uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  dev::crc_packed_body<4, 2, true>(a, lds);
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63u) == 0) {
+    stamps[2 * wave] = t0;
+    stamps[2 * wave + 1] = t1;
+  }
+}
+
 namespace {
 DeviceTables* g_tabs = nullptr;
 std::uint8_t* g_dummy = nullptr;
@@ -323,5 +337,25 @@ extern "C" int explore_run_irr(int v, const std::uint8_t* base, const std::uint6
   launch_prepass(len, a.nblocks, g_scan, g_tiles, g_wstart, a.nwaves, st);
   kIrr[v].launch(a, st);
   launch_fixup(a, st);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int explore_stamped(const std::uint8_t* base, std::uint64_t n, std::uint32_t* out,
+                               unsigned long long* stamps, void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!g_tabs && explore_run(kNV, base, n, 4096, out, stream)) return 1;
+  RowsArgs a{};
+  a.base = base;
+  a.stride = 4096;
+  a.len = 4096;
+  a.init_default = 0xFFFFFFFFu;
+  a.out_xor = 0xFFFFFFFFu;
+  a.out = out;
+  a.seams = g_seams;
+  a.tabs = g_tabs;
+  a.dummy = g_dummy;
+  a.nblocks = static_cast<std::uint32_t>(n);
+  a.nwaves = g_ncu * 16;
+  hipLaunchKernelGGL(k_packed_stamped, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

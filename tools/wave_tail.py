@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Per-wave start/end times of the packed kernel (s_memrealtime, 100 MHz): how long the slowest
+waves keep the launch alive after the median wave has finished (tail of a static partition)."""
+import ctypes, os, sys
+import numpy as np
+import torch
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import tinykvpp_amd as tk
+lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libexplore.so"))
+lib.explore_stamped.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+torch.cuda.set_device(0); tk.set_device(0)
+n = 1 << 20
+data = torch.empty(n * 4096, dtype=torch.uint8, device="cuda")
+tk.fill_synthetic_uniform(data, 4096, n)
+out = torch.empty(n, dtype=torch.int32, device="cuda")
+W = torch.cuda.get_device_properties(0).multi_processor_count * 16
+st = torch.empty(2 * W, dtype=torch.int64, device="cuda")
+sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+for rep in range(4):
+    assert lib.explore_stamped(ctypes.c_void_p(data.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
+                               ctypes.c_void_p(st.data_ptr()), sp) == 0
+    torch.cuda.synchronize()
+    s = st.cpu().numpy().reshape(-1, 2).astype(np.float64) * 10.0  # ns
+    t0 = s[:, 0].min()
+    start, end = s[:, 0] - t0, s[:, 1] - t0
+    dur = end - start
+    print(f"rep {rep}: kernel span {end.max()/1e3:.1f} us; wave end p50 {np.median(end)/1e3:.1f} "
+          f"p90 {np.percentile(end, 90)/1e3:.1f} p99 {np.percentile(end, 99)/1e3:.1f} max {end.max()/1e3:.1f} us; "
+          f"start spread {start.max()/1e3:.1f} us; dur p50 {np.median(dur)/1e3:.1f} min {dur.min()/1e3:.1f} max {dur.max()/1e3:.1f}",
+          flush=True)
+# per-XCD view (blocks round-robin over 8 XCDs: wave w -> WG w//16 -> XCD (w//16) % 8, a label only)
+xcd = (np.arange(W) // 16) % 8
+for x in range(8):
+    print(f"xcd-group {x}: median wave duration {np.median(dur[xcd == x])/1e3:.1f} us, max end {end[xcd == x].max()/1e3:.1f}")
