@@ -124,8 +124,8 @@ def cpu_baseline(host, nblocks, blen, seconds_target=8.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-csv", default=None,
@@ -178,20 +178,6 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    # correctness of this exact buffer (checked outside the timed region)
-    crcs = out.cpu().numpy().view(np.uint32).copy()
-    probe = np.zeros(64, np.uint32)
-    if blen is None:
-        ora.oracle_crc_synthetic_lens.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
-        ora.oracle_crc_synthetic_lens(1, first, 64, lens.ctypes.data, probe.ctypes.data)
-    else:
-        ora.oracle_crc_synthetic(1, first, 64, blen, probe.ctypes.data)
-    bit_exact = bool(np.array_equal(crcs[:64], probe))
-    if rank == 0 and world == 1:
-        with open(os.path.join(ROOT, "tests", "golden", "synthetic.json")) as f:
-            g = json.load(f)[args.config]
-        bit_exact = bit_exact and int(np.bitwise_xor.reduce(crcs)) == g["xor"]
-
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
@@ -207,6 +193,21 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+
+    # correctness of this exact buffer, from the last timed step (checked after the timed region so
+    # no CPU pause lets the clocks fall between warmup and timing)
+    crcs = out.cpu().numpy().view(np.uint32).copy()
+    probe = np.zeros(64, np.uint32)
+    if blen is None:
+        ora.oracle_crc_synthetic_lens.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
+        ora.oracle_crc_synthetic_lens(1, first, 64, lens.ctypes.data, probe.ctypes.data)
+    else:
+        ora.oracle_crc_synthetic(1, first, 64, blen, probe.ctypes.data)
+    bit_exact = bool(np.array_equal(crcs[:64], probe))
+    if rank == 0 and world == 1:
+        with open(os.path.join(ROOT, "tests", "golden", "synthetic.json")) as f:
+            g = json.load(f)[args.config]
+        bit_exact = bit_exact and int(np.bitwise_xor.reduce(crcs)) == g["xor"]
     if world > 1:
         elapsed, kernel_ms, bit_exact = reduce_timing(elapsed, kernel_ms, bit_exact, dist, dev)
 

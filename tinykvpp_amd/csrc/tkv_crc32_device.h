@@ -617,6 +617,179 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
   }
 }
 
+// Packed kernel with dynamic work distribution inside each workgroup. The batch is cut into chunks
+// of C whole blocks (CR = C*R rows, CR >= CROWS and a multiple of DEPTH; C <= 64); workgroup g owns
+// a contiguous static range of chunks, and its waves take chunks from that range through one global
+// atomic counter per workgroup. The statically partitioned body leaves the slowest waves of a CU
+// running long after the median wave has finished (tools/wave_tail.py); here a wave that runs ahead
+// takes more chunks.
+// Pipeline: DEPTH rows in flight, ILP rows per step, chunk-aligned iterations of DEPTH rows. The id
+// of chunk k+1 is requested when chunk k starts and read (v_readfirstlane) after iteration 0 of
+// chunk k, whose row loads were issued after the atomic: the wait for those rows already covers
+// the atomic's return, so the request never drains the row pipeline. In the last iteration of a
+// chunk the issue cursor runs into the next chunk.
+template <int DEPTH, int ILP, bool R1, int CROWS>
+__device__ __forceinline__ void crc_packed_dyn_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
+  static_assert(CROWS % DEPTH == 0 && CROWS >= 2 * DEPTH && CROWS <= 64, "chunk shape");
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t wpg = blockDim.x >> 6;
+  std::uint32_t* ctr = a.wg_ctr + blockIdx.x * kCtrStride;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);  // the reset has reached L2 before any wave of this group grabs
+  }
+  fill_lds(a.tabs, lds);
+  const LaneConst kc = lane_const(lane);
+  const std::uint32_t hcon = a.tabs->horner[lane & 31u];
+  const bool lo_half = lane < 32u;
+  const std::uint32_t inj_const =
+      lo_half ? 0u
+              : static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(a.init_default),
+                                                                lane & 31u, 1)) & hcon;
+  __syncthreads();
+
+  const std::uint32_t R = R1 ? 1u : a.len / kRow;
+  std::uint32_t C = R1 ? static_cast<std::uint32_t>(CROWS) : (CROWS + R - 1) / R;
+  if (!R1)
+    while ((C * R) % DEPTH) ++C;
+  const std::uint32_t NIT = C * R / DEPTH;            // iterations per chunk (>= 2)
+  const std::uint32_t NC = (a.nblocks + C - 1) / C;   // chunks in the batch; only the last is partial
+  const std::uint32_t c0 = static_cast<std::uint32_t>(blockIdx.x * static_cast<std::uint64_t>(NC) / gridDim.x);
+  const std::uint32_t ncw =
+      static_cast<std::uint32_t>((blockIdx.x + 1) * static_cast<std::uint64_t>(NC) / gridDim.x) - c0;
+  if (wid >= ncw) return;
+  const std::uint64_t brow = static_cast<std::uint64_t>(R) * kRow;  // bytes per block
+  const std::uintptr_t loff = lane * kSeg;
+
+  // The counter address goes through an opaque VGPR zero: with a provably uniform address the
+  // compiler's atomic optimizer rewrites the add into a wave-aggregated form that broadcasts the
+  // result with v_readfirstlane at once, i.e. a vmcnt(0) drain of the row pipeline at every grab.
+  std::uint32_t vzero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+  std::uint32_t* const vctr = ctr + vzero;
+
+  struct Chunk {
+    std::uint32_t fb, nb, vrows;  // first block, blocks, rows holding data
+    std::uintptr_t base;          // address of its first row
+  };
+  auto chunk = [&](std::uint32_t q) {
+    Chunk c;
+    c.fb = (c0 + q) * C;
+    c.nb = a.nblocks - c.fb < C ? a.nblocks - c.fb : C;
+    c.vrows = c.nb * R;
+    c.base = reinterpret_cast<std::uintptr_t>(a.base) + static_cast<std::uint64_t>(c.fb) * brow;
+    return c;
+  };
+  auto load_row = [&](std::uintptr_t rowp, uint4 (&q)[4]) {
+    const std::uintptr_t p = rowp + loff;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i);
+  };
+
+  Chunk cur = chunk(wid), nxt = cur;
+  bool nvalid = false;
+  auto grab = [&]() -> std::uint32_t {  // lane 0: wave-local id of the next chunk, minus wpg
+    std::uint32_t v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(vctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+  };
+  std::uint32_t nv = grab();
+  uint4 buf[DEPTH][4];
+#pragma unroll
+  for (int s = 0; s < DEPTH - ILP; ++s)
+    load_row(cur.base + static_cast<std::uint64_t>(s < cur.vrows ? s : cur.vrows - 1) * kRow, buf[s]);
+
+  // One flat loop over iterations of DEPTH rows (a nested chunk loop makes the compiler's wait
+  // counters merge pessimistically at the inner loop head and drain the pipeline).
+  std::uint32_t it = 0, B = 0, r = 0, kb = 0, keep = 0;
+  for (;;) {
+    const std::uint32_t row0 = it * DEPTH;
+    const bool last_it = it + 1 == NIT;
+    const std::uintptr_t clast = cur.base + static_cast<std::uint64_t>(cur.vrows - 1) * kRow;
+#pragma unroll
+    for (int q = 0; q < DEPTH; q += ILP) {
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) {
+        const int x = q + DEPTH - ILP + i;  // issue row row0 + x
+        std::uintptr_t rp;
+        if (x < DEPTH || !last_it) {
+          const std::uint32_t ri = row0 + x;
+          rp = ri < cur.vrows ? cur.base + static_cast<std::uint64_t>(ri) * kRow : clast;
+        } else {
+          const std::uint32_t ri = x - DEPTH;  // row of the next chunk
+          const std::uint32_t rn = ri < nxt.vrows ? ri : nxt.vrows - 1;
+          rp = nvalid ? nxt.base + static_cast<std::uint64_t>(rn) * kRow : clast;
+        }
+        load_row(rp, buf[x % DEPTH]);
+      }
+      // Keep the row loads ahead of this step's table work: left alone, the scheduler sinks them
+      // below the first lookups (their scalar addresses come late), halving the rows in flight.
+      __builtin_amdgcn_sched_barrier(0);
+      Reg p[ILP];
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) p[i] = Reg{0, 0};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].x, kc);
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].y, kc);
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].z, kc);
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].w, kc);
+      }
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) {
+        const std::uint32_t v = lane_shift(lds, p[i].value(), kc);
+        if (row0 + q + i < cur.vrows) {
+          std::uint32_t term;
+          if (R1 || r == 0) {
+            term = inj_const;
+            if (a.init_raw) {
+              const std::uint32_t init = sload32(a.init_raw, cur.fb + kb);
+              term = lo_half ? 0u
+                             : static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init),
+                                                                                lane & 31u, 1)) & hcon;
+            }
+          } else {
+            term = lo_half ? static_cast<std::uint32_t>(
+                                 __builtin_amdgcn_sbfe(static_cast<std::int32_t>(B), lane, 1)) & hcon
+                           : 0u;
+          }
+          const std::uint32_t Bn = __builtin_amdgcn_readlane(wave_xor_to_lane63(v ^ term), 63);
+          if (R1 || ++r == R) {
+            keep = lane == kb ? (Bn ^ a.out_xor) : keep;
+            ++kb;
+            r = 0;
+            B = 0;
+          } else {
+            B = Bn;
+          }
+        }
+      }
+      if (q == 0 && it == 1) {  // rows just processed were issued after the grab: its id is back
+        const std::uint32_t qn = wpg + __builtin_amdgcn_readfirstlane(nv);
+        nvalid = qn < ncw;
+        if (nvalid) nxt = chunk(qn);
+      }
+    }
+    if (last_it) {
+      if (lane < cur.nb) a.out[cur.fb + lane] = keep;
+      if (!nvalid) break;
+      cur = nxt;
+      nvalid = false;
+      it = 0;
+      kb = 0;
+      nv = grab();
+    } else {
+      ++it;
+    }
+  }
+}
+
 // Combine the partials of blocks that were split between waves. One thread per wave; the thread
 // whose wave holds a block's head row walks the following waves' first pieces.
 __device__ __forceinline__ void crc_fixup_body(const RowsArgs& a) {

@@ -77,7 +77,11 @@ struct RowsArgs {
   std::uint32_t total_rows;          // uniform only (irregular reads row_scan[nblocks])
   std::uint32_t nwaves;
   std::uint32_t snap_blocks;         // uniform: partition by whole blocks (no seams)
+  std::uint32_t* wg_ctr;             // packed: one work counter per workgroup, kCtrStride words apart
 };
+
+// Packed kernel work counters: one per workgroup, each on its own 128-byte line.
+constexpr std::uint32_t kCtrStride = 32;
 
 // rows(b): wave-rows a block of n bytes occupies (every block, even n = 0, owns >= 1 row), and
 // h(b): bytes of its head row (row 0), in [0, kRow].

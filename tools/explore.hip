@@ -156,6 +156,18 @@ __global__ __launch_bounds__(1024) void k_packed_stamped(RowsArgs a, unsigned lo
   }
 }
 
+__global__ __launch_bounds__(1024) void k_dyn_stamped(RowsArgs a, unsigned long long* stamps) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  const std::uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  dev::crc_packed_dyn_body<4, 2, true, 16>(a, lds);
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63u) == 0) {
+    stamps[2 * wave] = t0;
+    stamps[2 * wave + 1] = t1;
+  }
+}
+
 namespace {
 DeviceTables* g_tabs = nullptr;
 std::uint8_t* g_dummy = nullptr;
@@ -184,6 +196,21 @@ __global__ __launch_bounds__(T) void k_packed(RowsArgs a) {
   dev::crc_packed_body<D, I, R1, SP>(a, lds);
 }
 
+template <int D, int I, bool R1, int T, int CR>
+__global__ __launch_bounds__(T) void k_packed_dyn(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  dev::crc_packed_dyn_body<D, I, R1, CR>(a, lds);
+}
+
+std::uint32_t* g_ctr = nullptr;
+
+template <int D, int I, int CR, int T = 1024>
+void PD(RowsArgs a, hipStream_t s) {
+  a.wg_ctr = g_ctr;
+  if (a.len == kRow) hipLaunchKernelGGL((k_packed_dyn<D, I, true, T, CR>), dim3(g_ncu), dim3(T), 0, s, a);
+  else hipLaunchKernelGGL((k_packed_dyn<D, I, false, T, CR>), dim3(g_ncu), dim3(T), 0, s, a);
+}
+
 template <int D, int I, int T = 1024, bool SP = false>
 void PK(RowsArgs a, hipStream_t s) {
   a.nwaves = g_ncu * (T / 64);
@@ -200,6 +227,8 @@ const V kVariants[] = {
     {"interf L0 V0", IF<0, 0>}, {"interf L72 V0", IF<72, 0>}, {"interf L0 V128", IF<0, 128>},
     {"interf L72 V128", IF<72, 128>}, {"interf L36 V0", IF<36, 0>}, {"interf L144 V0", IF<144, 0>},
     {"interf L0 V256", IF<0, 256>},
+    {"dyn D4 I2 C8", PD<4, 2, 8>}, {"dyn D4 I2 C16", PD<4, 2, 16>}, {"dyn D4 I2 C32", PD<4, 2, 32>},
+    {"dyn D4 I2 C64", PD<4, 2, 64>}, {"dyn T768 D4 I2 C16", PD<4, 2, 16, 768>},
     {"packed D4 I2", PK<4, 2>}, {"packed D4 I1", PK<4, 1>}, {"packed D3 I1", PK<3, 1>},
     {"packed T512 D8 I4", PK<8, 4, 512>}, {"packed T512 D6 I3", PK<6, 3, 512>},
     {"packed T768 D6 I2", PK<6, 2, 768>}, {"packed T768 D6 I3", PK<6, 3, 768>},
@@ -275,6 +304,7 @@ extern "C" int explore_run(int v, const std::uint8_t* base, std::uint64_t n, std
     hipMalloc(&g_dummy, 256);
     hipMemset(g_dummy, 0, 256);
     hipMalloc(&g_seams, sizeof(Seam) * 2 * g_ncu * kWavesPerWG);
+    hipMalloc(&g_ctr, 4 * kCtrStride * g_ncu);
   }
   if (v == kNV) {
     hipLaunchKernelGGL(k_stream, dim3(g_ncu * 8), dim3(256), 0, st, reinterpret_cast<const uint4*>(base),
@@ -341,7 +371,7 @@ extern "C" int explore_run_irr(int v, const std::uint8_t* base, const std::uint6
 }
 
 extern "C" int explore_stamped(const std::uint8_t* base, std::uint64_t n, std::uint32_t* out,
-                               unsigned long long* stamps, void* stream) {
+                               unsigned long long* stamps, void* stream, int dyn) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!g_tabs && explore_run(kNV, base, n, 4096, out, stream)) return 1;
   RowsArgs a{};
@@ -356,6 +386,8 @@ extern "C" int explore_stamped(const std::uint8_t* base, std::uint64_t n, std::u
   a.dummy = g_dummy;
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = g_ncu * 16;
-  hipLaunchKernelGGL(k_packed_stamped, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
+  a.wg_ctr = g_ctr;
+  if (dyn) hipLaunchKernelGGL(k_dyn_stamped, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
+  else hipLaunchKernelGGL(k_packed_stamped, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -8,19 +8,22 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import tinykvpp_amd as tk
 lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libexplore.so"))
-lib.explore_stamped.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+lib.explore_stamped.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 torch.cuda.set_device(0); tk.set_device(0)
+DYN = int(sys.argv[1]) if len(sys.argv) > 1 else 0  # 1: dynamically scheduled packed body
 n = 1 << 20
 data = torch.empty(n * 4096, dtype=torch.uint8, device="cuda")
 tk.fill_synthetic_uniform(data, 4096, n)
 out = torch.empty(n, dtype=torch.int32, device="cuda")
+ref = tk.crc32_batch_uniform(data, 4096, n).clone()
 W = torch.cuda.get_device_properties(0).multi_processor_count * 16
 st = torch.empty(2 * W, dtype=torch.int64, device="cuda")
 sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 for rep in range(4):
     assert lib.explore_stamped(ctypes.c_void_p(data.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
-                               ctypes.c_void_p(st.data_ptr()), sp) == 0
+                               ctypes.c_void_p(st.data_ptr()), sp, DYN) == 0
     torch.cuda.synchronize()
+    assert torch.equal(out, ref), "stamped kernel output differs"
     s = st.cpu().numpy().reshape(-1, 2).astype(np.float64) * 10.0  # ns
     t0 = s[:, 0].min()
     start, end = s[:, 0] - t0, s[:, 1] - t0
