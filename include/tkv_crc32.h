@@ -103,6 +103,51 @@ int tkv_wal_verify(const uint8_t *h_wal, uint64_t size, uint64_t *n_good, uint64
  * h_sizes[i] (>= 8), write crc32 of bytes [8, size) LE at offset 4 (wal.cpp:54-58). */
 int tkv_wal_stamp(uint8_t *h_buf, const uint64_t *h_offsets, const uint32_t *h_sizes, uint64_t n);
 
+/* ---- SSTable data-block stamping (the format is defined here) ----------- */
+
+/* The reference writes sstable_data_block_header::crc32_ = 0 (sstable_writer.cpp:138-144) and never
+ * reads it (sstable_reader.cpp:61-89), so this stamp is this library's format decision, not
+ * reference behaviour ("parity unpinned"). A data-block image as get_data_block builds it
+ * (sstable_writer.cpp:150-168) is varint(20) | header[20] | varint(n) | body[n], padded to the size
+ * the index entry records (index_entry::data_block_size_, sstable_format.hpp:117-121); the header's
+ * crc32_ field (sstable_format.hpp:97) therefore sits at image byte TKV_SST_CRC_OFFSET. The stamp is
+ * the CRC-32 of the whole image [0, size) with those 4 bytes read as zero, stored little-endian in
+ * the field. Images must be at least TKV_SST_MIN_IMAGE bytes and shorter than 4 GiB. */
+#define TKV_SST_CRC_OFFSET 17u
+#define TKV_SST_MIN_IMAGE 22u
+
+/* Stamp n data-block images in place in a host buffer (an SSTable file image being written). */
+int tkv_sst_stamp_blocks(uint8_t *h_file, const uint64_t *h_offsets, const uint64_t *h_sizes, uint64_t n);
+
+/* Verify n images of a host buffer; *n_bad = number of mismatching images, *first_bad = index of
+ * the first (n when none). Returns TKV_OK or TKV_CORRUPTED (read_data_block's corrupted status,
+ * sstable_reader.cpp:73-86). */
+int tkv_sst_verify_blocks(const uint8_t *h_file, const uint64_t *h_offsets, const uint64_t *h_sizes, uint64_t n,
+                          uint64_t *n_bad, uint64_t *first_bad);
+
+/* Device-resident images: d_out[i] = the stamp value of image i (CRC with the field read as zero),
+ * whatever the field holds now. With store != 0 the value is also written into the field (stamping
+ * on the device). Asynchronous on `stream`. */
+int tkv_sst_block_crcs_device(uint8_t *d_file, const uint64_t *d_offsets, const uint32_t *d_sizes, uint32_t *d_out,
+                              uint64_t n, int store, void *stream);
+
+/* ---- CRC-32C (Castagnoli) — SURVEY.md §8f rank 4 ------------------------------------------------ */
+
+/* Same engine and kernels with the tables of the Castagnoli polynomial (reflected 0x82F63B78,
+ * init/xorout 0xFFFFFFFF: iSCSI, RFC 3720 §B.4). Not reference behaviour; offered for a
+ * format-versioned alternative. Arguments and conventions as for the tkv_crc32_* functions. */
+#define TKV_CRC32C_POLYNOMIAL 0x82F63B78u
+int tkv_crc32c_update(uint32_t raw_state, const void *data, size_t len, uint32_t *out_raw);
+int tkv_crc32c_update_device(uint32_t raw_state, const void *d_data, size_t len, uint32_t *d_out_raw,
+                             void *stream);
+int tkv_crc32c_batch_device(const uint8_t *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths,
+                            const uint32_t *d_init_raw, uint32_t *d_out_final, uint64_t n, void *stream);
+int tkv_crc32c_batch_uniform_device(const uint8_t *d_base, uint64_t stride, uint64_t len,
+                                    const uint32_t *d_init_raw, uint32_t *d_out_final, uint64_t n,
+                                    void *stream);
+int tkv_crc32c_batch_host(const uint8_t *h_base, const uint64_t *h_offsets, const uint32_t *h_lengths,
+                          const uint32_t *h_init_raw, uint32_t *h_out_final, uint64_t n);
+
 /* ---- synthetic data (SURVEY.md §8d generator; bench/test inputs) ------------------------------- */
 
 int tkv_fill_synthetic_uniform(uint8_t *d_dst, uint64_t stride, uint64_t len, uint64_t first_block,
@@ -115,6 +160,8 @@ int tkv_fill_synthetic_blocks(uint8_t *d_base, const uint64_t *d_offsets, const 
 /* Copy the constant tables the kernels use (layout of tkv::DeviceTables) into `out`; returns the
  * byte size needed (call with out = NULL to query). */
 size_t tkv_debug_tables(void *out, size_t cap);
+/* Same for any reflected polynomial (TKV_CRC32_POLYNOMIAL, TKV_CRC32C_POLYNOMIAL). */
+size_t tkv_debug_tables_poly(uint32_t poly, void *out, size_t cap);
 
 /* Host GF(2) helpers the decomposition rests on: a*b mod P and x^(8n) mod P, reflected. */
 uint32_t tkv_debug_multmodp(uint32_t a, uint32_t b);

@@ -125,3 +125,44 @@ void oracle_crc_batch(const uint8_t *base, const uint64_t *offsets, const uint32
     out[i] = oracle_update(s, base + offsets[i], lengths[i]) ^ ORACLE_INIT;
   }
 }
+
+/* ---- CRC-32C (not in the reference) ----
+ * Published algorithm: CRC-32C / Castagnoli, RFC 3720 §B.4 (iSCSI): reflected polynomial
+ * 0x82F63B78, init 0xFFFFFFFF, xorout 0xFFFFFFFF, same byte-at-a-time Sarwate loop as
+ * crc32.cpp:9-16 with the other table. Pinned by the RFC 3720 §B.4 vectors and the catalogue check
+ * value crc32c("123456789") = 0xE3069283 in tests/test_oracle.py. */
+#define ORACLE_POLY_C 0x82F63B78u
+static uint32_t g_table_c[256];
+static int g_table_c_ready = 0;
+
+void oracle_table_c(uint32_t out[256]) {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int bit = 0; bit < 8; ++bit) c = (c & 1u) ? (c >> 1) ^ ORACLE_POLY_C : (c >> 1);
+    out[i] = c;
+  }
+}
+
+uint32_t oracle_update_c(uint32_t raw, const uint8_t *p, size_t n) {
+  if (!g_table_c_ready) {
+    oracle_table_c(g_table_c);
+    g_table_c_ready = 1;
+  }
+  for (size_t i = 0; i < n; ++i) raw = (raw >> 8) ^ g_table_c[(p[i] ^ raw) & 0xFFu];
+  return raw;
+}
+
+uint32_t oracle_crc32c(const uint8_t *p, size_t n) { return oracle_update_c(ORACLE_INIT, p, n) ^ ORACLE_INIT; }
+
+/* ---- SSTable data-block stamp (format of include/tkv_crc32.h; parity unpinned) ----
+ * Image = varint(20) | header[20] | varint(n) | body (sstable_writer.cpp:150-168); the header's
+ * crc32_ (sstable_format.hpp:97) is at image byte 17. Stamp = crc32 of the image with those 4 bytes
+ * read as zero: computed here literally, by feeding zeros in their place. */
+uint32_t oracle_sst_stamp(const uint8_t *img, size_t size) {
+  static const uint8_t zeros[4] = {0, 0, 0, 0};
+  if (size < 22) return 0;
+  uint32_t raw = oracle_update(ORACLE_INIT, img, 17);
+  raw = oracle_update(raw, zeros, 4);
+  raw = oracle_update(raw, img + 21, size - 21);
+  return raw ^ ORACLE_INIT;
+}

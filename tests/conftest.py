@@ -39,11 +39,30 @@ class Oracle:
         o.oracle_zipf_lengths.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p]
         o.oracle_crc_synthetic_lens.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
         o.oracle_crc_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p]
+        o.oracle_crc32c.restype = ctypes.c_uint32
+        o.oracle_crc32c.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        o.oracle_update_c.restype = ctypes.c_uint32
+        o.oracle_update_c.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+        o.oracle_table_c.argtypes = [ctypes.c_void_p]
+        o.oracle_sst_stamp.restype = ctypes.c_uint32
+        o.oracle_sst_stamp.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
         self.lib = o
 
     def crc(self, data: bytes) -> int:
         a = np.frombuffer(bytes(data), np.uint8)
         return self.lib.oracle_crc32(a.ctypes.data if a.size else None, a.size)
+
+    def crc_c(self, data: bytes) -> int:
+        a = np.frombuffer(bytes(data), np.uint8)
+        return self.lib.oracle_crc32c(a.ctypes.data if a.size else None, a.size)
+
+    def update_c(self, raw: int, data: bytes) -> int:
+        a = np.frombuffer(bytes(data), np.uint8)
+        return self.lib.oracle_update_c(raw, a.ctypes.data if a.size else None, a.size)
+
+    def sst_stamp(self, image: bytes) -> int:
+        a = np.frombuffer(bytes(image), np.uint8)
+        return self.lib.oracle_sst_stamp(a.ctypes.data, a.size)
 
     def update(self, raw: int, data: bytes) -> int:
         a = np.frombuffer(bytes(data), np.uint8)

@@ -39,10 +39,10 @@ def test_no_gpu_is_an_error_not_a_fallback(lib):
     assert e.value.code == 2  # io_error: no device, and no CPU path to fall back to
 
 
-def load_tables(lib):
-    n = lib.tkv_debug_tables(None, 0)
+def load_tables(lib, poly=0xEDB88320):
+    n = lib.tkv_debug_tables_poly(poly, None, 0)
     buf = np.zeros(n // 4, np.uint32)
-    lib.tkv_debug_tables(buf.ctypes.data, n)
+    lib.tkv_debug_tables_poly(poly, buf.ctypes.data, n)
     o = 0
     slice_ = buf[o:o + 1024].reshape(4, 256); o += 1024
     lane = buf[o:o + 8 * 16 * 64].reshape(8, 16, 64); o += 8 * 16 * 64
@@ -50,7 +50,9 @@ def load_tables(lib):
     row_pow = buf[o:o + 64]; o += 64
     head = buf[o:o + (ROW + 1) * 32].reshape(ROW + 1, 32); o += (ROW + 1) * 32
     shift32 = buf[o:o + 128].reshape(8, 16); o += 128
+    built_for = int(buf[o]); o += 4  # poly + 3 pad words
     assert o * 4 == n
+    assert built_for == poly
     return slice_, lane, horner, row_pow, head, shift32
 
 
@@ -79,6 +81,25 @@ def test_gf2_helpers(lib, oracle):
         z = lib.tkv_debug_x8nmodp(n)
         for v in rng.integers(0, 2**32, 4, dtype=np.uint64):
             assert lib.tkv_debug_multmodp(z, int(v)) == shift_zeros(oracle, int(v), n)
+
+
+def test_crc32c_tables(lib, oracle):
+    """The Castagnoli tables obey the same identities under the CRC-32C oracle."""
+    s, lane, horner, row_pow, head, shift32 = load_tables(lib, 0x82F63B78)
+    t = np.zeros(256, np.uint32)
+    oracle.lib.oracle_table_c(t.ctypes.data)
+    assert np.array_equal(s[0], t)
+    zc = lambda reg, n: oracle.update_c(reg, b"\0" * n)  # noqa: E731
+    for k in range(1, 4):
+        assert int(s[k][77]) == zc(int(s[0][77]), k)
+    for l in (0, 40, 63):
+        assert int(lane[5][11][l]) == zc(11 << 20, (63 - l) * SEG)
+    assert int(horner[9]) == zc(1 << 9, ROW)
+    assert int(head[1234][30]) == zc(1 << 30, 1234)
+    assert int(shift32[2][3]) == zc(3 << 8, 32)
+    assert int(row_pow[1]) == zc(0x80000000, 2 * ROW)
+    # the tables differ from the reference's: the polynomial really is a parameter
+    assert not np.array_equal(s[0], load_tables(lib)[0][0])
 
 
 def test_lane_shift_horner_head_tables(tables, oracle):

@@ -1,0 +1,121 @@
+"""GPU parity for the §8f rows beyond the WAL: CRC-32C on the same engine and SSTable data-block
+stamping. CRC-32C is checked against the oracle restatement pinned by RFC 3720 §B.4; the SSTable
+stamp against the oracle's literal zero-field CRC (the format is this library's: parity unpinned
+by the reference, whose crc32_ fields stay 0, sstable_writer.cpp:138-144)."""
+import numpy as np
+import pytest
+
+import tinykvpp_amd as tk
+import tinykvpp_amd.sst as sst
+from test_oracle import RFC3720_B4
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+# ---- CRC-32C ----------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("data,want", RFC3720_B4)
+def test_crc32c_published_vectors(gpu, data, want):
+    assert tk.crc32c().update(data).finalize() == want
+
+
+def test_crc32c_incremental_and_device(gpu, oracle):
+    rng = np.random.default_rng(11)
+    data = rng.bytes(300_000)
+    c = tk.crc32c()
+    for a, b in ((0, 7), (7, 70_001), (70_001, 300_000)):
+        c = c.update(data[a:b])
+    assert c.finalize() == oracle.crc_c(data)
+    t = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(gpu)
+    assert tk.crc32c().update(t).finalize() == oracle.crc_c(data)
+
+
+@pytest.mark.parametrize("blen,n", [(4096, 300_000), (65536, 4096), (1000, 5000), (4100, 777)])
+def test_crc32c_uniform(gpu, oracle, blen, n):
+    """(4096, 300 000) and (65536, 4096) take the packed kernel; the others the generic rows."""
+    rng = np.random.default_rng(blen)
+    host = rng.integers(0, 256, blen * n, dtype=np.uint8)
+    got = u32(tk.crc32_batch_uniform(torch.from_numpy(host).to(gpu), blen, n, algo="crc32c"))
+    idx = rng.integers(0, n, 64)
+    for i in idx:
+        assert int(got[i]) == oracle.crc_c(host[i * blen:(i + 1) * blen].tobytes())
+
+
+def test_crc32c_irregular_and_host(gpu, oracle):
+    rng = np.random.default_rng(7)
+    lens = rng.integers(0, 20_000, 3000).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.int64))]) + rng.integers(0, 3, lens.size).cumsum()
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1] + 8), dtype=np.uint8)
+    want = np.array([oracle.crc_c(host[o:o + l].tobytes()) for o, l in zip(offs, lens)], np.uint32)
+    d = torch.from_numpy(host).to(gpu)
+    got = u32(tk.crc32_batch(d, torch.from_numpy(offs.astype(np.int64)).to(gpu),
+                             torch.from_numpy(lens.astype(np.int32)).to(gpu), algo="crc32c"))
+    assert np.array_equal(got, want)
+    assert np.array_equal(tk.crc32_batch_host(host, offs.astype(np.uint64), lens, algo="crc32c"), want)
+    # the two families really differ
+    assert not np.array_equal(tk.crc32_batch_host(host, offs.astype(np.uint64), lens), want)
+
+
+# ---- SSTable data-block stamping ----------------------------------------------------------------------
+
+def make_file(rng, nblocks):
+    """An SSTable-like file image: data-block images back to back (sstable_writer.cpp:131-169)."""
+    imgs = []
+    for _ in range(nblocks):
+        entries = [(rng.bytes(int(rng.integers(8, 40))), rng.bytes(int(rng.integers(0, 300))))
+                   for _ in range(int(rng.integers(1, 30)))]
+        imgs.append(sst.encode_data_block_image(entries))
+    sizes = np.array([len(i) for i in imgs], np.uint64)
+    offs = np.concatenate([[0], np.cumsum(sizes[:-1])]).astype(np.uint64)
+    return np.frombuffer(b"".join(imgs), np.uint8).copy(), offs, sizes
+
+
+def test_sst_stamp_matches_oracle_and_verifies(gpu, oracle):
+    rng = np.random.default_rng(21)
+    f, offs, sizes = make_file(rng, 500)
+    sst.stamp_blocks(f, offs, sizes)
+    for o, s in zip(offs[::7], sizes[::7]):
+        img = f[int(o):int(o + s)].tobytes()
+        assert int.from_bytes(img[17:21], "little") == oracle.sst_stamp(img)
+    assert sst.verify_blocks(f, offs, sizes) == ("ok", 0, 500)
+
+
+@pytest.mark.parametrize("where", ["varint", "header", "crc_field", "body", "padding"])
+def test_sst_corruption_detected(gpu, where):
+    rng = np.random.default_rng(22)
+    f, offs, sizes = make_file(rng, 64)
+    sst.stamp_blocks(f, offs, sizes)
+    victim = 41
+    o, s = int(offs[victim]), int(sizes[victim])
+    pos = {"varint": 0, "header": 5, "crc_field": 19, "body": 30, "padding": s - 1}[where]
+    f[o + pos] ^= 0x10
+    assert sst.verify_blocks(f, offs, sizes) == ("corrupted", 1, victim)
+
+
+def test_sst_device_stamp_equals_host_stamp(gpu):
+    rng = np.random.default_rng(23)
+    f, offs, sizes = make_file(rng, 2000)
+    host = f.copy()
+    sst.stamp_blocks(host, offs, sizes)
+    f[offs.astype(np.int64)[:, None] + np.arange(17, 21)] = rng.integers(0, 256, (offs.size, 4), dtype=np.uint8)
+    d = torch.from_numpy(f).to(gpu)
+    o = torch.from_numpy(offs.astype(np.int64)).to(gpu)
+    sz = torch.from_numpy(sizes.astype(np.int32)).to(gpu)
+    vals = u32(sst.block_crcs_device(d, o, sz))          # whatever the fields hold
+    want = host[offs.astype(np.int64)[:, None] + np.arange(17, 21)].copy().view("<u4").ravel()
+    assert np.array_equal(vals, want)
+    sst.block_crcs_device(d, o, sz, store=True)           # stamp on the device
+    assert np.array_equal(d.cpu().numpy(), host)
+    assert sst.verify_blocks(d.cpu().numpy(), offs, sizes)[0] == "ok"
+
+
+def test_sst_rejects_short_images(gpu):
+    f = np.zeros(100, np.uint8)
+    with pytest.raises(tk.TkvError):
+        sst.stamp_blocks(f, [0], [21])

@@ -267,19 +267,22 @@ def aggregates(crcs):
     return int(np.bitwise_xor.reduce(crcs)), int(crcs.astype(np.uint64).sum() & 0xFFFFFFFF)
 
 
-@pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg5"])
 def test_full_size_uniform_configs(gpu, cfg):
+    """cfg5 (4 M x 64 KiB = 256 GiB, BASELINE's 8-GPU config) runs here as its eight 32 GiB
+    per-GPU shards in turn on one device; its aggregates pin the sharded result."""
     c = golden("synthetic.json")[cfg]
     n, blen = c["nblocks"], c["len"]
     got = np.zeros(n, np.uint32)
-    chunk = min(n, (4 << 30) // blen)  # 4 GiB of device data at a time
+    chunk = min(n, ((32 if cfg == "cfg5" else 4) << 30) // blen)  # device data per pass
     data = torch.empty(chunk * blen, dtype=torch.uint8, device=gpu)
     for first in range(0, n, chunk):
         m = min(chunk, n - first)
         tk.fill_synthetic_uniform(data, blen, m, first_block=first)
         got[first:first + m] = u32(tk.crc32_batch_uniform(data, blen, m))
-    assert [int(x) for x in got[:len(c["first"])]] == c["first"]
-    assert int(got[-1]) == c["last"]
+    if "first" in c:
+        assert [int(x) for x in got[:len(c["first"])]] == c["first"]
+        assert int(got[-1]) == c["last"]
     assert aggregates(got) == (c["xor"], c["sum32"])
 
 

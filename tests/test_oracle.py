@@ -98,3 +98,58 @@ def test_init_identity(oracle, n):
     for s in [0xFFFFFFFF, 0x12345678, 0]:
         shifted = oracle.update(s, b"\0" * n)
         assert oracle.update(s, d) == shifted ^ oracle.update(0, d)
+
+
+# ---- CRC-32C restatement: pinned by published vectors ----------------------
+
+RFC3720_B4 = [  # RFC 3720 §B.4 (iSCSI CRC32C examples), values as 32-bit integers
+    (bytes(32), 0x8A9136AA),
+    (bytes([0xFF] * 32), 0x62A8AB43),
+    (bytes(range(32)), 0x46DD794E),
+    (bytes(range(31, -1, -1)), 0x113FDB5C),
+    (b"123456789", 0xE3069283),  # CRC catalogue check value of CRC-32C (iSCSI)
+]
+
+
+@pytest.mark.parametrize("data,want", RFC3720_B4)
+def test_crc32c_published_vectors(oracle, data, want):
+    assert oracle.crc_c(data) == want
+
+
+def test_crc32c_incremental(oracle):
+    data = bytes(range(256)) * 5
+    raw = 0xFFFFFFFF
+    for a, b in ((0, 1), (1, 100), (100, 1280)):
+        raw = oracle.update_c(raw, data[a:b])
+    assert raw ^ 0xFFFFFFFF == oracle.crc_c(data)
+
+
+# ---- SSTable stamp restatement (format of include/tkv_crc32.h; parity unpinned) -------------------
+
+def test_sst_stamp_oracle_against_zlib(oracle):
+    import zlib
+    import tinykvpp_amd.sst as sst
+    rng = np.random.default_rng(5)
+    for n_entries in (1, 3, 40):
+        entries = [(rng.bytes(int(rng.integers(1, 40))), rng.bytes(int(rng.integers(0, 200))))
+                   for _ in range(n_entries)]
+        img = bytearray(sst.encode_data_block_image(entries))
+        img[sst.CRC_OFFSET:sst.CRC_OFFSET + 4] = rng.bytes(4)  # whatever the field holds
+        zeroed = bytes(img[:17]) + bytes(4) + bytes(img[21:])
+        assert oracle.sst_stamp(bytes(img)) == zlib.crc32(zeroed)
+
+
+def test_sst_image_layout():
+    """get_data_block's image (sstable_writer.cpp:137-168): varint(20) | header | varint(n) | body,
+    allocated as 8 + 20 + 8 + n bytes; header fields per sstable_format.hpp:91-99."""
+    import struct
+    import tinykvpp_amd.sst as sst
+    entries = [(b"key1", b"value1"), (b"k2", b"v")]
+    img = sst.encode_data_block_image(entries)
+    n = (8 + 4 + 6) + (8 + 2 + 1)
+    assert len(img) == 8 + 20 + 8 + n
+    assert img[0] == 20
+    count, usize, csize, comp, crc = struct.unpack_from("<IIIB3xI", img, 1)
+    assert (count, usize, csize, comp, crc) == (2, n, n, 0, 0)
+    assert img[21] == n and img[22:22 + 5] == b"\x04key1"
+    assert sst.CRC_OFFSET == 1 + 16

@@ -2,7 +2,8 @@
 
 The product is libtkv_crc32.so (HIP kernels for gfx950 + C ABI, include/tkv_crc32.h). This package
 is the Python mirror of the reference interface (frankie::core::crc32, crc32.hpp:32-49) and of the
-WAL CRC call sites (wal.cpp:54-58, 89-96), over ctypes.
+WAL CRC call sites (wal.cpp:54-58, 89-96), over ctypes; plus SSTable block stamping (sst) and the
+CRC-32C variant (crc32c), SURVEY.md §8f.
 """
 from ._lib import TkvError, check, load_library  # noqa: F401
 from .crc32 import (  # noqa: F401
@@ -10,6 +11,7 @@ from .crc32 import (  # noqa: F401
     crc32_batch,
     crc32_batch_host,
     crc32_batch_uniform,
+    crc32c,
     device_count,
     fill_synthetic_blocks,
     fill_synthetic_uniform,
@@ -20,4 +22,4 @@ from .crc32 import (  # noqa: F401
     kCRC32TableSize,
     set_device,
 )
-from . import wal  # noqa: F401
+from . import sst, wal  # noqa: F401

@@ -46,7 +46,16 @@ SIGNATURES = {
     "tkv_wal_stamp": (_int, [_u8p, _vp, _vp, _u64]),
     "tkv_fill_synthetic_uniform": (_int, [_u8p, _u64, _u64, _u64, _u64, _u64, _vp]),
     "tkv_fill_synthetic_blocks": (_int, [_u8p, _vp, _vp, _u64, _u64, _u64, _vp]),
+    "tkv_sst_stamp_blocks": (_int, [_u8p, _vp, _vp, _u64]),
+    "tkv_sst_verify_blocks": (_int, [_u8p, _vp, _vp, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    "tkv_sst_block_crcs_device": (_int, [_u8p, _vp, _vp, _vp, _u64, _int, _vp]),
+    "tkv_crc32c_update": (_int, [_u32, _vp, _sz, ctypes.POINTER(_u32)]),
+    "tkv_crc32c_update_device": (_int, [_u32, _vp, _sz, _vp, _vp]),
+    "tkv_crc32c_batch_device": (_int, [_u8p, _vp, _vp, _vp, _vp, _u64, _vp]),
+    "tkv_crc32c_batch_uniform_device": (_int, [_u8p, _u64, _u64, _vp, _vp, _u64, _vp]),
+    "tkv_crc32c_batch_host": (_int, [_u8p, _vp, _vp, _vp, _vp, _u64]),
     "tkv_debug_tables": (_sz, [_vp, _sz]),
+    "tkv_debug_tables_poly": (_sz, [_u32, _vp, _sz]),
     "tkv_debug_multmodp": (_u32, [_u32, _u32]),
     "tkv_debug_x8nmodp": (_u32, [_u64]),
 }

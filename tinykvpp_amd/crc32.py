@@ -53,10 +53,18 @@ def _host_view(data):
     return arr.ctypes.data, arr.nbytes, arr
 
 
+def _fn(algo, name):
+    """C ABI entry ``tkv_<algo>_<name>`` (algo: "crc32" = the reference's CRC, "crc32c")."""
+    if algo not in ("crc32", "crc32c"):
+        raise ValueError(f"unknown checksum family {algo!r}")
+    return getattr(load_library(), f"tkv_{algo}_{name}")
+
+
 class crc32:  # noqa: N801 - reference class name (crc32.hpp:32)
     """CRC-32/ISO-HDLC accumulator; raw register starts at 0xFFFFFFFF (crc32.hpp:48)."""
 
     __slots__ = ("_crc",)
+    _algo = "crc32"
 
     def __init__(self):
         self._crc = kCRC32DefaultValue
@@ -67,7 +75,6 @@ class crc32:  # noqa: N801 - reference class name (crc32.hpp:32)
         ``data``: bytes-like / numpy (host memory) or a torch uint8 tensor (device memory; the
         device path is asynchronous on ``stream`` but this call waits for the 4-byte result).
         """
-        lib = load_library()
         try:
             import torch
             is_dev = isinstance(data, torch.Tensor) and data.is_cuda
@@ -76,13 +83,13 @@ class crc32:  # noqa: N801 - reference class name (crc32.hpp:32)
         if is_dev:
             t = data.contiguous().view(torch.uint8)
             out = torch.empty(1, dtype=torch.int32, device=t.device)
-            check(lib.tkv_crc32_update_device(self._crc, ctypes.c_void_p(t.data_ptr()), t.numel(),
-                                              ctypes.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+            check(_fn(self._algo, "update_device")(self._crc, ctypes.c_void_p(t.data_ptr()), t.numel(),
+                                                   ctypes.c_void_p(out.data_ptr()), _stream_ptr(stream)))
             self._crc = int(out.cpu().numpy().view(np.uint32)[0])
         else:
             ptr, n, keep = _host_view(data)
             res = ctypes.c_uint32(0)
-            check(lib.tkv_crc32_update(self._crc, ctypes.c_void_p(ptr), n, ctypes.byref(res)))
+            check(_fn(self._algo, "update")(self._crc, ctypes.c_void_p(ptr), n, ctypes.byref(res)))
             del keep
             self._crc = res.value
         return self
@@ -100,6 +107,14 @@ class crc32:  # noqa: N801 - reference class name (crc32.hpp:32)
         return self._crc
 
 
+class crc32c(crc32):  # noqa: N801
+    """CRC-32C (Castagnoli, reflected 0x82F63B78, init/xorout 0xFFFFFFFF; RFC 3720 §B.4) on the same
+    engine: SURVEY.md §8f rank 4, a format-versioned alternative, not reference behaviour."""
+
+    __slots__ = ()
+    _algo = "crc32c"
+
+
 # ---- batch engine -------------------------------------------------------------------------------
 
 def _u32_view(t):
@@ -107,7 +122,7 @@ def _u32_view(t):
     return t.view(torch.int32) if t.dtype != torch.int32 else t
 
 
-def crc32_batch(data, offsets, lengths, init_raw=None, out=None, stream=None):
+def crc32_batch(data, offsets, lengths, init_raw=None, out=None, stream=None, algo="crc32"):
     """Irregular batch on the GPU: block i = data[offsets[i] : offsets[i] + lengths[i]].
 
     data: uint8 CUDA tensor; offsets: int64 CUDA tensor; lengths: int32 CUDA tensor (< 2^32 bytes
@@ -124,14 +139,15 @@ def crc32_batch(data, offsets, lengths, init_raw=None, out=None, stream=None):
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=data.device)
     initp = ctypes.c_void_p(init_raw.data_ptr()) if init_raw is not None else None
-    check(load_library().tkv_crc32_batch_device(
+    check(_fn(algo, "batch_device")(
         ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
         ctypes.c_void_p(lengths.data_ptr()), initp, ctypes.c_void_p(out.data_ptr()), n,
         _stream_ptr(stream)))
     return out
 
 
-def crc32_batch_uniform(data, length, n, stride=None, init_raw=None, out=None, stream=None, offset=0):
+def crc32_batch_uniform(data, length, n, stride=None, init_raw=None, out=None, stream=None, offset=0,
+                        algo="crc32"):
     """Uniform batch on the GPU: block i = data[offset + i*stride : + length] (stride = length)."""
     import torch
     stride = length if stride is None else stride
@@ -140,13 +156,13 @@ def crc32_batch_uniform(data, length, n, stride=None, init_raw=None, out=None, s
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=data.device)
     initp = ctypes.c_void_p(init_raw.data_ptr()) if init_raw is not None else None
-    check(load_library().tkv_crc32_batch_uniform_device(
+    check(_fn(algo, "batch_uniform_device")(
         ctypes.c_void_p(data.data_ptr() + offset), stride, length, initp,
         ctypes.c_void_p(out.data_ptr()), n, _stream_ptr(stream)))
     return out
 
 
-def crc32_batch_host(data, offsets, lengths, init_raw=None, devices=None):
+def crc32_batch_host(data, offsets, lengths, init_raw=None, devices=None, algo="crc32"):
     """Host-memory batch (numpy): pinned staging, H2D / kernel / D2H overlapped. Returns uint32."""
     lib = load_library()
     buf = np.ascontiguousarray(data).view(np.uint8)
@@ -156,10 +172,12 @@ def crc32_batch_host(data, offsets, lengths, init_raw=None, devices=None):
     out = np.zeros(off.size, np.uint32)
     initp = None if ini is None else ctypes.c_void_p(ini.ctypes.data)
     if devices is None:
-        check(lib.tkv_crc32_batch_host(ctypes.c_void_p(buf.ctypes.data), ctypes.c_void_p(off.ctypes.data),
-                                       ctypes.c_void_p(ln.ctypes.data), initp,
-                                       ctypes.c_void_p(out.ctypes.data), off.size))
+        check(_fn(algo, "batch_host")(ctypes.c_void_p(buf.ctypes.data), ctypes.c_void_p(off.ctypes.data),
+                                      ctypes.c_void_p(ln.ctypes.data), initp,
+                                      ctypes.c_void_p(out.ctypes.data), off.size))
     else:
+        if algo != "crc32":
+            raise ValueError("the multi-GPU host batch serves the reference CRC-32 only")
         devs = (ctypes.c_int * len(devices))(*devices)
         check(lib.tkv_crc32_batch_host_multi(devs, len(devices), ctypes.c_void_p(buf.ctypes.data),
                                              ctypes.c_void_p(off.ctypes.data), ctypes.c_void_p(ln.ctypes.data),

@@ -106,21 +106,22 @@ __device__ __forceinline__ std::uint32_t wave_xor_to_lane63(std::uint32_t v) {
 }
 
 // a*b mod P in the reflected representation (x^0 = 0x80000000).
-__device__ __forceinline__ std::uint32_t multmodp(std::uint32_t a, std::uint32_t b) {
+__device__ __forceinline__ std::uint32_t multmodp(std::uint32_t a, std::uint32_t b, std::uint32_t poly) {
   std::uint32_t p = 0;
   for (int i = 31; i >= 0; --i) {
     if (a & (1u << i)) p ^= b;
-    b = (b & 1u) ? (b >> 1) ^ kPoly : (b >> 1);
+    b = (b & 1u) ? (b >> 1) ^ poly : (b >> 1);
   }
   return p;
 }
 
 // reg * x^(8*kRow*k) mod P.
 __device__ __forceinline__ std::uint32_t shift_rows(const DeviceTables* t, std::uint32_t reg, std::uint32_t k) {
+  const std::uint32_t poly = t->poly;
   std::uint32_t m = 0x80000000u;  // x^0
   for (int i = 0; k != 0; ++i, k >>= 1)
-    if (k & 1u) m = multmodp(m, t->row_pow[i]);
-  return multmodp(m, reg);
+    if (k & 1u) m = multmodp(m, t->row_pow[i], poly);
+  return multmodp(m, reg, poly);
 }
 
 struct Cursor {
@@ -331,7 +332,7 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
   const LaneConst kc = lane_const(lane);
   std::uint32_t hcon = a.tabs->horner[lane];
   if constexpr (UNIFORM) {
-    if (lane >= 32u) hcon = multmodp(a.head_z, 1u << (lane - 32u));  // Shift_h(1 << (l-32))
+    if (lane >= 32u) hcon = multmodp(a.head_z, 1u << (lane - 32u), a.tabs->poly);  // Shift_h(1 << (l-32))
   }
   __syncthreads();
 

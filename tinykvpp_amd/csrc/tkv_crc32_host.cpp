@@ -16,6 +16,7 @@
 
 #include "tkv_crc32.h"
 #include "tkv_crc32_internal.h"
+#include "tkv_engine.h"
 
 namespace tkv {
 
@@ -32,58 +33,65 @@ hipError_t launch_fill_blocks(std::uint8_t* base, const std::uint64_t* offsets, 
                               std::uint64_t first, std::uint64_t nblocks, std::uint64_t seed, hipStream_t st);
 
 // ---- GF(2) arithmetic in the reflected representation (x^0 = 0x80000000) -------------------------
-std::uint32_t multmodp(std::uint32_t a, std::uint32_t b) {
+std::uint32_t multmodp(std::uint32_t a, std::uint32_t b, std::uint32_t poly) {
   std::uint32_t p = 0;
   for (int i = 31; i >= 0; --i) {
     if (a & (1u << i)) p ^= b;
-    b = (b & 1u) ? (b >> 1) ^ kPoly : (b >> 1);
+    b = (b & 1u) ? (b >> 1) ^ poly : (b >> 1);
   }
   return p;
 }
 
-std::uint32_t x8nmodp(std::uint64_t nbytes) {
+std::uint32_t x8nmodp(std::uint64_t nbytes, std::uint32_t poly) {
   // x^(8n) = product over set bits k of n of x^(8*2^k); x^(8*2^k) by repeated squaring of x^8.
   std::uint32_t result = 0x80000000u;  // x^0
   std::uint32_t sq = 0x00800000u;      // x^8
   while (nbytes) {
-    if (nbytes & 1u) result = multmodp(result, sq);
-    sq = multmodp(sq, sq);
+    if (nbytes & 1u) result = multmodp(result, sq, poly);
+    sq = multmodp(sq, sq, poly);
     nbytes >>= 1;
   }
   return result;
 }
 
-std::uint32_t shift_bytes(std::uint32_t reg, std::uint64_t nbytes) { return multmodp(x8nmodp(nbytes), reg); }
+std::uint32_t shift_bytes(std::uint32_t reg, std::uint64_t nbytes, std::uint32_t poly) {
+  return multmodp(x8nmodp(nbytes, poly), reg, poly);
+}
 
-void build_tables(DeviceTables* t) {
-  // T0: the Sarwate table of crc32.hpp:16-30; Tk[i] = T0[T(k-1)[i] & 0xFF] ^ (T(k-1)[i] >> 8).
+void build_tables(DeviceTables* t, std::uint32_t poly) {
+  // T0: the Sarwate table of crc32.hpp:16-30 (for poly = kPoly);
+  // Tk[i] = T0[T(k-1)[i] & 0xFF] ^ (T(k-1)[i] >> 8).
+  const auto mm = [poly](std::uint32_t a, std::uint32_t b) { return multmodp(a, b, poly); };
+  const auto x8n = [poly](std::uint64_t n) { return x8nmodp(n, poly); };
+  t->poly = poly;
+  t->pad_[0] = t->pad_[1] = t->pad_[2] = 0;
   for (std::uint32_t i = 0; i < 256; ++i) {
     std::uint32_t c = i;
-    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? kPoly : 0u);
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? poly : 0u);
     t->slice[0][i] = c;
   }
   for (int k = 1; k < 4; ++k)
     for (std::uint32_t i = 0; i < 256; ++i)
       t->slice[k][i] = t->slice[0][t->slice[k - 1][i] & 0xFFu] ^ (t->slice[k - 1][i] >> 8);
   for (int l = 0; l < 64; ++l) {
-    const std::uint32_t m = x8nmodp(static_cast<std::uint64_t>(63 - l) * kSeg);
+    const std::uint32_t m = x8n(static_cast<std::uint64_t>(63 - l) * kSeg);
     for (int j = 0; j < 8; ++j)
-      for (std::uint32_t v = 0; v < 16; ++v) t->lane_shift[j][v][l] = multmodp(m, v << (4 * j));
+      for (std::uint32_t v = 0; v < 16; ++v) t->lane_shift[j][v][l] = mm(m, v << (4 * j));
   }
-  const std::uint32_t mrow = x8nmodp(kRow);
-  for (int l = 0; l < 64; ++l) t->horner[l] = l < 32 ? multmodp(mrow, 1u << l) : 0u;
+  const std::uint32_t mrow = x8n(kRow);
+  for (int l = 0; l < 64; ++l) t->horner[l] = l < 32 ? mm(mrow, 1u << l) : 0u;
   std::uint32_t p = mrow;
   for (int k = 0; k < 64; ++k) {
     t->row_pow[k] = p;
-    p = multmodp(p, p);
+    p = mm(p, p);
   }
-  const std::uint32_t z32 = x8nmodp(32);
+  const std::uint32_t z32 = x8n(32);
   for (int j = 0; j < 8; ++j)
-    for (std::uint32_t v = 0; v < 16; ++v) t->shift32[j][v] = multmodp(z32, v << (4 * j));
+    for (std::uint32_t v = 0; v < 16; ++v) t->shift32[j][v] = mm(z32, v << (4 * j));
   std::uint32_t z = 0x80000000u;  // x^(8h), h = 0..kRow
   for (int h = 0; h <= kRow; ++h) {
-    for (int i = 0; i < 32; ++i) t->head_shift[h][i] = multmodp(z, 1u << i);
-    z = multmodp(z, 0x00800000u);
+    for (int i = 0; i < 32; ++i) t->head_shift[h][i] = mm(z, 1u << i);
+    z = mm(z, 0x00800000u);
   }
 }
 
@@ -116,163 +124,8 @@ struct StreamScratch {
   std::uint64_t cap_blocks = 0;
 };
 
-struct DevCtx {
-  int dev = -1;
-  int ncu = 0;
-  std::uint32_t W = 0;  // waves of a full launch (one 16-wave workgroup per CU)
-  DeviceTables* d_tabs = nullptr;
-  std::uint8_t* d_dummy = nullptr;
-  std::mutex mu;
-  std::map<void*, std::unique_ptr<StreamScratch>> scratch;
-  // synchronous update() staging (guarded by upd_mu)
-  std::mutex upd_mu;
-  hipStream_t st = nullptr;
-  std::uint8_t* h_stage = nullptr;
-  std::uint8_t* d_stage = nullptr;
-  std::uint32_t* d_io = nullptr;
-  std::uint32_t* h_io = nullptr;
-  std::size_t stage_cap = 0;
-};
-
-std::mutex g_mu;
-DevCtx* g_ctx[64] = {};
-
-int get_ctx(DevCtx** out) {
-  int dev = 0;
-  TKV_HIP(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64) return fail(TKV_INVALID_ARGUMENT, "device index out of range");
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_ctx[dev]) {
-    auto* c = new DevCtx();
-    c->dev = dev;
-    hipDeviceProp_t prop;
-    TKV_HIP(hipGetDeviceProperties(&prop, dev));
-    c->ncu = prop.multiProcessorCount;
-    c->W = static_cast<std::uint32_t>(c->ncu) * kWavesPerWG;
-    std::unique_ptr<DeviceTables> h(new DeviceTables);
-    build_tables(h.get());
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&c->d_tabs), sizeof(DeviceTables)));
-    TKV_HIP(hipMemcpy(c->d_tabs, h.get(), sizeof(DeviceTables), hipMemcpyHostToDevice));
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&c->d_dummy), 256));
-    TKV_HIP(hipMemset(c->d_dummy, 0, 256));
-    g_ctx[dev] = c;
-  }
-  *out = g_ctx[dev];
-  return TKV_OK;
-}
-
-int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** out) {
-  std::lock_guard<std::mutex> lk(c->mu);
-  auto& slot = c->scratch[stream];
-  if (!slot) {
-    slot.reset(new StreamScratch());
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->seams), sizeof(Seam) * 2 * c->W));
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->wave_start), sizeof(std::uint32_t) * c->W));
-  }
-  StreamScratch* s = slot.get();
-  if (nblocks > s->cap_blocks) {
-    std::uint64_t cap = std::max<std::uint64_t>(nblocks, 2 * s->cap_blocks);
-    if (s->row_scan) {
-      // Freed blocks may still be in use by earlier work on this stream.
-      TKV_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-      TKV_HIP(hipFree(s->row_scan));
-      TKV_HIP(hipFree(s->tiles));
-    }
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&s->row_scan), sizeof(std::uint32_t) * (cap + 1)));
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&s->tiles),
-                      sizeof(std::uint32_t) * (prepass_tiles(static_cast<std::uint32_t>(cap)) + 1)));
-    s->cap_blocks = cap;
-  }
-  *out = s;
-  return TKV_OK;
-}
-
-bool ptr_ok(const void* p) { return p != nullptr; }
-
-RowsArgs base_args(DevCtx* c, StreamScratch* s) {
-  RowsArgs a{};
-  a.tabs = c->d_tabs;
-  a.dummy = c->d_dummy;
-  a.seams = s->seams;
-  a.init_default = kInit;
-  a.out_xor = kInit;
-  a.nwaves = c->W;
-  return a;
-}
-
-// Uniform-length batch (also used for single spans).
-int run_uniform(DevCtx* c, const std::uint8_t* d_base, std::uint64_t stride, std::uint64_t len,
-                const std::uint32_t* d_init, std::uint32_t init_default, std::uint32_t out_xor, std::uint32_t* d_out,
-                std::uint64_t n, hipStream_t st) {
-  if (n == 0) return TKV_OK;
-  if (len > 0xFFFFFFFFull || n > 0xFFFFFFFFull) return fail(TKV_INVALID_ARGUMENT, "block length or count >= 2^32");
-  const std::uint64_t R = rows_for_len(static_cast<std::uint32_t>(len));
-  if (n * R > 0xFFFFFFFFull) return fail(TKV_INVALID_ARGUMENT, "batch larger than 2^32 rows (16 TiB)");
-  StreamScratch* s = nullptr;
-  if (int rc = get_scratch(c, st, 0, &s)) return rc;
-  RowsArgs a = base_args(c, s);
-  a.base = d_base;
-  a.stride = stride;
-  a.len = static_cast<std::uint32_t>(len);
-  a.head_z = x8nmodp(head_len(a.len));
-  a.init_raw = d_init;
-  a.init_default = init_default;
-  a.out_xor = out_xor;
-  a.out = d_out;
-  a.nblocks = static_cast<std::uint32_t>(n);
-  a.total_rows = static_cast<std::uint32_t>(n * R);
-  const bool aligned = (reinterpret_cast<std::uintptr_t>(d_base) % 16 == 0) && (stride % 16 == 0) && (len % 16 == 0);
-  const std::uint64_t packed_waves = static_cast<std::uint64_t>(c->ncu) * kWavesPerWG;
-  if (aligned && n >= packed_waves && len != 0 && len % kRow == 0 && stride == len) {
-    a.nwaves = static_cast<std::uint32_t>(packed_waves);
-    a.snap_blocks = 1;
-    TKV_HIP(launch_packed(a, static_cast<unsigned>(c->ncu), st));  // whole blocks per wave, no seams
-    return TKV_OK;
-  }
-  // Launch only as many workgroups as there are rows to give them (small batches).
-  std::uint64_t grid = std::min<std::uint64_t>(c->ncu, (a.total_rows + kRowsWavesPerWG - 1) / kRowsWavesPerWG);
-  if (grid == 0) grid = 1;
-  a.nwaves = static_cast<std::uint32_t>(grid * kRowsWavesPerWG);
-  a.snap_blocks = n >= a.nwaves ? 1u : 0u;
-  TKV_HIP(launch_rows(a, aligned, true, static_cast<unsigned>(grid), st));
-  if (!a.snap_blocks) TKV_HIP(launch_fixup(a, st));
-  return TKV_OK;
-}
-
-int run_irregular(DevCtx* c, const std::uint8_t* d_base, const std::uint64_t* d_off, const std::uint32_t* d_len,
-                  const std::uint32_t* d_init, std::uint32_t* d_out, std::uint64_t n, hipStream_t st) {
-  if (n == 0) return TKV_OK;
-  if (n >= 0xFFFFFFFFull) return fail(TKV_INVALID_ARGUMENT, "batch of 2^32 or more blocks");
-  StreamScratch* s = nullptr;
-  if (int rc = get_scratch(c, st, n, &s)) return rc;
-  RowsArgs a = base_args(c, s);
-  a.base = d_base;
-  a.offsets = d_off;
-  a.lengths = d_len;
-  a.row_scan = s->row_scan;
-  a.wave_start = s->wave_start;
-  a.init_raw = d_init;
-  a.out = d_out;
-  a.nblocks = static_cast<std::uint32_t>(n);
-  a.nwaves = static_cast<std::uint32_t>(c->ncu) * kRowsWavesPerWG;
-  TKV_HIP(launch_prepass(d_len, a.nblocks, s->row_scan, s->tiles, s->wave_start, a.nwaves, st));
-  TKV_HIP(launch_rows(a, false, false, static_cast<unsigned>(c->ncu), st));
-  TKV_HIP(launch_fixup(a, st));
-  return TKV_OK;
-}
-
-bool is_pinned_or_device(const void* p) {
-  hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return attr.type == hipMemoryTypeHost || attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
-}
-
-// ---- host-memory pipeline ---------------------------------------------------------------------------
+// Pinned staging of the host-memory pipeline: two slabs, two streams (one per slab).
 constexpr std::size_t kSlab = std::size_t(256) << 20;  // bytes of block data per pipeline stage
-
 struct HostPipe {
   hipStream_t st[2] = {nullptr, nullptr};
   hipEvent_t done[2] = {nullptr, nullptr};
@@ -325,6 +178,167 @@ int pipe_init(HostPipe& p, std::size_t max_blocks) {
   return TKV_OK;
 }
 
+struct DevCtx {
+  int dev = -1;
+  int ncu = 0;
+  std::uint32_t W = 0;  // waves of a full launch (one 16-wave workgroup per CU)
+  DeviceTables* d_tabs[kNumAlgos] = {};  // per checksum family (Algo)
+  std::uint8_t* d_dummy = nullptr;
+  std::mutex mu;
+  std::map<void*, std::unique_ptr<StreamScratch>> scratch;
+  // synchronous update() staging (guarded by upd_mu)
+  std::mutex upd_mu;
+  hipStream_t st = nullptr;
+  std::uint8_t* h_stage = nullptr;
+  std::uint8_t* d_stage = nullptr;
+  std::uint32_t* d_io = nullptr;
+  std::uint32_t* h_io = nullptr;
+  std::size_t stage_cap = 0;
+  // host-memory batch pipeline, kept between calls (guarded by pipe_mu)
+  std::mutex pipe_mu;
+  std::unique_ptr<HostPipe> pipe;
+};
+
+std::mutex g_mu;
+DevCtx* g_ctx[64] = {};
+
+int get_ctx(DevCtx** out) {
+  int dev = 0;
+  TKV_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return fail(TKV_INVALID_ARGUMENT, "device index out of range");
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_ctx[dev]) {
+    auto* c = new DevCtx();
+    c->dev = dev;
+    hipDeviceProp_t prop;
+    TKV_HIP(hipGetDeviceProperties(&prop, dev));
+    c->ncu = prop.multiProcessorCount;
+    c->W = static_cast<std::uint32_t>(c->ncu) * kWavesPerWG;
+    std::unique_ptr<DeviceTables> h(new DeviceTables);
+    for (int algo = 0; algo < kNumAlgos; ++algo) {
+      build_tables(h.get(), algo_poly(algo));
+      TKV_HIP(hipMalloc(reinterpret_cast<void**>(&c->d_tabs[algo]), sizeof(DeviceTables)));
+      TKV_HIP(hipMemcpy(c->d_tabs[algo], h.get(), sizeof(DeviceTables), hipMemcpyHostToDevice));
+    }
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&c->d_dummy), 256));
+    TKV_HIP(hipMemset(c->d_dummy, 0, 256));
+    g_ctx[dev] = c;
+  }
+  *out = g_ctx[dev];
+  return TKV_OK;
+}
+
+int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** out) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  auto& slot = c->scratch[stream];
+  if (!slot) {
+    slot.reset(new StreamScratch());
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->seams), sizeof(Seam) * 2 * c->W));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->wave_start), sizeof(std::uint32_t) * c->W));
+  }
+  StreamScratch* s = slot.get();
+  if (nblocks > s->cap_blocks) {
+    std::uint64_t cap = std::max<std::uint64_t>(nblocks, 2 * s->cap_blocks);
+    if (s->row_scan) {
+      // Freed blocks may still be in use by earlier work on this stream.
+      TKV_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+      TKV_HIP(hipFree(s->row_scan));
+      TKV_HIP(hipFree(s->tiles));
+    }
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&s->row_scan), sizeof(std::uint32_t) * (cap + 1)));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&s->tiles),
+                      sizeof(std::uint32_t) * (prepass_tiles(static_cast<std::uint32_t>(cap)) + 1)));
+    s->cap_blocks = cap;
+  }
+  *out = s;
+  return TKV_OK;
+}
+
+bool ptr_ok(const void* p) { return p != nullptr; }
+
+RowsArgs base_args(DevCtx* c, StreamScratch* s, int algo) {
+  RowsArgs a{};
+  a.tabs = c->d_tabs[algo];
+  a.dummy = c->d_dummy;
+  a.seams = s->seams;
+  a.init_default = kInit;
+  a.out_xor = kInit;
+  a.nwaves = c->W;
+  return a;
+}
+
+// Uniform-length batch (also used for single spans).
+int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t stride, std::uint64_t len,
+                const std::uint32_t* d_init, std::uint32_t init_default, std::uint32_t out_xor, std::uint32_t* d_out,
+                std::uint64_t n, hipStream_t st) {
+  if (n == 0) return TKV_OK;
+  if (len > 0xFFFFFFFFull || n > 0xFFFFFFFFull) return fail(TKV_INVALID_ARGUMENT, "block length or count >= 2^32");
+  const std::uint64_t R = rows_for_len(static_cast<std::uint32_t>(len));
+  if (n * R > 0xFFFFFFFFull) return fail(TKV_INVALID_ARGUMENT, "batch larger than 2^32 rows (16 TiB)");
+  StreamScratch* s = nullptr;
+  if (int rc = get_scratch(c, st, 0, &s)) return rc;
+  RowsArgs a = base_args(c, s, algo);
+  a.base = d_base;
+  a.stride = stride;
+  a.len = static_cast<std::uint32_t>(len);
+  a.head_z = x8nmodp(head_len(a.len), algo_poly(algo));
+  a.init_raw = d_init;
+  a.init_default = init_default;
+  a.out_xor = out_xor;
+  a.out = d_out;
+  a.nblocks = static_cast<std::uint32_t>(n);
+  a.total_rows = static_cast<std::uint32_t>(n * R);
+  const bool aligned = (reinterpret_cast<std::uintptr_t>(d_base) % 16 == 0) && (stride % 16 == 0) && (len % 16 == 0);
+  const std::uint64_t packed_waves = static_cast<std::uint64_t>(c->ncu) * kWavesPerWG;
+  if (aligned && n >= packed_waves && len != 0 && len % kRow == 0 && stride == len) {
+    a.nwaves = static_cast<std::uint32_t>(packed_waves);
+    a.snap_blocks = 1;
+    TKV_HIP(launch_packed(a, static_cast<unsigned>(c->ncu), st));  // whole blocks per wave, no seams
+    return TKV_OK;
+  }
+  // Launch only as many workgroups as there are rows to give them (small batches).
+  std::uint64_t grid = std::min<std::uint64_t>(c->ncu, (a.total_rows + kRowsWavesPerWG - 1) / kRowsWavesPerWG);
+  if (grid == 0) grid = 1;
+  a.nwaves = static_cast<std::uint32_t>(grid * kRowsWavesPerWG);
+  a.snap_blocks = n >= a.nwaves ? 1u : 0u;
+  TKV_HIP(launch_rows(a, aligned, true, static_cast<unsigned>(grid), st));
+  if (!a.snap_blocks) TKV_HIP(launch_fixup(a, st));
+  return TKV_OK;
+}
+
+int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::uint64_t* d_off, const std::uint32_t* d_len,
+                  const std::uint32_t* d_init, std::uint32_t* d_out, std::uint64_t n, hipStream_t st) {
+  if (n == 0) return TKV_OK;
+  if (n >= 0xFFFFFFFFull) return fail(TKV_INVALID_ARGUMENT, "batch of 2^32 or more blocks");
+  StreamScratch* s = nullptr;
+  if (int rc = get_scratch(c, st, n, &s)) return rc;
+  RowsArgs a = base_args(c, s, algo);
+  a.base = d_base;
+  a.offsets = d_off;
+  a.lengths = d_len;
+  a.row_scan = s->row_scan;
+  a.wave_start = s->wave_start;
+  a.init_raw = d_init;
+  a.out = d_out;
+  a.nblocks = static_cast<std::uint32_t>(n);
+  a.nwaves = static_cast<std::uint32_t>(c->ncu) * kRowsWavesPerWG;
+  TKV_HIP(launch_prepass(d_len, a.nblocks, s->row_scan, s->tiles, s->wave_start, a.nwaves, st));
+  TKV_HIP(launch_rows(a, false, false, static_cast<unsigned>(c->ncu), st));
+  TKV_HIP(launch_fixup(a, st));
+  return TKV_OK;
+}
+
+bool is_pinned_or_device(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost || attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+// ---- host-memory pipeline ---------------------------------------------------------------------------
+
 // Copy blocks [b0, b0+cnt) into dst at the slab offsets so_[i]; large slabs use several threads.
 void gather(std::uint8_t* dst, const std::uint8_t* src, const std::uint64_t* off, const std::uint32_t* len,
             std::uint64_t b0, std::size_t cnt, const std::uint64_t* so_) {
@@ -345,7 +359,7 @@ void gather(std::uint8_t* dst, const std::uint8_t* src, const std::uint64_t* off
 
 // Blocks in [lo, hi) of a host batch, processed slab by slab. Blocks larger than a slab are
 // chained through update_device in slab-sized pieces on stream 0.
-int host_batch(DevCtx* c, const std::uint8_t* h_base, const std::uint64_t* off, const std::uint32_t* len,
+int host_batch(DevCtx* c, int algo, const std::uint8_t* h_base, const std::uint64_t* off, const std::uint32_t* len,
                const std::uint32_t* init, std::uint32_t* out, std::uint64_t lo, std::uint64_t hi) {
   if (hi <= lo) return TKV_OK;
   // Largest number of blocks a slab can hold (all >= 1 byte... zero-length blocks count too).
@@ -363,8 +377,16 @@ int host_batch(DevCtx* c, const std::uint8_t* h_base, const std::uint64_t* off, 
       max_blocks = std::max(max_blocks, cnt);
     }
   }
-  HostPipe p;
-  if (int rc = pipe_init(p, max_blocks)) return rc;
+  std::lock_guard<std::mutex> plk(c->pipe_mu);
+  if (!c->pipe || c->pipe->cap_blocks < max_blocks) {
+    c->pipe.reset();  // the old pipe's streams are idle: every call retires its slabs before returning
+    c->pipe.reset(new HostPipe());
+    if (int rc = pipe_init(*c->pipe, max_blocks)) {
+      c->pipe.reset();
+      return rc;
+    }
+  }
+  HostPipe& p = *c->pipe;
   const bool src_pinned = is_pinned_or_device(h_base);
   struct Pending {
     std::uint64_t lo = 0, cnt = 0;
@@ -393,7 +415,7 @@ int host_batch(DevCtx* c, const std::uint8_t* h_base, const std::uint64_t* off, 
         p.h_init[0][0] = raw;
         TKV_HIP(hipMemcpyAsync(p.d_data[0], p.h_data[0], m, hipMemcpyHostToDevice, p.st[0]));
         TKV_HIP(hipMemcpyAsync(p.d_init[0], p.h_init[0], 4, hipMemcpyHostToDevice, p.st[0]));
-        if (int rc = run_uniform(c, p.d_data[0], m, m, p.d_init[0], kInit, 0u, p.d_out[0], 1, p.st[0])) return rc;
+        if (int rc = run_uniform(c, algo, p.d_data[0], m, m, p.d_init[0], kInit, 0u, p.d_out[0], 1, p.st[0])) return rc;
         TKV_HIP(hipMemcpyAsync(p.h_out[0], p.d_out[0], 4, hipMemcpyDeviceToHost, p.st[0]));
         TKV_HIP(hipStreamSynchronize(p.st[0]));
         raw = p.h_out[0][0];
@@ -432,12 +454,13 @@ int host_batch(DevCtx* c, const std::uint8_t* h_base, const std::uint64_t* off, 
     TKV_HIP(hipMemcpyAsync(p.d_init[k], p.h_init[k], cnt * 4, hipMemcpyHostToDevice, p.st[k]));
     if (uniform) {
       // equal lengths, packed back to back in the slab: the uniform (packed) kernels, no prepass
-      if (int rc = run_uniform(c, p.d_data[k], len[b0], len[b0], p.d_init[k], kInit, kInit, p.d_out[k], cnt, p.st[k]))
+      if (int rc = run_uniform(c, algo, p.d_data[k], len[b0], len[b0], p.d_init[k], kInit, kInit, p.d_out[k], cnt,
+                               p.st[k]))
         return rc;
     } else {
       TKV_HIP(hipMemcpyAsync(p.d_off[k], p.h_off[k], cnt * 8, hipMemcpyHostToDevice, p.st[k]));
       TKV_HIP(hipMemcpyAsync(p.d_len[k], p.h_len[k], cnt * 4, hipMemcpyHostToDevice, p.st[k]));
-      if (int rc = run_irregular(c, p.d_data[k], p.d_off[k], p.d_len[k], p.d_init[k], p.d_out[k], cnt, p.st[k]))
+      if (int rc = run_irregular(c, algo, p.d_data[k], p.d_off[k], p.d_len[k], p.d_init[k], p.d_out[k], cnt, p.st[k]))
         return rc;
     }
     TKV_HIP(hipMemcpyAsync(p.h_out[k], p.d_out[k], cnt * 4, hipMemcpyDeviceToHost, p.st[k]));
@@ -451,41 +474,19 @@ int host_batch(DevCtx* c, const std::uint8_t* h_base, const std::uint64_t* off, 
 }
 
 }  // namespace
-}  // namespace tkv
 
-using namespace tkv;
+// ---- entry points shared by the CRC-32 and CRC-32C C ABI ------------------------------------
 
-extern "C" {
-
-int tkv_device_count(void) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) {
-    (void)hipGetLastError();
-    return 0;
-  }
-  return n;
-}
-
-int tkv_set_device(int device) {
-  int n = tkv_device_count();
-  if (device < 0 || device >= n) return fail(TKV_INVALID_ARGUMENT, "no such device");
-  TKV_HIP(hipSetDevice(device));
-  DevCtx* c = nullptr;
-  return get_ctx(&c);
-}
-
-const char* tkv_last_error(void) { return g_err.c_str(); }
-
-int tkv_crc32_update_device(uint32_t raw_state, const void* d_data, size_t len, uint32_t* d_out_raw, void* stream) {
+int update_device_impl(int algo, uint32_t raw_state, const void* d_data, size_t len, uint32_t* d_out_raw, void* stream) {
   if (!ptr_ok(d_out_raw) || (len && !ptr_ok(d_data))) return fail(TKV_INVALID_ARGUMENT, "null pointer");
   DevCtx* c = nullptr;
   if (int rc = get_ctx(&c)) return rc;
   // One block of `len` bytes continued from raw_state; raw register out (no xorout).
   const auto* base = static_cast<const std::uint8_t*>(d_data ? d_data : c->d_dummy);
-  return run_uniform(c, base, len, len, nullptr, raw_state, 0u, d_out_raw, 1, static_cast<hipStream_t>(stream));
+  return run_uniform(c, algo, base, len, len, nullptr, raw_state, 0u, d_out_raw, 1, static_cast<hipStream_t>(stream));
 }
 
-int tkv_crc32_update(uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
+int update_impl(int algo, uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
   if (!ptr_ok(out_raw) || (len && !ptr_ok(data))) return fail(TKV_INVALID_ARGUMENT, "null pointer");
   DevCtx* c = nullptr;
   if (int rc = get_ctx(&c)) return rc;
@@ -515,7 +516,7 @@ int tkv_crc32_update(uint32_t raw_state, const void* data, size_t len, uint32_t*
       std::memcpy(c->h_stage, src, m);
       TKV_HIP(hipMemcpyAsync(c->d_stage, c->h_stage, m, hipMemcpyHostToDevice, c->st));
     }
-    if (int rc = run_uniform(c, c->d_stage, m, m, nullptr, raw, 0u, c->d_io, 1, c->st)) return rc;
+    if (int rc = run_uniform(c, algo, c->d_stage, m, m, nullptr, raw, 0u, c->d_io, 1, c->st)) return rc;
     TKV_HIP(hipMemcpyAsync(c->h_io, c->d_io, 4, hipMemcpyDeviceToHost, c->st));
     TKV_HIP(hipStreamSynchronize(c->st));
     raw = c->h_io[0];
@@ -526,39 +527,38 @@ int tkv_crc32_update(uint32_t raw_state, const void* data, size_t len, uint32_t*
   return TKV_OK;
 }
 
-int tkv_crc32_batch_device(const uint8_t* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
-                           const uint32_t* d_init_raw, uint32_t* d_out_final, uint64_t n, void* stream) {
+int batch_device_impl(int algo, const uint8_t* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
+                      const uint32_t* d_init_raw, uint32_t* d_out_final, uint64_t n, void* stream) {
   if (n == 0) return TKV_OK;
   if (!ptr_ok(d_base) || !ptr_ok(d_offsets) || !ptr_ok(d_lengths) || !ptr_ok(d_out_final))
     return fail(TKV_INVALID_ARGUMENT, "null pointer");
   DevCtx* c = nullptr;
   if (int rc = get_ctx(&c)) return rc;
-  return run_irregular(c, d_base, d_offsets, d_lengths, d_init_raw, d_out_final, n, static_cast<hipStream_t>(stream));
+  return run_irregular(c, algo, d_base, d_offsets, d_lengths, d_init_raw, d_out_final, n, static_cast<hipStream_t>(stream));
 }
 
-int tkv_crc32_batch_uniform_device(const uint8_t* d_base, uint64_t stride, uint64_t len, const uint32_t* d_init_raw,
-                                   uint32_t* d_out_final, uint64_t n, void* stream) {
+int batch_uniform_impl(int algo, const uint8_t* d_base, uint64_t stride, uint64_t len, const uint32_t* d_init_raw,
+                       uint32_t* d_out_final, uint64_t n, void* stream) {
   if (n == 0) return TKV_OK;
   if ((len && !ptr_ok(d_base)) || !ptr_ok(d_out_final)) return fail(TKV_INVALID_ARGUMENT, "null pointer");
   DevCtx* c = nullptr;
   if (int rc = get_ctx(&c)) return rc;
   const auto* base = d_base ? d_base : c->d_dummy;
-  return run_uniform(c, base, stride, len, d_init_raw, kInit, kInit, d_out_final, n, static_cast<hipStream_t>(stream));
+  return run_uniform(c, algo, base, stride, len, d_init_raw, kInit, kInit, d_out_final, n, static_cast<hipStream_t>(stream));
 }
 
-int tkv_crc32_batch_host(const uint8_t* h_base, const uint64_t* h_offsets, const uint32_t* h_lengths,
-                         const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
+int batch_host_impl(int algo, const uint8_t* h_base, const uint64_t* h_offsets, const uint32_t* h_lengths,
+                    const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
   if (n == 0) return TKV_OK;
   if (!ptr_ok(h_base) || !ptr_ok(h_offsets) || !ptr_ok(h_lengths) || !ptr_ok(h_out_final))
     return fail(TKV_INVALID_ARGUMENT, "null pointer");
   DevCtx* c = nullptr;
   if (int rc = get_ctx(&c)) return rc;
-  return host_batch(c, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, 0, n);
+  return host_batch(c, algo, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, 0, n);
 }
 
-int tkv_crc32_batch_host_multi(const int* devices, int ndev, const uint8_t* h_base, const uint64_t* h_offsets,
-                               const uint32_t* h_lengths, const uint32_t* h_init_raw, uint32_t* h_out_final,
-                               uint64_t n) {
+int batch_host_multi_impl(int algo, const int* devices, int ndev, const uint8_t* h_base, const uint64_t* h_offsets,
+                          const uint32_t* h_lengths, const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
   if (ndev <= 0 || !ptr_ok(devices)) return fail(TKV_INVALID_ARGUMENT, "no devices");
   if (n == 0) return TKV_OK;
   if (!ptr_ok(h_base) || !ptr_ok(h_offsets) || !ptr_ok(h_lengths) || !ptr_ok(h_out_final))
@@ -588,7 +588,7 @@ int tkv_crc32_batch_host_multi(const int* devices, int ndev, const uint8_t* h_ba
       }
       DevCtx* c = nullptr;
       rcs[d] = get_ctx(&c);
-      if (rcs[d] == TKV_OK) rcs[d] = host_batch(c, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, cut[d], cut[d + 1]);
+      if (rcs[d] == TKV_OK) rcs[d] = host_batch(c, algo, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, cut[d], cut[d + 1]);
       errs[d] = g_err;
     });
   }
@@ -598,67 +598,80 @@ int tkv_crc32_batch_host_multi(const int* devices, int ndev, const uint8_t* h_ba
   return TKV_OK;
 }
 
-int tkv_wal_verify(const uint8_t* h_wal, uint64_t size, uint64_t* n_good, uint64_t* stop_offset) {
-  if ((size && !ptr_ok(h_wal)) || !ptr_ok(n_good) || !ptr_ok(stop_offset))
-    return fail(TKV_INVALID_ARGUMENT, "null pointer");
-  // Walk the record_len chain (wal.cpp:63-87): each record is [u32 record_len][u32 crc][payload].
-  constexpr std::uint64_t kMeta = 26;  // wal.hpp:21-27 kMetadataSize
-  std::vector<std::uint64_t> off;
-  std::vector<std::uint32_t> len, stored;
-  std::uint64_t pos = 0;
-  bool structural_error = false;
-  while (pos < size) {
-    const std::uint64_t left = size - pos;
-    if (left < kMeta) {
-      structural_error = true;  // wal.cpp:68-70
-      break;
-    }
-    std::uint32_t rlen, crc;
-    std::memcpy(&rlen, h_wal + pos, 4);
-    std::memcpy(&crc, h_wal + pos + 4, 4);
-    if (static_cast<std::uint64_t>(rlen) + 8 > left) {
-      structural_error = true;  // wal.cpp:82-87
-      break;
-    }
-    off.push_back(pos + 8);
-    len.push_back(rlen);
-    stored.push_back(crc);
-    pos += 8 + static_cast<std::uint64_t>(rlen);
-  }
-  std::vector<std::uint32_t> got(off.size());
-  if (!off.empty()) {
-    if (int rc = tkv_crc32_batch_host(h_wal, off.data(), len.data(), nullptr, got.data(), off.size())) return rc;
-  }
-  std::uint64_t good = 0, stop = 0;
-  for (; good < off.size(); ++good) {
-    if (got[good] != stored[good]) break;  // wal.cpp:93-96
-    // key/value bounds inside the payload (wal.cpp:118-121)
-    const std::uint8_t* rec = h_wal + off[good] - 8;
-    std::uint32_t klen, vlen;
-    std::memcpy(&klen, rec + 18, 4);
-    std::memcpy(&vlen, rec + 22, 4);
-    if (kMeta + static_cast<std::uint64_t>(klen) + vlen > 8 + static_cast<std::uint64_t>(len[good])) break;
-  }
-  stop = good < off.size() ? off[good] - 8 : pos;
-  *n_good = good;
-  *stop_offset = stop;
-  if (good < off.size() || structural_error) return fail(TKV_CORRUPTED, "corrupted WAL record");
-  return TKV_OK;
+int set_error(int code, const char* msg) { return fail(code, msg); }
+
+const DeviceTables* device_tables(int algo) {
+  DevCtx* c = nullptr;
+  if (get_ctx(&c)) return nullptr;
+  return c->d_tabs[algo];
 }
 
-int tkv_wal_stamp(uint8_t* h_buf, const uint64_t* h_offsets, const uint32_t* h_sizes, uint64_t n) {
-  if (n == 0) return TKV_OK;
-  if (!ptr_ok(h_buf) || !ptr_ok(h_offsets) || !ptr_ok(h_sizes)) return fail(TKV_INVALID_ARGUMENT, "null pointer");
-  std::vector<std::uint64_t> off(n);
-  std::vector<std::uint32_t> len(n), crc(n);
-  for (std::uint64_t i = 0; i < n; ++i) {
-    if (h_sizes[i] < 8) return fail(TKV_INVALID_ARGUMENT, "WAL record shorter than its 8-byte prefix");
-    off[i] = h_offsets[i] + 8;  // wal.cpp:54-57: CRC over [8, size)
-    len[i] = h_sizes[i] - 8;
+}  // namespace tkv
+
+using namespace tkv;
+
+extern "C" {
+
+int tkv_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
   }
-  if (int rc = tkv_crc32_batch_host(h_buf, off.data(), len.data(), nullptr, crc.data(), n)) return rc;
-  for (std::uint64_t i = 0; i < n; ++i) std::memcpy(h_buf + h_offsets[i] + 4, &crc[i], 4);  // wal.cpp:58
-  return TKV_OK;
+  return n;
+}
+
+int tkv_set_device(int device) {
+  int n = tkv_device_count();
+  if (device < 0 || device >= n) return fail(TKV_INVALID_ARGUMENT, "no such device");
+  TKV_HIP(hipSetDevice(device));
+  DevCtx* c = nullptr;
+  return get_ctx(&c);
+}
+
+const char* tkv_last_error(void) { return g_err.c_str(); }
+
+int tkv_crc32_update_device(uint32_t raw_state, const void* d_data, size_t len, uint32_t* d_out_raw, void* stream) {
+  return update_device_impl(kAlgoCrc32, raw_state, d_data, len, d_out_raw, stream);
+}
+int tkv_crc32_update(uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
+  return update_impl(kAlgoCrc32, raw_state, data, len, out_raw);
+}
+int tkv_crc32_batch_device(const uint8_t* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
+                           const uint32_t* d_init_raw, uint32_t* d_out_final, uint64_t n, void* stream) {
+  return batch_device_impl(kAlgoCrc32, d_base, d_offsets, d_lengths, d_init_raw, d_out_final, n, stream);
+}
+int tkv_crc32_batch_uniform_device(const uint8_t* d_base, uint64_t stride, uint64_t len, const uint32_t* d_init_raw,
+                                   uint32_t* d_out_final, uint64_t n, void* stream) {
+  return batch_uniform_impl(kAlgoCrc32, d_base, stride, len, d_init_raw, d_out_final, n, stream);
+}
+int tkv_crc32_batch_host(const uint8_t* h_base, const uint64_t* h_offsets, const uint32_t* h_lengths,
+                         const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
+  return batch_host_impl(kAlgoCrc32, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, n);
+}
+int tkv_crc32_batch_host_multi(const int* devices, int ndev, const uint8_t* h_base, const uint64_t* h_offsets,
+                               const uint32_t* h_lengths, const uint32_t* h_init_raw, uint32_t* h_out_final,
+                               uint64_t n) {
+  return batch_host_multi_impl(kAlgoCrc32, devices, ndev, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, n);
+}
+
+int tkv_crc32c_update(uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
+  return update_impl(kAlgoCrc32c, raw_state, data, len, out_raw);
+}
+int tkv_crc32c_update_device(uint32_t raw_state, const void* d_data, size_t len, uint32_t* d_out_raw, void* stream) {
+  return update_device_impl(kAlgoCrc32c, raw_state, d_data, len, d_out_raw, stream);
+}
+int tkv_crc32c_batch_device(const uint8_t* d_base, const uint64_t* d_offsets, const uint32_t* d_lengths,
+                            const uint32_t* d_init_raw, uint32_t* d_out_final, uint64_t n, void* stream) {
+  return batch_device_impl(kAlgoCrc32c, d_base, d_offsets, d_lengths, d_init_raw, d_out_final, n, stream);
+}
+int tkv_crc32c_batch_uniform_device(const uint8_t* d_base, uint64_t stride, uint64_t len, const uint32_t* d_init_raw,
+                                    uint32_t* d_out_final, uint64_t n, void* stream) {
+  return batch_uniform_impl(kAlgoCrc32c, d_base, stride, len, d_init_raw, d_out_final, n, stream);
+}
+int tkv_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_offsets, const uint32_t* h_lengths,
+                          const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
+  return batch_host_impl(kAlgoCrc32c, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, n);
 }
 
 int tkv_fill_synthetic_uniform(uint8_t* d_dst, uint64_t stride, uint64_t len, uint64_t first_block, uint64_t nblocks,
@@ -679,8 +692,10 @@ int tkv_fill_synthetic_blocks(uint8_t* d_base, const uint64_t* d_offsets, const 
   return TKV_OK;
 }
 
-size_t tkv_debug_tables(void* out, size_t cap) {
-  if (out && cap >= sizeof(DeviceTables)) build_tables(static_cast<DeviceTables*>(out));
+size_t tkv_debug_tables(void* out, size_t cap) { return tkv_debug_tables_poly(kPoly, out, cap); }
+
+size_t tkv_debug_tables_poly(uint32_t poly, void* out, size_t cap) {
+  if (out && cap >= sizeof(DeviceTables)) build_tables(static_cast<DeviceTables*>(out), poly);
   return sizeof(DeviceTables);
 }
 

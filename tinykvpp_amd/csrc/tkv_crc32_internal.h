@@ -17,6 +17,12 @@ namespace tkv {
 // CRC-32/ISO-HDLC parameters of frankie::core::crc32 (/root/reference/src/core/crc32.hpp:9-11).
 constexpr std::uint32_t kPoly = 0xEDB88320u;  // reflected polynomial
 constexpr std::uint32_t kInit = 0xFFFFFFFFu;  // init and xorout
+// CRC-32C (Castagnoli, RFC 3720 §B.4): same reflection, init and xorout; SURVEY.md §8f rank 4.
+constexpr std::uint32_t kPolyC = 0x82F63B78u;
+
+// Checksum families the engine serves; each has its own DeviceTables on every device.
+enum Algo : int { kAlgoCrc32 = 0, kAlgoCrc32c = 1, kNumAlgos = 2 };
+constexpr std::uint32_t algo_poly(int algo) { return algo == kAlgoCrc32c ? kPolyC : kPoly; }
 
 // Work decomposition of the row kernel.
 constexpr int kSeg = 64;                 // contiguous bytes one lane folds per row
@@ -44,6 +50,8 @@ struct DeviceTables {
   std::uint32_t row_pow[64];            // x^(8*kRow*2^k) mod P (reflected), k = 0..63
   std::uint32_t head_shift[kRow + 1][32];  // [h][i] = Shift_h(1 << i): init injection at a head row
   std::uint32_t shift32[8][16];         // [j][v] = Shift_32(v << 4j): joins two 32-byte half chains
+  std::uint32_t poly;                   // reflected polynomial the tables were built for
+  std::uint32_t pad_[3];
 };
 
 // One partial result of a block that was split between waves (irregular / huge-block path).
@@ -89,9 +97,9 @@ TKV_HD inline std::uint32_t rows_for_len(std::uint32_t n) { return n == 0 ? 1u :
 TKV_HD inline std::uint32_t head_len(std::uint32_t n) { return n - (rows_for_len(n) - 1u) * kRow; }
 
 // Host-side math shared with tests (tkv_crc32_host.cpp).
-std::uint32_t multmodp(std::uint32_t a, std::uint32_t b);   // a*b mod P, reflected
-std::uint32_t x8nmodp(std::uint64_t nbytes);                // x^(8n) mod P, reflected
-std::uint32_t shift_bytes(std::uint32_t reg, std::uint64_t nbytes);
-void build_tables(DeviceTables* t);
+std::uint32_t multmodp(std::uint32_t a, std::uint32_t b, std::uint32_t poly = kPoly);  // a*b mod P
+std::uint32_t x8nmodp(std::uint64_t nbytes, std::uint32_t poly = kPoly);              // x^(8n) mod P
+std::uint32_t shift_bytes(std::uint32_t reg, std::uint64_t nbytes, std::uint32_t poly = kPoly);
+void build_tables(DeviceTables* t, std::uint32_t poly = kPoly);
 
 }  // namespace tkv

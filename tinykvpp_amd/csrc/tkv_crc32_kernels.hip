@@ -147,6 +147,32 @@ __global__ void fill_uniform(std::uint8_t* dst, std::uint64_t stride, std::uint6
   }
 }
 
+// SSTable stamp fix-up (tkv_sst_block_crcs_device): out[i] holds the CRC of image i as it lies, with
+// whatever its crc32_ field holds (bytes [17, 21)). By linearity, the CRC with those bytes read as
+// zero is out[i] ^ crc_0(E), E = the field bytes followed by size-21 zero bytes, and
+// crc_0(E) = Shift_{size-21}(crc_0(field)). One thread per image; store != 0 writes the result into
+// the field. Images shorter than kSstMinImage keep the CRC of the image as it lies.
+constexpr std::uint32_t kSstCrcOffset = 17, kSstMinImage = 22;
+__global__ void sst_fix(std::uint8_t* file, const std::uint64_t* offsets, const std::uint32_t* sizes,
+                        std::uint32_t* out, std::uint64_t n, int store, const DeviceTables* tabs) {
+  const std::uint64_t i = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+  if (i >= n) return;
+  const std::uint32_t size = sizes[i];
+  if (size < kSstMinImage) return;
+  std::uint8_t* f = file + offsets[i] + kSstCrcOffset;
+  std::uint32_t c = 0;  // crc_0 of the 4 field bytes (Sarwate steps, crc32.cpp:12-14 without init)
+  for (int k = 0; k < 4; ++k) c = (c >> 8) ^ tabs->slice[0][(c ^ f[k]) & 0xFFu];
+  const std::uint32_t z = size - (kSstCrcOffset + 4);  // zero bytes after the field
+  const std::uint32_t h = z % kRow;
+  std::uint32_t c2 = 0;
+  for (int b = 0; b < 32; ++b)
+    if (c >> b & 1u) c2 ^= tabs->head_shift[h][b];  // Shift_h(c)
+  const std::uint32_t v = out[i] ^ dev::shift_rows(tabs, c2, z / kRow);
+  out[i] = v;
+  if (store)
+    for (int k = 0; k < 4; ++k) f[k] = static_cast<std::uint8_t>(v >> (8 * k));
+}
+
 // Arbitrary blocks (offsets/lengths, any alignment): one workgroup per block, byte stores.
 __global__ void fill_blocks(std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
                             std::uint64_t first, std::uint64_t nblocks, std::uint64_t seed) {
@@ -197,6 +223,14 @@ hipError_t launch_prepass(const std::uint32_t* lengths, std::uint32_t n, std::ui
 }
 
 std::uint32_t prepass_tiles(std::uint32_t n) { return (n + kScanTile - 1) / kScanTile; }
+
+hipError_t launch_sst_fix(std::uint8_t* file, const std::uint64_t* offsets, const std::uint32_t* sizes,
+                          std::uint32_t* out, std::uint64_t n, int store, const DeviceTables* tabs, hipStream_t st) {
+  const std::uint64_t grid = (n + 255) / 256;
+  if (grid) hipLaunchKernelGGL(sst_fix, dim3(static_cast<unsigned>(grid)), dim3(256), 0, st, file, offsets, sizes, out,
+                               n, store, tabs);
+  return hipGetLastError();
+}
 
 hipError_t launch_fill_uniform(std::uint8_t* dst, std::uint64_t stride, std::uint64_t len, std::uint64_t first,
                                std::uint64_t nblocks, std::uint64_t seed, hipStream_t st) {

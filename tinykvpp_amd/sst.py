@@ -1,0 +1,93 @@
+"""SSTable data-block stamping and verification on the GPU CRC engine.
+
+The reference leaves the checksum fields dead: get_data_block writes
+``sstable_data_block_header::crc32_ = 0`` (/root/reference/src/storage/sstable_writer.cpp:138-144)
+and read_data_block never checks it (sstable_reader.cpp:61-89). The format here is this library's
+decision (include/tkv_crc32.h, "parity unpinned"): a data-block image, as get_data_block builds it
+(sstable_writer.cpp:150-168), is
+
+    varint(20) | header[20] | varint(n) | body[n] | padding up to 36 + n bytes
+
+with header = u32 entry_count | u32 uncompressed_size | u32 compressed_size | u8 compression |
+3 pad | u32 crc32_ (sstable_format.hpp:91-99), so crc32_ sits at image byte CRC_OFFSET = 17. The
+stamp is crc32 over the whole image with those 4 bytes read as zero, stored little-endian.
+"""
+import ctypes
+import struct
+
+import numpy as np
+
+from ._lib import CORRUPTED, OK, check, load_library
+
+CRC_OFFSET = 17   # 1-byte varint(20) + 16 header bytes before crc32_
+MIN_IMAGE = 22    # varint(20) + header + varint(0)
+
+
+def _varint(v):
+    """codec::encode_varint (core/serialization/codec.hpp:31-39): LEB128."""
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def encode_data_block_image(entries):
+    """Unstamped image of a data block holding ``entries`` [(ikey, value), ...], laid out as
+    sstable_writer::get_data_block does: the body is write_string(ikey) | write_string(value) per
+    entry (sstable_writer.cpp:113) and the block size counts 4 + |ikey| + 4 + |value| per entry
+    (:60,122); the reference leaves arena bytes in the slack past the written entries and in the
+    image padding, which are zero here."""
+    body = b"".join(_varint(len(k)) + k + _varint(len(v)) + v for k, v in entries)
+    size = sum(8 + len(k) + len(v) for k, v in entries)
+    body = body[:size].ljust(size, b"\0")
+    header = struct.pack("<IIIB3xI", len(entries), size, size, 0, 0)
+    image = _varint(len(header)) + header + _varint(size) + body
+    return image.ljust(8 + len(header) + 8 + size, b"\0")
+
+
+def _host_arrays(offsets, sizes):
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+    if off.size != sz.size:
+        raise ValueError("offsets and sizes differ in length")
+    return off, sz
+
+
+def stamp_blocks(file, offsets, sizes):
+    """Stamp images in place in a writable uint8 numpy buffer (the SSTable file being written)."""
+    if not isinstance(file, np.ndarray) or file.dtype != np.uint8 or not file.flags.writeable:
+        raise ValueError("file must be a writable uint8 numpy array")
+    off, sz = _host_arrays(offsets, sizes)
+    check(load_library().tkv_sst_stamp_blocks(ctypes.c_void_p(file.ctypes.data), ctypes.c_void_p(off.ctypes.data),
+                                              ctypes.c_void_p(sz.ctypes.data), off.size))
+
+
+def verify_blocks(file, offsets, sizes):
+    """Verify images of a host buffer. Returns (status, n_bad, first_bad); status "ok" or "corrupted"."""
+    buf = np.ascontiguousarray(np.frombuffer(file, np.uint8) if not isinstance(file, np.ndarray) else file)
+    off, sz = _host_arrays(offsets, sizes)
+    n_bad, first = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    rc = load_library().tkv_sst_verify_blocks(ctypes.c_void_p(buf.ctypes.data), ctypes.c_void_p(off.ctypes.data),
+                                              ctypes.c_void_p(sz.ctypes.data), off.size, ctypes.byref(n_bad),
+                                              ctypes.byref(first))
+    if rc not in (OK, CORRUPTED):
+        check(rc)
+    return ("ok" if rc == OK else "corrupted"), n_bad.value, first.value
+
+
+def block_crcs_device(file, offsets, sizes, store=False, out=None, stream=None):
+    """Device-resident images (torch uint8 CUDA tensor, int64 offsets, int32 sizes): the stamp value
+    of every image (its CRC with the field read as zero); store=True also writes it into the field."""
+    import torch
+    from .crc32 import _stream_ptr
+    for name, t, dt in (("offsets", offsets, torch.int64), ("sizes", sizes, torch.int32)):
+        if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous CUDA {dt} tensor")
+    if out is None:
+        out = torch.empty(offsets.numel(), dtype=torch.int32, device=file.device)
+    check(load_library().tkv_sst_block_crcs_device(
+        ctypes.c_void_p(file.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), ctypes.c_void_p(sizes.data_ptr()),
+        ctypes.c_void_p(out.data_ptr()), offsets.numel(), int(bool(store)), _stream_ptr(stream)))
+    return out

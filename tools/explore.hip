@@ -279,8 +279,6 @@ std::uint64_t g_cap = 0;
 }  // namespace
 
 namespace tkv {
-void build_tables(DeviceTables* t);
-std::uint32_t x8nmodp(std::uint64_t nbytes);
 hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
 hipError_t launch_prepass(const std::uint32_t* lengths, std::uint32_t n, std::uint32_t* row_scan,
                           std::uint32_t* tile_sums, std::uint32_t* wave_start, std::uint32_t W, hipStream_t st);
