@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Throughput of the SURVEY §8f rows on one MI355X (one JSON line each):
+
+  wal_stamp    group commit: tkv_wal_stamp over N encoded records in host memory (wal.cpp:54-58)
+  wal_verify   recovery: tkv_wal_verify over the slurped WAL image (wal.cpp:63-130, engine.cpp:31-53)
+  sst_stamp    tkv_sst_stamp_blocks over a host SSTable image of ~4 KiB data blocks
+  sst_device   tkv_sst_block_crcs_device over the same images resident in HBM (kernel + fix-up)
+  crc32c_cfg2  CRC-32C over 1 M x 4 KiB device-resident blocks (cfg2 shape)
+
+Host-memory rows include the PCIe copies (pageable source: host memcpy into pinned staging); the
+CPU column times the oracle's reference loop on a bounded sample of the same records, 1 thread.
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import tinykvpp_amd as tk  # noqa: E402
+import tinykvpp_amd.sst as sst  # noqa: E402
+from conftest import Oracle  # noqa: E402
+
+torch.cuda.set_device(0)
+tk.set_device(0)
+lib = tk.load_library()
+ora = Oracle(os.path.join(ROOT, "oracle", "liboracle.so"))
+rng = np.random.default_rng(1)
+GiB = 1 << 30
+
+
+def emit(name, nbytes, secs, unit_count, extra=None):
+    line = {"row": name, "GB/s": round(nbytes / secs / 1e9, 2), "bytes": int(nbytes), "units": int(unit_count),
+            "ms": round(secs * 1e3, 3)}
+    line.update(extra or {})
+    print(json.dumps(line), flush=True)
+
+
+def timeit(fn, reps=5):
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+# ---- WAL image: records with Zipf-ish key/value sizes (wal.cpp:19-61 layout) -------------------------
+n_rec = 400_000
+klen = rng.integers(8, 64, n_rec).astype(np.uint32)
+vlen = np.minimum(rng.zipf(1.6, n_rec) * 64, 16_000).astype(np.uint32)
+size = 26 + klen + vlen
+offs = np.concatenate([[0], np.cumsum(size[:-1], dtype=np.uint64)]).astype(np.uint64)
+total = int(size.sum())
+wal = rng.integers(0, 256, total, dtype=np.uint8)
+hdr = np.zeros((n_rec, 26), np.uint8)
+hdr[:, 0:4] = (size - 8).astype("<u4").view(np.uint8).reshape(-1, 4)
+hdr[:, 8] = 0
+hdr[:, 9:17] = np.arange(n_rec, dtype="<u8").view(np.uint8).reshape(-1, 8)
+hdr[:, 17] = 0
+hdr[:, 18:22] = klen.astype("<u4").view(np.uint8).reshape(-1, 4)
+hdr[:, 22:26] = vlen.astype("<u4").view(np.uint8).reshape(-1, 4)
+idx = offs.astype(np.int64)[:, None] + np.arange(26)
+wal[idx] = hdr
+sizes32 = size.astype(np.uint32)
+
+
+def stamp():
+    tk.check(lib.tkv_wal_stamp(ctypes.c_void_p(wal.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                               ctypes.c_void_p(sizes32.ctypes.data), n_rec))
+
+
+t = timeit(stamp)
+# CPU reference on a sample of records (payload [8, size) per record, wal.cpp:54-57)
+samp = 20_000
+t0 = time.perf_counter()
+for o, s in zip(offs[:samp], size[:samp]):
+    ora.crc(wal[int(o) + 8:int(o) + int(s)].tobytes())
+cpu = (time.perf_counter() - t0) / samp * n_rec
+emit("wal_stamp", total, t, n_rec, {"records": n_rec, "cpu_1core_GB/s_incl_python_loop": round(total / cpu / 1e9, 3)})
+
+good, stop = ctypes.c_uint64(), ctypes.c_uint64()
+
+
+def verify():
+    rc = lib.tkv_wal_verify(ctypes.c_void_p(wal.ctypes.data), total, ctypes.byref(good), ctypes.byref(stop))
+    assert rc == 0 and good.value == n_rec and stop.value == total, (rc, good.value, stop.value)
+
+
+t = timeit(verify)
+emit("wal_verify", total, t, n_rec, {"records": n_rec, "verified": good.value})
+poffs, plens = offs + 8, (size - 8).astype(np.uint32)
+t = timeit(lambda: tk.crc32_batch_host(wal, poffs, plens))
+emit("wal_payload_batch_host", total, t, n_rec, {"what": "the CRC part of wal_verify alone"})
+t0 = time.perf_counter()
+for _ in range(3):
+    lib.tkv_wal_verify(ctypes.c_void_p(wal.ctypes.data), total, ctypes.byref(good), ctypes.byref(stop))
+t1 = time.perf_counter()
+for _ in range(3):
+    stamp()
+t2 = time.perf_counter()
+emit("wal_verify_vs_stamp_back_to_back", total, (t1 - t0) / 3, n_rec, {"stamp_ms": round((t2 - t1) / 3 * 1e3, 3)})
+
+# ---- SSTable image: ~4 KiB data blocks -----------------------------------------------------------------
+nblk = 250_000
+body = 4096 - 36
+sizes = np.full(nblk, 36 + body, np.uint64)
+soffs = (np.arange(nblk, dtype=np.uint64) * sizes[0]).astype(np.uint64)
+sfile = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8)
+sfile[soffs.astype(np.int64)] = 20
+
+
+def sstamp():
+    sst.stamp_blocks(sfile, soffs, sizes)
+
+
+t = timeit(sstamp)
+emit("sst_stamp", sfile.nbytes, t, nblk, {"block_image_bytes": int(sizes[0])})
+assert sst.verify_blocks(sfile, soffs, sizes)[0] == "ok"
+
+d = torch.from_numpy(sfile).cuda()
+do = torch.from_numpy(soffs.astype(np.int64)).cuda()
+ds = torch.from_numpy(sizes.astype(np.int32)).cuda()
+out = torch.empty(nblk, dtype=torch.int32, device="cuda")
+st = torch.cuda.current_stream()
+for _ in range(20):
+    sst.block_crcs_device(d, do, ds, out=out)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(st)
+for _ in range(50):
+    sst.block_crcs_device(d, do, ds, out=out)
+e1.record(st)
+torch.cuda.synchronize()
+t = e0.elapsed_time(e1) / 50 / 1e3
+want = sfile[soffs.astype(np.int64)[:, None] + np.arange(17, 21)].copy().view("<u4").ravel()
+emit("sst_device", sfile.nbytes, t, nblk, {"bit_exact_vs_host_stamp": bool(np.array_equal(out.cpu().numpy().view(np.uint32), want))})
+del d
+
+# ---- CRC-32C, cfg2 shape ---------------------------------------------------------------------------------
+n = 1 << 20
+data = torch.empty(n * 4096, dtype=torch.uint8, device="cuda")
+tk.fill_synthetic_uniform(data, 4096, n)
+outc = torch.empty(n, dtype=torch.int32, device="cuda")
+for _ in range(100):
+    tk.crc32_batch_uniform(data, 4096, n, out=outc, algo="crc32c")
+e0.record(st)
+for _ in range(100):
+    tk.crc32_batch_uniform(data, 4096, n, out=outc, algo="crc32c")
+e1.record(st)
+torch.cuda.synchronize()
+t = e0.elapsed_time(e1) / 100 / 1e3
+probe = data[:64 * 4096].cpu().numpy()
+ok = all(ora.crc_c(probe[i * 4096:(i + 1) * 4096].tobytes()) == int(outc[i:i + 1].cpu().numpy().view(np.uint32)[0])
+         for i in range(0, 64, 7))
+emit("crc32c_cfg2", n * 4096, t, n, {"frac_of_8TB/s": round(n * 4096 / t / 8e12, 4), "bit_exact_sample": ok})
