@@ -165,6 +165,10 @@ size_t tkv_debug_tables_poly(uint32_t poly, void *out, size_t cap);
 
 /* Host GF(2) helpers the decomposition rests on: a*b mod P and x^(8n) mod P, reflected. */
 uint32_t tkv_debug_multmodp(uint32_t a, uint32_t b);
+/* The record chain tkv_wal_verify walks (host only, no CRC): writes up to `cap` record start offsets,
+ * the offset after the last record and whether a header did not fit; returns the record count. */
+size_t tkv_debug_wal_chain(const uint8_t *h_wal, uint64_t size, uint64_t *out_pos, size_t cap, uint64_t *end,
+                           int *err);
 uint32_t tkv_debug_x8nmodp(uint64_t nbytes);
 
 #ifdef __cplusplus

@@ -357,6 +357,22 @@ void gather(std::uint8_t* dst, const std::uint8_t* src, const std::uint64_t* off
   for (auto& t : th) t.join();
 }
 
+// memcpy of one large range into pinned staging, split over host threads when it is large.
+void copy_span(std::uint8_t* dst, const std::uint8_t* src, std::uint64_t n) {
+  const unsigned nt = n >= (std::uint64_t(32) << 20) ? 8u : 1u;
+  if (nt == 1) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([=] {
+      const std::uint64_t a = n * t / nt, e = n * (t + 1) / nt;
+      std::memcpy(dst + a, src + a, e - a);
+    });
+  for (auto& t : th) t.join();
+}
+
 // Blocks in [lo, hi) of a host batch, processed slab by slab. Blocks larger than a slab are
 // chained through update_device in slab-sized pieces on stream 0.
 int host_batch(DevCtx* c, int algo, const std::uint8_t* h_base, const std::uint64_t* off, const std::uint32_t* len,
@@ -430,10 +446,11 @@ int host_batch(DevCtx* c, int algo, const std::uint8_t* h_base, const std::uint6
     if (int rc = retire(k)) return rc;
     std::size_t cnt = 0, bytes = 0;
     const std::uint64_t b0 = b;
-    bool contiguous = true, uniform = true;
+    bool contiguous = true, uniform = true, ascending = true;
     while (b < hi && len[b] <= kSlab && bytes + len[b] <= kSlab && cnt < p.cap_blocks) {
       if (cnt) {
         contiguous = contiguous && off[b] == off[b - 1] + len[b - 1];
+        ascending = ascending && off[b] >= off[b - 1] + len[b - 1];
         uniform = uniform && len[b] == len[b0];
       }
       p.h_off[k][cnt] = bytes;
@@ -443,14 +460,29 @@ int host_batch(DevCtx* c, int algo, const std::uint8_t* h_base, const std::uint6
       ++cnt;
       ++b;
     }
-    // Contiguous blocks from pinned memory go straight to the device; anything else is gathered
-    // into the pinned staging slab (several host threads for large slabs).
-    if (contiguous && src_pinned) {
-      TKV_HIP(hipMemcpyAsync(p.d_data[k], h_base + off[b0], bytes, hipMemcpyHostToDevice, p.st[k]));
+    // How the slab's bytes reach the device:
+    //  * span: ascending blocks whose covering range [off[b0], end of last) is at most 1/4 larger
+    //    than their payload (WAL records, SSTable images: small headers between payloads) go over
+    //    as that one range - straight from pinned memory, else one threaded memcpy into staging -
+    //    and keep their offsets relative to it;
+    //  * anything else is gathered block by block into the pinned staging slab.
+    const std::uint64_t lo = off[b0], span = ascending ? off[b - 1] + len[b - 1] - lo : ~0ull;
+    const bool span_mode = ascending && span <= kSlab && span <= bytes + bytes / 4 + 4096;
+    if (span_mode) {
+      if (!contiguous)
+        for (std::size_t i = 0; i < cnt; ++i) p.h_off[k][i] = off[b0 + i] - lo;
+      if (src_pinned) {
+        TKV_HIP(hipMemcpyAsync(p.d_data[k], h_base + lo, span, hipMemcpyHostToDevice, p.st[k]));
+      } else {
+        copy_span(p.h_data[k], h_base + lo, span);
+        TKV_HIP(hipMemcpyAsync(p.d_data[k], p.h_data[k], span, hipMemcpyHostToDevice, p.st[k]));
+      }
     } else {
+      contiguous = false;
       gather(p.h_data[k], h_base, off, len, b0, cnt, p.h_off[k]);
       TKV_HIP(hipMemcpyAsync(p.d_data[k], p.h_data[k], bytes, hipMemcpyHostToDevice, p.st[k]));
     }
+    uniform = uniform && (contiguous || !span_mode);  // the uniform kernels need blocks back to back
     TKV_HIP(hipMemcpyAsync(p.d_init[k], p.h_init[k], cnt * 4, hipMemcpyHostToDevice, p.st[k]));
     if (uniform) {
       // equal lengths, packed back to back in the slab: the uniform (packed) kernels, no prepass

@@ -4,7 +4,12 @@
 // checksum over record or block bytes runs on the GPU through the engine (tkv_engine.h).
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "tkv_crc32.h"
@@ -27,6 +32,131 @@ std::uint32_t field_term(std::uint32_t v, std::uint64_t z) {
   return shift_bytes(c, z, kPoly);
 }
 
+// ---- WAL record_len chain (wal.cpp:63-87) ----------------------------------------------------------
+constexpr std::uint64_t kWalMeta = 26;  // wal.hpp:21-27 kMetadataSize
+
+struct Chain {
+  std::vector<std::uint64_t> pos;  // record starts, in order
+  std::vector<std::uint32_t> len;  // their record_len (payload bytes after the 8-byte prefix)
+  std::vector<std::uint32_t> crc;  // their stored crc32 (offset 4)
+  std::vector<std::uint8_t> kv_ok; // 26 + klen + vlen fits the record (wal.cpp:118-121)
+  std::uint64_t end = 0;           // first position after the last record (a record start >= limit)
+  bool err = false;                // the chain hit a header that does not fit (wal.cpp:68-70, 82-87)
+
+  void append(const Chain& o, std::size_t from) {
+    pos.insert(pos.end(), o.pos.begin() + from, o.pos.end());
+    len.insert(len.end(), o.len.begin() + from, o.len.end());
+    crc.insert(crc.end(), o.crc.begin() + from, o.crc.end());
+    kv_ok.insert(kv_ok.end(), o.kv_ok.begin() + from, o.kv_ok.end());
+    end = o.end;
+    err = o.err;
+  }
+};
+
+// Sequential walk from `start` over the records that START before `limit`.
+void walk(const std::uint8_t* w, std::uint64_t size, std::uint64_t start, std::uint64_t limit, Chain& c) {
+  std::uint64_t p = start;
+  while (p < limit) {
+    if (size - p < kWalMeta) {
+      c.err = true;
+      break;
+    }
+    std::uint32_t rlen, crc, klen, vlen;
+    std::memcpy(&rlen, w + p, 4);
+    if (static_cast<std::uint64_t>(rlen) + 8 > size - p) {
+      c.err = true;
+      break;
+    }
+    std::memcpy(&crc, w + p + 4, 4);  // the header's other fields share its cache line
+    std::memcpy(&klen, w + p + 18, 4);
+    std::memcpy(&vlen, w + p + 22, 4);
+    c.pos.push_back(p);
+    c.len.push_back(rlen);
+    c.crc.push_back(crc);
+    c.kv_ok.push_back(kWalMeta + static_cast<std::uint64_t>(klen) + vlen <= 8 + static_cast<std::uint64_t>(rlen));
+    p += 8 + static_cast<std::uint64_t>(rlen);
+  }
+  c.end = p;
+}
+
+// Host threads for CPU-side work: the CPUs this process may run on, capped by OMP_NUM_THREADS (the
+// GPU boxes' per-job CPU share) and 16.
+unsigned host_threads() {
+  unsigned n = 16;
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::min<unsigned>(n, static_cast<unsigned>(CPU_COUNT(&set)));
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+    const long v = std::strtol(e, nullptr, 10);
+    if (v > 0) n = std::min<unsigned>(n, static_cast<unsigned>(v));
+  }
+  return std::max(1u, n);
+}
+
+// A header the reference encoder would write (wal.cpp:19-61): record_len = 18 + klen + vlen and the
+// two flag bytes are 0/1. Used only to choose speculative starting points; never trusted.
+bool plausible(const std::uint8_t* w, std::uint64_t size, std::uint64_t p) {
+  if (size - p < kWalMeta) return false;
+  std::uint32_t rlen, klen, vlen;
+  std::memcpy(&rlen, w + p, 4);
+  std::memcpy(&klen, w + p + 18, 4);
+  std::memcpy(&vlen, w + p + 22, 4);
+  return w[p + 8] <= 1 && w[p + 17] <= 1 && static_cast<std::uint64_t>(rlen) == 18ull + klen + vlen &&
+         static_cast<std::uint64_t>(rlen) + 8 <= size - p;
+}
+
+// The chain of the whole image, identical to a sequential walk from 0. Each record start depends on
+// the previous one, so one thread walking a large WAL is bound by DRAM latency (one dependent miss
+// per record). Here the image is cut into K pieces; the walker of piece k>0 starts at the first
+// plausible header at or after the cut (speculation). Stitching is exact: piece k's chain is used
+// from the true entry point e_k (where the verified chain of pieces < k crosses the cut) onward only
+// if e_k is one of its record starts (chains that share a start coincide from there); otherwise
+// piece k is walked again from e_k.
+Chain wal_chain(const std::uint8_t* w, std::uint64_t size) {
+  constexpr std::uint64_t kPiece = std::uint64_t(8) << 20;
+  const unsigned K = static_cast<unsigned>(
+      std::min<std::uint64_t>(host_threads(), std::max<std::uint64_t>(1, size / kPiece)));
+  std::vector<std::uint64_t> cut(K + 1);
+  for (unsigned k = 0; k <= K; ++k) cut[k] = size * k / K;
+  std::vector<Chain> part(K);
+  auto run = [&](unsigned k) {
+    Chain local;  // built thread-locally: the Chain headers in `part` share cache lines
+    std::uint64_t p = cut[k];
+    if (k > 0) {
+      while (p < cut[k + 1] && !plausible(w, size, p)) ++p;
+      if (p >= cut[k + 1]) {
+        local.end = p;
+        local.err = true;  // no usable start: forces a re-walk if the chain needs this piece
+        part[k] = std::move(local);
+        return;
+      }
+    }
+    walk(w, size, p, cut[k + 1], local);
+    part[k] = std::move(local);
+  };
+  if (K == 1) {
+    run(0);
+    return std::move(part[0]);
+  }
+  std::vector<std::thread> th;
+  for (unsigned k = 0; k < K; ++k) th.emplace_back(run, k);
+  for (auto& t : th) t.join();
+  Chain c = std::move(part[0]);
+  for (unsigned k = 1; k < K && !c.err; ++k) {
+    const std::uint64_t e = c.end;  // true entry point into piece k (or beyond it)
+    if (e >= cut[k + 1]) continue;  // one record spans piece k entirely
+    const auto& pk = part[k].pos;
+    const auto it = std::lower_bound(pk.begin(), pk.end(), e);
+    if (it != pk.end() && *it == e) {
+      c.append(part[k], static_cast<std::size_t>(it - pk.begin()));
+    } else {
+      Chain r;
+      walk(w, size, e, cut[k + 1], r);
+      c.append(r, 0);
+    }
+  }
+  return c;
+}
+
 int sst_check(const std::uint64_t* h_sizes, std::uint64_t n) {
   for (std::uint64_t i = 0; i < n; ++i)
     if (h_sizes[i] < TKV_SST_MIN_IMAGE || h_sizes[i] > 0xFFFFFFFFull)
@@ -40,48 +170,22 @@ extern "C" {
 int tkv_wal_verify(const uint8_t* h_wal, uint64_t size, uint64_t* n_good, uint64_t* stop_offset) {
   if ((size && !ptr_ok(h_wal)) || !ptr_ok(n_good) || !ptr_ok(stop_offset))
     return set_error(TKV_INVALID_ARGUMENT, "null pointer");
-  // Walk the record_len chain (wal.cpp:63-87): each record is [u32 record_len][u32 crc][payload].
-  constexpr std::uint64_t kMeta = 26;  // wal.hpp:21-27 kMetadataSize
-  std::vector<std::uint64_t> off;
-  std::vector<std::uint32_t> len, stored;
-  std::uint64_t pos = 0;
-  bool structural_error = false;
-  while (pos < size) {
-    const std::uint64_t left = size - pos;
-    if (left < kMeta) {
-      structural_error = true;  // wal.cpp:68-70
-      break;
-    }
-    std::uint32_t rlen, crc;
-    std::memcpy(&rlen, h_wal + pos, 4);
-    std::memcpy(&crc, h_wal + pos + 4, 4);
-    if (static_cast<std::uint64_t>(rlen) + 8 > left) {
-      structural_error = true;  // wal.cpp:82-87
-      break;
-    }
-    off.push_back(pos + 8);
-    len.push_back(rlen);
-    stored.push_back(crc);
-    pos += 8 + static_cast<std::uint64_t>(rlen);
+  // The record_len chain (wal.cpp:63-87), walked in parallel (wal_chain): records are
+  // [u32 record_len][u32 crc][payload of record_len bytes].
+  const Chain ch = wal_chain(h_wal, size);
+  const std::size_t nrec = ch.pos.size();
+  std::vector<std::uint64_t> off(nrec);
+  std::vector<std::uint32_t> got(nrec);
+  for (std::size_t i = 0; i < nrec; ++i) off[i] = ch.pos[i] + 8;
+  if (nrec) {
+    if (int rc = batch_host_impl(kAlgoCrc32, h_wal, off.data(), ch.len.data(), nullptr, got.data(), nrec)) return rc;
   }
-  std::vector<std::uint32_t> got(off.size());
-  if (!off.empty()) {
-    if (int rc = batch_host_impl(kAlgoCrc32, h_wal, off.data(), len.data(), nullptr, got.data(), off.size())) return rc;
-  }
-  std::uint64_t good = 0, stop = 0;
-  for (; good < off.size(); ++good) {
-    if (got[good] != stored[good]) break;  // wal.cpp:93-96
-    // key/value bounds inside the payload (wal.cpp:118-121)
-    const std::uint8_t* rec = h_wal + off[good] - 8;
-    std::uint32_t klen, vlen;
-    std::memcpy(&klen, rec + 18, 4);
-    std::memcpy(&vlen, rec + 22, 4);
-    if (kMeta + static_cast<std::uint64_t>(klen) + vlen > 8 + static_cast<std::uint64_t>(len[good])) break;
-  }
-  stop = good < off.size() ? off[good] - 8 : pos;
+  std::uint64_t good = 0;
+  // first record whose CRC (wal.cpp:93-96) or key/value bounds (wal.cpp:118-121) fail
+  while (good < nrec && got[good] == ch.crc[good] && ch.kv_ok[good]) ++good;
   *n_good = good;
-  *stop_offset = stop;
-  if (good < off.size() || structural_error) return set_error(TKV_CORRUPTED, "corrupted WAL record");
+  *stop_offset = good < nrec ? ch.pos[good] : ch.end;
+  if (good < nrec || ch.err) return set_error(TKV_CORRUPTED, "corrupted WAL record");
   return TKV_OK;
 }
 
@@ -149,6 +253,15 @@ int tkv_sst_block_crcs_device(uint8_t* d_file, const uint64_t* d_offsets, const 
   const hipError_t e = launch_sst_fix(d_file, d_offsets, d_sizes, d_out, n, store, tabs, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return set_error(TKV_IO_ERROR, hipGetErrorString(e));
   return TKV_OK;
+}
+
+size_t tkv_debug_wal_chain(const uint8_t* h_wal, uint64_t size, uint64_t* out_pos, size_t cap, uint64_t* end,
+                           int* err) {
+  const Chain c = wal_chain(h_wal, size);
+  if (out_pos) std::memcpy(out_pos, c.pos.data(), std::min(cap, c.pos.size()) * sizeof(std::uint64_t));
+  if (end) *end = c.end;
+  if (err) *err = c.err ? 1 : 0;
+  return c.pos.size();
 }
 
 }  // extern "C"
