@@ -147,6 +147,9 @@ int tkv_crc32c_batch_uniform_device(const uint8_t *d_base, uint64_t stride, uint
                                     void *stream);
 int tkv_crc32c_batch_host(const uint8_t *h_base, const uint64_t *h_offsets, const uint32_t *h_lengths,
                           const uint32_t *h_init_raw, uint32_t *h_out_final, uint64_t n);
+int tkv_crc32c_batch_host_multi(const int *devices, int ndev, const uint8_t *h_base, const uint64_t *h_offsets,
+                                const uint32_t *h_lengths, const uint32_t *h_init_raw, uint32_t *h_out_final,
+                                uint64_t n);
 
 /* ---- synthetic data (SURVEY.md §8d generator; bench/test inputs) ------------------------------- */
 

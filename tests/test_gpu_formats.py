@@ -58,6 +58,7 @@ def test_crc32c_irregular_and_host(gpu, oracle):
                              torch.from_numpy(lens.astype(np.int32)).to(gpu), algo="crc32c"))
     assert np.array_equal(got, want)
     assert np.array_equal(tk.crc32_batch_host(host, offs.astype(np.uint64), lens, algo="crc32c"), want)
+    assert np.array_equal(tk.crc32_batch_host(host, offs.astype(np.uint64), lens, algo="crc32c", devices=[0, 0]), want)
     # the two families really differ
     assert not np.array_equal(tk.crc32_batch_host(host, offs.astype(np.uint64), lens), want)
 

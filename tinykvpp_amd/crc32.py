@@ -164,7 +164,6 @@ def crc32_batch_uniform(data, length, n, stride=None, init_raw=None, out=None, s
 
 def crc32_batch_host(data, offsets, lengths, init_raw=None, devices=None, algo="crc32"):
     """Host-memory batch (numpy): pinned staging, H2D / kernel / D2H overlapped. Returns uint32."""
-    lib = load_library()
     buf = np.ascontiguousarray(data).view(np.uint8)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
     ln = np.ascontiguousarray(lengths, dtype=np.uint32)
@@ -176,10 +175,8 @@ def crc32_batch_host(data, offsets, lengths, init_raw=None, devices=None, algo="
                                       ctypes.c_void_p(ln.ctypes.data), initp,
                                       ctypes.c_void_p(out.ctypes.data), off.size))
     else:
-        if algo != "crc32":
-            raise ValueError("the multi-GPU host batch serves the reference CRC-32 only")
         devs = (ctypes.c_int * len(devices))(*devices)
-        check(lib.tkv_crc32_batch_host_multi(devs, len(devices), ctypes.c_void_p(buf.ctypes.data),
+        check(_fn(algo, "batch_host_multi")(devs, len(devices), ctypes.c_void_p(buf.ctypes.data),
                                              ctypes.c_void_p(off.ctypes.data), ctypes.c_void_p(ln.ctypes.data),
                                              initp, ctypes.c_void_p(out.ctypes.data), off.size))
     return out

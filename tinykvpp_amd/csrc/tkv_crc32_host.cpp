@@ -705,6 +705,11 @@ int tkv_crc32c_batch_host(const uint8_t* h_base, const uint64_t* h_offsets, cons
                           const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
   return batch_host_impl(kAlgoCrc32c, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, n);
 }
+int tkv_crc32c_batch_host_multi(const int* devices, int ndev, const uint8_t* h_base, const uint64_t* h_offsets,
+                                const uint32_t* h_lengths, const uint32_t* h_init_raw, uint32_t* h_out_final,
+                                uint64_t n) {
+  return batch_host_multi_impl(kAlgoCrc32c, devices, ndev, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, n);
+}
 
 int tkv_fill_synthetic_uniform(uint8_t* d_dst, uint64_t stride, uint64_t len, uint64_t first_block, uint64_t nblocks,
                                uint64_t seed, void* stream) {
