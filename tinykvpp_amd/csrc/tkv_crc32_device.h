@@ -464,7 +464,7 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
 // (4 KiB blocks), so no Horner state at all. The SIMDs are issue-bound here (PMC: every SIMD issues
 // ~96 % of cycles), so the loop is written for instruction count: incremental row addressing, no
 // divisions, selects instead of divergent branches.
-template <int DEPTH, int ILP, bool R1, bool SPLIT = false>
+template <int DEPTH, int ILP, bool R1, bool SPLIT = false, std::uint32_t ROT = 0>
 __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
   fill_lds(a.tabs, lds);
@@ -493,10 +493,19 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
   const std::uint32_t nrows = nb * R;  // wave-local rows j = 0 .. nrows-1, contiguous in memory
   const std::uintptr_t lane_base =
       reinterpret_cast<std::uintptr_t>(a.base) + static_cast<std::uint64_t>(b0) * R * kRow + lane * kSeg;
+  // ROT != 0: the wave walks its blocks starting at block (wave*ROT) mod nb and wraps around, so at
+  // any instant the waves sit at different offsets inside their ranges (address bits below the
+  // range size differ from wave to wave instead of being equal).
+  const std::uint32_t rot_b = ROT ? static_cast<std::uint32_t>((wave * static_cast<std::uint64_t>(ROT)) % nb) : 0u;
+  const std::uint32_t rotr = rot_b * R;
 
   uint4 buf[DEPTH][4];
   auto issue = [&](std::uint32_t j, uint4 (&q)[4]) {
-    const std::uint32_t jc = j < nrows ? j : nrows - 1;  // rows past the range reload the last one
+    std::uint32_t jc = j < nrows ? j : nrows - 1;  // rows past the range reload the last one
+    if constexpr (ROT != 0) {
+      jc += rotr;
+      jc -= jc >= nrows ? nrows : 0u;
+    }
     const std::uintptr_t p = lane_base + static_cast<std::uint64_t>(jc) * kRow;
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i);
@@ -512,7 +521,9 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
     if (head) {
       term = inj_const;
       if (a.init_raw) {
-        const std::uint32_t init = sload32(a.init_raw, b0 + k);
+        std::uint32_t kk = k + rot_b;
+        kk -= kk >= nb ? nb : 0u;
+        const std::uint32_t init = sload32(a.init_raw, b0 + kk);
         term = lo_half ? 0u : static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init),
                                                                                 lane & 31u, 1)) & hcon;
       }
@@ -526,7 +537,9 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
       const std::uint32_t slot = k & 63u;
       keep = lane == slot ? (Bn ^ a.out_xor) : keep;
       if (slot == 63u || k + 1 == nb) {
-        if (lane <= slot) a.out[b0 + k - slot + lane] = keep;
+        std::uint32_t li = k - slot + lane + rot_b;  // wave-local block of lane's result
+        li -= li >= nb ? nb : 0u;
+        if (lane <= slot) a.out[b0 + li] = keep;
       }
       r = 0;
       ++k;

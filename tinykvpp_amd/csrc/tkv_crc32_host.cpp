@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -124,6 +125,17 @@ struct StreamScratch {
   std::uint64_t cap_blocks = 0;
 };
 
+// Spans up to this size take update()'s latency path (mapped pinned memory, one launch);
+// TKV_UPDATE_SMALL_BYTES overrides the threshold (0 disables the path; for A/B measurements).
+constexpr std::size_t kSmallSpan = std::size_t(256) << 10;
+std::size_t small_span_limit() {
+  static const std::size_t v = [] {
+    const char* e = std::getenv("TKV_UPDATE_SMALL_BYTES");
+    return e ? std::min<std::size_t>(std::strtoull(e, nullptr, 10), kSmallSpan) : kSmallSpan;
+  }();
+  return v;
+}
+
 // Pinned staging of the host-memory pipeline: two slabs, two streams (one per slab).
 constexpr std::size_t kSlab = std::size_t(256) << 20;  // bytes of block data per pipeline stage
 struct HostPipe {
@@ -194,6 +206,11 @@ struct DevCtx {
   std::uint32_t* d_io = nullptr;
   std::uint32_t* h_io = nullptr;
   std::size_t stage_cap = 0;
+  // small spans: mapped pinned buffers the kernel reads and writes in place (no copy engines)
+  std::uint8_t* h_small = nullptr;
+  const std::uint8_t* d_small = nullptr;  // device view of h_small
+  std::uint32_t* h_res = nullptr;
+  std::uint32_t* d_res = nullptr;         // device view of h_res
   // host-memory batch pipeline, kept between calls (guarded by pipe_mu)
   std::mutex pipe_mu;
   std::unique_ptr<HostPipe> pipe;
@@ -527,6 +544,22 @@ int update_impl(int algo, uint32_t raw_state, const void* data, size_t len, uint
     TKV_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_io), 16, hipHostMallocDefault));
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&c->d_io), 16));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_small), kSmallSpan, hipHostMallocMapped));
+    TKV_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(const_cast<std::uint8_t**>(&c->d_small)), c->h_small, 0));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_res), 64,
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    TKV_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_res), c->h_res, 0));
+  }
+  if (len <= small_span_limit()) {
+    // Latency path (one WAL record per call, wal.cpp:54-57): the kernel reads the span from mapped
+    // pinned memory and writes the register back into mapped memory - one launch and one sync,
+    // no copy-engine round trips.
+    if (len) std::memcpy(c->h_small, data, len);
+    const std::uint8_t* base = len ? c->d_small : c->d_dummy;
+    if (int rc = run_uniform(c, algo, base, len, len, nullptr, raw_state, 0u, c->d_res, 1, c->st)) return rc;
+    TKV_HIP(hipStreamSynchronize(c->st));
+    *out_raw = *reinterpret_cast<volatile std::uint32_t*>(c->h_res);
+    return TKV_OK;
   }
   const std::size_t want = std::min<std::size_t>(std::max<std::size_t>(len, 1 << 16), kSlab);
   if (want > c->stage_cap) {

@@ -160,3 +160,26 @@ probe = data[:64 * 4096].cpu().numpy()
 ok = all(ora.crc_c(probe[i * 4096:(i + 1) * 4096].tobytes()) == int(outc[i:i + 1].cpu().numpy().view(np.uint32)[0])
          for i in range(0, 64, 7))
 emit("crc32c_cfg2", n * 4096, t, n, {"frac_of_8TB/s": round(n * 4096 / t / 8e12, 4), "bit_exact_sample": ok})
+
+# ---- latency of small calls (the per-record drop-in path and small group commits) ----------------------
+def lat(fn, reps=200):
+    fn()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return (time.perf_counter() - t0) / reps * 1e6
+
+
+for nbytes in (36, 4096, 65536, 1 << 20):
+    payload = rng.bytes(nbytes)
+    c = tk.crc32()
+    us = lat(lambda: c.update(payload))
+    print(json.dumps({"row": "update_latency", "bytes": nbytes, "us_per_call": round(us, 2)}), flush=True)
+for nrec in (1, 16, 256, 4096):
+    recs = np.ascontiguousarray(wal[:int(offs[nrec])]) if nrec < n_rec else wal
+    o = offs[:nrec].copy()
+    s32 = sizes32[:nrec].copy()
+    us = lat(lambda: tk.check(lib.tkv_wal_stamp(ctypes.c_void_p(recs.ctypes.data), ctypes.c_void_p(o.ctypes.data),
+                                               ctypes.c_void_p(s32.ctypes.data), nrec)), reps=50)
+    print(json.dumps({"row": "wal_stamp_latency", "records": nrec, "bytes": int(offs[nrec]), "us_per_call": round(us, 2)}),
+          flush=True)

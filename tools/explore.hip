@@ -17,9 +17,11 @@ __global__ __launch_bounds__(kThreads) void k_rows(RowsArgs a) {
 }
 
 // Ideal streaming read: every lane reads consecutive 16-byte words, XOR-reduces, one store per wave.
-__global__ __launch_bounds__(256) void k_stream(const uint4* p, std::uint64_t n16, std::uint32_t* out) {
+template <int T = 256>
+__global__ __launch_bounds__(T) void k_stream(const uint4* p, std::uint64_t n16, std::uint32_t* out) {
   std::uint32_t x = 0;
-  for (std::uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += gridDim.x * 256ull) {
+  for (std::uint64_t i = blockIdx.x * static_cast<std::uint64_t>(T) + threadIdx.x; i < n16;
+       i += gridDim.x * static_cast<std::uint64_t>(T)) {
     const uint4 v = p[i];
     x ^= v.x ^ v.y ^ v.z ^ v.w;
   }
@@ -34,7 +36,7 @@ __global__ __launch_bounds__(256) void k_stream(const uint4* p, std::uint64_t n1
 // PAT 2: lane l reads [2048(i/2) + 32l + 16(i%2), +16) (32-byte lane segments)
 // FIN 0: XOR into a register, one store per wave; FIN 1: per-row DPP reduce + lane-0 store per row;
 // FIN 2: per-row reduce, results kept in lane (row % 64) and stored 64 at a time (coalesced).
-template <int PAT, int DEPTH, int FIN, int MIS = 0>
+template <int PAT, int DEPTH, int FIN, int MIS = 0, int STR = 0>
 __global__ __launch_bounds__(1024) void k_pat(const std::uint8_t* base, std::uint32_t nrows, std::uint32_t W,
                                               std::uint32_t* out) {
   base += MIS;  // byte misalignment of every load (unaligned global_load_dwordx4)
@@ -43,7 +45,10 @@ __global__ __launch_bounds__(1024) void k_pat(const std::uint8_t* base, std::uin
   const std::uint32_t g0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(nrows) / W);
   const std::uint32_t g1 = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(nrows) / W);
   auto addr = [&](std::uint32_t g, int i) -> std::uintptr_t {
-    const std::uintptr_t rb = reinterpret_cast<std::uintptr_t>(base) + static_cast<std::uint64_t>(g < g1 ? g : g0) * 4096u;
+    const std::uint32_t gl = g < g1 ? g : g0;
+    // STR: the wave's j-th row is global row wave + j*W (all waves sweep one moving window)
+    const std::uint64_t phys = STR ? static_cast<std::uint64_t>(gl - g0) * W + wave : gl;
+    const std::uintptr_t rb = reinterpret_cast<std::uintptr_t>(base) + phys * 4096u;
     if constexpr (PAT == 0) return rb + 64u * lane + 16u * i;
     else if constexpr (PAT == 1) return rb + 1024u * i + 16u * lane;
     else return rb + 2048u * (i / 2) + 32u * lane + 16u * (i % 2);
@@ -184,16 +189,23 @@ void L(RowsArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_rows<D, I, M>), dim3(g_ncu), dim3(kThreads), 0, s, a);
 }
 
-template <int PAT, int D, int F, int MIS = 0>
+template <int PAT, int D, int F, int MIS = 0, int STR = 0>
 void P(RowsArgs a, hipStream_t s) {
-  hipLaunchKernelGGL((k_pat<PAT, D, F, MIS>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows - 1, a.nwaves,
+  hipLaunchKernelGGL((k_pat<PAT, D, F, MIS, STR>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows - 1, a.nwaves,
                      a.out);
 }
 
-template <int D, int I, bool R1, int T, bool SP>
+template <int D, int I, bool R1, int T, bool SP, std::uint32_t ROT = 0>
 __global__ __launch_bounds__(T) void k_packed(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<D, I, R1, SP>(a, lds);
+  dev::crc_packed_body<D, I, R1, SP, ROT>(a, lds);
+}
+
+template <std::uint32_t ROT>
+void PR(RowsArgs a, hipStream_t s) {
+  a.nwaves = g_ncu * 16;
+  if (a.len == kRow) hipLaunchKernelGGL((k_packed<4, 2, true, 1024, false, ROT>), dim3(g_ncu), dim3(1024), 0, s, a);
+  else hipLaunchKernelGGL((k_packed<4, 2, false, 1024, false, ROT>), dim3(g_ncu), dim3(1024), 0, s, a);
 }
 
 template <int D, int I, bool R1, int T, int CR>
@@ -227,6 +239,7 @@ const V kVariants[] = {
     {"interf L0 V0", IF<0, 0>}, {"interf L72 V0", IF<72, 0>}, {"interf L0 V128", IF<0, 128>},
     {"interf L72 V128", IF<72, 128>}, {"interf L36 V0", IF<36, 0>}, {"interf L144 V0", IF<144, 0>},
     {"interf L0 V256", IF<0, 256>},
+    {"packed rot1", PR<1>}, {"packed rot61", PR<61>}, {"packed rot16", PR<16>},
     {"dyn D4 I2 C8", PD<4, 2, 8>}, {"dyn D4 I2 C16", PD<4, 2, 16>}, {"dyn D4 I2 C32", PD<4, 2, 32>},
     {"dyn D4 I2 C64", PD<4, 2, 64>}, {"dyn T768 D4 I2 C16", PD<4, 2, 16, 768>},
     {"packed D4 I2", PK<4, 2>}, {"packed D4 I1", PK<4, 1>}, {"packed D3 I1", PK<3, 1>},
@@ -239,6 +252,8 @@ const V kVariants[] = {
     {"crc D4 I2", L<4, 2, 0>}, {"crc D6 I2", L<6, 2, 0>},
     {"mem D2 I1", L<2, 1, 1>}, {"mem D4 I1", L<4, 1, 1>}, {"mem D4 I2", L<4, 2, 1>},
     {"mem D8 I1", L<8, 1, 1>},
+    {"pat seg64 D4 fin0 strided", P<0, 4, 0, 0, 1>}, {"pat coal D4 fin0 strided", P<1, 4, 0, 0, 1>},
+    {"pat seg64 D4 fin2 strided", P<0, 4, 2, 0, 1>}, {"stream T1024 ncu", nullptr},
     {"pat seg64 D4 fin2 mis0", P<0, 4, 2, 0>}, {"pat seg64 D4 fin2 mis4", P<0, 4, 2, 4>},
     {"pat seg64 D4 fin2 mis5", P<0, 4, 2, 5>}, {"pat seg64 D4 fin2 mis8", P<0, 4, 2, 8>},
     {"pat seg64 D2 fin0", P<0, 2, 0>}, {"pat seg64 D4 fin0", P<0, 4, 0>}, {"pat seg64 D4 fin1", P<0, 4, 1>},
@@ -305,7 +320,12 @@ extern "C" int explore_run(int v, const std::uint8_t* base, std::uint64_t n, std
     hipMalloc(&g_ctr, 4 * kCtrStride * g_ncu);
   }
   if (v == kNV) {
-    hipLaunchKernelGGL(k_stream, dim3(g_ncu * 8), dim3(256), 0, st, reinterpret_cast<const uint4*>(base),
+    hipLaunchKernelGGL(k_stream<256>, dim3(g_ncu * 8), dim3(256), 0, st, reinterpret_cast<const uint4*>(base),
+                       n * len / 16, out);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
+  if (kVariants[v].launch == nullptr) {  // "stream T1024 ncu": the ideal read at the CRC kernels' shape
+    hipLaunchKernelGGL(k_stream<1024>, dim3(g_ncu), dim3(1024), 0, st, reinterpret_cast<const uint4*>(base),
                        n * len / 16, out);
     return hipGetLastError() == hipSuccess ? 0 : 2;
   }
