@@ -211,6 +211,37 @@ def test_irregular_vs_oracle(gpu, oracle, nblocks, maxlen, packed):
     assert np.array_equal(got, oracle.batch(host, offs, lens, init))
 
 
+@pytest.mark.parametrize("mix", ["all_small", "boundary", "alternating", "small_at_buffer_edges"])
+def test_small_block_split(gpu, oracle, mix):
+    """The prepass splits blocks at kSmallMax = 1024 bytes: small ones are folded four to a wave by
+    crc_small, large ones by the row kernel on a compacted list; results land at batch indices."""
+    rng = np.random.default_rng(len(mix))
+    if mix == "all_small":
+        lens = rng.integers(0, 1025, 20000)
+    elif mix == "boundary":
+        lens = np.tile(np.array([0, 1, 3, 15, 16, 17, 1023, 1024, 1025, 1026, 2047, 4095, 4096, 4097]), 300)
+    elif mix == "alternating":
+        lens = np.where(np.arange(6001) % 2 == 0, rng.integers(0, 1025, 6001), rng.integers(1025, 30000, 6001))
+    else:
+        lens = rng.integers(0, 1025, 3001)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+    if mix == "alternating":
+        offs += rng.integers(0, 16, lens.size).cumsum()  # gaps: any alignment
+    size = int((offs + lens).max()) + (0 if mix == "small_at_buffer_edges" else 40)
+    host = rng.integers(0, 256, max(size, 1), dtype=np.uint8)
+    d = torch.from_numpy(host).to(gpu)
+    o = torch.from_numpy(offs).to(gpu)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    want = oracle.batch(host, offs, lens.astype(np.int32))
+    assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), want)
+    init = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    got = u32(tk.crc32_batch(d, o, ln, init_raw=torch.from_numpy(init.view(np.int32)).to(gpu)))
+    assert np.array_equal(got, oracle.batch(host, offs, lens.astype(np.int32), init))
+    # a second, smaller batch on the same stream reuses the scratch of the first
+    m = max(1, lens.size // 7)
+    assert np.array_equal(u32(tk.crc32_batch(d, o[:m].contiguous(), ln[:m].contiguous())), want[:m])
+
+
 def test_irregular_zipf_sample(gpu, oracle):
     """First 4096 blocks of cfg4 (Zipf 256 B - 1 MiB), packed back to back, unaligned starts."""
     c = golden("synthetic.json")["cfg4"]

@@ -133,8 +133,8 @@ struct Cursor {
 };
 
 template <bool UNIFORM>
-__device__ __forceinline__ void load_desc(const RowsArgs& a, Cursor& c) {
-  const std::uint32_t b = c.b < a.nblocks ? c.b : a.nblocks - 1;
+__device__ __forceinline__ void load_desc(const RowsArgs& a, Cursor& c, std::uint32_t nblk) {
+  const std::uint32_t b = c.b < nblk ? c.b : nblk - 1;
   if constexpr (UNIFORM) {
     c.blk = a.base + static_cast<std::uint64_t>(b) * a.stride;
     c.n = a.len;
@@ -146,11 +146,11 @@ __device__ __forceinline__ void load_desc(const RowsArgs& a, Cursor& c) {
 }
 
 template <bool UNIFORM>
-__device__ __forceinline__ void advance(const RowsArgs& a, Cursor& c) {
+__device__ __forceinline__ void advance(const RowsArgs& a, Cursor& c, std::uint32_t nblk) {
   if (++c.r == c.R) {
     c.r = 0;
     ++c.b;
-    load_desc<UNIFORM>(a, c);
+    load_desc<UNIFORM>(a, c, nblk);
   }
 }
 
@@ -286,7 +286,8 @@ __device__ __forceinline__ void finish_row(const RowsArgs& a, const Cursor& c, s
   const std::uint32_t Bn = __builtin_amdgcn_readlane(wave_xor_to_lane63(v), 63);
   if (c.r + 1 == c.R || last_of_range) {
     if (st.piece_has_row0 && c.r + 1 == c.R) {
-      if (lane == 0) a.out[c.b] = Bn ^ a.out_xor;
+      const std::uint32_t ob = a.out_idx ? sload32(a.out_idx, c.b) : c.b;
+      if (lane == 0) a.out[ob] = Bn ^ a.out_xor;
     } else {
       // (explicit slots: a runtime index into these arrays would put them in scratch memory)
       const std::uint32_t flags = kSeamValid | (st.piece_has_row0 ? kSeamHasRow0 : 0u);
@@ -341,6 +342,7 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
 
   // This wave's contiguous range of rows [g0, g1).
   std::uint32_t g0, g1;
+  std::uint32_t nblk = a.nblocks;
   Cursor cur;
   if constexpr (UNIFORM) {
     const std::uint32_t R = rows_for_len(a.len);
@@ -354,7 +356,9 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
     cur.b = g0 / R;
     cur.r = g0 - cur.b * R;
   } else {
-    const std::uint64_t TR = sload32(a.row_scan, a.nblocks);
+    // large blocks only (compacted by the prepass); small ones are crc_small's
+    nblk = sload32(a.counts, 0);
+    const std::uint64_t TR = sload32(a.counts, 2);
     g0 = static_cast<std::uint32_t>(wave * TR / W);
     g1 = static_cast<std::uint32_t>((wave + 1) * TR / W);
     cur.b = g0 < g1 ? sload32(a.wave_start, wave) : 0u;
@@ -368,7 +372,7 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
   for (int s = 0; s < 2; ++s) st.s_block[s] = st.s_part[s] = st.s_after[s] = st.s_flags[s] = 0;
 
   if (g0 < g1) {
-    load_desc<UNIFORM>(a, cur);
+    load_desc<UNIFORM>(a, cur, nblk);
     st.piece_has_row0 = cur.r == 0;
 
     // Lane contributions of n rows before the Horner step, Shift_{(63-l)*64}(crc_0(segment)), with
@@ -406,7 +410,7 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
     for (int s = 0; s < DEPTH - ILP; ++s) {
       cq[s] = lc;
       issue_row<NP, UNIFORM>(a, lc, gl < g1, lane, buf[s]);
-      advance<UNIFORM>(a, lc);
+      advance<UNIFORM>(a, lc, nblk);
       ++gl;
     }
     for (std::uint32_t g = g0; g < g1; g += DEPTH) {
@@ -418,7 +422,7 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
           const int s = (k + DEPTH - ILP + j) % DEPTH;
           cq[s] = lc;
           issue_row<NP, UNIFORM>(a, lc, gl < g1, lane, buf[s]);
-          advance<UNIFORM>(a, lc);
+          advance<UNIFORM>(a, lc, nblk);
           ++gl;
         }
         const std::uint32_t gk = g + k;
@@ -452,6 +456,131 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
       rec.rows_after = st.s_after[s];
       rec.flags = st.s_flags[s];
       a.seams[2 * static_cast<std::uint64_t>(wave) + s] = rec;
+    }
+  }
+}
+
+// Small blocks of an irregular batch (len <= kSmallMax = 1 KiB, listed by the prepass in
+// s_off/s_len/s_idx): a 16-lane group folds one block, right-aligned in a 1 KiB mini-row (lane g
+// owns bytes [64 g, 64 g + 64) of it; bytes in front of the block are zero), so a wave folds four
+// blocks per step where the row kernel would spend a whole 4 KiB row on each. Lane shifts are the
+// LS entries of lane 48 + g (Shift_{(15-g)*64}), the init term is spread over the group (two bits
+// per lane: bit_i(init) * Shift_len(1 << i)), and the first four DPP steps of the wave reduction
+// sum each 16-lane row. Waves own contiguous ranges of steps (4 blocks per step). Pipeline: data of
+// step t+2 is issued while step t folds; descriptors are fetched 4 steps ahead of their data.
+__device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t* lds) {
+  constexpr int RING = 4;
+  fill_lds(a.tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint32_t grp = lane >> 4, gl = lane & 15u;
+  LaneConst kc = lane_const(lane);
+  kc.lsbase = kLdsLaneBase + (48u + gl) * 4u;
+  __syncthreads();
+
+  const std::uint32_t NS = sload32(a.counts, 1);
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves;
+  const std::uint64_t S = (NS + 3u) / 4u;
+  const std::uint32_t t0 = static_cast<std::uint32_t>(wave * S / W);
+  const std::uint32_t t1 = static_cast<std::uint32_t>((wave + 1) * S / W);
+  if (t0 >= t1) return;
+  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
+  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
+
+  // descriptor ring (slot = step % RING): byte offset, length, batch index; kept valid-masked
+  std::uint64_t d_off[RING];
+  std::uint32_t d_len[RING], d_idx[RING];
+  auto fetch = [&](std::uint32_t t, int slot) {
+    const std::uint32_t j = 4u * t + grp;
+    const bool ok = t < t1 && j < NS;
+    const std::uint32_t jj = ok ? j : 0u;
+    d_off[slot] = ok ? a.s_off[jj] : 0ull;
+    d_len[slot] = ok ? a.s_len[jj] : 0u;
+    d_idx[slot] = ok ? a.s_idx[jj] : 0xFFFFFFFFu;
+  };
+  // data ring: five 16-byte pieces covering the lane's segment, plus what the fold step needs
+  uint4 q[RING][5];
+  std::uint32_t m_len[RING], m_idx[RING], m_end[RING];
+  auto issue = [&](int slot) {
+    const std::uint32_t n = d_len[slot];
+    const bool ok = d_idx[slot] != 0xFFFFFFFFu;
+    const std::uintptr_t blo = base + d_off[slot];
+    const std::uintptr_t bhi = blo + n;
+    const std::uintptr_t seg = static_cast<std::uintptr_t>(static_cast<std::int64_t>(bhi) - static_cast<std::int64_t>(kSmallMax)) +
+                               gl * kSeg;
+    const std::uintptr_t al = seg & ~static_cast<std::uintptr_t>(15);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const std::uintptr_t p = al + 16u * i;
+      q[slot][i] = gload16(ok && (p + 16 > blo) && (p < bhi) ? p : dmy);
+    }
+    m_len[slot] = n;
+    m_idx[slot] = d_idx[slot];
+    m_end[slot] = static_cast<std::uint32_t>(bhi & 15u);
+  };
+  auto fold = [&](int slot) {
+    const std::uint32_t n = m_len[slot];
+    std::uint32_t raw[20];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      raw[4 * i + 0] = q[slot][i].x;
+      raw[4 * i + 1] = q[slot][i].y;
+      raw[4 * i + 2] = q[slot][i].z;
+      raw[4 * i + 3] = q[slot][i].w;
+    }
+    // realign by the block end's offset within 16 bytes (per group: bitwise selects - a ternary
+    // here is turned into a dynamically indexed array, i.e. scratch memory)
+    const std::uint32_t sft = m_end[slot];
+    const std::uint32_t m8 = 0u - ((sft >> 3) & 1u), m4 = 0u - ((sft >> 2) & 1u);
+#pragma unroll
+    for (int i = 0; i < 18; ++i) raw[i] ^= (raw[i] ^ raw[i + 2]) & m8;
+#pragma unroll
+    for (int i = 0; i < 19; ++i) raw[i] ^= (raw[i] ^ raw[i + 1]) & m4;
+    std::uint32_t dw[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dw[k] = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sft & 3u);
+    // zero the bytes in front of the block (a straddling piece holds its neighbour's bytes)
+    const std::int32_t off0 = static_cast<std::int32_t>(n) - static_cast<std::int32_t>(kSmallMax) +
+                              static_cast<std::int32_t>(gl * kSeg);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const std::int32_t before = -(off0 + 4 * k);
+      const std::uint32_t sh = static_cast<std::uint32_t>(before < 0 ? 0 : (before > 4 ? 4 : before)) * 8u;
+      dw[k] &= static_cast<std::uint32_t>(0xFFFFFFFFull << sh);
+    }
+    Reg p{0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) slice4(lds, p, dw[k], kc);
+    std::uint32_t v = lane_shift(lds, p.value(), kc);
+    const bool ok = m_idx[slot] != 0xFFFFFFFFu;
+    if (ok) {
+      const std::uint32_t init = a.init_raw ? a.init_raw[m_idx[slot]] : a.init_default;
+      const std::uint32_t hs0 = a.tabs->head_shift[n][gl], hs1 = a.tabs->head_shift[n][16u + gl];
+      v ^= (static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), gl, 1)) & hs0) ^
+           (static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), 16u + gl, 1)) & hs1);
+    }
+    v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v ^= __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v ^= __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    v ^= __builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, false);  // row_mirror: row sum in all 16 lanes
+    if (ok && gl == 15u) a.out[m_idx[slot]] = v ^ a.out_xor;
+  };
+
+  // prologue: descriptors of steps t0..t0+3, data of steps t0, t0+1
+#pragma unroll
+  for (int k = 0; k < RING; ++k) fetch(t0 + k, k);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    issue(k);
+    fetch(t0 + k + RING, k);
+  }
+  for (std::uint32_t t = t0; t < t1; t += RING) {
+#pragma unroll
+    for (int k = 0; k < RING; ++k) {
+      const int ahead = (k + 2) % RING;  // step t+k+2: its descriptor arrived RING steps ago
+      issue(ahead);
+      fetch(t + k + 2 + RING, ahead);
+      if (t + k < t1) fold(k);
     }
   }
 }
@@ -820,7 +949,7 @@ __device__ __forceinline__ void crc_fixup_body(const RowsArgs& a) {
       acc ^= shift_rows(a.tabs, t.partial, t.rows_after);
       after = t.rows_after;
     }
-    a.out[s.block] = acc ^ a.out_xor;
+    a.out[a.out_idx ? a.out_idx[s.block] : s.block] = acc ^ a.out_xor;
   }
 }
 

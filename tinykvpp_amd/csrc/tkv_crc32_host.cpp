@@ -25,8 +25,10 @@ namespace tkv {
 hipError_t launch_rows(const RowsArgs& a, bool aligned, bool uniform, unsigned grid, hipStream_t st);
 hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
 hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st);
-hipError_t launch_prepass(const std::uint32_t* lengths, std::uint32_t n, std::uint32_t* row_scan,
-                          std::uint32_t* tile_sums, std::uint32_t* wave_start, std::uint32_t W, hipStream_t st);
+hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
+                          std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
+                          std::uint32_t W, hipStream_t st);
+hipError_t launch_small(const RowsArgs& a, unsigned grid, hipStream_t st);
 std::uint32_t prepass_tiles(std::uint32_t n);
 hipError_t launch_fill_uniform(std::uint8_t* dst, std::uint64_t stride, std::uint64_t len, std::uint64_t first,
                                std::uint64_t nblocks, std::uint64_t seed, hipStream_t st);
@@ -119,9 +121,13 @@ int hip_fail(hipError_t e, const char* what) {
 // written and read by kernels of that stream only).
 struct StreamScratch {
   Seam* seams = nullptr;
-  std::uint32_t* row_scan = nullptr;
-  std::uint32_t* tiles = nullptr;
   std::uint32_t* wave_start = nullptr;
+  std::uint32_t* counts = nullptr;
+  // irregular prepass, sized for cap_blocks blocks (one allocation, carved below)
+  void* blob = nullptr;
+  std::uint64_t* scan = nullptr;
+  std::uint64_t* tiles = nullptr;
+  PrepassOut po{};
   std::uint64_t cap_blocks = 0;
 };
 
@@ -252,21 +258,36 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     slot.reset(new StreamScratch());
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->seams), sizeof(Seam) * 2 * c->W));
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->wave_start), sizeof(std::uint32_t) * c->W));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->counts), sizeof(std::uint32_t) * 4));
   }
   StreamScratch* s = slot.get();
   if (nblocks > s->cap_blocks) {
-    std::uint64_t cap = std::max<std::uint64_t>(nblocks, 2 * s->cap_blocks);
-    if (s->row_scan) {
+    const std::uint64_t cap = std::max<std::uint64_t>(nblocks, 2 * s->cap_blocks);
+    if (s->blob) {
       // Freed blocks may still be in use by earlier work on this stream.
       TKV_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-      TKV_HIP(hipFree(s->row_scan));
-      TKV_HIP(hipFree(s->tiles));
+      TKV_HIP(hipFree(s->blob));
+      s->blob = nullptr;
+      s->cap_blocks = 0;
     }
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&s->row_scan), sizeof(std::uint32_t) * (cap + 1)));
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&s->tiles),
-                      sizeof(std::uint32_t) * (prepass_tiles(static_cast<std::uint32_t>(cap)) + 1)));
+    const std::uint64_t ntiles = prepass_tiles(static_cast<std::uint32_t>(cap)) + 1;
+    // 8-byte arrays first: scan, tiles, s_off, big_off; then the 4-byte ones
+    const std::uint64_t bytes = 8 * (cap + ntiles + 2 * cap) + 4 * (5 * cap + 1);
+    TKV_HIP(hipMalloc(&s->blob, bytes));
+    auto* p8 = static_cast<std::uint64_t*>(s->blob);
+    s->scan = p8;
+    s->tiles = p8 + cap;
+    s->po.s_off = p8 + cap + ntiles;
+    s->po.big_off = p8 + 2 * cap + ntiles;
+    auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 3 * cap + ntiles);
+    s->po.s_len = p4;
+    s->po.s_idx = p4 + cap;
+    s->po.big_len = p4 + 2 * cap;
+    s->po.big_idx = p4 + 3 * cap;
+    s->po.row_scan = p4 + 4 * cap;  // cap + 1 entries
     s->cap_blocks = cap;
   }
+  s->po.wave_start = s->wave_start;
   *out = s;
   return TKV_OK;
 }
@@ -331,15 +352,21 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   if (int rc = get_scratch(c, st, n, &s)) return rc;
   RowsArgs a = base_args(c, s, algo);
   a.base = d_base;
-  a.offsets = d_off;
-  a.lengths = d_len;
-  a.row_scan = s->row_scan;
+  a.offsets = s->po.big_off;  // the row kernel walks the compacted large blocks
+  a.lengths = s->po.big_len;
+  a.out_idx = s->po.big_idx;
+  a.row_scan = s->po.row_scan;
   a.wave_start = s->wave_start;
+  a.counts = s->counts;
+  a.s_off = s->po.s_off;
+  a.s_len = s->po.s_len;
+  a.s_idx = s->po.s_idx;
   a.init_raw = d_init;
   a.out = d_out;
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = static_cast<std::uint32_t>(c->ncu) * kRowsWavesPerWG;
-  TKV_HIP(launch_prepass(d_len, a.nblocks, s->row_scan, s->tiles, s->wave_start, a.nwaves, st));
+  TKV_HIP(launch_prepass(d_off, d_len, a.nblocks, s->scan, s->tiles, s->counts, s->po, a.nwaves, st));
+  TKV_HIP(launch_small(a, static_cast<unsigned>(c->ncu), st));
   TKV_HIP(launch_rows(a, false, false, static_cast<unsigned>(c->ncu), st));
   TKV_HIP(launch_fixup(a, st));
   return TKV_OK;

@@ -86,7 +86,31 @@ struct RowsArgs {
   std::uint32_t nwaves;
   std::uint32_t snap_blocks;         // uniform: partition by whole blocks (no seams)
   std::uint32_t* wg_ctr;             // packed: one work counter per workgroup, kCtrStride words apart
+  // irregular batches after the prepass split: `offsets`/`lengths` then list the
+  // large blocks only (compacted), out_idx maps a compacted block to its batch index, and the small
+  // blocks (len <= kSmallMax) are listed in s_off/s_len/s_idx for crc_small.
+  const std::uint32_t* out_idx;      // nullable: result of compacted block k goes to out[out_idx[k]]
+  const std::uint32_t* counts;       // device: [0] large blocks, [1] small blocks, [2] rows of large blocks
+  const std::uint64_t* s_off;
+  const std::uint32_t* s_len;
+  const std::uint32_t* s_idx;
 };
+
+// Outputs of the irregular prepass (scratch of one stream).
+struct PrepassOut {
+  std::uint64_t* s_off;
+  std::uint32_t* s_len;
+  std::uint32_t* s_idx;
+  std::uint64_t* big_off;
+  std::uint32_t* big_len;
+  std::uint32_t* big_idx;
+  std::uint32_t* row_scan;
+  std::uint32_t* wave_start;
+};
+
+// Blocks of at most kSmallMax bytes are folded four to a wave (16 lanes x 64 B each) by crc_small
+// instead of occupying a whole 4 KiB row each.
+constexpr std::uint32_t kSmallMax = 1024;
 
 // Packed kernel work counters: one per workgroup, each on its own 128-byte line.
 constexpr std::uint32_t kCtrStride = 32;

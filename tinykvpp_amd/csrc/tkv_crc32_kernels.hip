@@ -56,73 +56,108 @@ __global__ __launch_bounds__(kThreads) void crc_packed(RowsArgs a) {
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 
+__global__ __launch_bounds__(kRowsThreads) void crc_small(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  if (dev::sload32(a.counts, 1) == 0) return;  // no small blocks: skip the table fill
+  dev::crc_small_body(a, lds);
+}
+
 }  // namespace
 
-// ---- irregular-batch prepass: rows per block, exclusive scan, first block of every wave ------------
+// ---- irregular-batch prepass -----------------------------------------------------------------------
+// One exclusive scan over the blocks of the pair (small blocks, rows of large blocks), packed in a
+// u64 (small count in the low word, rows in the high word), then a scatter that
+//   * lists small blocks (len <= kSmallMax) in s_off/s_len/s_idx for crc_small,
+//   * compacts large blocks into big_off/big_len/big_idx with their row offsets (row_scan) for the
+//     row kernel, and records the first large block of every row-kernel wave (wave_start),
+//   * leaves counts = {large blocks, small blocks, rows of large blocks}.
 constexpr int kScanTile = 4096;  // blocks per scan workgroup (1024 threads x 4)
 
+__device__ __forceinline__ std::uint64_t scan_item(std::uint32_t len) {
+  return len <= kSmallMax ? 1ull : static_cast<std::uint64_t>(rows_for_len(len)) << 32;
+}
+
 __global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint32_t* lengths, std::uint32_t n,
-                                                      std::uint32_t* row_scan, std::uint32_t* tile_sums) {
-  __shared__ std::uint32_t part[1024];
+                                                      std::uint64_t* scan, std::uint64_t* tile_sums) {
+  __shared__ std::uint64_t part[1024];
   const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * 4u;
-  std::uint32_t v[4], s = 0;
+  std::uint64_t v[4], s = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    v[i] = (base + i < n) ? rows_for_len(lengths[base + i]) : 0u;
+    v[i] = (base + i < n) ? scan_item(lengths[base + i]) : 0ull;
     s += v[i];
   }
   part[threadIdx.x] = s;
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan of thread sums
-    const std::uint32_t x = threadIdx.x >= static_cast<unsigned>(off) ? part[threadIdx.x - off] : 0u;
+    const std::uint64_t x = threadIdx.x >= static_cast<unsigned>(off) ? part[threadIdx.x - off] : 0ull;
     __syncthreads();
     part[threadIdx.x] += x;
     __syncthreads();
   }
-  std::uint32_t run = part[threadIdx.x] - s;  // exclusive
+  std::uint64_t run = part[threadIdx.x] - s;  // exclusive
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    if (base + i < n) row_scan[base + i] = run;
+    if (base + i < n) scan[base + i] = run;
     run += v[i];
   }
   if (threadIdx.x == 1023) tile_sums[blockIdx.x] = part[1023];
 }
 
-__global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint32_t* tile_sums, std::uint32_t ntiles,
-                                                       std::uint32_t* row_scan, std::uint32_t n) {
-  __shared__ std::uint32_t part[1024];
-  std::uint32_t carry = 0;
+__global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums, std::uint32_t ntiles,
+                                                       std::uint32_t n, std::uint32_t* counts) {
+  __shared__ std::uint64_t part[1024];
+  std::uint64_t carry = 0;
   for (std::uint32_t t0 = 0; t0 < ntiles; t0 += 1024) {
     const std::uint32_t i = t0 + threadIdx.x;
-    const std::uint32_t x = i < ntiles ? tile_sums[i] : 0u;
+    const std::uint64_t x = i < ntiles ? tile_sums[i] : 0ull;
     part[threadIdx.x] = x;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {
-      const std::uint32_t y = threadIdx.x >= static_cast<unsigned>(off) ? part[threadIdx.x - off] : 0u;
+      const std::uint64_t y = threadIdx.x >= static_cast<unsigned>(off) ? part[threadIdx.x - off] : 0ull;
       __syncthreads();
       part[threadIdx.x] += y;
       __syncthreads();
     }
     if (i < ntiles) tile_sums[i] = carry + part[threadIdx.x] - x;  // exclusive tile offset
-    const std::uint32_t tot = part[1023];
+    const std::uint64_t tot = part[1023];
     __syncthreads();
     carry += tot;
   }
-  if (threadIdx.x == 0) row_scan[n] = carry;  // total rows
+  if (threadIdx.x == 0) {
+    const std::uint32_t ns = static_cast<std::uint32_t>(carry);
+    counts[0] = n - ns;                                // large blocks
+    counts[1] = ns;                                    // small blocks
+    counts[2] = static_cast<std::uint32_t>(carry >> 32);  // rows of the large blocks
+  }
 }
 
-__global__ void rows_finish(const std::uint32_t* lengths, std::uint32_t n, std::uint32_t* row_scan,
-                            const std::uint32_t* tile_offs, std::uint32_t* wave_start, std::uint32_t W) {
+__global__ void rows_finish(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
+                            const std::uint64_t* scan, const std::uint64_t* tile_offs, const std::uint32_t* counts,
+                            PrepassOut o, std::uint32_t W) {
   const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
   if (b >= n) return;
-  const std::uint64_t lo = row_scan[b] + tile_offs[b / kScanTile];
-  row_scan[b] = static_cast<std::uint32_t>(lo);
-  const std::uint64_t hi = lo + rows_for_len(lengths[b]);
-  const std::uint64_t TR = row_scan[n];
+  const std::uint64_t e = scan[b] + tile_offs[b / kScanTile];
+  const std::uint32_t len = lengths[b];
+  const std::uint32_t nsmall = static_cast<std::uint32_t>(e);
+  if (len <= kSmallMax) {
+    o.s_off[nsmall] = offsets[b];
+    o.s_len[nsmall] = len;
+    o.s_idx[nsmall] = static_cast<std::uint32_t>(b);
+    return;
+  }
+  const std::uint32_t k = static_cast<std::uint32_t>(b) - nsmall;  // compacted index
+  const std::uint64_t lo = e >> 32;
+  o.big_off[k] = offsets[b];
+  o.big_len[k] = len;
+  o.big_idx[k] = static_cast<std::uint32_t>(b);
+  o.row_scan[k] = static_cast<std::uint32_t>(lo);
+  const std::uint64_t hi = lo + rows_for_len(len);
+  const std::uint64_t TR = counts[2];
   // waves whose first row g0(w) = floor(w*TR/W) lies in [lo, hi): w in [ceil(lo*W/TR), ceil(hi*W/TR))
   const std::uint64_t wlo = (lo * W + TR - 1) / TR;
   const std::uint64_t whi = (hi * W + TR - 1) / TR;
-  for (std::uint64_t w = wlo; w < whi && w < W; ++w) wave_start[w] = static_cast<std::uint32_t>(b);
+  for (std::uint64_t w = wlo; w < whi && w < W; ++w) o.wave_start[w] = k;
 }
 
 // ---- synthetic data: byte j of block b = LE byte j%8 of
@@ -212,13 +247,19 @@ hipError_t launch_fixup(const RowsArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_prepass(const std::uint32_t* lengths, std::uint32_t n, std::uint32_t* row_scan,
-                          std::uint32_t* tile_sums, std::uint32_t* wave_start, std::uint32_t W, hipStream_t st) {
+hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
+                          std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
+                          std::uint32_t W, hipStream_t st) {
   const std::uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
-  hipLaunchKernelGGL(rows_tile_scan, dim3(ntiles), dim3(1024), 0, st, lengths, n, row_scan, tile_sums);
-  hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, ntiles, row_scan, n);
-  hipLaunchKernelGGL(rows_finish, dim3((n + 255) / 256), dim3(256), 0, st, lengths, n, row_scan, tile_sums,
-                     wave_start, W);
+  hipLaunchKernelGGL(rows_tile_scan, dim3(ntiles), dim3(1024), 0, st, lengths, n, scan, tile_sums);
+  hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, ntiles, n, counts);
+  hipLaunchKernelGGL(rows_finish, dim3((n + 255) / 256), dim3(256), 0, st, offsets, lengths, n, scan, tile_sums,
+                     counts, o, W);
+  return hipGetLastError();
+}
+
+hipError_t launch_small(const RowsArgs& a, unsigned grid, hipStream_t st) {
+  hipLaunchKernelGGL(crc_small, dim3(grid), dim3(kRowsThreads), 0, st, a);
   return hipGetLastError();
 }
 

@@ -287,16 +287,21 @@ const IV kIrr[] = {
     {"irr T768 D4 I2", 768, LI<4, 2, 768>}, {"irr T512 D8 I4", 512, LI<8, 4, 512>},
 };
 constexpr int kNIrr = sizeof(kIrr) / sizeof(kIrr[0]);
-std::uint32_t* g_scan = nullptr;
-std::uint32_t* g_tiles = nullptr;
+void* g_blob = nullptr;
+std::uint64_t* g_scan64 = nullptr;
+std::uint64_t* g_tiles64 = nullptr;
 std::uint32_t* g_wstart = nullptr;
+std::uint32_t* g_counts = nullptr;
+PrepassOut g_po{};
 std::uint64_t g_cap = 0;
 }  // namespace
 
 namespace tkv {
 hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
-hipError_t launch_prepass(const std::uint32_t* lengths, std::uint32_t n, std::uint32_t* row_scan,
-                          std::uint32_t* tile_sums, std::uint32_t* wave_start, std::uint32_t W, hipStream_t st);
+hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
+                          std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
+                          std::uint32_t W, hipStream_t st);
+hipError_t launch_small(const RowsArgs& a, unsigned grid, hipStream_t st);
 }  // namespace tkv
 
 extern "C" int explore_count() { return kNV + 1; }
@@ -360,20 +365,36 @@ extern "C" int explore_run_irr(int v, const std::uint8_t* base, const std::uint6
     if (explore_run(kNV, base, 0, 16, out, stream)) return 1;  // one-time init of tables etc.
   }
   if (n > g_cap) {
-    hipFree(g_scan);
-    hipFree(g_tiles);
-    hipFree(g_wstart);
-    hipMalloc(&g_scan, 4 * (n + 1));
-    hipMalloc(&g_tiles, 4 * (n / 4096 + 2));
-    hipMalloc(&g_wstart, 4 * g_ncu * 16);
+    hipFree(g_blob);
+    const std::uint64_t nt = n / 4096 + 2;
+    hipMalloc(&g_blob, 8 * (n + nt + 2 * n) + 4 * (5 * n + 1));
+    auto* p8 = static_cast<std::uint64_t*>(g_blob);
+    g_scan64 = p8;
+    g_tiles64 = p8 + n;
+    g_po.s_off = p8 + n + nt;
+    g_po.big_off = p8 + 2 * n + nt;
+    auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 3 * n + nt);
+    g_po.s_len = p4;
+    g_po.s_idx = p4 + n;
+    g_po.big_len = p4 + 2 * n;
+    g_po.big_idx = p4 + 3 * n;
+    g_po.row_scan = p4 + 4 * n;
+    if (!g_wstart) hipMalloc(&g_wstart, 4 * g_ncu * 16);
+    if (!g_counts) hipMalloc(&g_counts, 16);
+    g_po.wave_start = g_wstart;
     g_cap = n;
   }
   RowsArgs a{};
   a.base = base;
-  a.offsets = off;
-  a.lengths = len;
-  a.row_scan = g_scan;
+  a.offsets = g_po.big_off;
+  a.lengths = g_po.big_len;
+  a.out_idx = g_po.big_idx;
+  a.row_scan = g_po.row_scan;
   a.wave_start = g_wstart;
+  a.counts = g_counts;
+  a.s_off = g_po.s_off;
+  a.s_len = g_po.s_len;
+  a.s_idx = g_po.s_idx;
   a.init_default = 0xFFFFFFFFu;
   a.out_xor = 0xFFFFFFFFu;
   a.out = out;
@@ -382,7 +403,10 @@ extern "C" int explore_run_irr(int v, const std::uint8_t* base, const std::uint6
   a.dummy = g_dummy;
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = g_ncu * (kIrr[v].threads / 64);
-  launch_prepass(len, a.nblocks, g_scan, g_tiles, g_wstart, a.nwaves, st);
+  launch_prepass(off, len, a.nblocks, g_scan64, g_tiles64, g_counts, g_po, a.nwaves, st);
+  RowsArgs as = a;
+  as.nwaves = g_ncu * kRowsWavesPerWG;  // crc_small runs at the product shape
+  launch_small(as, g_ncu, st);
   kIrr[v].launch(a, st);
   launch_fixup(a, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
