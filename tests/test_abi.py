@@ -245,3 +245,25 @@ def test_wave_start_partition(W):
             if g0 < g1:
                 b = starts[w]
                 assert rs[b] <= g0 < rs[b + 1]
+
+
+def test_model_small_block_groups(model, oracle):
+    """crc_small's arithmetic (kSmallMax = 1 KiB): a block of n <= 1024 bytes right-aligned in a
+    1 KiB mini-row, 16 lanes x 64 B, lane g shifted with the LS entry of lane 48 + g, and the init
+    term spread over the group as two bits per lane with head_shift[n]."""
+    rng = np.random.default_rng(12)
+    for n in [0, 1, 3, 4, 17, 63, 64, 65, 500, 1023, 1024]:
+        data = rng.integers(0, 256, n, dtype=np.uint8)
+        init = int(rng.integers(0, 2**32))
+        img = np.zeros(1024, np.uint8)
+        img[1024 - n:] = data
+        # the model's slicing runs on 64 lanes of 64 B: put the mini-row in lanes 48..63
+        row = np.zeros(ROW, np.uint8)
+        row[ROW - 1024:] = img
+        p = model.slice_lanes(row)[48:]
+        v = 0
+        for g in range(16):
+            for j in range(8):
+                v ^= int(model.lane[j][(p[g] >> (4 * j)) & 15, 48 + g])
+            v ^= bits_dot(init & (1 << g), model.head[n]) ^ bits_dot(init & (1 << (16 + g)), model.head[n])
+        assert v ^ 0xFFFFFFFF == oracle.update(init, data.tobytes()) ^ 0xFFFFFFFF
