@@ -276,7 +276,10 @@ __device__ __forceinline__ void finish_row(const RowsArgs& a, const Cursor& c, s
                                            WaveState& st) {
   const bool lo_half = lane < 32u;
   std::uint32_t init = 0;
-  if (c.r == 0) init = a.init_raw ? sload32(a.init_raw, c.b) : a.init_default;
+  if (c.r == 0) {
+    // per-block init of a compacted large block: its batch index is out_idx[c.b]
+    init = a.init_raw ? sload32(a.init_raw, a.out_idx ? sload32(a.out_idx, c.b) : c.b) : a.init_default;
+  }
   std::uint32_t hk = hcon;
   if constexpr (!UNIFORM) hk = lo_half ? hcon : hs;
   // lanes 0..31: bit l of B times Shift_4096(1<<l); lanes 32..63 on a head row: bit l-32 of init
@@ -311,6 +314,9 @@ __device__ __forceinline__ void finish_row(const RowsArgs& a, const Cursor& c, s
   }
 }
 
+// Small blocks of an irregular batch (defined below; runs inside the irregular row kernel).
+__device__ __forceinline__ void small_phase(const RowsArgs& a, std::uint32_t* lds);
+
 // Fill the 160 KiB LDS table image (slicing tables replicated 32x, lane-shift nibble tables).
 __device__ __forceinline__ void fill_lds(const DeviceTables* tabs, std::uint32_t* lds) {
   for (std::uint32_t i = threadIdx.x; i < kLdsSliceWords; i += blockDim.x) {
@@ -336,6 +342,7 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
     if (lane >= 32u) hcon = multmodp(a.head_z, 1u << (lane - 32u), a.tabs->poly);  // Shift_h(1 << (l-32))
   }
   __syncthreads();
+  if constexpr (!UNIFORM && MODE == 0) small_phase(a, lds);  // the batch's small blocks first
 
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint64_t W = a.nwaves;
@@ -468,14 +475,14 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
 // per lane: bit_i(init) * Shift_len(1 << i)), and the first four DPP steps of the wave reduction
 // sum each 16-lane row. Waves own contiguous ranges of steps (4 blocks per step). Pipeline: data of
 // step t+2 is issued while step t folds; descriptors are fetched 4 steps ahead of their data.
-__device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t* lds) {
+// The tables must already be in LDS (fill_lds + barrier). Runs inside the irregular row kernel,
+// before its rows, on the same partition of waves.
+__device__ __forceinline__ void small_phase(const RowsArgs& a, std::uint32_t* lds) {
   constexpr int RING = 4;
-  fill_lds(a.tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
   const std::uint32_t grp = lane >> 4, gl = lane & 15u;
   LaneConst kc = lane_const(lane);
   kc.lsbase = kLdsLaneBase + (48u + gl) * 4u;
-  __syncthreads();
 
   const std::uint32_t NS = sload32(a.counts, 1);
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -490,20 +497,21 @@ __device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t*
   // descriptor ring (slot = step % RING): byte offset, length, batch index; kept valid-masked
   std::uint64_t d_off[RING];
   std::uint32_t d_len[RING], d_idx[RING];
+  auto step_ok = [&](std::uint32_t t) { return t < t1 && 4u * t + grp < NS; };
   auto fetch = [&](std::uint32_t t, int slot) {
-    const std::uint32_t j = 4u * t + grp;
-    const bool ok = t < t1 && j < NS;
-    const std::uint32_t jj = ok ? j : 0u;
-    d_off[slot] = ok ? a.s_off[jj] : 0ull;
-    d_len[slot] = ok ? a.s_len[jj] : 0u;
-    d_idx[slot] = ok ? a.s_idx[jj] : 0xFFFFFFFFu;
+    // unconditional loads (index clamped), results left untouched until issue() uses them four
+    // steps later: any branch or select on them here would make the compiler wait for them now
+    const std::uint32_t jj = step_ok(t) ? 4u * t + grp : 0u;
+    d_off[slot] = a.s_off[jj];
+    d_len[slot] = a.s_len[jj];
+    d_idx[slot] = a.s_idx[jj];
   };
   // data ring: five 16-byte pieces covering the lane's segment, plus what the fold step needs
   uint4 q[RING][5];
-  std::uint32_t m_len[RING], m_idx[RING], m_end[RING];
-  auto issue = [&](int slot) {
-    const std::uint32_t n = d_len[slot];
-    const bool ok = d_idx[slot] != 0xFFFFFFFFu;
+  std::uint32_t m_len[RING], m_idx[RING], m_end[RING], m_hs0[RING], m_hs1[RING], m_init[RING];
+  auto issue = [&](int slot, std::uint32_t t) {
+    const bool ok = step_ok(t);
+    const std::uint32_t n = ok ? d_len[slot] : 0u;
     const std::uintptr_t blo = base + d_off[slot];
     const std::uintptr_t bhi = blo + n;
     const std::uintptr_t seg = static_cast<std::uintptr_t>(static_cast<std::int64_t>(bhi) - static_cast<std::int64_t>(kSmallMax)) +
@@ -515,8 +523,14 @@ __device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t*
       q[slot][i] = gload16(ok && (p + 16 > blo) && (p < bhi) ? p : dmy);
     }
     m_len[slot] = n;
-    m_idx[slot] = d_idx[slot];
+    m_idx[slot] = ok ? d_idx[slot] : 0xFFFFFFFFu;
     m_end[slot] = static_cast<std::uint32_t>(bhi & 15u);
+    // init-term operands travel with the data (loaded now, used two steps later)
+    const std::uint32_t nn = ok ? n : 0u;
+    m_hs0[slot] = a.tabs->head_shift[nn][gl];
+    m_hs1[slot] = a.tabs->head_shift[nn][16u + gl];
+    m_init[slot] = a.init_default;
+    if (a.init_raw) m_init[slot] = a.init_raw[m_idx[slot] != 0xFFFFFFFFu ? m_idx[slot] : 0u];
   };
   auto fold = [&](int slot) {
     const std::uint32_t n = m_len[slot];
@@ -553,12 +567,9 @@ __device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t*
     for (int k = 0; k < 16; ++k) slice4(lds, p, dw[k], kc);
     std::uint32_t v = lane_shift(lds, p.value(), kc);
     const bool ok = m_idx[slot] != 0xFFFFFFFFu;
-    if (ok) {
-      const std::uint32_t init = a.init_raw ? a.init_raw[m_idx[slot]] : a.init_default;
-      const std::uint32_t hs0 = a.tabs->head_shift[n][gl], hs1 = a.tabs->head_shift[n][16u + gl];
-      v ^= (static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), gl, 1)) & hs0) ^
-           (static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), 16u + gl, 1)) & hs1);
-    }
+    const std::uint32_t init = ok ? m_init[slot] : 0u;
+    v ^= (static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), gl, 1)) & m_hs0[slot]) ^
+         (static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), 16u + gl, 1)) & m_hs1[slot]);
     v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
     v ^= __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
     v ^= __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
@@ -571,18 +582,24 @@ __device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t*
   for (int k = 0; k < RING; ++k) fetch(t0 + k, k);
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    issue(k);
+    issue(k, t0 + k);
     fetch(t0 + k + RING, k);
   }
   for (std::uint32_t t = t0; t < t1; t += RING) {
 #pragma unroll
     for (int k = 0; k < RING; ++k) {
       const int ahead = (k + 2) % RING;  // step t+k+2: its descriptor arrived RING steps ago
-      issue(ahead);
+      issue(ahead, t + k + 2);
       fetch(t + k + 2 + RING, ahead);
       if (t + k < t1) fold(k);
     }
   }
+}
+
+__device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t* lds) {
+  fill_lds(a.tabs, lds);
+  __syncthreads();
+  small_phase(a, lds);
 }
 
 // Packed uniform fast path: block b = [base + b*len, +len) with len a multiple of kRow (4 KiB) and

@@ -366,7 +366,6 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = static_cast<std::uint32_t>(c->ncu) * kRowsWavesPerWG;
   TKV_HIP(launch_prepass(d_off, d_len, a.nblocks, s->scan, s->tiles, s->counts, s->po, a.nwaves, st));
-  TKV_HIP(launch_small(a, static_cast<unsigned>(c->ncu), st));
   TKV_HIP(launch_rows(a, false, false, static_cast<unsigned>(c->ncu), st));
   TKV_HIP(launch_fixup(a, st));
   return TKV_OK;

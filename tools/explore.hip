@@ -404,9 +404,6 @@ extern "C" int explore_run_irr(int v, const std::uint8_t* base, const std::uint6
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = g_ncu * (kIrr[v].threads / 64);
   launch_prepass(off, len, a.nblocks, g_scan64, g_tiles64, g_counts, g_po, a.nwaves, st);
-  RowsArgs as = a;
-  as.nwaves = g_ncu * kRowsWavesPerWG;  // crc_small runs at the product shape
-  launch_small(as, g_ncu, st);
   kIrr[v].launch(a, st);
   launch_fixup(a, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;

@@ -1,0 +1,7 @@
+set -e
+R=$GRAFT_REPO_ROOT
+cd $R
+timeout -k 10 600 python3 -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 300 python3 bench.py --config cfg4 > gpurun_out/bench_cfg4.json 2> gpurun_out/bench_cfg4.err
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_cfg4 -o run -- python3 $R/bench.py --config cfg4 --no-cpu-baseline > $R/gpurun_out/prof_cfg4.log 2>&1
