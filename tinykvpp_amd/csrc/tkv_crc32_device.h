@@ -294,6 +294,12 @@ __device__ __forceinline__ void finish_row(const RowsArgs& a, const Cursor& c, s
     } else {
       // (explicit slots: a runtime index into these arrays would put them in scratch memory)
       const std::uint32_t flags = kSeamValid | (st.piece_has_row0 ? kSeamHasRow0 : 0u);
+      if (st.piece_has_row0) {
+        // head piece of a block cut between waves: seed its result with xorout; crc_fixup XORs
+        // every piece's shifted partial into it (this kernel precedes crc_fixup on the stream)
+        const std::uint32_t ob = a.out_idx ? sload32(a.out_idx, c.b) : c.b;
+        if (lane == 0) a.out[ob] = a.out_xor;
+      }
       if (st.first_piece) {
         st.s_block[0] = c.b;
         st.s_part[0] = Bn;
@@ -950,24 +956,18 @@ __device__ __forceinline__ void crc_packed_dyn_body(const RowsArgs& a, std::uint
   }
 }
 
-// Combine the partials of blocks that were split between waves. One thread per wave; the thread
-// whose wave holds a block's head row walks the following waves' first pieces.
+// Combine the partials of blocks that were split between waves: one thread per seam record (two
+// per wave) shifts its piece's partial past the rows that follow it in the block and XORs it into
+// the block's result, which the head piece seeded with xorout. All pieces of a block combine in
+// parallel (a block cut across thousands of waves - one huge span - costs one atomic each).
 __device__ __forceinline__ void crc_fixup_body(const RowsArgs& a) {
-  const std::uint64_t w = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
-  if (w >= a.nwaves) return;
-  for (int slot = 0; slot < 2; ++slot) {
-    const Seam s = a.seams[2 * w + slot];
-    if ((s.flags & kSeamValid) == 0 || (s.flags & kSeamHasRow0) == 0) continue;
-    std::uint32_t acc = shift_rows(a.tabs, s.partial, s.rows_after);
-    std::uint32_t after = s.rows_after;
-    for (std::uint64_t ww = w + 1; after != 0 && ww < a.nwaves; ++ww) {
-      const Seam t = a.seams[2 * ww];
-      if ((t.flags & kSeamValid) == 0) continue;  // wave with an empty row range
-      acc ^= shift_rows(a.tabs, t.partial, t.rows_after);
-      after = t.rows_after;
-    }
-    a.out[a.out_idx ? a.out_idx[s.block] : s.block] = acc ^ a.out_xor;
-  }
+  const std::uint64_t i = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+  if (i >= 2ull * a.nwaves) return;
+  const Seam s = a.seams[i];
+  if ((s.flags & kSeamValid) == 0) return;
+  const std::uint32_t contrib = shift_rows(a.tabs, s.partial, s.rows_after);
+  const std::uint64_t ob = a.out_idx ? a.out_idx[s.block] : s.block;
+  __hip_atomic_fetch_xor(a.out + ob, contrib, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace dev

@@ -242,7 +242,7 @@ hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st) {
 }
 
 hipError_t launch_fixup(const RowsArgs& a, hipStream_t st) {
-  const unsigned grid = (a.nwaves + 255u) / 256u;
+  const unsigned grid = (2u * a.nwaves + 255u) / 256u;  // one thread per seam record
   hipLaunchKernelGGL(crc_fixup, dim3(grid), dim3(256), 0, st, a);
   return hipGetLastError();
 }

@@ -170,11 +170,14 @@ def lat(fn, reps=200):
     return (time.perf_counter() - t0) / reps * 1e6
 
 
-for nbytes in (36, 4096, 65536, 1 << 20):
-    payload = rng.bytes(nbytes)
-    c = tk.crc32()
-    us = lat(lambda: c.update(payload))
-    print(json.dumps({"row": "update_latency", "bytes": nbytes, "us_per_call": round(us, 2)}), flush=True)
+res = ctypes.c_uint32()
+for nbytes in (36, 4096, 65536, 262144, 1 << 20, 16 << 20):
+    payload = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    us = lat(lambda: tk.check(lib.tkv_crc32_update(0xFFFFFFFF, ctypes.c_void_p(payload.ctypes.data), nbytes,
+                                                   ctypes.byref(res))), reps=50)
+    ok = (res.value ^ 0xFFFFFFFF) == ora.crc(payload.tobytes())
+    print(json.dumps({"row": "update_latency", "bytes": nbytes, "us_per_call": round(us, 2), "bit_exact": ok}),
+          flush=True)
 for nrec in (1, 16, 256, 4096):
     recs = np.ascontiguousarray(wal[:int(offs[nrec])]) if nrec < n_rec else wal
     o = offs[:nrec].copy()

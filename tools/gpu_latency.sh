@@ -1,5 +1,4 @@
 set -e
 cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python3 -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
 timeout -k 10 400 python3 tools/bench_formats.py > gpurun_out/bench_formats.jsonl 2> gpurun_out/bench_formats.err
 TKV_UPDATE_SMALL_BYTES=0 timeout -k 10 400 python3 tools/bench_formats.py > gpurun_out/bench_formats_nosmall.jsonl 2>> gpurun_out/bench_formats.err
