@@ -154,11 +154,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # One rank per GPU. TKV_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices
+    # round-robin); the default, nccl (RCCL), carries only the barrier and the timing max-reduce.
+    backend = os.environ.get("TKV_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     tk.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     nblocks, blen, desc = CONFIGS[args.config]
     first, nblocks = rank_shard(rank, nblocks)
@@ -222,7 +230,8 @@ def main():
     if world == 1 and g["nblocks"] == nblocks:  # the whole config on this GPU: golden aggregate
         bit_exact = bit_exact and int(np.bitwise_xor.reduce(crcs)) == g["xor"]
     if world > 1:
-        elapsed, kernel_ms, bit_exact = reduce_timing(elapsed, kernel_ms, bit_exact, dist, dev)
+        elapsed, kernel_ms, bit_exact = reduce_timing(elapsed, kernel_ms, bit_exact, dist,
+                                                      dev if backend == "nccl" else None)
 
     bytes_per_step = total
     total_bytes = bytes_per_step * args.steps * world
