@@ -20,6 +20,7 @@ ap.add_argument("--gib", type=float, default=4.0)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--only", default="")
+ap.add_argument("--zero", action="store_true", help="zero-filled buffer (data-dependent power / clock probe)")
 ap.add_argument("--irregular", action="store_true", help="cfg4 Zipf batch through the irregular-kernel variants")
 a = ap.parse_args()
 
@@ -76,6 +77,8 @@ if a.irregular:
 n = int(a.gib * (1 << 30)) // a.len
 data = torch.empty(n * a.len, dtype=torch.uint8, device="cuda")
 tk.fill_synthetic_uniform(data, a.len, n)
+if a.zero:
+    data.zero_()
 ref = tk.crc32_batch_uniform(data, a.len, n).clone()
 out = torch.empty(n, dtype=torch.int32, device="cuda")
 st = torch.cuda.current_stream()
