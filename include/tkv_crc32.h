@@ -173,6 +173,10 @@ uint32_t tkv_debug_multmodp(uint32_t a, uint32_t b);
 size_t tkv_debug_wal_chain(const uint8_t *h_wal, uint64_t size, uint64_t *out_pos, size_t cap, uint64_t *end,
                            int *err);
 uint32_t tkv_debug_x8nmodp(uint64_t nbytes);
+/* Host batches from pinned host memory are read in place by the kernels (zero copy) unless this is
+ * 0 (then they take the staged copy pipeline, as pageable memory does). Returns the previous
+ * setting. Default 1; the environment variable TKV_HOST_MAPPED=0 sets 0 at load time. */
+int tkv_debug_set_host_mapped(int enable);
 
 #ifdef __cplusplus
 }

@@ -292,6 +292,83 @@ def test_host_batch_block_larger_than_slab(gpu, oracle):
     assert [int(x) for x in got] == want
 
 
+def pinned_copy(a):
+    """numpy view of a pinned (hipHostMalloc) copy of ``a``: the kernels can read it in place."""
+    t = torch.empty(a.size, dtype=torch.uint8).pin_memory()
+    t.numpy()[:] = a
+    return t, t.numpy()
+
+
+@pytest.mark.parametrize("packed", [False, True])
+def test_host_batch_pinned_zero_copy(gpu, oracle, packed):
+    """Pinned sources are read in place by the kernels (no staging copy); results equal the staged
+    pipeline's and the oracle's, with and without per-block initial registers."""
+    rng = np.random.default_rng(21)
+    host, offs, lens = irregular_case(rng, 5000, 70000, packed=packed)
+    keep, pin = pinned_copy(host)
+    want = oracle.batch(host, offs, lens)
+    lib = tk.load_library()
+    assert lib.tkv_debug_set_host_mapped(1) == 1
+    got = tk.crc32_batch_host(pin, offs, lens)
+    assert np.array_equal(got, want)
+    init = rng.integers(0, 1 << 32, offs.size, dtype=np.uint64).astype(np.uint32)
+    want_i = oracle.batch(host, offs, lens, init)
+    assert np.array_equal(tk.crc32_batch_host(pin, offs, lens, init_raw=init), want_i)
+    assert lib.tkv_debug_set_host_mapped(0) == 1
+    try:
+        assert np.array_equal(tk.crc32_batch_host(pin, offs, lens, init_raw=init), want_i)
+    finally:
+        lib.tkv_debug_set_host_mapped(1)
+    assert np.array_equal(tk.crc32_batch_host(pin, offs, lens, devices=[0, 0]), want)
+    assert np.array_equal(tk.crc32_batch_host(pin, offs, lens, algo="crc32c"),
+                          tk.crc32_batch_host(host, offs, lens, algo="crc32c"))
+
+
+def test_host_batch_pinned_uniform_and_huge(gpu, oracle):
+    """Uniform contiguous pinned batches take the packed kernel in place; a block larger than a
+    staging slab is one block of the in-place irregular batch (no chaining)."""
+    n, blen = 5000, 65536  # 312.5 MiB: room for a block larger than a 256 MiB staging slab
+    dev = torch.empty(n * blen, dtype=torch.uint8, device="cuda")
+    tk.fill_synthetic_uniform(dev, blen, n, first_block=5)
+    keep = dev.cpu().pin_memory()
+    pin = keep.numpy()
+    want = np.zeros(n, np.uint32)
+    oracle.lib.oracle_crc_synthetic(1, 5, n, blen, want.ctypes.data)
+    offs = np.arange(n, dtype=np.uint64) * blen
+    assert np.array_equal(tk.crc32_batch_host(pin, offs, np.full(n, blen, np.uint32)), want)
+    big = (300 << 20) + 5
+    assert big <= pin.size
+    got = tk.crc32_batch_host(pin, [0, 7, 1 << 20], [big, 100, 4096])
+    assert [int(x) for x in got] == [oracle.crc(pin[:big].tobytes()), oracle.crc(pin[7:107].tobytes()),
+                                     oracle.crc(pin[1 << 20:(1 << 20) + 4096].tobytes())]
+
+
+def test_host_batch_registered_range_checked(gpu, oracle):
+    """Part of a pageable buffer pinned with hipHostRegister: a batch inside the registered range
+    may be read in place, one that leaves it must be staged (never read by the kernels past the
+    registration) - both give the oracle's CRCs."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    rng = np.random.default_rng(22)
+    big = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
+    page = 1 << 16
+    start = (-big.ctypes.data) % page
+    reg = big[start:start + (4 << 20)]  # registered window, page aligned
+    assert hip.hipHostRegister(reg.ctypes.data, reg.size, 0) == 0
+    try:
+        inside_o = np.array([0, 4096, (4 << 20) - 65536], np.uint64)
+        inside_l = np.array([4096, 100000, 65536], np.uint32)
+        assert np.array_equal(tk.crc32_batch_host(reg, inside_o, inside_l), oracle.batch(reg, inside_o, inside_l))
+        tail = big[start:]  # same base, but the last block runs past the registered window
+        out_o = np.array([0, (4 << 20) - 4096], np.uint64)
+        out_l = np.array([4096, 2 << 20], np.uint32)
+        assert np.array_equal(tk.crc32_batch_host(tail, out_o, out_l), oracle.batch(tail, out_o, out_l))
+    finally:
+        hip.hipHostUnregister(reg.ctypes.data)
+
+
 # ---- full-size BASELINE configs through golden aggregates ----------------------------------------
 
 def aggregates(crcs):

@@ -59,6 +59,7 @@ SIGNATURES = {
     "tkv_debug_tables_poly": (_sz, [_u32, _vp, _sz]),
     "tkv_debug_multmodp": (_u32, [_u32, _u32]),
     "tkv_debug_x8nmodp": (_u32, [_u64]),
+    "tkv_debug_set_host_mapped": (_int, [_int]),
     "tkv_debug_wal_chain": (_sz, [_u8p, _u64, _vp, _sz, ctypes.POINTER(_u64), ctypes.POINTER(_int)]),
 }
 

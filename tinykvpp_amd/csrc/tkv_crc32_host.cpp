@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -198,6 +199,57 @@ int pipe_init(HostPipe& p, std::size_t max_blocks) {
   return TKV_OK;
 }
 
+// Host batches the device can read in place (see mapped_view): no data staging at all. Only the
+// per-block metadata (offsets, lengths, initial registers, results) moves, in chunks of up to
+// kMapChunk blocks on two alternating streams so a chunk's metadata is prepared while the previous
+// chunk's kernels read the caller's bytes over PCIe.
+constexpr std::size_t kMapChunk = std::size_t(1) << 21;
+struct MapPipe {
+  hipStream_t st[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  std::uint64_t* h_off[2] = {nullptr, nullptr};
+  std::uint32_t* h_len[2] = {nullptr, nullptr};
+  std::uint32_t* h_init[2] = {nullptr, nullptr};
+  std::uint32_t* h_out[2] = {nullptr, nullptr};
+  std::uint64_t* d_off[2] = {nullptr, nullptr};
+  std::uint32_t* d_len[2] = {nullptr, nullptr};
+  std::uint32_t* d_init[2] = {nullptr, nullptr};
+  std::uint32_t* d_out[2] = {nullptr, nullptr};
+  std::size_t cap = 0;
+  ~MapPipe() {
+    for (int i = 0; i < 2; ++i) {
+      if (st[i]) (void)hipStreamSynchronize(st[i]);
+      if (done[i]) (void)hipEventDestroy(done[i]);
+      if (st[i]) (void)hipStreamDestroy(st[i]);
+      (void)hipHostFree(h_off[i]);
+      (void)hipHostFree(h_len[i]);
+      (void)hipHostFree(h_init[i]);
+      (void)hipHostFree(h_out[i]);
+      (void)hipFree(d_off[i]);
+      (void)hipFree(d_len[i]);
+      (void)hipFree(d_init[i]);
+      (void)hipFree(d_out[i]);
+    }
+  }
+};
+
+int map_pipe_init(MapPipe& p, std::size_t cap) {
+  p.cap = cap;
+  for (int i = 0; i < 2; ++i) {
+    TKV_HIP(hipStreamCreateWithFlags(&p.st[i], hipStreamNonBlocking));
+    TKV_HIP(hipEventCreateWithFlags(&p.done[i], hipEventDisableTiming));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_off[i]), cap * 8, hipHostMallocDefault));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_len[i]), cap * 4, hipHostMallocDefault));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_init[i]), cap * 4, hipHostMallocDefault));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&p.h_out[i]), cap * 4, hipHostMallocDefault));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&p.d_off[i]), cap * 8));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&p.d_len[i]), cap * 4));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&p.d_init[i]), cap * 4));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&p.d_out[i]), cap * 4));
+  }
+  return TKV_OK;
+}
+
 struct DevCtx {
   int dev = -1;
   int ncu = 0;
@@ -222,6 +274,7 @@ struct DevCtx {
   // host-memory batch pipeline, kept between calls (guarded by pipe_mu)
   std::mutex pipe_mu;
   std::unique_ptr<HostPipe> pipe;
+  std::unique_ptr<MapPipe> mpipe;  // zero-copy batches (guarded by pipe_mu)
 };
 
 std::mutex g_mu;
@@ -418,11 +471,118 @@ void copy_span(std::uint8_t* dst, const std::uint8_t* src, std::uint64_t n) {
   for (auto& t : th) t.join();
 }
 
+// Device view of the caller's host range [base + lo_byte, base + hi_byte) when the device can read
+// it in place: pinned host memory (hipHostMalloc, or hipHostRegister'd, mapped at the same address
+// on this device) or device memory, with the whole range inside one allocation. Else nullptr.
+// TKV_HOST_MAPPED=0 disables the zero-copy path (A/B measurements).
+std::atomic<int> g_host_mapped{[] {
+  const char* e = std::getenv("TKV_HOST_MAPPED");
+  return (e && e[0] == '0') ? 0 : 1;
+}()};
+
+const std::uint8_t* mapped_view(const std::uint8_t* base, std::uint64_t lo_byte, std::uint64_t hi_byte) {
+  if (!g_host_mapped.load(std::memory_order_relaxed) || hi_byte <= lo_byte) return nullptr;
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, base + lo_byte) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (attr.type != hipMemoryTypeHost && attr.type != hipMemoryTypeDevice) return nullptr;
+  if (attr.devicePointer != static_cast<const void*>(base + lo_byte)) return nullptr;  // same address only
+  void* start = nullptr;
+  std::size_t size = 0;
+  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                             reinterpret_cast<hipDeviceptr_t>(const_cast<std::uint8_t*>(base + lo_byte))) != hipSuccess ||
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
+                             reinterpret_cast<hipDeviceptr_t>(const_cast<std::uint8_t*>(base + lo_byte))) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  const auto s0 = reinterpret_cast<std::uintptr_t>(start);
+  const auto b = reinterpret_cast<std::uintptr_t>(base);
+  if (s0 == 0 || b + lo_byte < s0 || b + hi_byte > s0 + size) return nullptr;
+  return base;
+}
+
+// Blocks [lo, hi) of a host batch whose bytes the kernels read in place through `dbase` (the
+// device view of h_base): metadata chunks alternate between two streams; results come back per
+// chunk. Uniform contiguous chunks take the packed kernel with no metadata at all.
+int mapped_batch(DevCtx* c, int algo, const std::uint8_t* dbase, const std::uint64_t* off, const std::uint32_t* len,
+                 const std::uint32_t* init, std::uint32_t* out, std::uint64_t lo, std::uint64_t hi) {
+  const std::size_t want = static_cast<std::size_t>(std::min<std::uint64_t>(hi - lo, kMapChunk));
+  std::lock_guard<std::mutex> plk(c->pipe_mu);
+  if (!c->mpipe || c->mpipe->cap < want) {
+    c->mpipe.reset();
+    c->mpipe.reset(new MapPipe());
+    if (int rc = map_pipe_init(*c->mpipe, std::max<std::size_t>(want, 1024))) {
+      c->mpipe.reset();
+      return rc;
+    }
+  }
+  MapPipe& p = *c->mpipe;
+  struct Pending {
+    std::uint64_t lo = 0, cnt = 0;
+    bool active = false;
+  } pend[2];
+  auto retire = [&](int k) -> int {
+    if (!pend[k].active) return TKV_OK;
+    TKV_HIP(hipEventSynchronize(p.done[k]));
+    std::memcpy(out + pend[k].lo, p.h_out[k], pend[k].cnt * 4);
+    pend[k].active = false;
+    return TKV_OK;
+  };
+  int k = 0;
+  for (std::uint64_t b0 = lo; b0 < hi; b0 += p.cap) {
+    const std::size_t cnt = static_cast<std::size_t>(std::min<std::uint64_t>(hi - b0, p.cap));
+    if (int rc = retire(k)) return rc;
+    bool uniform = true;
+    for (std::size_t i = 1; i < cnt && uniform; ++i)
+      uniform = len[b0 + i] == len[b0] && off[b0 + i] == off[b0] + i * static_cast<std::uint64_t>(len[b0]);
+    const std::uint32_t* d_init = nullptr;
+    if (init) {
+      std::memcpy(p.h_init[k], init + b0, cnt * 4);
+      TKV_HIP(hipMemcpyAsync(p.d_init[k], p.h_init[k], cnt * 4, hipMemcpyHostToDevice, p.st[k]));
+      d_init = p.d_init[k];
+    }
+    if (uniform) {
+      if (int rc = run_uniform(c, algo, dbase + off[b0], len[b0], len[b0], d_init, kInit, kInit, p.d_out[k], cnt,
+                               p.st[k]))
+        return rc;
+    } else {
+      std::memcpy(p.h_off[k], off + b0, cnt * 8);
+      std::memcpy(p.h_len[k], len + b0, cnt * 4);
+      TKV_HIP(hipMemcpyAsync(p.d_off[k], p.h_off[k], cnt * 8, hipMemcpyHostToDevice, p.st[k]));
+      TKV_HIP(hipMemcpyAsync(p.d_len[k], p.h_len[k], cnt * 4, hipMemcpyHostToDevice, p.st[k]));
+      if (int rc = run_irregular(c, algo, dbase, p.d_off[k], p.d_len[k], d_init, p.d_out[k], cnt, p.st[k])) return rc;
+    }
+    TKV_HIP(hipMemcpyAsync(p.h_out[k], p.d_out[k], cnt * 4, hipMemcpyDeviceToHost, p.st[k]));
+    TKV_HIP(hipEventRecord(p.done[k], p.st[k]));
+    pend[k] = {b0, cnt, true};
+    k ^= 1;
+  }
+  for (int i = 0; i < 2; ++i)
+    if (int rc = retire(i)) return rc;
+  return TKV_OK;
+}
+
 // Blocks in [lo, hi) of a host batch, processed slab by slab. Blocks larger than a slab are
 // chained through update_device in slab-sized pieces on stream 0.
 int host_batch(DevCtx* c, int algo, const std::uint8_t* h_base, const std::uint64_t* off, const std::uint32_t* len,
                const std::uint32_t* init, std::uint32_t* out, std::uint64_t lo, std::uint64_t hi) {
   if (hi <= lo) return TKV_OK;
+  {
+    // Zero copy when the device can read the caller's buffer in place (pinned host memory).
+    std::uint64_t lo_byte = ~0ull, hi_byte = 0;
+    for (std::uint64_t b = lo; b < hi; ++b)
+      if (len[b]) {
+        lo_byte = std::min<std::uint64_t>(lo_byte, off[b]);
+        hi_byte = std::max<std::uint64_t>(hi_byte, off[b] + len[b]);
+      }
+    if (hi_byte > lo_byte) {
+      if (const std::uint8_t* dbase = mapped_view(h_base, lo_byte, hi_byte))
+        return mapped_batch(c, algo, dbase, off, len, init, out, lo, hi);
+    }
+  }
   // Largest number of blocks a slab can hold (all >= 1 byte... zero-length blocks count too).
   std::size_t max_blocks = 1;
   {
@@ -799,5 +959,6 @@ size_t tkv_debug_tables_poly(uint32_t poly, void* out, size_t cap) {
 
 uint32_t tkv_debug_multmodp(uint32_t a, uint32_t b) { return multmodp(a, b); }
 uint32_t tkv_debug_x8nmodp(uint64_t nbytes) { return x8nmodp(nbytes); }
+int tkv_debug_set_host_mapped(int enable) { return tkv::g_host_mapped.exchange(enable ? 1 : 0); }
 
 }  // extern "C"

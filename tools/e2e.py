@@ -41,8 +41,10 @@ host = host_t.numpy()
 offs = np.arange(n, dtype=np.uint64) * a.len
 lens = np.full(n, a.len, np.uint32)
 
-for mode in ("pinned", "pageable"):
-    src = host if mode == "pinned" else np.array(host[: min(total, 4 << 30)])
+lib = tk.load_library()
+for mode in ("pinned", "pinned-staged", "pageable"):
+    lib.tkv_debug_set_host_mapped(0 if mode == "pinned-staged" else 1)  # zero copy vs staged copies
+    src = host if mode.startswith("pinned") else np.array(host[: min(total, 4 << 30)])
     nn = src.size // a.len
     got = tk.crc32_batch_host(src, offs[:nn], lens[:nn])  # warm-up + correctness
     ok = bool(np.array_equal(got, want[:nn]))
