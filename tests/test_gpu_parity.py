@@ -128,6 +128,61 @@ def test_wal_many_records(gpu, oracle):
     assert tk.wal.verify(image) == ("ok", 3000, len(image))
 
 
+def big_wal(rng, n_rec, giant_at=None, giant_len=0):
+    """A WAL image of n_rec records laid out as wal.cpp:19-61 (numpy, unstamped); optionally one
+    giant value at record giant_at. Returns (image, offsets, sizes)."""
+    klen = rng.integers(0, 40, n_rec).astype(np.uint64)
+    vlen = np.minimum(rng.zipf(1.6, n_rec) * 64, 16000).astype(np.uint64)
+    if giant_at is not None:
+        vlen[giant_at] = giant_len
+    size = 26 + klen + vlen
+    offs = np.zeros(n_rec, np.uint64)
+    offs[1:] = np.cumsum(size[:-1])
+    img = rng.integers(0, 256, int(size.sum()), dtype=np.uint8)
+    hdr = np.zeros((n_rec, 26), np.uint8)
+    hdr[:, 0:4] = (size - 8).astype("<u4").view(np.uint8).reshape(-1, 4)
+    hdr[:, 9:17] = np.arange(n_rec, dtype="<u8").view(np.uint8).reshape(-1, 8)
+    hdr[:, 18:22] = klen.astype("<u4").view(np.uint8).reshape(-1, 4)
+    hdr[:, 22:26] = vlen.astype("<u4").view(np.uint8).reshape(-1, 4)
+    img[offs.astype(np.int64)[:, None] + np.arange(26)] = hdr
+    return img, offs, size.astype(np.uint32)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_wal_verify_large_image_phases(gpu, oracle, pinned):
+    """A >= 64 MiB WAL is walked and checksummed in phases (the CRC batch of a phase overlaps the
+    walk of the next): results, first-corruption position and truncation behave as one pass."""
+    import ctypes
+    rng = np.random.default_rng(41)
+    img, offs, size = big_wal(rng, 120000, giant_at=50000, giant_len=30 << 20)
+    lib = tk.load_library()
+    keep = None
+    if pinned:
+        keep = torch.from_numpy(img).pin_memory()
+        img = keep.numpy()
+    tk.check(lib.tkv_wal_stamp(ctypes.c_void_p(img.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                               ctypes.c_void_p(size.ctypes.data), offs.size))
+    for i in (0, 49999, 50000, 50001, 119999):  # stamps equal the oracle's (wal.cpp:54-58)
+        o, n = int(offs[i]), int(size[i])
+        assert int(img[o + 4:o + 8].view("<u4")[0]) == oracle.crc(img[o + 8:o + n].tobytes())
+    assert img.size >= 64 << 20
+    good, stop = ctypes.c_uint64(0), ctypes.c_uint64(0)
+
+    def verify(buf, nbytes):
+        rc = lib.tkv_wal_verify(ctypes.c_void_p(buf.ctypes.data), nbytes, ctypes.byref(good), ctypes.byref(stop))
+        return rc, good.value, stop.value
+
+    assert verify(img, img.size) == (0, offs.size, img.size)
+    for bad in (3, 50000, 90001):  # first phase, the giant record, a late phase
+        o = int(offs[bad]) + 26
+        img[o] ^= 0x10
+        rc, g, st = verify(img, img.size)
+        img[o] ^= 0x10
+        assert rc != 0 and (g, st) == (bad, int(offs[bad]))
+    rc, g, st = verify(img, img.size - 5)  # truncated tail: the last record does not fit
+    assert rc != 0 and (g, st) == (offs.size - 1, int(offs[-1]))
+
+
 # ---- uniform batches ---------------------------------------------------------------------------
 
 @pytest.mark.parametrize("blen,n", [(4096, 5000), (65536, 300), (4096, 7), (16, 100000), (1000, 9000),
@@ -341,6 +396,20 @@ def test_host_batch_pinned_uniform_and_huge(gpu, oracle):
     got = tk.crc32_batch_host(pin, [0, 7, 1 << 20], [big, 100, 4096])
     assert [int(x) for x in got] == [oracle.crc(pin[:big].tobytes()), oracle.crc(pin[7:107].tobytes()),
                                      oracle.crc(pin[1 << 20:(1 << 20) + 4096].tobytes())]
+
+
+def test_host_batch_pinned_sees_host_writes_between_calls(gpu, oracle):
+    """In-place reads of pinned memory see every host write made before the call (no stale device
+    cache lines from an earlier call over the same buffer)."""
+    rng = np.random.default_rng(23)
+    keep, pin = pinned_copy(rng.integers(0, 256, 8 << 20, dtype=np.uint8))
+    offs = np.arange(0, 8 << 20, 65536, dtype=np.uint64)
+    lens = np.full(offs.size, 65536, np.uint32)
+    for it in range(6):
+        got = tk.crc32_batch_host(pin, offs, lens)
+        assert np.array_equal(got, oracle.batch(pin, offs, lens)), it
+        pos = rng.integers(0, pin.size, 1000)
+        pin[pos] ^= rng.integers(1, 256, pos.size, dtype=np.uint8)  # host writes, then the next call
 
 
 def test_host_batch_registered_range_checked(gpu, oracle):

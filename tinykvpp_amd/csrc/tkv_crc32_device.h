@@ -616,8 +616,11 @@ __device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t*
 // (4 KiB blocks), so no Horner state at all. The SIMDs are issue-bound here (PMC: every SIMD issues
 // ~96 % of cycles), so the loop is written for instruction count: incremental row addressing, no
 // divisions, selects instead of divergent branches.
-template <int DEPTH, int ILP, bool R1, bool SPLIT = false, std::uint32_t ROT = 0>
+// CHK (explorer only, R1, nblocks a multiple of 64*waves): chunk-strided map - wave w owns chunks
+// w, w+W, w+2W, ... of 2^CHK consecutive blocks instead of one contiguous range.
+template <int DEPTH, int ILP, bool R1, bool SPLIT = false, std::uint32_t ROT = 0, int CHK = 0>
 __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(CHK == 0 || (R1 && ROT == 0 && CHK <= 6), "chunk-strided map: R1 only, chunks of <= 64 blocks");
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
   fill_lds(a.tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
@@ -643,6 +646,10 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
   const std::uint32_t nb = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W) - b0;
   if (nb == 0) return;
   const std::uint32_t nrows = nb * R;  // wave-local rows j = 0 .. nrows-1, contiguous in memory
+  // CHK: global block of wave-local block j
+  auto gblk = [&](std::uint32_t j) -> std::uint64_t {
+    return (static_cast<std::uint64_t>(j >> CHK) * W + wave) * (1u << CHK) + (j & ((1u << CHK) - 1u));
+  };
   const std::uintptr_t lane_base =
       reinterpret_cast<std::uintptr_t>(a.base) + static_cast<std::uint64_t>(b0) * R * kRow + lane * kSeg;
   // ROT != 0: the wave walks its blocks starting at block (wave*ROT) mod nb and wraps around, so at
@@ -658,7 +665,8 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
       jc += rotr;
       jc -= jc >= nrows ? nrows : 0u;
     }
-    const std::uintptr_t p = lane_base + static_cast<std::uint64_t>(jc) * kRow;
+    const std::uintptr_t p = CHK ? reinterpret_cast<std::uintptr_t>(a.base) + lane * kSeg + gblk(jc) * kRow
+                                 : lane_base + static_cast<std::uint64_t>(jc) * kRow;
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i);
   };
@@ -691,7 +699,7 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
       if (slot == 63u || k + 1 == nb) {
         std::uint32_t li = k - slot + lane + rot_b;  // wave-local block of lane's result
         li -= li >= nb ? nb : 0u;
-        if (lane <= slot) a.out[b0 + li] = keep;
+        if (lane <= slot) a.out[CHK ? gblk(k - slot + lane) : b0 + li] = keep;
       }
       r = 0;
       ++k;

@@ -23,13 +23,32 @@ bool ptr_ok(const void* p) { return p != nullptr; }
 // crc_0 of the 4 little-endian bytes of v followed by z zero bytes: the term that turns the CRC of an
 // SSTable image with `v` in its crc32_ field into the CRC with the field read as zero (linearity of
 // the CRC over GF(2); the same identity sst_fix applies on the device).
+// Shift_(2^k bytes) as byte-sliced linear maps, k < 40: Shift_z(c) is one 4-lookup step per set bit
+// of z (about 40 lookups for a 4 KiB image) instead of a bitwise GF(2) multiply per image.
+struct PowTables {
+  std::uint32_t t[40][4][256];
+  PowTables() {
+    for (int k = 0; k < 40; ++k)
+      for (int j = 0; j < 4; ++j)
+        for (std::uint32_t v = 0; v < 256; ++v) t[k][j][v] = shift_bytes(v << (8 * j), std::uint64_t(1) << k, kPoly);
+  }
+};
+const PowTables& pow_tables() {
+  static const PowTables* p = new PowTables();
+  return *p;
+}
+
 std::uint32_t field_term(std::uint32_t v, std::uint64_t z) {
   std::uint32_t c = 0;
   for (int k = 0; k < 4; ++k) {
     c ^= (v >> (8 * k)) & 0xFFu;
     for (int b = 0; b < 8; ++b) c = (c >> 1) ^ ((c & 1u) ? kPoly : 0u);
   }
-  return shift_bytes(c, z, kPoly);
+  const PowTables& pt = pow_tables();
+  for (int k = 0; z; ++k, z >>= 1)
+    if (z & 1u)
+      c = pt.t[k][0][c & 0xFFu] ^ pt.t[k][1][(c >> 8) & 0xFFu] ^ pt.t[k][2][(c >> 16) & 0xFFu] ^ pt.t[k][3][c >> 24];
+  return c;
 }
 
 // ---- WAL record_len chain (wal.cpp:63-87) ----------------------------------------------------------
@@ -92,6 +111,22 @@ unsigned host_threads() {
   return std::max(1u, n);
 }
 
+// fn(i) for i in [0, n): on host threads when n is large (field writes scattered over a big image).
+template <class F>
+void parallel_for(std::uint64_t n, F fn) {
+  const unsigned nt = n >= (1u << 14) ? host_threads() : 1u;
+  if (nt == 1) {
+    for (std::uint64_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([=] {
+      for (std::uint64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) fn(i);
+    });
+  for (auto& t : th) t.join();
+}
+
 // A header the reference encoder would write (wal.cpp:19-61): record_len = 18 + klen + vlen and the
 // two flag bytes are 0/1. Used only to choose speculative starting points; never trusted.
 bool plausible(const std::uint8_t* w, std::uint64_t size, std::uint64_t p) {
@@ -111,12 +146,15 @@ bool plausible(const std::uint8_t* w, std::uint64_t size, std::uint64_t p) {
 // from the true entry point e_k (where the verified chain of pieces < k crosses the cut) onward only
 // if e_k is one of its record starts (chains that share a start coincide from there); otherwise
 // piece k is walked again from e_k.
-Chain wal_chain(const std::uint8_t* w, std::uint64_t size) {
+// Records that START in [start, limit); c.end is the first record start >= limit (or where the
+// chain broke).
+Chain wal_chain(const std::uint8_t* w, std::uint64_t size, std::uint64_t start, std::uint64_t limit) {
   constexpr std::uint64_t kPiece = std::uint64_t(8) << 20;
+  const std::uint64_t span = limit > start ? limit - start : 0;
   const unsigned K = static_cast<unsigned>(
-      std::min<std::uint64_t>(host_threads(), std::max<std::uint64_t>(1, size / kPiece)));
+      std::min<std::uint64_t>(host_threads(), std::max<std::uint64_t>(1, span / kPiece)));
   std::vector<std::uint64_t> cut(K + 1);
-  for (unsigned k = 0; k <= K; ++k) cut[k] = size * k / K;
+  for (unsigned k = 0; k <= K; ++k) cut[k] = start + span * k / K;
   std::vector<Chain> part(K);
   auto run = [&](unsigned k) {
     Chain local;  // built thread-locally: the Chain headers in `part` share cache lines
@@ -157,6 +195,8 @@ Chain wal_chain(const std::uint8_t* w, std::uint64_t size) {
   return c;
 }
 
+Chain wal_chain(const std::uint8_t* w, std::uint64_t size) { return wal_chain(w, size, 0, size); }
+
 int sst_check(const std::uint64_t* h_sizes, std::uint64_t n) {
   for (std::uint64_t i = 0; i < n; ++i)
     if (h_sizes[i] < TKV_SST_MIN_IMAGE || h_sizes[i] > 0xFFFFFFFFull)
@@ -171,18 +211,49 @@ int tkv_wal_verify(const uint8_t* h_wal, uint64_t size, uint64_t* n_good, uint64
   if ((size && !ptr_ok(h_wal)) || !ptr_ok(n_good) || !ptr_ok(stop_offset))
     return set_error(TKV_INVALID_ARGUMENT, "null pointer");
   // The record_len chain (wal.cpp:63-87), walked in parallel (wal_chain): records are
-  // [u32 record_len][u32 crc][payload of record_len bytes].
-  const Chain ch = wal_chain(h_wal, size);
-  const std::size_t nrec = ch.pos.size();
-  std::vector<std::uint64_t> off(nrec);
-  std::vector<std::uint32_t> got(nrec);
-  for (std::size_t i = 0; i < nrec; ++i) off[i] = ch.pos[i] + 8;
-  if (nrec) {
-    if (int rc = batch_host_impl(kAlgoCrc32, h_wal, off.data(), ch.len.data(), nullptr, got.data(), nrec)) return rc;
+  // [u32 record_len][u32 crc][payload of record_len bytes]. Large images go in phases: the CRC
+  // batch of phase j runs (GPU, on a helper thread) while the host walks phase j+1.
+  const unsigned J = size >= (std::uint64_t(64) << 20) ? 4u : 1u;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return set_error(TKV_IO_ERROR, "hipGetDevice failed");
+  std::vector<Chain> phase;
+  phase.reserve(J);  // helper threads read phase[j] while later phases are appended
+  std::vector<std::vector<std::uint32_t>> got(J);
+  std::vector<std::vector<std::uint64_t>> off(J);
+  std::vector<int> rcs(J, TKV_OK);
+  std::vector<std::thread> crc_th;
+  std::uint64_t start = 0;
+  for (unsigned j = 0; j < J; ++j) {
+    const std::uint64_t limit = j + 1 == J ? size : std::max(start, size * (j + 1) / J);
+    phase.push_back(wal_chain(h_wal, size, start, limit));
+    const Chain& ch = phase.back();
+    const std::size_t nrec = ch.pos.size();
+    off[j].resize(nrec);
+    got[j].resize(nrec);
+    for (std::size_t i = 0; i < nrec; ++i) off[j][i] = ch.pos[i] + 8;
+    if (nrec)
+      crc_th.emplace_back([&, j, nrec] {
+        if (hipSetDevice(dev) != hipSuccess) {
+          rcs[j] = TKV_IO_ERROR;
+          return;
+        }
+        rcs[j] = batch_host_impl(kAlgoCrc32, h_wal, off[j].data(), phase[j].len.data(), nullptr, got[j].data(), nrec);
+      });
+    start = ch.end;
+    if (ch.err || start >= size) break;
   }
+  for (auto& t : crc_th) t.join();
+  for (unsigned j = 0; j < J; ++j)
+    if (rcs[j] != TKV_OK) return set_error(rcs[j], "WAL verify: CRC batch failed");
+  Chain ch = std::move(phase[0]);
+  for (std::size_t j = 1; j < phase.size(); ++j) ch.append(phase[j], 0);
+  std::vector<std::uint32_t> all;
+  all.reserve(ch.pos.size());
+  for (std::size_t j = 0; j < phase.size(); ++j) all.insert(all.end(), got[j].begin(), got[j].end());
+  const std::size_t nrec = ch.pos.size();
   std::uint64_t good = 0;
   // first record whose CRC (wal.cpp:93-96) or key/value bounds (wal.cpp:118-121) fail
-  while (good < nrec && got[good] == ch.crc[good] && ch.kv_ok[good]) ++good;
+  while (good < nrec && all[good] == ch.crc[good] && ch.kv_ok[good]) ++good;
   *n_good = good;
   *stop_offset = good < nrec ? ch.pos[good] : ch.end;
   if (good < nrec || ch.err) return set_error(TKV_CORRUPTED, "corrupted WAL record");
@@ -200,7 +271,7 @@ int tkv_wal_stamp(uint8_t* h_buf, const uint64_t* h_offsets, const uint32_t* h_s
     len[i] = h_sizes[i] - 8;
   }
   if (int rc = batch_host_impl(kAlgoCrc32, h_buf, off.data(), len.data(), nullptr, crc.data(), n)) return rc;
-  for (std::uint64_t i = 0; i < n; ++i) std::memcpy(h_buf + h_offsets[i] + 4, &crc[i], 4);  // wal.cpp:58
+  parallel_for(n, [&](std::uint64_t i) { std::memcpy(h_buf + h_offsets[i] + 4, &crc[i], 4); });  // wal.cpp:58
   return TKV_OK;
 }
 
@@ -210,12 +281,12 @@ int tkv_sst_stamp_blocks(uint8_t* h_file, const uint64_t* h_offsets, const uint6
   if (!ptr_ok(h_file) || !ptr_ok(h_offsets) || !ptr_ok(h_sizes)) return set_error(TKV_INVALID_ARGUMENT, "null pointer");
   if (int rc = sst_check(h_sizes, n)) return rc;
   std::vector<std::uint32_t> len(n), crc(n);
-  for (std::uint64_t i = 0; i < n; ++i) {
+  parallel_for(n, [&](std::uint64_t i) {
     std::memset(h_file + h_offsets[i] + TKV_SST_CRC_OFFSET, 0, 4);  // the field reads as zero
     len[i] = static_cast<std::uint32_t>(h_sizes[i]);
-  }
+  });
   if (int rc = batch_host_impl(kAlgoCrc32, h_file, h_offsets, len.data(), nullptr, crc.data(), n)) return rc;
-  for (std::uint64_t i = 0; i < n; ++i) std::memcpy(h_file + h_offsets[i] + TKV_SST_CRC_OFFSET, &crc[i], 4);
+  parallel_for(n, [&](std::uint64_t i) { std::memcpy(h_file + h_offsets[i] + TKV_SST_CRC_OFFSET, &crc[i], 4); });
   return TKV_OK;
 }
 
@@ -230,14 +301,31 @@ int tkv_sst_verify_blocks(const uint8_t* h_file, const uint64_t* h_offsets, cons
   std::vector<std::uint32_t> len(n), got(n);
   for (std::uint64_t i = 0; i < n; ++i) len[i] = static_cast<std::uint32_t>(h_sizes[i]);
   if (int rc = batch_host_impl(kAlgoCrc32, h_file, h_offsets, len.data(), nullptr, got.data(), n)) return rc;
-  for (std::uint64_t i = 0; i < n; ++i) {
-    std::uint32_t stored;
-    std::memcpy(&stored, h_file + h_offsets[i] + TKV_SST_CRC_OFFSET, 4);
-    const std::uint32_t want = got[i] ^ field_term(stored, h_sizes[i] - TKV_SST_CRC_OFFSET - 4);
-    if (want != stored) {
-      if (*n_bad == 0) *first_bad = i;
-      ++*n_bad;
+  // stored vs CRC with the field read as zero, on host threads for large files
+  const unsigned nt = n >= (1u << 14) ? host_threads() : 1u;
+  std::vector<std::uint64_t> bad(nt, 0), first(nt, n);
+  auto part = [&](unsigned t) {
+    for (std::uint64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
+      std::uint32_t stored;
+      std::memcpy(&stored, h_file + h_offsets[i] + TKV_SST_CRC_OFFSET, 4);
+      const std::uint32_t want = got[i] ^ field_term(stored, h_sizes[i] - TKV_SST_CRC_OFFSET - 4);
+      if (want != stored) {
+        if (bad[t] == 0) first[t] = i;
+        ++bad[t];
+      }
     }
+  };
+  pow_tables();
+  if (nt == 1) {
+    part(0);
+  } else {
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) th.emplace_back(part, t);
+    for (auto& t : th) t.join();
+  }
+  for (unsigned t = 0; t < nt; ++t) {
+    if (bad[t] && *n_bad == 0) *first_bad = first[t];
+    *n_bad += bad[t];
   }
   return *n_bad ? set_error(TKV_CORRUPTED, "corrupted SSTable data block") : TKV_OK;
 }

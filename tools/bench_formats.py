@@ -107,6 +107,26 @@ for _ in range(3):
 t2 = time.perf_counter()
 emit("wal_verify_vs_stamp_back_to_back", total, (t1 - t0) / 3, n_rec, {"stamp_ms": round((t2 - t1) / 3 * 1e3, 3)})
 
+# same WAL image in pinned host memory (a WAL append buffer allocated with hipHostMalloc): the kernels
+# read it in place, no staging copies
+wal_pin_t = torch.from_numpy(wal).pin_memory()
+wal_pin = wal_pin_t.numpy()
+t = timeit(lambda: tk.check(lib.tkv_wal_stamp(ctypes.c_void_p(wal_pin.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                                              ctypes.c_void_p(sizes32.ctypes.data), n_rec)))
+emit("wal_stamp_pinned", total, t, n_rec, {"records": n_rec, "source": "pinned, read in place"})
+
+
+def verify_pinned():
+    rc = lib.tkv_wal_verify(ctypes.c_void_p(wal_pin.ctypes.data), total, ctypes.byref(good), ctypes.byref(stop))
+    assert rc == 0 and good.value == n_rec and stop.value == total, (rc, good.value, stop.value)
+
+
+t = timeit(verify_pinned)
+emit("wal_verify_pinned", total, t, n_rec, {"records": n_rec, "verified": good.value, "source": "pinned, read in place"})
+t = timeit(lambda: tk.crc32_batch_host(wal_pin, poffs, plens))
+emit("wal_payload_batch_host_pinned", total, t, n_rec, {"what": "the CRC part of wal_verify_pinned alone"})
+del wal_pin, wal_pin_t
+
 # ---- SSTable image: ~4 KiB data blocks -----------------------------------------------------------------
 nblk = 250_000
 body = 4096 - 36
@@ -123,6 +143,14 @@ def sstamp():
 t = timeit(sstamp)
 emit("sst_stamp", sfile.nbytes, t, nblk, {"block_image_bytes": int(sizes[0])})
 assert sst.verify_blocks(sfile, soffs, sizes)[0] == "ok"
+sfile_pin_t = torch.from_numpy(sfile).pin_memory()
+sfile_pin = sfile_pin_t.numpy()
+t = timeit(lambda: sst.stamp_blocks(sfile_pin, soffs, sizes))
+emit("sst_stamp_pinned", sfile.nbytes, t, nblk, {"block_image_bytes": int(sizes[0]), "source": "pinned, read in place"})
+t = timeit(lambda: sst.verify_blocks(sfile_pin, soffs, sizes))
+emit("sst_verify_pinned", sfile.nbytes, t, nblk, {"block_image_bytes": int(sizes[0]), "source": "pinned, read in place"})
+assert np.array_equal(sfile_pin, sfile)
+del sfile_pin, sfile_pin_t
 
 d = torch.from_numpy(sfile).cuda()
 do = torch.from_numpy(soffs.astype(np.int64)).cuda()

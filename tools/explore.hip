@@ -195,10 +195,19 @@ void P(RowsArgs a, hipStream_t s) {
                      a.out);
 }
 
-template <int D, int I, bool R1, int T, bool SP, std::uint32_t ROT = 0>
+template <int D, int I, bool R1, int T, bool SP, std::uint32_t ROT = 0, int CHK = 0>
 __global__ __launch_bounds__(T) void k_packed(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<D, I, R1, SP, ROT>(a, lds);
+  dev::crc_packed_body<D, I, R1, SP, ROT, CHK>(a, lds);
+}
+
+// chunk-strided block map (4 KiB blocks only; other lengths fall back to the product map)
+template <int CHK>
+void PC(RowsArgs a, hipStream_t s) {
+  a.nwaves = g_ncu * 16;
+  if (a.len == kRow && a.nblocks % (a.nwaves * 64u) == 0)
+    hipLaunchKernelGGL((k_packed<4, 2, true, 1024, false, 0, CHK>), dim3(g_ncu), dim3(1024), 0, s, a);
+  else hipLaunchKernelGGL((k_packed<4, 2, false, 1024, false>), dim3(g_ncu), dim3(1024), 0, s, a);
 }
 
 template <std::uint32_t ROT>
@@ -239,6 +248,7 @@ const V kVariants[] = {
     {"interf L0 V0", IF<0, 0>}, {"interf L72 V0", IF<72, 0>}, {"interf L0 V128", IF<0, 128>},
     {"interf L72 V128", IF<72, 128>}, {"interf L36 V0", IF<36, 0>}, {"interf L144 V0", IF<144, 0>},
     {"interf L0 V256", IF<0, 256>},
+    {"packed chunk64", PC<6>}, {"packed chunk16", PC<4>}, {"packed chunk4", PC<2>},
     {"packed rot1", PR<1>}, {"packed rot61", PR<61>}, {"packed rot16", PR<16>},
     {"dyn D4 I2 C8", PD<4, 2, 8>}, {"dyn D4 I2 C16", PD<4, 2, 16>}, {"dyn D4 I2 C32", PD<4, 2, 32>},
     {"dyn D4 I2 C64", PD<4, 2, 64>}, {"dyn T768 D4 I2 C16", PD<4, 2, 16, 768>},
