@@ -80,7 +80,9 @@ int tkv_crc32_batch_uniform_device(const uint8_t *d_base, uint64_t stride, uint6
 
 /* Irregular batch in HOST memory on the current device: blocks are streamed through pinned
  * staging buffers with H2D copy / kernel / D2H copy overlapped on two streams. Synchronous.
- * h_base may be pageable or pinned (pinned avoids one host memcpy). */
+ * h_base may be pageable or pinned: when every block lies inside one pinned allocation mapped at
+ * the same address on the device (hipHostMalloc, hipHostRegister), the kernels read the blocks in
+ * place over PCIe and only offsets, lengths and results are copied. */
 int tkv_crc32_batch_host(const uint8_t *h_base, const uint64_t *h_offsets, const uint32_t *h_lengths,
                          const uint32_t *h_init_raw, uint32_t *h_out_final, uint64_t n);
 
