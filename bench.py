@@ -146,6 +146,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="cfg3: skip the host-memory end-to-end measurement")
     ap.add_argument("--traffic-csv", default=None,
                     help="rocprofv3 --pmc counter_collection.csv (FETCH_SIZE) of this command, for roofline.traffic")
     args = ap.parse_args()
@@ -267,6 +268,23 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_step},
         "cpu_baseline": None,
     }
+    if args.config == "cfg3" and not args.no_e2e:
+        # BASELINE cfg3 "+ H2D/D2H timed": the same blocks starting and ending in host memory (pinned,
+        # read in place by the kernels over PCIe; results copied back), per rank; never `value`.
+        host_p = torch.empty(total, dtype=torch.uint8).pin_memory()
+        host_p.copy_(data)
+        hp = host_p.numpy()
+        offs_h = np.arange(nblocks, dtype=np.uint64) * blen
+        lens_h = np.full(nblocks, blen, np.uint32)
+        got = tk.crc32_batch_host(hp, offs_h, lens_h)
+        t0 = time.perf_counter()
+        for _ in range(2):
+            tk.crc32_batch_host(hp, offs_h, lens_h)
+        dt_e2e = (time.perf_counter() - t0) / 2
+        line["e2e_host"] = {"value": round(total / (1 << 30) / dt_e2e, 2), "unit": "GiB/s",
+                            "GB_per_s": round(total / 1e9 / dt_e2e, 2), "source": "pinned host memory, read in place",
+                            "bit_exact": bool(np.array_equal(got, crcs))}
+        del host_p, hp
     if rank == 0 and world == 1 and not args.no_cpu_baseline and blen is not None:
         nb_host = min(nblocks, (4 << 30) // blen)  # at most 4 GiB of the batch goes to host memory
         host = data[:nb_host * blen].cpu().numpy()
