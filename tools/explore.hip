@@ -148,6 +148,68 @@ __global__ __launch_bounds__(1024) void k_interf(const std::uint8_t* base, std::
 
 
 
+// Interference probe 2: NL lookups per row split over CH independent dependent chains, each lookup
+// a conflict-free ds_read of WB bytes per lane (4 = ds_read_b32, 8 = ds_read_b64), same loads and
+// pipeline as k_interf. Separates LDS bytes, LDS instruction count and chain latency.
+template <int NL, int WB, int CH>
+__global__ __launch_bounds__(1024) void k_interf2(const std::uint8_t* base, std::uint32_t nrows, std::uint32_t W,
+                                                  std::uint32_t* out) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  for (std::uint32_t i = threadIdx.x; i < kLdsWords; i += 1024) lds[i] = i * 2654435761u;
+  __syncthreads();
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint32_t wave = blockIdx.x * 16 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t g0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(nrows) / W);
+  const std::uint32_t g1 = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(nrows) / W);
+  constexpr int DEPTH = 4;
+  auto addr = [&](std::uint32_t g, int i) -> std::uintptr_t {
+    return reinterpret_cast<std::uintptr_t>(base) + static_cast<std::uint64_t>(g < g1 ? g : g0) * 4096u +
+           64u * lane + 16u * i;
+  };
+  uint4 buf[DEPTH][4];
+  std::uint32_t keep = 0;
+#pragma unroll
+  for (int s = 0; s < DEPTH - 1; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) buf[s][i] = dev::gload16(addr(g0 + s, i));
+  for (std::uint32_t g = g0; g < g1; g += DEPTH) {
+#pragma unroll
+    for (int k = 0; k < DEPTH; ++k) {
+      const int s = (k + DEPTH - 1) % DEPTH;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) buf[s][i] = dev::gload16(addr(g + k + DEPTH - 1, i));
+      if (g + k >= g1) break;
+      std::uint32_t y[CH];
+#pragma unroll
+      for (int c = 0; c < CH; ++c) y[c] = buf[k][c & 3].x ^ buf[k][(c + 1) & 3].w ^ c;
+#pragma unroll
+      for (int j = 0; j < NL / CH; ++j)
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          // conflict-free: b32 lane c of each half reads bank c; b64 lane l reads banks 2l, 2l+1 (mod 64)
+          const std::uint32_t a = WB == 4 ? (((y[c] & 0xFFu) << 8) | (lane & 31u) << 2)
+                                          : (((y[c] & 0x7Fu) << 9) | (lane << 3));
+          if constexpr (WB == 4) {
+            y[c] = dev::lds_at(lds, a) ^ (y[c] >> 8);
+          } else {
+            const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + a);
+            y[c] = v.x ^ v.y ^ (y[c] >> 8);
+          }
+        }
+      std::uint32_t yy = 0;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) yy ^= y[c];
+      const std::uint32_t r = __builtin_amdgcn_readlane(dev::wave_xor_to_lane63(yy), 63);
+      const std::uint32_t gi = g + k;
+      if (lane == (gi & 63u)) keep = r;
+      if ((gi & 63u) == 63u || gi + 1 == g1) {
+        const std::uint32_t first = gi & ~63u;
+        if (first + lane >= g0 && first + lane <= gi) out[first + lane] = keep;
+      }
+    }
+  }
+}
+
 // Diagnostic: per-wave start/end s_memrealtime (100 MHz) of the production packed body.
 __global__ __launch_bounds__(1024) void k_packed_stamped(RowsArgs a, unsigned long long* stamps) {
   __shared__ std::uint32_t lds[kLdsWords];
@@ -244,7 +306,16 @@ void IF(RowsArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_interf<NL, NV>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows, a.nwaves, a.out);
 }
 
+template <int NL, int WB, int CH>
+void IF2(RowsArgs a, hipStream_t s) {
+  hipLaunchKernelGGL((k_interf2<NL, WB, CH>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows, a.nwaves, a.out);
+}
+
 const V kVariants[] = {
+    {"i2 L0", IF2<0, 4, 1>}, {"i2 L72 b32 ch1", IF2<72, 4, 1>}, {"i2 L72 b32 ch2", IF2<72, 4, 2>},
+    {"i2 L72 b32 ch4", IF2<72, 4, 4>}, {"i2 L72 b32 ch8", IF2<72, 4, 8>}, {"i2 L36 b64 ch2", IF2<36, 8, 2>},
+    {"i2 L72 b64 ch2", IF2<72, 8, 2>}, {"i2 L36 b32 ch2", IF2<36, 4, 2>}, {"i2 L144 b32 ch4", IF2<144, 4, 4>},
+    {"i2 L144 b32 ch8", IF2<144, 4, 8>},
     {"interf L0 V0", IF<0, 0>}, {"interf L72 V0", IF<72, 0>}, {"interf L0 V128", IF<0, 128>},
     {"interf L72 V128", IF<72, 128>}, {"interf L36 V0", IF<36, 0>}, {"interf L144 V0", IF<144, 0>},
     {"interf L0 V256", IF<0, 256>},
