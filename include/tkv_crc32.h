@@ -133,6 +133,26 @@ int tkv_sst_verify_blocks(const uint8_t *h_file, const uint64_t *h_offsets, cons
 int tkv_sst_block_crcs_device(uint8_t *d_file, const uint64_t *d_offsets, const uint32_t *d_sizes, uint32_t *d_out,
                               uint64_t n, int store, void *stream);
 
+/* ---- SSTable index image + footer stamping (format defined here; parity unpinned) ------------------
+ * research/12-integrity-crash-consistency.md §5 asks for a checksum over the index image and the
+ * footer, kept in the footer's existing crc32_ field (sstable_format.hpp:129-135). The reference
+ * writes only 8 footer bytes (kFooterSize, sstable_format.hpp:140), and in the order
+ * (index_size, index_offset) (sstable_writer.cpp get_footer) while decode_footer reads
+ * (index_offset, index_size) (sstable_format.cpp:99-106). The footer here is the full 20-byte struct
+ * in declaration order, little-endian:
+ *     u32 index_offset | u32 index_size | u32 bloom_offset | u32 bloom_size | u32 crc32_
+ * and crc32_ = CRC-32 of (index image || footer bytes [0, 16)), i.e. the index bytes as get_index
+ * lays them out (sstable_writer.cpp get_index) followed by the footer's first four fields. */
+#define TKV_SST_FOOTER_SIZE 20u
+#define TKV_SST_FOOTER_CRC_OFFSET 16u
+
+/* Write the crc32_ field of h_footer (20 bytes; its first 16 bytes already filled) from the index
+ * image [h_index, h_index + index_size) (index_size may be 0). */
+int tkv_sst_stamp_footer(const uint8_t *h_index, uint64_t index_size, uint8_t *h_footer);
+
+/* Check the stored crc32_ of h_footer against the index image: TKV_OK or TKV_CORRUPTED. */
+int tkv_sst_verify_footer(const uint8_t *h_index, uint64_t index_size, const uint8_t *h_footer);
+
 /* ---- CRC-32C (Castagnoli) — SURVEY.md §8f rank 4 ------------------------------------------------ */
 
 /* Same engine and kernels with the tables of the Castagnoli polynomial (reflected 0x82F63B78,

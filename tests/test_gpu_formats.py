@@ -163,3 +163,58 @@ def test_sst_and_wal_on_pinned_buffers(gpu, oracle):
     wp[int(of[700]) + 30] ^= 0x40  # payload byte of record 700 (every record is >= 26 bytes... key/value)
     rc = lib.tkv_wal_verify(ctypes.c_void_p(wp.ctypes.data), wp.size, ctypes.byref(good), ctypes.byref(stop))
     assert rc != 0 and good.value <= 700 and stop.value <= int(of[700])
+
+
+# ---- SSTable index image + footer (format: include/tkv_crc32.h; parity unpinned) ------------------
+
+def make_index(rng, offs, sizes):
+    """Index entries as sstable_writer::record_data_block records them (smallest key, offset, size)."""
+    return sst.encode_index_image([(rng.bytes(int(rng.integers(1, 64))), int(o), int(s))
+                                   for o, s in zip(offs, sizes)])
+
+
+@pytest.mark.parametrize("nblocks", [0, 1, 37, 3000])
+def test_sst_footer_stamp_matches_oracle(gpu, oracle, nblocks):
+    rng = np.random.default_rng(100 + nblocks)
+    _, offs, sizes = make_file(rng, max(nblocks, 1))
+    index = make_index(rng, offs[:nblocks], sizes[:nblocks]) if nblocks else b""
+    index_offset = int(offs[-1] + sizes[-1])
+    footer = sst.stamp_footer(index, sst.encode_footer(index_offset, len(index)))
+    want = oracle.crc(index + footer[:16])
+    assert int.from_bytes(footer[16:20], "little") == want
+    assert footer[:16] == sst.encode_footer(index_offset, len(index))[:16]
+    assert sst.verify_footer(index, footer) == "ok"
+
+
+def test_sst_footer_detects_index_and_field_corruption(gpu):
+    rng = np.random.default_rng(5)
+    _, offs, sizes = make_file(rng, 200)
+    index = bytearray(make_index(rng, offs, sizes))
+    footer = bytearray(sst.stamp_footer(bytes(index), sst.encode_footer(123456, len(index), 7, 8)))
+    for pos in (0, 8, len(index) // 2, len(index) - 1):          # count, first key, an offset, last size
+        bad = bytearray(index)
+        bad[pos] ^= 0x10
+        assert sst.verify_footer(bytes(bad), bytes(footer)) == "corrupted"
+    for pos in (0, 5, 9, 13, 17):                                # each footer field, crc32_ itself
+        bad = bytearray(footer)
+        bad[pos] ^= 1
+        assert sst.verify_footer(bytes(index), bytes(bad)) == "corrupted"
+    assert sst.verify_footer(bytes(index[:-1]), bytes(footer)) == "corrupted"   # truncated index
+    with pytest.raises(ValueError):
+        sst.stamp_footer(bytes(index), bytes(footer[:16]))
+
+
+def test_sst_whole_file_roundtrip(gpu):
+    """A whole SSTable image: data blocks, index, footer (sstable_writer flush order). Every block
+    and the index/footer stamped on the GPU, then verified from the file bytes alone."""
+    rng = np.random.default_rng(8)
+    f, offs, sizes = make_file(rng, 400)
+    sst.stamp_blocks(f, offs, sizes)
+    index = make_index(rng, offs, sizes)
+    footer = sst.stamp_footer(index, sst.encode_footer(f.size, len(index)))
+    image = f.tobytes() + index + footer
+    # reader side: footer first (sstable_reader.cpp:19-38), then the index it points to, then blocks
+    foot = image[-sst.FOOTER_SIZE:]
+    io, isz = int.from_bytes(foot[0:4], "little"), int.from_bytes(foot[4:8], "little")
+    assert sst.verify_footer(image[io:io + isz], foot) == "ok"
+    assert sst.verify_blocks(np.frombuffer(image, np.uint8), offs, sizes) == ("ok", 0, 400)

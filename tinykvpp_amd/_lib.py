@@ -49,6 +49,8 @@ SIGNATURES = {
     "tkv_sst_stamp_blocks": (_int, [_u8p, _vp, _vp, _u64]),
     "tkv_sst_verify_blocks": (_int, [_u8p, _vp, _vp, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "tkv_sst_block_crcs_device": (_int, [_u8p, _vp, _vp, _vp, _u64, _int, _vp]),
+    "tkv_sst_stamp_footer": (_int, [_u8p, _u64, _vp]),
+    "tkv_sst_verify_footer": (_int, [_u8p, _u64, _vp]),
     "tkv_crc32c_update": (_int, [_u32, _vp, _sz, ctypes.POINTER(_u32)]),
     "tkv_crc32c_update_device": (_int, [_u32, _vp, _sz, _vp, _vp]),
     "tkv_crc32c_batch_device": (_int, [_u8p, _vp, _vp, _vp, _vp, _u64, _vp]),

@@ -343,6 +343,38 @@ int tkv_sst_block_crcs_device(uint8_t* d_file, const uint64_t* d_offsets, const 
   return TKV_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// CRC-32 of index image || footer[0, 16): one engine update over the index, chained into a second
+// over the footer's fields (the raw register carries across, as crc32::update chaining does).
+int footer_crc(const std::uint8_t* h_index, std::uint64_t index_size, const std::uint8_t* h_footer,
+               std::uint32_t* crc) {
+  if ((index_size && !ptr_ok(h_index)) || !ptr_ok(h_footer)) return set_error(TKV_INVALID_ARGUMENT, "null pointer");
+  std::uint32_t raw = 0xFFFFFFFFu;
+  if (int rc = update_impl(kAlgoCrc32, raw, h_index, index_size, &raw)) return rc;
+  if (int rc = update_impl(kAlgoCrc32, raw, h_footer, TKV_SST_FOOTER_CRC_OFFSET, &raw)) return rc;
+  *crc = raw ^ 0xFFFFFFFFu;
+  return TKV_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int tkv_sst_stamp_footer(const uint8_t* h_index, uint64_t index_size, uint8_t* h_footer) {
+  std::uint32_t crc = 0;
+  if (int rc = footer_crc(h_index, index_size, h_footer, &crc)) return rc;
+  std::memcpy(h_footer + TKV_SST_FOOTER_CRC_OFFSET, &crc, 4);
+  return TKV_OK;
+}
+
+int tkv_sst_verify_footer(const uint8_t* h_index, uint64_t index_size, const uint8_t* h_footer) {
+  std::uint32_t crc = 0, stored = 0;
+  if (int rc = footer_crc(h_index, index_size, h_footer, &crc)) return rc;
+  std::memcpy(&stored, h_footer + TKV_SST_FOOTER_CRC_OFFSET, 4);
+  return stored == crc ? TKV_OK : set_error(TKV_CORRUPTED, "corrupted SSTable index or footer");
+}
+
 size_t tkv_debug_wal_chain(const uint8_t* h_wal, uint64_t size, uint64_t* out_pos, size_t cap, uint64_t* end,
                            int* err) {
   const Chain c = wal_chain(h_wal, size);

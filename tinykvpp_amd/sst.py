@@ -91,3 +91,51 @@ def block_crcs_device(file, offsets, sizes, store=False, out=None, stream=None):
         ctypes.c_void_p(file.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), ctypes.c_void_p(sizes.data_ptr()),
         ctypes.c_void_p(out.data_ptr()), offsets.numel(), int(bool(store)), _stream_ptr(stream)))
     return out
+
+
+# ---- index image + footer (include/tkv_crc32.h "SSTable index image + footer stamping") ----------
+FOOTER_SIZE = 20      # sizeof(sstable_footer) (sstable_format.hpp:129-135)
+FOOTER_CRC_OFFSET = 16
+
+
+def encode_index_image(entries):
+    """Index image as sstable_writer::get_index lays it out: u64 entry count, then per entry
+    write_string(smallest_key) | u64 data_block_offset | u64 data_block_size (write_string is
+    varint length + bytes, buffer_writer.hpp:75-77). ``entries`` is [(smallest_key, offset, size)]."""
+    out = bytearray(struct.pack("<Q", len(entries)))
+    for key, off, size in entries:
+        out += _varint(len(key)) + key + struct.pack("<QQ", off, size)
+    return bytes(out)
+
+
+def encode_footer(index_offset, index_size, bloom_offset=0, bloom_size=0):
+    """Unstamped 20-byte footer in sstable_footer declaration order (crc32_ = 0)."""
+    return struct.pack("<IIIII", index_offset, index_size, bloom_offset, bloom_size, 0)
+
+
+def _index_ptr(index_image):
+    buf = np.ascontiguousarray(np.frombuffer(index_image, np.uint8) if not isinstance(index_image, np.ndarray)
+                               else index_image)
+    return buf, buf.size
+
+
+def stamp_footer(index_image, footer):
+    """Stamped copy of ``footer`` (20 bytes): crc32_ = CRC-32 of index image || footer[0:16]."""
+    if len(footer) != FOOTER_SIZE:
+        raise ValueError("footer must be 20 bytes")
+    idx, n = _index_ptr(index_image)
+    f = (ctypes.c_uint8 * FOOTER_SIZE).from_buffer_copy(bytes(footer))
+    check(load_library().tkv_sst_stamp_footer(ctypes.c_void_p(idx.ctypes.data if n else 0), n, f))
+    return bytes(f)
+
+
+def verify_footer(index_image, footer):
+    """"ok" when the footer's crc32_ matches the index image and its own fields, else "corrupted"."""
+    if len(footer) != FOOTER_SIZE:
+        raise ValueError("footer must be 20 bytes")
+    idx, n = _index_ptr(index_image)
+    f = (ctypes.c_uint8 * FOOTER_SIZE).from_buffer_copy(bytes(footer))
+    rc = load_library().tkv_sst_verify_footer(ctypes.c_void_p(idx.ctypes.data if n else 0), n, f)
+    if rc not in (OK, CORRUPTED):
+        check(rc)
+    return "ok" if rc == OK else "corrupted"
