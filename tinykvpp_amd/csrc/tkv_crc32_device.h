@@ -335,7 +335,10 @@ __device__ __forceinline__ void fill_lds(const DeviceTables* tabs, std::uint32_t
 
 // MODE 0: CRC. MODE 1 (explorer only): same loads, XOR of the data instead of the CRC (memory
 // ceiling of this access pattern).
-template <bool ALIGNED, bool UNIFORM, int DEPTH, int ILP, int MODE>
+// SMALL (irregular batches): when a wave runs its share of the small-block phase. 0: before its
+// rows; 1: even waves before their rows, odd waves after them, so the phase's latency-bound steps
+// overlap other waves' row streaming instead of all waves idling the HBM at once; 2: after its rows.
+template <bool ALIGNED, bool UNIFORM, int DEPTH, int ILP, int MODE, int SMALL = 0>
 __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
   constexpr int NP = ALIGNED ? 4 : 5;
@@ -348,9 +351,11 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
     if (lane >= 32u) hcon = multmodp(a.head_z, 1u << (lane - 32u), a.tabs->poly);  // Shift_h(1 << (l-32))
   }
   __syncthreads();
-  if constexpr (!UNIFORM && MODE == 0) small_phase(a, lds);  // the batch's small blocks first
-
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool small_first = SMALL == 0 || (SMALL == 1 && (wave & 1u) == 0u);
+  if constexpr (!UNIFORM && MODE == 0) {
+    if (small_first) small_phase(a, lds);
+  }
   const std::uint64_t W = a.nwaves;
 
   // This wave's contiguous range of rows [g0, g1).
@@ -460,6 +465,9 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
     }
   }
 
+  if constexpr (!UNIFORM && MODE == 0) {
+    if (!small_first) small_phase(a, lds);
+  }
   if (lane == 0) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {

@@ -49,7 +49,13 @@ __global__ __launch_bounds__(1024) void k_pat(const std::uint8_t* base, std::uin
     // STR: the wave's j-th row is global row wave + j*W (all waves sweep one moving window)
     const std::uint64_t phys = STR ? static_cast<std::uint64_t>(gl - g0) * W + wave : gl;
     const std::uintptr_t rb = reinterpret_cast<std::uintptr_t>(base) + phys * 4096u;
-    if constexpr (PAT == 0) return rb + 64u * lane + 16u * i;
+    if constexpr (PAT >= 128) {
+      // lane-contiguous segments of PAT bytes: a tile of 64*PAT bytes is PAT/64 rows; its j-th row
+      // reads bytes [64j, 64j+64) of every lane's segment
+      constexpr std::uint32_t J = PAT / 64;
+      const std::uint64_t t = phys / J, j = phys % J;
+      return reinterpret_cast<std::uintptr_t>(base) + t * 64u * PAT + lane * PAT + 64u * j + 16u * i;
+    } else if constexpr (PAT == 0) return rb + 64u * lane + 16u * i;
     else if constexpr (PAT == 1) return rb + 1024u * i + 16u * lane;
     else return rb + 2048u * (i / 2) + 32u * lane + 16u * (i % 2);
   };
@@ -341,13 +347,15 @@ const V kVariants[] = {
     {"pat seg64 D4 fin2", P<0, 4, 2>}, {"pat coal D2 fin0", P<1, 2, 0>}, {"pat coal D4 fin0", P<1, 4, 0>},
     {"pat coal D4 fin1", P<1, 4, 1>}, {"pat coal D4 fin2", P<1, 4, 2>}, {"pat seg32 D4 fin0", P<2, 4, 0>},
     {"pat seg32 D4 fin2", P<2, 4, 2>}, {"pat coal D6 fin0", P<1, 6, 0>}, {"pat seg64 D6 fin0", P<0, 6, 0>},
+    {"pat seg128 D4 fin0", P<128, 4, 0>}, {"pat seg256 D4 fin0", P<256, 4, 0>},
+    {"pat seg1024 D4 fin0", P<1024, 4, 0>},
 };
 constexpr int kNV = sizeof(kVariants) / sizeof(kVariants[0]);
 
-template <int D, int I, int T>
+template <int D, int I, int T, int SM = 0>
 __global__ __launch_bounds__(T) void k_irr(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_rows_body<false, false, D, I, 0>(a, lds);
+  dev::crc_rows_body<false, false, D, I, 0, SM>(a, lds);
 }
 
 struct IV {
@@ -356,9 +364,9 @@ struct IV {
   void (*launch)(RowsArgs, hipStream_t);
 };
 
-template <int D, int I, int T>
+template <int D, int I, int T, int SM = 0>
 void LI(RowsArgs a, hipStream_t s) {
-  hipLaunchKernelGGL((k_irr<D, I, T>), dim3(g_ncu), dim3(T), 0, s, a);
+  hipLaunchKernelGGL((k_irr<D, I, T, SM>), dim3(g_ncu), dim3(T), 0, s, a);
 }
 
 const IV kIrr[] = {
@@ -366,6 +374,7 @@ const IV kIrr[] = {
     {"irr T1024 D4 I2", 1024, LI<4, 2, 1024>}, {"irr T512 D4 I2", 512, LI<4, 2, 512>},
     {"irr T512 D6 I2", 512, LI<6, 2, 512>}, {"irr T512 D6 I3", 512, LI<6, 3, 512>},
     {"irr T768 D4 I2", 768, LI<4, 2, 768>}, {"irr T512 D8 I4", 512, LI<8, 4, 512>},
+    {"irr T768 D4 I2 small-alt", 768, LI<4, 2, 768, 1>}, {"irr T768 D4 I2 small-last", 768, LI<4, 2, 768, 2>},
 };
 constexpr int kNIrr = sizeof(kIrr) / sizeof(kIrr[0]);
 void* g_blob = nullptr;

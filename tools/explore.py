@@ -55,9 +55,10 @@ if a.irregular:
     sp = ctypes.c_void_p(st.cuda_stream)
     args = lambda i: (i, ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(d_off.data_ptr()),
                       ctypes.c_void_p(d_len.data_ptr()), lens.size, ctypes.c_void_p(out.data_ptr()), sp)
-    res = {i: [] for i in range(len(names))}
+    sel = [i for i in range(len(names)) if not a.only or names[i] in a.only.split(",")]
+    res = {i: [] for i in sel}
     for r in range(a.rounds):
-        for i in range(len(names)):
+        for i in sel:
             out.zero_()
             assert lib.explore_run_irr(*args(i)) == 0
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -69,7 +70,7 @@ if a.irregular:
             res[i].append(total / (e0.elapsed_time(e1) / a.reps) / 1e6)
             if r == 0 and not torch.equal(out, ref):
                 print(f"MISMATCH {names[i]}", flush=True)
-    for i in range(len(names)):
+    for i in sel:
         v = np.array(res[i])
         print(f"{names[i]:22s} median {np.median(v):8.1f} GB/s  min {v.min():8.1f}  max {v.max():8.1f}  "
               f"({np.median(v) / 8000 * 100:5.1f}% of 8 TB/s)", flush=True)
