@@ -50,6 +50,11 @@ def load_tables(lib, poly=0xEDB88320):
     row_pow = buf[o:o + 64]; o += 64
     head = buf[o:o + (ROW + 1) * 32].reshape(ROW + 1, 32); o += (ROW + 1) * 32
     shift32 = buf[o:o + 128].reshape(8, 16); o += 128
+    rows_shift = buf[o:o + 4096]; o += 4096
+    # rows_shift[k] = x^(8*4096*k): rows_shift[0] = x^0, [1] = row_pow[0], [2^k] = row_pow[k]
+    assert int(rows_shift[0]) == 0x80000000
+    for k in range(12):
+        assert int(rows_shift[1 << k]) == int(buf[1024 + 8 * 16 * 64 + 64 + k])
     built_for = int(buf[o]); o += 4  # poly + 3 pad words
     assert o * 4 == n
     assert built_for == poly

@@ -124,6 +124,15 @@ __device__ __forceinline__ std::uint32_t shift_rows(const DeviceTables* t, std::
   return multmodp(m, reg, poly);
 }
 
+// reg * x^(8*kRow*k) mod P: one multiply for k < 4096 (rows_shift table), one more per set bit above.
+__device__ __forceinline__ std::uint32_t shift_rows_tab(const DeviceTables* t, std::uint32_t reg, std::uint32_t k) {
+  const std::uint32_t poly = t->poly;
+  std::uint32_t m = sload32(t->rows_shift, k & 4095u);
+  for (int i = 12; (k >> i) != 0u; ++i)
+    if ((k >> i) & 1u) m = multmodp(m, sload32(t->row_pow, static_cast<std::uint32_t>(i)), poly);
+  return multmodp(m, reg, poly);
+}
+
 struct Cursor {
   std::uint32_t b;          // block index
   std::uint32_t r;          // row within the block
@@ -294,9 +303,10 @@ __device__ __forceinline__ void finish_row(const RowsArgs& a, const Cursor& c, s
     } else {
       // (explicit slots: a runtime index into these arrays would put them in scratch memory)
       const std::uint32_t flags = kSeamValid | (st.piece_has_row0 ? kSeamHasRow0 : 0u);
-      if (st.piece_has_row0) {
+      if (UNIFORM && st.piece_has_row0) {
         // head piece of a block cut between waves: seed its result with xorout; crc_fixup XORs
-        // every piece's shifted partial into it (this kernel precedes crc_fixup on the stream)
+        // every piece's shifted partial into it (this kernel precedes crc_fixup on the stream).
+        // Irregular batches combine in this kernel instead (combine_seams).
         const std::uint32_t ob = a.out_idx ? sload32(a.out_idx, c.b) : c.b;
         if (lane == 0) a.out[ob] = a.out_xor;
       }
@@ -468,7 +478,20 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
   if constexpr (!UNIFORM && MODE == 0) {
     if (!small_first) small_phase(a, lds);
   }
-  if (lane == 0) {
+  if constexpr (!UNIFORM) {
+    // Irregular batches: the prepass zeroed the result of every block cut between waves, so each
+    // piece XORs its partial, moved past the rows that follow it, straight into the result (the
+    // head piece adds xorout): out = xorout ^ sum of pieces, in any order, with no fix-up launch.
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (st.s_flags[s] & kSeamValid) {
+        const std::uint32_t contrib = shift_rows_tab(a.tabs, st.s_part[s], st.s_after[s]) ^
+                                      ((st.s_flags[s] & kSeamHasRow0) ? a.out_xor : 0u);
+        const std::uint32_t ob = a.out_idx ? sload32(a.out_idx, st.s_block[s]) : st.s_block[s];
+        if (lane == 0) __hip_atomic_fetch_xor(a.out + ob, contrib, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  } else if (lane == 0) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       Seam rec;

@@ -28,7 +28,7 @@ hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
 hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st);
 hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
                           std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
-                          std::uint32_t W, hipStream_t st);
+                          std::uint32_t W, std::uint32_t* out, hipStream_t st);
 hipError_t launch_small(const RowsArgs& a, unsigned grid, hipStream_t st);
 std::uint32_t prepass_tiles(std::uint32_t n);
 hipError_t launch_fill_uniform(std::uint8_t* dst, std::uint64_t stride, std::uint64_t len, std::uint64_t first,
@@ -88,6 +88,11 @@ void build_tables(DeviceTables* t, std::uint32_t poly) {
   for (int k = 0; k < 64; ++k) {
     t->row_pow[k] = p;
     p = mm(p, p);
+  }
+  std::uint32_t rk = 0x80000000u;  // x^(8*kRow*k), k = 0..4095
+  for (int k = 0; k < 4096; ++k) {
+    t->rows_shift[k] = rk;
+    rk = mm(rk, mrow);
   }
   const std::uint32_t z32 = x8n(32);
   for (int j = 0; j < 8; ++j)
@@ -420,9 +425,8 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   a.out = d_out;
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = static_cast<std::uint32_t>(c->ncu) * kRowsWavesPerWG;
-  TKV_HIP(launch_prepass(d_off, d_len, a.nblocks, s->scan, s->tiles, s->counts, s->po, a.nwaves, st));
-  TKV_HIP(launch_rows(a, false, false, static_cast<unsigned>(c->ncu), st));
-  TKV_HIP(launch_fixup(a, st));
+  TKV_HIP(launch_prepass(d_off, d_len, a.nblocks, s->scan, s->tiles, s->counts, s->po, a.nwaves, d_out, st));
+  TKV_HIP(launch_rows(a, false, false, static_cast<unsigned>(c->ncu), st));  // combines its own seams
   return TKV_OK;
 }
 

@@ -50,6 +50,7 @@ struct DeviceTables {
   std::uint32_t row_pow[64];            // x^(8*kRow*2^k) mod P (reflected), k = 0..63
   std::uint32_t head_shift[kRow + 1][32];  // [h][i] = Shift_h(1 << i): init injection at a head row
   std::uint32_t shift32[8][16];         // [j][v] = Shift_32(v << 4j): joins two 32-byte half chains
+  std::uint32_t rows_shift[4096];       // [k] = x^(8*kRow*k) mod P: moves a piece's partial past k rows
   std::uint32_t poly;                   // reflected polynomial the tables were built for
   std::uint32_t pad_[3];
 };

@@ -132,12 +132,12 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
   }
 }
 
-__global__ void rows_finish(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
-                            const std::uint64_t* scan, const std::uint64_t* tile_offs, const std::uint32_t* counts,
-                            PrepassOut o, std::uint32_t W) {
-  const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
-  if (b >= n) return;
-  const std::uint64_t e = scan[b] + tile_offs[b / kScanTile];
+// Scatter of one block (rows_finish): e = its exclusive (small count, rows) pair, TR = rows of all
+// large blocks. A large block cut between row-kernel waves gets its result zeroed here, since the
+// row kernel XORs every piece of it into the result (crc_rows_body, irregular batches).
+__device__ __forceinline__ void finish_block(const std::uint64_t* offsets, const std::uint32_t* lengths,
+                                             std::uint64_t b, std::uint64_t e, std::uint64_t TR, const PrepassOut& o,
+                                             std::uint32_t W, std::uint32_t* out) {
   const std::uint32_t len = lengths[b];
   const std::uint32_t nsmall = static_cast<std::uint32_t>(e);
   if (len <= kSmallMax) {
@@ -153,11 +153,60 @@ __global__ void rows_finish(const std::uint64_t* offsets, const std::uint32_t* l
   o.big_idx[k] = static_cast<std::uint32_t>(b);
   o.row_scan[k] = static_cast<std::uint32_t>(lo);
   const std::uint64_t hi = lo + rows_for_len(len);
-  const std::uint64_t TR = counts[2];
   // waves whose first row g0(w) = floor(w*TR/W) lies in [lo, hi): w in [ceil(lo*W/TR), ceil(hi*W/TR))
   const std::uint64_t wlo = (lo * W + TR - 1) / TR;
   const std::uint64_t whi = (hi * W + TR - 1) / TR;
   for (std::uint64_t w = wlo; w < whi && w < W; ++w) o.wave_start[w] = k;
+  // cut iff some wave starts strictly inside the block (g0 is nondecreasing in w)
+  if (whi > wlo && (whi - 1) * TR / W > lo) out[b] = 0u;
+}
+
+__global__ void rows_finish(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
+                            const std::uint64_t* scan, const std::uint64_t* tile_offs, const std::uint32_t* counts,
+                            PrepassOut o, std::uint32_t W, std::uint32_t* out) {
+  const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+  if (b >= n) return;
+  finish_block(offsets, lengths, b, scan[b] + tile_offs[b / kScanTile], counts[2], o, W, out);
+}
+
+// rows_finish with the scan of the tile sums folded in (ntiles <= kFusedTiles): every workgroup sums
+// the tile sums in front of its own tile and over all tiles itself (at most 4 loads per thread), so
+// no single-workgroup tile-scan launch sits between the tile scan and the scatter. Workgroup 0
+// publishes counts for the row kernel.
+constexpr std::uint32_t kFusedTiles = 1024;
+constexpr std::uint32_t kFinishThreads = 256;
+__global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
+    const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n, const std::uint64_t* scan,
+    const std::uint64_t* tile_sums, std::uint32_t ntiles, std::uint32_t* counts, PrepassOut o, std::uint32_t W,
+    std::uint32_t* out) {
+  __shared__ std::uint64_t red[2][kFinishThreads];
+  const std::uint32_t my_tile = blockIdx.x * kFinishThreads / kScanTile;  // kScanTile % 256 == 0
+  std::uint64_t before = 0, all = 0;
+  for (std::uint32_t i = threadIdx.x; i < ntiles; i += kFinishThreads) {
+    const std::uint64_t v = tile_sums[i];
+    all += v;
+    before += i < my_tile ? v : 0ull;
+  }
+  red[0][threadIdx.x] = before;
+  red[1][threadIdx.x] = all;
+  __syncthreads();
+  for (std::uint32_t h = kFinishThreads / 2; h > 0; h >>= 1) {
+    if (threadIdx.x < h) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + h];
+      red[1][threadIdx.x] += red[1][threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  const std::uint64_t tile_off = red[0][0], total = red[1][0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const std::uint32_t ns = static_cast<std::uint32_t>(total);
+    counts[0] = n - ns;                                    // large blocks
+    counts[1] = ns;                                        // small blocks
+    counts[2] = static_cast<std::uint32_t>(total >> 32);  // rows of the large blocks
+  }
+  const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(kFinishThreads) + threadIdx.x;
+  if (b >= n) return;
+  finish_block(offsets, lengths, b, scan[b] + tile_off, total >> 32, o, W, out);
 }
 
 // ---- synthetic data: byte j of block b = LE byte j%8 of
@@ -249,12 +298,17 @@ hipError_t launch_fixup(const RowsArgs& a, hipStream_t st) {
 
 hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
                           std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
-                          std::uint32_t W, hipStream_t st) {
+                          std::uint32_t W, std::uint32_t* out, hipStream_t st) {
   const std::uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
   hipLaunchKernelGGL(rows_tile_scan, dim3(ntiles), dim3(1024), 0, st, lengths, n, scan, tile_sums);
-  hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, ntiles, n, counts);
-  hipLaunchKernelGGL(rows_finish, dim3((n + 255) / 256), dim3(256), 0, st, offsets, lengths, n, scan, tile_sums,
-                     counts, o, W);
+  if (ntiles <= kFusedTiles) {
+    hipLaunchKernelGGL(rows_finish_fused, dim3((n + kFinishThreads - 1) / kFinishThreads), dim3(kFinishThreads), 0,
+                       st, offsets, lengths, n, scan, tile_sums, ntiles, counts, o, W, out);
+  } else {
+    hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, ntiles, n, counts);
+    hipLaunchKernelGGL(rows_finish, dim3((n + 255) / 256), dim3(256), 0, st, offsets, lengths, n, scan, tile_sums,
+                       counts, o, W, out);
+  }
   return hipGetLastError();
 }
 

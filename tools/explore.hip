@@ -390,7 +390,7 @@ namespace tkv {
 hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
 hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
                           std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
-                          std::uint32_t W, hipStream_t st);
+                          std::uint32_t W, std::uint32_t* out, hipStream_t st);
 hipError_t launch_small(const RowsArgs& a, unsigned grid, hipStream_t st);
 }  // namespace tkv
 
@@ -493,9 +493,8 @@ extern "C" int explore_run_irr(int v, const std::uint8_t* base, const std::uint6
   a.dummy = g_dummy;
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = g_ncu * (kIrr[v].threads / 64);
-  launch_prepass(off, len, a.nblocks, g_scan64, g_tiles64, g_counts, g_po, a.nwaves, st);
+  launch_prepass(off, len, a.nblocks, g_scan64, g_tiles64, g_counts, g_po, a.nwaves, out, st);
   kIrr[v].launch(a, st);
-  launch_fixup(a, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
