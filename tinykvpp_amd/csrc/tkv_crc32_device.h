@@ -649,11 +649,17 @@ __device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t*
 // divisions, selects instead of divergent branches.
 // CHK (explorer only, R1, nblocks a multiple of 64*waves): chunk-strided map - wave w owns chunks
 // w, w+W, w+2W, ... of 2^CHK consecutive blocks instead of one contiguous range.
-template <int DEPTH, int ILP, bool R1, bool SPLIT = false, std::uint32_t ROT = 0, int CHK = 0>
-__device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds) {
+// PROG (explorer only): lane 0 stamps s_memrealtime into a.prog[wave * kProgSlots + s] after the table
+// fill (s = 0), before every PROG-th row (s = 1 + j / PROG) and at the end (last slot used + 1).
+// SUB: the caller has filled the LDS tables and passes the wave's block range [sub_b0, sub_b0 + sub_nb)
+// (crc_packed_xq_body's static region).
+template <int DEPTH, int ILP, bool R1, bool SPLIT = false, std::uint32_t ROT = 0, int CHK = 0, int PROG = 0,
+          bool SUB = false>
+__device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds, std::uint32_t sub_b0 = 0,
+                                                std::uint32_t sub_nb = 0) {
   static_assert(CHK == 0 || (R1 && ROT == 0 && CHK <= 6), "chunk-strided map: R1 only, chunks of <= 64 blocks");
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
-  fill_lds(a.tabs, lds);
+  if constexpr (!SUB) fill_lds(a.tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
   const LaneConst kc = lane_const(lane);
   const std::uint32_t hcon = a.tabs->horner[lane & 31u];  // Shift_4096(1 << (l & 31))
@@ -668,13 +674,14 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
     s32lo = (&a.tabs->shift32[0][0])[lane];
     s32hi = (&a.tabs->shift32[0][0])[64 + lane];
   }
-  __syncthreads();
+  if constexpr (!SUB) __syncthreads();
 
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint64_t W = a.nwaves;
   const std::uint32_t R = R1 ? 1u : a.len / kRow;
-  const std::uint32_t b0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W);
-  const std::uint32_t nb = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W) - b0;
+  const std::uint32_t b0 = SUB ? sub_b0 : static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W);
+  const std::uint32_t nb =
+      SUB ? sub_nb : static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W) - b0;
   if (nb == 0) return;
   const std::uint32_t nrows = nb * R;  // wave-local rows j = 0 .. nrows-1, contiguous in memory
   // CHK: global block of wave-local block j
@@ -687,6 +694,13 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
   // any instant the waves sit at different offsets inside their ranges (address bits below the
   // range size differ from wave to wave instead of being equal).
   const std::uint32_t rot_b = ROT ? static_cast<std::uint32_t>((wave * static_cast<std::uint64_t>(ROT)) % nb) : 0u;
+  auto stamp = [&](std::uint32_t slot) {
+    if constexpr (PROG > 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0 && slot < kProgSlots) a.prog[static_cast<std::uint64_t>(wave) * kProgSlots + slot] = t;
+    }
+  };
+  stamp(0);
   const std::uint32_t rotr = rot_b * R;
 
   uint4 buf[DEPTH][4];
@@ -743,6 +757,9 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
 #pragma unroll
   for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
   for (std::uint32_t j = 0; j < nrows; j += DEPTH) {
+    if constexpr (PROG > 0) {
+      if (j % PROG == 0) stamp(1 + j / PROG);
+    }
 #pragma unroll
     for (int q = 0; q < DEPTH; q += ILP) {
 #pragma unroll
@@ -820,6 +837,7 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
       }
     }
   }
+  if constexpr (PROG > 0) stamp(2 + (nrows - 1) / PROG);
 }
 
 // Packed kernel with dynamic work distribution inside each workgroup. The batch is cut into chunks

@@ -95,7 +95,9 @@ struct RowsArgs {
   const std::uint64_t* s_off;
   const std::uint32_t* s_len;
   const std::uint32_t* s_idx;
+  unsigned long long* prog;          // explorer only: per-wave progress stamps (crc_packed_body PROG)
 };
+constexpr std::uint32_t kProgSlots = 64;
 
 // Outputs of the irregular prepass (scratch of one stream).
 struct PrepassOut {

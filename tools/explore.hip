@@ -10,6 +10,238 @@
 
 using namespace tkv;
 
+namespace tkv::dev {
+// (explorer only; measured slower than the static packed body)
+// Packed kernel with chip-wide dynamic work distribution (per-XCD queues with stealing). Two launches
+// of the static body overlapped on two streams run 6 % faster than back to back
+// (tools/overlap_probe.py), and per-wave progress stamps (tools/progress_probe.py) show why: a launch
+// ends with ~140 us at half rate, while the waves that finished early (p10 at 0.6 of the span) leave
+// their CUs idle. Here the batch is split in two regions:
+// - static (SF/16 of the blocks; SF = 0: none): wave w owns a contiguous range, as crc_packed_body;
+// - pool (the rest), cut into chunks of C whole blocks (C*R rows, >= CROWS, a multiple of DEPTH).
+//   Chunk range y of 8 equal ranges is the pool of the workgroups with blockIdx % 8 == y (their
+//   round-robin XCD, a label only); a wave whose pool is dry steals from the following pools.
+// With SF = 0 a wave's first chunk is static (the pool's i-th chunk for its i-th wave). Chunk ids
+// come from the pool's head counter, requested one chunk ahead and read after the first iteration
+// of the current chunk (crc_packed_dyn_body), so the request never drains the row pipeline.
+// ctr[y * kCtrStride] is pool y's head, ctr[8 * kCtrStride] counts finished waves; the last wave to
+// finish zeroes them all for the next launch on this stream (they must be zero before the first).
+// PERM != 0 (explorer): the pool's q-th chunk is chunk (q * PERM) mod pool size (sizes powers of 2).
+template <int DEPTH, int ILP, bool R1, int CROWS, std::uint32_t PERM = 0, int SF = 0>
+__device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
+  static_assert(CROWS % DEPTH == 0 && CROWS >= 2 * DEPTH && CROWS <= 64, "chunk shape");
+  static_assert(SF >= 0 && SF < 16, "static share in 1/16ths");
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t wpg = blockDim.x >> 6;
+  fill_lds(a.tabs, lds);
+  const LaneConst kc = lane_const(lane);
+  const std::uint32_t hcon = a.tabs->horner[lane & 31u];
+  const bool lo_half = lane < 32u;
+  const std::uint32_t inj_const =
+      lo_half ? 0u
+              : static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(a.init_default),
+                                                                lane & 31u, 1)) & hcon;
+  __syncthreads();
+
+  const std::uint32_t R = R1 ? 1u : a.len / kRow;
+  std::uint32_t C = R1 ? static_cast<std::uint32_t>(CROWS) : (CROWS + R - 1) / R;
+  if (!R1)
+    while ((C * R) % DEPTH) ++C;
+  const std::uint32_t G = gridDim.x;
+  const std::uint32_t W = G * wpg;
+  const std::uint32_t wave = blockIdx.x * wpg + wid;
+  // static region [0, S): wave w owns [w*S/W, (w+1)*S/W); pool region [S, nblocks)
+  const std::uint32_t S = SF ? static_cast<std::uint32_t>(static_cast<std::uint64_t>(a.nblocks) * SF / 16u) : 0u;
+  const std::uint32_t NC = (a.nblocks - S + C - 1) / C;  // pool chunks; only the last is partial
+  const std::uint64_t brow = static_cast<std::uint64_t>(R) * kRow;  // bytes per block
+  const std::uintptr_t loff = lane * kSeg;
+
+  std::uint32_t vzero;  // opaque zero: keeps the atomic optimizer from draining (crc_packed_dyn_body)
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+  std::uint32_t* const vctr = a.wg_ctr + vzero;
+  auto plo = [&](std::uint32_t y) { return static_cast<std::uint32_t>(static_cast<std::uint64_t>(y) * NC / 8u); };
+  auto psize = [&](std::uint32_t y) { return plo(y + 1) - plo(y); };
+  // pool chunks handed out statically (SF = 0 only): one per wave of the pool's workgroups
+  auto pstat = [&](std::uint32_t y) { return (SF == 0 && y < G) ? ((G - 1u - y) / 8u + 1u) * wpg : 0u; };
+  const std::uint32_t xp = blockIdx.x & 7u;
+  const std::uint32_t xi = (blockIdx.x >> 3) * wpg + wid;  // wave index inside its pool
+
+  struct Chunk {
+    std::uint32_t fb, nb, vrows, nit;  // first block, blocks, rows holding data, iterations
+    std::uintptr_t base;               // address of its first row
+  };
+  auto span = [&](std::uint32_t fb, std::uint32_t nb) {
+    Chunk c;
+    c.fb = fb;
+    c.nb = nb;
+    c.vrows = nb * R;
+    c.nit = (c.vrows + DEPTH - 1) / DEPTH;
+    c.nit = c.nit < 2u ? 2u : c.nit;
+    c.base = reinterpret_cast<std::uintptr_t>(a.base) + static_cast<std::uint64_t>(fb) * brow;
+    return c;
+  };
+  auto pchunk = [&](std::uint32_t y, std::uint32_t q) {  // q-th chunk of pool y
+    if constexpr (PERM != 0) q = static_cast<std::uint32_t>((static_cast<std::uint64_t>(q) * PERM) % psize(y));
+    const std::uint32_t fb = S + (plo(y) + q) * C;
+    return span(fb, a.nblocks - fb < C ? a.nblocks - fb : C);
+  };
+  auto load_row = [&](std::uintptr_t rowp, uint4 (&q)[4]) {
+    const std::uintptr_t p = rowp + loff;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i);
+  };
+  std::uint32_t gp = xp;   // pool the pending grab goes to
+  std::uint32_t seen = 0;  // pools found exhausted
+  auto grab = [&]() -> std::uint32_t {
+    std::uint32_t v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(vctr + gp * kCtrStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+  };
+  // Blocking search from pool gp on (start, and after a pool runs dry): false once all 8 are dry.
+  auto steal = [&](Chunk& out) -> bool {
+    while (seen < 8u) {
+      const std::uint32_t q = pstat(gp) + __builtin_amdgcn_readfirstlane(grab());
+      if (q < psize(gp)) {
+        out = pchunk(gp, q);
+        return true;
+      }
+      ++seen;
+      gp = (gp + 1u) & 7u;
+    }
+    return false;
+  };
+
+  Chunk cur{}, nxt{};
+  bool live = true;
+  if constexpr (SF != 0) {  // static region: the packed loop itself (no per-row chunk bookkeeping)
+    const std::uint32_t s0 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave) * S / W);
+    const std::uint32_t s1 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave + 1) * S / W);
+    if (s1 > s0) dev::crc_packed_body<DEPTH, ILP, R1, false, 0, 0, 0, true>(a, lds, s0, s1 - s0);
+  }
+  if (!SF && xi < psize(xp)) cur = pchunk(xp, xi);
+  else live = steal(cur);
+  if (live) {
+    std::uint32_t nv = grab();
+    bool nvalid = false;
+    uint4 buf[DEPTH][4];
+    auto prologue = [&]() {
+#pragma unroll
+      for (int s = 0; s < DEPTH - ILP; ++s)
+        load_row(cur.base + static_cast<std::uint64_t>(s < static_cast<int>(cur.vrows) ? s : cur.vrows - 1) * kRow,
+                 buf[s]);
+    };
+    prologue();
+    std::uint32_t it = 0, B = 0, r = 0, kb = 0, keep = 0;
+    for (;;) {
+      const std::uint32_t row0 = it * DEPTH;
+      const bool last_it = it + 1 == cur.nit;
+      const std::uintptr_t clast = cur.base + static_cast<std::uint64_t>(cur.vrows - 1) * kRow;
+#pragma unroll
+      for (int q = 0; q < DEPTH; q += ILP) {
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) {
+          const int x = q + DEPTH - ILP + i;  // issue row row0 + x
+          std::uintptr_t rp;
+          if (x < DEPTH || !last_it) {
+            const std::uint32_t ri = row0 + x;
+            rp = ri < cur.vrows ? cur.base + static_cast<std::uint64_t>(ri) * kRow : clast;
+          } else {
+            const std::uint32_t ri = x - DEPTH;  // row of the next chunk
+            const std::uint32_t rn = ri < nxt.vrows ? ri : nxt.vrows - 1;
+            rp = nvalid ? nxt.base + static_cast<std::uint64_t>(rn) * kRow : clast;
+          }
+          load_row(rp, buf[x % DEPTH]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        Reg p[ILP];
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) p[i] = Reg{0, 0};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+          for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].x, kc);
+#pragma unroll
+          for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].y, kc);
+#pragma unroll
+          for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].z, kc);
+#pragma unroll
+          for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].w, kc);
+        }
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) {
+          const std::uint32_t v = lane_shift(lds, p[i].value(), kc);
+          if (row0 + q + i < cur.vrows) {
+            std::uint32_t term;
+            if (R1 || r == 0) {
+              term = inj_const;
+              if (a.init_raw) {
+                const std::uint32_t init = sload32(a.init_raw, cur.fb + kb);
+                term = lo_half ? 0u
+                               : static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init),
+                                                                                  lane & 31u, 1)) & hcon;
+              }
+            } else {
+              term = lo_half ? static_cast<std::uint32_t>(
+                                   __builtin_amdgcn_sbfe(static_cast<std::int32_t>(B), lane, 1)) & hcon
+                             : 0u;
+            }
+            const std::uint32_t Bn = __builtin_amdgcn_readlane(wave_xor_to_lane63(v ^ term), 63);
+            if (R1 || ++r == R) {
+              keep = lane == (kb & 63u) ? (Bn ^ a.out_xor) : keep;
+              ++kb;
+              if ((kb & 63u) == 0u) a.out[cur.fb + kb - 64u + lane] = keep;  // 64 results at a time
+              r = 0;
+              B = 0;
+            } else {
+              B = Bn;
+            }
+          }
+        }
+        if (q == 0 && it == 1) {  // rows just processed were issued after the grab: its id is back
+          const std::uint32_t qn = pstat(gp) + __builtin_amdgcn_readfirstlane(nv);
+          nvalid = qn < psize(gp);
+          if (nvalid) nxt = pchunk(gp, qn);
+        }
+      }
+      if (last_it) {
+        if (kb & 63u) {
+          const std::uint32_t first = kb & ~63u;
+          if (lane < (kb & 63u)) a.out[cur.fb + first + lane] = keep;
+        }
+        it = 0;
+        kb = 0;
+        if (nvalid) {
+          cur = nxt;
+          nvalid = false;
+          nv = grab();
+        } else {  // pool gp ran dry: search the others, then restart the row pipeline
+          ++seen;
+          gp = (gp + 1u) & 7u;
+          if (!steal(cur)) break;
+          nv = grab();
+          prologue();
+        }
+      } else {
+        ++it;
+      }
+    }
+  }
+  // The last wave out zeroes the pool heads and the exit count for the next launch.
+  if (lane == 0) {
+    std::uint32_t* done = vctr + 8u * kCtrStride;
+    if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == W - 1u) {
+#pragma unroll
+      for (std::uint32_t y = 0; y < 8u; ++y)
+        __hip_atomic_store(vctr + y * kCtrStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace tkv::dev
+
 template <int D, int I, int M>
 __global__ __launch_bounds__(kThreads) void k_rows(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
@@ -300,6 +532,49 @@ void PD(RowsArgs a, hipStream_t s) {
   else hipLaunchKernelGGL((k_packed_dyn<D, I, false, T, CR>), dim3(g_ncu), dim3(T), 0, s, a);
 }
 
+template <int D, int I, bool R1, int T, int CR, std::uint32_t PM, int SF>
+__global__ __launch_bounds__(T) void k_packed_xq(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  dev::crc_packed_xq_body<D, I, R1, CR, PM, SF>(a, lds);
+}
+
+std::uint32_t* g_xq = nullptr;  // pool heads + exit count of the xq variants (zeroed once)
+
+template <int D, int I, int CR, std::uint32_t PM = 0, int SF = 0, int T = 1024>
+void PX(RowsArgs a, hipStream_t s) {
+  a.wg_ctr = g_xq;
+  if (a.len == kRow) hipLaunchKernelGGL((k_packed_xq<D, I, true, T, CR, PM, SF>), dim3(g_ncu), dim3(T), 0, s, a);
+  else hipLaunchKernelGGL((k_packed_xq<D, I, false, T, CR, PM, SF>), dim3(g_ncu), dim3(T), 0, s, a);
+}
+
+// Start-stagger probe: before the production packed body, each wave (PERWAVE) or workgroup sleeps
+// a pseudo-random 0..K-1 units of s_sleep 127 (~4 us each), so that waves do not all walk their
+// ranges in lockstep from the same moment.
+template <int K, bool PERWAVE>
+__global__ __launch_bounds__(1024) void k_packed_stag(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  const std::uint32_t id = PERWAVE ? blockIdx.x * 16u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : blockIdx.x;
+  const std::uint32_t n = ((id * 2654435761u) >> 16) % K;
+  for (std::uint32_t i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+  if (a.len == kRow) dev::crc_packed_body<4, 2, true>(a, lds);
+  else dev::crc_packed_body<4, 2, false>(a, lds);
+}
+
+template <int K, bool PW>
+void PS(RowsArgs a, hipStream_t s) {
+  a.nwaves = g_ncu * 16;
+  hipLaunchKernelGGL((k_packed_stag<K, PW>), dim3(g_ncu), dim3(1024), 0, s, a);
+}
+
+// grid of M workgroups per CU (M rounds): a CU whose workgroup finishes early takes the next one
+template <int M>
+void PG(RowsArgs a, hipStream_t s) {
+  a.nwaves = g_ncu * M * 16;
+  if (a.len == kRow && a.nblocks >= a.nwaves)
+    hipLaunchKernelGGL((k_packed<4, 2, true, 1024, false>), dim3(g_ncu * M), dim3(1024), 0, s, a);
+  else hipLaunchKernelGGL((k_packed<4, 2, false, 1024, false>), dim3(g_ncu * M), dim3(1024), 0, s, a);
+}
+
 template <int D, int I, int T = 1024, bool SP = false>
 void PK(RowsArgs a, hipStream_t s) {
   a.nwaves = g_ncu * (T / 64);
@@ -329,6 +604,12 @@ const V kVariants[] = {
     {"packed rot1", PR<1>}, {"packed rot61", PR<61>}, {"packed rot16", PR<16>},
     {"dyn D4 I2 C8", PD<4, 2, 8>}, {"dyn D4 I2 C16", PD<4, 2, 16>}, {"dyn D4 I2 C32", PD<4, 2, 32>},
     {"dyn D4 I2 C64", PD<4, 2, 64>}, {"dyn T768 D4 I2 C16", PD<4, 2, 16, 768>},
+    {"xq D4 I2 C16", PX<4, 2, 16>},
+    {"hy S14 C8", PX<4, 2, 8, 0, 14>}, {"hy S12 C8", PX<4, 2, 8, 0, 12>}, {"hy S10 C8", PX<4, 2, 8, 0, 10>},
+    {"hy S12 C16", PX<4, 2, 16, 0, 12>}, {"hy S12 C32", PX<4, 2, 32, 0, 12>}, {"hy S8 C16", PX<4, 2, 16, 0, 8>},
+    {"stag wave 4", PS<4, true>}, {"stag wave 16", PS<16, true>}, {"stag wg 4", PS<4, false>},
+    {"stag wg 16", PS<16, false>}, {"stag wave 1", PS<1, true>},
+    {"grid x2", PG<2>}, {"grid x3", PG<3>}, {"grid x4", PG<4>}, {"grid x8", PG<8>}, {"grid x16", PG<16>},
     {"packed D4 I2", PK<4, 2>}, {"packed D4 I1", PK<4, 1>}, {"packed D3 I1", PK<3, 1>},
     {"packed T512 D8 I4", PK<8, 4, 512>}, {"packed T512 D6 I3", PK<6, 3, 512>},
     {"packed T768 D6 I2", PK<6, 2, 768>}, {"packed T768 D6 I3", PK<6, 3, 768>},
@@ -413,6 +694,8 @@ extern "C" int explore_run(int v, const std::uint8_t* base, std::uint64_t n, std
     hipMemset(g_dummy, 0, 256);
     hipMalloc(&g_seams, sizeof(Seam) * 2 * g_ncu * kWavesPerWG);
     hipMalloc(&g_ctr, 4 * kCtrStride * g_ncu);
+    hipMalloc(&g_xq, 4 * kCtrStride * 9);
+    hipMemset(g_xq, 0, 4 * kCtrStride * 9);
   }
   if (v == kNV) {
     hipLaunchKernelGGL(k_stream<256>, dim3(g_ncu * 8), dim3(256), 0, st, reinterpret_cast<const uint4*>(base),
@@ -517,5 +800,33 @@ extern "C" int explore_stamped(const std::uint8_t* base, std::uint64_t n, std::u
   a.wg_ctr = g_ctr;
   if (dyn) hipLaunchKernelGGL(k_dyn_stamped, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
   else hipLaunchKernelGGL(k_packed_stamped, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Progress stamps of the production packed body (tools/progress_probe.py).
+template <bool R1, int PROG>
+__global__ __launch_bounds__(1024) void k_packed_prog(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  dev::crc_packed_body<4, 2, R1, false, 0, 0, PROG>(a, lds);
+}
+
+extern "C" int explore_prog(const std::uint8_t* base, std::uint64_t n, std::uint32_t len, std::uint32_t* out,
+                            unsigned long long* stamps, void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!g_tabs && explore_run(kNV, base, 0, 16, out, stream)) return 1;
+  RowsArgs a{};
+  a.base = base;
+  a.stride = len;
+  a.len = len;
+  a.init_default = 0xFFFFFFFFu;
+  a.out_xor = 0xFFFFFFFFu;
+  a.out = out;
+  a.tabs = g_tabs;
+  a.dummy = g_dummy;
+  a.nblocks = static_cast<std::uint32_t>(n);
+  a.nwaves = g_ncu * 16;
+  a.prog = stamps;
+  if (len == kRow) hipLaunchKernelGGL((k_packed_prog<true, 16>), dim3(g_ncu), dim3(1024), 0, st, a);
+  else hipLaunchKernelGGL((k_packed_prog<false, 64>), dim3(g_ncu), dim3(1024), 0, st, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

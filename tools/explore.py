@@ -97,7 +97,7 @@ for r in range(a.rounds):
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / a.reps
         res[i].append(n * a.len / ms / 1e6)
-        if r == 0 and names[i].startswith(("crc", "packed", "dyn")):
+        if r == 0 and names[i].startswith(("crc", "packed", "dyn", "xq")):
             ok = torch.equal(out, ref)
             if not ok:
                 print(f"MISMATCH {names[i]}", flush=True)
