@@ -63,6 +63,12 @@ int tkv_crc32_update(uint32_t raw_state, const void *data, size_t len, uint32_t 
 int tkv_crc32_update_device(uint32_t raw_state, const void *d_data, size_t len, uint32_t *d_out_raw,
                             void *stream);
 
+/* CRC of the concatenation A || B from crc1 = CRC(A), crc2 = CRC(B) (finalized values) and
+ * len2 = |B| (zlib's crc32_combine): Shift_len2(crc1) ^ crc2, GF(2) arithmetic on the 4-byte
+ * values only (host, no data, no device). The reference has no equivalent; it serves callers that
+ * checksum the pieces of one record or file separately (the multi-device batch does this itself). */
+uint32_t tkv_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+
 /* ---- batch APIs (new: the reference has only per-record calls, wal.cpp:54-57,89-92) ------------ */
 
 /* Irregular batch in device memory: block i is [d_base + d_offsets[i], + d_lengths[i]) (any
@@ -87,7 +93,9 @@ int tkv_crc32_batch_host(const uint8_t *h_base, const uint64_t *h_offsets, const
                          const uint32_t *h_init_raw, uint32_t *h_out_final, uint64_t n);
 
 /* Same, split across `ndev` devices by bytes (one host thread and stream pair per device, no
- * collective). */
+ * collective). A block of at least 1 MiB that straddles the boundary between two devices' byte
+ * shares is cut there; its pieces run on both devices and their registers combine on the host
+ * (tkv_crc32_combine), so one huge block also spreads over the devices. */
 int tkv_crc32_batch_host_multi(const int *devices, int ndev, const uint8_t *h_base, const uint64_t *h_offsets,
                                const uint32_t *h_lengths, const uint32_t *h_init_raw, uint32_t *h_out_final,
                                uint64_t n);
@@ -172,6 +180,7 @@ int tkv_crc32c_batch_host(const uint8_t *h_base, const uint64_t *h_offsets, cons
 int tkv_crc32c_batch_host_multi(const int *devices, int ndev, const uint8_t *h_base, const uint64_t *h_offsets,
                                 const uint32_t *h_lengths, const uint32_t *h_init_raw, uint32_t *h_out_final,
                                 uint64_t n);
+uint32_t tkv_crc32c_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
 
 /* ---- synthetic data (SURVEY.md §8d generator; bench/test inputs) ------------------------------- */
 

@@ -272,3 +272,23 @@ def test_model_small_block_groups(model, oracle):
                 v ^= int(model.lane[j][(p[g] >> (4 * j)) & 15, 48 + g])
             v ^= bits_dot(init & (1 << g), model.head[n]) ^ bits_dot(init & (1 << (16 + g)), model.head[n])
         assert v ^ 0xFFFFFFFF == oracle.update(init, data.tobytes()) ^ 0xFFFFFFFF
+
+
+def test_combine_matches_concatenation(lib, oracle):
+    """tkv_crc32_combine / tkv_crc32c_combine (host arithmetic on 4-byte values, no device): the CRC
+    of A || B from CRC(A), CRC(B), |B|, against zlib.crc32 and the oracle's CRC-32C of the
+    concatenation; empty pieces included."""
+    import zlib
+    rng = np.random.default_rng(31)
+    for la, lb in [(0, 0), (0, 5), (7, 0), (1, 1), (100, 3), (4096, 4097), (70000, 123457)]:
+        a = rng.integers(0, 256, la, dtype=np.uint8).tobytes()
+        b = rng.integers(0, 256, lb, dtype=np.uint8).tobytes()
+        assert lib.tkv_crc32_combine(zlib.crc32(a), zlib.crc32(b), lb) == zlib.crc32(a + b)
+        assert tk.crc32_combine(oracle.crc(a), oracle.crc(b), lb) == oracle.crc(a + b)
+        assert (tk.crc32_combine(oracle.crc_c(a), oracle.crc_c(b), lb, algo="crc32c") ==
+                oracle.crc_c(a + b))
+    # lengths far beyond any buffer: Shift_n by square-and-multiply; Shift_m(Shift_n(x)) = Shift_(m+n)(x)
+    x = 0x12345678
+    n, m = (1 << 40) + 3, (1 << 33) + 11
+    assert (lib.tkv_crc32_combine(lib.tkv_crc32_combine(x, 0, n), 0, m) ==
+            lib.tkv_crc32_combine(x, 0, n + m))

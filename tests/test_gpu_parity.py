@@ -347,6 +347,27 @@ def test_host_batch_block_larger_than_slab(gpu, oracle):
     assert [int(x) for x in got] == want
 
 
+@pytest.mark.parametrize("ndev", [2, 3, 4])
+def test_host_multi_splits_large_blocks(gpu, oracle, ndev):
+    """Blocks of >= 1 MiB that straddle a device share are cut at the share boundary and their
+    pieces combine on the host: a single 9 MiB block over ndev devices, and a mixed batch
+    with per-block initial registers, both equal to the oracle. Device 0 stands in for every device."""
+    rng = np.random.default_rng(41 + ndev)
+    n = 9 << 20
+    host = rng.integers(0, 256, n + 4096, dtype=np.uint8)
+    got = tk.crc32_batch_host(host, [3], [n], devices=[0] * ndev)
+    assert int(got[0]) == oracle.crc(host[3:3 + n].tobytes())
+    offs = np.array([0, 5, (3 << 20) + 9, 17, (5 << 20) + 1, 11], np.uint64)
+    lens = np.array([(3 << 20) + 1, 0, (2 << 20) + 77, 100, 1 << 20, (4 << 20) - 3], np.uint32)
+    init = rng.integers(0, 1 << 32, offs.size, dtype=np.uint64).astype(np.uint32)
+    for algo in ("crc32", "crc32c"):
+        got = tk.crc32_batch_host(host, offs, lens, init_raw=init, devices=[0] * ndev, algo=algo)
+        want = tk.crc32_batch_host(host, offs, lens, init_raw=init, algo=algo)
+        assert np.array_equal(got, want)
+    assert np.array_equal(tk.crc32_batch_host(host, offs, lens, init_raw=init, devices=[0] * ndev),
+                          oracle.batch(host, offs, lens, init))
+
+
 def pinned_copy(a):
     """numpy view of a pinned (hipHostMalloc) copy of ``a``: the kernels can read it in place."""
     t = torch.empty(a.size, dtype=torch.uint8).pin_memory()

@@ -11,6 +11,7 @@ from .crc32 import (  # noqa: F401
     crc32_batch,
     crc32_batch_host,
     crc32_batch_uniform,
+    crc32_combine,
     crc32c,
     device_count,
     fill_synthetic_blocks,

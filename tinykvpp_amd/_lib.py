@@ -42,6 +42,7 @@ SIGNATURES = {
     "tkv_crc32_batch_uniform_device": (_int, [_u8p, _u64, _u64, _vp, _vp, _u64, _vp]),
     "tkv_crc32_batch_host": (_int, [_u8p, _vp, _vp, _vp, _vp, _u64]),
     "tkv_crc32_batch_host_multi": (_int, [_vp, _int, _u8p, _vp, _vp, _vp, _vp, _u64]),
+    "tkv_crc32_combine": (_u32, [_u32, _u32, _u64]),
     "tkv_wal_verify": (_int, [_u8p, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "tkv_wal_stamp": (_int, [_u8p, _vp, _vp, _u64]),
     "tkv_fill_synthetic_uniform": (_int, [_u8p, _u64, _u64, _u64, _u64, _u64, _vp]),
@@ -57,6 +58,7 @@ SIGNATURES = {
     "tkv_crc32c_batch_uniform_device": (_int, [_u8p, _u64, _u64, _vp, _vp, _u64, _vp]),
     "tkv_crc32c_batch_host": (_int, [_u8p, _vp, _vp, _vp, _vp, _u64]),
     "tkv_crc32c_batch_host_multi": (_int, [_vp, _int, _u8p, _vp, _vp, _vp, _vp, _u64]),
+    "tkv_crc32c_combine": (_u32, [_u32, _u32, _u64]),
     "tkv_debug_tables": (_sz, [_vp, _sz]),
     "tkv_debug_tables_poly": (_sz, [_u32, _vp, _sz]),
     "tkv_debug_multmodp": (_u32, [_u32, _u32]),

@@ -182,6 +182,11 @@ def crc32_batch_host(data, offsets, lengths, init_raw=None, devices=None, algo="
     return out
 
 
+def crc32_combine(crc1, crc2, len2, algo="crc32"):
+    """CRC of A || B from CRC(A), CRC(B) and len(B) (zlib's crc32_combine; tkv_crc32_combine)."""
+    return int(_fn(algo, "combine")(crc1, crc2, len2))
+
+
 def fill_synthetic_uniform(data, length, n, first_block=0, seed=1, stride=None, stream=None):
     """Write the SURVEY §8d generator's blocks [first_block, first_block+n) into ``data`` (GPU)."""
     stride = length if stride is None else stride

@@ -814,24 +814,66 @@ int batch_host_impl(int algo, const uint8_t* h_base, const uint64_t* h_offsets, 
   return host_batch(c, algo, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, 0, n);
 }
 
+// Blocks of at least this many bytes that straddle a device's byte share are cut at the share
+// boundary; their pieces run on different devices and combine on the host.
+constexpr std::uint64_t kSplitMin = std::uint64_t(1) << 20;
+
 int batch_host_multi_impl(int algo, const int* devices, int ndev, const uint8_t* h_base, const uint64_t* h_offsets,
                           const uint32_t* h_lengths, const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
   if (ndev <= 0 || !ptr_ok(devices)) return fail(TKV_INVALID_ARGUMENT, "no devices");
   if (n == 0) return TKV_OK;
   if (!ptr_ok(h_base) || !ptr_ok(h_offsets) || !ptr_ok(h_lengths) || !ptr_ok(h_out_final))
     return fail(TKV_INVALID_ARGUMENT, "null pointer");
-  // Byte-balanced contiguous split of the block list.
+  // Byte-balanced contiguous split of the block list: device d takes the bytes
+  // [total*d/ndev, total*(d+1)/ndev) of the blocks laid end to end in index order.
   std::uint64_t total = 0;
   for (std::uint64_t i = 0; i < n; ++i) total += h_lengths[i];
   std::vector<std::uint64_t> cut(ndev + 1, n);
   cut[0] = 0;
+  bool split = false;
   {
     std::uint64_t acc = 0, i = 0;
     for (int d = 1; d < ndev; ++d) {
       const std::uint64_t target = total * d / ndev;
       while (i < n && acc + h_lengths[i] <= target) acc += h_lengths[i++];
       cut[d] = i;
+      // block i straddles the boundary (acc < target < acc + len): cut it if it is large
+      if (i < n && acc < target && h_lengths[i] >= kSplitMin) split = true;
     }
+  }
+  // Per device, either an index range of the caller's arrays or (split) its own piece list.
+  struct Work {
+    std::vector<std::uint64_t> off;
+    std::vector<std::uint32_t> len, init, out;
+    std::vector<std::uint64_t> block;  // batch index of each piece
+    std::vector<std::uint8_t> head;    // piece starts its block (takes the block's init)
+  };
+  std::vector<Work> work(split ? ndev : 0);
+  const std::uint32_t poly = algo_poly(algo);
+  if (split) {
+    std::uint64_t pos = 0;  // byte position of block i's start in the end-to-end stream
+    int d = 0;
+    for (std::uint64_t i = 0; i < n; ++i) {
+      const std::uint64_t len = h_lengths[i];
+      std::uint64_t done = 0;
+      do {
+        while (d + 1 < ndev && pos + done >= total * (d + 1) / ndev && (len == 0 || done < len)) ++d;
+        std::uint64_t take = len - done;
+        if (len >= kSplitMin && d + 1 < ndev) {
+          const std::uint64_t end = total * (d + 1) / ndev;  // this device's share ends here
+          if (pos + len > end && end > pos + done) take = end - (pos + done);
+        }
+        Work& w = work[d];
+        w.off.push_back(h_offsets[i] + done);
+        w.len.push_back(static_cast<std::uint32_t>(take));
+        w.init.push_back(done == 0 ? (h_init_raw ? h_init_raw[i] : kInit) : 0u);
+        w.block.push_back(i);
+        w.head.push_back(done == 0);
+        done += take;
+      } while (done < len);
+      pos += len;
+    }
+    for (auto& w : work) w.out.resize(w.off.size());
   }
   std::vector<int> rcs(ndev, TKV_OK);
   std::vector<std::string> errs(ndev);
@@ -845,13 +887,40 @@ int batch_host_multi_impl(int algo, const int* devices, int ndev, const uint8_t*
       }
       DevCtx* c = nullptr;
       rcs[d] = get_ctx(&c);
-      if (rcs[d] == TKV_OK) rcs[d] = host_batch(c, algo, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, cut[d], cut[d + 1]);
+      if (rcs[d] == TKV_OK) {
+        if (split) {
+          Work& w = work[d];
+          if (!w.off.empty())
+            rcs[d] = host_batch(c, algo, h_base, w.off.data(), w.len.data(), w.init.data(), w.out.data(), 0, w.off.size());
+        } else {
+          rcs[d] = host_batch(c, algo, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, cut[d], cut[d + 1]);
+        }
+      }
       errs[d] = g_err;
     });
   }
   for (auto& t : th) t.join();
   for (int d = 0; d < ndev; ++d)
     if (rcs[d]) return fail(rcs[d], "device " + std::to_string(devices[d]) + ": " + errs[d]);
+  if (split) {
+    // Pieces arrive in block order across the devices: a head piece's register continues through the
+    // following pieces of its block, r = Shift_len(r) ^ crc_0(piece) (tkv_crc32_combine).
+    std::uint64_t cur = n;
+    std::uint32_t raw = 0;
+    for (auto& w : work) {
+      for (std::size_t k = 0; k < w.off.size(); ++k) {
+        const std::uint32_t r = w.out[k] ^ kInit;  // raw register of the piece
+        if (w.head[k]) {
+          if (cur != n) h_out_final[cur] = raw ^ kInit;
+          cur = w.block[k];
+          raw = r;
+        } else {
+          raw = shift_bytes(raw, w.len[k], poly) ^ r;
+        }
+      }
+    }
+    if (cur != n) h_out_final[cur] = raw ^ kInit;
+  }
   return TKV_OK;
 }
 
@@ -910,6 +979,13 @@ int tkv_crc32_batch_host_multi(const int* devices, int ndev, const uint8_t* h_ba
                                const uint32_t* h_lengths, const uint32_t* h_init_raw, uint32_t* h_out_final,
                                uint64_t n) {
   return batch_host_multi_impl(kAlgoCrc32, devices, ndev, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, n);
+}
+
+uint32_t tkv_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
+  return tkv::shift_bytes(crc1, len2, kPoly) ^ crc2;
+}
+uint32_t tkv_crc32c_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
+  return tkv::shift_bytes(crc1, len2, kPolyC) ^ crc2;
 }
 
 int tkv_crc32c_update(uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
