@@ -292,3 +292,35 @@ def test_combine_matches_concatenation(lib, oracle):
     n, m = (1 << 40) + 3, (1 << 33) + 11
     assert (lib.tkv_crc32_combine(lib.tkv_crc32_combine(x, 0, n), 0, m) ==
             lib.tkv_crc32_combine(x, 0, n + m))
+
+
+def skewed_ranges(nblocks, G, skew=154):
+    """Python restatement of crc_packed_body's SKEW partition (tkv_crc32_device.h): workgroup g gets
+    blocks [g*n/G, (g+1)*n/G); its wave in slot k (class c = k // 4) a share ~ (skew/256)^c."""
+    w = [256, skew, skew * skew // 256]
+    w.append(w[2] * skew // 256)
+    tot = 4 * sum(w)
+    out = []
+    for g in range(G):
+        g0, gn = g * nblocks // G, (g + 1) * nblocks // G - g * nblocks // G
+        for k in range(16):
+            c, m = k >> 2, k & 3
+            pre = 4 * sum(w[:c]) + m * w[c]
+            b0 = g0 + gn * pre // tot
+            out.append((b0, g0 + gn * (pre + w[c]) // tot - b0))
+    return out
+
+
+@pytest.mark.parametrize("nblocks,G", [(4096, 256), (262144, 256), (524288, 256), (5000, 7), (16, 1), (1000003, 304)])
+def test_skewed_packed_partition_covers_batch(nblocks, G):
+    """The skewed static partition of the packed kernel hands every block to exactly one wave, in
+    order, and gives slot class 0 the largest share."""
+    r = skewed_ranges(nblocks, G)
+    pos = 0
+    for b0, nb in r:
+        assert b0 == pos and nb >= 0
+        pos += nb
+    assert pos == nblocks
+    if nblocks >= 64 * G:
+        first = r[:16]
+        assert first[0][1] >= first[4][1] >= first[8][1] >= first[12][1]

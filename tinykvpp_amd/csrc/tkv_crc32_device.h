@@ -348,7 +348,8 @@ __device__ __forceinline__ void fill_lds(const DeviceTables* tabs, std::uint32_t
 // SMALL (irregular batches): when a wave runs its share of the small-block phase. 0: before its
 // rows; 1: even waves before their rows, odd waves after them, so the phase's latency-bound steps
 // overlap other waves' row streaming instead of all waves idling the HBM at once; 2: after its rows.
-template <bool ALIGNED, bool UNIFORM, int DEPTH, int ILP, int MODE, int SMALL = 0>
+// PRIO: issue priority from the rows a wave has left (as crc_packed_body).
+template <bool ALIGNED, bool UNIFORM, int DEPTH, int ILP, int MODE, int SMALL = 0, int PRIO = 0>
 __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
   constexpr int NP = ALIGNED ? 4 : 5;
@@ -442,6 +443,13 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
       ++gl;
     }
     for (std::uint32_t g = g0; g < g1; g += DEPTH) {
+      if constexpr (PRIO != 0) {
+        const std::uint32_t lvl = static_cast<std::uint32_t>(static_cast<std::uint64_t>(g1 - g) * 4u / (g1 - g0 + 1u));
+        if (lvl >= 3u) __builtin_amdgcn_s_setprio(3);
+        else if (lvl == 2u) __builtin_amdgcn_s_setprio(2);
+        else if (lvl == 1u) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
 #pragma unroll
       for (int k = 0; k < DEPTH; k += ILP) {
         // refill the slots freed by the previous step
@@ -653,8 +661,11 @@ __device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t*
 // fill (s = 0), before every PROG-th row (s = 1 + j / PROG) and at the end (last slot used + 1).
 // SUB: the caller has filled the LDS tables and passes the wave's block range [sub_b0, sub_b0 + sub_nb)
 // (crc_packed_xq_body's static region).
+// SKEW (0: off): the waves of a 1024-thread workgroup share its equal slice of the batch in
+// proportion to 256 * (SKEW/256)^(slot/4): slots 0-3 (the first wave on each SIMD) get the largest
+// ranges, slots 12-15 the smallest, matching the issue arbitration that favours a SIMD's older waves.
 template <int DEPTH, int ILP, bool R1, bool SPLIT = false, std::uint32_t ROT = 0, int CHK = 0, int PROG = 0,
-          bool SUB = false>
+          bool SUB = false, int SKEW = 0, int PRIO = 0>
 __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds, std::uint32_t sub_b0 = 0,
                                                 std::uint32_t sub_nb = 0) {
   static_assert(CHK == 0 || (R1 && ROT == 0 && CHK <= 6), "chunk-strided map: R1 only, chunks of <= 64 blocks");
@@ -679,9 +690,26 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint64_t W = a.nwaves;
   const std::uint32_t R = R1 ? 1u : a.len / kRow;
-  const std::uint32_t b0 = SUB ? sub_b0 : static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W);
-  const std::uint32_t nb =
-      SUB ? sub_nb : static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W) - b0;
+  std::uint32_t b0, nb;
+  if constexpr (SUB) {
+    b0 = sub_b0;
+    nb = sub_nb;
+  } else if constexpr (SKEW != 0) {
+    static_assert(CHK == 0 && ROT == 0, "skewed ranges: contiguous map only");
+    constexpr std::uint32_t w0 = 256, w1 = SKEW, w2 = w1 * SKEW / 256, w3 = w2 * SKEW / 256;
+    constexpr std::uint32_t tot = 4 * (w0 + w1 + w2 + w3);
+    const std::uint32_t k = wave & 15u, c = k >> 2, m = k & 3u;
+    const std::uint32_t pre = (c > 0 ? 4 * w0 : 0u) + (c > 1 ? 4 * w1 : 0u) + (c > 2 ? 4 * w2 : 0u) +
+                              m * (c == 0 ? w0 : c == 1 ? w1 : c == 2 ? w2 : w3);
+    const std::uint32_t wk = c == 0 ? w0 : c == 1 ? w1 : c == 2 ? w2 : w3;
+    const std::uint64_t g = wave >> 4, G = W >> 4;
+    const std::uint64_t g0 = g * a.nblocks / G, gn = (g + 1) * a.nblocks / G - g0;
+    b0 = static_cast<std::uint32_t>(g0 + gn * pre / tot);
+    nb = static_cast<std::uint32_t>(g0 + gn * (pre + wk) / tot) - b0;
+  } else {
+    b0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W);
+    nb = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W) - b0;
+  }
   if (nb == 0) return;
   const std::uint32_t nrows = nb * R;  // wave-local rows j = 0 .. nrows-1, contiguous in memory
   // CHK: global block of wave-local block j
@@ -759,6 +787,15 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
   for (std::uint32_t j = 0; j < nrows; j += DEPTH) {
     if constexpr (PROG > 0) {
       if (j % PROG == 0) stamp(1 + j / PROG);
+    }
+    if constexpr (PRIO != 0) {
+      // Issue priority from the work left: the SIMD arbiter serves a SIMD's oldest wave first, so
+      // without this the first wave on each SIMD finishes its range long before the fourth.
+      const std::uint32_t lvl = static_cast<std::uint32_t>(static_cast<std::uint64_t>(nrows - j) * 4u / (nrows + 1u));
+      if (lvl >= 3u) __builtin_amdgcn_s_setprio(3);
+      else if (lvl == 2u) __builtin_amdgcn_s_setprio(2);
+      else if (lvl == 1u) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
     }
 #pragma unroll
     for (int q = 0; q < DEPTH; q += ILP) {

@@ -45,13 +45,19 @@ __global__ __launch_bounds__(kRowsThreads) void crc_rows(RowsArgs a) {
 }
 
 // Packed uniform batches (len % 4 KiB == 0, stride == len, 16-byte aligned): DESIGN.md §4.
+// Issue priority follows the work a wave has left (PRIO); blocks of several rows also skew the
+// workgroup's slice towards the SIMDs' older waves (SKEW 154/256 per slot class). Measured in one
+// process against the plain static partition: +1.1 % on 4 KiB blocks (where the skew loses), +3.3 %
+// on 64 KiB blocks (profiles/r1/launch_prio2_cfg*.txt).
 constexpr int kPackedDepth = 4;
 constexpr int kPackedIlp = 2;
+constexpr int kPackedSkew = 154;
 
 template <bool R1>
 __global__ __launch_bounds__(kThreads) void crc_packed(RowsArgs a) {
+  static_assert(kThreads == 1024, "the skewed partition assumes 16 waves per workgroup");
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<kPackedDepth, kPackedIlp, R1>(a, lds);
+  dev::crc_packed_body<kPackedDepth, kPackedIlp, R1, false, 0, 0, 0, false, R1 ? 0 : kPackedSkew, 1>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }

@@ -461,6 +461,19 @@ __global__ __launch_bounds__(1024) void k_packed_stamped(RowsArgs a, unsigned lo
   }
 }
 
+template <int SK>
+__global__ __launch_bounds__(1024) void k_skew_stamped(RowsArgs a, unsigned long long* stamps) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  const std::uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  dev::crc_packed_body<4, 2, true, false, 0, 0, 0, false, SK>(a, lds);
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63u) == 0) {
+    stamps[2 * wave] = t0;
+    stamps[2 * wave + 1] = t1;
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_dyn_stamped(RowsArgs a, unsigned long long* stamps) {
   __shared__ std::uint32_t lds[kLdsWords];
   const std::uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6);
@@ -566,6 +579,19 @@ void PS(RowsArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_packed_stag<K, PW>), dim3(g_ncu), dim3(1024), 0, s, a);
 }
 
+template <int SK, int PR>
+__global__ __launch_bounds__(1024) void k_packed_skew(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  if (a.len == kRow) dev::crc_packed_body<4, 2, true, false, 0, 0, 0, false, SK, PR>(a, lds);
+  else dev::crc_packed_body<4, 2, false, false, 0, 0, 0, false, SK, PR>(a, lds);
+}
+
+template <int SK, int PR = 0>
+void PW(RowsArgs a, hipStream_t s) {
+  a.nwaves = g_ncu * 16;
+  hipLaunchKernelGGL((k_packed_skew<SK, PR>), dim3(g_ncu), dim3(1024), 0, s, a);
+}
+
 // grid of M workgroups per CU (M rounds): a CU whose workgroup finishes early takes the next one
 template <int M>
 void PG(RowsArgs a, hipStream_t s) {
@@ -607,6 +633,8 @@ const V kVariants[] = {
     {"xq D4 I2 C16", PX<4, 2, 16>},
     {"hy S14 C8", PX<4, 2, 8, 0, 14>}, {"hy S12 C8", PX<4, 2, 8, 0, 12>}, {"hy S10 C8", PX<4, 2, 8, 0, 10>},
     {"hy S12 C16", PX<4, 2, 16, 0, 12>}, {"hy S12 C32", PX<4, 2, 32, 0, 12>}, {"hy S8 C16", PX<4, 2, 16, 0, 8>},
+    {"skew 0.8", PW<205>}, {"skew 0.6", PW<154>}, {"prio", PW<0, 1>}, {"prio skew 0.8", PW<205, 1>},
+    {"prio skew 0.6", PW<154, 1>},
     {"stag wave 4", PS<4, true>}, {"stag wave 16", PS<16, true>}, {"stag wg 4", PS<4, false>},
     {"stag wg 16", PS<16, false>}, {"stag wave 1", PS<1, true>},
     {"grid x2", PG<2>}, {"grid x3", PG<3>}, {"grid x4", PG<4>}, {"grid x8", PG<8>}, {"grid x16", PG<16>},
@@ -633,10 +661,10 @@ const V kVariants[] = {
 };
 constexpr int kNV = sizeof(kVariants) / sizeof(kVariants[0]);
 
-template <int D, int I, int T, int SM = 0>
+template <int D, int I, int T, int SM = 0, int PR = 0>
 __global__ __launch_bounds__(T) void k_irr(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_rows_body<false, false, D, I, 0, SM>(a, lds);
+  dev::crc_rows_body<false, false, D, I, 0, SM, PR>(a, lds);
 }
 
 struct IV {
@@ -645,9 +673,9 @@ struct IV {
   void (*launch)(RowsArgs, hipStream_t);
 };
 
-template <int D, int I, int T, int SM = 0>
+template <int D, int I, int T, int SM = 0, int PR = 0>
 void LI(RowsArgs a, hipStream_t s) {
-  hipLaunchKernelGGL((k_irr<D, I, T, SM>), dim3(g_ncu), dim3(T), 0, s, a);
+  hipLaunchKernelGGL((k_irr<D, I, T, SM, PR>), dim3(g_ncu), dim3(T), 0, s, a);
 }
 
 const IV kIrr[] = {
@@ -655,6 +683,7 @@ const IV kIrr[] = {
     {"irr T1024 D4 I2", 1024, LI<4, 2, 1024>}, {"irr T512 D4 I2", 512, LI<4, 2, 512>},
     {"irr T512 D6 I2", 512, LI<6, 2, 512>}, {"irr T512 D6 I3", 512, LI<6, 3, 512>},
     {"irr T768 D4 I2", 768, LI<4, 2, 768>}, {"irr T512 D8 I4", 512, LI<8, 4, 512>},
+    {"irr T768 D4 I2 prio", 768, LI<4, 2, 768, 0, 1>}, {"irr T1024 D4 I2 prio", 1024, LI<4, 2, 1024, 0, 1>},
     {"irr T768 D4 I2 small-alt", 768, LI<4, 2, 768, 1>}, {"irr T768 D4 I2 small-last", 768, LI<4, 2, 768, 2>},
 };
 constexpr int kNIrr = sizeof(kIrr) / sizeof(kIrr[0]);
@@ -798,7 +827,9 @@ extern "C" int explore_stamped(const std::uint8_t* base, std::uint64_t n, std::u
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = g_ncu * 16;
   a.wg_ctr = g_ctr;
-  if (dyn) hipLaunchKernelGGL(k_dyn_stamped, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
+  if (dyn == 2) hipLaunchKernelGGL(k_skew_stamped<154>, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
+  else if (dyn == 3) hipLaunchKernelGGL(k_skew_stamped<205>, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
+  else if (dyn) hipLaunchKernelGGL(k_dyn_stamped, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
   else hipLaunchKernelGGL(k_packed_stamped, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

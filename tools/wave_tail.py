@@ -36,3 +36,12 @@ for rep in range(4):
 xcd = (np.arange(W) // 16) % 8
 for x in range(8):
     print(f"xcd-group {x}: median wave duration {np.median(dur[xcd == x])/1e3:.1f} us, max end {end[xcd == x].max()/1e3:.1f}")
+# per wave slot inside the workgroup (0..15): is the spread systematic (issue arbitration) or random?
+slot = np.arange(W) % 16
+print("median wave duration by slot (us): " + " ".join(f"{np.median(dur[slot == k])/1e3:.0f}" for k in range(16)))
+wg = np.arange(W) // 16
+wgdur = np.array([end[wg == g].max() for g in range(W // 16)])
+print(f"workgroup end (slowest wave) p10/p50/p90/max: {np.percentile(wgdur,10)/1e3:.0f}/{np.median(wgdur)/1e3:.0f}/"
+      f"{np.percentile(wgdur,90)/1e3:.0f}/{wgdur.max()/1e3:.0f} us")
+rank = np.argsort(np.argsort(dur.reshape(-1, 16), axis=1), axis=1)  # 0 = fastest wave of its workgroup
+print("mean rank (0 = fastest in its workgroup) by slot: " + " ".join(f"{rank[:, k].mean():.1f}" for k in range(16)))
