@@ -87,28 +87,32 @@ def load_oracle():
     return o
 
 
-def cpu_baseline(host, nblocks, blen, seconds_target=16.0, total_blocks=None):
+def cpu_baseline(host, nblocks, blen, seconds_target=16.0, total_blocks=None, offs=None, lens=None):
     """Time the reference crc32 (oracle/_ref, else the oracle port) on host cores over a bounded
-    contiguous sample of the batch's own bytes; contiguous per-thread block ranges."""
+    contiguous sample of the batch's own bytes; contiguous per-thread block ranges. Uniform blocks
+    of `blen` bytes, or (offs, lens) for an irregular batch (blen = mean length, for the sizing)."""
     ref_path = os.path.join(ROOT, "oracle", "_ref", "libref_crc32.so")
+    if offs is None:
+        offs = np.arange(nblocks, dtype=np.uint64) * blen
+        lens = np.full(nblocks, blen, np.uint32)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
     if os.path.exists(ref_path):
         lib = ctypes.CDLL(ref_path)
-        fn = lib.ref_crc32_blocks
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
+        fn = lib.ref_crc32_irregular
+        fn.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_size_t, ctypes.c_void_p]
         kind = "reference"
     else:
         lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+        lib.oracle_crc_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p]
         fn = None
         kind = "port"
 
     def run(lo, hi, out):
         if fn is not None:
-            fn(host.ctypes.data + lo * blen, blen, blen, hi - lo, out.ctypes.data + lo * 4)
+            fn(host.ctypes.data, offs.ctypes.data + lo * 8, lens.ctypes.data + lo * 4, hi - lo, out.ctypes.data + lo * 4)
         else:
-            lib.oracle_crc_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p]
-            offs = (np.arange(lo, hi, dtype=np.uint64) * blen)
-            lens = np.full(hi - lo, blen, np.uint32)
-            lib.oracle_crc_batch(host.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, hi - lo,
+            lib.oracle_crc_batch(host.ctypes.data, offs.ctypes.data + lo * 8, lens.ctypes.data + lo * 4, None, hi - lo,
                                  out.ctypes.data + lo * 4)
 
     cores = max(1, min(len(os.sched_getaffinity(0)), 16))  # the GPU box's CPU share is 16
@@ -118,7 +122,7 @@ def cpu_baseline(host, nblocks, blen, seconds_target=16.0, total_blocks=None):
     cal = min(nblocks, 4096)
     run(0, cal, out)
     per_block = (time.perf_counter() - t0) / cal
-    one_core_gibs = cal * blen / (1 << 30) / max(per_block * cal, 1e-9)
+    one_core_gibs = int(lens[:cal].astype(np.uint64).sum()) / (1 << 30) / max(per_block * cal, 1e-9)
     sample = int(min(nblocks, max(cores * 1024, seconds_target * cores / max(per_block, 1e-12))))
     step = (sample + cores - 1) // cores
     # passes over the sample until ~seconds_target core-seconds of CRC work have run (>= 1 pass)
@@ -132,10 +136,12 @@ def cpu_baseline(host, nblocks, blen, seconds_target=16.0, total_blocks=None):
             t.join()
         dt += time.perf_counter() - t0
         passes += 1
-    return {"value": round(passes * sample * blen / (1 << 30) / dt, 4), "unit": "GiB/s", "cores": cores, "kind": kind,
-            "sample": f"{passes} pass(es) over the first {sample} of the {total_blocks or nblocks} x {blen} B blocks "
-                      f"(same bytes as the GPU run), {cores} threads, contiguous block ranges, {dt:.2f} s wall, "
-                      f"~{dt * cores:.0f} core-seconds",
+    sbytes = int(lens[:sample].astype(np.uint64).sum())
+    what = f"{blen} B blocks" if lens.min() == lens.max() else "blocks (Zipf lengths)"
+    return {"value": round(passes * sbytes / (1 << 30) / dt, 4), "unit": "GiB/s", "cores": cores, "kind": kind,
+            "sample": f"{passes} pass(es) over the first {sample} of the {total_blocks or nblocks} {what}, "
+                      f"{sbytes / (1 << 30):.2f} GiB (same bytes as the GPU run), {cores} threads, contiguous block "
+                      f"ranges, {dt:.2f} s wall, ~{dt * cores:.0f} core-seconds",
             "one_core_gibs": round(one_core_gibs, 4)}, out[:sample]
 
 
@@ -285,10 +291,16 @@ def main():
                             "GB_per_s": round(total / 1e9 / dt_e2e, 2), "source": "pinned host memory, read in place",
                             "bit_exact": bool(np.array_equal(got, crcs))}
         del host_p, hp
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and blen is not None:
-        nb_host = min(nblocks, (4 << 30) // blen)  # at most 4 GiB of the batch goes to host memory
-        host = data[:nb_host * blen].cpu().numpy()
-        cb, cpu_crcs = cpu_baseline(host, nb_host, blen, total_blocks=nblocks)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if blen is not None:
+            nb_host = min(nblocks, (4 << 30) // blen)  # at most 4 GiB of the batch goes to host memory
+            host = data[:nb_host * blen].cpu().numpy()
+            cb, cpu_crcs = cpu_baseline(host, nb_host, blen, total_blocks=nblocks)
+        else:  # cfg4: the leading blocks up to 4 GiB, at their own (unaligned) offsets
+            nb_host = int(np.searchsorted(offs + lens.astype(np.int64), 4 << 30, side="right"))
+            host = data[:int(offs[nb_host - 1] + lens[nb_host - 1])].cpu().numpy()
+            cb, cpu_crcs = cpu_baseline(host, nb_host, max(1, int(lens[:nb_host].mean())), total_blocks=nblocks,
+                                        offs=offs[:nb_host], lens=lens[:nb_host])
         cb["agrees_with_gpu"] = bool(np.array_equal(cpu_crcs, crcs[:cpu_crcs.size]))
         line["cpu_baseline"] = cb
     if rank == 0:

@@ -42,4 +42,10 @@ void ref_crc32_blocks(const unsigned char *base, std::size_t stride, std::size_t
   for (std::size_t i = 0; i < count; ++i) out[i] = ref_crc32(base + i * stride, len);
 }
 
+// Batch of blocks at arbitrary offsets and lengths: out[i] = crc of [base + off[i], + len[i]).
+void ref_crc32_irregular(const unsigned char *base, const std::uint64_t *off, const std::uint32_t *len,
+                         std::size_t count, std::uint32_t *out) {
+  for (std::size_t i = 0; i < count; ++i) out[i] = ref_crc32(base + off[i], len[i]);
+}
+
 }  // extern "C"

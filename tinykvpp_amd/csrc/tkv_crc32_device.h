@@ -330,6 +330,26 @@ __device__ __forceinline__ void finish_row(const RowsArgs& a, const Cursor& c, s
   }
 }
 
+// Issue priority from the work a wave has left (`left` of `total` rows): the SIMD arbiter serves a
+// SIMD's oldest wave first, so with equal ranges the first wave on each SIMD finishes long before
+// the fourth. PRIO 1: levels 3..0 over the quarters of the range; PRIO p > 1:
+// thresholds at 2^(1-p), 2^(-p), 2^(-1-p) of it left (3: 1/4, 1/8, 1/16, the product setting).
+template <int PRIO>
+__device__ __forceinline__ void set_prio_from_left(std::uint32_t left, std::uint32_t total) {
+  const std::uint64_t rem = left;
+  std::uint32_t lvl;
+  if constexpr (PRIO == 1) {
+    lvl = static_cast<std::uint32_t>(rem * 4u / (total + 1ull));
+  } else {
+    constexpr std::uint32_t sh = PRIO + 1;
+    lvl = (rem << sh) > 4ull * total ? 3u : (rem << sh) > 2ull * total ? 2u : (rem << sh) > total ? 1u : 0u;
+  }
+  if (lvl >= 3u) __builtin_amdgcn_s_setprio(3);
+  else if (lvl == 2u) __builtin_amdgcn_s_setprio(2);
+  else if (lvl == 1u) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
 // Small blocks of an irregular batch (defined below; runs inside the irregular row kernel).
 __device__ __forceinline__ void small_phase(const RowsArgs& a, std::uint32_t* lds);
 
@@ -443,13 +463,7 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
       ++gl;
     }
     for (std::uint32_t g = g0; g < g1; g += DEPTH) {
-      if constexpr (PRIO != 0) {
-        const std::uint32_t lvl = static_cast<std::uint32_t>(static_cast<std::uint64_t>(g1 - g) * 4u / (g1 - g0 + 1u));
-        if (lvl >= 3u) __builtin_amdgcn_s_setprio(3);
-        else if (lvl == 2u) __builtin_amdgcn_s_setprio(2);
-        else if (lvl == 1u) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-      }
+      if constexpr (PRIO != 0) set_prio_from_left<PRIO>(g1 - g, g1 - g0);
 #pragma unroll
       for (int k = 0; k < DEPTH; k += ILP) {
         // refill the slots freed by the previous step
@@ -788,15 +802,7 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
     if constexpr (PROG > 0) {
       if (j % PROG == 0) stamp(1 + j / PROG);
     }
-    if constexpr (PRIO != 0) {
-      // Issue priority from the work left: the SIMD arbiter serves a SIMD's oldest wave first, so
-      // without this the first wave on each SIMD finishes its range long before the fourth.
-      const std::uint32_t lvl = static_cast<std::uint32_t>(static_cast<std::uint64_t>(nrows - j) * 4u / (nrows + 1u));
-      if (lvl >= 3u) __builtin_amdgcn_s_setprio(3);
-      else if (lvl == 2u) __builtin_amdgcn_s_setprio(2);
-      else if (lvl == 1u) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
+    if constexpr (PRIO != 0) set_prio_from_left<PRIO>(nrows - j, nrows);
 #pragma unroll
     for (int q = 0; q < DEPTH; q += ILP) {
 #pragma unroll

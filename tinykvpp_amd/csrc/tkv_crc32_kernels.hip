@@ -41,23 +41,25 @@ struct Shape {
 template <bool ALIGNED, bool UNIFORM>
 __global__ __launch_bounds__(kRowsThreads) void crc_rows(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_rows_body<ALIGNED, UNIFORM, Shape<ALIGNED>::kDepth, Shape<ALIGNED>::kIlp, 0>(a, lds);
+  // issue priority from the rows left (set_prio_from_left): +0.7 % on cfg4 (profiles/r1/launch_irr_pri3.txt)
+  dev::crc_rows_body<ALIGNED, UNIFORM, Shape<ALIGNED>::kDepth, Shape<ALIGNED>::kIlp, 0, 0, 3>(a, lds);
 }
 
 // Packed uniform batches (len % 4 KiB == 0, stride == len, 16-byte aligned): DESIGN.md §4.
 // Issue priority follows the work a wave has left (PRIO); blocks of several rows also skew the
 // workgroup's slice towards the SIMDs' older waves (SKEW 154/256 per slot class). Measured in one
-// process against the plain static partition: +1.1 % on 4 KiB blocks (where the skew loses), +3.3 %
-// on 64 KiB blocks (profiles/r1/launch_prio2_cfg*.txt).
+// process against the plain static partition: +0.8 to +1.4 % on 4 KiB blocks (where the skew
+// loses), +3.7 % on 64 KiB blocks (profiles/r1/launch_prio*_cfg*.txt).
 constexpr int kPackedDepth = 4;
 constexpr int kPackedIlp = 2;
 constexpr int kPackedSkew = 154;
+constexpr int kPackedPrio = 3;  // set_prio_from_left thresholds 1/4, 1/8, 1/16
 
 template <bool R1>
 __global__ __launch_bounds__(kThreads) void crc_packed(RowsArgs a) {
   static_assert(kThreads == 1024, "the skewed partition assumes 16 waves per workgroup");
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<kPackedDepth, kPackedIlp, R1, false, 0, 0, 0, false, R1 ? 0 : kPackedSkew, 1>(a, lds);
+  dev::crc_packed_body<kPackedDepth, kPackedIlp, R1, false, 0, 0, 0, false, R1 ? 0 : kPackedSkew, kPackedPrio>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }

@@ -634,7 +634,9 @@ const V kVariants[] = {
     {"hy S14 C8", PX<4, 2, 8, 0, 14>}, {"hy S12 C8", PX<4, 2, 8, 0, 12>}, {"hy S10 C8", PX<4, 2, 8, 0, 10>},
     {"hy S12 C16", PX<4, 2, 16, 0, 12>}, {"hy S12 C32", PX<4, 2, 32, 0, 12>}, {"hy S8 C16", PX<4, 2, 16, 0, 8>},
     {"skew 0.8", PW<205>}, {"skew 0.6", PW<154>}, {"prio", PW<0, 1>}, {"prio skew 0.8", PW<205, 1>},
-    {"prio skew 0.6", PW<154, 1>},
+    {"prio skew 0.6", PW<154, 1>}, {"pri2", PW<0, 2>}, {"pri3", PW<0, 3>}, {"pri2 skew 0.6", PW<154, 2>},
+    {"pri3 skew 0.6", PW<154, 3>}, {"pri4", PW<0, 4>}, {"pri5", PW<0, 5>}, {"pri4 skew 0.6", PW<154, 4>},
+    {"pri5 skew 0.6", PW<154, 5>}, {"pri3 skew 0.5", PW<128, 3>}, {"pri3 skew 0.7", PW<179, 3>},
     {"stag wave 4", PS<4, true>}, {"stag wave 16", PS<16, true>}, {"stag wg 4", PS<4, false>},
     {"stag wg 16", PS<16, false>}, {"stag wave 1", PS<1, true>},
     {"grid x2", PG<2>}, {"grid x3", PG<3>}, {"grid x4", PG<4>}, {"grid x8", PG<8>}, {"grid x16", PG<16>},
@@ -683,7 +685,7 @@ const IV kIrr[] = {
     {"irr T1024 D4 I2", 1024, LI<4, 2, 1024>}, {"irr T512 D4 I2", 512, LI<4, 2, 512>},
     {"irr T512 D6 I2", 512, LI<6, 2, 512>}, {"irr T512 D6 I3", 512, LI<6, 3, 512>},
     {"irr T768 D4 I2", 768, LI<4, 2, 768>}, {"irr T512 D8 I4", 512, LI<8, 4, 512>},
-    {"irr T768 D4 I2 prio", 768, LI<4, 2, 768, 0, 1>}, {"irr T1024 D4 I2 prio", 1024, LI<4, 2, 1024, 0, 1>},
+    {"irr T768 D4 I2 prio", 768, LI<4, 2, 768, 0, 1>}, {"irr T768 D4 I2 pri3", 768, LI<4, 2, 768, 0, 3>}, {"irr T1024 D4 I2 prio", 1024, LI<4, 2, 1024, 0, 1>},
     {"irr T768 D4 I2 small-alt", 768, LI<4, 2, 768, 1>}, {"irr T768 D4 I2 small-last", 768, LI<4, 2, 768, 2>},
 };
 constexpr int kNIrr = sizeof(kIrr) / sizeof(kIrr[0]);
