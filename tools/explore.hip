@@ -461,12 +461,12 @@ __global__ __launch_bounds__(1024) void k_packed_stamped(RowsArgs a, unsigned lo
   }
 }
 
-template <int SK>
+template <int SK, int PR = 0>
 __global__ __launch_bounds__(1024) void k_skew_stamped(RowsArgs a, unsigned long long* stamps) {
   __shared__ std::uint32_t lds[kLdsWords];
   const std::uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  dev::crc_packed_body<4, 2, true, false, 0, 0, 0, false, SK>(a, lds);
+  dev::crc_packed_body<4, 2, true, false, 0, 0, 0, false, SK, PR>(a, lds);
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
   if ((threadIdx.x & 63u) == 0) {
     stamps[2 * wave] = t0;
@@ -601,6 +601,20 @@ void PG(RowsArgs a, hipStream_t s) {
   else hipLaunchKernelGGL((k_packed<4, 2, false, 1024, false>), dim3(g_ncu * M), dim3(1024), 0, s, a);
 }
 
+// Packed shapes with the product's work-left priority (no skew: it assumes 1024 threads).
+template <int D, int I, bool R1, int T>
+__global__ __launch_bounds__(T) void k_packed_pr(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  dev::crc_packed_body<D, I, R1, false, 0, 0, 0, false, 0, 3>(a, lds);
+}
+
+template <int D, int I, int T>
+void PP(RowsArgs a, hipStream_t s) {
+  a.nwaves = g_ncu * (T / 64);
+  if (a.len == kRow) hipLaunchKernelGGL((k_packed_pr<D, I, true, T>), dim3(g_ncu), dim3(T), 0, s, a);
+  else hipLaunchKernelGGL((k_packed_pr<D, I, false, T>), dim3(g_ncu), dim3(T), 0, s, a);
+}
+
 template <int D, int I, int T = 1024, bool SP = false>
 void PK(RowsArgs a, hipStream_t s) {
   a.nwaves = g_ncu * (T / 64);
@@ -633,6 +647,9 @@ const V kVariants[] = {
     {"xq D4 I2 C16", PX<4, 2, 16>},
     {"hy S14 C8", PX<4, 2, 8, 0, 14>}, {"hy S12 C8", PX<4, 2, 8, 0, 12>}, {"hy S10 C8", PX<4, 2, 8, 0, 10>},
     {"hy S12 C16", PX<4, 2, 16, 0, 12>}, {"hy S12 C32", PX<4, 2, 32, 0, 12>}, {"hy S8 C16", PX<4, 2, 16, 0, 8>},
+    {"pp T1024 D4 I2", PP<4, 2, 1024>}, {"pp T1024 D4 I1", PP<4, 1, 1024>}, {"pp T1024 D3 I1", PP<3, 1, 1024>},
+    {"pp T768 D4 I2", PP<4, 2, 768>}, {"pp T768 D6 I2", PP<6, 2, 768>}, {"pp T768 D6 I3", PP<6, 3, 768>},
+    {"pp T512 D8 I4", PP<8, 4, 512>}, {"pp T512 D6 I2", PP<6, 2, 512>}, {"pp T512 D8 I2", PP<8, 2, 512>},
     {"skew 0.8", PW<205>}, {"skew 0.6", PW<154>}, {"prio", PW<0, 1>}, {"prio skew 0.8", PW<205, 1>},
     {"prio skew 0.6", PW<154, 1>}, {"pri2", PW<0, 2>}, {"pri3", PW<0, 3>}, {"pri2 skew 0.6", PW<154, 2>},
     {"pri3 skew 0.6", PW<154, 3>}, {"pri4", PW<0, 4>}, {"pri5", PW<0, 5>}, {"pri4 skew 0.6", PW<154, 4>},
@@ -829,7 +846,8 @@ extern "C" int explore_stamped(const std::uint8_t* base, std::uint64_t n, std::u
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = g_ncu * 16;
   a.wg_ctr = g_ctr;
-  if (dyn == 2) hipLaunchKernelGGL(k_skew_stamped<154>, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
+  if (dyn == 4) hipLaunchKernelGGL((k_skew_stamped<0, 3>), dim3(g_ncu), dim3(1024), 0, st, a, stamps);
+  else if (dyn == 2) hipLaunchKernelGGL(k_skew_stamped<154>, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
   else if (dyn == 3) hipLaunchKernelGGL(k_skew_stamped<205>, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
   else if (dyn) hipLaunchKernelGGL(k_dyn_stamped, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
   else hipLaunchKernelGGL(k_packed_stamped, dim3(g_ncu), dim3(1024), 0, st, a, stamps);
