@@ -678,6 +678,8 @@ __device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t*
 // SKEW (0: off): the waves of a 1024-thread workgroup share its equal slice of the batch in
 // proportion to 256 * (SKEW/256)^(slot/4): slots 0-3 (the first wave on each SIMD) get the largest
 // ranges, slots 12-15 the smallest, matching the issue arbitration that favours a SIMD's older waves.
+// PRIO (0: off): set_prio_from_left<PRIO> once per DEPTH rows (the product uses 3, and SKEW 154 for
+// blocks of more than one row; tkv_crc32_kernels.hip).
 template <int DEPTH, int ILP, bool R1, bool SPLIT = false, std::uint32_t ROT = 0, int CHK = 0, int PROG = 0,
           bool SUB = false, int SKEW = 0, int PRIO = 0>
 __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds, std::uint32_t sub_b0 = 0,

@@ -19,6 +19,7 @@ ref = tk.crc32_batch_uniform(data, 4096, n).clone()
 W = torch.cuda.get_device_properties(0).multi_processor_count * 16
 st = torch.empty(2 * W, dtype=torch.int64, device="cuda")
 sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+wg_ends = []
 for rep in range(4):
     assert lib.explore_stamped(ctypes.c_void_p(data.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
                                ctypes.c_void_p(st.data_ptr()), sp, DYN) == 0
@@ -28,6 +29,7 @@ for rep in range(4):
     t0 = s[:, 0].min()
     start, end = s[:, 0] - t0, s[:, 1] - t0
     dur = end - start
+    wg_ends.append(end.reshape(-1, 16).max(axis=1))
     print(f"rep {rep}: kernel span {end.max()/1e3:.1f} us; wave end p50 {np.median(end)/1e3:.1f} "
           f"p90 {np.percentile(end, 90)/1e3:.1f} p99 {np.percentile(end, 99)/1e3:.1f} max {end.max()/1e3:.1f} us; "
           f"start spread {start.max()/1e3:.1f} us; dur p50 {np.median(dur)/1e3:.1f} min {dur.min()/1e3:.1f} max {dur.max()/1e3:.1f}",
@@ -45,3 +47,9 @@ print(f"workgroup end (slowest wave) p10/p50/p90/max: {np.percentile(wgdur,10)/1
       f"{np.percentile(wgdur,90)/1e3:.0f}/{wgdur.max()/1e3:.0f} us")
 rank = np.argsort(np.argsort(dur.reshape(-1, 16), axis=1), axis=1)  # 0 = fastest wave of its workgroup
 print("mean rank (0 = fastest in its workgroup) by slot: " + " ".join(f"{rank[:, k].mean():.1f}" for k in range(16)))
+# is a workgroup's lateness systematic (same blockIdx late in every launch) or random?
+E = np.array(wg_ends)
+E = E - E.mean(axis=1, keepdims=True)
+c = np.corrcoef(E)
+print("correlation of workgroup end times between launches: " +
+      " ".join(f"{c[i, j]:.2f}" for i in range(len(E)) for j in range(i + 1, len(E))))
