@@ -653,8 +653,7 @@ const V kVariants[] = {
     {"skew 0.8", PW<205>}, {"skew 0.6", PW<154>}, {"prio", PW<0, 1>}, {"prio skew 0.8", PW<205, 1>},
     {"prio skew 0.6", PW<154, 1>}, {"pri2", PW<0, 2>}, {"pri3", PW<0, 3>}, {"pri2 skew 0.6", PW<154, 2>},
     {"pri3 skew 0.6", PW<154, 3>}, {"pri4", PW<0, 4>}, {"pri5", PW<0, 5>}, {"pri4 skew 0.6", PW<154, 4>},
-    {"pri5 skew 0.6", PW<154, 5>}, {"pri3 skew 0.5", PW<128, 3>}, {"pri3 skew 0.7", PW<179, 3>},
-    {"stag wave 4", PS<4, true>}, {"stag wave 16", PS<16, true>}, {"stag wg 4", PS<4, false>},
+    {"pri5 skew 0.6", PW<154, 5>}, {"pri3 skew 0.5", PW<128, 3>}, {"pri3 skew 0.7", PW<179, 3>},    {"stag wave 4", PS<4, true>}, {"stag wave 16", PS<16, true>}, {"stag wg 4", PS<4, false>},
     {"stag wg 16", PS<16, false>}, {"stag wave 1", PS<1, true>},
     {"grid x2", PG<2>}, {"grid x3", PG<3>}, {"grid x4", PG<4>}, {"grid x8", PG<8>}, {"grid x16", PG<16>},
     {"packed D4 I2", PK<4, 2>}, {"packed D4 I1", PK<4, 1>}, {"packed D3 I1", PK<3, 1>},
