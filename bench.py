@@ -125,10 +125,11 @@ def cpu_baseline(host, nblocks, blen, seconds_target=16.0, total_blocks=None, of
     one_core_gibs = int(lens[:cal].astype(np.uint64).sum()) / (1 << 30) / max(per_block * cal, 1e-9)
     sample = int(min(nblocks, max(cores * 1024, seconds_target * cores / max(per_block, 1e-12))))
     step = (sample + cores - 1) // cores
+    ranges = [(min(sample, i * step), min(sample, (i + 1) * step)) for i in range(cores)]  # contiguous, maybe empty
     # passes over the sample until ~seconds_target core-seconds of CRC work have run (>= 1 pass)
     passes, dt = 0, 0.0
     while passes == 0 or (dt * cores < seconds_target and passes < 8):
-        ths = [threading.Thread(target=run, args=(i * step, min(sample, (i + 1) * step), out)) for i in range(cores)]
+        ths = [threading.Thread(target=run, args=(lo, hi, out)) for lo, hi in ranges]
         t0 = time.perf_counter()
         for t in ths:
             t.start()
@@ -137,12 +138,33 @@ def cpu_baseline(host, nblocks, blen, seconds_target=16.0, total_blocks=None, of
         dt += time.perf_counter() - t0
         passes += 1
     sbytes = int(lens[:sample].astype(np.uint64).sum())
+    # SURVEY §8d's optional comparison row, NOT the reference algorithm: slicing-by-8 on the same
+    # sample, threads and ranges (oracle/crc32_oracle.c), one pass.
+    s8lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+    s8 = s8lib.oracle_crc_batch_s8
+    s8.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]
+    out8 = np.zeros(sample, np.uint32)
+    s8lib.oracle_update_s8(ctypes.c_uint32(0), None, ctypes.c_size_t(0))  # build its tables before the threads
+
+    def run8(lo, hi):
+        s8(host.ctypes.data, offs.ctypes.data + lo * 8, lens.ctypes.data + lo * 4, hi - lo, out8.ctypes.data + lo * 4)
+
+    ths = [threading.Thread(target=run8, args=(lo, hi)) for lo, hi in ranges]
+    t8 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    t8 = time.perf_counter() - t8
+    slicing8 = {"value": round(sbytes / (1 << 30) / t8, 4), "unit": "GiB/s", "cores": cores,
+                "kind": "not reference: slicing-by-8 (oracle/crc32_oracle.c), same sample and threads, one pass",
+                "agrees_with_reference": bool(np.array_equal(out8, out[:sample]))}
     what = f"{blen} B blocks" if lens.min() == lens.max() else "blocks (Zipf lengths)"
     return {"value": round(passes * sbytes / (1 << 30) / dt, 4), "unit": "GiB/s", "cores": cores, "kind": kind,
             "sample": f"{passes} pass(es) over the first {sample} of the {total_blocks or nblocks} {what}, "
                       f"{sbytes / (1 << 30):.2f} GiB (same bytes as the GPU run), {cores} threads, contiguous block "
                       f"ranges, {dt:.2f} s wall, ~{dt * cores:.0f} core-seconds",
-            "one_core_gibs": round(one_core_gibs, 4)}, out[:sample]
+            "one_core_gibs": round(one_core_gibs, 4), "slicing_by_8": slicing8}, out[:sample]
 
 
 def main():

@@ -166,3 +166,42 @@ uint32_t oracle_sst_stamp(const uint8_t *img, size_t size) {
   raw = oracle_update(raw, img + 21, size - 21);
   return raw ^ ORACLE_INIT;
 }
+
+/* ---- Slicing-by-8 (NOT the reference algorithm; CPU comparison row only) ----
+ * SURVEY.md §8d's optional "slicing-by-8 CPU row, clearly labelled 'not reference'": the same
+ * CRC-32/ISO-HDLC eight bytes per step with tables T_k[i] = Shift_k o T (Intel's slicing-by-8).
+ * bench.py times it beside the reference on the same bytes; tests/test_oracle.py checks it against
+ * oracle_update. Never part of the product path. */
+static uint32_t g_s8[8][256];
+static int g_s8_ready = 0;
+
+static void ensure_s8(void) {
+  if (g_s8_ready) return;
+  ensure_table();
+  for (int i = 0; i < 256; ++i) {
+    g_s8[0][i] = g_table[i];
+    for (int k = 1; k < 8; ++k) g_s8[k][i] = (g_s8[k - 1][i] >> 8) ^ g_table[g_s8[k - 1][i] & 0xFFu];
+  }
+  g_s8_ready = 1;
+}
+
+uint32_t oracle_update_s8(uint32_t raw, const uint8_t *p, size_t n) {
+  ensure_s8();
+  while (n >= 8) {
+    uint32_t lo, hi;
+    memcpy(&lo, p, 4);
+    memcpy(&hi, p + 4, 4);
+    lo ^= raw;
+    raw = g_s8[7][lo & 0xFFu] ^ g_s8[6][(lo >> 8) & 0xFFu] ^ g_s8[5][(lo >> 16) & 0xFFu] ^ g_s8[4][lo >> 24] ^
+          g_s8[3][hi & 0xFFu] ^ g_s8[2][(hi >> 8) & 0xFFu] ^ g_s8[1][(hi >> 16) & 0xFFu] ^ g_s8[0][hi >> 24];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) raw = (raw >> 8) ^ g_table[(*p++ ^ raw) & 0xFFu];
+  return raw;
+}
+
+void oracle_crc_batch_s8(const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
+                         uint32_t *out) {
+  for (uint64_t i = 0; i < n; ++i) out[i] = oracle_update_s8(ORACLE_INIT, base + offsets[i], lengths[i]) ^ ORACLE_INIT;
+}

@@ -4,6 +4,7 @@ Vectors: test/crc32_test.cpp:81-124 known answers, WAL records laid out per src/
 prefixes of a synthetic block, and the SURVEY §8c/§8d synthetic-batch goldens — all produced by the
 reference's compiled crc32.cpp (tests/golden/make_golden.py) and cross-checked with zlib.
 """
+import ctypes
 import struct
 import zlib
 
@@ -81,6 +82,26 @@ def test_against_zlib_random(oracle):
     for n in list(range(0, 70)) + [255, 256, 1000, 4095, 4096, 4097, 65537]:
         d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
         assert oracle.crc(d) == zlib.crc32(d)
+
+
+def test_slicing_by_8_comparison_row(oracle):
+    """bench.py's 'not reference' slicing-by-8 CPU row computes the same CRC (any length, any start)."""
+    lib = oracle.lib
+    lib.oracle_update_s8.restype = ctypes.c_uint32
+    lib.oracle_update_s8.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+    lib.oracle_crc_batch_s8.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]
+    rng = np.random.default_rng(5)
+    buf = rng.integers(0, 256, 70000, dtype=np.uint8)
+    sizes = list(range(0, 40)) + [255, 4096, 4099, 65536]
+    offs = np.array([(7 * i) % 997 for i in range(len(sizes))], np.uint64)
+    lens = np.array(sizes, np.uint32)
+    out = np.zeros(len(sizes), np.uint32)
+    lib.oracle_crc_batch_s8(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, len(sizes), out.ctypes.data)
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        d = buf[int(o):int(o) + int(n)].tobytes()
+        assert int(out[i]) == zlib.crc32(d) == oracle.crc(d)
+        assert lib.oracle_update_s8(0x12345678, buf[int(o):].ctypes.data, int(n)) == \
+            oracle.lib.oracle_update(0x12345678, buf[int(o):].ctypes.data, int(n))
 
 
 def test_against_compiled_reference(oracle, ref_lib):
