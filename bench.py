@@ -11,7 +11,9 @@ are the timing barrier and the max-over-ranks reduction.
 Prints one JSON line (rank 0). Extra fields: roofline (dominant kernel: algorithmic bytes per
 launch / HIP-event launch time vs 8 TB/s HBM peak), cpu_baseline (the reference's own crc32.cpp
 compiled from /root/reference into oracle/_ref, or the oracle port, on host cores over the same
-buffers), bit_exact (this run's CRCs vs the oracle / golden aggregates).
+buffers; plus a slicing-by-8 row that is not the reference), bit_exact (this run's CRCs vs the
+oracle / golden aggregates), pipelined_two_streams (the same steps alternating two HIP streams, as a
+caller checksumming a stream of batches may run them; never `value`).
 """
 import argparse
 import ctypes
@@ -175,6 +177,7 @@ def main():
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="cfg3: skip the host-memory end-to-end measurement")
+    ap.add_argument("--no-pipelined", action="store_true", help="skip the two-stream pipelined rate (extra field)")
     ap.add_argument("--traffic-csv", default=None,
                     help="rocprofv3 --pmc counter_collection.csv (FETCH_SIZE) of this command, for roofline.traffic")
     args = ap.parse_args()
@@ -218,15 +221,15 @@ def main():
         d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
         tk.fill_synthetic_blocks(data, d_off, d_len, first_block=first)
 
-        def step(strm=None):
-            tk.crc32_batch(data, d_off, d_len, out=out, stream=strm)
+        def step(strm=None, o=out):
+            tk.crc32_batch(data, d_off, d_len, out=o, stream=strm)
     else:
         total = nblocks * blen
         data = torch.empty(total, dtype=torch.uint8, device=dev)
         tk.fill_synthetic_uniform(data, blen, nblocks, first_block=first)
 
-        def step(strm=None):
-            tk.crc32_batch_uniform(data, blen, nblocks, out=out, stream=strm)
+        def step(strm=None, o=out):
+            tk.crc32_batch_uniform(data, blen, nblocks, out=o, stream=strm)
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -296,6 +299,24 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_step},
         "cpu_baseline": None,
     }
+    if world == 1 and not args.no_pipelined:
+        # A caller checksumming a stream of batches may alternate two HIP streams: each launch's
+        # workgroups then take the CUs its predecessor's tail frees. Same K steps,
+        # same work per step, results checked; reported beside `value`, never as `value`.
+        strms = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+        outs = [out, torch.empty_like(out)]
+        for i in range(20):
+            step(strms[i % 2], outs[i % 2])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(strms[i % 2], outs[i % 2])
+        torch.cuda.synchronize()
+        dt2 = time.perf_counter() - t0
+        same = bool(torch.equal(outs[0], outs[1])) and bool(np.array_equal(outs[0].cpu().numpy().view(np.uint32), crcs))
+        line["pipelined_two_streams"] = {"value": round(total * args.steps / (1 << 30) / dt2, 2), "unit": "GiB/s",
+                                         "ms_per_step": round(dt2 * 1e3 / args.steps, 4), "bit_exact": same,
+                                         "note": "consecutive steps alternate two streams; not `value`"}
     if args.config == "cfg3" and not args.no_e2e:
         # BASELINE cfg3 "+ H2D/D2H timed": the same blocks starting and ending in host memory (pinned,
         # read in place by the kernels over PCIe; results copied back), per rank; never `value`.
