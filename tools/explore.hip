@@ -27,11 +27,12 @@ namespace tkv::dev {
 // ctr[y * kCtrStride] is pool y's head, ctr[8 * kCtrStride] counts finished waves; the last wave to
 // finish zeroes them all for the next launch on this stream (they must be zero before the first).
 // PERM != 0 (explorer): the pool's q-th chunk is chunk (q * PERM) mod pool size (sizes powers of 2).
-template <int DEPTH, int ILP, bool R1, int CROWS, std::uint32_t PERM = 0, int SF = 0>
+// SD: SF is in 1/SD-ths of the blocks; SP: issue priority (set_prio_from_left<SP>) in the static region.
+template <int DEPTH, int ILP, bool R1, int CROWS, std::uint32_t PERM = 0, int SF = 0, int SD = 16, int SP = 0>
 __device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
   static_assert(CROWS % DEPTH == 0 && CROWS >= 2 * DEPTH && CROWS <= 64, "chunk shape");
-  static_assert(SF >= 0 && SF < 16, "static share in 1/16ths");
+  static_assert(SF >= 0 && SF < SD, "static share in 1/SD-ths");
   const std::uint32_t lane = threadIdx.x & 63u;
   const std::uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint32_t wpg = blockDim.x >> 6;
@@ -53,7 +54,7 @@ __device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint3
   const std::uint32_t W = G * wpg;
   const std::uint32_t wave = blockIdx.x * wpg + wid;
   // static region [0, S): wave w owns [w*S/W, (w+1)*S/W); pool region [S, nblocks)
-  const std::uint32_t S = SF ? static_cast<std::uint32_t>(static_cast<std::uint64_t>(a.nblocks) * SF / 16u) : 0u;
+  const std::uint32_t S = SF ? static_cast<std::uint32_t>(static_cast<std::uint64_t>(a.nblocks) * SF / SD) : 0u;
   const std::uint32_t NC = (a.nblocks - S + C - 1) / C;  // pool chunks; only the last is partial
   const std::uint64_t brow = static_cast<std::uint64_t>(R) * kRow;  // bytes per block
   const std::uintptr_t loff = lane * kSeg;
@@ -118,7 +119,7 @@ __device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint3
   if constexpr (SF != 0) {  // static region: the packed loop itself (no per-row chunk bookkeeping)
     const std::uint32_t s0 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave) * S / W);
     const std::uint32_t s1 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave + 1) * S / W);
-    if (s1 > s0) dev::crc_packed_body<DEPTH, ILP, R1, false, 0, 0, 0, true>(a, lds, s0, s1 - s0);
+    if (s1 > s0) dev::crc_packed_body<DEPTH, ILP, R1, false, 0, 0, 0, true, 0, SP>(a, lds, s0, s1 - s0);
   }
   if (!SF && xi < psize(xp)) cur = pchunk(xp, xi);
   else live = steal(cur);
@@ -545,19 +546,19 @@ void PD(RowsArgs a, hipStream_t s) {
   else hipLaunchKernelGGL((k_packed_dyn<D, I, false, T, CR>), dim3(g_ncu), dim3(T), 0, s, a);
 }
 
-template <int D, int I, bool R1, int T, int CR, std::uint32_t PM, int SF>
+template <int D, int I, bool R1, int T, int CR, std::uint32_t PM, int SF, int SD, int SP>
 __global__ __launch_bounds__(T) void k_packed_xq(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_xq_body<D, I, R1, CR, PM, SF>(a, lds);
+  dev::crc_packed_xq_body<D, I, R1, CR, PM, SF, SD, SP>(a, lds);
 }
 
 std::uint32_t* g_xq = nullptr;  // pool heads + exit count of the xq variants (zeroed once)
 
-template <int D, int I, int CR, std::uint32_t PM = 0, int SF = 0, int T = 1024>
+template <int D, int I, int CR, std::uint32_t PM = 0, int SF = 0, int T = 1024, int SD = 16, int SP = 0>
 void PX(RowsArgs a, hipStream_t s) {
   a.wg_ctr = g_xq;
-  if (a.len == kRow) hipLaunchKernelGGL((k_packed_xq<D, I, true, T, CR, PM, SF>), dim3(g_ncu), dim3(T), 0, s, a);
-  else hipLaunchKernelGGL((k_packed_xq<D, I, false, T, CR, PM, SF>), dim3(g_ncu), dim3(T), 0, s, a);
+  if (a.len == kRow) hipLaunchKernelGGL((k_packed_xq<D, I, true, T, CR, PM, SF, SD, SP>), dim3(g_ncu), dim3(T), 0, s, a);
+  else hipLaunchKernelGGL((k_packed_xq<D, I, false, T, CR, PM, SF, SD, SP>), dim3(g_ncu), dim3(T), 0, s, a);
 }
 
 // Start-stagger probe: before the production packed body, each wave (PERWAVE) or workgroup sleeps
@@ -646,7 +647,10 @@ const V kVariants[] = {
     {"dyn D4 I2 C64", PD<4, 2, 64>}, {"dyn T768 D4 I2 C16", PD<4, 2, 16, 768>},
     {"xq D4 I2 C16", PX<4, 2, 16>},
     {"hy S14 C8", PX<4, 2, 8, 0, 14>}, {"hy S12 C8", PX<4, 2, 8, 0, 12>}, {"hy S10 C8", PX<4, 2, 8, 0, 10>},
-    {"hy S12 C16", PX<4, 2, 16, 0, 12>}, {"hy S12 C32", PX<4, 2, 32, 0, 12>}, {"hy S8 C16", PX<4, 2, 16, 0, 8>},
+    {"hy S12 C16", PX<4, 2, 16, 0, 12>},
+    {"tail S60/64 C8 p3", PX<4, 2, 8, 0, 60, 1024, 64, 3>}, {"tail S62/64 C8 p3", PX<4, 2, 8, 0, 62, 1024, 64, 3>},
+    {"tail S63/64 C8 p3", PX<4, 2, 8, 0, 63, 1024, 64, 3>}, {"tail S60/64 C16 p3", PX<4, 2, 16, 0, 60, 1024, 64, 3>},
+    {"tail S56/64 C8 p3", PX<4, 2, 8, 0, 56, 1024, 64, 3>}, {"hy S12 C32", PX<4, 2, 32, 0, 12>}, {"hy S8 C16", PX<4, 2, 16, 0, 8>},
     {"pp T1024 D4 I2", PP<4, 2, 1024>}, {"pp T1024 D4 I1", PP<4, 1, 1024>}, {"pp T1024 D3 I1", PP<3, 1, 1024>},
     {"pp T768 D4 I2", PP<4, 2, 768>}, {"pp T768 D6 I2", PP<6, 2, 768>}, {"pp T768 D6 I3", PP<6, 3, 768>},
     {"pp T512 D8 I4", PP<8, 4, 512>}, {"pp T512 D6 I2", PP<6, 2, 512>}, {"pp T512 D8 I2", PP<8, 2, 512>},
