@@ -28,7 +28,12 @@ namespace tkv::dev {
 // finish zeroes them all for the next launch on this stream (they must be zero before the first).
 // PERM != 0 (explorer): the pool's q-th chunk is chunk (q * PERM) mod pool size (sizes powers of 2).
 // SD: SF is in 1/SD-ths of the blocks; SP: issue priority (set_prio_from_left<SP>) in the static region.
-template <int DEPTH, int ILP, bool R1, int CROWS, std::uint32_t PERM = 0, int SF = 0, int SD = 16, int SP = 0>
+// LEAN: no exit counter and no blind walk over dry pools. The heads of this launch are a.wg_ctr; the
+// host alternates two head sets between launches and passes the other one in a.prog, which
+// workgroup 0 zeroes for the next launch. A wave whose pool ran dry reads all eight heads (one sc1
+// load per lane 0-7) and grabs from the pool with the most chunks left, until none has any.
+template <int DEPTH, int ILP, bool R1, int CROWS, std::uint32_t PERM = 0, int SF = 0, int SD = 16, int SP = 0,
+          bool LEAN = false>
 __device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
   static_assert(CROWS % DEPTH == 0 && CROWS >= 2 * DEPTH && CROWS <= 64, "chunk shape");
@@ -102,6 +107,33 @@ __device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint3
   };
   // Blocking search from pool gp on (start, and after a pool runs dry): false once all 8 are dry.
   auto steal = [&](Chunk& out) -> bool {
+    if constexpr (LEAN) {
+      for (int tries = 0; tries < 64; ++tries) {
+        std::int32_t left = -1;
+        if (lane < 8u) {
+          const std::uint32_t h = __hip_atomic_load(vctr + lane * kCtrStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          left = static_cast<std::int32_t>(psize(lane)) - static_cast<std::int32_t>(h);
+        }
+        std::int32_t best = 0;
+        std::uint32_t by = 0;
+#pragma unroll
+        for (std::uint32_t y = 0; y < 8u; ++y) {
+          const std::int32_t l = __builtin_amdgcn_readlane(left, y);
+          if (l > best) {
+            best = l;
+            by = y;
+          }
+        }
+        if (best <= 0) return false;
+        gp = by;
+        const std::uint32_t q = __builtin_amdgcn_readfirstlane(grab());
+        if (q < psize(gp)) {
+          out = pchunk(gp, q);
+          return true;
+        }
+      }
+      return false;
+    }
     while (seen < 8u) {
       const std::uint32_t q = pstat(gp) + __builtin_amdgcn_readfirstlane(grab());
       if (q < psize(gp)) {
@@ -116,6 +148,11 @@ __device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint3
 
   Chunk cur{}, nxt{};
   bool live = true;
+  if constexpr (LEAN) {
+    if (blockIdx.x == 0 && threadIdx.x < 8u)
+      __hip_atomic_store(reinterpret_cast<std::uint32_t*>(a.prog) + threadIdx.x * kCtrStride, 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
   if constexpr (SF != 0) {  // static region: the packed loop itself (no per-row chunk bookkeeping)
     const std::uint32_t s0 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave) * S / W);
     const std::uint32_t s1 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave + 1) * S / W);
@@ -219,7 +256,7 @@ __device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint3
           nv = grab();
         } else {  // pool gp ran dry: search the others, then restart the row pipeline
           ++seen;
-          gp = (gp + 1u) & 7u;
+          if constexpr (!LEAN) gp = (gp + 1u) & 7u;
           if (!steal(cur)) break;
           nv = grab();
           prologue();
@@ -230,7 +267,7 @@ __device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint3
     }
   }
   // The last wave out zeroes the pool heads and the exit count for the next launch.
-  if (lane == 0) {
+  if (!LEAN && lane == 0) {
     std::uint32_t* done = vctr + 8u * kCtrStride;
     if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == W - 1u) {
 #pragma unroll
@@ -546,13 +583,26 @@ void PD(RowsArgs a, hipStream_t s) {
   else hipLaunchKernelGGL((k_packed_dyn<D, I, false, T, CR>), dim3(g_ncu), dim3(T), 0, s, a);
 }
 
-template <int D, int I, bool R1, int T, int CR, std::uint32_t PM, int SF, int SD, int SP>
+template <int D, int I, bool R1, int T, int CR, std::uint32_t PM, int SF, int SD, int SP, bool LN = false>
 __global__ __launch_bounds__(T) void k_packed_xq(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_xq_body<D, I, R1, CR, PM, SF, SD, SP>(a, lds);
+  dev::crc_packed_xq_body<D, I, R1, CR, PM, SF, SD, SP, LN>(a, lds);
 }
 
 std::uint32_t* g_xq = nullptr;  // pool heads + exit count of the xq variants (zeroed once)
+std::uint32_t* g_lean = nullptr;  // two head sets of the LEAN variants (zeroed once, then by the kernels)
+
+template <int D, int I, int CR, int SF, int SD>
+void PL(RowsArgs a, hipStream_t s) {
+  static int par = 0;
+  par ^= 1;
+  a.wg_ctr = g_lean + par * 8 * kCtrStride;
+  a.prog = reinterpret_cast<unsigned long long*>(g_lean + (par ^ 1) * 8 * kCtrStride);
+  if (a.len == kRow)
+    hipLaunchKernelGGL((k_packed_xq<D, I, true, 1024, CR, 0, SF, SD, 3, true>), dim3(g_ncu), dim3(1024), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_packed_xq<D, I, false, 1024, CR, 0, SF, SD, 3, true>), dim3(g_ncu), dim3(1024), 0, s, a);
+}
 
 template <int D, int I, int CR, std::uint32_t PM = 0, int SF = 0, int T = 1024, int SD = 16, int SP = 0>
 void PX(RowsArgs a, hipStream_t s) {
@@ -650,7 +700,10 @@ const V kVariants[] = {
     {"hy S12 C16", PX<4, 2, 16, 0, 12>},
     {"tail S60/64 C8 p3", PX<4, 2, 8, 0, 60, 1024, 64, 3>}, {"tail S62/64 C8 p3", PX<4, 2, 8, 0, 62, 1024, 64, 3>},
     {"tail S63/64 C8 p3", PX<4, 2, 8, 0, 63, 1024, 64, 3>}, {"tail S60/64 C16 p3", PX<4, 2, 16, 0, 60, 1024, 64, 3>},
-    {"tail S56/64 C8 p3", PX<4, 2, 8, 0, 56, 1024, 64, 3>}, {"hy S12 C32", PX<4, 2, 32, 0, 12>}, {"hy S8 C16", PX<4, 2, 16, 0, 8>},
+    {"tail S56/64 C8 p3", PX<4, 2, 8, 0, 56, 1024, 64, 3>},
+    {"lean S56/64 C8", PL<4, 2, 8, 56, 64>}, {"lean S60/64 C8", PL<4, 2, 8, 60, 64>},
+    {"lean S62/64 C8", PL<4, 2, 8, 62, 64>}, {"lean S60/64 C16", PL<4, 2, 16, 60, 64>},
+    {"lean S48/64 C8", PL<4, 2, 8, 48, 64>}, {"lean S32/64 C16", PL<4, 2, 16, 32, 64>}, {"hy S12 C32", PX<4, 2, 32, 0, 12>}, {"hy S8 C16", PX<4, 2, 16, 0, 8>},
     {"pp T1024 D4 I2", PP<4, 2, 1024>}, {"pp T1024 D4 I1", PP<4, 1, 1024>}, {"pp T1024 D3 I1", PP<3, 1, 1024>},
     {"pp T768 D4 I2", PP<4, 2, 768>}, {"pp T768 D6 I2", PP<6, 2, 768>}, {"pp T768 D6 I3", PP<6, 3, 768>},
     {"pp T512 D8 I4", PP<8, 4, 512>}, {"pp T512 D6 I2", PP<6, 2, 512>}, {"pp T512 D8 I2", PP<8, 2, 512>},
@@ -747,6 +800,8 @@ extern "C" int explore_run(int v, const std::uint8_t* base, std::uint64_t n, std
     hipMalloc(&g_ctr, 4 * kCtrStride * g_ncu);
     hipMalloc(&g_xq, 4 * kCtrStride * 9);
     hipMemset(g_xq, 0, 4 * kCtrStride * 9);
+    hipMalloc(&g_lean, 4 * kCtrStride * 16);
+    hipMemset(g_lean, 0, 4 * kCtrStride * 16);
   }
   if (v == kNV) {
     hipLaunchKernelGGL(k_stream<256>, dim3(g_ncu * 8), dim3(256), 0, st, reinterpret_cast<const uint4*>(base),
