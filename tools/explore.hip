@@ -592,6 +592,73 @@ __global__ __launch_bounds__(T) void k_packed_xq(RowsArgs a) {
 std::uint32_t* g_xq = nullptr;  // pool heads + exit count of the xq variants (zeroed once)
 std::uint32_t* g_lean = nullptr;  // two head sets of the LEAN variants (zeroed once, then by the kernels)
 
+// Static share SF/SD of the blocks as the product (priority 3, skew for multi-row blocks), then the
+// rest in chunks of C blocks taken from eight heads (alternating head sets as PL), each chunk run by
+// the product loop itself (crc_packed_body on the chunk's block range: a full pipeline per chunk, no
+// per-row bookkeeping). A wave whose head is dry grabs from the fullest head.
+template <int C, int SF, int SD, bool R1>
+__global__ __launch_bounds__(1024) void k_packed_chunks(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  dev::fill_lds(a.tabs, lds);
+  __syncthreads();
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint32_t wpg = blockDim.x >> 6;
+  const std::uint32_t wave = blockIdx.x * wpg + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t W = gridDim.x * wpg;
+  if (blockIdx.x == 0 && threadIdx.x < 8u)
+    __hip_atomic_store(reinterpret_cast<std::uint32_t*>(a.prog) + threadIdx.x * kCtrStride, 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  const std::uint32_t S = static_cast<std::uint32_t>(static_cast<std::uint64_t>(a.nblocks) * SF / SD);
+  const std::uint32_t s0 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave) * S / W);
+  const std::uint32_t s1 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave + 1) * S / W);
+  if (s1 > s0) dev::crc_packed_body<4, 2, R1, false, 0, 0, 0, true, 0, 3>(a, lds, s0, s1 - s0);
+  const std::uint32_t NC = (a.nblocks - S + C - 1) / C;
+  auto plo = [&](std::uint32_t y) { return static_cast<std::uint32_t>(static_cast<std::uint64_t>(y) * NC / 8u); };
+  auto psize = [&](std::uint32_t y) { return plo(y + 1) - plo(y); };
+  std::uint32_t vzero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+  std::uint32_t* const vctr = a.wg_ctr + vzero;
+  std::uint32_t gp = blockIdx.x & 7u;
+  for (int tries = 0; tries < 1 << 20; ++tries) {
+    std::uint32_t v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(vctr + gp * kCtrStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const std::uint32_t q = __builtin_amdgcn_readfirstlane(v);
+    if (q < psize(gp)) {
+      const std::uint32_t fb = S + (plo(gp) + q) * C;
+      dev::crc_packed_body<4, 2, R1, false, 0, 0, 0, true, 0, 0>(a, lds, fb, a.nblocks - fb < C ? a.nblocks - fb : C);
+      continue;
+    }
+    std::int32_t left = -1;
+    if (lane < 8u) {
+      const std::uint32_t h = __hip_atomic_load(vctr + lane * kCtrStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      left = static_cast<std::int32_t>(psize(lane)) - static_cast<std::int32_t>(h);
+    }
+    std::int32_t best = 0;
+    std::uint32_t by = 0;
+#pragma unroll
+    for (std::uint32_t y = 0; y < 8u; ++y) {
+      const std::int32_t l = __builtin_amdgcn_readlane(left, y);
+      if (l > best) {
+        best = l;
+        by = y;
+      }
+    }
+    if (best <= 0) break;
+    gp = by;
+  }
+}
+
+template <int C, int SF, int SD>
+void PC2(RowsArgs a, hipStream_t s) {
+  static int par = 0;
+  par ^= 1;
+  a.nwaves = g_ncu * 16;
+  a.wg_ctr = g_lean + par * 8 * kCtrStride;
+  a.prog = reinterpret_cast<unsigned long long*>(g_lean + (par ^ 1) * 8 * kCtrStride);
+  if (a.len == kRow) hipLaunchKernelGGL((k_packed_chunks<C, SF, SD, true>), dim3(g_ncu), dim3(1024), 0, s, a);
+  else hipLaunchKernelGGL((k_packed_chunks<C, SF, SD, false>), dim3(g_ncu), dim3(1024), 0, s, a);
+}
+
 template <int D, int I, int CR, int SF, int SD>
 void PL(RowsArgs a, hipStream_t s) {
   static int par = 0;
@@ -703,7 +770,11 @@ const V kVariants[] = {
     {"tail S56/64 C8 p3", PX<4, 2, 8, 0, 56, 1024, 64, 3>},
     {"lean S56/64 C8", PL<4, 2, 8, 56, 64>}, {"lean S60/64 C8", PL<4, 2, 8, 60, 64>},
     {"lean S62/64 C8", PL<4, 2, 8, 62, 64>}, {"lean S60/64 C16", PL<4, 2, 16, 60, 64>},
-    {"lean S48/64 C8", PL<4, 2, 8, 48, 64>}, {"lean S32/64 C16", PL<4, 2, 16, 32, 64>}, {"hy S12 C32", PX<4, 2, 32, 0, 12>}, {"hy S8 C16", PX<4, 2, 16, 0, 8>},
+    {"lean S48/64 C8", PL<4, 2, 8, 48, 64>}, {"lean S32/64 C16", PL<4, 2, 16, 32, 64>},
+    {"chunks S60/64 C32", PC2<32, 60, 64>}, {"chunks S62/64 C32", PC2<32, 62, 64>},
+    {"chunks S60/64 C64", PC2<64, 60, 64>}, {"chunks S56/64 C64", PC2<64, 56, 64>},
+    {"chunks S62/64 C16", PC2<16, 62, 64>},
+    {"chunks S60/64 C2", PC2<2, 60, 64>}, {"chunks S62/64 C2", PC2<2, 62, 64>}, {"chunks S60/64 C4", PC2<4, 60, 64>}, {"hy S12 C32", PX<4, 2, 32, 0, 12>}, {"hy S8 C16", PX<4, 2, 16, 0, 8>},
     {"pp T1024 D4 I2", PP<4, 2, 1024>}, {"pp T1024 D4 I1", PP<4, 1, 1024>}, {"pp T1024 D3 I1", PP<3, 1, 1024>},
     {"pp T768 D4 I2", PP<4, 2, 768>}, {"pp T768 D6 I2", PP<6, 2, 768>}, {"pp T768 D6 I3", PP<6, 3, 768>},
     {"pp T512 D8 I4", PP<8, 4, 512>}, {"pp T512 D6 I2", PP<6, 2, 512>}, {"pp T512 D8 I2", PP<8, 2, 512>},
