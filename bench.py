@@ -236,21 +236,24 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # One HIP event pair on the launch stream brackets the K steps; the average launch duration is
+    # their span / K. Event markers between steps would each hold the next launch back by ~10 us
+    # (rocprofv3 kernel trace: back-to-back launches start 0 us after their predecessor ends,
+    # 10.4 us with two markers between them), a cost no caller pays.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
-        starts[i].record(stream)
         step(stream)
-        ends[i].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
     # correctness of this exact buffer, from the last timed step (checked after the timed region so
     # no CPU pause lets the clocks fall between warmup and timing)
