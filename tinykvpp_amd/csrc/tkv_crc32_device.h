@@ -688,13 +688,16 @@ __device__ __forceinline__ void crc_small_body(const RowsArgs& a, std::uint32_t*
 // ranges, slots 12-15 the smallest, matching the issue arbitration that favours a SIMD's older waves.
 // PRIO (0: off): set_prio_from_left<PRIO> once per DEPTH rows (the product uses 3, and SKEW 154 for
 // blocks of more than one row; tkv_crc32_kernels.hip).
+// EARLY: a wave issues its first DEPTH-ILP row loads before the LDS table fill, so the fill and the
+// first loads' latency overlap (explorer probe).
 template <int DEPTH, int ILP, bool R1, bool SPLIT = false, std::uint32_t ROT = 0, int CHK = 0, int PROG = 0,
-          bool SUB = false, int SKEW = 0, int PRIO = 0>
+          bool SUB = false, int SKEW = 0, int PRIO = 0, bool EARLY = false>
 __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds, std::uint32_t sub_b0 = 0,
                                                 std::uint32_t sub_nb = 0) {
   static_assert(CHK == 0 || (R1 && ROT == 0 && CHK <= 6), "chunk-strided map: R1 only, chunks of <= 64 blocks");
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
-  if constexpr (!SUB) fill_lds(a.tabs, lds);
+  static_assert(!EARLY || (!SUB && ROT == 0 && CHK == 0), "early issue: whole-kernel contiguous map only");
+  if constexpr (!SUB && !EARLY) fill_lds(a.tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
   const LaneConst kc = lane_const(lane);
   const std::uint32_t hcon = a.tabs->horner[lane & 31u];  // Shift_4096(1 << (l & 31))
@@ -709,7 +712,7 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
     s32lo = (&a.tabs->shift32[0][0])[lane];
     s32hi = (&a.tabs->shift32[0][0])[64 + lane];
   }
-  if constexpr (!SUB) __syncthreads();
+  if constexpr (!SUB && !EARLY) __syncthreads();
 
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint64_t W = a.nwaves;
@@ -734,7 +737,7 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
     b0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W);
     nb = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W) - b0;
   }
-  if (nb == 0) return;
+  if (!EARLY && nb == 0) return;  // EARLY: such a wave still fills its share of the tables
   const std::uint32_t nrows = nb * R;  // wave-local rows j = 0 .. nrows-1, contiguous in memory
   // CHK: global block of wave-local block j
   auto gblk = [&](std::uint32_t j) -> std::uint64_t {
@@ -806,8 +809,18 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
     }
   };
 
+  if constexpr (EARLY) {
+    if (nb != 0) {
 #pragma unroll
-  for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
+      for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
+    }
+    fill_lds(a.tabs, lds);
+    __syncthreads();
+    if (nb == 0) return;
+  } else {
+#pragma unroll
+    for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
+  }
   for (std::uint32_t j = 0; j < nrows; j += DEPTH) {
     if constexpr (PROG > 0) {
       if (j % PROG == 0) stamp(1 + j / PROG);

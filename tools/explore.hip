@@ -697,17 +697,17 @@ void PS(RowsArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_packed_stag<K, PW>), dim3(g_ncu), dim3(1024), 0, s, a);
 }
 
-template <int SK, int PR>
+template <int SK, int PR, bool EA = false>
 __global__ __launch_bounds__(1024) void k_packed_skew(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  if (a.len == kRow) dev::crc_packed_body<4, 2, true, false, 0, 0, 0, false, SK, PR>(a, lds);
-  else dev::crc_packed_body<4, 2, false, false, 0, 0, 0, false, SK, PR>(a, lds);
+  if (a.len == kRow) dev::crc_packed_body<4, 2, true, false, 0, 0, 0, false, SK, PR, EA>(a, lds);
+  else dev::crc_packed_body<4, 2, false, false, 0, 0, 0, false, SK, PR, EA>(a, lds);
 }
 
-template <int SK, int PR = 0>
+template <int SK, int PR = 0, bool EA = false>
 void PW(RowsArgs a, hipStream_t s) {
   a.nwaves = g_ncu * 16;
-  hipLaunchKernelGGL((k_packed_skew<SK, PR>), dim3(g_ncu), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL((k_packed_skew<SK, PR, EA>), dim3(g_ncu), dim3(1024), 0, s, a);
 }
 
 // grid of M workgroups per CU (M rounds): a CU whose workgroup finishes early takes the next one
@@ -781,7 +781,7 @@ const V kVariants[] = {
     {"skew 0.8", PW<205>}, {"skew 0.6", PW<154>}, {"prio", PW<0, 1>}, {"prio skew 0.8", PW<205, 1>},
     {"prio skew 0.6", PW<154, 1>}, {"pri2", PW<0, 2>}, {"pri3", PW<0, 3>}, {"pri2 skew 0.6", PW<154, 2>},
     {"pri3 skew 0.6", PW<154, 3>}, {"pri4", PW<0, 4>}, {"pri5", PW<0, 5>}, {"pri4 skew 0.6", PW<154, 4>},
-    {"pri5 skew 0.6", PW<154, 5>}, {"pri3 skew 0.5", PW<128, 3>}, {"pri3 skew 0.7", PW<179, 3>},    {"stag wave 4", PS<4, true>}, {"stag wave 16", PS<16, true>}, {"stag wg 4", PS<4, false>},
+    {"pri5 skew 0.6", PW<154, 5>}, {"pri3 skew 0.5", PW<128, 3>}, {"pri3 skew 0.7", PW<179, 3>}, {"pri3 early", PW<0, 3, true>}, {"pri3 skew 0.6 early", PW<154, 3, true>},    {"stag wave 4", PS<4, true>}, {"stag wave 16", PS<16, true>}, {"stag wg 4", PS<4, false>},
     {"stag wg 16", PS<16, false>}, {"stag wave 1", PS<1, true>},
     {"grid x2", PG<2>}, {"grid x3", PG<3>}, {"grid x4", PG<4>}, {"grid x8", PG<8>}, {"grid x16", PG<16>},
     {"packed D4 I2", PK<4, 2>}, {"packed D4 I1", PK<4, 1>}, {"packed D3 I1", PK<3, 1>},
