@@ -153,20 +153,20 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
 // Scatter of one block (rows_finish): e = its exclusive (small count, rows) pair, TR = rows of all
 // large blocks. A large block cut between row-kernel waves gets its result zeroed here, since the
 // row kernel XORs every piece of it into the result (crc_rows_body, irregular batches).
-__device__ __forceinline__ void finish_block(const std::uint64_t* offsets, const std::uint32_t* lengths,
-                                             std::uint64_t b, std::uint64_t e, std::uint64_t TR, const PrepassOut& o,
-                                             std::uint32_t W, std::uint32_t* out) {
-  const std::uint32_t len = lengths[b];
+// len and off are the block's length and offset (loaded by the caller).
+__device__ __forceinline__ void finish_block(std::uint64_t off, std::uint32_t len, std::uint64_t b, std::uint64_t e,
+                                             std::uint64_t TR, const PrepassOut& o, std::uint32_t W,
+                                             std::uint32_t* out) {
   const std::uint32_t nsmall = static_cast<std::uint32_t>(e);
   if (len <= kSmallMax) {
-    o.s_off[nsmall] = offsets[b];
+    o.s_off[nsmall] = off;
     o.s_len[nsmall] = len;
     o.s_idx[nsmall] = static_cast<std::uint32_t>(b);
     return;
   }
   const std::uint32_t k = static_cast<std::uint32_t>(b) - nsmall;  // compacted index
   const std::uint64_t lo = e >> 32;
-  o.big_off[k] = offsets[b];
+  o.big_off[k] = off;
   o.big_len[k] = len;
   o.big_idx[k] = static_cast<std::uint32_t>(b);
   o.row_scan[k] = static_cast<std::uint32_t>(lo);
@@ -184,7 +184,7 @@ __global__ void rows_finish(const std::uint64_t* offsets, const std::uint32_t* l
                             PrepassOut o, std::uint32_t W, std::uint32_t* out) {
   const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
   if (b >= n) return;
-  finish_block(offsets, lengths, b, scan[b] + tile_offs[b / kScanTile], counts[2], o, W, out);
+  finish_block(offsets[b], lengths[b], b, scan[b] + tile_offs[b / kScanTile], counts[2], o, W, out);
 }
 
 // rows_finish with the scan of the tile sums folded in (ntiles <= kFusedTiles): every workgroup sums
@@ -197,34 +197,47 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n, const std::uint64_t* scan,
     const std::uint64_t* tile_sums, std::uint32_t ntiles, std::uint32_t* counts, PrepassOut o, std::uint32_t W,
     std::uint32_t* out) {
-  __shared__ std::uint64_t red[2][kFinishThreads];
+  constexpr std::uint32_t kWaves = kFinishThreads / 64;
+  __shared__ std::uint64_t red[2][kWaves];
   const std::uint32_t my_tile = blockIdx.x * kFinishThreads / kScanTile;  // kScanTile % 256 == 0
+  // The block's own operands are loaded first, so their latency overlaps the tile-sum reduction.
+  const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(kFinishThreads) + threadIdx.x;
+  const bool live = b < n;
+  const std::uint32_t len = live ? lengths[b] : 0u;
+  const std::uint64_t off = live ? offsets[b] : 0ull;
+  const std::uint64_t sc = live ? scan[b] : 0ull;
   std::uint64_t before = 0, all = 0;
   for (std::uint32_t i = threadIdx.x; i < ntiles; i += kFinishThreads) {
     const std::uint64_t v = tile_sums[i];
     all += v;
     before += i < my_tile ? v : 0ull;
   }
-  red[0][threadIdx.x] = before;
-  red[1][threadIdx.x] = all;
-  __syncthreads();
-  for (std::uint32_t h = kFinishThreads / 2; h > 0; h >>= 1) {
-    if (threadIdx.x < h) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + h];
-      red[1][threadIdx.x] += red[1][threadIdx.x + h];
-    }
-    __syncthreads();
+  // Wave sums by cross-lane exchange, then the kWaves partial sums through LDS (one barrier).
+#pragma unroll
+  for (unsigned m = 32; m > 0; m >>= 1) {
+    before += __shfl_xor(before, m, 64);
+    all += __shfl_xor(all, m, 64);
   }
-  const std::uint64_t tile_off = red[0][0], total = red[1][0];
+  const unsigned wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63u) == 0) {
+    red[0][wid] = before;
+    red[1][wid] = all;
+  }
+  __syncthreads();
+  std::uint64_t tile_off = 0, total = 0;
+#pragma unroll
+  for (unsigned w = 0; w < kWaves; ++w) {
+    tile_off += red[0][w];
+    total += red[1][w];
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const std::uint32_t ns = static_cast<std::uint32_t>(total);
     counts[0] = n - ns;                                    // large blocks
     counts[1] = ns;                                        // small blocks
     counts[2] = static_cast<std::uint32_t>(total >> 32);  // rows of the large blocks
   }
-  const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(kFinishThreads) + threadIdx.x;
-  if (b >= n) return;
-  finish_block(offsets, lengths, b, scan[b] + tile_off, total >> 32, o, W, out);
+  if (!live) return;
+  finish_block(off, len, b, sc + tile_off, total >> 32, o, W, out);
 }
 
 // ---- synthetic data: byte j of block b = LE byte j%8 of
