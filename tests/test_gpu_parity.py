@@ -297,6 +297,27 @@ def test_small_block_split(gpu, oracle, mix):
     assert np.array_equal(u32(tk.crc32_batch(d, o[:m].contiguous(), ln[:m].contiguous())), want[:m])
 
 
+def test_irregular_more_than_fused_tiles(gpu, oracle):
+    """Batches of more than 1024 scan tiles (4096 blocks each) take the unfused prepass: tile scan,
+    single-workgroup scan of the tile sums, then the scatter (launch_prepass, tkv_crc32_kernels.hip).
+    4 M + 4097 mostly tiny blocks with a large one every 997 blocks, so both the small-block phase
+    and the row kernel's wave partition see tiles past the fused limit."""
+    rng = np.random.default_rng(4097)
+    n = 4096 * 1024 + 4097
+    lens = rng.integers(0, 65, n).astype(np.int64)
+    lens[::997] = rng.integers(1025, 9000, lens[::997].size)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+    host = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+    d = torch.from_numpy(host).to(gpu)
+    o = torch.from_numpy(offs).to(gpu)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    want = oracle.batch(host, offs, lens)
+    assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), want)
+    # the same stream's scratch then serves a fused-size batch
+    m = 4096 * 1024 - 1
+    assert np.array_equal(u32(tk.crc32_batch(d, o[:m].contiguous(), ln[:m].contiguous())), want[:m])
+
+
 def test_irregular_zipf_sample(gpu, oracle):
     """First 4096 blocks of cfg4 (Zipf 256 B - 1 MiB), packed back to back, unaligned starts."""
     c = golden("synthetic.json")["cfg4"]
