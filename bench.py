@@ -46,14 +46,73 @@ def rank_shard(rank, nblocks):
     return rank * nblocks, nblocks
 
 
-def reduce_timing(elapsed, kernel_ms, bit_exact, dist, dev=None):
-    """Max over ranks of wall time and per-launch time; AND of the ranks' bit-exact checks."""
+def reduce_timing(elapsed, kernel_ms, bit_exact, dist, dev=None, full=True):
+    """Max over ranks of wall time and per-launch time; AND of the ranks' bit-exact checks and of
+    their full-shard coverage; the number of ranks that took part (SUM of ones, must equal
+    WORLD_SIZE)."""
     import torch
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    ok = torch.tensor([1 if bit_exact else 0], dtype=torch.int32, device=dev)
+    ok = torch.tensor([1 if bit_exact else 0, 1 if full else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    return float(t[0]), float(t[1]), bool(ok.item())
+    seen = torch.ones(1, dtype=torch.int32, device=dev)
+    dist.all_reduce(seen, op=dist.ReduceOp.SUM)
+    return float(t[0]), float(t[1]), bool(ok[0].item()), int(seen.item()), bool(ok[1].item())
+
+
+def shard_golden(config, first, nblocks):
+    """Golden XOR/SUM32 of synthetic blocks [first, first + nblocks) of `config` (tests/golden/
+    synthetic.json "shards", written by tests/golden/make_golden.py --shards from the reference
+    crc32 and the oracle), or None when no committed shard matches (then only the 64-block probe
+    checks the run)."""
+    with open(os.path.join(ROOT, "tests", "golden", "synthetic.json")) as f:
+        g = json.load(f)
+    for sh in g.get("shards", {}).get(config, []):
+        if sh["first_block"] == first and sh["nblocks"] == nblocks:
+            return sh
+    return None
+
+
+def check_shard(crcs, golden):
+    """Every block of the shard against its golden aggregate (XOR and SUM32 of the CRCs)."""
+    x = int(np.bitwise_xor.reduce(crcs))
+    s = int(crcs.astype(np.uint64).sum() & 0xFFFFFFFF)
+    return x == golden["xor"] and s == golden["sum32"]
+
+
+def verify_rank(ora, config, first, crcs, blen=None, lens=None):
+    """This rank's CRCs of synthetic blocks [first, first + len(crcs)): the first 64 blocks against
+    the oracle, and every block against the shard's golden XOR/SUM32 when one is committed.
+    Returns (bit_exact, full) where full says the whole shard was covered."""
+    probe = np.zeros(64, np.uint32)
+    if blen is None:
+        ora.oracle_crc_synthetic_lens.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
+        ora.oracle_crc_synthetic_lens(1, first, 64, np.ascontiguousarray(lens[:64], np.uint64).ctypes.data,
+                                      probe.ctypes.data)
+    else:
+        ora.oracle_crc_synthetic(1, first, 64, blen, probe.ctypes.data)
+    ok = bool(np.array_equal(crcs[:64], probe))
+    gold = shard_golden(config, first, crcs.size)
+    if gold is not None:
+        ok = ok and check_shard(crcs, gold)
+    return ok, gold is not None
+
+
+def warm_up(step, steps, min_ms):
+    """At least `steps` untimed steps, continued until `min_ms` of wall time have passed: the
+    shader clock ramps over the first few hundred ms of load, and a handful of steps (--warmup 5 is
+    ~4 ms on cfg2) leaves the timed steps on a cold clock (profiles/r1/irr_compare_warmup.txt: the
+    first rounds read up to 10 % low). Steps are issued in groups of 8 with a sync between groups,
+    so the host does not queue seconds of work ahead of the clock check."""
+    import torch
+    t0 = time.perf_counter()
+    done = 0
+    while done < steps or (time.perf_counter() - t0) * 1e3 < min_ms:
+        for _ in range(8 if done >= steps else min(8, steps - done)):
+            step()
+            done += 1
+        torch.cuda.synchronize()
+    return done, (time.perf_counter() - t0) * 1e3
 
 
 def pmc_traffic(csv_path, config):
@@ -174,6 +233,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--min-warmup-ms", type=float, default=1000.0,
+                    help="keep warming up (untimed) until this much wall time has passed (clock ramp)")
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="cfg3: skip the host-memory end-to-end measurement")
@@ -232,9 +293,7 @@ def main():
             tk.crc32_batch_uniform(data, blen, nblocks, out=o, stream=strm)
     torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+    warm_steps, warm_ms = warm_up(step, args.warmup, args.min_warmup_ms)
 
     # One HIP event pair on the launch stream brackets the K steps; the average launch duration is
     # their span / K. Event markers between steps would each hold the next launch back by ~10 us
@@ -258,20 +317,16 @@ def main():
     # correctness of this exact buffer, from the last timed step (checked after the timed region so
     # no CPU pause lets the clocks fall between warmup and timing)
     crcs = out.cpu().numpy().view(np.uint32).copy()
-    probe = np.zeros(64, np.uint32)
-    if blen is None:
-        ora.oracle_crc_synthetic_lens.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
-        ora.oracle_crc_synthetic_lens(1, first, 64, lens.ctypes.data, probe.ctypes.data)
-    else:
-        ora.oracle_crc_synthetic(1, first, 64, blen, probe.ctypes.data)
-    bit_exact = bool(np.array_equal(crcs[:64], probe))
-    with open(os.path.join(ROOT, "tests", "golden", "synthetic.json")) as f:
-        g = json.load(f)[args.config]
-    if world == 1 and g["nblocks"] == nblocks:  # the whole config on this GPU: golden aggregate
-        bit_exact = bit_exact and int(np.bitwise_xor.reduce(crcs)) == g["xor"]
+    bit_exact, full = verify_rank(ora, args.config, first, crcs, blen, None if blen else lens)
+    ranks_seen = 1
     if world > 1:
-        elapsed, kernel_ms, bit_exact = reduce_timing(elapsed, kernel_ms, bit_exact, dist,
-                                                      dev if backend == "nccl" else None)
+        elapsed, kernel_ms, bit_exact, ranks_seen, full = reduce_timing(
+            elapsed, kernel_ms, bit_exact, dist, dev if backend == "nccl" else None, full)
+    if full:
+        scope = f"every block of every rank's shard (golden XOR/SUM32 of blocks [r*{nblocks}, (r+1)*{nblocks})) " \
+                "and its first 64 blocks against the oracle"
+    else:
+        scope = "first 64 blocks of each rank's shard against the oracle (no committed golden aggregate for some shard)"
 
     bytes_per_step = total
     total_bytes = bytes_per_step * args.steps * world
@@ -287,6 +342,8 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_run": {"steps": warm_steps, "ms": round(warm_ms, 1), "min_ms": args.min_warmup_ms,
+                       "note": "untimed; at least --warmup steps, continued until min_ms of wall time (clock ramp)"},
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
@@ -296,6 +353,8 @@ def main():
         "config": {"workload": f"{args.config}: {desc}", "blocks_per_gpu": nblocks, "block_bytes": blen or "zipf",
                    "bytes_per_gpu_per_step": bytes_per_step, "parallelism": f"batch split x{world}, no collective"},
         "bit_exact": bit_exact,
+        "bit_exact_scope": scope,
+        "ranks_seen": ranks_seen,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src, "kernel_ms": round(kernel_ms, 4),

@@ -205,3 +205,32 @@ void oracle_crc_batch_s8(const uint8_t *base, const uint64_t *offsets, const uin
                          uint32_t *out) {
   for (uint64_t i = 0; i < n; ++i) out[i] = oracle_update_s8(ORACLE_INIT, base + offsets[i], lengths[i]) ^ ORACLE_INIT;
 }
+
+/* Fast synthetic-block CRCs for the full-size checks (test side only): the §8d generator's 8-byte
+ * words fed straight into the slicing-by-8 step above, no byte buffer. Same results as
+ * oracle_crc_synthetic (tests/test_oracle.py checks both against each other and the golden
+ * fixtures); ~10x faster, so a CPU test can checksum a whole 4 GiB rank shard. */
+void oracle_crc_synthetic_s8(uint64_t seed, uint64_t first, uint64_t count, uint64_t len, uint32_t *out) {
+  ensure_s8();
+  for (uint64_t i = 0; i < count; ++i) {
+    uint64_t b = first + i;
+    uint32_t raw = ORACLE_INIT;
+    uint64_t j8 = 0;
+    for (; (j8 + 1) * 8 <= len; ++j8) {
+      uint64_t w = oracle_splitmix64((b << 24) ^ j8 ^ (seed << 56));
+      uint32_t lo = (uint32_t)w ^ raw, hi = (uint32_t)(w >> 32);
+      raw = g_s8[7][lo & 0xFFu] ^ g_s8[6][(lo >> 8) & 0xFFu] ^ g_s8[5][(lo >> 16) & 0xFFu] ^ g_s8[4][lo >> 24] ^
+            g_s8[3][hi & 0xFFu] ^ g_s8[2][(hi >> 8) & 0xFFu] ^ g_s8[1][(hi >> 16) & 0xFFu] ^ g_s8[0][hi >> 24];
+    }
+    if (j8 * 8 < len) {
+      uint64_t w = oracle_splitmix64((b << 24) ^ j8 ^ (seed << 56));
+      for (uint64_t k = 0; j8 * 8 + k < len; ++k) raw = (raw >> 8) ^ g_table[((uint8_t)(w >> (8 * k)) ^ raw) & 0xFFu];
+    }
+    out[i] = raw ^ ORACLE_INIT;
+  }
+}
+
+void oracle_crc_synthetic_lens_s8(uint64_t seed, uint64_t first, uint64_t count, const uint64_t *lens,
+                                  uint32_t *out) {
+  for (uint64_t i = 0; i < count; ++i) oracle_crc_synthetic_s8(seed, first + i, 1, lens[i], out + i);
+}

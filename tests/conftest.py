@@ -17,6 +17,36 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a GPU (MI355X); calls the HIP path through the C ABI")
 
 
+def _loaded_objects(substr):
+    """Shared objects of this process whose path contains `substr` (from /proc/self/maps)."""
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({ln.split()[-1] for ln in f if substr in ln and ln.rstrip().endswith(".so")})
+    except OSError:
+        return []
+
+
+def pytest_collection_finish(session):
+    """A GPU session states, before any test runs, which product library it loaded (absolute path,
+    as the dynamic loader mapped it) and which device architecture it runs on, so the record ties
+    the parity results to the gfx950 build of tinykvpp_amd/libtkv_crc32.so."""
+    if not any(item.get_closest_marker("gpu") for item in session.items):
+        return
+    tr = session.config.pluginmanager.get_plugin("terminalreporter")
+    say = tr.write_line if tr is not None else print
+    import torch
+    import tinykvpp_amd
+    tinykvpp_amd.load_library()
+    libs = _loaded_objects("libtkv_crc32")
+    say(f"[tkv] product library loaded: {', '.join(libs) or 'NOT MAPPED'}")
+    if torch.cuda.is_available():
+        p = torch.cuda.get_device_properties(0)
+        say(f"[tkv] device 0: {p.name}, arch {getattr(p, 'gcnArchName', '?')}, "
+            f"{p.multi_processor_count} CUs, {p.total_memory / 2**30:.0f} GiB; torch {torch.__version__}")
+    else:
+        say("[tkv] no GPU visible to torch")
+
+
 def golden(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return json.load(f)

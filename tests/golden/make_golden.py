@@ -15,7 +15,10 @@ Sources of the vectors:
                   [8, end) stored LE at offset 4), for the entries used in test/wal_test.cpp
   odd.json        prefixes of synthetic block 7 (SURVEY.md §8c "Odd lengths")
   synthetic.json  per-block CRCs of the §8d generator, first blocks of cfg2/cfg3/cfg4 plus the
-                  full-size aggregates (XOR and SUM32 over every block) with --aggregates
+                  full-size aggregates (XOR and SUM32 over every block) with --aggregates, and the
+                  per-rank shard aggregates of the multi-GPU bench (--shards): rank r of an N-GPU
+                  run checksums global blocks [r*n, (r+1)*n) of its config (bench.py rank_shard),
+                  so every rank's whole output is checked, not a probe of it
 """
 import argparse
 import ctypes
@@ -164,9 +167,84 @@ def synth_zipf(nblocks, full):
     return d
 
 
+def _agg(crcs):
+    return int(np.bitwise_xor.reduce(crcs)), int(crcs.astype(np.uint64).sum() & 0xFFFFFFFF)
+
+
+def _check_edges(first, count, length_of):
+    """The first and last block of a shard through the reference binary, the port and zlib."""
+    got = []
+    for b in (first, first + count - 1):
+        n = length_of(b)
+        buf = np.zeros(n, np.uint8)
+        ORA.oracle_fill(SEED, b, 0, buf.ctypes.data, n)
+        got.append(crc_all(buf.tobytes()))
+    return got
+
+
+def shards_uniform(unit, blen, nunits):
+    """XOR/SUM32 of synthetic blocks [u*unit, (u+1)*unit) of blen bytes, u = 0..nunits-1."""
+    res = []
+    for u in range(nunits):
+        allc = np.zeros(unit, np.uint32)
+        _parallel(lambda lo, hi: ORA.oracle_crc_synthetic(SEED, u * unit + lo, hi - lo, blen, allc[lo:].ctypes.data),
+                  unit)
+        edges = _check_edges(u * unit, unit, lambda b: blen)
+        assert edges == [int(allc[0]), int(allc[-1])], f"shard {u}: edge blocks disagree with the reference"
+        x, s = _agg(allc)
+        res.append({"first_block": u * unit, "nblocks": unit, "xor": x, "sum32": s})
+        print(f"  {blen} B shard {u}: xor {x:08x} sum32 {s:08x}", flush=True)
+    return res
+
+
+def shards_zipf(unit, nunits):
+    res = []
+    for u in range(nunits):
+        lens = np.zeros(unit, np.uint64)
+        ORA.oracle_zipf_lengths(SEED, u * unit, unit, lens.ctypes.data)
+        allc = np.zeros(unit, np.uint32)
+        _parallel(lambda lo, hi: ORA.oracle_crc_synthetic_lens(SEED, u * unit + lo, hi - lo, lens[lo:].ctypes.data,
+                                                               allc[lo:].ctypes.data), unit)
+        edges = _check_edges(u * unit, unit, lambda b: int(lens[b - u * unit]))
+        assert edges == [int(allc[0]), int(allc[-1])], f"zipf shard {u}: edge blocks disagree with the reference"
+        x, s = _agg(allc)
+        res.append({"first_block": u * unit, "nblocks": unit, "total_bytes": int(lens.sum()), "xor": x, "sum32": s})
+        print(f"  zipf shard {u}: xor {x:08x} sum32 {s:08x}", flush=True)
+    return res
+
+
+def shards(syn):
+    """Per-rank shard aggregates for bench.py --gpus N (N <= 8). cfg3 rank r = 64 KiB blocks
+    [r*256K, (r+1)*256K); cfg5 rank r = [r*512K, (r+1)*512K) = the cfg3-sized units 2r and 2r+1, and
+    the eight cfg5 shards together are the survey's 4 M x 64 KiB batch (XOR 5a7eaa3b)."""
+    out = {"rule": "rank r of an N-GPU run checksums global blocks [r*n, (r+1)*n), n = blocks per GPU"}
+    out["cfg2"] = shards_uniform(1 << 20, 4096, 8)
+    out["cfg4"] = shards_zipf(1 << 17, 8)
+    units = shards_uniform(1 << 18, 65536, 16)
+    out["cfg3"] = units[:8]
+    out["cfg5"] = []
+    for r in range(8):
+        a, b = units[2 * r], units[2 * r + 1]
+        out["cfg5"].append({"first_block": a["first_block"], "nblocks": a["nblocks"] + b["nblocks"],
+                            "xor": a["xor"] ^ b["xor"], "sum32": (a["sum32"] + b["sum32"]) & 0xFFFFFFFF})
+    for k in ("cfg2", "cfg3", "cfg4"):
+        if (out[k][0]["xor"], out[k][0]["sum32"]) != (syn[k].get("xor"), syn[k].get("sum32")) and "xor" in syn[k]:
+            sys.exit(f"{k}: shard 0 aggregate differs from the full-size aggregate")
+    x = s = 0
+    for sh in out["cfg5"]:
+        x ^= sh["xor"]
+        s = (s + sh["sum32"]) & 0xFFFFFFFF
+    if (x, s) != (syn["cfg5"]["xor"], syn["cfg5"]["sum32"]):
+        sys.exit(f"cfg5: shards combine to {x:08x}/{s:08x}, survey {syn['cfg5']['xor']:08x}/{syn['cfg5']['sum32']:08x}")
+    syn["cfg5"]["provenance"] = ("SURVEY.md §8c (reference crc32, survey session); recomputed here as the XOR/SUM32 "
+                                 "of the eight per-rank shards below (port, shard edge blocks through the reference)")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--aggregates", action="store_true", help="also compute full-size cfg2/3/4 aggregates")
+    ap.add_argument("--shards", action="store_true", help="also compute the per-rank shard aggregates (~5 min)")
     a = ap.parse_args()
     w = lambda name, obj: json.dump(obj, open(os.path.join(HERE, name), "w"), indent=1)
     w("kat.json", kat())
@@ -186,6 +264,8 @@ def main():
         for k, (x, s) in survey.items():
             if (syn[k]["xor"], syn[k]["sum32"]) != (x, s):
                 sys.exit(f"{k}: aggregate {syn[k]['xor']:08x}/{syn[k]['sum32']:08x} != survey {x:08x}/{s:08x}")
+    if a.shards:
+        syn["shards"] = shards(syn)
     w("synthetic.json", syn)
     print("golden fixtures written to", HERE)
 

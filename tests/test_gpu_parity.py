@@ -55,6 +55,49 @@ def test_update_device_tensor(gpu, oracle):
         assert tk.crc32().update(t).finalize() == oracle.crc(d.tobytes()), n
 
 
+def test_update_on_side_stream(gpu, oracle):
+    """update(tensor, stream=s) with s not the current stream: the kernel on s must see bytes the
+    current stream has just written, and the result must be read after the kernel on s."""
+    s = torch.cuda.Stream(device=gpu)
+    base = torch.arange(1 << 24, dtype=torch.int64, device=gpu)
+    for k in range(4):
+        x = ((base * (2 * k + 1)) >> 3).to(torch.uint8)  # written on the current stream, just before
+        got = tk.crc32().update(x, stream=s).finalize()
+        assert got == oracle.crc(x.cpu().numpy().tobytes()), k
+
+
+def test_batch_on_side_stream(gpu, oracle):
+    """crc32_batch_uniform / crc32_batch on a side stream, with the output allocated by the call:
+    ready once that stream is synchronised."""
+    s = torch.cuda.Stream(device=gpu)
+    n, blen = 3000, 4096
+    data = torch.empty(n * blen, dtype=torch.uint8, device=gpu)
+    tk.fill_synthetic_uniform(data, blen, n, first_block=11)
+    s.wait_stream(torch.cuda.current_stream())
+    out = tk.crc32_batch_uniform(data, blen, n, stream=s)
+    offs = torch.arange(n, dtype=torch.int64, device=gpu) * blen
+    lens = torch.full((n,), blen, dtype=torch.int32, device=gpu)
+    s.wait_stream(torch.cuda.current_stream())
+    out2 = tk.crc32_batch(data, offs, lens, stream=s)
+    s.synchronize()
+    want = oracle.synthetic(1, 11, n, blen)
+    assert np.array_equal(u32(out), want) and np.array_equal(u32(out2), want)
+
+
+def test_batch_argument_checks(gpu):
+    data = torch.zeros(1 << 16, dtype=torch.uint8, device=gpu)
+    offs = torch.zeros(4, dtype=torch.int64, device=gpu)
+    lens = torch.ones(4, dtype=torch.int32, device=gpu)
+    with pytest.raises(ValueError):
+        tk.crc32_batch(data, offs, lens, out=torch.empty(3, dtype=torch.int32, device=gpu))  # short out
+    with pytest.raises(ValueError):
+        tk.crc32_batch(data, offs, lens, init_raw=torch.empty(2, dtype=torch.int32, device=gpu))
+    with pytest.raises(ValueError):
+        tk.crc32_batch(data, offs.cpu(), lens)
+    with pytest.raises(ValueError):
+        tk.crc32_batch_uniform(data, 4096, 16, out=torch.empty(16, dtype=torch.int64, device=gpu))
+
+
 def test_update_chaining_raw_state(gpu, oracle):
     rng = np.random.default_rng(2)
     d = rng.integers(0, 256, 50000, dtype=np.uint8).tobytes()
@@ -495,10 +538,13 @@ def test_full_size_uniform_configs(gpu, cfg):
     got = np.zeros(n, np.uint32)
     chunk = min(n, ((32 if cfg == "cfg5" else 4) << 30) // blen)  # device data per pass
     data = torch.empty(chunk * blen, dtype=torch.uint8, device=gpu)
+    shards = {sh["first_block"]: sh for sh in golden("synthetic.json")["shards"][cfg]} if cfg == "cfg5" else {}
     for first in range(0, n, chunk):
         m = min(chunk, n - first)
         tk.fill_synthetic_uniform(data, blen, m, first_block=first)
         got[first:first + m] = u32(tk.crc32_batch_uniform(data, blen, m))
+        if first in shards:  # cfg5: each 32 GiB pass is one rank's shard
+            assert aggregates(got[first:first + m]) == (shards[first]["xor"], shards[first]["sum32"]), first
     if "first" in c:
         assert [int(x) for x in got[:len(c["first"])]] == c["first"]
         assert int(got[-1]) == c["last"]
@@ -516,3 +562,30 @@ def test_full_size_zipf_config(gpu, oracle):
     got = u32(tk.crc32_batch(d, o, ln))
     assert [int(x) for x in got[:256]] == c["first"]
     assert aggregates(got) == (c["xor"], c["sum32"])
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4"])
+def test_rank_shards_full_size(gpu, oracle, cfg):
+    """The per-rank shards of an 8-GPU bench run (rank r: global blocks [r*n, (r+1)*n), bench.py
+    rank_shard), each checksummed whole on this device and compared with its golden XOR/SUM32
+    (tests/golden/make_golden.py --shards). Rank 0 is the single-GPU config, checked above; cfg5's
+    eight shards are checked in test_full_size_uniform_configs."""
+    g = golden("synthetic.json")
+    for sh in g["shards"][cfg][1:]:
+        first, n = sh["first_block"], sh["nblocks"]
+        if cfg == "cfg4":
+            lens = oracle.zipf_lengths(1, first, n)
+            offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+            d = torch.empty(int(lens.sum()) + 64, dtype=torch.uint8, device=gpu)
+            o = torch.from_numpy(offs).to(gpu)
+            ln = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+            tk.fill_synthetic_blocks(d, o, ln, first_block=first)
+            got = u32(tk.crc32_batch(d, o, ln))
+            assert int(lens.sum()) == sh["total_bytes"]
+        else:
+            blen = g[cfg]["len"]
+            d = torch.empty(n * blen, dtype=torch.uint8, device=gpu)
+            tk.fill_synthetic_uniform(d, blen, n, first_block=first)
+            got = u32(tk.crc32_batch_uniform(d, blen, n))
+        del d
+        assert aggregates(got) == (sh["xor"], sh["sum32"]), f"{cfg} shard at block {first}"

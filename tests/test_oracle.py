@@ -174,3 +174,37 @@ def test_sst_image_layout():
     assert (count, usize, csize, comp, crc) == (2, n, n, 0, 0)
     assert img[21] == n and img[22:22 + 5] == b"\x04key1"
     assert sst.CRC_OFFSET == 1 + 16
+
+
+def test_fast_synthetic_path_matches_sarwate(oracle):
+    """oracle_crc_synthetic_s8 (used to checksum whole shards on CPU) == the Sarwate restatement on
+    the golden first blocks and on lengths that exercise its byte tail."""
+    g = golden("synthetic.json")
+    fn = oracle.lib.oracle_crc_synthetic_s8
+    fn.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_void_p]
+    for cfg in ("cfg2", "cfg3"):
+        out = np.zeros(64, np.uint32)
+        fn(1, 0, 64, g[cfg]["len"], out.ctypes.data)
+        assert [int(x) for x in out] == g[cfg]["first"]
+    for n in (0, 1, 3, 7, 8, 9, 255, 4097):
+        out = np.zeros(8, np.uint32)
+        fn(1, 100, 8, n, out.ctypes.data)
+        assert np.array_equal(out, oracle.synthetic(1, 100, 8, n))
+
+
+def test_shard_fixtures_are_consistent():
+    """Per-rank shard aggregates (make_golden.py --shards): rank 0's shard of cfg2/cfg3/cfg4 is the
+    whole single-GPU config, and the eight cfg5 shards recombine into the survey's 4 M x 64 KiB
+    aggregate (XOR 5a7eaa3b, SUM32 9d26ebfd)."""
+    g = golden("synthetic.json")
+    sh = g["shards"]
+    for cfg in ("cfg2", "cfg3", "cfg4"):
+        assert len(sh[cfg]) == 8
+        assert (sh[cfg][0]["xor"], sh[cfg][0]["sum32"]) == (g[cfg]["xor"], g[cfg]["sum32"])
+        assert [s["first_block"] for s in sh[cfg]] == [r * g[cfg]["nblocks"] for r in range(8)]
+    x = s = 0
+    for r, shard in enumerate(sh["cfg5"]):
+        assert shard["first_block"] == r * (1 << 19) and shard["nblocks"] == 1 << 19
+        x ^= shard["xor"]
+        s = (s + shard["sum32"]) & 0xFFFFFFFF
+    assert (x, s) == (0x5A7EAA3B, 0x9D26EBFD) == (g["cfg5"]["xor"], g["cfg5"]["sum32"])

@@ -72,8 +72,9 @@ class crc32:  # noqa: N801 - reference class name (crc32.hpp:32)
     def update(self, data, stream=None):
         """Continue the register over ``data`` (crc32.cpp:9-16) and return self (chainable).
 
-        ``data``: bytes-like / numpy (host memory) or a torch uint8 tensor (device memory; the
-        device path is asynchronous on ``stream`` but this call waits for the 4-byte result).
+        ``data``: bytes-like / numpy (host memory) or a torch uint8 tensor (device memory). The device
+        kernel runs on ``stream`` (default: the current stream) after the current stream's prior
+        work, and this call waits for its 4-byte result.
         """
         try:
             import torch
@@ -81,10 +82,15 @@ class crc32:  # noqa: N801 - reference class name (crc32.hpp:32)
         except ImportError:  # pragma: no cover - torch is part of the image
             is_dev = False
         if is_dev:
-            t = data.contiguous().view(torch.uint8)
+            cur = torch.cuda.current_stream(data.device)
+            t = data.contiguous().view(torch.uint8)  # any copy runs on the current stream
             out = torch.empty(1, dtype=torch.int32, device=t.device)
+            s = stream if stream is not None else cur
+            if s != cur:
+                s.wait_stream(cur)  # the kernel on `s` must see the bytes the current stream wrote
             check(_fn(self._algo, "update_device")(self._crc, ctypes.c_void_p(t.data_ptr()), t.numel(),
-                                                   ctypes.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+                                                   ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(s.cuda_stream)))
+            s.synchronize()  # the 4-byte result is read below, after the kernel on `s` has written it
             self._crc = int(out.cpu().numpy().view(np.uint32)[0])
         else:
             ptr, n, keep = _host_view(data)
@@ -122,22 +128,53 @@ def _u32_view(t):
     return t.view(torch.int32) if t.dtype != torch.int32 else t
 
 
+def _check_data(data):
+    import torch
+    if not isinstance(data, torch.Tensor) or not data.is_cuda or not data.is_contiguous():
+        raise ValueError("data must be a contiguous CUDA tensor")
+    if data.device.index != torch.cuda.current_device():
+        raise ValueError(f"data is on {data.device}, but the current device is cuda:{torch.cuda.current_device()}")
+
+
+def _check_vec(name, t, dtype, n, device):
+    """A per-block vector: contiguous, of `dtype`, on the data's device, with at least n entries."""
+    if not t.is_cuda or t.device != device or t.dtype != dtype or not t.is_contiguous() or t.numel() < n:
+        raise ValueError(f"{name} must be a contiguous {dtype} tensor on {device} with >= {n} entries")
+
+
+def _out_vec(out, n, device, stream):
+    """The result vector: allocated here (and tied to `stream` for the caching allocator) or checked."""
+    import torch
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=device)
+        if stream is not None and stream != torch.cuda.current_stream(device):
+            out.record_stream(stream)
+        return out
+    _check_vec("out", out, torch.int32, n, device)
+    return out
+
+
 def crc32_batch(data, offsets, lengths, init_raw=None, out=None, stream=None, algo="crc32"):
     """Irregular batch on the GPU: block i = data[offsets[i] : offsets[i] + lengths[i]].
 
     data: uint8 CUDA tensor; offsets: int64 CUDA tensor; lengths: int32 CUDA tensor (< 2^32 bytes
     each); init_raw: optional int32 CUDA tensor of raw registers (crc32::crc_). Returns an int32
     tensor of finalize() bit patterns (``.cpu().numpy().view(np.uint32)`` for unsigned values).
+    Shapes, dtypes and devices are checked here; the block ranges themselves are trusted, as at the
+    C ABI (include/tkv_crc32.h): every [offsets[i], offsets[i] + lengths[i]) must lie inside `data`.
+    The kernels run on ``stream`` (default: the current stream) and the result is ready when that
+    stream reaches this point, like any torch op issued on it.
     """
     import torch
     n = offsets.numel()
     if lengths.numel() != n:
         raise ValueError("offsets and lengths differ in length")
+    _check_data(data)
     for name, t, dt in (("offsets", offsets, torch.int64), ("lengths", lengths, torch.int32)):
-        if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
-            raise ValueError(f"{name} must be a contiguous CUDA {dt} tensor")
-    if out is None:
-        out = torch.empty(n, dtype=torch.int32, device=data.device)
+        _check_vec(name, t, dt, n, data.device)
+    out = _out_vec(out, n, data.device, stream)
+    if init_raw is not None:
+        _check_vec("init_raw", init_raw, torch.int32, n, data.device)
     initp = ctypes.c_void_p(init_raw.data_ptr()) if init_raw is not None else None
     check(_fn(algo, "batch_device")(
         ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
@@ -151,10 +188,12 @@ def crc32_batch_uniform(data, length, n, stride=None, init_raw=None, out=None, s
     """Uniform batch on the GPU: block i = data[offset + i*stride : + length] (stride = length)."""
     import torch
     stride = length if stride is None else stride
+    _check_data(data)
     if n and offset + (n - 1) * stride + length > data.numel():
         raise ValueError("batch exceeds the data tensor")
-    if out is None:
-        out = torch.empty(n, dtype=torch.int32, device=data.device)
+    out = _out_vec(out, n, data.device, stream)
+    if init_raw is not None:
+        _check_vec("init_raw", init_raw, torch.int32, n, data.device)
     initp = ctypes.c_void_p(init_raw.data_ptr()) if init_raw is not None else None
     check(_fn(algo, "batch_uniform_device")(
         ctypes.c_void_p(data.data_ptr() + offset), stride, length, initp,
