@@ -123,7 +123,7 @@ def pmc_traffic(csv_path, config):
     source: the committed profile of this config."""
     import csv
     from collections import defaultdict
-    step_kernels = (("crc_small", "crc_rows", "rows_tile_scan", "rows_scan_tiles", "rows_finish", "crc_fixup")
+    step_kernels = (("crc_rows", "rows_tile_scan", "rows_scan_tiles", "rows_finish", "crc_fixup")
                     if config == "cfg4" else ("crc_packed",))
     path = csv_path or os.path.join(ROOT, "profiles", "r1", f"pmc_{config}", "p3_counters.csv")
     if not os.path.exists(path):

@@ -49,7 +49,6 @@ def load_tables(lib, poly=0xEDB88320):
     horner = buf[o:o + 64]; o += 64
     row_pow = buf[o:o + 64]; o += 64
     head = buf[o:o + (ROW + 1) * 32].reshape(ROW + 1, 32); o += (ROW + 1) * 32
-    shift32 = buf[o:o + 128].reshape(8, 16); o += 128
     rows_shift = buf[o:o + 4096]; o += 4096
     # rows_shift[k] = x^(8*4096*k): rows_shift[0] = x^0, [1] = row_pow[0], [2^k] = row_pow[k]
     assert int(rows_shift[0]) == 0x80000000
@@ -58,7 +57,7 @@ def load_tables(lib, poly=0xEDB88320):
     built_for = int(buf[o]); o += 4  # poly + 3 pad words
     assert o * 4 == n
     assert built_for == poly
-    return slice_, lane, horner, row_pow, head, shift32
+    return slice_, lane, horner, row_pow, head
 
 
 @pytest.fixture(scope="module")
@@ -90,7 +89,7 @@ def test_gf2_helpers(lib, oracle):
 
 def test_crc32c_tables(lib, oracle):
     """The Castagnoli tables obey the same identities under the CRC-32C oracle."""
-    s, lane, horner, row_pow, head, shift32 = load_tables(lib, 0x82F63B78)
+    s, lane, horner, row_pow, head = load_tables(lib, 0x82F63B78)
     t = np.zeros(256, np.uint32)
     oracle.lib.oracle_table_c(t.ctypes.data)
     assert np.array_equal(s[0], t)
@@ -101,14 +100,13 @@ def test_crc32c_tables(lib, oracle):
         assert int(lane[5][11][l]) == zc(11 << 20, (63 - l) * SEG)
     assert int(horner[9]) == zc(1 << 9, ROW)
     assert int(head[1234][30]) == zc(1 << 30, 1234)
-    assert int(shift32[2][3]) == zc(3 << 8, 32)
     assert int(row_pow[1]) == zc(0x80000000, 2 * ROW)
     # the tables differ from the reference's: the polynomial really is a parameter
     assert not np.array_equal(s[0], load_tables(lib)[0][0])
 
 
 def test_lane_shift_horner_head_tables(tables, oracle):
-    _, lane, horner, row_pow, head, shift32 = tables
+    _, lane, horner, row_pow, head = tables
     for l in (0, 1, 31, 62, 63):
         for j in (0, 3, 7):
             for v in (1, 9, 15):
@@ -119,9 +117,6 @@ def test_lane_shift_horner_head_tables(tables, oracle):
     for h in (0, 1, 3, 4, 100, 4095, 4096):
         for i in (0, 17, 31):
             assert int(head[h][i]) == shift_zeros(oracle, 1 << i, h)
-    for j in (0, 4, 7):
-        for v in (1, 6, 15):
-            assert int(shift32[j][v]) == shift_zeros(oracle, v << (4 * j), 32)
 
 
 # ---- numpy model of the kernel ------------------------------------------------------------------
@@ -145,7 +140,7 @@ def bits_dot(sel, consts):
 
 class Model:
     def __init__(self, tables):
-        self.s, self.lane, self.horner, self.row_pow, self.head, _ = tables
+        self.s, self.lane, self.horner, self.row_pow, self.head = tables
 
     def slice_lanes(self, row):
         """16 slicing-by-4 steps per lane over a (64, 64)-byte row image; returns (64,) partials."""

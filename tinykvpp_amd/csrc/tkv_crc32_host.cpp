@@ -29,7 +29,6 @@ hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st);
 hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
                           std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
                           std::uint32_t W, std::uint32_t* out, hipStream_t st);
-hipError_t launch_small(const RowsArgs& a, unsigned grid, hipStream_t st);
 std::uint32_t prepass_tiles(std::uint32_t n);
 hipError_t launch_fill_uniform(std::uint8_t* dst, std::uint64_t stride, std::uint64_t len, std::uint64_t first,
                                std::uint64_t nblocks, std::uint64_t seed, hipStream_t st);
@@ -94,9 +93,6 @@ void build_tables(DeviceTables* t, std::uint32_t poly) {
     t->rows_shift[k] = rk;
     rk = mm(rk, mrow);
   }
-  const std::uint32_t z32 = x8n(32);
-  for (int j = 0; j < 8; ++j)
-    for (std::uint32_t v = 0; v < 16; ++v) t->shift32[j][v] = mm(z32, v << (4 * j));
   std::uint32_t z = 0x80000000u;  // x^(8h), h = 0..kRow
   for (int h = 0; h <= kRow; ++h) {
     for (int i = 0; i < 32; ++i) t->head_shift[h][i] = mm(z, 1u << i);

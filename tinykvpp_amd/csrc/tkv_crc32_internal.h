@@ -49,7 +49,6 @@ struct DeviceTables {
   std::uint32_t horner[64];             // lanes 0..31: Shift_{kRow}(1 << l); lanes 32..63: 0
   std::uint32_t row_pow[64];            // x^(8*kRow*2^k) mod P (reflected), k = 0..63
   std::uint32_t head_shift[kRow + 1][32];  // [h][i] = Shift_h(1 << i): init injection at a head row
-  std::uint32_t shift32[8][16];         // [j][v] = Shift_32(v << 4j): joins two 32-byte half chains
   std::uint32_t rows_shift[4096];       // [k] = x^(8*kRow*k) mod P: moves a piece's partial past k rows
   std::uint32_t poly;                   // reflected polynomial the tables were built for
   std::uint32_t pad_[3];
@@ -86,18 +85,15 @@ struct RowsArgs {
   std::uint32_t total_rows;          // uniform only (irregular reads row_scan[nblocks])
   std::uint32_t nwaves;
   std::uint32_t snap_blocks;         // uniform: partition by whole blocks (no seams)
-  std::uint32_t* wg_ctr;             // packed: one work counter per workgroup, kCtrStride words apart
   // irregular batches after the prepass split: `offsets`/`lengths` then list the
   // large blocks only (compacted), out_idx maps a compacted block to its batch index, and the small
-  // blocks (len <= kSmallMax) are listed in s_off/s_len/s_idx for crc_small.
+  // blocks (len <= kSmallMax) are listed in s_off/s_len/s_idx for the small-block phase.
   const std::uint32_t* out_idx;      // nullable: result of compacted block k goes to out[out_idx[k]]
   const std::uint32_t* counts;       // device: [0] large blocks, [1] small blocks, [2] rows of large blocks
   const std::uint64_t* s_off;
   const std::uint32_t* s_len;
   const std::uint32_t* s_idx;
-  unsigned long long* prog;          // explorer only: per-wave progress stamps (crc_packed_body PROG)
 };
-constexpr std::uint32_t kProgSlots = 64;
 
 // Outputs of the irregular prepass (scratch of one stream).
 struct PrepassOut {
@@ -111,12 +107,9 @@ struct PrepassOut {
   std::uint32_t* wave_start;
 };
 
-// Blocks of at most kSmallMax bytes are folded four to a wave (16 lanes x 64 B each) by crc_small
-// instead of occupying a whole 4 KiB row each.
+// Blocks of at most kSmallMax bytes are folded four to a wave (16 lanes x 64 B each) by the
+// small-block phase instead of occupying a whole 4 KiB row each.
 constexpr std::uint32_t kSmallMax = 1024;
-
-// Packed kernel work counters: one per workgroup, each on its own 128-byte line.
-constexpr std::uint32_t kCtrStride = 32;
 
 // rows(b): wave-rows a block of n bytes occupies (every block, even n = 0, owns >= 1 row), and
 // h(b): bytes of its head row (row 0), in [0, kRow].

@@ -42,7 +42,7 @@ template <bool ALIGNED, bool UNIFORM>
 __global__ __launch_bounds__(kRowsThreads) void crc_rows(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   // issue priority from the rows left (set_prio_from_left): +0.7 % on cfg4 (profiles/r1/launch_irr_pri3.txt)
-  dev::crc_rows_body<ALIGNED, UNIFORM, Shape<ALIGNED>::kDepth, Shape<ALIGNED>::kIlp, 0, 0, 3>(a, lds);
+  dev::crc_rows_body<ALIGNED, UNIFORM, Shape<ALIGNED>::kDepth, Shape<ALIGNED>::kIlp, 3>(a, lds);
 }
 
 // Packed uniform batches (len % 4 KiB == 0, stride == len, 16-byte aligned): DESIGN.md §4.
@@ -59,23 +59,17 @@ template <bool R1>
 __global__ __launch_bounds__(kThreads) void crc_packed(RowsArgs a) {
   static_assert(kThreads == 1024, "the skewed partition assumes 16 waves per workgroup");
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<kPackedDepth, kPackedIlp, R1, false, 0, 0, 0, false, R1 ? 0 : kPackedSkew, kPackedPrio>(a, lds);
+  dev::crc_packed_body<kPackedDepth, kPackedIlp, R1, R1 ? 0 : kPackedSkew, kPackedPrio>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
-
-__global__ __launch_bounds__(kRowsThreads) void crc_small(RowsArgs a) {
-  __shared__ std::uint32_t lds[kLdsWords];
-  if (dev::sload32(a.counts, 1) == 0) return;  // no small blocks: skip the table fill
-  dev::crc_small_body(a, lds);
-}
 
 }  // namespace
 
 // ---- irregular-batch prepass -----------------------------------------------------------------------
 // One exclusive scan over the blocks of the pair (small blocks, rows of large blocks), packed in a
 // u64 (small count in the low word, rows in the high word), then a scatter that
-//   * lists small blocks (len <= kSmallMax) in s_off/s_len/s_idx for crc_small,
+//   * lists small blocks (len <= kSmallMax) in s_off/s_len/s_idx for the small-block phase,
 //   * compacts large blocks into big_off/big_len/big_idx with their row offsets (row_scan) for the
 //     row kernel, and records the first large block of every row-kernel wave (wave_start),
 //   * leaves counts = {large blocks, small blocks, rows of large blocks}.
@@ -340,11 +334,6 @@ hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* len
     hipLaunchKernelGGL(rows_finish, dim3((n + 255) / 256), dim3(256), 0, st, offsets, lengths, n, scan, tile_sums,
                        counts, o, W, out);
   }
-  return hipGetLastError();
-}
-
-hipError_t launch_small(const RowsArgs& a, unsigned grid, hipStream_t st) {
-  hipLaunchKernelGGL(crc_small, dim3(grid), dim3(kRowsThreads), 0, st, a);
   return hipGetLastError();
 }
 

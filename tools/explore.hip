@@ -6,7 +6,7 @@
 
 #include <cstdio>
 
-#include "tkv_crc32_device.h"
+#include "explore_device.h"
 
 using namespace tkv;
 
@@ -34,7 +34,7 @@ namespace tkv::dev {
 // load per lane 0-7) and grabs from the pool with the most chunks left, until none has any.
 template <int DEPTH, int ILP, bool R1, int CROWS, std::uint32_t PERM = 0, int SF = 0, int SD = 16, int SP = 0,
           bool LEAN = false>
-__device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint32_t* lds) {
+__device__ __forceinline__ void crc_packed_xq_body(const XArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
   static_assert(CROWS % DEPTH == 0 && CROWS >= 2 * DEPTH && CROWS <= 64, "chunk shape");
   static_assert(SF >= 0 && SF < SD, "static share in 1/SD-ths");
@@ -156,7 +156,7 @@ __device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint3
   if constexpr (SF != 0) {  // static region: the packed loop itself (no per-row chunk bookkeeping)
     const std::uint32_t s0 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave) * S / W);
     const std::uint32_t s1 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave + 1) * S / W);
-    if (s1 > s0) dev::crc_packed_body<DEPTH, ILP, R1, false, 0, 0, 0, true, 0, SP>(a, lds, s0, s1 - s0);
+    if (s1 > s0) dev::x_packed_body<DEPTH, ILP, R1, false, 0, 0, 0, true, 0, SP>(a, lds, s0, s1 - s0);
   }
   if (!SF && xi < psize(xp)) cur = pchunk(xp, xi);
   else live = steal(cur);
@@ -281,9 +281,9 @@ __device__ __forceinline__ void crc_packed_xq_body(const RowsArgs& a, std::uint3
 }  // namespace tkv::dev
 
 template <int D, int I, int M>
-__global__ __launch_bounds__(kThreads) void k_rows(RowsArgs a) {
+__global__ __launch_bounds__(kThreads) void k_rows(XArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_rows_body<true, true, D, I, M>(a, lds);
+  dev::x_rows_body<true, true, D, I, M>(a, lds);
 }
 
 // Ideal streaming read: every lane reads consecutive 16-byte words, XOR-reduces, one store per wave.
@@ -487,11 +487,11 @@ __global__ __launch_bounds__(1024) void k_interf2(const std::uint8_t* base, std:
 }
 
 // Diagnostic: per-wave start/end s_memrealtime (100 MHz) of the production packed body.
-__global__ __launch_bounds__(1024) void k_packed_stamped(RowsArgs a, unsigned long long* stamps) {
+__global__ __launch_bounds__(1024) void k_packed_stamped(XArgs a, unsigned long long* stamps) {
   __shared__ std::uint32_t lds[kLdsWords];
   const std::uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  dev::crc_packed_body<4, 2, true>(a, lds);
+  dev::x_packed_body<4, 2, true>(a, lds);
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
   if ((threadIdx.x & 63u) == 0) {
     stamps[2 * wave] = t0;
@@ -500,11 +500,11 @@ __global__ __launch_bounds__(1024) void k_packed_stamped(RowsArgs a, unsigned lo
 }
 
 template <int SK, int PR = 0>
-__global__ __launch_bounds__(1024) void k_skew_stamped(RowsArgs a, unsigned long long* stamps) {
+__global__ __launch_bounds__(1024) void k_skew_stamped(XArgs a, unsigned long long* stamps) {
   __shared__ std::uint32_t lds[kLdsWords];
   const std::uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  dev::crc_packed_body<4, 2, true, false, 0, 0, 0, false, SK, PR>(a, lds);
+  dev::x_packed_body<4, 2, true, false, 0, 0, 0, false, SK, PR>(a, lds);
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
   if ((threadIdx.x & 63u) == 0) {
     stamps[2 * wave] = t0;
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(1024) void k_skew_stamped(RowsArgs a, unsigned long
   }
 }
 
-__global__ __launch_bounds__(1024) void k_dyn_stamped(RowsArgs a, unsigned long long* stamps) {
+__global__ __launch_bounds__(1024) void k_dyn_stamped(XArgs a, unsigned long long* stamps) {
   __shared__ std::uint32_t lds[kLdsWords];
   const std::uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -532,29 +532,29 @@ int g_ncu = 0;
 
 struct V {
   const char* name;
-  void (*launch)(RowsArgs, hipStream_t);
+  void (*launch)(XArgs, hipStream_t);
 };
 
 template <int D, int I, int M>
-void L(RowsArgs a, hipStream_t s) {
+void L(XArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_rows<D, I, M>), dim3(g_ncu), dim3(kThreads), 0, s, a);
 }
 
 template <int PAT, int D, int F, int MIS = 0, int STR = 0>
-void P(RowsArgs a, hipStream_t s) {
+void P(XArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_pat<PAT, D, F, MIS, STR>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows - 1, a.nwaves,
                      a.out);
 }
 
 template <int D, int I, bool R1, int T, bool SP, std::uint32_t ROT = 0, int CHK = 0>
-__global__ __launch_bounds__(T) void k_packed(RowsArgs a) {
+__global__ __launch_bounds__(T) void k_packed(XArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<D, I, R1, SP, ROT, CHK>(a, lds);
+  dev::x_packed_body<D, I, R1, SP, ROT, CHK>(a, lds);
 }
 
 // chunk-strided block map (4 KiB blocks only; other lengths fall back to the product map)
 template <int CHK>
-void PC(RowsArgs a, hipStream_t s) {
+void PC(XArgs a, hipStream_t s) {
   a.nwaves = g_ncu * 16;
   if (a.len == kRow && a.nblocks % (a.nwaves * 64u) == 0)
     hipLaunchKernelGGL((k_packed<4, 2, true, 1024, false, 0, CHK>), dim3(g_ncu), dim3(1024), 0, s, a);
@@ -562,29 +562,30 @@ void PC(RowsArgs a, hipStream_t s) {
 }
 
 template <std::uint32_t ROT>
-void PR(RowsArgs a, hipStream_t s) {
+void PR(XArgs a, hipStream_t s) {
   a.nwaves = g_ncu * 16;
   if (a.len == kRow) hipLaunchKernelGGL((k_packed<4, 2, true, 1024, false, ROT>), dim3(g_ncu), dim3(1024), 0, s, a);
   else hipLaunchKernelGGL((k_packed<4, 2, false, 1024, false, ROT>), dim3(g_ncu), dim3(1024), 0, s, a);
 }
 
 template <int D, int I, bool R1, int T, int CR>
-__global__ __launch_bounds__(T) void k_packed_dyn(RowsArgs a) {
+__global__ __launch_bounds__(T) void k_packed_dyn(XArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   dev::crc_packed_dyn_body<D, I, R1, CR>(a, lds);
 }
 
 std::uint32_t* g_ctr = nullptr;
+std::uint32_t* g_shift32 = nullptr;  // explorer SPLIT variants
 
 template <int D, int I, int CR, int T = 1024>
-void PD(RowsArgs a, hipStream_t s) {
+void PD(XArgs a, hipStream_t s) {
   a.wg_ctr = g_ctr;
   if (a.len == kRow) hipLaunchKernelGGL((k_packed_dyn<D, I, true, T, CR>), dim3(g_ncu), dim3(T), 0, s, a);
   else hipLaunchKernelGGL((k_packed_dyn<D, I, false, T, CR>), dim3(g_ncu), dim3(T), 0, s, a);
 }
 
 template <int D, int I, bool R1, int T, int CR, std::uint32_t PM, int SF, int SD, int SP, bool LN = false>
-__global__ __launch_bounds__(T) void k_packed_xq(RowsArgs a) {
+__global__ __launch_bounds__(T) void k_packed_xq(XArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   dev::crc_packed_xq_body<D, I, R1, CR, PM, SF, SD, SP, LN>(a, lds);
 }
@@ -597,7 +598,7 @@ std::uint32_t* g_lean = nullptr;  // two head sets of the LEAN variants (zeroed 
 // the product loop itself (crc_packed_body on the chunk's block range: a full pipeline per chunk, no
 // per-row bookkeeping). A wave whose head is dry grabs from the fullest head.
 template <int C, int SF, int SD, bool R1>
-__global__ __launch_bounds__(1024) void k_packed_chunks(RowsArgs a) {
+__global__ __launch_bounds__(1024) void k_packed_chunks(XArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   dev::fill_lds(a.tabs, lds);
   __syncthreads();
@@ -611,7 +612,7 @@ __global__ __launch_bounds__(1024) void k_packed_chunks(RowsArgs a) {
   const std::uint32_t S = static_cast<std::uint32_t>(static_cast<std::uint64_t>(a.nblocks) * SF / SD);
   const std::uint32_t s0 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave) * S / W);
   const std::uint32_t s1 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(wave + 1) * S / W);
-  if (s1 > s0) dev::crc_packed_body<4, 2, R1, false, 0, 0, 0, true, 0, 3>(a, lds, s0, s1 - s0);
+  if (s1 > s0) dev::x_packed_body<4, 2, R1, false, 0, 0, 0, true, 0, 3>(a, lds, s0, s1 - s0);
   const std::uint32_t NC = (a.nblocks - S + C - 1) / C;
   auto plo = [&](std::uint32_t y) { return static_cast<std::uint32_t>(static_cast<std::uint64_t>(y) * NC / 8u); };
   auto psize = [&](std::uint32_t y) { return plo(y + 1) - plo(y); };
@@ -625,7 +626,7 @@ __global__ __launch_bounds__(1024) void k_packed_chunks(RowsArgs a) {
     const std::uint32_t q = __builtin_amdgcn_readfirstlane(v);
     if (q < psize(gp)) {
       const std::uint32_t fb = S + (plo(gp) + q) * C;
-      dev::crc_packed_body<4, 2, R1, false, 0, 0, 0, true, 0, 0>(a, lds, fb, a.nblocks - fb < C ? a.nblocks - fb : C);
+      dev::x_packed_body<4, 2, R1, false, 0, 0, 0, true, 0, 0>(a, lds, fb, a.nblocks - fb < C ? a.nblocks - fb : C);
       continue;
     }
     std::int32_t left = -1;
@@ -649,7 +650,7 @@ __global__ __launch_bounds__(1024) void k_packed_chunks(RowsArgs a) {
 }
 
 template <int C, int SF, int SD>
-void PC2(RowsArgs a, hipStream_t s) {
+void PC2(XArgs a, hipStream_t s) {
   static int par = 0;
   par ^= 1;
   a.nwaves = g_ncu * 16;
@@ -660,7 +661,7 @@ void PC2(RowsArgs a, hipStream_t s) {
 }
 
 template <int D, int I, int CR, int SF, int SD>
-void PL(RowsArgs a, hipStream_t s) {
+void PL(XArgs a, hipStream_t s) {
   static int par = 0;
   par ^= 1;
   a.wg_ctr = g_lean + par * 8 * kCtrStride;
@@ -672,7 +673,7 @@ void PL(RowsArgs a, hipStream_t s) {
 }
 
 template <int D, int I, int CR, std::uint32_t PM = 0, int SF = 0, int T = 1024, int SD = 16, int SP = 0>
-void PX(RowsArgs a, hipStream_t s) {
+void PX(XArgs a, hipStream_t s) {
   a.wg_ctr = g_xq;
   if (a.len == kRow) hipLaunchKernelGGL((k_packed_xq<D, I, true, T, CR, PM, SF, SD, SP>), dim3(g_ncu), dim3(T), 0, s, a);
   else hipLaunchKernelGGL((k_packed_xq<D, I, false, T, CR, PM, SF, SD, SP>), dim3(g_ncu), dim3(T), 0, s, a);
@@ -682,37 +683,37 @@ void PX(RowsArgs a, hipStream_t s) {
 // a pseudo-random 0..K-1 units of s_sleep 127 (~4 us each), so that waves do not all walk their
 // ranges in lockstep from the same moment.
 template <int K, bool PERWAVE>
-__global__ __launch_bounds__(1024) void k_packed_stag(RowsArgs a) {
+__global__ __launch_bounds__(1024) void k_packed_stag(XArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   const std::uint32_t id = PERWAVE ? blockIdx.x * 16u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : blockIdx.x;
   const std::uint32_t n = ((id * 2654435761u) >> 16) % K;
   for (std::uint32_t i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-  if (a.len == kRow) dev::crc_packed_body<4, 2, true>(a, lds);
-  else dev::crc_packed_body<4, 2, false>(a, lds);
+  if (a.len == kRow) dev::x_packed_body<4, 2, true>(a, lds);
+  else dev::x_packed_body<4, 2, false>(a, lds);
 }
 
 template <int K, bool PW>
-void PS(RowsArgs a, hipStream_t s) {
+void PS(XArgs a, hipStream_t s) {
   a.nwaves = g_ncu * 16;
   hipLaunchKernelGGL((k_packed_stag<K, PW>), dim3(g_ncu), dim3(1024), 0, s, a);
 }
 
 template <int SK, int PR, bool EA = false>
-__global__ __launch_bounds__(1024) void k_packed_skew(RowsArgs a) {
+__global__ __launch_bounds__(1024) void k_packed_skew(XArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  if (a.len == kRow) dev::crc_packed_body<4, 2, true, false, 0, 0, 0, false, SK, PR, EA>(a, lds);
-  else dev::crc_packed_body<4, 2, false, false, 0, 0, 0, false, SK, PR, EA>(a, lds);
+  if (a.len == kRow) dev::x_packed_body<4, 2, true, false, 0, 0, 0, false, SK, PR, EA>(a, lds);
+  else dev::x_packed_body<4, 2, false, false, 0, 0, 0, false, SK, PR, EA>(a, lds);
 }
 
 template <int SK, int PR = 0, bool EA = false>
-void PW(RowsArgs a, hipStream_t s) {
+void PW(XArgs a, hipStream_t s) {
   a.nwaves = g_ncu * 16;
   hipLaunchKernelGGL((k_packed_skew<SK, PR, EA>), dim3(g_ncu), dim3(1024), 0, s, a);
 }
 
 // grid of M workgroups per CU (M rounds): a CU whose workgroup finishes early takes the next one
 template <int M>
-void PG(RowsArgs a, hipStream_t s) {
+void PG(XArgs a, hipStream_t s) {
   a.nwaves = g_ncu * M * 16;
   if (a.len == kRow && a.nblocks >= a.nwaves)
     hipLaunchKernelGGL((k_packed<4, 2, true, 1024, false>), dim3(g_ncu * M), dim3(1024), 0, s, a);
@@ -721,32 +722,32 @@ void PG(RowsArgs a, hipStream_t s) {
 
 // Packed shapes with the product's work-left priority (no skew: it assumes 1024 threads).
 template <int D, int I, bool R1, int T>
-__global__ __launch_bounds__(T) void k_packed_pr(RowsArgs a) {
+__global__ __launch_bounds__(T) void k_packed_pr(XArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<D, I, R1, false, 0, 0, 0, false, 0, 3>(a, lds);
+  dev::x_packed_body<D, I, R1, false, 0, 0, 0, false, 0, 3>(a, lds);
 }
 
 template <int D, int I, int T>
-void PP(RowsArgs a, hipStream_t s) {
+void PP(XArgs a, hipStream_t s) {
   a.nwaves = g_ncu * (T / 64);
   if (a.len == kRow) hipLaunchKernelGGL((k_packed_pr<D, I, true, T>), dim3(g_ncu), dim3(T), 0, s, a);
   else hipLaunchKernelGGL((k_packed_pr<D, I, false, T>), dim3(g_ncu), dim3(T), 0, s, a);
 }
 
 template <int D, int I, int T = 1024, bool SP = false>
-void PK(RowsArgs a, hipStream_t s) {
+void PK(XArgs a, hipStream_t s) {
   a.nwaves = g_ncu * (T / 64);
   if (a.len == kRow) hipLaunchKernelGGL((k_packed<D, I, true, T, SP>), dim3(g_ncu), dim3(T), 0, s, a);
   else hipLaunchKernelGGL((k_packed<D, I, false, T, SP>), dim3(g_ncu), dim3(T), 0, s, a);
 }
 
 template <int NL, int NV>
-void IF(RowsArgs a, hipStream_t s) {
+void IF(XArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_interf<NL, NV>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows, a.nwaves, a.out);
 }
 
 template <int NL, int WB, int CH>
-void IF2(RowsArgs a, hipStream_t s) {
+void IF2(XArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_interf2<NL, WB, CH>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows, a.nwaves, a.out);
 }
 
@@ -808,19 +809,19 @@ const V kVariants[] = {
 constexpr int kNV = sizeof(kVariants) / sizeof(kVariants[0]);
 
 template <int D, int I, int T, int SM = 0, int PR = 0>
-__global__ __launch_bounds__(T) void k_irr(RowsArgs a) {
+__global__ __launch_bounds__(T) void k_irr(XArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_rows_body<false, false, D, I, 0, SM, PR>(a, lds);
+  dev::x_rows_body<false, false, D, I, 0, SM, PR>(a, lds);
 }
 
 struct IV {
   const char* name;
   int threads;
-  void (*launch)(RowsArgs, hipStream_t);
+  void (*launch)(XArgs, hipStream_t);
 };
 
 template <int D, int I, int T, int SM = 0, int PR = 0>
-void LI(RowsArgs a, hipStream_t s) {
+void LI(XArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_irr<D, I, T, SM, PR>), dim3(g_ncu), dim3(T), 0, s, a);
 }
 
@@ -847,7 +848,6 @@ hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
 hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
                           std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
                           std::uint32_t W, std::uint32_t* out, hipStream_t st);
-hipError_t launch_small(const RowsArgs& a, unsigned grid, hipStream_t st);
 }  // namespace tkv
 
 extern "C" int explore_count() { return kNV + 1; }
@@ -873,6 +873,11 @@ extern "C" int explore_run(int v, const std::uint8_t* base, std::uint64_t n, std
     hipMemset(g_xq, 0, 4 * kCtrStride * 9);
     hipMalloc(&g_lean, 4 * kCtrStride * 16);
     hipMemset(g_lean, 0, 4 * kCtrStride * 16);
+    std::uint32_t s32[128];  // [j][v] = Shift_32(v << 4j)
+    for (int j = 0; j < 8; ++j)
+      for (std::uint32_t v = 0; v < 16; ++v) s32[16 * j + v] = multmodp(x8nmodp(32), v << (4 * j));
+    hipMalloc(&g_shift32, sizeof(s32));
+    hipMemcpy(g_shift32, s32, sizeof(s32), hipMemcpyHostToDevice);
   }
   if (v == kNV) {
     hipLaunchKernelGGL(k_stream<256>, dim3(g_ncu * 8), dim3(256), 0, st, reinterpret_cast<const uint4*>(base),
@@ -884,7 +889,7 @@ extern "C" int explore_run(int v, const std::uint8_t* base, std::uint64_t n, std
                        n * len / 16, out);
     return hipGetLastError() == hipSuccess ? 0 : 2;
   }
-  RowsArgs a{};
+  XArgs a{};
   a.base = base;
   a.stride = len;
   a.len = len;
@@ -899,6 +904,7 @@ extern "C" int explore_run(int v, const std::uint8_t* base, std::uint64_t n, std
   a.total_rows = static_cast<std::uint32_t>(n * rows_for_len(len));
   a.nwaves = g_ncu * kWavesPerWG;
   a.snap_blocks = 1;
+  a.shift32 = g_shift32;
   kVariants[v].launch(a, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
@@ -934,7 +940,7 @@ extern "C" int explore_run_irr(int v, const std::uint8_t* base, const std::uint6
     g_po.wave_start = g_wstart;
     g_cap = n;
   }
-  RowsArgs a{};
+  XArgs a{};
   a.base = base;
   a.offsets = g_po.big_off;
   a.lengths = g_po.big_len;
@@ -962,7 +968,7 @@ extern "C" int explore_stamped(const std::uint8_t* base, std::uint64_t n, std::u
                                unsigned long long* stamps, void* stream, int dyn) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!g_tabs && explore_run(kNV, base, n, 4096, out, stream)) return 1;
-  RowsArgs a{};
+  XArgs a{};
   a.base = base;
   a.stride = 4096;
   a.len = 4096;
@@ -985,16 +991,16 @@ extern "C" int explore_stamped(const std::uint8_t* base, std::uint64_t n, std::u
 
 // Progress stamps of the production packed body (tools/progress_probe.py).
 template <bool R1, int PROG>
-__global__ __launch_bounds__(1024) void k_packed_prog(RowsArgs a) {
+__global__ __launch_bounds__(1024) void k_packed_prog(XArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_body<4, 2, R1, false, 0, 0, PROG>(a, lds);
+  dev::x_packed_body<4, 2, R1, false, 0, 0, PROG>(a, lds);
 }
 
 extern "C" int explore_prog(const std::uint8_t* base, std::uint64_t n, std::uint32_t len, std::uint32_t* out,
                             unsigned long long* stamps, void* stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!g_tabs && explore_run(kNV, base, 0, 16, out, stream)) return 1;
-  RowsArgs a{};
+  XArgs a{};
   a.base = base;
   a.stride = len;
   a.len = len;
