@@ -39,6 +39,17 @@ def test_no_gpu_is_an_error_not_a_fallback(lib):
     assert e.value.code == 2  # io_error: no device, and no CPU path to fall back to
 
 
+def test_oversize_irregular_batch_is_rejected(lib):
+    """Irregular batches carry u32 block indices; a count the prepass cannot index (within one scan
+    tile of 2^32) is an invalid argument, checked before any device work (no GPU needed)."""
+    import ctypes
+    f = lib.tkv_crc32_batch_device
+    f.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_uint64, ctypes.c_void_p]
+    dummy = ctypes.c_void_p(16)  # never dereferenced: the size check comes first
+    for n in (0xFFFFFFFF, 0xFFFFFFFF - 8191, 1 << 40):
+        assert f(dummy, dummy, dummy, None, dummy, n, None) == 3  # TKV_INVALID_ARGUMENT
+
+
 def load_tables(lib, poly=0xEDB88320):
     n = lib.tkv_debug_tables_poly(poly, None, 0)
     buf = np.zeros(n // 4, np.uint32)

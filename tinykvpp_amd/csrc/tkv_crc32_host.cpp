@@ -29,7 +29,7 @@ hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st);
 hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
                           std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
                           std::uint32_t W, std::uint32_t* out, hipStream_t st);
-std::uint32_t prepass_tiles(std::uint32_t n);
+std::uint64_t prepass_tiles(std::uint64_t n);
 hipError_t launch_fill_uniform(std::uint8_t* dst, std::uint64_t stride, std::uint64_t len, std::uint64_t first,
                                std::uint64_t nblocks, std::uint64_t seed, hipStream_t st);
 hipError_t launch_fill_blocks(std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
@@ -318,7 +318,8 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
   }
   StreamScratch* s = slot.get();
   if (nblocks > s->cap_blocks) {
-    const std::uint64_t cap = std::max<std::uint64_t>(nblocks, 2 * s->cap_blocks);
+    // doubling growth, clamped to the largest irregular batch (nblocks <= kMaxIrregularBlocks)
+    const std::uint64_t cap = std::max<std::uint64_t>(nblocks, std::min<std::uint64_t>(2 * s->cap_blocks, kMaxIrregularBlocks));
     if (s->blob) {
       // Freed blocks may still be in use by earlier work on this stream.
       TKV_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
@@ -326,7 +327,7 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
       s->blob = nullptr;
       s->cap_blocks = 0;
     }
-    const std::uint64_t ntiles = prepass_tiles(static_cast<std::uint32_t>(cap)) + 1;
+    const std::uint64_t ntiles = prepass_tiles(cap) + 1;
     // 8-byte arrays first: scan, tiles, s_off, big_off; then the 4-byte ones
     const std::uint64_t bytes = 8 * (cap + ntiles + 2 * cap) + 4 * (5 * cap + 1);
     TKV_HIP(hipMalloc(&s->blob, bytes));
@@ -403,7 +404,7 @@ int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t s
 int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::uint64_t* d_off, const std::uint32_t* d_len,
                   const std::uint32_t* d_init, std::uint32_t* d_out, std::uint64_t n, hipStream_t st) {
   if (n == 0) return TKV_OK;
-  if (n >= 0xFFFFFFFFull) return fail(TKV_INVALID_ARGUMENT, "batch of 2^32 or more blocks");
+  if (n > kMaxIrregularBlocks) return fail(TKV_INVALID_ARGUMENT, "irregular batch of more than 2^32 - 2^13 blocks");
   StreamScratch* s = nullptr;
   if (int rc = get_scratch(c, st, n, &s)) return rc;
   RowsArgs a = base_args(c, s, algo);
@@ -785,6 +786,7 @@ int batch_device_impl(int algo, const uint8_t* d_base, const uint64_t* d_offsets
   if (n == 0) return TKV_OK;
   if (!ptr_ok(d_base) || !ptr_ok(d_offsets) || !ptr_ok(d_lengths) || !ptr_ok(d_out_final))
     return fail(TKV_INVALID_ARGUMENT, "null pointer");
+  if (n > kMaxIrregularBlocks) return fail(TKV_INVALID_ARGUMENT, "irregular batch of more than 2^32 - 2^13 blocks");
   DevCtx* c = nullptr;
   if (int rc = get_ctx(&c)) return rc;
   return run_irregular(c, algo, d_base, d_offsets, d_lengths, d_init_raw, d_out_final, n, static_cast<hipStream_t>(stream));

@@ -111,6 +111,10 @@ struct PrepassOut {
 // small-block phase instead of occupying a whole 4 KiB row each.
 constexpr std::uint32_t kSmallMax = 1024;
 
+// Irregular batches carry u32 block indices (prepass scan, compacted lists, results): the host caps
+// them below 2^32 with room for the prepass's tile rounding (4096 blocks per scan tile).
+constexpr std::uint64_t kMaxIrregularBlocks = 0xFFFFFFFFull - 8192u;
+
 // rows(b): wave-rows a block of n bytes occupies (every block, even n = 0, owns >= 1 row), and
 // h(b): bytes of its head row (row 0), in [0, kRow].
 TKV_HD inline std::uint32_t rows_for_len(std::uint32_t n) { return n == 0 ? 1u : (n - 1u) / kRow + 1u; }

@@ -299,6 +299,8 @@ __global__ void fill_blocks(std::uint8_t* base, const std::uint64_t* offsets, co
 }
 
 // ---- launchers (called from tkv_crc32_host.cpp) ----------------------------------------------------
+std::uint64_t prepass_tiles(std::uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
+
 hipError_t launch_rows(const RowsArgs& a, bool aligned, bool uniform, unsigned grid, hipStream_t st) {
   if (uniform) {
     if (aligned) hipLaunchKernelGGL((crc_rows<true, true>), dim3(grid), dim3(kRowsThreads), 0, st, a);
@@ -324,20 +326,24 @@ hipError_t launch_fixup(const RowsArgs& a, hipStream_t st) {
 hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
                           std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
                           std::uint32_t W, std::uint32_t* out, hipStream_t st) {
-  const std::uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
-  hipLaunchKernelGGL(rows_tile_scan, dim3(ntiles), dim3(1024), 0, st, lengths, n, scan, tile_sums);
+  // Grid sizes in 64-bit arithmetic: n may be close to 2^32 (the host caps it at kMaxIrregularBlocks).
+  const std::uint64_t ntiles = prepass_tiles(n);
+  const std::uint64_t nfused = (static_cast<std::uint64_t>(n) + kFinishThreads - 1) / kFinishThreads;
+  const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
+  hipLaunchKernelGGL(rows_tile_scan, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, lengths, n, scan,
+                     tile_sums);
   if (ntiles <= kFusedTiles) {
-    hipLaunchKernelGGL(rows_finish_fused, dim3((n + kFinishThreads - 1) / kFinishThreads), dim3(kFinishThreads), 0,
-                       st, offsets, lengths, n, scan, tile_sums, ntiles, counts, o, W, out);
+    hipLaunchKernelGGL(rows_finish_fused, dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, offsets,
+                       lengths, n, scan, tile_sums, static_cast<std::uint32_t>(ntiles), counts, o, W, out);
   } else {
-    hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, ntiles, n, counts);
-    hipLaunchKernelGGL(rows_finish, dim3((n + 255) / 256), dim3(256), 0, st, offsets, lengths, n, scan, tile_sums,
-                       counts, o, W, out);
+    hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, static_cast<std::uint32_t>(ntiles), n,
+                       counts);
+    hipLaunchKernelGGL(rows_finish, dim3(static_cast<unsigned>(nfinish)), dim3(256), 0, st, offsets, lengths, n, scan,
+                       tile_sums, counts, o, W, out);
   }
   return hipGetLastError();
 }
 
-std::uint32_t prepass_tiles(std::uint32_t n) { return (n + kScanTile - 1) / kScanTile; }
 
 hipError_t launch_sst_fix(std::uint8_t* file, const std::uint64_t* offsets, const std::uint32_t* sizes,
                           std::uint32_t* out, std::uint64_t n, int store, const DeviceTables* tabs, hipStream_t st) {
