@@ -204,6 +204,17 @@ uint32_t tkv_debug_multmodp(uint32_t a, uint32_t b);
 size_t tkv_debug_wal_chain(const uint8_t *h_wal, uint64_t size, uint64_t *out_pos, size_t cap, uint64_t *end,
                            int *err);
 uint32_t tkv_debug_x8nmodp(uint64_t nbytes);
+/* The split tkv_crc32_batch_host_multi plans for `ndev` devices (host only, no device, no CRC):
+ * writes up to `cap` pieces as 6 x u64 records {device, block, byte offset, length, initial raw
+ * register, starts its block} in device order, pieces in block order; returns the piece count. */
+size_t tkv_debug_multi_plan(int ndev, const uint64_t *h_offsets, const uint32_t *h_lengths,
+                            const uint32_t *h_init_raw, uint64_t n, uint64_t *out_rec, size_t cap);
+/* The host combine step of that plan: given each piece's finalized CRC (in the order
+ * tkv_debug_multi_plan lists them), writes every block's finalized CRC. 4-byte GF(2) arithmetic on
+ * registers only, for the reflected polynomial `poly`. */
+int tkv_debug_multi_combine(uint32_t poly, int ndev, const uint64_t *h_offsets, const uint32_t *h_lengths,
+                            const uint32_t *h_init_raw, uint64_t n, const uint32_t *piece_final,
+                            uint32_t *h_out_final);
 /* Host batches from pinned host memory are read in place by the kernels (zero copy) unless this is
  * 0 (then they take the staged copy pipeline, as pageable memory does). Returns the previous
  * setting. Default 1; the environment variable TKV_HOST_MAPPED=0 sets 0 at load time. */

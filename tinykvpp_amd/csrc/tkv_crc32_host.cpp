@@ -816,63 +816,99 @@ int batch_host_impl(int algo, const uint8_t* h_base, const uint64_t* h_offsets, 
 // boundary; their pieces run on different devices and combine on the host.
 constexpr std::uint64_t kSplitMin = std::uint64_t(1) << 20;
 
-int batch_host_multi_impl(int algo, const int* devices, int ndev, const uint8_t* h_base, const uint64_t* h_offsets,
-                          const uint32_t* h_lengths, const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
-  if (ndev <= 0 || !ptr_ok(devices)) return fail(TKV_INVALID_ARGUMENT, "no devices");
-  if (n == 0) return TKV_OK;
-  if (!ptr_ok(h_base) || !ptr_ok(h_offsets) || !ptr_ok(h_lengths) || !ptr_ok(h_out_final))
-    return fail(TKV_INVALID_ARGUMENT, "null pointer");
-  // Byte-balanced contiguous split of the block list: device d takes the bytes
-  // [total*d/ndev, total*(d+1)/ndev) of the blocks laid end to end in index order.
-  std::uint64_t total = 0;
-  for (std::uint64_t i = 0; i < n; ++i) total += h_lengths[i];
-  std::vector<std::uint64_t> cut(ndev + 1, n);
-  cut[0] = 0;
-  bool split = false;
-  {
-    std::uint64_t acc = 0, i = 0;
-    for (int d = 1; d < ndev; ++d) {
-      const std::uint64_t target = total * d / ndev;
-      while (i < n && acc + h_lengths[i] <= target) acc += h_lengths[i++];
-      cut[d] = i;
-      // block i straddles the boundary (acc < target < acc + len): cut it if it is large
-      if (i < n && acc < target && h_lengths[i] >= kSplitMin) split = true;
-    }
-  }
-  // Per device, either an index range of the caller's arrays or (split) its own piece list.
+// Split plan of a host batch over ndev devices. Byte-balanced contiguous split of
+// the block list: device d takes the bytes [total*d/ndev, total*(d+1)/ndev) of the blocks laid end
+// to end in index order. Without a cut block the plan is index ranges [cut[d], cut[d+1]) of the
+// caller's arrays; with one (a block >= kSplitMin straddling a share boundary) every device gets its
+// own piece list, pieces in block order, a cut block's head piece taking the block's init and the
+// following pieces starting from 0.
+struct MultiPlan {
   struct Work {
     std::vector<std::uint64_t> off;
     std::vector<std::uint32_t> len, init, out;
     std::vector<std::uint64_t> block;  // batch index of each piece
     std::vector<std::uint8_t> head;    // piece starts its block (takes the block's init)
   };
-  std::vector<Work> work(split ? ndev : 0);
-  const std::uint32_t poly = algo_poly(algo);
-  if (split) {
-    std::uint64_t pos = 0;  // byte position of block i's start in the end-to-end stream
-    int d = 0;
-    for (std::uint64_t i = 0; i < n; ++i) {
-      const std::uint64_t len = h_lengths[i];
-      std::uint64_t done = 0;
-      do {
-        while (d + 1 < ndev && pos + done >= total * (d + 1) / ndev && (len == 0 || done < len)) ++d;
-        std::uint64_t take = len - done;
-        if (len >= kSplitMin && d + 1 < ndev) {
-          const std::uint64_t end = total * (d + 1) / ndev;  // this device's share ends here
-          if (pos + len > end && end > pos + done) take = end - (pos + done);
-        }
-        Work& w = work[d];
-        w.off.push_back(h_offsets[i] + done);
-        w.len.push_back(static_cast<std::uint32_t>(take));
-        w.init.push_back(done == 0 ? (h_init_raw ? h_init_raw[i] : kInit) : 0u);
-        w.block.push_back(i);
-        w.head.push_back(done == 0);
-        done += take;
-      } while (done < len);
-      pos += len;
+  bool split = false;
+  std::vector<std::uint64_t> cut;
+  std::vector<Work> work;  // split plans only, one per device
+};
+
+MultiPlan plan_multi(int ndev, const uint64_t* h_offsets, const uint32_t* h_lengths, const uint32_t* h_init_raw,
+                     uint64_t n) {
+  MultiPlan p;
+  std::uint64_t total = 0;
+  for (std::uint64_t i = 0; i < n; ++i) total += h_lengths[i];
+  p.cut.assign(ndev + 1, n);
+  p.cut[0] = 0;
+  {
+    std::uint64_t acc = 0, i = 0;
+    for (int d = 1; d < ndev; ++d) {
+      const std::uint64_t target = total * d / ndev;
+      while (i < n && acc + h_lengths[i] <= target) acc += h_lengths[i++];
+      p.cut[d] = i;
+      // block i straddles the boundary (acc < target < acc + len): cut it if it is large
+      if (i < n && acc < target && h_lengths[i] >= kSplitMin) p.split = true;
     }
-    for (auto& w : work) w.out.resize(w.off.size());
   }
+  if (!p.split) return p;
+  p.work.resize(ndev);
+  std::uint64_t pos = 0;  // byte position of block i's start in the end-to-end stream
+  int d = 0;
+  for (std::uint64_t i = 0; i < n; ++i) {
+    const std::uint64_t len = h_lengths[i];
+    std::uint64_t done = 0;
+    do {
+      while (d + 1 < ndev && pos + done >= total * (d + 1) / ndev && (len == 0 || done < len)) ++d;
+      std::uint64_t take = len - done;
+      if (len >= kSplitMin && d + 1 < ndev) {
+        const std::uint64_t end = total * (d + 1) / ndev;  // this device's share ends here
+        if (pos + len > end && end > pos + done) take = end - (pos + done);
+      }
+      MultiPlan::Work& w = p.work[d];
+      w.off.push_back(h_offsets[i] + done);
+      w.len.push_back(static_cast<std::uint32_t>(take));
+      w.init.push_back(done == 0 ? (h_init_raw ? h_init_raw[i] : kInit) : 0u);
+      w.block.push_back(i);
+      w.head.push_back(done == 0);
+      done += take;
+    } while (done < len);
+    pos += len;
+  }
+  for (auto& w : p.work) w.out.resize(w.off.size());
+  return p;
+}
+
+// Results of a split plan: pieces arrive in block order across the devices, and a head piece's
+// register continues through the following pieces of its block, r = Shift_len(r) ^ crc_0(piece)
+// (tkv_crc32_combine). Only 4-byte registers are combined here; no data is read.
+void combine_multi(const MultiPlan& p, uint64_t n, std::uint32_t poly, uint32_t* h_out_final) {
+  std::uint64_t cur = n;
+  std::uint32_t raw = 0;
+  for (const auto& w : p.work) {
+    for (std::size_t k = 0; k < w.off.size(); ++k) {
+      const std::uint32_t r = w.out[k] ^ kInit;  // raw register of the piece
+      if (w.head[k]) {
+        if (cur != n) h_out_final[cur] = raw ^ kInit;
+        cur = w.block[k];
+        raw = r;
+      } else {
+        raw = shift_bytes(raw, w.len[k], poly) ^ r;
+      }
+    }
+  }
+  if (cur != n) h_out_final[cur] = raw ^ kInit;
+}
+
+// One host thread per device: hipSetDevice (tkv_set_device) binds the thread, and get_ctx then
+// creates or finds that device's own context (tables, dummy buffer, streams, scratch, staging).
+int batch_host_multi_impl(int algo, const int* devices, int ndev, const uint8_t* h_base, const uint64_t* h_offsets,
+                          const uint32_t* h_lengths, const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
+  if (ndev <= 0 || !ptr_ok(devices)) return fail(TKV_INVALID_ARGUMENT, "no devices");
+  if (n == 0) return TKV_OK;
+  if (!ptr_ok(h_base) || !ptr_ok(h_offsets) || !ptr_ok(h_lengths) || !ptr_ok(h_out_final))
+    return fail(TKV_INVALID_ARGUMENT, "null pointer");
+  MultiPlan plan = plan_multi(ndev, h_offsets, h_lengths, h_init_raw, n);
   std::vector<int> rcs(ndev, TKV_OK);
   std::vector<std::string> errs(ndev);
   std::vector<std::thread> th;
@@ -886,12 +922,13 @@ int batch_host_multi_impl(int algo, const int* devices, int ndev, const uint8_t*
       DevCtx* c = nullptr;
       rcs[d] = get_ctx(&c);
       if (rcs[d] == TKV_OK) {
-        if (split) {
-          Work& w = work[d];
+        if (plan.split) {
+          MultiPlan::Work& w = plan.work[d];
           if (!w.off.empty())
             rcs[d] = host_batch(c, algo, h_base, w.off.data(), w.len.data(), w.init.data(), w.out.data(), 0, w.off.size());
         } else {
-          rcs[d] = host_batch(c, algo, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, cut[d], cut[d + 1]);
+          rcs[d] = host_batch(c, algo, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, plan.cut[d],
+                              plan.cut[d + 1]);
         }
       }
       errs[d] = g_err;
@@ -900,25 +937,7 @@ int batch_host_multi_impl(int algo, const int* devices, int ndev, const uint8_t*
   for (auto& t : th) t.join();
   for (int d = 0; d < ndev; ++d)
     if (rcs[d]) return fail(rcs[d], "device " + std::to_string(devices[d]) + ": " + errs[d]);
-  if (split) {
-    // Pieces arrive in block order across the devices: a head piece's register continues through the
-    // following pieces of its block, r = Shift_len(r) ^ crc_0(piece) (tkv_crc32_combine).
-    std::uint64_t cur = n;
-    std::uint32_t raw = 0;
-    for (auto& w : work) {
-      for (std::size_t k = 0; k < w.off.size(); ++k) {
-        const std::uint32_t r = w.out[k] ^ kInit;  // raw register of the piece
-        if (w.head[k]) {
-          if (cur != n) h_out_final[cur] = raw ^ kInit;
-          cur = w.block[k];
-          raw = r;
-        } else {
-          raw = shift_bytes(raw, w.len[k], poly) ^ r;
-        }
-      }
-    }
-    if (cur != n) h_out_final[cur] = raw ^ kInit;
-  }
+  if (plan.split) combine_multi(plan, n, algo_poly(algo), h_out_final);
   return TKV_OK;
 }
 
@@ -1037,6 +1056,50 @@ size_t tkv_debug_tables_poly(uint32_t poly, void* out, size_t cap) {
 
 uint32_t tkv_debug_multmodp(uint32_t a, uint32_t b) { return multmodp(a, b); }
 uint32_t tkv_debug_x8nmodp(uint64_t nbytes) { return x8nmodp(nbytes); }
+size_t tkv_debug_multi_plan(int ndev, const uint64_t* h_offsets, const uint32_t* h_lengths, const uint32_t* h_init_raw,
+                            uint64_t n, uint64_t* out_rec, size_t cap) {
+  if (ndev <= 0 || n == 0 || !h_offsets || !h_lengths) return 0;
+  const MultiPlan p = plan_multi(ndev, h_offsets, h_lengths, h_init_raw, n);
+  size_t k = 0;
+  auto put = [&](int d, std::uint64_t b, std::uint64_t off, std::uint64_t len, std::uint64_t init, bool head) {
+    if (out_rec && k < cap) {
+      std::uint64_t* r = out_rec + 6 * k;
+      r[0] = static_cast<std::uint64_t>(d);
+      r[1] = b;
+      r[2] = off;
+      r[3] = len;
+      r[4] = init;
+      r[5] = head ? 1u : 0u;
+    }
+    ++k;
+  };
+  for (int d = 0; d < ndev; ++d) {
+    if (p.split) {
+      const auto& w = p.work[d];
+      for (size_t j = 0; j < w.off.size(); ++j) put(d, w.block[j], w.off[j], w.len[j], w.init[j], w.head[j] != 0);
+    } else {
+      for (std::uint64_t b = p.cut[d]; b < p.cut[d + 1]; ++b)
+        put(d, b, h_offsets[b], h_lengths[b], h_init_raw ? h_init_raw[b] : kInit, true);
+    }
+  }
+  return k;
+}
+
+int tkv_debug_multi_combine(uint32_t poly, int ndev, const uint64_t* h_offsets, const uint32_t* h_lengths,
+                            const uint32_t* h_init_raw, uint64_t n, const uint32_t* piece_final, uint32_t* h_out_final) {
+  if (ndev <= 0 || n == 0 || !h_offsets || !h_lengths || !piece_final || !h_out_final) return TKV_INVALID_ARGUMENT;
+  MultiPlan p = plan_multi(ndev, h_offsets, h_lengths, h_init_raw, n);
+  size_t k = 0;
+  if (!p.split) {
+    for (std::uint64_t b = 0; b < n; ++b) h_out_final[b] = piece_final[b];
+    return TKV_OK;
+  }
+  for (auto& w : p.work)
+    for (auto& o : w.out) o = piece_final[k++];
+  combine_multi(p, n, poly, h_out_final);
+  return TKV_OK;
+}
+
 int tkv_debug_set_host_mapped(int enable) { return tkv::g_host_mapped.exchange(enable ? 1 : 0); }
 
 }  // extern "C"
