@@ -103,11 +103,18 @@ int tkv_crc32_batch_host_multi(const int *devices, int ndev, const uint8_t *h_ba
 /* ---- WAL record verification (wal_entry::decode's CRC check, wal.cpp:63-96) ------------------- */
 
 /* Verify every record of a slurped WAL image (host memory, wal_reader::open, wal.cpp:204-240):
- * walks the record_len chain on the host, checks all CRCs in one batch on the GPU, and reports the
+ * copies it to the device, walks the record_len chain and checks all CRCs there, and reports the
  * number of leading good records in *n_good and the byte offset where decoding stopped in
  * *stop_offset. Returns TKV_OK when the whole image verified (clean EOF), TKV_CORRUPTED at the
  * first record whose length or CRC is bad (wal.cpp:68-96 order: header size, length, CRC). */
 int tkv_wal_verify(const uint8_t *h_wal, uint64_t size, uint64_t *n_good, uint64_t *stop_offset);
+
+/* Same for a WAL image already in DEVICE memory (synchronous on `stream`). The record_len chain is
+ * walked on the device (speculative parallel walk, exact stitching), then one CRC batch and a
+ * first-corruption search; results and status as tkv_wal_verify. tkv_wal_verify itself copies the
+ * host image to the device and takes this path (host-thread walk only as the exact fallback). */
+int tkv_wal_verify_device(const uint8_t *d_wal, uint64_t size, uint64_t *n_good, uint64_t *stop_offset,
+                          void *stream);
 
 /* Stamp n records in place (host memory): for record i at h_buf + h_offsets[i] of total size
  * h_sizes[i] (>= 8), write crc32 of bytes [8, size) LE at offset 4 (wal.cpp:54-58). */
@@ -215,6 +222,10 @@ size_t tkv_debug_multi_plan(int ndev, const uint64_t *h_offsets, const uint32_t 
 int tkv_debug_multi_combine(uint32_t poly, int ndev, const uint64_t *h_offsets, const uint32_t *h_lengths,
                             const uint32_t *h_init_raw, uint64_t n, const uint32_t *piece_final,
                             uint32_t *h_out_final);
+/* What the calling thread's last tkv_wal_verify / tkv_wal_verify_device did: out[0] = device walk
+ * passes, out[1] = 1 when it handed the image to the exact host-thread walk, out[2] = 1 when a
+ * host image was copied to the device, out[3] = pieces of the last pass's image. */
+void tkv_debug_wal_last(uint64_t out[4]);
 /* Host batches from pinned host memory are read in place by the kernels (zero copy) unless this is
  * 0 (then they take the staged copy pipeline, as pageable memory does). Returns the previous
  * setting. Default 1; the environment variable TKV_HOST_MAPPED=0 sets 0 at load time. */

@@ -1,0 +1,171 @@
+"""WAL recovery verify with the record chain walked on the device.
+
+tkv_wal_verify copies the slurped image to HBM and tkv_wal_verify_device takes an image already
+there; both walk the record_len chain of wal_entry::decode (/root/reference/src/engine/wal.cpp:63-130)
+on the GPU by speculative parallel walks with exact stitching, check every record's CRC in one batch
+and report the first corruption. Every case is compared with a sequential decode written here
+(header size, record_len, CRC via the test oracle, key/value bounds: wal.cpp:68-121), so the
+parity is against the reference's decode order, not against the library's own host walk.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import tinykvpp_amd as tk
+
+pytestmark = pytest.mark.gpu
+
+
+def sequential_decode(oracle, img, size):
+    """wal_entry::decode applied record after record (engine.cpp:31-53 recovery loop)."""
+    u32 = lambda p: int.from_bytes(img[p:p + 4].tobytes(), "little")  # noqa: E731
+    recs, p, broke = [], 0, False
+    while p < size:
+        if size - p < 26:
+            broke = True
+            break
+        rlen = u32(p)
+        if rlen + 8 > size - p:
+            broke = True
+            break
+        recs.append(p)
+        p += 8 + rlen
+    if recs:
+        r = np.array(recs, np.uint64)
+        rl = np.array([u32(int(x)) for x in r], np.uint64)
+        got = oracle.batch(img, r + 8, rl.astype(np.uint32))
+        stored = np.array([u32(int(x) + 4) for x in r], np.uint32)
+        kv = np.array([26 + u32(int(x) + 18) + u32(int(x) + 22) <= 8 + int(l) for x, l in zip(r, rl)])
+        bad = np.flatnonzero((got != stored) | ~kv)
+        if bad.size:
+            return "corrupted", int(bad[0]), int(r[bad[0]])
+    return ("corrupted" if broke else "ok"), len(recs), p
+
+
+def make_wal(rng, n_rec, vmax=16000, giant=(), fake_headers=0.0):
+    """Stamped WAL image (numpy) of n_rec records laid out as wal.cpp:19-61. `giant`: record
+    indices given 3-9 MiB values. fake_headers: fraction of values that embed a run of valid-looking
+    records (speculative starts inside values)."""
+    klen = rng.integers(0, 40, n_rec).astype(np.uint64)
+    vlen = np.minimum(rng.zipf(1.6, n_rec) * 48, vmax).astype(np.uint64)
+    for g in giant:
+        vlen[g] = int(rng.integers(3 << 20, 9 << 20))
+    size = 26 + klen + vlen
+    offs = np.zeros(n_rec, np.uint64)
+    offs[1:] = np.cumsum(size[:-1])
+    img = rng.integers(0, 256, int(size.sum()), dtype=np.uint8)
+    hdr = np.zeros((n_rec, 26), np.uint8)
+    hdr[:, 0:4] = (size - 8).astype("<u4").view(np.uint8).reshape(-1, 4)
+    hdr[:, 9:17] = np.arange(n_rec, dtype="<u8").view(np.uint8).reshape(-1, 8)
+    hdr[:, 18:22] = klen.astype("<u4").view(np.uint8).reshape(-1, 4)
+    hdr[:, 22:26] = vlen.astype("<u4").view(np.uint8).reshape(-1, 4)
+    img[offs.astype(np.int64)[:, None] + np.arange(26)] = hdr
+    if fake_headers:
+        # values that hold a chain of well-formed 40-byte records: plausible headers off the chain
+        fake = np.zeros(40, np.uint8)
+        fake[0:4] = np.frombuffer((32).to_bytes(4, "little"), np.uint8)
+        fake[18:22] = np.frombuffer((6).to_bytes(4, "little"), np.uint8)
+        fake[22:26] = np.frombuffer((8).to_bytes(4, "little"), np.uint8)
+        for i in np.flatnonzero(rng.random(n_rec) < fake_headers):
+            v0, vl = int(offs[i] + 26 + klen[i]), int(vlen[i])
+            reps = vl // 40
+            if reps:
+                img[v0:v0 + 40 * reps] = np.tile(fake, reps)
+    lib = tk.load_library()
+    size32 = size.astype(np.uint32)
+    tk.check(lib.tkv_wal_stamp(ctypes.c_void_p(img.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                               ctypes.c_void_p(size32.ctypes.data), n_rec))
+    return img, offs, size
+
+
+def both(img, size, shift=0):
+    """(host-image path, device-image path at byte offset `shift` of its allocation)."""
+    h = tk.wal.verify(img[:size].tobytes())
+    d = torch.zeros(size + shift, dtype=torch.uint8, device="cuda")
+    if size:
+        d[shift:] = torch.from_numpy(img[:size].copy()).cuda()
+    dv = tk.wal.verify_device(d[shift:], size)
+    torch.cuda.synchronize()
+    return h, dv
+
+
+@pytest.mark.parametrize("shift", [0, 3])
+def test_small_records_clean_and_corrupted(gpu, oracle, shift):
+    rng = np.random.default_rng(5)
+    img, offs, size = make_wal(rng, 120000, vmax=600)
+    n = img.size
+    want = sequential_decode(oracle, img, n)
+    assert want == ("ok", offs.size, n)
+    assert both(img, n, shift) == (want, want)
+    for bad in (0, 1, 777, 60000, 119999):  # payload flips: CRC mismatch at that record
+        o = int(offs[bad]) + int(size[bad]) - 1
+        img[o] ^= 0x01
+        want = sequential_decode(oracle, img, n)
+        assert want == ("corrupted", bad, int(offs[bad]))
+        assert both(img, n, shift) == (want, want)
+        img[o] ^= 0x01
+
+
+def test_giant_records_and_torn_tail(gpu, oracle):
+    rng = np.random.default_rng(6)
+    img, offs, size = make_wal(rng, 30000, giant=(10, 11, 20000, 29999))
+    for n in (img.size, img.size - 5, int(offs[11]) + 30, int(offs[20000]) + 26 + 4096):
+        want = sequential_decode(oracle, img, n)
+        assert both(img, n) == (want, want), n
+
+
+def test_corrupted_record_len_and_overrun(gpu, oracle):
+    """A record_len that lies sends the chain through garbage (the speculative pieces after it
+    disagree, the walk resumes or stops exactly where the sequential decode does)."""
+    rng = np.random.default_rng(7)
+    img, offs, size = make_wal(rng, 50000, vmax=2000)
+    n = img.size
+    for bad, delta in ((100, 7), (25000, 4096), (49990, -3)):
+        o = int(offs[bad])
+        old = img[o:o + 4].copy()
+        img[o:o + 4] = np.frombuffer((int(size[bad]) - 8 + delta).to_bytes(4, "little"), np.uint8)
+        want = sequential_decode(oracle, img, n)
+        assert want[0] == "corrupted" and want[1] == bad
+        assert both(img, n) == (want, want)
+        img[o:o + 4] = np.frombuffer((0xFFFFFF00).to_bytes(4, "little"), np.uint8)  # overruns the image
+        want = sequential_decode(oracle, img, n)
+        assert want == ("corrupted", bad, o)
+        assert both(img, n) == (want, want)
+        img[o:o + 4] = old
+
+
+def test_fake_headers_inside_values(gpu, oracle):
+    """Values full of well-formed records: speculative starts land off the true chain and must be
+    discarded by the stitch (exact result, clean and with a late corruption)."""
+    rng = np.random.default_rng(8)
+    img, offs, size = make_wal(rng, 40000, vmax=9000, fake_headers=0.5)
+    n = img.size
+    want = sequential_decode(oracle, img, n)
+    assert want == ("ok", offs.size, n)
+    assert both(img, n) == (want, want)
+    o = int(offs[39000]) + 26
+    img[o] ^= 0x80
+    want = sequential_decode(oracle, img, n)
+    assert both(img, n) == (want, want)
+
+
+@pytest.mark.parametrize("n", [0, 1, 25, 26, 27, 33, 34, 35, 2047, 2048, 2049, 4096 + 17])
+def test_tiny_and_piece_boundary_images(gpu, oracle, n):
+    rng = np.random.default_rng(9)
+    img, offs, size = make_wal(rng, 400, vmax=200)
+    want = sequential_decode(oracle, img, n)
+    assert both(img, n) == (want, want)
+
+
+def test_golden_records_on_device(gpu):
+    from conftest import golden
+    recs = [bytes.fromhex(r["hex"]) for r in golden("wal.json")["records"]]
+    image = b"".join(recs)
+    d = torch.frombuffer(bytearray(image), dtype=torch.uint8).cuda()
+    assert tk.wal.verify_device(d) == ("ok", len(recs), len(image))
+    bad = bytearray(image)
+    bad[len(recs[0]) + 4] ^= 0xFF  # wal_test.cpp:809-850: parked at record 1
+    d = torch.frombuffer(bad, dtype=torch.uint8).cuda()
+    assert tk.wal.verify_device(d) == ("corrupted", 1, len(recs[0]))

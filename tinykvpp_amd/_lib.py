@@ -44,6 +44,7 @@ SIGNATURES = {
     "tkv_crc32_batch_host_multi": (_int, [_vp, _int, _u8p, _vp, _vp, _vp, _vp, _u64]),
     "tkv_crc32_combine": (_u32, [_u32, _u32, _u64]),
     "tkv_wal_verify": (_int, [_u8p, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    "tkv_wal_verify_device": (_int, [_u8p, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64), _vp]),
     "tkv_wal_stamp": (_int, [_u8p, _vp, _vp, _u64]),
     "tkv_fill_synthetic_uniform": (_int, [_u8p, _u64, _u64, _u64, _u64, _u64, _vp]),
     "tkv_fill_synthetic_blocks": (_int, [_u8p, _vp, _vp, _u64, _u64, _u64, _vp]),
@@ -65,6 +66,7 @@ SIGNATURES = {
     "tkv_debug_x8nmodp": (_u32, [_u64]),
     "tkv_debug_set_host_mapped": (_int, [_int]),
     "tkv_debug_wal_chain": (_sz, [_u8p, _u64, _vp, _sz, ctypes.POINTER(_u64), ctypes.POINTER(_int)]),
+    "tkv_debug_wal_last": (None, [_vp]),
     "tkv_debug_multi_plan": (_sz, [_int, _vp, _vp, _vp, _u64, _vp, _sz]),
     "tkv_debug_multi_combine": (_int, [_u32, _int, _vp, _vp, _vp, _u64, _vp, _vp]),
 }

@@ -14,6 +14,7 @@
 
 #include "tkv_crc32.h"
 #include "tkv_engine.h"
+#include "tkv_wal_device.h"
 
 using namespace tkv;
 
@@ -197,6 +198,8 @@ Chain wal_chain(const std::uint8_t* w, std::uint64_t size, std::uint64_t start, 
 
 Chain wal_chain(const std::uint8_t* w, std::uint64_t size) { return wal_chain(w, size, 0, size); }
 
+int wal_verify_host_walk(const uint8_t* h_wal, uint64_t size, uint64_t* n_good, uint64_t* stop_offset);
+
 int sst_check(const std::uint64_t* h_sizes, std::uint64_t n) {
   for (std::uint64_t i = 0; i < n; ++i)
     if (h_sizes[i] < TKV_SST_MIN_IMAGE || h_sizes[i] > 0xFFFFFFFFull)
@@ -210,6 +213,39 @@ extern "C" {
 int tkv_wal_verify(const uint8_t* h_wal, uint64_t size, uint64_t* n_good, uint64_t* stop_offset) {
   if ((size && !ptr_ok(h_wal)) || !ptr_ok(n_good) || !ptr_ok(stop_offset))
     return set_error(TKV_INVALID_ARGUMENT, "null pointer");
+  // The image goes to the device once; the chain walk, the CRC batch and the first-corruption
+  // search run there (tkv_wal_device.hip). The host walk below is the exact fallback for images the
+  // device cannot hold or whose chain the speculative device walk could not settle.
+  bool host_walk = false;
+  const int rc = wal_verify_host_image_impl(h_wal, size, n_good, stop_offset, &host_walk);
+  if (!host_walk) return rc;
+  return wal_verify_host_walk(h_wal, size, n_good, stop_offset);
+}
+
+int tkv_wal_verify_device(const uint8_t* d_wal, uint64_t size, uint64_t* n_good, uint64_t* stop_offset,
+                          void* stream) {
+  if ((size && !ptr_ok(d_wal)) || !ptr_ok(n_good) || !ptr_ok(stop_offset))
+    return set_error(TKV_INVALID_ARGUMENT, "null pointer");
+  if (size == 0) {
+    *n_good = *stop_offset = 0;
+    return TKV_OK;
+  }
+  bool host_walk = false;
+  const int rc = wal_verify_device_impl(d_wal, size, n_good, stop_offset, static_cast<hipStream_t>(stream), &host_walk);
+  if (!host_walk) return rc;
+  // exact fallback: the image comes back to the host for the sequential-stitched host walk
+  std::vector<std::uint8_t> h(size);
+  if (hipMemcpy(h.data(), d_wal, size, hipMemcpyDeviceToHost) != hipSuccess)
+    return set_error(TKV_IO_ERROR, "WAL image copy to host failed");
+  return wal_verify_host_walk(h.data(), size, n_good, stop_offset);
+}
+
+}  // extern "C"
+
+namespace {
+// The host-walk verify (exact for every image): the record_len chain walked on host threads, the
+// CRCs checked on the GPU through the host batch API.
+int wal_verify_host_walk(const uint8_t* h_wal, uint64_t size, uint64_t* n_good, uint64_t* stop_offset) {
   // The record_len chain (wal.cpp:63-87), walked in parallel (wal_chain): records are
   // [u32 record_len][u32 crc][payload of record_len bytes]. Large images go in phases: the CRC
   // batch of phase j runs (GPU, on a helper thread) while the host walks phase j+1.
@@ -259,6 +295,9 @@ int tkv_wal_verify(const uint8_t* h_wal, uint64_t size, uint64_t* n_good, uint64
   if (good < nrec || ch.err) return set_error(TKV_CORRUPTED, "corrupted WAL record");
   return TKV_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int tkv_wal_stamp(uint8_t* h_buf, const uint64_t* h_offsets, const uint32_t* h_sizes, uint64_t n) {
   if (n == 0) return TKV_OK;

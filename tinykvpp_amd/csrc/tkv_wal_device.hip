@@ -1,0 +1,711 @@
+// WAL recovery verify on the device: the record_len chain walk of
+// wal_entry::decode (/root/reference/src/engine/wal.cpp:63-130) over a WAL image resident in HBM,
+// the CRC check of every record (wal.cpp:89-96) and the key/value bounds check (wal.cpp:118-121),
+// ending in the first corruption - without walking the chain on the host.
+//
+// The record chain is a linked list through the image (record i+1 starts 8 + record_len bytes after
+// record i), so it is walked speculatively in parallel and stitched exactly:
+//  1. wal_scan (one streaming pass): the image is cut into pieces of kWalPiece bytes, and the first
+//     plausible header of every piece (one the reference encoder could have written,
+//     wal.cpp:19-61) becomes its speculative start S_k; piece 0 starts at 0.
+//  2. wal_spec: one lane per piece walks the chain from S_k over the records that start in the
+//     piece: X_k = the first record start at or past the piece's end (or the header that broke).
+//  3. wal_jump: next(k) = the piece holding X_k. The true chain visits the pieces 0, next(0),
+//     next(next(0)), ...; pointer doubling marks exactly those pieces in log2(#pieces) rounds, and
+//     wal_link hands every on-path piece its entry E = X of its predecessor.
+//  4. wal_count: an on-path piece whose entry is its speculative start keeps its speculative walk;
+//     otherwise it walks again from E. Its speculative exit was right when the exact walk leaves at
+//     the same X (and breaks, or not, the same way). Entries are exact up to and including the
+//     first piece k* whose speculative exit was wrong (a corrupted record_len, or a fake header in a
+//     key or value that led the speculation astray): later pieces are dropped, and when no record up
+//     to k*'s exact exit fails, the next pass resumes there (a true record start) as a new image.
+//  5. wal_check: one exclusive scan gives every piece its first record index; each lane walks its
+//     piece again and checks every record of at most kWalLaneMax payload bytes itself (slicing-by-4
+//     lookups into the engine's LDS tables, the payload zero-padded in front to whole dwords). Larger
+//     records are listed for one CRC batch through the engine's irregular path (tkv_crc32_batch_device
+//     kernels) and checked by wal_check_big. The first bad record is an atomic minimum of record
+//     indices.
+// Every step reads the image in HBM; the host only reads back a few counters.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "tkv_crc32.h"
+#include "tkv_crc32_device.h"
+#include "tkv_engine.h"
+#include "tkv_wal_device.h"
+
+namespace tkv {
+namespace {
+
+constexpr std::uint64_t kWalPiece = 2048;     // bytes of image per speculative walker
+constexpr std::uint64_t kWalMeta = 26;        // wal.hpp:21-27 kMetadataSize
+constexpr std::uint32_t kWalLaneMax = 1024;   // payloads up to this size are checked by their lane
+constexpr std::uint64_t kNone = ~0ull;
+constexpr unsigned kScanThreads = 256;        // wal_scan: 16 positions per thread, 4 KiB per workgroup
+constexpr unsigned kCheckThreads = 1024;      // wal_check: one workgroup per CU (128 KiB of LDS tables)
+
+struct WalArgs {
+  const std::uint8_t* w;
+  std::uint64_t size;
+  std::uint32_t K;           // pieces
+  std::uint64_t* S;          // speculative start of piece k (kNone: no plausible header)
+  std::uint64_t* X;          // exit of its speculative chain, or the start of the header that broke it
+  std::uint64_t* spec_cnt;   // records of the speculative chain: (all << 32) | (larger than kWalLaneMax)
+  std::uint32_t* next;       // piece of X (K: end of image, broken chain or no start)
+  std::uint8_t* broke;       // the speculative chain hit a header that does not fit (at X)
+  std::uint32_t* Ja;         // pointer-doubling jump tables
+  std::uint32_t* Jb;
+  std::uint8_t* on;          // piece is on the true chain
+  std::uint64_t* entry;      // true entry point of an on-path piece
+  std::uint64_t* cnt;        // records of an on-path piece from its entry, packed as spec_cnt
+  std::uint64_t* base;       // exclusive scan of cnt: first record index (high), first big record (low)
+  std::uint64_t* Xe;         // exit of its exact walk from the entry (or the header that broke it)
+  std::uint8_t* Be;          // the exact walk broke
+  std::uint64_t* bad_at;     // piece's first failing record: index, and its start in bad_pos
+  std::uint64_t* bad_pos;
+  std::uint64_t* big_off;    // records larger than kWalLaneMax: payload offset, length, index, stored CRC
+  std::uint32_t* big_len;
+  std::uint64_t* big_idx;
+  std::uint32_t* big_crc;
+  std::uint32_t* got;        // engine CRC of each big payload (finalized)
+  const std::uint32_t* inj;  // inj[L] = Shift_L(0xFFFFFFFF), L <= kWalLaneMax: the init term
+  const DeviceTables* tabs;
+  std::uint64_t* res;        // [0] first piece with a wrong speculative exit, [1] chain end and
+                             // [2] chain broke (from the path's last piece), [3] first bad record,
+                             // [4] its start, [5] records of the path up to k* (or all)
+};
+
+// Little-endian u32 at byte p of the image, p + 4 <= size: dword loads aligned to the absolute
+// address, realigned with v_alignbyte. The second dword is read only when it starts inside the
+// image, so no load touches a dword past the image's last byte (nor a page past its allocation);
+// the first may start up to 3 bytes before w, inside the same aligned dword as w itself.
+__device__ __forceinline__ std::uint32_t ld32(const std::uint8_t* w, std::uint64_t p, std::uint64_t size) {
+  const std::uintptr_t q = reinterpret_cast<std::uintptr_t>(w) + p;
+  const std::uintptr_t a = q & ~static_cast<std::uintptr_t>(3);
+  const std::uintptr_t end = reinterpret_cast<std::uintptr_t>(w) + size;
+  const std::uint32_t lo = *reinterpret_cast<const std::uint32_t*>(a);
+  const std::uint32_t hi = (q & 3u) && a + 4 < end ? *reinterpret_cast<const std::uint32_t*>(a + 4) : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, static_cast<std::uint32_t>(q & 3u));
+}
+
+__device__ __forceinline__ std::uint64_t gid() {
+  return blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+}
+
+// 1. First plausible header per piece, one coalesced pass over the image. Thread t owns the 16
+// positions of the absolute 16-byte chunk t (relative positions 16t - off0 + j) and holds the 48
+// bytes [16t, 16t + 48) of its chunk in registers: a header at position p needs bytes p..p+25
+// (record_len, op/tombstone flags at p+8 and p+17, klen and vlen at p+18 and p+22; wal.cpp:30-52).
+// Chunks are read only when they hold image bytes. A wave covers 1 KiB, i.e. at most two pieces:
+// wave minimum per piece, one atomic per piece and wave.
+__global__ __launch_bounds__(kScanThreads) void wal_scan(WalArgs a) {
+  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
+  const std::uintptr_t al = w0 & ~static_cast<std::uintptr_t>(15);
+  const std::uint64_t off0 = w0 - al;
+  const std::uint64_t t = gid();
+  const std::uintptr_t c0 = al + 16 * t;  // this thread's chunk
+  const std::uintptr_t end = w0 + a.size;
+  std::uint32_t dw[12];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const std::uintptr_t ca = c0 + 16u * c;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (ca < end) v = *reinterpret_cast<const uint4*>(ca);
+    dw[4 * c + 0] = v.x;
+    dw[4 * c + 1] = v.y;
+    dw[4 * c + 2] = v.z;
+    dw[4 * c + 3] = v.w;
+  }
+  auto byte = [&](int o) { return (dw[o >> 2] >> (8 * (o & 3))) & 0xFFu; };
+  auto u32at = [&](int o) { return (o & 3) ? __builtin_amdgcn_alignbyte(dw[(o >> 2) + 1], dw[o >> 2], o & 3) : dw[o >> 2]; };
+  const std::int64_t p0 = static_cast<std::int64_t>(16 * t) - static_cast<std::int64_t>(off0);
+  std::uint64_t best = kNone;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const std::int64_t p = p0 + j;
+    if (p >= 0 && static_cast<std::uint64_t>(p) < a.size && a.size - static_cast<std::uint64_t>(p) >= kWalMeta &&
+        byte(j + 8) <= 1u && byte(j + 17) <= 1u) {
+      const std::uint64_t rlen = u32at(j), klen = u32at(j + 18), vlen = u32at(j + 22);
+      if (rlen == 18u + klen + vlen && rlen + 8 <= a.size - static_cast<std::uint64_t>(p) &&
+          best == kNone)
+        best = static_cast<std::uint64_t>(p);
+    }
+  }
+  // the wave's positions span pieces pa and pa + 1
+  const std::int64_t wave_p0 = static_cast<std::int64_t>(16 * (t & ~63ull)) - static_cast<std::int64_t>(off0);
+  const std::uint64_t pa = wave_p0 < 0 ? 0 : static_cast<std::uint64_t>(wave_p0) / kWalPiece;
+  std::uint64_t mA = (best != kNone && best / kWalPiece == pa) ? best : kNone;
+  std::uint64_t mB = (best != kNone && best / kWalPiece != pa) ? best : kNone;
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) {
+    const std::uint64_t oA = __shfl_xor(mA, m, 64), oB = __shfl_xor(mB, m, 64);
+    mA = oA < mA ? oA : mA;
+    mB = oB < mB ? oB : mB;
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    if (mA != kNone && pa != 0) atomicMin(reinterpret_cast<unsigned long long*>(&a.S[pa]), mA);
+    if (mB != kNone && pa + 1 < a.K) atomicMin(reinterpret_cast<unsigned long long*>(&a.S[pa + 1]), mB);
+  }
+}
+
+// 2. Speculative walk of one piece from its first plausible header (piece 0 from 0). Counts the
+// chain's records (all, and those too large to check in-lane) for wal_count to reuse.
+__global__ void wal_spec(WalArgs a) {
+  const std::uint64_t k = gid();
+  if (k >= a.K) return;
+  const std::uint64_t s = k == 0 ? 0 : a.S[k];
+  if (k == 0) a.S[0] = 0;
+  if (s == kNone) {
+    a.X[k] = kNone;
+    a.next[k] = a.K;
+    a.broke[k] = 0;
+    a.spec_cnt[k] = 0;
+    return;
+  }
+  const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
+  std::uint64_t p = s, n_all = 0, n_big = 0;
+  bool bad = false;
+  while (p < limit) {  // wal.cpp:63-87: header size, then record_len against what is left
+    if (a.size - p < kWalMeta) {
+      bad = true;
+      break;
+    }
+    const std::uint64_t rlen = ld32(a.w, p, a.size);
+    if (rlen + 8 > a.size - p) {
+      bad = true;
+      break;
+    }
+    ++n_all;
+    n_big += rlen > kWalLaneMax ? 1u : 0u;
+    p += 8 + rlen;
+  }
+  a.X[k] = p;
+  a.broke[k] = bad ? 1 : 0;
+  a.spec_cnt[k] = (n_all << 32) | n_big;
+  a.next[k] = (bad || p >= a.size) ? a.K : static_cast<std::uint32_t>(p / kWalPiece);
+}
+
+__global__ void wal_jump_init(WalArgs a) {
+  const std::uint64_t k = gid();
+  if (k >= a.K) return;
+  a.Ja[k] = a.next[k];
+  a.on[k] = k == 0 ? 1 : 0;
+  a.bad_at[k] = kNone;
+}
+
+// 3. One doubling round: marks J(k) for every marked k (J = next^(2^t)), then J <- J o J. Marks set
+// during the round by other threads are pieces of the true path too, so reading them early is safe.
+__global__ void wal_jump(const std::uint32_t* J, std::uint32_t* J2, std::uint8_t* on, std::uint32_t K) {
+  const std::uint64_t k = gid();
+  if (k >= K) return;
+  const std::uint32_t j = J[k];
+  if (j < K && on[k]) on[j] = 1;
+  J2[k] = j < K ? J[j] : K;
+}
+
+// Entry points: each on-path piece hands its exit to the piece that holds it (one writer each:
+// the path is a simple chain).
+__global__ void wal_link(WalArgs a) {
+  const std::uint64_t k = gid();
+  if (k >= a.K || !a.on[k]) return;
+  if (k == 0) a.entry[0] = 0;
+  const std::uint32_t n = a.next[k];
+  if (n < a.K) a.entry[n] = a.X[k];
+}
+
+// 4. Records of an on-path piece from its entry (the speculative walk's when it started there, an
+// exact walk otherwise): count, exit, break. res[0] = the first piece whose speculative exit was
+// wrong. Off-path pieces count 0.
+__global__ void wal_count(WalArgs a) {
+  const std::uint64_t k = gid();
+  if (k >= a.K) return;
+  if (!a.on[k]) {
+    a.cnt[k] = 0;
+    return;
+  }
+  const std::uint64_t e = a.entry[k];
+  std::uint64_t p, packed;
+  bool bad;
+  if (e == a.S[k]) {
+    p = a.X[k];
+    bad = a.broke[k] != 0;
+    packed = a.spec_cnt[k];
+  } else {
+    const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
+    std::uint64_t n_all = 0, n_big = 0;
+    p = e;
+    bad = false;
+    while (p < limit) {  // wal.cpp:63-87
+      if (a.size - p < kWalMeta) {
+        bad = true;
+        break;
+      }
+      const std::uint64_t rlen = ld32(a.w, p, a.size);
+      if (rlen + 8 > a.size - p) {
+        bad = true;
+        break;
+      }
+      ++n_all;
+      n_big += rlen > kWalLaneMax ? 1u : 0u;
+      p += 8 + rlen;
+    }
+    packed = (n_all << 32) | n_big;
+    if (p != a.X[k] || bad != (a.broke[k] != 0)) atomicMin(reinterpret_cast<unsigned long long*>(&a.res[0]), k);
+  }
+  a.cnt[k] = packed;
+  a.Xe[k] = p;
+  a.Be[k] = bad ? 1 : 0;
+  if (a.next[k] >= a.K) {
+    a.res[1] = p;
+    a.res[2] = bad ? 1 : 0;
+  }
+}
+
+// Records past the first piece with a wrong speculative exit are not on the true chain (or not
+// known to be): drop them.
+__global__ void wal_trim(WalArgs a, std::uint64_t kstar) {
+  const std::uint64_t k = gid();
+  if (k < a.K && k > kstar) a.cnt[k] = 0;
+}
+
+// CRC-32 (finalized) of the payload [q, q + L) in image bytes, L <= kWalLaneMax, folded by this
+// lane alone: the payload is zero-padded in front to whole dwords (leading zeros leave an init-0
+// register at 0) and folded with slicing-by-4 lookups into the LDS tables; the init register enters
+// as inj[L] = Shift_L(0xFFFFFFFF) (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). Dwords are read aligned to
+// the absolute address and realigned with v_alignbyte; no dword past the payload's last one is read.
+__device__ __forceinline__ std::uint32_t lane_crc(const std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
+                                                  std::uint64_t q, std::uint32_t L) {
+  const std::uint32_t z = (4u - (L & 3u)) & 3u;  // zero bytes in front
+  const std::uintptr_t s = reinterpret_cast<std::uintptr_t>(a.w) + q - z;
+  const std::uint32_t t = static_cast<std::uint32_t>(s & 3u);
+  const std::uintptr_t al = s - t;
+  const std::uint32_t n = (z + L) >> 2;
+  dev::Reg r{0, 0};
+  std::uint32_t lo = n ? *reinterpret_cast<const std::uint32_t*>(al) : 0u;
+  for (std::uint32_t j = 0; j < n; ++j) {
+    // next aligned dword: needed for the realignment (t != 0) or as the next dword (t == 0)
+    const bool more = t != 0 || j + 1 < n;
+    const std::uint32_t hi = more ? *reinterpret_cast<const std::uint32_t*>(al + 4u * (j + 1)) : 0u;
+    std::uint32_t d = t ? __builtin_amdgcn_alignbyte(hi, lo, t) : lo;
+    if (j == 0) d &= static_cast<std::uint32_t>(0xFFFFFFFFull << (8 * z));
+    dev::slice4(lds, r, d, kc);
+    lo = hi;
+  }
+  return r.value() ^ a.inj[L] ^ 0xFFFFFFFFu;
+}
+
+// 5. Every record of an on-path piece (up to k*), in chain order: key/value bounds, and the CRC of
+// payloads up to kWalLaneMax bytes checked by the lane itself; larger records go to the big list.
+// The piece's first failing record is kept for the position lookup.
+__global__ __launch_bounds__(kCheckThreads) void wal_check(WalArgs a) {
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  // slicing tables only (the lane shifts of the row kernels are not needed here)
+  for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
+    const std::uint32_t pair = u >> 9, e = (u >> 1) & 255u, tt = u & 1u;
+    const std::uint32_t v = a.tabs->slice[2 * pair + tt][e];
+    uint4* dst = reinterpret_cast<uint4*>(lds + pair * 16384u + e * 64u + tt * 32u);
+#pragma unroll
+    for (std::uint32_t k = 0; k < 8u; ++k) dst[(k + u) & 7u] = make_uint4(v, v, v, v);
+  }
+  __syncthreads();
+  const std::uint64_t k = gid();
+  if (k >= a.K || !a.on[k] || a.cnt[k] == 0) return;
+  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
+  const std::uint64_t n_all = a.cnt[k] >> 32;
+  std::uint64_t idx = a.base[k] >> 32, bi = a.base[k] & 0xFFFFFFFFull, p = a.entry[k];
+  std::uint64_t first = kNone, first_pos = 0;
+  for (std::uint64_t i = 0; i < n_all; ++i, ++idx) {
+    const std::uint32_t rlen = ld32(a.w, p, a.size);
+    const std::uint32_t stored = ld32(a.w, p + 4, a.size);
+    const std::uint64_t klen = ld32(a.w, p + 18, a.size), vlen = ld32(a.w, p + 22, a.size);
+    bool bad = kWalMeta + klen + vlen > 8ull + rlen;  // wal.cpp:118-121
+    if (rlen <= kWalLaneMax) {
+      bad = bad || lane_crc(lds, kc, a, p + 8, rlen) != stored;  // wal.cpp:89-96
+    } else {
+      a.big_off[bi] = p + 8;
+      a.big_len[bi] = rlen;
+      a.big_idx[bi] = idx;
+      a.big_crc[bi] = stored;
+      ++bi;
+    }
+    if (bad && first == kNone) {
+      first = idx;
+      first_pos = p;
+    }
+    p += 8 + static_cast<std::uint64_t>(rlen);
+  }
+  if (first != kNone) {
+    a.bad_at[k] = first;
+    a.bad_pos[k] = first_pos;
+    atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), first);
+  }
+}
+
+__global__ void wal_check_big(WalArgs a, std::uint64_t n) {
+  const std::uint64_t i = gid();
+  if (i < n && a.got[i] != a.big_crc[i]) atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), a.big_idx[i]);
+}
+
+// Start of the first bad record (res[3]): from the piece that found it, or from the big list.
+__global__ void wal_bad_pos(WalArgs a, std::uint64_t n_big) {
+  const std::uint64_t i = gid();
+  const std::uint64_t want = a.res[3];
+  if (i < a.K && a.bad_at[i] == want) a.res[4] = a.bad_pos[i];
+  if (i < n_big && a.big_idx[i] == want) a.res[4] = a.big_off[i] - 8;
+}
+
+// Per-device scratch, grown by doubling and kept between calls (guarded by mu).
+struct WalScratch {
+  std::mutex mu;
+  std::uint64_t cap_pieces = 0, cap_big = 0;
+  void* pieces = nullptr;  // per piece: 10 u64, 3 u32, 3 u8 (carve)
+  void* bigs = nullptr;    // per big record: 2 u64, 3 u32
+  void* cub = nullptr;
+  std::size_t cub_bytes = 0;
+  std::uint64_t* res = nullptr;
+  std::uint64_t* h_res = nullptr;
+  std::uint32_t* inj = nullptr;  // Shift_L(0xFFFFFFFF), L = 0..kWalLaneMax
+  // host images: device copy, pinned staging slabs for pageable sources, own stream
+  std::uint8_t* d_img = nullptr;
+  std::uint64_t cap_img = 0;
+  std::uint8_t* slab[2] = {nullptr, nullptr};
+  hipEvent_t slab_free[2] = {nullptr, nullptr};
+  hipStream_t st = nullptr;
+  ~WalScratch() {
+    if (st) (void)hipStreamSynchronize(st);
+    (void)hipFree(d_img);
+    for (int i = 0; i < 2; ++i) {
+      (void)hipHostFree(slab[i]);
+      if (slab_free[i]) (void)hipEventDestroy(slab_free[i]);
+    }
+    if (st) (void)hipStreamDestroy(st);
+    (void)hipFree(pieces);
+    (void)hipFree(bigs);
+    (void)hipFree(cub);
+    (void)hipFree(res);
+    (void)hipFree(inj);
+    (void)hipHostFree(h_res);
+  }
+};
+
+std::mutex g_wal_mu;
+WalScratch* g_wal[64] = {};
+
+// What the calling thread's last WAL verify did (tkv_debug_wal_last).
+thread_local std::uint64_t g_last[4] = {0, 0, 0, 0};  // passes, host walk needed, image copied, pieces
+
+#define WAL_HIP(call)                                                            \
+  do {                                                                           \
+    hipError_t e_ = (call);                                                      \
+    if (e_ != hipSuccess) return set_error(TKV_IO_ERROR, hipGetErrorString(e_)); \
+  } while (0)
+
+int grow_pieces(WalScratch& s, std::uint64_t K) {
+  if (K <= s.cap_pieces) return TKV_OK;
+  const std::uint64_t cap = std::max<std::uint64_t>(K, 2 * s.cap_pieces);
+  WAL_HIP(hipFree(s.pieces));
+  s.pieces = nullptr;
+  s.cap_pieces = 0;
+  WAL_HIP(hipMalloc(&s.pieces, cap * (10 * 8 + 3 * 4 + 3)));
+  s.cap_pieces = cap;
+  return TKV_OK;
+}
+
+int grow_big(WalScratch& s, std::uint64_t n) {
+  if (n <= s.cap_big) return TKV_OK;
+  const std::uint64_t cap = std::max<std::uint64_t>(n, 2 * s.cap_big);
+  WAL_HIP(hipFree(s.bigs));
+  s.bigs = nullptr;
+  s.cap_big = 0;
+  WAL_HIP(hipMalloc(&s.bigs, cap * (2 * 8 + 3 * 4)));
+  s.cap_big = cap;
+  return TKV_OK;
+}
+
+WalArgs carve(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std::uint32_t K, const DeviceTables* tabs) {
+  WalArgs a{};
+  a.w = w;
+  a.size = size;
+  a.K = K;
+  const std::uint64_t C = s.cap_pieces;
+  auto* p8 = static_cast<std::uint64_t*>(s.pieces);
+  std::uint64_t** u64s[] = {&a.S, &a.X, &a.spec_cnt, &a.entry, &a.cnt, &a.base, &a.Xe, &a.bad_at, &a.bad_pos};
+  for (std::size_t i = 0; i < sizeof(u64s) / sizeof(u64s[0]); ++i) *u64s[i] = p8 + i * C;
+  auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 10 * C);
+  a.next = p4;
+  a.Ja = p4 + C;
+  a.Jb = p4 + 2 * C;
+  auto* p1 = reinterpret_cast<std::uint8_t*>(p4 + 3 * C);
+  a.broke = p1;
+  a.on = p1 + C;
+  a.Be = p1 + 2 * C;
+  const std::uint64_t B = s.cap_big;
+  if (B) {
+    auto* b8 = static_cast<std::uint64_t*>(s.bigs);
+    a.big_off = b8;
+    a.big_idx = b8 + B;
+    auto* b4 = reinterpret_cast<std::uint32_t*>(b8 + 2 * B);
+    a.big_len = b4;
+    a.big_crc = b4 + B;
+    a.got = b4 + 2 * B;
+  }
+  a.inj = s.inj;
+  a.tabs = tabs;
+  a.res = s.res;
+  return a;
+}
+
+unsigned blocks(std::uint64_t n, unsigned t) { return static_cast<unsigned>((n + t - 1) / t); }
+
+// CRC batches of at most this many records (the irregular path's u32 block indices).
+constexpr std::uint64_t kWalCrcChunk = std::uint64_t(1) << 31;
+
+struct PassResult {
+  std::uint64_t good = 0;  // records verified good from the pass's start
+  std::uint64_t stop = 0;  // where decoding stopped (relative to the pass's start)
+  bool corrupted = false;
+  bool resume = false;     // the chain continues at `stop` (a true record start) beyond what was checked
+};
+
+// One pass over the image [w, w + size), which starts with a record (or is empty).
+int wal_pass(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream_t st, PassResult* r) {
+  const std::uint32_t K = static_cast<std::uint32_t>((size + kWalPiece - 1) / kWalPiece);
+  const DeviceTables* tabs = device_tables(kAlgoCrc32);
+  if (!tabs) return TKV_IO_ERROR;
+  if (int rc = grow_pieces(s, K)) return rc;
+  WalArgs a = carve(s, w, size, K, tabs);
+  s.h_res[0] = kNone;
+  s.h_res[1] = size;
+  s.h_res[2] = 0;
+  s.h_res[3] = kNone;
+  s.h_res[4] = 0;
+  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 5 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
+  WAL_HIP(hipMemsetAsync(a.S, 0xFF, K * sizeof(std::uint64_t), st));
+
+  // 1-3: speculative starts and walks, the pieces on the true chain, their entries
+  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(w);
+  const std::uint64_t chunks = ((w0 & 15u) + size + 15) / 16;
+  hipLaunchKernelGGL(wal_scan, dim3(blocks(chunks, kScanThreads)), dim3(kScanThreads), 0, st, a);
+  hipLaunchKernelGGL(wal_spec, dim3(blocks(K, 256)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(wal_jump_init, dim3(blocks(K, 256)), dim3(256), 0, st, a);
+  std::uint32_t* J = a.Ja;
+  std::uint32_t* J2 = a.Jb;
+  for (std::uint64_t reach = 1; reach < K; reach <<= 1) {
+    hipLaunchKernelGGL(wal_jump, dim3(blocks(K, 256)), dim3(256), 0, st, J, J2, a.on, K);
+    std::swap(J, J2);
+  }
+  hipLaunchKernelGGL(wal_link, dim3(blocks(K, 256)), dim3(256), 0, st, a);
+  // 4: record counts from the entries
+  hipLaunchKernelGGL(wal_count, dim3(blocks(K, 256)), dim3(256), 0, st, a);
+  WAL_HIP(hipGetLastError());
+  WAL_HIP(hipMemcpyAsync(s.h_res, s.res, 3 * sizeof(std::uint64_t), hipMemcpyDeviceToHost, st));
+  WAL_HIP(hipStreamSynchronize(st));
+  const std::uint64_t kstar = s.h_res[0];
+  std::uint64_t chain_end = s.h_res[1];
+  bool broke = s.h_res[2] != 0;
+  const bool partial = kstar < K;
+  if (partial) {
+    hipLaunchKernelGGL(wal_trim, dim3(blocks(K, 256)), dim3(256), 0, st, a, kstar);
+    std::uint8_t be = 0;
+    WAL_HIP(hipMemcpyAsync(s.h_res + 1, a.Xe + kstar, 8, hipMemcpyDeviceToHost, st));
+    WAL_HIP(hipMemcpyAsync(&be, a.Be + kstar, 1, hipMemcpyDeviceToHost, st));
+    WAL_HIP(hipStreamSynchronize(st));
+    chain_end = s.h_res[1];
+    broke = be != 0;
+  }
+  // 5: record numbering, the in-lane and batched CRC checks, the first bad record
+  std::size_t need = 0;
+  WAL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, a.cnt, a.base, K, st));
+  if (need > s.cub_bytes) {
+    WAL_HIP(hipStreamSynchronize(st));
+    WAL_HIP(hipFree(s.cub));
+    s.cub = nullptr;
+    s.cub_bytes = 0;
+    WAL_HIP(hipMalloc(&s.cub, need));
+    s.cub_bytes = need;
+  }
+  WAL_HIP(hipcub::DeviceScan::ExclusiveSum(s.cub, need, a.cnt, a.base, K, st));
+  WAL_HIP(hipMemcpyAsync(s.h_res + 5, a.base + (K - 1), 8, hipMemcpyDeviceToHost, st));
+  WAL_HIP(hipMemcpyAsync(s.h_res + 6, a.cnt + (K - 1), 8, hipMemcpyDeviceToHost, st));
+  WAL_HIP(hipStreamSynchronize(st));
+  const std::uint64_t tot = s.h_res[5] + s.h_res[6];  // (records << 32) | big records
+  const std::uint64_t n = tot >> 32, n_big = tot & 0xFFFFFFFFull;
+  std::uint64_t first = n;
+  if (n) {
+    if (int rc = grow_big(s, std::max<std::uint64_t>(n_big, 1))) return rc;
+    a = carve(s, w, size, K, tabs);
+    hipLaunchKernelGGL(wal_check, dim3(blocks(K, kCheckThreads)), dim3(kCheckThreads), 0, st, a);
+    WAL_HIP(hipGetLastError());
+    for (std::uint64_t i = 0; i < n_big; i += kWalCrcChunk) {
+      const std::uint64_t m = std::min(kWalCrcChunk, n_big - i);
+      if (int rc = batch_device_impl(kAlgoCrc32, w, a.big_off + i, a.big_len + i, nullptr, a.got + i, m, st)) return rc;
+    }
+    if (n_big) hipLaunchKernelGGL(wal_check_big, dim3(blocks(n_big, 256)), dim3(256), 0, st, a, n_big);
+    hipLaunchKernelGGL(wal_bad_pos, dim3(blocks(std::max<std::uint64_t>(K, n_big), 256)), dim3(256), 0, st, a, n_big);
+    WAL_HIP(hipGetLastError());
+    WAL_HIP(hipMemcpyAsync(s.h_res + 3, s.res + 3, 2 * sizeof(std::uint64_t), hipMemcpyDeviceToHost, st));
+    WAL_HIP(hipStreamSynchronize(st));
+    first = std::min<std::uint64_t>(s.h_res[3], n);
+  }
+  r->good = first;
+  r->corrupted = first < n || broke;
+  r->stop = first < n ? s.h_res[4] : chain_end;
+  r->resume = !r->corrupted && partial && chain_end < size;
+  return TKV_OK;
+}
+
+// The calling thread's device's scratch (created on first use, with its result words and the
+// init-term table).
+int scratch(WalScratch** out) {
+  int dev = 0;
+  WAL_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return set_error(TKV_INVALID_ARGUMENT, "device index out of range");
+  WalScratch* sp;
+  {
+    std::lock_guard<std::mutex> lk(g_wal_mu);
+    if (!g_wal[dev]) g_wal[dev] = new WalScratch();
+    sp = g_wal[dev];
+  }
+  std::lock_guard<std::mutex> lk(sp->mu);
+  if (!sp->res) {
+    WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->res), 8 * sizeof(std::uint64_t)));
+    WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&sp->h_res), 8 * sizeof(std::uint64_t), hipHostMallocDefault));
+    WAL_HIP(hipStreamCreateWithFlags(&sp->st, hipStreamNonBlocking));
+    std::vector<std::uint32_t> inj(kWalLaneMax + 1);
+    for (std::uint32_t L = 0; L <= kWalLaneMax; ++L) inj[L] = shift_bytes(kInit, L, kPoly);
+    WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->inj), inj.size() * 4));
+    WAL_HIP(hipMemcpy(sp->inj, inj.data(), inj.size() * 4, hipMemcpyHostToDevice));
+  }
+  *out = sp;
+  return TKV_OK;
+}
+
+int verify_locked(WalScratch& s, const std::uint8_t* d_wal, std::uint64_t size, std::uint64_t* n_good,
+                  std::uint64_t* stop_offset, hipStream_t st, bool* needs_host_walk) {
+  // Each pass checks the true chain at least through its first piece; a pass that stops short of
+  // the end without a verdict resumes at a true record start. Adversarial images that keep the
+  // speculation wrong go to the exact host walk after kMaxPasses.
+  constexpr int kMaxPasses = 8;
+  std::uint64_t start = 0, good = 0;
+  g_last[0] = g_last[1] = 0;
+  g_last[3] = (size + kWalPiece - 1) / kWalPiece;
+  for (int pass = 0; pass < kMaxPasses; ++pass) {
+    PassResult r;
+    g_last[0] = static_cast<std::uint64_t>(pass) + 1;
+    if (int rc = wal_pass(s, d_wal + start, size - start, st, &r)) return rc;
+    good += r.good;
+    if (!r.resume) {
+      *n_good = good;
+      *stop_offset = start + r.stop;
+      return r.corrupted ? set_error(TKV_CORRUPTED, "corrupted WAL record") : TKV_OK;
+    }
+    start += r.stop;
+  }
+  *needs_host_walk = true;
+  g_last[1] = 1;
+  return TKV_OK;
+}
+
+// memcpy of a large range into pinned staging on several host threads.
+void stage_copy(std::uint8_t* dst, const std::uint8_t* src, std::uint64_t n) {
+  const unsigned nt = n >= (std::uint64_t(16) << 20) ? 8u : 1u;
+  if (nt == 1) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([=] {
+      const std::uint64_t a = n * t / nt, e = n * (t + 1) / nt;
+      std::memcpy(dst + a, src + a, e - a);
+    });
+  for (auto& t : th) t.join();
+}
+
+constexpr std::uint64_t kStageSlab = std::uint64_t(64) << 20;
+
+}  // namespace
+
+int wal_verify_device_impl(const std::uint8_t* d_wal, std::uint64_t size, std::uint64_t* n_good,
+                           std::uint64_t* stop_offset, hipStream_t st, bool* needs_host_walk) {
+  *needs_host_walk = false;
+  *n_good = 0;
+  *stop_offset = 0;
+  g_last[0] = g_last[1] = g_last[2] = g_last[3] = 0;
+  if (size == 0) return TKV_OK;
+  if ((size + kWalPiece - 1) / kWalPiece >= 0xFFFFFFFFull)
+    return set_error(TKV_INVALID_ARGUMENT, "WAL image too large for the device walk");
+  WalScratch* sp = nullptr;
+  if (int rc = scratch(&sp)) return rc;
+  WalScratch& s = *sp;
+  std::lock_guard<std::mutex> lk(s.mu);
+  return verify_locked(s, d_wal, size, n_good, stop_offset, st, needs_host_walk);
+}
+
+int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
+                               std::uint64_t* stop_offset, bool* needs_host_walk) {
+  *needs_host_walk = false;
+  *n_good = 0;
+  *stop_offset = 0;
+  g_last[0] = g_last[1] = g_last[2] = g_last[3] = 0;
+  if (size == 0) return TKV_OK;
+  if ((size + kWalPiece - 1) / kWalPiece >= 0xFFFFFFFFull) {
+    *needs_host_walk = true;
+    return TKV_OK;
+  }
+  WalScratch* sp = nullptr;
+  if (int rc = scratch(&sp)) return rc;
+  WalScratch& s = *sp;
+  std::lock_guard<std::mutex> lk(s.mu);
+  g_last[2] = 1;
+  if (size > s.cap_img) {
+    (void)hipStreamSynchronize(s.st);
+    (void)hipFree(s.d_img);
+    s.d_img = nullptr;
+    s.cap_img = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&s.d_img), size) != hipSuccess) {
+      (void)hipGetLastError();  // the image does not fit the device: exact host walk instead
+      *needs_host_walk = true;
+      g_last[1] = 1;
+      return TKV_OK;
+    }
+    s.cap_img = size;
+  }
+  hipPointerAttribute_t attr;
+  const bool pinned = hipPointerGetAttributes(&attr, h_wal) == hipSuccess && attr.type == hipMemoryTypeHost;
+  if (!pinned) (void)hipGetLastError();
+  if (pinned) {
+    WAL_HIP(hipMemcpyAsync(s.d_img, h_wal, size, hipMemcpyHostToDevice, s.st));
+  } else {
+    // two pinned slabs: host threads fill one while the copy engine drains the other
+    for (int i = 0; i < 2; ++i) {
+      if (!s.slab[i]) {
+        WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.slab[i]), kStageSlab, hipHostMallocDefault));
+        WAL_HIP(hipEventCreateWithFlags(&s.slab_free[i], hipEventDisableTiming));
+      }
+    }
+    int k = 0;
+    for (std::uint64_t off = 0; off < size; off += kStageSlab, k ^= 1) {
+      const std::uint64_t m = std::min(kStageSlab, size - off);
+      WAL_HIP(hipEventSynchronize(s.slab_free[k]));
+      stage_copy(s.slab[k], h_wal + off, m);
+      WAL_HIP(hipMemcpyAsync(s.d_img + off, s.slab[k], m, hipMemcpyHostToDevice, s.st));
+      WAL_HIP(hipEventRecord(s.slab_free[k], s.st));
+    }
+  }
+  return verify_locked(s, s.d_img, size, n_good, stop_offset, s.st, needs_host_walk);
+}
+
+}  // namespace tkv
+
+extern "C" void tkv_debug_wal_last(uint64_t out[4]) {
+  for (int i = 0; i < 4; ++i) out[i] = tkv::g_last[i];
+}

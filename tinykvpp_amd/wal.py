@@ -7,9 +7,11 @@ Mirrors the CRC call sites of frankie::engine::wal_entry (/root/reference/src/en
   * decode (wal.cpp:63-130): eof on empty input; corrupted when fewer than 26 bytes remain, when
     record_len + 8 exceeds the input, on a CRC mismatch, or when key/value overflow the record.
 
-Here a whole slurped WAL (wal_reader::open, wal.cpp:204-240) is verified in ONE GPU batch after a
-host walk of the record_len chain (tkv_wal_verify), and many records are stamped in one batch
-(tkv_wal_stamp) — the recovery loop of engine::create (engine.cpp:31-53) and group commit.
+Here a whole slurped WAL (wal_reader::open, wal.cpp:204-240) is verified on the GPU: the image is
+copied to the device once, the record_len chain is walked there (speculative parallel walk with exact
+stitching) and every record's CRC is checked in ONE batch (tkv_wal_verify; tkv_wal_verify_device for
+an image already in HBM). Many records are stamped in one batch (tkv_wal_stamp) — the recovery loop
+of engine::create (engine.cpp:31-53) and group commit.
 """
 import ctypes
 import struct
@@ -53,10 +55,31 @@ def verify(wal_bytes):
     status is "ok" (every record verified, clean eof) or "corrupted" (first bad record at
     stop_offset, the position wal_entry::decode leaves the view parked on, wal_test.cpp:809-850).
     """
-    buf = np.frombuffer(bytes(wal_bytes), np.uint8)
+    if isinstance(wal_bytes, np.ndarray):
+        buf = np.ascontiguousarray(wal_bytes).reshape(-1).view(np.uint8)
+    else:
+        buf = np.frombuffer(wal_bytes, np.uint8)  # bytes / bytearray / memoryview: no copy
     good, stop = ctypes.c_uint64(0), ctypes.c_uint64(0)
     rc = load_library().tkv_wal_verify(ctypes.c_void_p(buf.ctypes.data) if buf.size else None, buf.size,
                                        ctypes.byref(good), ctypes.byref(stop))
+    if rc not in (OK, CORRUPTED):
+        check(rc)
+    return ("ok" if rc == OK else "corrupted"), good.value, stop.value
+
+
+def verify_device(image, size=None, stream=None):
+    """Verify a WAL image held in a uint8 CUDA tensor (first ``size`` bytes; default all).
+    Returns (status, n_good_records, stop_offset) as verify()."""
+    import torch
+    if image.dtype != torch.uint8 or not image.is_cuda or not image.is_contiguous():
+        raise ValueError("image must be a contiguous uint8 CUDA tensor")
+    n = image.numel() if size is None else int(size)
+    if n > image.numel():
+        raise ValueError("size exceeds the tensor")
+    st = torch.cuda.current_stream(image.device) if stream is None else stream
+    good, stop = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    rc = load_library().tkv_wal_verify_device(ctypes.c_void_p(image.data_ptr()), n, ctypes.byref(good),
+                                              ctypes.byref(stop), ctypes.c_void_p(st.cuda_stream))
     if rc not in (OK, CORRUPTED):
         check(rc)
     return ("ok" if rc == OK else "corrupted"), good.value, stop.value

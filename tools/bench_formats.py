@@ -2,7 +2,9 @@
 """Throughput of the SURVEY §8f rows on one MI355X (one JSON line each):
 
   wal_stamp    group commit: tkv_wal_stamp over N encoded records in host memory (wal.cpp:54-58)
-  wal_verify   recovery: tkv_wal_verify over the slurped WAL image (wal.cpp:63-130, engine.cpp:31-53)
+  wal_verify   recovery: tkv_wal_verify over the slurped WAL image (wal.cpp:63-130, engine.cpp:31-53):
+               image copied to HBM, chain walk + CRC batch on the device; also for an image already
+               in HBM (tkv_wal_verify_device) and for a 1 GiB WAL of 26-90 B records
   sst_stamp    tkv_sst_stamp_blocks over a host SSTable image of ~4 KiB data blocks
   sst_device   tkv_sst_block_crcs_device over the same images resident in HBM (kernel + fix-up)
   crc32c_cfg2  CRC-32C over 1 M x 4 KiB device-resident blocks (cfg2 shape)
@@ -126,6 +128,52 @@ emit("wal_verify_pinned", total, t, n_rec, {"records": n_rec, "verified": good.v
 t = timeit(lambda: tk.crc32_batch_host(wal_pin, poffs, plens))
 emit("wal_payload_batch_host_pinned", total, t, n_rec, {"what": "the CRC part of wal_verify_pinned alone"})
 del wal_pin, wal_pin_t
+
+# the same image already resident in HBM (tkv_wal_verify_device: walk + CRC batch + first-bad search)
+wal_dev = torch.from_numpy(wal).cuda()
+t = timeit(lambda: tk.wal.verify_device(wal_dev))
+assert tk.wal.verify_device(wal_dev) == ("ok", n_rec, total)
+emit("wal_verify_device", total, t, n_rec, {"records": n_rec, "source": "device-resident image"})
+del wal_dev
+
+# ---- WAL of small records (26-90 B: puts of short keys and values), 1 GiB: the walk dominates -----------
+sk = rng.integers(4, 24, 20_000_000).astype(np.uint32)
+sv = rng.integers(0, 40, 20_000_000).astype(np.uint32)
+ssz = 26 + sk + sv
+n_small = int(np.searchsorted(np.cumsum(ssz, dtype=np.uint64), np.uint64(1 << 30)))
+sk, sv, ssz = sk[:n_small], sv[:n_small], ssz[:n_small]
+soffs_w = np.concatenate([[0], np.cumsum(ssz[:-1], dtype=np.uint64)]).astype(np.uint64)
+stotal = int(ssz.sum())
+swal = rng.integers(0, 256, stotal, dtype=np.uint8)
+for col, vals in ((0, ssz - 8), (18, sk), (22, sv)):
+    for b in range(4):
+        swal[soffs_w.astype(np.int64) + col + b] = ((vals >> (8 * b)) & 0xFF).astype(np.uint8)
+for col in (8, 17):
+    swal[soffs_w.astype(np.int64) + col] = 0
+ssz32 = ssz.astype(np.uint32)
+tk.check(lib.tkv_wal_stamp(ctypes.c_void_p(swal.ctypes.data), ctypes.c_void_p(soffs_w.ctypes.data),
+                           ctypes.c_void_p(ssz32.ctypes.data), n_small))
+assert tk.wal.verify(swal) == ("ok", n_small, stotal)
+t = timeit(lambda: tk.wal.verify(swal), reps=3)
+emit("wal_verify_small_records", stotal, t, n_small, {"records": n_small, "mean_record_bytes": round(stotal / n_small, 1),
+                                                     "source": "pageable host image"})
+swal_pin_t = torch.from_numpy(swal).pin_memory()
+t = timeit(lambda: tk.wal.verify(swal_pin_t.numpy()), reps=3)
+emit("wal_verify_small_records_pinned", stotal, t, n_small, {"records": n_small, "source": "pinned host image"})
+del swal_pin_t
+swal_dev = torch.from_numpy(swal).cuda()
+assert tk.wal.verify_device(swal_dev) == ("ok", n_small, stotal)
+t = timeit(lambda: tk.wal.verify_device(swal_dev))
+emit("wal_verify_small_records_device", stotal, t, n_small, {"records": n_small, "source": "device-resident image"})
+# the previous design: record_len chain walked on host threads, CRCs in one GPU batch
+host_walk = []
+for k in range(1):
+    t0 = time.perf_counter()
+    cnt = lib.tkv_debug_wal_chain(ctypes.c_void_p(swal.ctypes.data), stotal, None, 0, None, None)
+    host_walk.append(time.perf_counter() - t0)
+emit("wal_small_records_host_chain_walk_only", stotal, float(np.median(host_walk)), int(cnt),
+     {"what": "tkv_debug_wal_chain: the host-thread walk alone (the exact fallback)"})
+del swal_dev, swal
 
 # ---- SSTable image: ~4 KiB data blocks -----------------------------------------------------------------
 nblk = 250_000
