@@ -9,22 +9,24 @@
 //     plausible header of every piece (one the reference encoder could have written,
 //     wal.cpp:19-61) becomes its speculative start S_k; piece 0 starts at 0.
 //  2. wal_spec: one lane per piece walks the chain from S_k over the records that start in the
-//     piece: X_k = the first record start at or past the piece's end (or the header that broke).
+//     piece (X_k = the first record start at or past the piece's end, or the header that broke),
+//     and checks them as it goes: key/value bounds, and the CRC of every payload of at most
+//     kWalLaneMax bytes folded by the lane itself (slicing-by-4 lookups into the engine's tables in
+//     LDS, the payload zero-padded in front to whole dwords). Larger records (at most two start in a
+//     piece) wait in the piece's slots for one CRC batch through the engine's irregular path.
 //  3. wal_jump: next(k) = the piece holding X_k. The true chain visits the pieces 0, next(0),
 //     next(next(0)), ...; pointer doubling marks exactly those pieces in log2(#pieces) rounds, and
 //     wal_link hands every on-path piece its entry E = X of its predecessor.
-//  4. wal_count: an on-path piece whose entry is its speculative start keeps its speculative walk;
-//     otherwise it walks again from E. Its speculative exit was right when the exact walk leaves at
-//     the same X (and breaks, or not, the same way). Entries are exact up to and including the
-//     first piece k* whose speculative exit was wrong (a corrupted record_len, or a fake header in a
-//     key or value that led the speculation astray): later pieces are dropped, and when no record up
-//     to k*'s exact exit fails, the next pass resumes there (a true record start) as a new image.
-//  5. wal_check: one exclusive scan gives every piece its first record index; each lane walks its
-//     piece again and checks every record of at most kWalLaneMax payload bytes itself (slicing-by-4
-//     lookups into the engine's LDS tables, the payload zero-padded in front to whole dwords). Larger
-//     records are listed for one CRC batch through the engine's irregular path (tkv_crc32_batch_device
-//     kernels) and checked by wal_check_big. The first bad record is an atomic minimum of record
-//     indices.
+//  4. wal_count: an on-path piece whose entry is its speculative start keeps its speculative walk
+//     and checks; otherwise it walks again from E (and wal_recheck checks it again). Its speculative
+//     exit was right when the exact walk leaves at the same X (and breaks, or not, the same way).
+//     Entries are exact up to and including the first piece k* whose speculative exit was wrong (a
+//     corrupted record_len, or a fake header in a key or value that led the speculation astray):
+//     later pieces are dropped, and when no record up to k*'s exact exit fails, the next pass
+//     resumes there (a true record start) as a new image.
+//  5. one exclusive scan numbers the records; wal_gather turns each piece's first failing record
+//     into a record index and moves the big-record slots into a dense list for the CRC batch;
+//     wal_check_big checks those. The first bad record is an atomic minimum of record indices.
 // Every step reads the image in HBM; the host only reads back a few counters.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -50,28 +52,36 @@ constexpr std::uint64_t kWalMeta = 26;        // wal.hpp:21-27 kMetadataSize
 constexpr std::uint32_t kWalLaneMax = 1024;   // payloads up to this size are checked by their lane
 constexpr std::uint64_t kNone = ~0ull;
 constexpr unsigned kScanThreads = 256;        // wal_scan: 16 positions per thread, 4 KiB per workgroup
-constexpr unsigned kCheckThreads = 1024;      // wal_check: one workgroup per CU (128 KiB of LDS tables)
+constexpr unsigned kCheckThreads = 1024;      // wal_spec/wal_recheck: one workgroup per CU (128 KiB of LDS)
 
 struct WalArgs {
   const std::uint8_t* w;
   std::uint64_t size;
   std::uint32_t K;           // pieces
-  std::uint64_t* S;          // speculative start of piece k (kNone: no plausible header)
+  // per piece
+  std::uint64_t* S;          // speculative start (kNone: no plausible header)
   std::uint64_t* X;          // exit of its speculative chain, or the start of the header that broke it
   std::uint64_t* spec_cnt;   // records of the speculative chain: (all << 32) | (larger than kWalLaneMax)
   std::uint32_t* next;       // piece of X (K: end of image, broken chain or no start)
   std::uint8_t* broke;       // the speculative chain hit a header that does not fit (at X)
+  std::uint64_t* first_loc;  // first failing record of the piece's checked walk (local index, kNone)
+  std::uint64_t* first_pos;  // and its start
+  std::uint64_t* slot_off;   // two slots per piece: records larger than kWalLaneMax (payload offset,
+  std::uint32_t* slot_len;   //   length, stored CRC, local index)
+  std::uint32_t* slot_crc;
+  std::uint32_t* slot_loc;
   std::uint32_t* Ja;         // pointer-doubling jump tables
   std::uint32_t* Jb;
   std::uint8_t* on;          // piece is on the true chain
+  std::uint8_t* recheck;     // entered off its speculative start: walked and checked again
   std::uint64_t* entry;      // true entry point of an on-path piece
   std::uint64_t* cnt;        // records of an on-path piece from its entry, packed as spec_cnt
   std::uint64_t* base;       // exclusive scan of cnt: first record index (high), first big record (low)
   std::uint64_t* Xe;         // exit of its exact walk from the entry (or the header that broke it)
   std::uint8_t* Be;          // the exact walk broke
-  std::uint64_t* bad_at;     // piece's first failing record: index, and its start in bad_pos
-  std::uint64_t* bad_pos;
-  std::uint64_t* big_off;    // records larger than kWalLaneMax: payload offset, length, index, stored CRC
+  std::uint64_t* bad_at;     // index of the piece's first failing record
+  // per big record (dense, in record order)
+  std::uint64_t* big_off;
   std::uint32_t* big_len;
   std::uint64_t* big_idx;
   std::uint32_t* big_crc;
@@ -80,7 +90,7 @@ struct WalArgs {
   const DeviceTables* tabs;
   std::uint64_t* res;        // [0] first piece with a wrong speculative exit, [1] chain end and
                              // [2] chain broke (from the path's last piece), [3] first bad record,
-                             // [4] its start, [5] records of the path up to k* (or all)
+                             // [4] its start, [5] pieces re-checked
 };
 
 // Little-endian u32 at byte p of the image, p + 4 <= size: dword loads aligned to the absolute
@@ -102,15 +112,26 @@ __device__ __forceinline__ std::uint64_t gid() {
 
 // 1. First plausible header per piece, one coalesced pass over the image. Thread t owns the 16
 // positions of the absolute 16-byte chunk t (relative positions 16t - off0 + j) and holds the 48
-// bytes [16t, 16t + 48) of its chunk in registers: a header at position p needs bytes p..p+25
-// (record_len, op/tombstone flags at p+8 and p+17, klen and vlen at p+18 and p+22; wal.cpp:30-52).
-// Chunks are read only when they hold image bytes. A wave covers 1 KiB, i.e. at most two pieces:
-// wave minimum per piece, one atomic per piece and wave.
-__global__ __launch_bounds__(kScanThreads) void wal_scan(WalArgs a) {
+// bytes [16t, 16t + 48) of its chunk in registers. A header at position p has its op and tombstone
+// bytes (p+8, p+17) at 0 or 1 (wal.cpp:30-52): both are tested for all 16 positions at once with
+// byte-parallel arithmetic on the registers, and only positions that pass get the full check
+// (record_len = 18 + klen + vlen, fitting the image; re-read through L1). Chunks are read only when
+// they hold image bytes. A wave covers 1 KiB, i.e. at most two pieces: wave minimum per piece, one
+// atomic per piece and wave.
+__device__ __forceinline__ std::uint32_t le1_bytes4(std::uint32_t d) {
+  // 4-bit mask: bit i set iff byte i of d is 0 or 1
+  const std::uint32_t x = d & 0xFEFEFEFEu;
+  const std::uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu) & 0x80808080u;
+  return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+
+// Positions [plo, phi) only (pieces [plo, phi) / kWalPiece; t0, the first chunk, a multiple of 64).
+__global__ __launch_bounds__(kScanThreads) void wal_scan(WalArgs a, std::uint64_t t0, std::uint64_t plo,
+                                                          std::uint64_t phi) {
   const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
   const std::uintptr_t al = w0 & ~static_cast<std::uintptr_t>(15);
   const std::uint64_t off0 = w0 - al;
-  const std::uint64_t t = gid();
+  const std::uint64_t t = t0 + gid();
   const std::uintptr_t c0 = al + 16 * t;  // this thread's chunk
   const std::uintptr_t end = w0 + a.size;
   std::uint32_t dw[12];
@@ -124,20 +145,28 @@ __global__ __launch_bounds__(kScanThreads) void wal_scan(WalArgs a) {
     dw[4 * c + 2] = v.z;
     dw[4 * c + 3] = v.w;
   }
-  auto byte = [&](int o) { return (dw[o >> 2] >> (8 * (o & 3))) & 0xFFu; };
-  auto u32at = [&](int o) { return (o & 3) ? __builtin_amdgcn_alignbyte(dw[(o >> 2) + 1], dw[o >> 2], o & 3) : dw[o >> 2]; };
-  const std::int64_t p0 = static_cast<std::int64_t>(16 * t) - static_cast<std::int64_t>(off0);
-  std::uint64_t best = kNone;
+  // bit b of M: byte 8 + b of the window is 0 or 1 (b < 28)
+  std::uint32_t M = 0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const std::int64_t p = p0 + j;
-    if (p >= 0 && static_cast<std::uint64_t>(p) < a.size && a.size - static_cast<std::uint64_t>(p) >= kWalMeta &&
-        byte(j + 8) <= 1u && byte(j + 17) <= 1u) {
-      const std::uint64_t rlen = u32at(j), klen = u32at(j + 18), vlen = u32at(j + 22);
-      if (rlen == 18u + klen + vlen && rlen + 8 <= a.size - static_cast<std::uint64_t>(p) &&
-          best == kNone)
-        best = static_cast<std::uint64_t>(p);
+  for (int i = 2; i < 9; ++i) M |= le1_bytes4(dw[i]) << (4 * (i - 2));
+  std::uint32_t cand = M & (M >> 9) & 0xFFFFu;  // bit j: bytes j+8 and j+17 are 0/1
+  // positions inside the image with a full header left
+  const std::int64_t p0 = static_cast<std::int64_t>(16 * t) - static_cast<std::int64_t>(off0);
+  const std::int64_t last = std::min<std::int64_t>(static_cast<std::int64_t>(a.size) - static_cast<std::int64_t>(kWalMeta),
+                                                    static_cast<std::int64_t>(phi) - 1);
+  const std::int64_t lo = static_cast<std::int64_t>(plo) - p0, hi = last - p0;
+  for (int j = 0; j < 16; ++j)
+    if (j < lo || j > hi) cand &= ~(1u << j);
+  std::uint64_t best = kNone;
+  while (cand) {
+    const int j = __builtin_ctz(cand);
+    const std::uint64_t p = static_cast<std::uint64_t>(p0 + j);
+    const std::uint64_t rlen = ld32(a.w, p, a.size), klen = ld32(a.w, p + 18, a.size), vlen = ld32(a.w, p + 22, a.size);
+    if (rlen == 18u + klen + vlen && rlen + 8 <= a.size - p) {
+      best = p;
+      break;
     }
+    cand &= cand - 1;
   }
   // the wave's positions span pieces pa and pa + 1
   const std::int64_t wave_p0 = static_cast<std::int64_t>(16 * (t & ~63ull)) - static_cast<std::int64_t>(off0);
@@ -156,11 +185,116 @@ __global__ __launch_bounds__(kScanThreads) void wal_scan(WalArgs a) {
   }
 }
 
-// 2. Speculative walk of one piece from its first plausible header (piece 0 from 0). Counts the
-// chain's records (all, and those too large to check in-lane) for wal_count to reuse.
-__global__ void wal_spec(WalArgs a) {
-  const std::uint64_t k = gid();
-  if (k >= a.K) return;
+// CRC-32 (finalized) of the payload [q, q + L) in image bytes, L <= kWalLaneMax, folded by this
+// lane alone: the payload is zero-padded in front to whole dwords (leading zeros leave an init-0
+// register at 0) and folded with slicing-by-4 lookups into the LDS tables; the init register enters
+// as inj[L] = Shift_L(0xFFFFFFFF) (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). Dwords are read aligned to
+// the absolute address and realigned with v_alignbyte, four at a time with the next four already in
+// flight (the fold chain hides their latency); no dword past the payload's last one is read.
+__device__ __forceinline__ std::uint32_t lane_crc(const std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
+                                                  std::uint64_t q, std::uint32_t L) {
+  const std::uint32_t z = (4u - (L & 3u)) & 3u;  // zero bytes in front
+  const std::uintptr_t s = reinterpret_cast<std::uintptr_t>(a.w) + q - z;
+  const std::uint32_t t = static_cast<std::uint32_t>(s & 3u);
+  const std::uintptr_t al = s - t;
+  const std::uint32_t n = (z + L) >> 2;               // dwords to fold
+  const std::uint32_t mlast = t ? n : (n ? n - 1 : 0);  // last aligned dword read
+  auto R = [&](std::uint32_t m) { return *reinterpret_cast<const std::uint32_t*>(al + 4u * (m < mlast ? m : mlast)); };
+  dev::Reg r{0, 0};
+  std::uint32_t w[5] = {R(0), R(1), R(2), R(3), R(4)};  // aligned dwords j .. j+4
+  std::uint32_t j = 0;
+  std::uint32_t head = static_cast<std::uint32_t>(0xFFFFFFFFull << (8 * z));  // first dword: zeros in front
+  for (; j + 4 <= n; j += 4) {
+    const std::uint32_t f0 = R(j + 5), f1 = R(j + 6), f2 = R(j + 7), f3 = R(j + 8);  // next group in flight
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      std::uint32_t d = t ? __builtin_amdgcn_alignbyte(w[i + 1], w[i], t) : w[i];
+      dev::slice4(lds, r, d & head, kc);
+      head = 0xFFFFFFFFu;
+    }
+    w[0] = w[4];
+    w[1] = f0;
+    w[2] = f1;
+    w[3] = f2;
+    w[4] = f3;
+  }
+  for (std::uint32_t i = 0; j < n; ++j, ++i) {  // the last 0-3 dwords (w[] holds them)
+    const std::uint32_t lo = i == 0 ? w[0] : i == 1 ? w[1] : w[2];
+    const std::uint32_t hi = i == 0 ? w[1] : i == 1 ? w[2] : w[3];
+    const std::uint32_t d = t ? __builtin_amdgcn_alignbyte(hi, lo, t) : lo;
+    dev::slice4(lds, r, d & head, kc);
+    head = 0xFFFFFFFFu;
+  }
+  return r.value() ^ a.inj[L] ^ 0xFFFFFFFFu;
+}
+
+// Slicing tables into LDS (the row kernels' lane-shift tables are not needed here).
+__device__ __forceinline__ void fill_slices(const DeviceTables* tabs, std::uint32_t* lds) {
+  for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
+    const std::uint32_t pair = u >> 9, e = (u >> 1) & 255u, tt = u & 1u;
+    const std::uint32_t v = tabs->slice[2 * pair + tt][e];
+    uint4* dst = reinterpret_cast<uint4*>(lds + pair * 16384u + e * 64u + tt * 32u);
+#pragma unroll
+    for (std::uint32_t k = 0; k < 8u; ++k) dst[(k + u) & 7u] = make_uint4(v, v, v, v);
+  }
+  __syncthreads();
+}
+
+// Walk piece k from `start` over the records that start in the piece (wal.cpp:63-87: header size,
+// then record_len against what is left) and check each one: key/value bounds (wal.cpp:118-121) and,
+// for payloads up to kWalLaneMax bytes, the CRC (wal.cpp:89-96) in this lane. Larger records (at most
+// two start in a piece) are kept in the piece's two slots for the CRC batch. Writes the piece's exit,
+// break, counts, first failing record (local index) and slots.
+__device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
+                                           std::uint64_t k, std::uint64_t start, std::uint64_t* exit_out,
+                                           std::uint8_t* broke_out, std::uint64_t* cnt_out) {
+  const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
+  std::uint64_t p = start, n_all = 0, n_big = 0, first = kNone, first_pos = 0;
+  bool bad_hdr = false;
+  while (p < limit) {
+    if (a.size - p < kWalMeta) {
+      bad_hdr = true;
+      break;
+    }
+    const std::uint32_t rlen = ld32(a.w, p, a.size);
+    if (static_cast<std::uint64_t>(rlen) + 8 > a.size - p) {
+      bad_hdr = true;
+      break;
+    }
+    const std::uint32_t stored = ld32(a.w, p + 4, a.size);
+    const std::uint64_t klen = ld32(a.w, p + 18, a.size), vlen = ld32(a.w, p + 22, a.size);
+    bool bad = kWalMeta + klen + vlen > 8ull + rlen;
+    if (rlen <= kWalLaneMax) {
+      bad = bad || lane_crc(lds, kc, a, p + 8, rlen) != stored;
+    } else {
+      const std::uint64_t sl = 2 * k + (n_big & 1u);
+      a.slot_off[sl] = p + 8;
+      a.slot_len[sl] = rlen;
+      a.slot_crc[sl] = stored;
+      a.slot_loc[sl] = static_cast<std::uint32_t>(n_all);
+      ++n_big;
+    }
+    if (bad && first == kNone) {
+      first = n_all;
+      first_pos = p;
+    }
+    ++n_all;
+    p += 8 + static_cast<std::uint64_t>(rlen);
+  }
+  *exit_out = p;
+  *broke_out = bad_hdr ? 1 : 0;
+  *cnt_out = (n_all << 32) | n_big;
+  a.first_loc[k] = first;
+  a.first_pos[k] = first_pos;
+}
+
+// 2. Speculative walk and check of pieces [k_lo, k_hi) from their first plausible header (piece 0
+// from 0).
+__global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  fill_slices(a.tabs, lds);
+  const std::uint64_t k = k_lo + gid();
+  if (k >= k_hi) return;
   const std::uint64_t s = k == 0 ? 0 : a.S[k];
   if (k == 0) a.S[0] = 0;
   if (s == kNone) {
@@ -168,29 +302,17 @@ __global__ void wal_spec(WalArgs a) {
     a.next[k] = a.K;
     a.broke[k] = 0;
     a.spec_cnt[k] = 0;
+    a.first_loc[k] = kNone;
     return;
   }
-  const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
-  std::uint64_t p = s, n_all = 0, n_big = 0;
-  bool bad = false;
-  while (p < limit) {  // wal.cpp:63-87: header size, then record_len against what is left
-    if (a.size - p < kWalMeta) {
-      bad = true;
-      break;
-    }
-    const std::uint64_t rlen = ld32(a.w, p, a.size);
-    if (rlen + 8 > a.size - p) {
-      bad = true;
-      break;
-    }
-    ++n_all;
-    n_big += rlen > kWalLaneMax ? 1u : 0u;
-    p += 8 + rlen;
-  }
-  a.X[k] = p;
-  a.broke[k] = bad ? 1 : 0;
-  a.spec_cnt[k] = (n_all << 32) | n_big;
-  a.next[k] = (bad || p >= a.size) ? a.K : static_cast<std::uint32_t>(p / kWalPiece);
+  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
+  std::uint64_t x, c;
+  std::uint8_t br;
+  walk_check(lds, kc, a, k, s, &x, &br, &c);
+  a.X[k] = x;
+  a.broke[k] = br;
+  a.spec_cnt[k] = c;
+  a.next[k] = (br || x >= a.size) ? a.K : static_cast<std::uint32_t>(x / kWalPiece);
 }
 
 __global__ void wal_jump_init(WalArgs a) {
@@ -198,6 +320,7 @@ __global__ void wal_jump_init(WalArgs a) {
   if (k >= a.K) return;
   a.Ja[k] = a.next[k];
   a.on[k] = k == 0 ? 1 : 0;
+  a.recheck[k] = 0;
   a.bad_at[k] = kNone;
 }
 
@@ -221,9 +344,9 @@ __global__ void wal_link(WalArgs a) {
   if (n < a.K) a.entry[n] = a.X[k];
 }
 
-// 4. Records of an on-path piece from its entry (the speculative walk's when it started there, an
-// exact walk otherwise): count, exit, break. res[0] = the first piece whose speculative exit was
-// wrong. Off-path pieces count 0.
+// 4. Records of an on-path piece from its entry: the speculative walk's when it started there;
+// otherwise an exact walk (the records are checked again by wal_recheck). res[0] = the first piece
+// whose speculative exit was wrong; res[5] counts re-checked pieces. Off-path pieces count 0.
 __global__ void wal_count(WalArgs a) {
   const std::uint64_t k = gid();
   if (k >= a.K) return;
@@ -258,6 +381,8 @@ __global__ void wal_count(WalArgs a) {
       p += 8 + rlen;
     }
     packed = (n_all << 32) | n_big;
+    a.recheck[k] = 1;
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.res[5]), 1ull);
     if (p != a.X[k] || bad != (a.broke[k] != 0)) atomicMin(reinterpret_cast<unsigned long long*>(&a.res[0]), k);
   }
   a.cnt[k] = packed;
@@ -269,6 +394,18 @@ __global__ void wal_count(WalArgs a) {
   }
 }
 
+// Pieces entered off their speculative start: check their records from the true entry.
+__global__ __launch_bounds__(kCheckThreads) void wal_recheck(WalArgs a) {
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  fill_slices(a.tabs, lds);
+  const std::uint64_t k = gid();
+  if (k >= a.K || !a.recheck[k]) return;
+  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
+  std::uint64_t x, c;
+  std::uint8_t br;
+  walk_check(lds, kc, a, k, a.entry[k], &x, &br, &c);
+}
+
 // Records past the first piece with a wrong speculative exit are not on the true chain (or not
 // known to be): drop them.
 __global__ void wal_trim(WalArgs a, std::uint64_t kstar) {
@@ -276,76 +413,23 @@ __global__ void wal_trim(WalArgs a, std::uint64_t kstar) {
   if (k < a.K && k > kstar) a.cnt[k] = 0;
 }
 
-// CRC-32 (finalized) of the payload [q, q + L) in image bytes, L <= kWalLaneMax, folded by this
-// lane alone: the payload is zero-padded in front to whole dwords (leading zeros leave an init-0
-// register at 0) and folded with slicing-by-4 lookups into the LDS tables; the init register enters
-// as inj[L] = Shift_L(0xFFFFFFFF) (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). Dwords are read aligned to
-// the absolute address and realigned with v_alignbyte; no dword past the payload's last one is read.
-__device__ __forceinline__ std::uint32_t lane_crc(const std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
-                                                  std::uint64_t q, std::uint32_t L) {
-  const std::uint32_t z = (4u - (L & 3u)) & 3u;  // zero bytes in front
-  const std::uintptr_t s = reinterpret_cast<std::uintptr_t>(a.w) + q - z;
-  const std::uint32_t t = static_cast<std::uint32_t>(s & 3u);
-  const std::uintptr_t al = s - t;
-  const std::uint32_t n = (z + L) >> 2;
-  dev::Reg r{0, 0};
-  std::uint32_t lo = n ? *reinterpret_cast<const std::uint32_t*>(al) : 0u;
-  for (std::uint32_t j = 0; j < n; ++j) {
-    // next aligned dword: needed for the realignment (t != 0) or as the next dword (t == 0)
-    const bool more = t != 0 || j + 1 < n;
-    const std::uint32_t hi = more ? *reinterpret_cast<const std::uint32_t*>(al + 4u * (j + 1)) : 0u;
-    std::uint32_t d = t ? __builtin_amdgcn_alignbyte(hi, lo, t) : lo;
-    if (j == 0) d &= static_cast<std::uint32_t>(0xFFFFFFFFull << (8 * z));
-    dev::slice4(lds, r, d, kc);
-    lo = hi;
-  }
-  return r.value() ^ a.inj[L] ^ 0xFFFFFFFFu;
-}
-
-// 5. Every record of an on-path piece (up to k*), in chain order: key/value bounds, and the CRC of
-// payloads up to kWalLaneMax bytes checked by the lane itself; larger records go to the big list.
-// The piece's first failing record is kept for the position lookup.
-__global__ __launch_bounds__(kCheckThreads) void wal_check(WalArgs a) {
-  __shared__ std::uint32_t lds[kLdsSliceWords];
-  // slicing tables only (the lane shifts of the row kernels are not needed here)
-  for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
-    const std::uint32_t pair = u >> 9, e = (u >> 1) & 255u, tt = u & 1u;
-    const std::uint32_t v = a.tabs->slice[2 * pair + tt][e];
-    uint4* dst = reinterpret_cast<uint4*>(lds + pair * 16384u + e * 64u + tt * 32u);
-#pragma unroll
-    for (std::uint32_t k = 0; k < 8u; ++k) dst[(k + u) & 7u] = make_uint4(v, v, v, v);
-  }
-  __syncthreads();
+// 5. Record numbering: the first failing record of each counted piece becomes a record index, and
+// the big-record slots move to the dense list the CRC batch reads.
+__global__ void wal_gather(WalArgs a) {
   const std::uint64_t k = gid();
-  if (k >= a.K || !a.on[k] || a.cnt[k] == 0) return;
-  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
-  const std::uint64_t n_all = a.cnt[k] >> 32;
-  std::uint64_t idx = a.base[k] >> 32, bi = a.base[k] & 0xFFFFFFFFull, p = a.entry[k];
-  std::uint64_t first = kNone, first_pos = 0;
-  for (std::uint64_t i = 0; i < n_all; ++i, ++idx) {
-    const std::uint32_t rlen = ld32(a.w, p, a.size);
-    const std::uint32_t stored = ld32(a.w, p + 4, a.size);
-    const std::uint64_t klen = ld32(a.w, p + 18, a.size), vlen = ld32(a.w, p + 22, a.size);
-    bool bad = kWalMeta + klen + vlen > 8ull + rlen;  // wal.cpp:118-121
-    if (rlen <= kWalLaneMax) {
-      bad = bad || lane_crc(lds, kc, a, p + 8, rlen) != stored;  // wal.cpp:89-96
-    } else {
-      a.big_off[bi] = p + 8;
-      a.big_len[bi] = rlen;
-      a.big_idx[bi] = idx;
-      a.big_crc[bi] = stored;
-      ++bi;
-    }
-    if (bad && first == kNone) {
-      first = idx;
-      first_pos = p;
-    }
-    p += 8 + static_cast<std::uint64_t>(rlen);
+  if (k >= a.K || a.cnt[k] == 0) return;
+  const std::uint64_t b_all = a.base[k] >> 32, b_big = a.base[k] & 0xFFFFFFFFull;
+  const std::uint64_t n_big = a.cnt[k] & 0xFFFFFFFFull;
+  if (a.first_loc[k] != kNone) {
+    a.bad_at[k] = b_all + a.first_loc[k];
+    atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), b_all + a.first_loc[k]);
   }
-  if (first != kNone) {
-    a.bad_at[k] = first;
-    a.bad_pos[k] = first_pos;
-    atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), first);
+  for (std::uint64_t j = 0; j < n_big; ++j) {
+    const std::uint64_t sl = 2 * k + j;
+    a.big_off[b_big + j] = a.slot_off[sl];
+    a.big_len[b_big + j] = a.slot_len[sl];
+    a.big_crc[b_big + j] = a.slot_crc[sl];
+    a.big_idx[b_big + j] = b_all + a.slot_loc[sl];
   }
 }
 
@@ -358,7 +442,7 @@ __global__ void wal_check_big(WalArgs a, std::uint64_t n) {
 __global__ void wal_bad_pos(WalArgs a, std::uint64_t n_big) {
   const std::uint64_t i = gid();
   const std::uint64_t want = a.res[3];
-  if (i < a.K && a.bad_at[i] == want) a.res[4] = a.bad_pos[i];
+  if (i < a.K && a.cnt[i] != 0 && a.bad_at[i] == want) a.res[4] = a.first_pos[i];
   if (i < n_big && a.big_idx[i] == want) a.res[4] = a.big_off[i] - 8;
 }
 
@@ -366,7 +450,7 @@ __global__ void wal_bad_pos(WalArgs a, std::uint64_t n_big) {
 struct WalScratch {
   std::mutex mu;
   std::uint64_t cap_pieces = 0, cap_big = 0;
-  void* pieces = nullptr;  // per piece: 10 u64, 3 u32, 3 u8 (carve)
+  void* pieces = nullptr;  // per piece: 13 u64, 9 u32, 4 u8 (carve)
   void* bigs = nullptr;    // per big record: 2 u64, 3 u32
   void* cub = nullptr;
   std::size_t cub_bytes = 0;
@@ -378,9 +462,15 @@ struct WalScratch {
   std::uint64_t cap_img = 0;
   std::uint8_t* slab[2] = {nullptr, nullptr};
   hipEvent_t slab_free[2] = {nullptr, nullptr};
-  hipStream_t st = nullptr;
+  hipEvent_t landed[2] = {nullptr, nullptr};  // copy of a chunk done (copy stream -> compute stream)
+  hipStream_t st = nullptr;   // copies of host images
+  hipStream_t stc = nullptr;  // device work on host images (overlaps the copies)
   ~WalScratch() {
     if (st) (void)hipStreamSynchronize(st);
+    if (stc) (void)hipStreamSynchronize(stc);
+    for (int i = 0; i < 2; ++i)
+      if (landed[i]) (void)hipEventDestroy(landed[i]);
+    if (stc) (void)hipStreamDestroy(stc);
     (void)hipFree(d_img);
     for (int i = 0; i < 2; ++i) {
       (void)hipHostFree(slab[i]);
@@ -414,7 +504,7 @@ int grow_pieces(WalScratch& s, std::uint64_t K) {
   WAL_HIP(hipFree(s.pieces));
   s.pieces = nullptr;
   s.cap_pieces = 0;
-  WAL_HIP(hipMalloc(&s.pieces, cap * (10 * 8 + 3 * 4 + 3)));
+  WAL_HIP(hipMalloc(&s.pieces, cap * (13 * 8 + 9 * 4 + 4)));
   s.cap_pieces = cap;
   return TKV_OK;
 }
@@ -437,16 +527,22 @@ WalArgs carve(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std::uin
   a.K = K;
   const std::uint64_t C = s.cap_pieces;
   auto* p8 = static_cast<std::uint64_t*>(s.pieces);
-  std::uint64_t** u64s[] = {&a.S, &a.X, &a.spec_cnt, &a.entry, &a.cnt, &a.base, &a.Xe, &a.bad_at, &a.bad_pos};
+  std::uint64_t** u64s[] = {&a.S, &a.X, &a.spec_cnt, &a.first_loc, &a.first_pos, &a.entry, &a.cnt, &a.base, &a.Xe,
+                            &a.bad_at};
   for (std::size_t i = 0; i < sizeof(u64s) / sizeof(u64s[0]); ++i) *u64s[i] = p8 + i * C;
-  auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 10 * C);
+  a.slot_off = p8 + 10 * C;  // 2C
+  auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 13 * C);
   a.next = p4;
   a.Ja = p4 + C;
   a.Jb = p4 + 2 * C;
-  auto* p1 = reinterpret_cast<std::uint8_t*>(p4 + 3 * C);
+  a.slot_len = p4 + 3 * C;  // 2C each
+  a.slot_crc = p4 + 5 * C;
+  a.slot_loc = p4 + 7 * C;
+  auto* p1 = reinterpret_cast<std::uint8_t*>(p4 + 9 * C);
   a.broke = p1;
   a.on = p1 + C;
   a.Be = p1 + 2 * C;
+  a.recheck = p1 + 3 * C;
   const std::uint64_t B = s.cap_big;
   if (B) {
     auto* b8 = static_cast<std::uint64_t*>(s.bigs);
@@ -475,8 +571,10 @@ struct PassResult {
   bool resume = false;     // the chain continues at `stop` (a true record start) beyond what was checked
 };
 
-// One pass over the image [w, w + size), which starts with a record (or is empty).
-int wal_pass(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream_t st, PassResult* r) {
+// A pass over the image [w, w + size), which starts with a record (or is empty), in three parts:
+// pass_begin (result words, speculative starts cleared), pass_front over ranges of pieces (scan and
+// speculative walk; each range's bytes and the next 1 KiB + 26 bytes must be resident), pass_tail.
+int pass_begin(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream_t st, WalArgs* out) {
   const std::uint32_t K = static_cast<std::uint32_t>((size + kWalPiece - 1) / kWalPiece);
   const DeviceTables* tabs = device_tables(kAlgoCrc32);
   if (!tabs) return TKV_IO_ERROR;
@@ -487,14 +585,30 @@ int wal_pass(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream
   s.h_res[2] = 0;
   s.h_res[3] = kNone;
   s.h_res[4] = 0;
-  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 5 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
+  s.h_res[5] = 0;
+  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 6 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
   WAL_HIP(hipMemsetAsync(a.S, 0xFF, K * sizeof(std::uint64_t), st));
+  *out = a;
+  return TKV_OK;
+}
 
-  // 1-3: speculative starts and walks, the pieces on the true chain, their entries
-  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(w);
-  const std::uint64_t chunks = ((w0 & 15u) + size + 15) / 16;
-  hipLaunchKernelGGL(wal_scan, dim3(blocks(chunks, kScanThreads)), dim3(kScanThreads), 0, st, a);
-  hipLaunchKernelGGL(wal_spec, dim3(blocks(K, 256)), dim3(256), 0, st, a);
+void pass_front(const WalArgs& a, std::uint64_t k_lo, std::uint64_t k_hi, hipStream_t st) {
+  if (k_hi <= k_lo) return;
+  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
+  const std::uint64_t off0 = w0 & 15u;
+  const std::uint64_t plo = k_lo * kWalPiece, phi = std::min<std::uint64_t>(k_hi * kWalPiece, a.size);
+  const std::uint64_t t0 = ((plo + off0) / 16) & ~63ull;  // whole waves (the kernel's piece arithmetic)
+  const std::uint64_t t1 = (phi + off0 + 15) / 16;
+  hipLaunchKernelGGL(wal_scan, dim3(blocks(t1 - t0, kScanThreads)), dim3(kScanThreads), 0, st, a, t0, plo, phi);
+  hipLaunchKernelGGL(wal_spec, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
+}
+
+int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
+  const std::uint8_t* w = a.w;
+  const std::uint64_t size = a.size;
+  const std::uint32_t K = a.K;
+  const DeviceTables* tabs = a.tabs;
+  // 3: the pieces on the true chain and their entries
   hipLaunchKernelGGL(wal_jump_init, dim3(blocks(K, 256)), dim3(256), 0, st, a);
   std::uint32_t* J = a.Ja;
   std::uint32_t* J2 = a.Jb;
@@ -506,12 +620,13 @@ int wal_pass(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream
   // 4: record counts from the entries
   hipLaunchKernelGGL(wal_count, dim3(blocks(K, 256)), dim3(256), 0, st, a);
   WAL_HIP(hipGetLastError());
-  WAL_HIP(hipMemcpyAsync(s.h_res, s.res, 3 * sizeof(std::uint64_t), hipMemcpyDeviceToHost, st));
+  WAL_HIP(hipMemcpyAsync(s.h_res, s.res, 6 * sizeof(std::uint64_t), hipMemcpyDeviceToHost, st));
   WAL_HIP(hipStreamSynchronize(st));
   const std::uint64_t kstar = s.h_res[0];
   std::uint64_t chain_end = s.h_res[1];
   bool broke = s.h_res[2] != 0;
   const bool partial = kstar < K;
+  if (s.h_res[5]) hipLaunchKernelGGL(wal_recheck, dim3(blocks(K, kCheckThreads)), dim3(kCheckThreads), 0, st, a);
   if (partial) {
     hipLaunchKernelGGL(wal_trim, dim3(blocks(K, 256)), dim3(256), 0, st, a, kstar);
     std::uint8_t be = 0;
@@ -521,7 +636,7 @@ int wal_pass(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream
     chain_end = s.h_res[1];
     broke = be != 0;
   }
-  // 5: record numbering, the in-lane and batched CRC checks, the first bad record
+  // 5: record numbering, first failing in-lane record, the CRC batch of the big ones
   std::size_t need = 0;
   WAL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, a.cnt, a.base, K, st));
   if (need > s.cub_bytes) {
@@ -542,7 +657,7 @@ int wal_pass(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream
   if (n) {
     if (int rc = grow_big(s, std::max<std::uint64_t>(n_big, 1))) return rc;
     a = carve(s, w, size, K, tabs);
-    hipLaunchKernelGGL(wal_check, dim3(blocks(K, kCheckThreads)), dim3(kCheckThreads), 0, st, a);
+    hipLaunchKernelGGL(wal_gather, dim3(blocks(K, 256)), dim3(256), 0, st, a);
     WAL_HIP(hipGetLastError());
     for (std::uint64_t i = 0; i < n_big; i += kWalCrcChunk) {
       const std::uint64_t m = std::min(kWalCrcChunk, n_big - i);
@@ -562,6 +677,14 @@ int wal_pass(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream
   return TKV_OK;
 }
 
+// A whole pass over a resident image.
+int wal_pass(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream_t st, PassResult* r) {
+  WalArgs a;
+  if (int rc = pass_begin(s, w, size, st, &a)) return rc;
+  pass_front(a, 0, a.K, st);
+  return pass_tail(s, a, st, r);
+}
+
 // The calling thread's device's scratch (created on first use, with its result words and the
 // init-term table).
 int scratch(WalScratch** out) {
@@ -579,6 +702,8 @@ int scratch(WalScratch** out) {
     WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->res), 8 * sizeof(std::uint64_t)));
     WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&sp->h_res), 8 * sizeof(std::uint64_t), hipHostMallocDefault));
     WAL_HIP(hipStreamCreateWithFlags(&sp->st, hipStreamNonBlocking));
+    WAL_HIP(hipStreamCreateWithFlags(&sp->stc, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) WAL_HIP(hipEventCreateWithFlags(&sp->landed[i], hipEventDisableTiming));
     std::vector<std::uint32_t> inj(kWalLaneMax + 1);
     for (std::uint32_t L = 0; L <= kWalLaneMax; ++L) inj[L] = shift_bytes(kInit, L, kPoly);
     WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->inj), inj.size() * 4));
@@ -589,7 +714,8 @@ int scratch(WalScratch** out) {
 }
 
 int verify_locked(WalScratch& s, const std::uint8_t* d_wal, std::uint64_t size, std::uint64_t* n_good,
-                  std::uint64_t* stop_offset, hipStream_t st, bool* needs_host_walk) {
+                  std::uint64_t* stop_offset, hipStream_t st, bool* needs_host_walk,
+                  const PassResult* first_pass = nullptr) {
   // Each pass checks the true chain at least through its first piece; a pass that stops short of
   // the end without a verdict resumes at a true record start. Adversarial images that keep the
   // speculation wrong go to the exact host walk after kMaxPasses.
@@ -600,7 +726,8 @@ int verify_locked(WalScratch& s, const std::uint8_t* d_wal, std::uint64_t size, 
   for (int pass = 0; pass < kMaxPasses; ++pass) {
     PassResult r;
     g_last[0] = static_cast<std::uint64_t>(pass) + 1;
-    if (int rc = wal_pass(s, d_wal + start, size - start, st, &r)) return rc;
+    if (pass == 0 && first_pass) r = *first_pass;
+    else if (int rc = wal_pass(s, d_wal + start, size - start, st, &r)) return rc;
     good += r.good;
     if (!r.resume) {
       *n_good = good;
@@ -682,26 +809,48 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
   hipPointerAttribute_t attr;
   const bool pinned = hipPointerGetAttributes(&attr, h_wal) == hipSuccess && attr.type == hipMemoryTypeHost;
   if (!pinned) (void)hipGetLastError();
-  if (pinned) {
-    WAL_HIP(hipMemcpyAsync(s.d_img, h_wal, size, hipMemcpyHostToDevice, s.st));
-  } else {
-    // two pinned slabs: host threads fill one while the copy engine drains the other
+  if (!pinned) {
     for (int i = 0; i < 2; ++i) {
       if (!s.slab[i]) {
         WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.slab[i]), kStageSlab, hipHostMallocDefault));
         WAL_HIP(hipEventCreateWithFlags(&s.slab_free[i], hipEventDisableTiming));
       }
     }
-    int k = 0;
-    for (std::uint64_t off = 0; off < size; off += kStageSlab, k ^= 1) {
-      const std::uint64_t m = std::min(kStageSlab, size - off);
+  }
+  // The image goes over in chunks on the copy stream (pageable sources through two pinned slabs that
+  // host threads fill while the copy engine drains the other). As each chunk lands, the compute
+  // stream scans and speculatively walks the pieces before it whose records' bytes are all resident
+  // (pieces ending at least kFrontMargin bytes before the end of what has landed), so only the last
+  // chunk's pieces and the stitching remain once the copy is done.
+  constexpr std::uint64_t kFrontMargin = kWalPiece + kWalLaneMax + 64;
+  WalArgs a;
+  if (int rc = pass_begin(s, s.d_img, size, s.stc, &a)) return rc;
+  std::uint64_t fronted = 0;
+  int k = 0;
+  for (std::uint64_t off = 0; off < size; off += kStageSlab, k ^= 1) {
+    const std::uint64_t m = std::min(kStageSlab, size - off);
+    if (pinned) {
+      WAL_HIP(hipMemcpyAsync(s.d_img + off, h_wal + off, m, hipMemcpyHostToDevice, s.st));
+    } else {
       WAL_HIP(hipEventSynchronize(s.slab_free[k]));
       stage_copy(s.slab[k], h_wal + off, m);
       WAL_HIP(hipMemcpyAsync(s.d_img + off, s.slab[k], m, hipMemcpyHostToDevice, s.st));
       WAL_HIP(hipEventRecord(s.slab_free[k], s.st));
     }
+    WAL_HIP(hipEventRecord(s.landed[k], s.st));
+    WAL_HIP(hipStreamWaitEvent(s.stc, s.landed[k], 0));
+    const bool last = off + m >= size;
+    const std::uint64_t k_hi = last ? a.K : (off + m > kFrontMargin ? (off + m - kFrontMargin) / kWalPiece : 0);
+    if (k_hi > fronted) {
+      pass_front(a, fronted, k_hi, s.stc);
+      fronted = k_hi;
+    }
   }
-  return verify_locked(s, s.d_img, size, n_good, stop_offset, s.st, needs_host_walk);
+  WAL_HIP(hipGetLastError());
+  PassResult r;
+  g_last[0] = 1;
+  if (int rc = pass_tail(s, a, s.stc, &r)) return rc;
+  return verify_locked(s, s.d_img, size, n_good, stop_offset, s.stc, needs_host_walk, &r);
 }
 
 }  // namespace tkv
