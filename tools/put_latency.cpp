@@ -1,0 +1,65 @@
+// Per-put cost of the drop-in (not product code): frankie::core::crc32{}.update(record).finalize()
+// through include/frankie_crc32.hpp (libtkv_crc32.so, the GPU path) next to the reference's own
+// crc32.cpp (oracle/_ref/libref_crc32.so, loaded with dlopen; test-side only), for the WAL record
+// sizes of wal_entry::encode (/root/reference/src/engine/wal.cpp:54-57), and the batched
+// alternative: tkv_wal_stamp over N records (group commit). One JSON line per measurement.
+// Build: make -C tools put_latency (needs oracle/_ref built from /root/reference).
+#include <dlfcn.h>
+
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "frankie_crc32.hpp"
+
+using clk = std::chrono::steady_clock;
+
+int main(int argc, char** argv) {
+  const char* ref_path = argc > 1 ? argv[1] : "oracle/_ref/libref_crc32.so";
+  void* h = dlopen(ref_path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    std::fprintf(stderr, "cannot load %s: %s\n", ref_path, dlerror());
+    return 1;
+  }
+  using ref_fn = std::uint32_t (*)(const unsigned char*, std::size_t);
+  auto ref_crc32 = reinterpret_cast<ref_fn>(dlsym(h, "ref_crc32"));
+  if (!ref_crc32 || tkv_set_device(0) != TKV_OK) return 1;
+  std::mt19937_64 rng(1);
+  std::vector<unsigned char> buf(1 << 20);
+  for (auto& b : buf) b = static_cast<unsigned char>(rng());
+  for (std::size_t n : {28ul, 36ul, 128ul, 1024ul, 4096ul}) {
+    const auto* p = reinterpret_cast<const std::byte*>(buf.data());
+    std::uint32_t sink = 0;
+    for (int i = 0; i < 50; ++i) sink ^= frankie::core::crc32{}.update({p, n}).finalize();
+    const int reps = 2000;
+    auto t0 = clk::now();
+    for (int i = 0; i < reps; ++i) sink ^= frankie::core::crc32{}.update({p + (i & 255), n}).finalize();
+    const double gpu_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / reps;
+    t0 = clk::now();
+    const int rreps = 200000;
+    for (int i = 0; i < rreps; ++i) sink ^= ref_crc32(buf.data() + (i & 255), n);
+    const double ref_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / rreps;
+    const bool same = frankie::core::crc32{}.update({p, n}).finalize() == ref_crc32(buf.data(), n);
+    std::printf("{\"row\": \"drop_in_update\", \"bytes\": %zu, \"gpu_us_per_call\": %.2f, \"reference_cpu_us_per_call\": %.3f, "
+                "\"bit_exact\": %s, \"sink\": %u}\n", n, gpu_us, ref_us, same ? "true" : "false", sink & 1u);
+  }
+  // group commit: N records of 36 bytes stamped in one call (wal.cpp:54-58 per record)
+  for (std::size_t nrec : {1ul, 16ul, 256ul, 4096ul}) {
+    std::vector<std::uint64_t> off(nrec);
+    std::vector<std::uint32_t> sz(nrec, 36);
+    for (std::size_t i = 0; i < nrec; ++i) off[i] = 36 * i;
+    std::vector<unsigned char> img(36 * nrec);
+    std::memcpy(img.data(), buf.data(), img.size());
+    for (int i = 0; i < 10; ++i) tkv_wal_stamp(img.data(), off.data(), sz.data(), nrec);
+    const int reps = 200;
+    auto t0 = clk::now();
+    for (int i = 0; i < reps; ++i) tkv_wal_stamp(img.data(), off.data(), sz.data(), nrec);
+    const double us = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / reps;
+    std::printf("{\"row\": \"group_commit_stamp\", \"records\": %zu, \"record_bytes\": 36, \"us_per_call\": %.2f, "
+                "\"us_per_record\": %.3f}\n", nrec, us, us / nrec);
+  }
+  return 0;
+}
