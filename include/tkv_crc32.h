@@ -226,6 +226,10 @@ int tkv_debug_multi_combine(uint32_t poly, int ndev, const uint64_t *h_offsets, 
  * passes, out[1] = 1 when it handed the image to the exact host-thread walk, out[2] = 1 when a
  * host image was copied to the device, out[3] = pieces of the last pass's image. */
 void tkv_debug_wal_last(uint64_t out[4]);
+/* Which path the last irregular batch on `stream` took: 1 = byte-stream row walk (blocks back to
+ * back, each at least 64 bytes), 0 = general row walk; -1 on error. Synchronizes
+ * the stream. */
+int tkv_debug_irregular_mode(void *stream);
 /* Host batches from pinned host memory are read in place by the kernels (zero copy) unless this is
  * 0 (then they take the staged copy pipeline, as pageable memory does). Returns the previous
  * setting. Default 1; the environment variable TKV_HOST_MAPPED=0 sets 0 at load time. */

@@ -61,11 +61,16 @@ def load_tables(lib, poly=0xEDB88320):
     row_pow = buf[o:o + 64]; o += 64
     head = buf[o:o + (ROW + 1) * 32].reshape(ROW + 1, 32); o += (ROW + 1) * 32
     rows_shift = buf[o:o + 4096]; o += 4096
+    inv_shift = buf[o:o + ROW + 1]; o += ROW + 1
+    # inv_shift[d] = x^(-8d): multiplying by x^(8d) (Shift_d of it) gives x^0 back
+    if poly == POLY:  # the debug GF(2) helpers are the CRC-32 polynomial's
+        for d in (0, 1, 3, 100, 4096):
+            assert lib.tkv_debug_multmodp(lib.tkv_debug_x8nmodp(d), int(inv_shift[d])) == 0x80000000
     # rows_shift[k] = x^(8*4096*k): rows_shift[0] = x^0, [1] = row_pow[0], [2^k] = row_pow[k]
     assert int(rows_shift[0]) == 0x80000000
     for k in range(12):
         assert int(rows_shift[1 << k]) == int(buf[1024 + 8 * 16 * 64 + 64 + k])
-    built_for = int(buf[o]); o += 4  # poly + 3 pad words
+    built_for = int(buf[o]); o += 3  # poly + 2 pad words
     assert o * 4 == n
     assert built_for == poly
     return slice_, lane, horner, row_pow, head
@@ -330,3 +335,38 @@ def test_skewed_packed_partition_covers_batch(nblocks, G):
     if nblocks >= 64 * G:
         first = r[:16]
         assert first[0][1] >= first[4][1] >= first[8][1] >= first[12][1]
+
+
+def stream_row0(w, TR, W, skew=154):
+    """Python restatement of dev::stream_row0 (tkv_crc32_device.h): first row of stream-mode wave w."""
+    wt = [256, skew, skew * skew // 256]
+    wt.append(wt[2] * skew // 256)
+    tot = 4 * sum(wt)
+    k = w & 15
+    c, m = k >> 2, k & 3
+    pre = 4 * sum(wt[:c]) + m * wt[c]
+    g, G = w >> 4, W >> 4
+    r0 = g * TR // G
+    return r0 + ((g + 1) * TR // G - r0) * pre // tot
+
+
+@pytest.mark.parametrize("TR,W", [(1, 16), (15, 16), (1327104, 4096), (1281, 4096), (5000, 4864), (99, 32)])
+def test_stream_partition(TR, W):
+    """Stream-mode waves cover the TR rows exactly once, in order (row0 nondecreasing, row0(W) = TR),
+    and the prepass's binary search (stream_first_wave) finds the first wave at or after each row."""
+    r0 = [stream_row0(w, TR, W) for w in range(W + 1)]
+    assert r0[0] == 0 and r0[W] == TR
+    assert all(a <= b for a, b in zip(r0, r0[1:]))
+    import bisect
+    for r in sorted({0, 1, TR // 3, TR - 1, TR} | set(range(0, TR + 1, max(1, TR // 97)))):
+        lo, hi = 0, W
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if r0[mid] >= r:
+                hi = mid
+            else:
+                lo = mid + 1
+        assert lo == bisect.bisect_left(r0, r)
+        if 0 < r <= TR:  # the wave holding row r-1 is the last one starting at or before it
+            w = lo - 1
+            assert r0[w] <= r - 1 < r0[w + 1]

@@ -630,6 +630,296 @@ __device__ __forceinline__ void small_phase(const RowsArgs& a, std::uint32_t* ld
   }
 }
 
+// Inclusive prefix XOR of v over the 64 lanes (DPP row shifts within rows of 16, then row
+// broadcasts across rows).
+__device__ __forceinline__ std::uint32_t wave_prefix_xor(std::uint32_t v) {
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  v ^= __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+__device__ __forceinline__ std::uint64_t readlane64(std::uint64_t v, std::uint32_t l) {
+  const std::uint32_t lo = __builtin_amdgcn_readlane(static_cast<std::uint32_t>(v), l);
+  const std::uint32_t hi = __builtin_amdgcn_readlane(static_cast<std::uint32_t>(v >> 32), l);
+  return (static_cast<std::uint64_t>(hi) << 32) | lo;
+}
+
+// Stream-mode row partition: wave w (of W, 16 to a workgroup) walks rows [stream_row0(w), stream_row0(w+1))
+// of the TR rows; stream_row0(W) = TR. Workgroup g gets rows [g*TR/G, (g+1)*TR/G) and shares them among
+// its waves as crc_packed_body's SKEW partition does (slot class c = slot/4 weighted (SKEW/256)^c).
+template <int SKEW>
+__device__ __forceinline__ std::uint64_t stream_row0(std::uint64_t w, std::uint64_t TR, std::uint64_t W) {
+  if constexpr (SKEW == 0) {
+    return w * TR / W;
+  } else {
+    constexpr std::uint32_t w0 = 256, w1 = SKEW, w2 = w1 * SKEW / 256, w3 = w2 * SKEW / 256;
+    constexpr std::uint32_t tot = 4 * (w0 + w1 + w2 + w3);
+    const std::uint32_t k = static_cast<std::uint32_t>(w & 15u), c = k >> 2, m = k & 3u;
+    const std::uint32_t pre = (c > 0 ? 4 * w0 : 0u) + (c > 1 ? 4 * w1 : 0u) + (c > 2 ? 4 * w2 : 0u) +
+                              m * (c == 0 ? w0 : c == 1 ? w1 : c == 2 ? w2 : w3);
+    const std::uint64_t g = w >> 4, G = W >> 4;
+    const std::uint64_t r0 = g * TR / G, gn = (g + 1) * TR / G - r0;
+    return r0 + gn * pre / tot;
+  }
+}
+// Smallest wave w in [0, W] with row0[w] >= r, from the table row0[0..W] of stream_row0 (which is
+// nondecreasing in w): a binary search of cached loads instead of 64-bit divisions.
+__device__ __forceinline__ std::uint32_t stream_first_wave(const std::uint32_t* row0, std::uint64_t r, std::uint32_t W) {
+  std::uint32_t lo = 0, hi = W;
+  while (lo < hi) {
+    const std::uint32_t mid = (lo + hi) >> 1;
+    if (row0[mid] >= r) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
+// Byte-stream row walk of an irregular batch whose blocks lie back to back (stream mode, chosen by
+// the prepass). The stream is cut into full 4 KiB rows from row 0 = its start
+// rounded down to 16 bytes (bytes in front of it read as zero, bytes past its end are never used),
+// so every row is aligned, no row is partial and there is no small-block phase. Waves own
+// contiguous ranges of rows and fold them exactly as the packed kernel does, keeping
+// B = crc_0(stream bytes from the wave's first row) by Horner over rows. Block ends do not stop
+// the walk: for a block ending at E inside row g, in lane l's segment at byte r in (0, 64], the lane
+// captures its chain register after floor(r/4) dwords during the fold, finishes the last r mod 4
+// bytes with Sarwate steps (Q = crc_0 of its segment up to E), and the wave's prefix XOR of the
+// lane values gives Y = Shift_4096(B) ^ (lanes before l, moved to the row end). Then
+// crc_0(wave bytes up to E) = Shift_(rowend - E)^-1 (Y) ^ Q, which stream_finish turns into each
+// block's CRC. Each wave stores (Y, Q) per block end it meets and its own B at the end of its range.
+template <int PRIO>
+__device__ __forceinline__ void crc_stream_body(const RowsArgs& a, std::uint32_t* lds) {
+  constexpr int DEPTH = 4, ILP = 2;
+  fill_lds(a.tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const LaneConst kc = lane_const(lane);
+  const std::uint32_t hcon = a.tabs->horner[lane];  // Shift_4096(1 << l) for l < 32, else 0
+  const bool lo_half = lane < 32u;
+  __syncthreads();
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t TR = sload32(a.counts, 2);
+  const std::uint32_t g0 = sload32(a.s_row0, wave);
+  const std::uint32_t g1 = sload32(a.s_row0, wave + 1);
+  if (g0 >= g1) {
+    if (lane == 0) a.s_wtot[wave] = 0u;
+    return;
+  }
+  const std::uint32_t n = a.nblocks;
+  const std::uint64_t s0rel = sload64(a.s_info, 1);
+  const std::uintptr_t zrow = reinterpret_cast<std::uintptr_t>(a.base) + sload64(a.s_info, 0);
+  const std::uintptr_t send = zrow + sload64(a.s_ends, n - 1);
+  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
+  const std::uint32_t nrows = g1 - g0;
+  const std::uintptr_t lane_base = zrow + static_cast<std::uint64_t>(g0) * kRow + lane * kSeg;
+
+  // block ends, 64 at a time: lane i of `win` holds E[bw + i]
+  std::uint32_t b = sload32(a.wave_start, wave);  // first block ending in or after row g0
+  std::uint32_t bw = b;
+  auto load_win = [&](std::uint32_t from) -> std::uint64_t {
+    const std::uint32_t i = from + lane;
+    return i < n ? a.s_ends[i] : ~0ull;
+  };
+  // Two windows: the next one is loaded 64 ends ahead, so reading an end never waits on a load
+  // issued behind the row loads in flight (a vmcnt wait drains every outstanding load before it).
+  std::uint64_t win = load_win(bw), win2 = load_win(bw + 64u);
+  std::uint32_t ci = 0;
+  std::uint64_t e_next = readlane64(win, 0);
+
+  // Per-end records (Y, Q) are gathered in registers, lane k of keep_y/keep_q holding block kb + k
+  // (kmask: lanes filled), and written 64 at a time: a store in the row loop is counted by the
+  // same vmcnt as the row loads behind it, so one store per end would stall the next row's wait on
+  // its write acknowledgement (-4 % on cfg4). Ends too far past kb for the current window (a row
+  // pair with more than 32 ends) are stored directly.
+  std::uint32_t kb = b, keep_y = 0, keep_q = 0;
+  std::uint64_t kmask = 0;
+  auto flush = [&]() {
+    if (kmask != 0) {
+      if ((kmask >> lane) & 1u) {
+        a.s_yq[kb + lane] = static_cast<std::uint64_t>(keep_y) | (static_cast<std::uint64_t>(keep_q) << 32);
+        a.s_wv[kb + lane] = wave;
+      }
+      kmask = 0;
+    }
+  };
+
+  // Block ends in the row [rs, rs + 4096): the lane whose segment holds one learns (r, block), and
+  // keep lane b - kb learns which lane that is (src; rmask: keep lanes fed by this row).
+  auto take_ends = [&](std::uint64_t rs, std::uint32_t& my_r, std::uint32_t& my_b, std::uint32_t& src,
+                       std::uint64_t& rmask) -> bool {
+    bool any = false;
+    my_r = 0xFFu;  // no end in this lane's segment
+    rmask = 0;
+    while (e_next <= rs + kRow) {
+      const std::uint32_t rel = static_cast<std::uint32_t>(e_next - rs);  // 1..4096
+      const std::uint32_t l = (rel + 63u) / 64u - 1u;
+      my_r = lane == l ? rel - 64u * l : my_r;
+      my_b = lane == l ? b : my_b;
+      const std::uint32_t k = b - kb;
+      if (k < 64u) {
+        src = lane == k ? l : src;
+        rmask |= 1ull << k;
+      }
+      any = true;
+      ++b;
+      if (++ci == 64u) {
+        bw += 64u;
+        win = win2;
+        win2 = load_win(bw + 64u);
+        ci = 0;
+      }
+      e_next = b < n ? readlane64(win, ci) : ~0ull;
+    }
+    return any;
+  };
+
+  uint4 buf[DEPTH][4];
+  // Row loads. Only the stream's last row can reach past its end; the wave that owns it walks it
+  // after its main loop with guarded loads (pieces past the end read `dummy`).
+  const bool owns_last = g1 == TR;
+  const std::uint32_t nmain = nrows - (owns_last ? 1u : 0u);
+  auto issue = [&](std::uint32_t j, uint4 (&q)[4]) {
+    const std::uint32_t jc = j < nmain ? j : (nmain ? nmain - 1 : 0u);  // rows past the range reload
+    const std::uintptr_t p = lane_base + static_cast<std::uint64_t>(jc) * kRow;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = gload16(nmain ? p + 16u * i : dmy);
+  };
+  auto issue_last = [&](uint4 (&q)[4]) {
+    const std::uintptr_t p = lane_base + static_cast<std::uint64_t>(nrows - 1) * kRow;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i < send ? p + 16u * i : dmy);
+  };
+
+  // The stream's first row, lane 0: bytes in front of the stream start read as zero (leading zeros
+  // are free).
+  auto head_mask = [&](uint4& q0) {
+    if (lane == 0u) {
+      const std::uint32_t s = static_cast<std::uint32_t>(s0rel);
+      std::uint32_t* w = reinterpret_cast<std::uint32_t*>(&q0);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const std::int32_t before = static_cast<std::int32_t>(s) - 4 * d;  // bytes of dword d in front
+        const std::uint32_t sh = static_cast<std::uint32_t>(before <= 0 ? 0 : (before >= 4 ? 4 : before)) * 8u;
+        w[d] &= static_cast<std::uint32_t>(0xFFFFFFFFull << sh);
+      }
+    }
+  };
+
+  std::uint32_t B = 0;  // crc_0 of the wave's rows so far
+  // Fold ILP rows (interleaved chains); with CAP each lane also keeps its chain register after
+  // k = my_r / 4 dwords and dword k itself (k == 16: the whole segment).
+  auto fold = [&](auto cap_const, const uint4 (*q)[4], const std::uint32_t* my_r, std::uint32_t* v,
+                  std::uint32_t* capv, std::uint32_t* capd) {
+    constexpr bool CAP = decltype(cap_const)::value;
+    Reg p[ILP];
+    std::uint32_t k[ILP];
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      p[i] = Reg{0, 0};
+      k[i] = my_r[i] >> 2;
+      capv[i] = 0;
+      capd[i] = 0;
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) {
+        const uint4& c = q[i][t >> 2];
+        const std::uint32_t d = (t & 3) == 0 ? c.x : (t & 3) == 1 ? c.y : (t & 3) == 2 ? c.z : c.w;
+        if constexpr (CAP) {
+          const bool hit = k[i] == static_cast<std::uint32_t>(t);
+          capv[i] = hit ? p[i].value() : capv[i];
+          capd[i] = hit ? d : capd[i];
+        }
+        slice4(lds, p[i], d, kc);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      if constexpr (CAP) capv[i] = k[i] == 16u ? p[i].value() : capv[i];
+      v[i] = lane_shift(lds, p[i].value(), kc);
+    }
+  };
+  // Horner step over one row; at a row with block ends, the (Y, Q) of each end.
+  auto finish = [&](std::uint32_t v, bool ends, std::uint32_t my_r, std::uint32_t my_b, std::uint32_t src,
+                    std::uint64_t rmask, std::uint32_t capv, std::uint32_t capd) {
+    const std::uint32_t term =
+        lo_half ? static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(B), lane, 1)) & hcon : 0u;
+    const std::uint32_t Bn = __builtin_amdgcn_readlane(wave_xor_to_lane63(v ^ term), 63);
+    if (ends) {
+      const std::uint32_t I = wave_prefix_xor(v);
+      const std::uint32_t I63 = __builtin_amdgcn_readlane(I, 63);
+      const std::uint32_t Y = Bn ^ I63 ^ I ^ v;  // Shift_4096(B) ^ lanes before this one
+      const std::uint32_t m = my_r & 3u;
+      std::uint32_t x = capv ^ (capd & static_cast<std::uint32_t>((1ull << (8 * m)) - 1ull));
+#pragma unroll
+      for (std::uint32_t j = 0; j < 3u; ++j)
+        if (j < m) x = (x >> 8) ^ lds_at(lds, ((x & 0xFFu) << 8) | kc.L0);  // Sarwate step (T0)
+      const std::uint32_t py = static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src << 2), static_cast<int>(Y)));
+      const std::uint32_t pq = static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src << 2), static_cast<int>(x)));
+      const bool mine = (rmask >> lane) & 1u;
+      keep_y = mine ? py : keep_y;
+      keep_q = mine ? pq : keep_q;
+      kmask |= rmask;
+      if (my_r != 0xFFu && my_b - kb >= 64u) {  // past the keep window: store now
+        a.s_yq[my_b] = static_cast<std::uint64_t>(Y) | (static_cast<std::uint64_t>(x) << 32);
+        a.s_wv[my_b] = wave;
+      }
+    }
+    B = Bn;
+  };
+  // n (1 or ILP) rows at wave-local row jq from buffer slots q[0..n)
+  auto rows = [&](int n, std::uint32_t jq, const uint4 (*q)[4]) {
+    if (b - kb >= 32u) {  // room for the ends of this row pair in the keep window
+      flush();
+      kb = b;
+    }
+    std::uint32_t my_r[ILP], my_b[ILP] = {0, 0}, src[ILP] = {0, 0};
+    std::uint64_t rmask[ILP] = {0, 0};
+    bool ends[ILP];
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+      my_r[i] = 0xFFu;
+      ends[i] = false;
+      if (i < n) {
+        ends[i] = take_ends(static_cast<std::uint64_t>(g0 + jq + i) * kRow, my_r[i], my_b[i], src[i], rmask[i]);
+        any = any || ends[i];
+      }
+    }
+    std::uint32_t v[ILP], capv[ILP], capd[ILP];
+    if (any) fold(std::true_type{}, q, my_r, v, capv, capd);
+    else fold(std::false_type{}, q, my_r, v, capv, capd);
+#pragma unroll
+    for (int i = 0; i < ILP; ++i)
+      if (i < n) finish(v[i], ends[i], my_r[i], my_b[i], src[i], rmask[i], capv[i], capd[i]);
+  };
+
+#pragma unroll
+  for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
+  if (g0 == 0u && nmain) head_mask(buf[0][0]);  // the stream's first row
+  for (std::uint32_t j = 0; j < nmain; j += DEPTH) {
+    if constexpr (PRIO != 0) set_prio_from_left<PRIO>(nmain - j, nmain);
+#pragma unroll
+    for (int qd = 0; qd < DEPTH; qd += ILP) {
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) issue(j + qd + DEPTH - ILP + i, buf[(qd + DEPTH - ILP + i) % DEPTH]);
+      const std::uint32_t jq = j + qd;
+      if (jq >= nmain) break;
+      rows(jq + ILP <= nmain ? ILP : static_cast<int>(nmain - jq), jq, &buf[qd]);
+    }
+  }
+  if (owns_last) {  // the stream's last row (it holds the last block's end)
+    issue_last(buf[0]);
+    if (nrows == 1 && g0 == 0u) head_mask(buf[0][0]);
+    rows(1, nrows - 1, &buf[0]);
+  }
+  flush();
+  if (lane == 0) a.s_wtot[wave] = B;
+}
+
 // Packed uniform fast path: block b = [base + b*len, +len) with len a multiple of kRow (4 KiB) and
 // 16-byte aligned base, so every row is full, row g of the batch sits at base + g*kRow, and the head
 // length is kRow (init injection constants = the Horner constants). Each wave owns the contiguous

@@ -14,6 +14,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "tkv_crc32.h"
@@ -26,9 +27,12 @@ namespace tkv {
 hipError_t launch_rows(const RowsArgs& a, bool aligned, bool uniform, unsigned grid, hipStream_t st);
 hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
 hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st);
-hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
-                          std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
-                          std::uint32_t W, std::uint32_t* out, hipStream_t st);
+hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
+                          std::uint32_t n, std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* tile_ok,
+                          std::uint32_t* counts, std::uint64_t* sinfo, std::uint64_t* ends, const PrepassOut& o,
+                          std::uint32_t W, std::uint32_t ncu, std::uint32_t* out, std::uint32_t* row0,
+                          hipStream_t st);
+hipError_t launch_stream_tail(const RowsArgs& a, hipStream_t st, unsigned grid);
 std::uint64_t prepass_tiles(std::uint64_t n);
 hipError_t launch_fill_uniform(std::uint8_t* dst, std::uint64_t stride, std::uint64_t len, std::uint64_t first,
                                std::uint64_t nblocks, std::uint64_t seed, hipStream_t st);
@@ -67,7 +71,7 @@ void build_tables(DeviceTables* t, std::uint32_t poly) {
   const auto mm = [poly](std::uint32_t a, std::uint32_t b) { return multmodp(a, b, poly); };
   const auto x8n = [poly](std::uint64_t n) { return x8nmodp(n, poly); };
   t->poly = poly;
-  t->pad_[0] = t->pad_[1] = t->pad_[2] = 0;
+  t->pad_[0] = t->pad_[1] = 0;
   for (std::uint32_t i = 0; i < 256; ++i) {
     std::uint32_t c = i;
     for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? poly : 0u);
@@ -92,6 +96,41 @@ void build_tables(DeviceTables* t, std::uint32_t poly) {
   for (int k = 0; k < 4096; ++k) {
     t->rows_shift[k] = rk;
     rk = mm(rk, mrow);
+  }
+  // x^(-8d), d = 0..kRow: Shift_1 (one zero byte) is an invertible linear map on the register
+  // (x is a unit mod P: P has a constant term), so its inverse comes from Gaussian elimination over
+  // GF(2) on the 32 columns Shift_1(1 << i); x^(-8d) = InvShift_1^d(x^0).
+  {
+    std::uint32_t a[32], inv[32];  // row i of the matrix: bit j = bit i of Shift_1(1 << j)
+    std::uint32_t col[32];
+    for (int j = 0; j < 32; ++j) col[j] = mm(x8n(1), 1u << j);
+    for (int i = 0; i < 32; ++i) {
+      a[i] = 0;
+      for (int j = 0; j < 32; ++j) a[i] |= ((col[j] >> i) & 1u) << j;
+      inv[i] = 1u << i;
+    }
+    for (int c = 0; c < 32; ++c) {
+      int piv = c;
+      while (!((a[piv] >> c) & 1u)) ++piv;  // exists: Shift_1 is invertible
+      std::swap(a[c], a[piv]);
+      std::swap(inv[c], inv[piv]);
+      for (int r = 0; r < 32; ++r)
+        if (r != c && ((a[r] >> c) & 1u)) {
+          a[r] ^= a[c];
+          inv[r] ^= inv[c];
+        }
+    }
+    // inv[i] bit j = entry (i, j) of the inverse matrix: InvShift_1(v) bit i = parity(inv[i] & v)
+    auto inv1 = [&](std::uint32_t v) {
+      std::uint32_t r = 0;
+      for (int i = 0; i < 32; ++i) r |= static_cast<std::uint32_t>(__builtin_parity(inv[i] & v)) << i;
+      return r;
+    };
+    std::uint32_t v = 0x80000000u;
+    for (int d = 0; d <= kRow; ++d) {
+      t->inv_shift[d] = v;
+      v = inv1(v);
+    }
   }
   std::uint32_t z = 0x80000000u;  // x^(8h), h = 0..kRow
   for (int h = 0; h <= kRow; ++h) {
@@ -129,6 +168,7 @@ struct StreamScratch {
   void* blob = nullptr;
   std::uint64_t* scan = nullptr;
   std::uint64_t* tiles = nullptr;
+  std::uint32_t* tile_ok = nullptr;  // per scan tile: its blocks qualify for stream mode
   PrepassOut po{};
   std::uint64_t cap_blocks = 0;
 };
@@ -314,7 +354,8 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     slot.reset(new StreamScratch());
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->seams), sizeof(Seam) * 2 * c->W));
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->wave_start), sizeof(std::uint32_t) * c->W));
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->counts), sizeof(std::uint32_t) * 4));
+    // counts[0..3], then (u64) the stream-mode info at counts + 4
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->counts), sizeof(std::uint32_t) * 16));
   }
   StreamScratch* s = slot.get();
   if (nblocks > s->cap_blocks) {
@@ -329,7 +370,7 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     }
     const std::uint64_t ntiles = prepass_tiles(cap) + 1;
     // 8-byte arrays first: scan, tiles, s_off, big_off; then the 4-byte ones
-    const std::uint64_t bytes = 8 * (cap + ntiles + 2 * cap) + 4 * (5 * cap + 1);
+    const std::uint64_t bytes = 8 * (cap + ntiles + 2 * cap) + 4 * (5 * cap + 1) + 4 * ntiles;
     TKV_HIP(hipMalloc(&s->blob, bytes));
     auto* p8 = static_cast<std::uint64_t*>(s->blob);
     s->scan = p8;
@@ -342,6 +383,7 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     s->po.big_len = p4 + 2 * cap;
     s->po.big_idx = p4 + 3 * cap;
     s->po.row_scan = p4 + 4 * cap;  // cap + 1 entries
+    s->tile_ok = p4 + 5 * cap + 1;
     s->cap_blocks = cap;
   }
   s->po.wave_start = s->wave_start;
@@ -422,8 +464,20 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   a.out = d_out;
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = static_cast<std::uint32_t>(c->ncu) * kRowsWavesPerWG;
-  TKV_HIP(launch_prepass(d_off, d_len, a.nblocks, s->scan, s->tiles, s->counts, s->po, a.nwaves, d_out, st));
+  // stream mode (chosen by the prepass on the device) reuses the large-block list for the block ends,
+  // the small-block offsets for the per-end registers and the seam records for the wave registers
+  auto* sinfo = reinterpret_cast<std::uint64_t*>(s->counts + 4);
+  a.s_ends = s->po.big_off;
+  a.s_info = sinfo;
+  a.s_yq = s->po.s_off;
+  a.s_wtot = reinterpret_cast<std::uint32_t*>(s->seams);  // c->W entries, then the row table (c->W + 1)
+  auto* row0 = a.s_wtot + c->W;                             // (the seam records hold 16 words per wave)
+  a.s_row0 = row0;
+  a.s_wv = s->po.big_idx;
+  TKV_HIP(launch_prepass(d_base, d_off, d_len, a.nblocks, s->scan, s->tiles, s->tile_ok, s->counts, sinfo, s->po.big_off,
+                         s->po, a.nwaves, static_cast<std::uint32_t>(c->ncu), d_out, row0, st));
   TKV_HIP(launch_rows(a, false, false, static_cast<unsigned>(c->ncu), st));  // combines its own seams
+  TKV_HIP(launch_stream_tail(a, st, static_cast<unsigned>(c->ncu)));
   return TKV_OK;
 }
 
@@ -1098,6 +1152,18 @@ int tkv_debug_multi_combine(uint32_t poly, int ndev, const uint64_t* h_offsets, 
     for (auto& o : w.out) o = piece_final[k++];
   combine_multi(p, n, poly, h_out_final);
   return TKV_OK;
+}
+
+int tkv_debug_irregular_mode(void* stream) {
+  DevCtx* c = nullptr;
+  if (get_ctx(&c)) return -1;
+  StreamScratch* s = nullptr;
+  if (get_scratch(c, stream, 0, &s)) return -1;
+  std::uint32_t mode = 0;
+  if (hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess ||
+      hipMemcpy(&mode, s->counts + 3, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return static_cast<int>(mode);
 }
 
 int tkv_debug_set_host_mapped(int enable) { return tkv::g_host_mapped.exchange(enable ? 1 : 0); }

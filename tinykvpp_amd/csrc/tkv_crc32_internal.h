@@ -50,8 +50,9 @@ struct DeviceTables {
   std::uint32_t row_pow[64];            // x^(8*kRow*2^k) mod P (reflected), k = 0..63
   std::uint32_t head_shift[kRow + 1][32];  // [h][i] = Shift_h(1 << i): init injection at a head row
   std::uint32_t rows_shift[4096];       // [k] = x^(8*kRow*k) mod P: moves a piece's partial past k rows
+  std::uint32_t inv_shift[kRow + 1];    // [d] = x^(-8d) mod P: moves a register back by d bytes (stream)
   std::uint32_t poly;                   // reflected polynomial the tables were built for
-  std::uint32_t pad_[3];
+  std::uint32_t pad_[2];
 };
 
 // One partial result of a block that was split between waves (irregular / huge-block path).
@@ -93,7 +94,18 @@ struct RowsArgs {
   const std::uint64_t* s_off;
   const std::uint32_t* s_len;
   const std::uint32_t* s_idx;
+  // irregular batches in stream mode (counts[3] == kModeStream, chosen by the prepass: blocks back
+  // to back, each at least kStreamMinLen bytes). Rows of 4 KiB cover the stream
+  // from row 0 = the stream start rounded down to 16 bytes.
+  const std::uint64_t* s_ends;       // E[b] = end of block b in bytes from row 0
+  const std::uint64_t* s_info;       // [0] offset of row 0 from base, [1] stream start within row 0
+  std::uint64_t* s_yq;               // per block: Y | Q << 32 at its end (crc_stream_body)
+  std::uint32_t* s_wtot;             // per wave: crc_0 of its rows alone (crc_stream_body)
+  const std::uint32_t* s_row0;       // [w] = first row of wave w, [nwaves] = rows (rows_tile_scan)
+  std::uint32_t* s_wv;               // per block: the wave that met its end (crc_stream_body)
 };
+constexpr std::uint32_t kModeStream = 1;
+constexpr std::uint32_t kStreamMinLen = 64;  // at most one block end per 64-byte lane segment
 
 // Outputs of the irregular prepass (scratch of one stream).
 struct PrepassOut {

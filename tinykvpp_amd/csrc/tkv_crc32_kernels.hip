@@ -41,8 +41,24 @@ struct Shape {
 template <bool ALIGNED, bool UNIFORM>
 __global__ __launch_bounds__(kRowsThreads) void crc_rows(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
+  if constexpr (!UNIFORM) {
+    // irregular batch whose blocks lie back to back: the prepass chose the byte-stream row walk
+    // (crc_stream, launched next)
+    if (dev::sload32(a.counts, 3) == kModeStream) return;
+  }
   // issue priority from the rows left (set_prio_from_left): +0.7 % on cfg4 (profiles/r1/launch_irr_pri3.txt)
   dev::crc_rows_body<ALIGNED, UNIFORM, Shape<ALIGNED>::kDepth, Shape<ALIGNED>::kIlp, 3>(a, lds);
+}
+
+// Byte-stream row walk of an irregular batch in stream mode: the packed kernel's
+// shape, issue priority and skewed row partition; returns at once on general batches.
+// Skewed row partition (stream_row0): +0.5 % on cfg4 against the even split (in-process A/B).
+constexpr unsigned kStreamThreads = kThreads;
+constexpr int kStreamSkew = 154;
+__global__ __launch_bounds__(kStreamThreads) void crc_stream(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  if (dev::sload32(a.counts, 3) != kModeStream) return;
+  dev::crc_stream_body<3>(a, lds);  // issue priority from the rows left: +0.8 % on cfg4 (in-process A/B)
 }
 
 // Packed uniform batches (len % 4 KiB == 0, stride == len, 16-byte aligned): DESIGN.md §4.
@@ -79,17 +95,47 @@ __device__ __forceinline__ std::uint64_t scan_item(std::uint32_t len) {
   return len <= kSmallMax ? 1ull : static_cast<std::uint64_t>(rows_for_len(len)) << 32;
 }
 
-__global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint32_t* lengths, std::uint32_t n,
-                                                      std::uint64_t* scan, std::uint64_t* tile_sums) {
+// Also records per tile whether its blocks qualify for stream mode: each at least kStreamMinLen
+// bytes and ending where the next one starts.
+// Stream mode's geometry: row 0 starts at the stream start rounded down to 16 bytes (offset zoff
+// from base, the stream starting s0rel bytes into it) and TR rows of 4 KiB cover the stream. Only
+// meaningful when the blocks lie back to back in order (the prepass checks that).
+struct StreamGeom {
+  std::uint64_t zoff, s0rel, rows;
+};
+__device__ __forceinline__ StreamGeom stream_geometry(const std::uint8_t* base, const std::uint64_t* offsets,
+                                                      const std::uint32_t* lengths, std::uint32_t n) {
+  const std::uint64_t off0 = offsets[0];
+  const std::uint64_t s0rel = (reinterpret_cast<std::uintptr_t>(base) + off0) & 15u;
+  const std::uint64_t zoff = off0 - s0rel;
+  const std::uint64_t end = offsets[n - 1] + lengths[n - 1];
+  return {zoff, s0rel, end > zoff ? (end - zoff + kRow - 1) / kRow : 0};
+}
+
+__global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase, const std::uint64_t* offsets,
+                                                      const std::uint32_t* lengths, std::uint32_t n,
+                                                      std::uint64_t* scan, std::uint64_t* tile_sums,
+                                                      std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws) {
   __shared__ std::uint64_t wsum[16];
+  // stream mode's wave partition (used only if the prepass picks stream mode): row0[0..Ws], grid-stride
+  for (std::uint32_t w = blockIdx.x * 1024u + threadIdx.x; w <= Ws; w += gridDim.x * 1024u) {
+    const std::uint64_t TR = stream_geometry(sbase, offsets, lengths, n).rows;
+    row0[w] = static_cast<std::uint32_t>(dev::stream_row0<kStreamSkew>(w, TR, Ws));
+  }
   const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * 4u;
   const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   std::uint64_t v[4], s = 0;
+  bool ok = true;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    v[i] = (base + i < n) ? scan_item(lengths[base + i]) : 0ull;
+    const std::uint64_t b = base + i;
+    const std::uint32_t len = b < n ? lengths[b] : 0u;
+    v[i] = b < n ? scan_item(len) : 0ull;
     s += v[i];
+    if (b < n) ok = ok && len >= kStreamMinLen && (b + 1 >= n || offsets[b] + len == offsets[b + 1]);
   }
+  const bool tile_all_ok = __syncthreads_and(ok ? 1 : 0) != 0;
+  if (threadIdx.x == 0) tile_ok[blockIdx.x] = tile_all_ok ? 1u : 0u;
   // Inclusive scan of the thread sums inside the wave (cross-lane shifts, no barriers), then the
   // 16 wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
   std::uint64_t inc = s;
@@ -141,6 +187,7 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
     counts[0] = n - ns;                                // large blocks
     counts[1] = ns;                                    // small blocks
     counts[2] = static_cast<std::uint32_t>(carry >> 32);  // rows of the large blocks
+    counts[3] = 0;                                         // general path (no stream mode here)
   }
 }
 
@@ -187,12 +234,40 @@ __global__ void rows_finish(const std::uint64_t* offsets, const std::uint32_t* l
 // publishes counts for the row kernel.
 constexpr std::uint32_t kFusedTiles = 1024;
 constexpr std::uint32_t kFinishThreads = 256;
+// Stream mode (every tile qualified): instead of the small/large lists, every block
+// gets its end E[b] in bytes from row 0 (the stream start rounded down to 16 bytes), and every
+// row-kernel wave the first block ending in or after its first row; counts = {0, 0, rows, 1} and
+// s_info = {row 0's offset from base, stream start within row 0}.
+__device__ __forceinline__ void stream_block(const std::uint8_t* base, const std::uint64_t* offsets,
+                                             const std::uint32_t* lengths, std::uint32_t n, std::uint64_t b,
+                                             std::uint64_t off, std::uint32_t len, std::uint32_t W,
+                                             const std::uint32_t* row0, std::uint32_t* counts, std::uint64_t* ends,
+                                             std::uint64_t* sinfo, std::uint32_t* wave_start) {
+  const StreamGeom g = stream_geometry(base, offsets, lengths, n);
+  if (b == 0) {
+    counts[0] = 0;
+    counts[1] = 0;
+    counts[2] = static_cast<std::uint32_t>(g.rows);
+    counts[3] = kModeStream;
+    sinfo[0] = g.zoff;
+    sinfo[1] = g.s0rel;
+  }
+  const std::uint64_t e = off + len - g.zoff;
+  ends[b] = e;
+  // waves whose first row lies in (row of the previous end, row of this end]
+  const std::uint64_t rb1 = (e - 1) / kRow + 1;                   // row of this end, plus one
+  const std::uint64_t rp1 = b == 0 ? 0 : (e - len - 1) / kRow + 1;  // same for the previous end
+  for (std::uint32_t w = dev::stream_first_wave(row0, rp1, W); w < W && row0[w] < rb1; ++w)
+    wave_start[w] = static_cast<std::uint32_t>(b);
+}
+
 __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
-    const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n, const std::uint64_t* scan,
-    const std::uint64_t* tile_sums, std::uint32_t ntiles, std::uint32_t* counts, PrepassOut o, std::uint32_t W,
-    std::uint32_t* out) {
+    const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
+    const std::uint64_t* scan, const std::uint64_t* tile_sums, const std::uint32_t* tile_ok, std::uint32_t ntiles,
+    std::uint32_t* counts, PrepassOut o, std::uint32_t W, std::uint32_t* out, std::uint64_t* ends,
+    std::uint64_t* sinfo, std::uint32_t Ws, const std::uint32_t* row0) {
   constexpr std::uint32_t kWaves = kFinishThreads / 64;
-  __shared__ std::uint64_t red[2][kWaves];
+  __shared__ std::uint64_t red[3][kWaves];
   const std::uint32_t my_tile = blockIdx.x * kFinishThreads / kScanTile;  // kScanTile % 256 == 0
   // The block's own operands are loaded first, so their latency overlaps the tile-sum reduction.
   const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(kFinishThreads) + threadIdx.x;
@@ -200,38 +275,87 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
   const std::uint32_t len = live ? lengths[b] : 0u;
   const std::uint64_t off = live ? offsets[b] : 0ull;
   const std::uint64_t sc = live ? scan[b] : 0ull;
-  std::uint64_t before = 0, all = 0;
+  std::uint64_t before = 0, all = 0, bad = 0;
   for (std::uint32_t i = threadIdx.x; i < ntiles; i += kFinishThreads) {
     const std::uint64_t v = tile_sums[i];
     all += v;
     before += i < my_tile ? v : 0ull;
+    bad += tile_ok[i] ? 0u : 1u;
   }
   // Wave sums by cross-lane exchange, then the kWaves partial sums through LDS (one barrier).
 #pragma unroll
   for (unsigned m = 32; m > 0; m >>= 1) {
     before += __shfl_xor(before, m, 64);
     all += __shfl_xor(all, m, 64);
+    bad += __shfl_xor(bad, m, 64);
   }
   const unsigned wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63u) == 0) {
     red[0][wid] = before;
     red[1][wid] = all;
+    red[2][wid] = bad;
   }
   __syncthreads();
-  std::uint64_t tile_off = 0, total = 0;
+  std::uint64_t tile_off = 0, total = 0, nbad = 0;
 #pragma unroll
   for (unsigned w = 0; w < kWaves; ++w) {
     tile_off += red[0][w];
     total += red[1][w];
+    nbad += red[2][w];
+  }
+  if (nbad == 0) {  // every block qualifies: stream mode
+    if (live) stream_block(base, offsets, lengths, n, b, off, len, Ws, row0, counts, ends, sinfo, o.wave_start);
+    return;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const std::uint32_t ns = static_cast<std::uint32_t>(total);
     counts[0] = n - ns;                                    // large blocks
     counts[1] = ns;                                        // small blocks
     counts[2] = static_cast<std::uint32_t>(total >> 32);  // rows of the large blocks
+    counts[3] = 0;                                         // general path
   }
   if (!live) return;
   finish_block(off, len, b, sc + tile_off, total >> 32, o, W, out);
+}
+
+// ---- stream mode: every block's CRC from the row kernel's per-end and per-wave registers ------------
+// x^(8d) mod P for any byte distance d.
+__device__ __forceinline__ std::uint32_t stream_x8n(const DeviceTables* t, std::uint64_t d) {
+  return dev::multmodp(dev::shift_rows_tab(t, 0x80000000u, static_cast<std::uint32_t>(d >> 12)),
+                       t->head_shift[d & 4095u][31], t->poly);
+}
+
+// Block b = [E[b-1], E[b]) of the stream (block 0 starts at the stream start s0; the bytes of row 0
+// before it were read as zeros). Let S(e) = crc_0(stream bytes [0, e)), wave w hold rows
+// [g0(w), g1(w)) with T_w = s_wtot[w] = crc_0 of those rows alone, and
+// L(e) = crc_0(bytes of e's wave up to e) = Shift_(rowend - e)^-1 (Y) ^ Q from the row kernel. Then
+// S(e) = Shift_(e - 4096 g0(w))(S(4096 g0(w))) ^ L(e), and S at a wave start is the sum of the earlier
+// waves' T_v each shifted to that point, so with e' = E[b-1] in wave w' and e = E[b] in wave w:
+//   crc_0(block) = S(e) ^ Shift_len(S(e')) = L(e) ^ Shift_len(L(e')) ^ sum_{w' <= v < w} Shift_(e - 4096 g1(v))(T_v)
+// (the wave sums before w' cancel). Most blocks lie in one wave and the last sum is empty. For
+// block 0, L(s0) = 0 and w' = 0. The register from init is Shift_len(init) ^ crc_0(block).
+__global__ void stream_finish(RowsArgs a) {
+  if (dev::sload32(a.counts, 3) != kModeStream) return;
+  const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+  if (b >= a.nblocks) return;
+  const DeviceTables* t = a.tabs;
+  const std::uint32_t poly = t->poly;
+  auto L = [&](std::uint64_t e, std::uint64_t yq) -> std::uint32_t {
+    const std::uint64_t rowend = ((e - 1) / kRow + 1) * kRow;
+    return dev::multmodp(t->inv_shift[rowend - e], static_cast<std::uint32_t>(yq), poly) ^
+           static_cast<std::uint32_t>(yq >> 32);
+  };
+  const std::uint64_t e = a.s_ends[b];
+  const std::uint64_t ep = b ? a.s_ends[b - 1] : 0;
+  const std::uint64_t len = b ? e - ep : e - a.s_info[1];
+  std::uint32_t crc0 = L(e, a.s_yq[b]);
+  const std::uint32_t w = a.s_wv[b], wp = b ? a.s_wv[b - 1] : 0u;
+  for (std::uint32_t v = wp; v < w; ++v)
+    crc0 ^= dev::multmodp(stream_x8n(t, e - static_cast<std::uint64_t>(a.s_row0[v + 1]) * kRow), a.s_wtot[v], poly);
+  const std::uint32_t lp = b ? L(ep, a.s_yq[b - 1]) : 0u;
+  const std::uint32_t init = a.init_raw ? a.init_raw[b] : a.init_default;
+  const std::uint32_t raw = dev::multmodp(stream_x8n(t, len), init ^ lp, poly) ^ crc0;
+  a.out[b] = raw ^ a.out_xor;
 }
 
 // ---- synthetic data: byte j of block b = LE byte j%8 of
@@ -323,18 +447,22 @@ hipError_t launch_fixup(const RowsArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
-                          std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
-                          std::uint32_t W, std::uint32_t* out, hipStream_t st) {
+hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
+                          std::uint32_t n, std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* tile_ok,
+                          std::uint32_t* counts, std::uint64_t* sinfo, std::uint64_t* ends, const PrepassOut& o,
+                          std::uint32_t W, std::uint32_t ncu, std::uint32_t* out, std::uint32_t* row0,
+                          hipStream_t st) {
+  const std::uint32_t Ws = ncu * (kStreamThreads / 64);  // crc_stream's waves
   // Grid sizes in 64-bit arithmetic: n may be close to 2^32 (the host caps it at kMaxIrregularBlocks).
   const std::uint64_t ntiles = prepass_tiles(n);
   const std::uint64_t nfused = (static_cast<std::uint64_t>(n) + kFinishThreads - 1) / kFinishThreads;
   const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
-  hipLaunchKernelGGL(rows_tile_scan, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, lengths, n, scan,
-                     tile_sums);
+  hipLaunchKernelGGL(rows_tile_scan, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets, lengths,
+                     n, scan, tile_sums, tile_ok, row0, Ws);
   if (ntiles <= kFusedTiles) {
-    hipLaunchKernelGGL(rows_finish_fused, dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, offsets,
-                       lengths, n, scan, tile_sums, static_cast<std::uint32_t>(ntiles), counts, o, W, out);
+    hipLaunchKernelGGL(rows_finish_fused, dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
+                       offsets, lengths, n, scan, tile_sums, tile_ok, static_cast<std::uint32_t>(ntiles), counts, o,
+                       W, out, ends, sinfo, Ws, row0);
   } else {
     hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, static_cast<std::uint32_t>(ntiles), n,
                        counts);
@@ -344,6 +472,16 @@ hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* len
   return hipGetLastError();
 }
 
+
+// Stream-mode tail of an irregular batch (both kernels return at once unless the prepass chose
+// stream mode): the row walk over the whole stream, then one thread per block.
+hipError_t launch_stream_tail(const RowsArgs& a, hipStream_t st, unsigned grid) {
+  RowsArgs b = a;
+  b.nwaves = grid * (kStreamThreads / 64);
+  hipLaunchKernelGGL(crc_stream, dim3(grid), dim3(kStreamThreads), 0, st, b);
+  hipLaunchKernelGGL(stream_finish, dim3((a.nblocks + 255u) / 256u), dim3(256), 0, st, b);
+  return hipGetLastError();
+}
 
 hipError_t launch_sst_fix(std::uint8_t* file, const std::uint64_t* offsets, const std::uint32_t* sizes,
                           std::uint32_t* out, std::uint64_t n, int store, const DeviceTables* tabs, hipStream_t st) {

@@ -839,15 +839,18 @@ std::uint64_t* g_scan64 = nullptr;
 std::uint64_t* g_tiles64 = nullptr;
 std::uint32_t* g_wstart = nullptr;
 std::uint32_t* g_counts = nullptr;
+std::uint32_t* g_tile_ok = nullptr;
 PrepassOut g_po{};
 std::uint64_t g_cap = 0;
 }  // namespace
 
 namespace tkv {
 hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
-hipError_t launch_prepass(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
-                          std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* counts, const PrepassOut& o,
-                          std::uint32_t W, std::uint32_t* out, hipStream_t st);
+hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
+                          std::uint32_t n, std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* tile_ok,
+                          std::uint32_t* counts, std::uint64_t* sinfo, std::uint64_t* ends, const PrepassOut& o,
+                          std::uint32_t W, std::uint32_t ncu, std::uint32_t* out, std::uint32_t* row0,
+                          hipStream_t st);
 }  // namespace tkv
 
 extern "C" int explore_count() { return kNV + 1; }
@@ -936,7 +939,9 @@ extern "C" int explore_run_irr(int v, const std::uint8_t* base, const std::uint6
     g_po.big_idx = p4 + 3 * n;
     g_po.row_scan = p4 + 4 * n;
     if (!g_wstart) hipMalloc(&g_wstart, 4 * g_ncu * 16);
-    if (!g_counts) hipMalloc(&g_counts, 16);
+    if (!g_counts) hipMalloc(&g_counts, 64);
+    hipFree(g_tile_ok);
+    hipMalloc(&g_tile_ok, 4 * nt);
     g_po.wave_start = g_wstart;
     g_cap = n;
   }
@@ -959,7 +964,12 @@ extern "C" int explore_run_irr(int v, const std::uint8_t* base, const std::uint6
   a.dummy = g_dummy;
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = g_ncu * (kIrr[v].threads / 64);
-  launch_prepass(off, len, a.nblocks, g_scan64, g_tiles64, g_counts, g_po, a.nwaves, out, st);
+  // The explorer's irregular variants run the general path only: on batches that qualify for stream
+  // mode (blocks back to back, each >= 64 B) the prepass builds no small/large lists, so use them on
+  // batches with gaps between blocks.
+  launch_prepass(base, off, len, a.nblocks, g_scan64, g_tiles64, g_tile_ok, g_counts,
+                 reinterpret_cast<std::uint64_t*>(g_counts + 4), g_po.big_off, g_po, a.nwaves, g_ncu, out,
+                 reinterpret_cast<std::uint32_t*>(g_seams) + 16 * g_ncu, st);
   kIrr[v].launch(a, st);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
