@@ -120,13 +120,20 @@ def pmc_traffic(csv_path, config):
     separate run: counters are never collected inside the timed run): per kernel of the step, the
     median over its dispatches, summed. FETCH_SIZE is in KiB and counts half the bytes of a wide
     streaming read on gfx950, so bytes = FETCH_SIZE*1024*2 (MI355X_MICROARCH.md §HBM). Default
-    source: the committed profile of this config."""
+    source: the committed profile of this config (round 2's pass where one exists: cfg4's step changed
+    to the stream-mode kernels, and cfg5 had none in round 1)."""
     import csv
     from collections import defaultdict
-    step_kernels = (("crc_rows", "rows_tile_scan", "rows_scan_tiles", "rows_finish", "crc_fixup")
-                    if config == "cfg4" else ("crc_packed",))
-    path = csv_path or os.path.join(ROOT, "profiles", "r1", f"pmc_{config}", "p3_counters.csv")
-    if not os.path.exists(path):
+    step_kernels = (("crc_rows", "crc_stream", "stream_finish", "rows_tile_scan", "rows_scan_tiles",
+                     "rows_finish", "crc_fixup") if config == "cfg4" else ("crc_packed",))
+    path = csv_path
+    if path is None:
+        for cand in (os.path.join(ROOT, "profiles", "r2", f"pmc_{config}", "FETCH_SIZE_counters.csv"),
+                     os.path.join(ROOT, "profiles", "r1", f"pmc_{config}", "p3_counters.csv")):
+            if os.path.exists(cand):
+                path = cand
+                break
+    if path is None or not os.path.exists(path):
         return None, None
     per = defaultdict(list)
     for r in csv.DictReader(open(path)):
