@@ -267,7 +267,10 @@ def main():
     torch.cuda.set_device(local)
     tk.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # TKV_BENCH_FORCE_DIST=1 runs the process group, barriers and reductions even at WORLD_SIZE 1
+    # (under torch.distributed.run), so a one-GPU box exercises the multi-rank code path over RCCL.
+    use_dist = world > 1 or os.environ.get("TKV_BENCH_FORCE_DIST") == "1"
+    if use_dist:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -300,6 +303,13 @@ def main():
             tk.crc32_batch_uniform(data, blen, nblocks, out=o, stream=strm)
     torch.cuda.synchronize()
 
+    if use_dist:
+        # The first collective builds the communicator (RCCL: hundreds of ms). Paid here, before the
+        # warm-up, so the barrier in front of the timed steps is short and the clocks stay up: with
+        # the lazy build there, the timed steps of a one-rank RCCL run read 7 % low
+        # (profiles/r2/dist/bench_nccl_ws1_lazy.json).
+        dist.barrier()
+        reduce_timing(0.0, 0.0, True, dist, dev if backend == "nccl" else None)
     warm_steps, warm_ms = warm_up(step, args.warmup, args.min_warmup_ms)
 
     # One HIP event pair on the launch stream brackets the K steps; the average launch duration is
@@ -307,7 +317,7 @@ def main():
     # (rocprofv3 kernel trace: back-to-back launches start 0 us after their predecessor ends,
     # 10.4 us with two markers between them), a cost no caller pays.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -316,7 +326,7 @@ def main():
         step(stream)
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
@@ -326,7 +336,7 @@ def main():
     crcs = out.cpu().numpy().view(np.uint32).copy()
     bit_exact, full = verify_rank(ora, args.config, first, crcs, blen, None if blen else lens)
     ranks_seen = 1
-    if world > 1:
+    if use_dist:
         elapsed, kernel_ms, bit_exact, ranks_seen, full = reduce_timing(
             elapsed, kernel_ms, bit_exact, dist, dev if backend == "nccl" else None, full)
     if full:
@@ -417,7 +427,7 @@ def main():
         line["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -6,9 +6,15 @@
 // [[nodiscard]] uint32_t finalize() const noexcept and void reset() noexcept — so wal.cpp's
 // `core::crc32{}.update({...}).finalize()` (wal.cpp:54-57, 89-92) and test/crc32_test.cpp compile
 // unchanged. update() forwards to the C ABI (tkv_crc32_update, include/tkv_crc32.h), which runs the
-// gfx950 HIP kernel; there is no CPU implementation behind it. The reference's update is noexcept
-// with no error path, so a device failure is reported on stderr and aborts (a wrong checksum would
-// be worse than a crash for an integrity routine).
+// gfx950 HIP kernel. The reference's update is noexcept with no error path, so a device failure is
+// reported on stderr and aborts (a wrong checksum would be worse than a crash for an integrity
+// routine).
+//
+// Opt-in host path for short spans: compile with -DTKV_DROPIN_HOST_MAX=N and spans of at most N
+// bytes go to tkv_crc32_update_host (slicing-by-8 on the calling core, no device involved) instead
+// of a GPU round trip: the reference's per-put record stamp (wal.cpp:54-57) then costs what it
+// costs in the reference (INTEGRATION.md §1 has the numbers). The default, 0, keeps every span on
+// the GPU. Spans above N still abort on a device failure; nothing falls back to the host.
 //
 // Build: add include/ to the include path and link libtkv_crc32.so.
 #pragma once
@@ -21,6 +27,10 @@
 #include <span>
 
 #include "tkv_crc32.h"
+
+#ifndef TKV_DROPIN_HOST_MAX
+#define TKV_DROPIN_HOST_MAX 0
+#endif
 
 namespace frankie::core {
 
@@ -50,7 +60,9 @@ class crc32 final {
   // Continues the stored register over `data` without XORing with 0xFFFFFFFF (crc32.cpp:9-16).
   [[nodiscard]] crc32 &update(std::span<const std::byte> data) noexcept {
     std::uint32_t next = crc_;
-    const int rc = tkv_crc32_update(crc_, data.data(), data.size(), &next);
+    const bool host = kHostSpanMax > 0 && data.size() <= kHostSpanMax;
+    const int rc = host ? tkv_crc32_update_host(crc_, data.data(), data.size(), &next)
+                        : tkv_crc32_update(crc_, data.data(), data.size(), &next);
     if (rc != TKV_OK) {
       std::fprintf(stderr, "frankie::core::crc32::update: GPU CRC failed (status %d): %s\n", rc, tkv_last_error());
       std::abort();
@@ -67,6 +79,8 @@ class crc32 final {
 
  private:
   static constexpr const auto TABLE{generate_crc32_table()};  // crc32.hpp:46 (kept for layout parity)
+  // Spans up to this many bytes take the host path (TKV_DROPIN_HOST_MAX; 0 = none).
+  static constexpr std::size_t kHostSpanMax{TKV_DROPIN_HOST_MAX};
 
   std::uint32_t crc_{kCRC32DefaultValue};
 };

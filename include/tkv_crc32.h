@@ -63,6 +63,15 @@ int tkv_crc32_update(uint32_t raw_state, const void *data, size_t len, uint32_t 
 int tkv_crc32_update_device(uint32_t raw_state, const void *d_data, size_t len, uint32_t *d_out_raw,
                             void *stream);
 
+/* Host-CPU latency path for ONE short span (slicing-by-8; no device, never fails on valid
+ * arguments): the same register semantics as tkv_crc32_update. No other entry point calls it: it is
+ * not a fallback. The drop-in header include/frankie_crc32.hpp routes spans of at most
+ * TKV_DROPIN_HOST_MAX bytes here when the integrator defines that macro (default 0: off), for the
+ * reference's per-put record stamp (wal.cpp:54-57), where a GPU round trip costs ~20 us against
+ * ~0.03 us on the host. */
+int tkv_crc32_update_host(uint32_t raw_state, const void *data, size_t len, uint32_t *out_raw);
+int tkv_crc32c_update_host(uint32_t raw_state, const void *data, size_t len, uint32_t *out_raw);
+
 /* CRC of the concatenation A || B from crc1 = CRC(A), crc2 = CRC(B) (finalized values) and
  * len2 = |B| (zlib's crc32_combine): Shift_len2(crc1) ^ crc2, GF(2) arithmetic on the 4-byte
  * values only (host, no data, no device). The reference has no equivalent; it serves callers that

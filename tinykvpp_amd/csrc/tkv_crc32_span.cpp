@@ -1,0 +1,71 @@
+// Host latency path for one short span (opt-in).
+//
+// tinykvpp's only live caller checksums one ~36-byte WAL record per put (wal_entry::encode,
+// /root/reference/src/engine/wal.cpp:54-57). Through the GPU every such call is a launch and a
+// round trip (~20 us); on the host core that already holds the record it is a few table lookups.
+// This file is that host path: slicing-by-8 over tables built from the polynomial, the same
+// register semantics as crc32::update (crc32.cpp:9-16: no init or xorout applied here). Nothing in
+// the library calls it; the drop-in header uses it only for spans up to TKV_DROPIN_HOST_MAX bytes
+// when the integrator defines that macro (default 0: every span goes to the GPU), and the C ABI
+// exposes it as the separately named tkv_crc32[c]_update_host. It is not a fallback: the GPU entry
+// points never route here, with or without a device.
+#include <cstdint>
+#include <cstring>
+
+#include "tkv_crc32.h"
+
+namespace {
+
+// T[k][e]: register contribution of byte value e followed by k zero bytes (slicing-by-8 tables).
+struct SpanTables {
+  std::uint32_t t[8][256];
+  explicit SpanTables(std::uint32_t poly) {
+    for (std::uint32_t e = 0; e < 256; ++e) {
+      std::uint32_t c = e;
+      for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? poly : 0u);
+      t[0][e] = c;
+    }
+    for (std::uint32_t e = 0; e < 256; ++e)
+      for (int k = 1; k < 8; ++k) t[k][e] = (t[k - 1][e] >> 8) ^ t[0][t[k - 1][e] & 0xFFu];
+  }
+};
+
+const SpanTables& tables(std::uint32_t poly) {
+  static const SpanTables crc(TKV_CRC32_POLYNOMIAL);
+  static const SpanTables crcc(0x82F63B78u);
+  return poly == TKV_CRC32_POLYNOMIAL ? crc : crcc;
+}
+
+std::uint32_t span_update(const SpanTables& T, std::uint32_t r, const unsigned char* p, std::size_t n) {
+  while (n >= 8) {
+    std::uint64_t w;
+    std::memcpy(&w, p, 8);  // little-endian host (x86-64), as the device path assumes
+    w ^= r;
+    r = T.t[7][w & 0xFFu] ^ T.t[6][(w >> 8) & 0xFFu] ^ T.t[5][(w >> 16) & 0xFFu] ^ T.t[4][(w >> 24) & 0xFFu] ^
+        T.t[3][(w >> 32) & 0xFFu] ^ T.t[2][(w >> 40) & 0xFFu] ^ T.t[1][(w >> 48) & 0xFFu] ^ T.t[0][w >> 56];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) r = (r >> 8) ^ T.t[0][(r ^ *p++) & 0xFFu];
+  return r;
+}
+
+int update_host(std::uint32_t poly, std::uint32_t raw, const void* data, std::size_t len, std::uint32_t* out_raw) {
+  if (out_raw == nullptr || (data == nullptr && len != 0)) return TKV_INVALID_ARGUMENT;
+  *out_raw = len ? span_update(tables(poly), raw, static_cast<const unsigned char*>(data), len) : raw;
+  return TKV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tkv_crc32_update_host(uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
+  return update_host(TKV_CRC32_POLYNOMIAL, raw_state, data, len, out_raw);
+}
+
+int tkv_crc32c_update_host(uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
+  return update_host(0x82F63B78u, raw_state, data, len, out_raw);
+}
+
+}  // extern "C"

@@ -42,9 +42,21 @@ int main(int argc, char** argv) {
     const int rreps = 200000;
     for (int i = 0; i < rreps; ++i) sink ^= ref_crc32(buf.data() + (i & 255), n);
     const double ref_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / rreps;
-    const bool same = frankie::core::crc32{}.update({p, n}).finalize() == ref_crc32(buf.data(), n);
-    std::printf("{\"row\": \"drop_in_update\", \"bytes\": %zu, \"gpu_us_per_call\": %.2f, \"reference_cpu_us_per_call\": %.3f, "
-                "\"bit_exact\": %s, \"sink\": %u}\n", n, gpu_us, ref_us, same ? "true" : "false", sink & 1u);
+    // the opt-in host span path (what the drop-in runs for spans <= TKV_DROPIN_HOST_MAX)
+    t0 = clk::now();
+    for (int i = 0; i < rreps; ++i) {
+      std::uint32_t r = 0;
+      (void)tkv_crc32_update_host(0xFFFFFFFFu, buf.data() + (i & 255), n, &r);
+      sink ^= r;
+    }
+    const double host_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / rreps;
+    std::uint32_t hr = 0;
+    (void)tkv_crc32_update_host(0xFFFFFFFFu, buf.data(), n, &hr);
+    const bool same = frankie::core::crc32{}.update({p, n}).finalize() == ref_crc32(buf.data(), n) &&
+                      (hr ^ 0xFFFFFFFFu) == ref_crc32(buf.data(), n);
+    std::printf("{\"row\": \"drop_in_update\", \"bytes\": %zu, \"gpu_us_per_call\": %.2f, \"host_span_us_per_call\": %.3f, "
+                "\"reference_cpu_us_per_call\": %.3f, \"bit_exact\": %s, \"sink\": %u}\n", n, gpu_us, host_us, ref_us,
+                same ? "true" : "false", sink & 1u);
   }
   // group commit: N records of 36 bytes stamped in one call (wal.cpp:54-58 per record)
   for (std::size_t nrec : {1ul, 16ul, 256ul, 4096ul}) {

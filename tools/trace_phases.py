@@ -36,6 +36,20 @@ def main():
             span = int(rows[b - 1]["End_Timestamp"]) - int(rows[a]["Start_Timestamp"])
             ph["span_per_step_us"] = round(span / len(d) / 1e3, 2)
         out["phases"][name] = ph
+    # Every kernel of the timed steps: those that start after the last warm-up anchor ends and
+    # before the last timed anchor ends, with their mean duration and the idle time between launches.
+    allk = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+    lo = int(rows[warm - 1]["End_Timestamp"]) if warm else 0
+    hi = int(rows[warm + steps - 1]["End_Timestamp"])
+    win = [r for r in allk if lo <= int(r["Start_Timestamp"]) < hi]
+    per = {}
+    for r in win:
+        per.setdefault(r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-48:], []).append(
+            int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    out["timed_step_kernels"] = {k: {"launches": len(v), "avg_us": round(sum(v) / len(v) / 1e3, 2),
+                                     "min_us": round(min(v) / 1e3, 2)} for k, v in per.items()}
+    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win)
+    out["timed_idle_us_per_step"] = round(((hi - lo) - busy) / steps / 1e3, 2)
     print(json.dumps(out, indent=1))
 
 
