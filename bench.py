@@ -124,7 +124,7 @@ def pmc_traffic(csv_path, config):
     to the stream-mode kernels, and cfg5 had none in round 1)."""
     import csv
     from collections import defaultdict
-    step_kernels = (("crc_rows", "crc_stream", "stream_finish", "rows_tile_scan", "rows_scan_tiles",
+    step_kernels = (("crc_rows", "crc_stream", "rows_tile_scan", "rows_scan_tiles",
                      "rows_finish", "crc_fixup") if config == "cfg4" else ("crc_packed",))
     path = csv_path
     if path is None:

@@ -1,7 +1,7 @@
 """Irregular batches whose blocks lie back to back (each at least 64 bytes) take the byte-stream row
 walk: the prepass chooses it on the device, the row kernel walks full 4 KiB rows of
-the stream and records a (Y, Q) pair at every block end and a register per wave, and stream_finish
-turns those into block CRCs. Every case is compared block by block with the oracle (crc32.cpp:9-16 restated),
+the stream and records a (Y, Q) pair at every block end and a register per wave, and the general row
+kernel's launch (which has no rows to walk then) turns those into block CRCs. Every case is compared block by block with the oracle (crc32.cpp:9-16 restated),
 and the path actually taken is read back with tkv_debug_irregular_mode."""
 import ctypes
 

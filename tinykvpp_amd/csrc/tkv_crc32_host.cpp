@@ -32,7 +32,7 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
                           std::uint32_t* counts, std::uint64_t* sinfo, std::uint64_t* ends, const PrepassOut& o,
                           std::uint32_t W, std::uint32_t ncu, std::uint32_t* out, std::uint32_t* row0,
                           hipStream_t st);
-hipError_t launch_stream_tail(const RowsArgs& a, hipStream_t st, unsigned grid);
+hipError_t launch_stream_rows(const RowsArgs& a, hipStream_t st, unsigned grid);
 std::uint64_t prepass_tiles(std::uint64_t n);
 hipError_t launch_fill_uniform(std::uint8_t* dst, std::uint64_t stride, std::uint64_t len, std::uint64_t first,
                                std::uint64_t nblocks, std::uint64_t seed, hipStream_t st);
@@ -476,8 +476,10 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   a.s_wv = s->po.big_idx;
   TKV_HIP(launch_prepass(d_base, d_off, d_len, a.nblocks, s->scan, s->tiles, s->tile_ok, s->counts, sinfo, s->po.big_off,
                          s->po, a.nwaves, static_cast<std::uint32_t>(c->ncu), d_out, row0, st));
-  TKV_HIP(launch_rows(a, false, false, static_cast<unsigned>(c->ncu), st));  // combines its own seams
-  TKV_HIP(launch_stream_tail(a, st, static_cast<unsigned>(c->ncu)));
+  // stream mode: crc_stream walks the rows and crc_rows finishes the block CRCs; general path:
+  // crc_stream returns at once and crc_rows walks the rows (and combines its own seams)
+  TKV_HIP(launch_stream_rows(a, st, static_cast<unsigned>(c->ncu)));
+  TKV_HIP(launch_rows(a, false, false, static_cast<unsigned>(c->ncu), st));
   return TKV_OK;
 }
 

@@ -38,13 +38,58 @@ struct Shape {
   static constexpr int kIlp = 2;
 };
 
+// ---- stream mode: every block's CRC from crc_stream's per-end and per-wave registers -----------------
+// Run by crc_rows<false, false>, which is launched after crc_stream and has nothing else to do on a
+// stream-mode batch: the finish rides on that launch instead of a launch of its own.
+// x^(8d) mod P for any byte distance d.
+__device__ __forceinline__ std::uint32_t stream_x8n(const DeviceTables* t, std::uint64_t d) {
+  return dev::multmodp(dev::shift_rows_tab(t, 0x80000000u, static_cast<std::uint32_t>(d >> 12)),
+                       t->head_shift[d & 4095u][31], t->poly);
+}
+
+// Block b = [E[b-1], E[b]) of the stream (block 0 starts at the stream start s0; the bytes of row 0
+// before it were read as zeros). Let S(e) = crc_0(stream bytes [0, e)), wave w hold rows
+// [g0(w), g1(w)) with T_w = s_wtot[w] = crc_0 of those rows alone, and
+// L(e) = crc_0(bytes of e's wave up to e) = Shift_(rowend - e)^-1 (Y) ^ Q from the row kernel. Then
+// S(e) = Shift_(e - 4096 g0(w))(S(4096 g0(w))) ^ L(e), and S at a wave start is the sum of the earlier
+// waves' T_v each shifted to that point, so with e' = E[b-1] in wave w' and e = E[b] in wave w:
+//   crc_0(block) = S(e) ^ Shift_len(S(e')) = L(e) ^ Shift_len(L(e')) ^ sum_{w' <= v < w} Shift_(e - 4096 g1(v))(T_v)
+// (the wave sums before w' cancel). Most blocks lie in one wave and the last sum is empty. For
+// block 0, L(s0) = 0 and w' = 0. The register from init is Shift_len(init) ^ crc_0(block).
+__device__ __forceinline__ void stream_finish_block(const RowsArgs& a, std::uint64_t b) {
+  const DeviceTables* t = a.tabs;
+  const std::uint32_t poly = t->poly;
+  auto L = [&](std::uint64_t e, std::uint64_t yq) -> std::uint32_t {
+    const std::uint64_t rowend = ((e - 1) / kRow + 1) * kRow;
+    return dev::multmodp(t->inv_shift[rowend - e], static_cast<std::uint32_t>(yq), poly) ^
+           static_cast<std::uint32_t>(yq >> 32);
+  };
+  const std::uint64_t e = a.s_ends[b];
+  const std::uint64_t ep = b ? a.s_ends[b - 1] : 0;
+  const std::uint64_t len = b ? e - ep : e - a.s_info[1];
+  std::uint32_t crc0 = L(e, a.s_yq[b]);
+  const std::uint32_t w = a.s_wv[b], wp = b ? a.s_wv[b - 1] : 0u;
+  for (std::uint32_t v = wp; v < w; ++v)
+    crc0 ^= dev::multmodp(stream_x8n(t, e - static_cast<std::uint64_t>(a.s_row0[v + 1]) * kRow), a.s_wtot[v], poly);
+  const std::uint32_t lp = b ? L(ep, a.s_yq[b - 1]) : 0u;
+  const std::uint32_t init = a.init_raw ? a.init_raw[b] : a.init_default;
+  const std::uint32_t raw = dev::multmodp(stream_x8n(t, len), init ^ lp, poly) ^ crc0;
+  a.out[b] = raw ^ a.out_xor;
+}
+
 template <bool ALIGNED, bool UNIFORM>
 __global__ __launch_bounds__(kRowsThreads) void crc_rows(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   if constexpr (!UNIFORM) {
-    // irregular batch whose blocks lie back to back: the prepass chose the byte-stream row walk
-    // (crc_stream, launched next)
-    if (dev::sload32(a.counts, 3) == kModeStream) return;
+    // irregular batch whose blocks lie back to back: the prepass chose the byte-stream row walk,
+    // crc_stream (launched just before) has walked it, and this launch turns its registers into
+    // block CRCs
+    if (dev::sload32(a.counts, 3) == kModeStream) {
+      const std::uint64_t step = static_cast<std::uint64_t>(gridDim.x) * blockDim.x;
+      for (std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x; b < a.nblocks; b += step)
+        stream_finish_block(a, b);
+      return;
+    }
   }
   // issue priority from the rows left (set_prio_from_left): +0.7 % on cfg4 (profiles/r1/launch_irr_pri3.txt)
   dev::crc_rows_body<ALIGNED, UNIFORM, Shape<ALIGNED>::kDepth, Shape<ALIGNED>::kIlp, 3>(a, lds);
@@ -318,45 +363,6 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
   finish_block(off, len, b, sc + tile_off, total >> 32, o, W, out);
 }
 
-// ---- stream mode: every block's CRC from the row kernel's per-end and per-wave registers ------------
-// x^(8d) mod P for any byte distance d.
-__device__ __forceinline__ std::uint32_t stream_x8n(const DeviceTables* t, std::uint64_t d) {
-  return dev::multmodp(dev::shift_rows_tab(t, 0x80000000u, static_cast<std::uint32_t>(d >> 12)),
-                       t->head_shift[d & 4095u][31], t->poly);
-}
-
-// Block b = [E[b-1], E[b]) of the stream (block 0 starts at the stream start s0; the bytes of row 0
-// before it were read as zeros). Let S(e) = crc_0(stream bytes [0, e)), wave w hold rows
-// [g0(w), g1(w)) with T_w = s_wtot[w] = crc_0 of those rows alone, and
-// L(e) = crc_0(bytes of e's wave up to e) = Shift_(rowend - e)^-1 (Y) ^ Q from the row kernel. Then
-// S(e) = Shift_(e - 4096 g0(w))(S(4096 g0(w))) ^ L(e), and S at a wave start is the sum of the earlier
-// waves' T_v each shifted to that point, so with e' = E[b-1] in wave w' and e = E[b] in wave w:
-//   crc_0(block) = S(e) ^ Shift_len(S(e')) = L(e) ^ Shift_len(L(e')) ^ sum_{w' <= v < w} Shift_(e - 4096 g1(v))(T_v)
-// (the wave sums before w' cancel). Most blocks lie in one wave and the last sum is empty. For
-// block 0, L(s0) = 0 and w' = 0. The register from init is Shift_len(init) ^ crc_0(block).
-__global__ void stream_finish(RowsArgs a) {
-  if (dev::sload32(a.counts, 3) != kModeStream) return;
-  const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
-  if (b >= a.nblocks) return;
-  const DeviceTables* t = a.tabs;
-  const std::uint32_t poly = t->poly;
-  auto L = [&](std::uint64_t e, std::uint64_t yq) -> std::uint32_t {
-    const std::uint64_t rowend = ((e - 1) / kRow + 1) * kRow;
-    return dev::multmodp(t->inv_shift[rowend - e], static_cast<std::uint32_t>(yq), poly) ^
-           static_cast<std::uint32_t>(yq >> 32);
-  };
-  const std::uint64_t e = a.s_ends[b];
-  const std::uint64_t ep = b ? a.s_ends[b - 1] : 0;
-  const std::uint64_t len = b ? e - ep : e - a.s_info[1];
-  std::uint32_t crc0 = L(e, a.s_yq[b]);
-  const std::uint32_t w = a.s_wv[b], wp = b ? a.s_wv[b - 1] : 0u;
-  for (std::uint32_t v = wp; v < w; ++v)
-    crc0 ^= dev::multmodp(stream_x8n(t, e - static_cast<std::uint64_t>(a.s_row0[v + 1]) * kRow), a.s_wtot[v], poly);
-  const std::uint32_t lp = b ? L(ep, a.s_yq[b - 1]) : 0u;
-  const std::uint32_t init = a.init_raw ? a.init_raw[b] : a.init_default;
-  const std::uint32_t raw = dev::multmodp(stream_x8n(t, len), init ^ lp, poly) ^ crc0;
-  a.out[b] = raw ^ a.out_xor;
-}
 
 // ---- synthetic data: byte j of block b = LE byte j%8 of
 //      splitmix64((b << 24) ^ (j >> 3) ^ (seed << 56)). Test/bench input generation only. ----------
@@ -473,13 +479,12 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
 }
 
 
-// Stream-mode tail of an irregular batch (both kernels return at once unless the prepass chose
-// stream mode): the row walk over the whole stream, then one thread per block.
-hipError_t launch_stream_tail(const RowsArgs& a, hipStream_t st, unsigned grid) {
+// Stream-mode row walk of an irregular batch (returns at once unless the prepass chose stream mode);
+// launched before crc_rows<false, false>, which finishes the block CRCs.
+hipError_t launch_stream_rows(const RowsArgs& a, hipStream_t st, unsigned grid) {
   RowsArgs b = a;
   b.nwaves = grid * (kStreamThreads / 64);
   hipLaunchKernelGGL(crc_stream, dim3(grid), dim3(kStreamThreads), 0, st, b);
-  hipLaunchKernelGGL(stream_finish, dim3((a.nblocks + 255u) / 256u), dim3(256), 0, st, b);
   return hipGetLastError();
 }
 
