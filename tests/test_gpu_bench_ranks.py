@@ -1,0 +1,55 @@
+"""bench.py's multi-rank code path on the one GPU of a test box, launched the way the driver launches
+the scaling runs (python -m torch.distributed.run ... bench.py --gpus N):
+
+* one rank over RCCL with TKV_BENCH_FORCE_DIST=1: the process group, the barriers around the timed
+  steps and the max/min/sum reductions run on the device, as on an 8-GPU node;
+* two ranks sharing the GPU over gloo (TKV_BENCH_BACKEND=gloo): rank 1 checksums global blocks
+  [1 M, 2 M), which only its committed golden shard aggregate can check, and ranks_seen must be 2.
+
+Each line must report every block of every rank's shard bit-exact against tests/golden/synthetic.json
+(written from the reference's own crc32.cpp by tests/golden/make_golden.py)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_bench(nproc, extra_env, config="cfg2"):
+    env = dict(os.environ, **extra_env)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(nproc), "--config", config, "--steps", "3", "--warmup", "1", "--min-warmup-ms", "0",
+           "--no-cpu-baseline", "--no-pipelined"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints the one line
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_bench_one_rank_over_rccl(gpu):
+    line = run_bench(1, {"TKV_BENCH_FORCE_DIST": "1"})
+    assert line["n_gpus"] == 1 and line["ranks_seen"] == 1
+    assert line["bit_exact"] is True
+    assert line["bit_exact_scope"].startswith("every block of every rank's shard")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["cfg2", "cfg4"])
+def test_bench_two_ranks_share_the_gpu(gpu, config):
+    line = run_bench(2, {"TKV_BENCH_BACKEND": "gloo"}, config)
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2
+    assert line["bit_exact"] is True
+    assert line["bit_exact_scope"].startswith("every block of every rank's shard")
