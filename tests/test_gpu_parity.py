@@ -107,6 +107,26 @@ def test_update_chaining_raw_state(gpu, oracle):
     assert c.finalize() == oracle.crc(d)
 
 
+def test_update_latency_path_every_length(gpu, oracle):
+    """Host spans of up to 16 KiB take the one-workgroup latency kernel (crc_span): every length
+    0..300, then a sweep to 16 KiB and just past it (the staged path), from random raw registers,
+    for both polynomials, each against the oracle (crc32.cpp:9-16 restated)."""
+    rng = np.random.default_rng(21)
+    buf = rng.integers(0, 256, (16 << 10) + 64, dtype=np.uint8).tobytes()
+    lens = list(range(301)) + list(range(301, 16 << 10, 97)) + [4095, 4096, 4097, (16 << 10) - 1, 16 << 10,
+                                                               (16 << 10) + 1, (16 << 10) + 63]
+    for n in lens:
+        raw = int(rng.integers(0, 2**32))
+        c = tk.crc32()
+        c._crc = raw
+        assert c.update(buf[:n]).raw == oracle.update(raw, buf[:n]), n
+    for n in (0, 1, 5, 36, 1000, 4097, 16 << 10):
+        raw = int(rng.integers(0, 2**32))
+        c = tk.crc32c()
+        c._crc = raw
+        assert c.update(buf[:n]).raw == oracle.update_c(raw, buf[:n]), n
+
+
 def test_odd_prefixes(gpu, oracle):
     g = golden("odd.json")
     buf = oracle.fill(g["seed"], g["block"], 0, 1 << 20)
@@ -401,6 +421,26 @@ def test_host_batch(gpu, oracle):
     assert np.array_equal(got, oracle.batch(host, offs, lens))
     got = tk.crc32_batch_host(host, offs, lens, devices=[0])
     assert np.array_equal(got, oracle.batch(host, offs, lens))
+
+
+@pytest.mark.parametrize("n,maxlen", [(1, 36), (2, 5), (17, 4096), (256, 200), (256, 256), (257, 40),
+                                      (3, 16 << 10), (4, 16 << 10), (40, 2000)])
+def test_host_small_batches(gpu, oracle, n, maxlen):
+    """Host batches of at most 256 spans of at most 16 KiB and 64 KiB in all (a WAL group commit)
+    take the one-launch latency path (crc_span, a workgroup per span); 257 spans, or more than
+    64 KiB in all, take the staged pipeline. Both against the oracle, with and without per-block
+    initial registers, both polynomials, lengths from 0, unaligned offsets."""
+    rng = np.random.default_rng(n * 7 + maxlen)
+    host = rng.integers(0, 256, n * maxlen + 64, dtype=np.uint8)
+    lens = rng.integers(0, maxlen + 1, n).astype(np.uint32)
+    lens[0] = maxlen
+    offs = np.array([int(rng.integers(0, host.size - int(ln))) for ln in lens], np.uint64)
+    assert np.array_equal(tk.crc32_batch_host(host, offs, lens), oracle.batch(host, offs, lens))
+    init = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    assert np.array_equal(tk.crc32_batch_host(host, offs, lens, init_raw=init), oracle.batch(host, offs, lens, init))
+    got_c = tk.crc32_batch_host(host, offs, lens, algo="crc32c")
+    want_c = [oracle.crc_c(host[int(o):int(o) + int(ln)].tobytes()) for o, ln in zip(offs, lens)]
+    assert [int(x) for x in got_c] == want_c
 
 
 def test_host_batch_block_larger_than_slab(gpu, oracle):

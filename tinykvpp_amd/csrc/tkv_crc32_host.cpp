@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -34,6 +35,9 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
                           hipStream_t st);
 hipError_t launch_stream_rows(const RowsArgs& a, hipStream_t st, unsigned grid);
 std::uint64_t prepass_tiles(std::uint64_t n);
+hipError_t launch_span(const std::uint8_t* stage, const SpanDesc& one, const SpanDesc* desc, std::uint32_t n,
+                       std::uint32_t out_xor, std::uint32_t* out, std::uint32_t* count, std::uint32_t base,
+                       std::uint32_t* done, std::uint32_t seq, const DeviceTables* tabs, hipStream_t st);
 hipError_t launch_fill_uniform(std::uint8_t* dst, std::uint64_t stride, std::uint64_t len, std::uint64_t first,
                                std::uint64_t nblocks, std::uint64_t seed, hipStream_t st);
 hipError_t launch_fill_blocks(std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
@@ -173,11 +177,15 @@ struct StreamScratch {
   std::uint64_t cap_blocks = 0;
 };
 
-// Spans up to this size take update()'s latency path (mapped pinned memory, one launch): measured
-// 24-26 us per call up to 4 KiB against ~30 us through the copy engines; past ~16 KiB the kernel's
-// own reads across PCIe cost more than the copies (256 KiB: 116 us mapped vs 50 us copied).
-// TKV_UPDATE_SMALL_BYTES overrides the threshold (0 disables the path; for A/B measurements).
-constexpr std::size_t kSmallSpan = std::size_t(16) << 10;
+// Spans up to this size take update()'s latency path (mapped pinned memory, one crc_span launch,
+// ~11 us per call up to 4 KiB, profiles/r2/put_latency/run*.jsonl); past ~16 KiB the kernel's
+// own reads across PCIe cost more than copies through the copy engines (256 KiB: 116 us mapped vs
+// 50 us copied, measured with the earlier row-kernel path). Host batches of at most kSpanBatchMax
+// such spans and kSpanStage bytes in all take the same kernel (one workgroup per span).
+// TKV_UPDATE_SMALL_BYTES overrides the threshold (0 disables both paths; for A/B measurements).
+constexpr std::size_t kSmallSpan = std::size_t(16) << 10;  // longest span for crc_span (its kSpanMax)
+constexpr std::size_t kSpanStage = std::size_t(64) << 10;  // mapped staging of the short-span paths
+constexpr std::uint32_t kSpanBatchMax = 256;                // spans per launch on the small-batch path
 std::size_t small_span_limit() {
   static const std::size_t v = [] {
     const char* e = std::getenv("TKV_UPDATE_SMALL_BYTES");
@@ -307,11 +315,16 @@ struct DevCtx {
   std::uint32_t* d_io = nullptr;
   std::uint32_t* h_io = nullptr;
   std::size_t stage_cap = 0;
-  // small spans: mapped pinned buffers the kernel reads and writes in place (no copy engines)
+  // short spans (crc_span): mapped pinned buffers the kernel reads and writes in place (no copy
+  // engines): span bytes, descriptors, and results followed by the done count (coherent)
   std::uint8_t* h_small = nullptr;
   const std::uint8_t* d_small = nullptr;  // device view of h_small
+  SpanDesc* h_desc = nullptr;
+  const SpanDesc* d_desc = nullptr;
   std::uint32_t* h_res = nullptr;
   std::uint32_t* d_res = nullptr;         // device view of h_res
+  std::uint32_t span_count = 0;           // spans counted on d_io[2] by all crc_span launches so far
+  std::uint32_t span_seq = 0;             // sequence number of the last crc_span launch
   // host-memory batch pipeline, kept between calls (guarded by pipe_mu)
   std::mutex pipe_mu;
   std::unique_ptr<HostPipe> pipe;
@@ -780,30 +793,91 @@ int update_device_impl(int algo, uint32_t raw_state, const void* d_data, size_t 
   return run_uniform(c, algo, base, len, len, nullptr, raw_state, 0u, d_out_raw, 1, static_cast<hipStream_t>(stream));
 }
 
+// One launch of crc_span over n spans already in the mapped staging (n == 1: `one`, else the mapped
+// descriptors), then a poll of the mapped done word for this launch's sequence number, which the
+// kernel releases after every result: polling saves ~5 us per call against sleeping in
+// hipStreamSynchronize. After 100 ms without it, hipStreamSynchronize reports whatever held the
+// kernel up. The span counter on the device (d_io[2]) only grows; the launch is done when it
+// reaches span_count + n. Caller holds upd_mu.
+int run_spans(DevCtx* c, int algo, const SpanDesc& one, std::uint32_t n, std::uint32_t out_xor, std::uint32_t* out) {
+  std::uint32_t* done = c->h_res + kSpanBatchMax;
+  if (++c->span_seq == 0) c->span_seq = 1;
+  const std::uint32_t seq = c->span_seq, base = c->span_count;
+  TKV_HIP(launch_span(c->d_small, one, n == 1 ? nullptr : c->d_desc, n, out_xor, c->d_res, c->d_io + 2, base,
+                      c->d_res + kSpanBatchMax, seq, c->d_tabs[algo], c->st));
+  if (n > 1) c->span_count = base + n;  // a one-span launch does not count
+  const auto t0 = std::chrono::steady_clock::now();
+  for (std::uint32_t i = 0; __atomic_load_n(done, __ATOMIC_ACQUIRE) != seq; ++i) {
+    if ((i & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100)) {
+      TKV_HIP(hipStreamSynchronize(c->st));
+      if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq) return fail(TKV_IO_ERROR, "span kernel did not report");
+      break;
+    }
+  }
+  for (std::uint32_t i = 0; i < n; ++i) out[i] = __atomic_load_n(c->h_res + i, __ATOMIC_RELAXED);
+  return TKV_OK;
+}
+
+// The latency paths' stream and mapped buffers, created on first use. Caller holds upd_mu.
+int ensure_upd(DevCtx* c) {
+  if (!c->st) {
+    TKV_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_io), 16, hipHostMallocDefault));
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&c->d_io), 16));  // [0]: staged update result, [2]: span count
+    TKV_HIP(hipMemset(c->d_io, 0, 16));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_small), kSpanStage, hipHostMallocMapped));
+    TKV_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(const_cast<std::uint8_t**>(&c->d_small)), c->h_small, 0));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_desc), sizeof(SpanDesc) * kSpanBatchMax, hipHostMallocMapped));
+    TKV_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(const_cast<SpanDesc**>(&c->d_desc)), c->h_desc, 0));
+    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_res), sizeof(std::uint32_t) * (kSpanBatchMax + 1),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    TKV_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_res), c->h_res, 0));
+  }
+  return TKV_OK;
+}
+
+// Small host batch (a WAL group commit of a few records, a few SSTable blocks) on the latency path:
+// every block copied to a 16-byte aligned position of the mapped staging, one crc_span launch with
+// a workgroup per block, finalize() values out. Returns 1 (nothing done) when the batch does not fit.
+int span_batch(DevCtx* c, int algo, const uint8_t* h_base, const uint64_t* h_offsets, const uint32_t* h_lengths,
+               const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
+  if (n > kSpanBatchMax) return 1;
+  std::uint64_t total = 0;
+  for (std::uint64_t i = 0; i < n; ++i) {
+    if (h_lengths[i] > small_span_limit()) return 1;
+    total += (static_cast<std::uint64_t>(h_lengths[i]) + 15u) & ~15ull;
+  }
+  if (total > kSpanStage) return 1;
+  std::lock_guard<std::mutex> lk(c->upd_mu);
+  if (int rc = ensure_upd(c)) return rc;
+  std::uint32_t pos = 0;
+  for (std::uint64_t i = 0; i < n; ++i) {
+    const std::uint32_t len = h_lengths[i];
+    if (len) std::memcpy(c->h_small + pos, h_base + h_offsets[i], len);
+    c->h_desc[i] = SpanDesc{pos, len, h_init_raw ? h_init_raw[i] : kInit, 0};
+    pos += (len + 15u) & ~15u;
+  }
+  return run_spans(c, algo, c->h_desc[0], static_cast<std::uint32_t>(n), kInit, h_out_final);
+}
+
 int update_impl(int algo, uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
   if (!ptr_ok(out_raw) || (len && !ptr_ok(data))) return fail(TKV_INVALID_ARGUMENT, "null pointer");
   DevCtx* c = nullptr;
   if (int rc = get_ctx(&c)) return rc;
   std::lock_guard<std::mutex> lk(c->upd_mu);
-  if (!c->st) {
-    TKV_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_io), 16, hipHostMallocDefault));
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&c->d_io), 16));
-    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_small), kSmallSpan, hipHostMallocMapped));
-    TKV_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(const_cast<std::uint8_t**>(&c->d_small)), c->h_small, 0));
-    TKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_res), 64,
-                          hipHostMallocMapped | hipHostMallocCoherent));
-    TKV_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_res), c->h_res, 0));
-  }
+  if (int rc = ensure_upd(c)) return rc;
   if (len <= small_span_limit()) {
-    // Latency path (one WAL record per call, wal.cpp:54-57): the kernel reads the span from mapped
-    // pinned memory and writes the register back into mapped memory - one launch and one sync,
-    // no copy-engine round trips.
-    if (len) std::memcpy(c->h_small, data, len);
-    const std::uint8_t* base = len ? c->d_small : c->d_dummy;
-    if (int rc = run_uniform(c, algo, base, len, len, nullptr, raw_state, 0u, c->d_res, 1, c->st)) return rc;
-    TKV_HIP(hipStreamSynchronize(c->st));
-    *out_raw = *reinterpret_cast<volatile std::uint32_t*>(c->h_res);
+    // Latency path (one WAL record per call, wal.cpp:54-57): one small kernel (crc_span) reads the
+    // span from mapped pinned memory and writes the register back into mapped memory - one launch
+    // and one sync, no copy-engine round trips. An empty span leaves the register as it is
+    // (crc32.cpp:9-16 loops zero times).
+    if (len == 0) {
+      *out_raw = raw_state;
+      return TKV_OK;
+    }
+    std::memcpy(c->h_small, data, len);
+    const SpanDesc one{0, static_cast<std::uint32_t>(len), raw_state, 0};
+    return run_spans(c, algo, one, 1, 0u, out_raw);
     return TKV_OK;
   }
   const std::size_t want = std::min<std::size_t>(std::max<std::size_t>(len, 1 << 16), kSlab);
@@ -865,6 +939,7 @@ int batch_host_impl(int algo, const uint8_t* h_base, const uint64_t* h_offsets, 
     return fail(TKV_INVALID_ARGUMENT, "null pointer");
   DevCtx* c = nullptr;
   if (int rc = get_ctx(&c)) return rc;
+  if (int rc = span_batch(c, algo, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, n); rc != 1) return rc;
   return host_batch(c, algo, h_base, h_offsets, h_lengths, h_init_raw, h_out_final, 0, n);
 }
 

@@ -105,6 +105,12 @@ struct RowsArgs {
   std::uint32_t* s_wv;               // per block: the wave that met its end (crc_stream_body)
 };
 constexpr std::uint32_t kModeStream = 1;
+
+// One short host span for crc_span: `len` bytes at byte `pos` (16-byte aligned) of the mapped
+// staging buffer, folded on from raw register `init`.
+struct SpanDesc {
+  std::uint32_t pos, len, init, pad;
+};
 constexpr std::uint32_t kStreamMinLen = 64;  // at most one block end per 64-byte lane segment
 
 // Outputs of the irregular prepass (scratch of one stream).

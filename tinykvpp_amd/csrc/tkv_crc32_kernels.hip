@@ -386,6 +386,77 @@ __global__ void fill_uniform(std::uint8_t* dst, std::uint64_t stride, std::uint6
   }
 }
 
+// Short host spans (crc32::update of one WAL record, wal.cpp:54-57, or a small group commit of a
+// few records): one workgroup of kSpanThreads per span of at most kSpanMax bytes, read from mapped
+// pinned memory at a 16-byte aligned position. Thread i folds dwords [i*per, (i+1)*per) from a
+// zero register with slicing-by-4 lookups into one copy of the tables in LDS (bytes past the
+// span's end in its last dword by Sarwate steps), moves its partial past the bytes that follow its
+// segment (one GF(2) multiply by x^(8d)), and the XOR of all partials plus Shift_len(init) is the
+// new raw register (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). Thread 0 writes register ^ out_xor to
+// out[b] (mapped host memory) and counts the span done on a device-memory counter (release at
+// system scope, so the result has reached the host first); the workgroup that completes the count
+// (counter value base + n - 1: the counter only grows, the host tracks base) writes `seq` to *done in
+// host memory, which the host polls. One PCIe write per launch: a count kept in host memory took
+// one serialized PCIe atomic per span (256 spans: 263 us). The row kernels would fill 160 KiB of LDS
+// per workgroup and need a seam fix-up launch; this is one small launch. One span travels in the
+// kernel arguments (desc == nullptr), more in a descriptor array in mapped memory.
+constexpr unsigned kSpanThreads = 256;
+constexpr std::uint32_t kSpanMax = 16u << 10;  // 16 dwords per thread at most
+__device__ __forceinline__ std::uint32_t span_x8n(const DeviceTables* t, std::uint32_t d) {  // d < 2^24
+  return dev::multmodp(t->rows_shift[d >> 12], t->head_shift[d & 4095u][31], t->poly);
+}
+__global__ __launch_bounds__(kSpanThreads) void crc_span(const std::uint8_t* stage, SpanDesc one, const SpanDesc* desc,
+                                                          std::uint32_t out_xor, std::uint32_t* out, std::uint32_t* count,
+                                                          std::uint32_t base, std::uint32_t* done, std::uint32_t seq,
+                                                          const DeviceTables* t) {
+  __shared__ std::uint32_t tb[4 * 256];
+  __shared__ std::uint32_t part[kSpanThreads / 64];
+  const SpanDesc sd = desc ? desc[blockIdx.x] : one;
+  const std::uint32_t len = sd.len;
+  const std::uint32_t nd = (len + 3u) / 4u;                           // dwords, the last may be partial
+  const std::uint32_t per = (nd + kSpanThreads - 1u) / kSpanThreads;  // <= 16
+  const std::uint32_t d0 = threadIdx.x * per;
+  const std::uint32_t d1 = d0 + per < nd ? d0 + per : nd;
+  const std::uint32_t* src = reinterpret_cast<const std::uint32_t*>(stage + sd.pos);
+  std::uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w[i] = d0 + i < d1 ? src[d0 + i] : 0u;  // all loads issued before the fold
+  for (std::uint32_t u = threadIdx.x; u < 1024u; u += kSpanThreads) tb[u] = t->slice[u >> 8][u & 255u];
+  const std::uint32_t b1 = 4u * d1 < len ? 4u * d1 : len;  // end of this thread's bytes
+  const std::uint32_t shift = span_x8n(t, len - b1);        // independent of the data: overlaps the loads
+  __syncthreads();
+  std::uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const std::uint32_t d = d0 + i;
+    if (d < d1) {
+      if (4u * d + 4u <= len) {
+        const std::uint32_t x = c ^ w[i];
+        c = tb[768u + (x & 255u)] ^ tb[512u + ((x >> 8) & 255u)] ^ tb[256u + ((x >> 16) & 255u)] ^ tb[x >> 24];
+      } else {
+        for (std::uint32_t k = 0; 4u * d + k < len; ++k) c = (c >> 8) ^ tb[(c ^ (w[i] >> (8u * k))) & 255u];
+      }
+    }
+  }
+  std::uint32_t v = d0 < d1 ? dev::multmodp(c, shift, t->poly) : 0u;
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) v ^= __shfl_xor(v, m, 64);
+  if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    std::uint32_t r = dev::multmodp(sd.init, span_x8n(t, len), t->poly);
+#pragma unroll
+    for (unsigned k = 0; k < kSpanThreads / 64; ++k) r ^= part[k];
+    out[blockIdx.x] = r ^ out_xor;
+    if (gridDim.x == 1u) {  // one span (update()): no count to keep
+      __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      const std::uint32_t old = __hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (old == base + gridDim.x - 1u) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // SSTable stamp fix-up (tkv_sst_block_crcs_device): out[i] holds the CRC of image i as it lies, with
 // whatever its crc32_ field holds (bytes [17, 21)). By linearity, the CRC with those bytes read as
 // zero is out[i] ^ crc_0(E), E = the field bytes followed by size-21 zero bytes, and
@@ -485,6 +556,17 @@ hipError_t launch_stream_rows(const RowsArgs& a, hipStream_t st, unsigned grid) 
   RowsArgs b = a;
   b.nwaves = grid * (kStreamThreads / 64);
   hipLaunchKernelGGL(crc_stream, dim3(grid), dim3(kStreamThreads), 0, st, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_span(const std::uint8_t* stage, const SpanDesc& one, const SpanDesc* desc, std::uint32_t n,
+                       std::uint32_t out_xor, std::uint32_t* out, std::uint32_t* count, std::uint32_t base,
+                       std::uint32_t* done, std::uint32_t seq, const DeviceTables* tabs, hipStream_t st) {
+  if (n == 0 || (desc == nullptr && (n != 1 || one.len > kSpanMax || (one.pos & 15u))) ||
+      (reinterpret_cast<std::uintptr_t>(stage) & 15u))
+    return hipErrorInvalidValue;  // the host checks every descriptor's length and alignment
+  hipLaunchKernelGGL(crc_span, dim3(n), dim3(kSpanThreads), 0, st, stage, one, desc, out_xor, out, count, base, done,
+                     seq, tabs);
   return hipGetLastError();
 }
 
