@@ -122,7 +122,9 @@ void split_batches(std::mt19937_64& rng) {
   }
 }
 
-// Several host threads calling into the same device at once (update, host batches, WAL stamp).
+// Several host threads calling into the same device at once: update() on spans of every size
+// (latency kernel up to 16 KiB, staged above), large host batches (staged pipeline), small host
+// batches (one latency-kernel launch) and the host span path.
 void concurrent_callers(std::mt19937_64& rng) {
   std::vector<std::vector<uint8_t>> data;
   for (int t = 0; t < 6; ++t) data.push_back(random_bytes(rng, (size_t(1) << 20) + 12345 * t));
@@ -132,11 +134,28 @@ void concurrent_callers(std::mt19937_64& rng) {
     th.emplace_back([&, t] {
       const auto& d = data[t];
       for (int it = 0; it < 20; ++it) {
-        if (t % 2 == 0) {
-          const size_t n = (it * 7919 + 31 * t) % d.size();
+        if (t % 3 == 0) {
+          const size_t n = it % 2 ? (it * 7919 + 31 * t) % d.size() : (it * 977 + 31 * t) % 20000;
           uint32_t raw = 0;
           if (tkv_crc32_update(0xFFFFFFFFu, d.data(), n, &raw) != TKV_OK || (raw ^ 0xFFFFFFFFu) != oracle_crc32(d.data(), n))
             ++bad[t];
+        } else if (t % 3 == 2) {
+          std::vector<uint64_t> off;
+          std::vector<uint32_t> len;
+          for (int i = 0; i < 1 + (it * 37) % 256; ++i) {
+            off.push_back((static_cast<uint64_t>(i) * 4099u + it) % (d.size() - 300));
+            len.push_back(static_cast<uint32_t>((i * 13 + it) % 250));
+          }
+          std::vector<uint32_t> got(off.size());
+          if (tkv_crc32_batch_host(d.data(), off.data(), len.data(), nullptr, got.data(), off.size()) != TKV_OK) ++bad[t];
+          for (size_t i = 0; i < off.size(); ++i) {
+            uint32_t hr = 0;
+            if (got[i] != oracle_crc32(d.data() + off[i], len[i]) ||
+                tkv_crc32_update_host(0xFFFFFFFFu, d.data() + off[i], len[i], &hr) != TKV_OK || (hr ^ 0xFFFFFFFFu) != got[i]) {
+              ++bad[t];
+              break;
+            }
+          }
         } else {
           std::vector<uint64_t> off;
           std::vector<uint32_t> len;
