@@ -208,3 +208,35 @@ def test_shard_fixtures_are_consistent():
         x ^= shard["xor"]
         s = (s + shard["sum32"]) & 0xFFFFFFFF
     assert (x, s) == (0x5A7EAA3B, 0x9D26EBFD) == (g["cfg5"]["xor"], g["cfg5"]["sum32"])
+
+
+def test_reference_wal_loops(ref_lib):
+    """oracle/_ref's restatement of the reference's recovery loop (wal_entry::decode until the image
+    ends, wal.cpp:63-130) and encode stamp (wal.cpp:54-58) over the reference's own crc32.cpp: the
+    CPU path tools/bench_formats.py times beside the GPU rows. Pinned by the golden records
+    (tests/golden/wal.json, written from the compiled reference)."""
+    import ctypes
+    recs = [bytes.fromhex(r["hex"]) for r in golden("wal.json")["records"]]
+    img = bytearray(b"".join(recs))
+    good, stop = ctypes.c_uint64(), ctypes.c_uint64()
+    ref_lib.ref_wal_verify.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    ref_lib.ref_wal_stamp.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+
+    def verify(b):
+        rc = ref_lib.ref_wal_verify(bytes(b), len(b), ctypes.byref(good), ctypes.byref(stop))
+        return rc, good.value, stop.value
+
+    assert verify(img) == (0, len(recs), len(img))
+    starts = np.cumsum([0] + [len(r) for r in recs])
+    bad = bytearray(img)
+    bad[int(starts[3]) + 20] ^= 0x40  # a CRC-covered byte of record 3 (its key_len): CRC mismatch there
+    assert verify(bad) == (4, 3, int(starts[3]))
+    assert verify(img[:-1]) == (4, len(recs) - 1, int(starts[-2]))  # torn tail
+    zeroed = bytearray(img)
+    for s in starts[:-1]:
+        zeroed[int(s) + 4:int(s) + 8] = b"\0\0\0\0"
+    offs = np.array(starts[:-1], np.uint64)
+    sizes = np.array([len(r) for r in recs], np.uint32)
+    buf = ctypes.create_string_buffer(bytes(zeroed), len(zeroed))
+    ref_lib.ref_wal_stamp(buf, offs.ctypes.data, sizes.ctypes.data, len(recs))
+    assert buf.raw[:len(img)] == bytes(img)

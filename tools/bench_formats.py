@@ -9,8 +9,11 @@
   sst_device   tkv_sst_block_crcs_device over the same images resident in HBM (kernel + fix-up)
   crc32c_cfg2  CRC-32C over 1 M x 4 KiB device-resident blocks (cfg2 shape)
 
-Host-memory rows include the PCIe copies (pageable source: host memcpy into pinned staging); the
-CPU column times the oracle's reference loop on a bounded sample of the same records, 1 thread.
+Host-memory rows include the PCIe copies (pageable source: host memcpy into pinned staging). Beside
+each row, "cpu_reference" times the reference's own path on one host core over the same bytes: its
+crc32.cpp compiled into oracle/_ref, driven by oracle/ref_shim.cpp's restatement of wal_entry::decode's
+loop (recovery), encode's stamp (group commit), or one crc32 per block (SSTable), with the results
+checked against the GPU's. The reference is single-threaded on these paths.
 """
 import ctypes
 import json
@@ -32,6 +35,22 @@ torch.cuda.set_device(0)
 tk.set_device(0)
 lib = tk.load_library()
 ora = Oracle(os.path.join(ROOT, "oracle", "liboracle.so"))
+ref = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref_crc32.so"))
+ref.ref_wal_verify.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+ref.ref_wal_stamp.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+ref.ref_crc32_irregular.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+
+
+def cpu_ref(nbytes, secs, agrees, what):
+    return {"cpu_reference": {"GB/s": round(nbytes / secs / 1e9, 3), "ms": round(secs * 1e3, 1), "cores": 1,
+                              "kind": "reference", "what": what, "agrees_with_gpu": bool(agrees)}}
+
+
+def ref_wal_verify(img):
+    g, p = ctypes.c_uint64(), ctypes.c_uint64()
+    t0 = time.perf_counter()
+    rc = ref.ref_wal_verify(ctypes.c_void_p(img.ctypes.data), img.size, ctypes.byref(g), ctypes.byref(p))
+    return time.perf_counter() - t0, ("ok" if rc == 0 else "corrupted", g.value, p.value)
 rng = np.random.default_rng(1)
 GiB = 1 << 30
 
@@ -79,13 +98,15 @@ def stamp():
 
 
 t = timeit(stamp)
-# CPU reference on a sample of records (payload [8, size) per record, wal.cpp:54-57)
-samp = 20_000
+# the reference's encode stamp over the same records, on a copy (wal.cpp:54-58), one core
+wal_ref = wal.copy()
 t0 = time.perf_counter()
-for o, s in zip(offs[:samp], size[:samp]):
-    ora.crc(wal[int(o) + 8:int(o) + int(s)].tobytes())
-cpu = (time.perf_counter() - t0) / samp * n_rec
-emit("wal_stamp", total, t, n_rec, {"records": n_rec, "cpu_1core_GB/s_incl_python_loop": round(total / cpu / 1e9, 3)})
+ref.ref_wal_stamp(ctypes.c_void_p(wal_ref.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                  ctypes.c_void_p(sizes32.ctypes.data), n_rec)
+cpu = time.perf_counter() - t0
+emit("wal_stamp", total, t, n_rec, {"records": n_rec, **cpu_ref(total, cpu, np.array_equal(wal_ref, wal),
+                                                                 "wal_entry::encode's stamp per record")})
+del wal_ref
 
 good, stop = ctypes.c_uint64(), ctypes.c_uint64()
 
@@ -96,7 +117,10 @@ def verify():
 
 
 t = timeit(verify)
-emit("wal_verify", total, t, n_rec, {"records": n_rec, "verified": good.value})
+cpu, res = ref_wal_verify(wal)
+emit("wal_verify", total, t, n_rec, {"records": n_rec, "verified": good.value,
+                                     **cpu_ref(total, cpu, res == ("ok", good.value, stop.value),
+                                               "wal_entry::decode until the image ends")})
 poffs, plens = offs + 8, (size - 8).astype(np.uint32)
 t = timeit(lambda: tk.crc32_batch_host(wal, poffs, plens))
 emit("wal_payload_batch_host", total, t, n_rec, {"what": "the CRC part of wal_verify alone"})
@@ -155,8 +179,11 @@ tk.check(lib.tkv_wal_stamp(ctypes.c_void_p(swal.ctypes.data), ctypes.c_void_p(so
                            ctypes.c_void_p(ssz32.ctypes.data), n_small))
 assert tk.wal.verify(swal) == ("ok", n_small, stotal)
 t = timeit(lambda: tk.wal.verify(swal), reps=3)
+cpu, res = ref_wal_verify(swal)
 emit("wal_verify_small_records", stotal, t, n_small, {"records": n_small, "mean_record_bytes": round(stotal / n_small, 1),
-                                                     "source": "pageable host image"})
+                                                     "source": "pageable host image",
+                                                     **cpu_ref(stotal, cpu, res == ("ok", n_small, stotal),
+                                                               "wal_entry::decode until the image ends")})
 swal_pin_t = torch.from_numpy(swal).pin_memory()
 t = timeit(lambda: tk.wal.verify(swal_pin_t.numpy()), reps=3)
 emit("wal_verify_small_records_pinned", stotal, t, n_small, {"records": n_small, "source": "pinned host image"})
@@ -189,7 +216,21 @@ def sstamp():
 
 
 t = timeit(sstamp)
-emit("sst_stamp", sfile.nbytes, t, nblk, {"block_image_bytes": int(sizes[0])})
+# the reference's crc32 over each stamped block image with its field read as zero: on a copy with
+# the fields zeroed, one core (the reference never computes these fields; parity unpinned)
+zf = sfile.copy()
+zf[soffs.astype(np.int64)[:, None] + np.arange(17, 21)] = 0
+rcrc = np.zeros(nblk, np.uint32)
+sz32 = sizes.astype(np.uint32)
+t0 = time.perf_counter()
+ref.ref_crc32_irregular(ctypes.c_void_p(zf.ctypes.data), ctypes.c_void_p(soffs.ctypes.data),
+                        ctypes.c_void_p(sz32.ctypes.data), nblk, ctypes.c_void_p(rcrc.ctypes.data))
+cpu = time.perf_counter() - t0
+stamped = sfile[soffs.astype(np.int64)[:, None] + np.arange(17, 21)].copy().view("<u4").ravel()
+emit("sst_stamp", sfile.nbytes, t, nblk, {"block_image_bytes": int(sizes[0]),
+                                          **cpu_ref(sfile.nbytes, cpu, np.array_equal(rcrc, stamped),
+                                                    "crc32 per block image, field as zero")})
+del zf
 assert sst.verify_blocks(sfile, soffs, sizes)[0] == "ok"
 sfile_pin_t = torch.from_numpy(sfile).pin_memory()
 sfile_pin = sfile_pin_t.numpy()
