@@ -841,7 +841,7 @@ int ensure_upd(DevCtx* c) {
 // a workgroup per block, finalize() values out. Returns 1 (nothing done) when the batch does not fit.
 int span_batch(DevCtx* c, int algo, const uint8_t* h_base, const uint64_t* h_offsets, const uint32_t* h_lengths,
                const uint32_t* h_init_raw, uint32_t* h_out_final, uint64_t n) {
-  if (n > kSpanBatchMax) return 1;
+  if (n > kSpanBatchMax || small_span_limit() == 0) return 1;
   std::uint64_t total = 0;
   for (std::uint64_t i = 0; i < n; ++i) {
     if (h_lengths[i] > small_span_limit()) return 1;
