@@ -15,8 +15,8 @@
 //     LDS, the payload zero-padded in front to whole dwords). Larger records (at most two start in a
 //     piece) wait in the piece's slots for one CRC batch through the engine's irregular path.
 //  3. wal_jump: next(k) = the piece holding X_k. The true chain visits the pieces 0, next(0),
-//     next(next(0)), ...; pointer doubling marks exactly those pieces in log2(#pieces) rounds, and
-//     wal_link hands every on-path piece its entry E = X of its predecessor.
+//     next(next(0)), ...; pointer jumping (x4 per round) marks exactly those pieces in
+//     log4(#pieces) rounds, and wal_link hands every on-path piece its entry E = X of its predecessor.
 //  4. wal_count: an on-path piece whose entry is its speculative start keeps its speculative walk
 //     and checks; otherwise it walks again from E (and wal_recheck checks it again). Its speculative
 //     exit was right when the exact walk leaves at the same X (and breaks, or not, the same way).
@@ -51,7 +51,7 @@ constexpr std::uint64_t kWalPiece = 2048;     // bytes of image per speculative 
 constexpr std::uint64_t kWalMeta = 26;        // wal.hpp:21-27 kMetadataSize
 constexpr std::uint32_t kWalLaneMax = 1024;   // payloads up to this size are checked by their lane
 constexpr std::uint64_t kNone = ~0ull;
-constexpr unsigned kScanThreads = 256;        // wal_scan: 16 positions per thread, 4 KiB per workgroup
+constexpr unsigned kScanThreads = 256;        // wal_scan: 16 positions per lane, 62 chunks per wave
 constexpr unsigned kCheckThreads = 1024;      // wal_spec/wal_recheck: one workgroup per CU (128 KiB of LDS)
 
 struct WalArgs {
@@ -70,7 +70,7 @@ struct WalArgs {
   std::uint32_t* slot_len;   //   length, stored CRC, local index)
   std::uint32_t* slot_crc;
   std::uint32_t* slot_loc;
-  std::uint32_t* Ja;         // pointer-doubling jump tables
+  std::uint32_t* Ja;         // pointer-jumping tables
   std::uint32_t* Jb;
   std::uint8_t* on;          // piece is on the true chain
   std::uint8_t* recheck;     // entered off its speculative start: walked and checked again
@@ -110,14 +110,21 @@ __device__ __forceinline__ std::uint64_t gid() {
   return blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
 }
 
-// 1. First plausible header per piece, one coalesced pass over the image. Thread t owns the 16
-// positions of the absolute 16-byte chunk t (relative positions 16t - off0 + j) and holds the 48
-// bytes [16t, 16t + 48) of its chunk in registers. A header at position p has its op and tombstone
-// bytes (p+8, p+17) at 0 or 1 (wal.cpp:30-52): both are tested for all 16 positions at once with
-// byte-parallel arithmetic on the registers, and only positions that pass get the full check
-// (record_len = 18 + klen + vlen, fitting the image; re-read through L1). Chunks are read only when
-// they hold image bytes. A wave covers 1 KiB, i.e. at most two pieces: wave minimum per piece, one
-// atomic per piece and wave.
+// 1. First plausible header per piece, one coalesced pass over the image. Lane l of a wave holds
+// the 16 bytes of absolute chunk t = t_wave + l (one 16-byte load) and reports the 16 positions of
+// that chunk, for l < kScanChunks; the last two lanes only lend their bytes. A header at position p
+// has its op and tombstone bytes (p+8, p+17) at 0 or 1 (wal.cpp:30-52). Each lane marks which of
+// its 16 bytes are 0 or 1 with byte-parallel arithmetic, takes its two right neighbours' marks by
+// cross-lane shifts, and so tests all 16 positions at once; only positions that pass get the full
+// check (record_len = 18 + klen + vlen, fitting the image; re-read through L1). The kernel is
+// VALU-issue-bound, so each chunk is read and marked once (it was three times, by the chunk's own
+// lane and its two left neighbours). A wave covers 992 bytes, i.e. at most two pieces: wave
+// minimum per piece, one atomic per piece and wave.
+constexpr unsigned kScanChunks = 62;
+// 64-bit value of lane l (wave-uniform l), read with every lane active.
+__device__ __forceinline__ std::uint64_t readlane64_u(std::uint64_t v, std::uint32_t l) {
+  return dev::readlane64(v, l);
+}
 __device__ __forceinline__ std::uint32_t le1_bytes4(std::uint32_t d) {
   // 4-bit mask: bit i set iff byte i of d is 0 or 1
   const std::uint32_t x = d & 0xFEFEFEFEu;
@@ -125,38 +132,35 @@ __device__ __forceinline__ std::uint32_t le1_bytes4(std::uint32_t d) {
   return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
 }
 
-// Positions [plo, phi) only (pieces [plo, phi) / kWalPiece; t0, the first chunk, a multiple of 64).
+// Positions [plo, phi) only (pieces [plo, phi) / kWalPiece; t0 = the chunk holding plo).
 __global__ __launch_bounds__(kScanThreads) void wal_scan(WalArgs a, std::uint64_t t0, std::uint64_t plo,
                                                           std::uint64_t phi) {
   const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
   const std::uintptr_t al = w0 & ~static_cast<std::uintptr_t>(15);
   const std::uint64_t off0 = w0 - al;
-  const std::uint64_t t = t0 + gid();
-  const std::uintptr_t c0 = al + 16 * t;  // this thread's chunk
-  const std::uintptr_t end = w0 + a.size;
-  std::uint32_t dw[12];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const std::uintptr_t ca = c0 + 16u * c;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (ca < end) v = *reinterpret_cast<const uint4*>(ca);
-    dw[4 * c + 0] = v.x;
-    dw[4 * c + 1] = v.y;
-    dw[4 * c + 2] = v.z;
-    dw[4 * c + 3] = v.w;
-  }
-  // bit b of M: byte 8 + b of the window is 0 or 1 (b < 28)
-  std::uint32_t M = 0;
-#pragma unroll
-  for (int i = 2; i < 9; ++i) M |= le1_bytes4(dw[i]) << (4 * (i - 2));
-  std::uint32_t cand = M & (M >> 9) & 0xFFFFu;  // bit j: bytes j+8 and j+17 are 0/1
-  // positions inside the image with a full header left
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint64_t t_wave = t0 + (gid() >> 6) * kScanChunks;
+  const std::uint64_t t = t_wave + lane;
+  const std::uintptr_t c0 = al + 16 * t;  // this lane's chunk
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (c0 < w0 + a.size) v = *reinterpret_cast<const uint4*>(c0);
+  const std::uint32_t f = le1_bytes4(v.x) | le1_bytes4(v.y) << 4 | le1_bytes4(v.z) << 8 | le1_bytes4(v.w) << 12;
+  const std::uint32_t f1 = static_cast<std::uint32_t>(__shfl_down(static_cast<int>(f), 1, 64));
+  const std::uint32_t f2 = static_cast<std::uint32_t>(__shfl_down(static_cast<int>(f), 2, 64));
+  const std::uint32_t M = (f >> 8) | (f1 << 8) | (f2 << 24);  // bit b: byte 8 + b of [16t, 16t + 48) is 0/1
+  std::uint32_t cand = M & (M >> 9) & 0xFFFFu;               // bit j: bytes j+8 and j+17 are 0/1
+  // positions inside [plo, phi) with a full header left: j in [lo, hi]
   const std::int64_t p0 = static_cast<std::int64_t>(16 * t) - static_cast<std::int64_t>(off0);
   const std::int64_t last = std::min<std::int64_t>(static_cast<std::int64_t>(a.size) - static_cast<std::int64_t>(kWalMeta),
                                                     static_cast<std::int64_t>(phi) - 1);
   const std::int64_t lo = static_cast<std::int64_t>(plo) - p0, hi = last - p0;
-  for (int j = 0; j < 16; ++j)
-    if (j < lo || j > hi) cand &= ~(1u << j);
+  if (lane >= kScanChunks || hi < 0 || lo > 15) {
+    cand = 0;
+  } else {
+    const std::uint32_t jlo = lo < 0 ? 0u : static_cast<std::uint32_t>(lo);
+    const std::uint32_t jhi = hi > 15 ? 15u : static_cast<std::uint32_t>(hi);
+    cand &= ((2u << jhi) - 1u) & ~((1u << jlo) - 1u);
+  }
   std::uint64_t best = kNone;
   while (cand) {
     const int j = __builtin_ctz(cand);
@@ -169,61 +173,67 @@ __global__ __launch_bounds__(kScanThreads) void wal_scan(WalArgs a, std::uint64_
     cand &= cand - 1;
   }
   // the wave's positions span pieces pa and pa + 1
-  const std::int64_t wave_p0 = static_cast<std::int64_t>(16 * (t & ~63ull)) - static_cast<std::int64_t>(off0);
+  const std::int64_t wave_p0 = static_cast<std::int64_t>(16 * t_wave) - static_cast<std::int64_t>(off0);
   const std::uint64_t pa = wave_p0 < 0 ? 0 : static_cast<std::uint64_t>(wave_p0) / kWalPiece;
-  std::uint64_t mA = (best != kNone && best / kWalPiece == pa) ? best : kNone;
-  std::uint64_t mB = (best != kNone && best / kWalPiece != pa) ? best : kNone;
-#pragma unroll
-  for (int m = 32; m > 0; m >>= 1) {
-    const std::uint64_t oA = __shfl_xor(mA, m, 64), oB = __shfl_xor(mB, m, 64);
-    mA = oA < mA ? oA : mA;
-    mB = oB < mB ? oB : mB;
-  }
-  if ((threadIdx.x & 63u) == 0) {
-    if (mA != kNone && pa != 0) atomicMin(reinterpret_cast<unsigned long long*>(&a.S[pa]), mA);
-    if (mB != kNone && pa + 1 < a.K) atomicMin(reinterpret_cast<unsigned long long*>(&a.S[pa + 1]), mB);
+  // Positions grow with the lane index, so a piece's first header in this wave is the one of the
+  // lowest lane that found one there: a ballot and a lane read, not a shuffle reduction.
+  const bool found = best != kNone;
+  const bool inA = found && best / kWalPiece == pa;
+  const std::uint64_t balA = __ballot(inA), balB = __ballot(found && !inA);
+  const std::uint64_t mA = readlane64_u(best, balA ? static_cast<std::uint32_t>(__builtin_ctzll(balA)) : 0u);
+  const std::uint64_t mB = readlane64_u(best, balB ? static_cast<std::uint32_t>(__builtin_ctzll(balB)) : 0u);
+  if (lane == 0) {
+    if (balA && pa != 0) atomicMin(reinterpret_cast<unsigned long long*>(&a.S[pa]), mA);
+    if (balB && pa + 1 < a.K) atomicMin(reinterpret_cast<unsigned long long*>(&a.S[pa + 1]), mB);
   }
 }
 
+// One slicing-by-4 step of the lane's register over dword w (the engine's replicated LDS tables).
+__device__ __forceinline__ void wal_fold(const std::uint32_t* lds, dev::Reg& r, std::uint32_t w, const dev::LaneConst& kc) {
+  dev::slice4(lds, r, w, kc);
+}
+
 // CRC-32 (finalized) of the payload [q, q + L) in image bytes, L <= kWalLaneMax, folded by this
-// lane alone: the payload is zero-padded in front to whole dwords (leading zeros leave an init-0
-// register at 0) and folded with slicing-by-4 lookups into the LDS tables; the init register enters
-// as inj[L] = Shift_L(0xFFFFFFFF) (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). Dwords are read aligned to
-// the absolute address and realigned with v_alignbyte, four at a time with the next four already in
-// flight (the fold chain hides their latency); no dword past the payload's last one is read.
+// lane alone with slicing-by-4 lookups into the LDS tables; the init register enters as
+// inj[L] = Shift_L(0xFFFFFFFF) (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). The payload is read as the
+// 16-byte aligned granules that hold it, two at a time with the next two in flight: the bytes in
+// front of the payload in its first granule are zeroed (leading zeros leave an init-0 register at
+// 0), whole dwords are folded, and the last 0-3 bytes take Sarwate steps. A granule never crosses a
+// page, so reading the whole of one that holds payload bytes cannot fault. Each lane reads its own
+// part of the image, so a CU's lanes touch far more lines than its L1 holds; 16-byte reads take a
+// quarter of the requests of the dword reads they replace (profiles/r2/wal_pmc/).
 __device__ __forceinline__ std::uint32_t lane_crc(const std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
                                                   std::uint64_t q, std::uint32_t L) {
-  const std::uint32_t z = (4u - (L & 3u)) & 3u;  // zero bytes in front
-  const std::uintptr_t s = reinterpret_cast<std::uintptr_t>(a.w) + q - z;
-  const std::uint32_t t = static_cast<std::uint32_t>(s & 3u);
-  const std::uintptr_t al = s - t;
-  const std::uint32_t n = (z + L) >> 2;               // dwords to fold
-  const std::uint32_t mlast = t ? n : (n ? n - 1 : 0);  // last aligned dword read
-  auto R = [&](std::uint32_t m) { return *reinterpret_cast<const std::uint32_t*>(al + 4u * (m < mlast ? m : mlast)); };
+  if (L == 0) return 0u;  // crc32 of nothing
+  const std::uintptr_t s = reinterpret_cast<std::uintptr_t>(a.w) + q;
+  const std::uintptr_t g0 = s & ~static_cast<std::uintptr_t>(15);
+  const std::uint32_t h = static_cast<std::uint32_t>(s - g0);  // bytes in front, zeroed
+  const std::uint32_t span = h + L;
+  const std::uint32_t nd = span >> 2, tb = span & 3u;          // whole dwords, then tail bytes
+  const std::uint32_t glast = (span - 1u) >> 4;                 // last granule with payload bytes
+  auto G = [&](std::uint32_t m) { return *reinterpret_cast<const uint4*>(g0 + 16u * (m < glast ? m : glast)); };
+  auto mask = [&](std::uint32_t k) -> std::uint32_t {  // bytes of dword k at or after the payload start
+    const std::int32_t lead = static_cast<std::int32_t>(h) - static_cast<std::int32_t>(4u * k);
+    return lead <= 0 ? 0xFFFFFFFFu : (lead >= 4 ? 0u : 0xFFFFFFFFu << (8 * lead));
+  };
   dev::Reg r{0, 0};
-  std::uint32_t w[5] = {R(0), R(1), R(2), R(3), R(4)};  // aligned dwords j .. j+4
-  std::uint32_t j = 0;
-  std::uint32_t head = static_cast<std::uint32_t>(0xFFFFFFFFull << (8 * z));  // first dword: zeros in front
-  for (; j + 4 <= n; j += 4) {
-    const std::uint32_t f0 = R(j + 5), f1 = R(j + 6), f2 = R(j + 7), f3 = R(j + 8);  // next group in flight
+  uint4 c0 = G(0), c1 = G(1);
+  for (std::uint32_t m = 0; 4u * m <= nd; m += 2) {
+    const uint4 n0 = G(m + 2), n1 = G(m + 3);  // the next two granules, in flight
+    const std::uint32_t d[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      std::uint32_t d = t ? __builtin_amdgcn_alignbyte(w[i + 1], w[i], t) : w[i];
-      dev::slice4(lds, r, d & head, kc);
-      head = 0xFFFFFFFFu;
+    for (std::uint32_t i = 0; i < 8; ++i) {
+      const std::uint32_t k = 4u * m + i;
+      if (k < nd) {
+        wal_fold(lds, r, m == 0 ? d[i] & mask(k) : d[i], kc);
+      } else if (k == nd && tb) {  // the last 1-3 bytes
+        std::uint32_t x = r.value(), b = m == 0 ? d[i] & mask(k) : d[i];
+        for (std::uint32_t t = 0; t < tb; ++t, b >>= 8) x = (x >> 8) ^ dev::lds_at(lds, (((x ^ b) & 0xFFu) << 8) | kc.L0);
+        r = dev::Reg{x, 0};
+      }
     }
-    w[0] = w[4];
-    w[1] = f0;
-    w[2] = f1;
-    w[3] = f2;
-    w[4] = f3;
-  }
-  for (std::uint32_t i = 0; j < n; ++j, ++i) {  // the last 0-3 dwords (w[] holds them)
-    const std::uint32_t lo = i == 0 ? w[0] : i == 1 ? w[1] : w[2];
-    const std::uint32_t hi = i == 0 ? w[1] : i == 1 ? w[2] : w[3];
-    const std::uint32_t d = t ? __builtin_amdgcn_alignbyte(hi, lo, t) : lo;
-    dev::slice4(lds, r, d & head, kc);
-    head = 0xFFFFFFFFu;
+    c0 = n0;
+    c1 = n1;
   }
   return r.value() ^ a.inj[L] ^ 0xFFFFFFFFu;
 }
@@ -238,6 +248,36 @@ __device__ __forceinline__ void fill_slices(const DeviceTables* tabs, std::uint3
     for (std::uint32_t k = 0; k < 8u; ++k) dst[(k + u) & 7u] = make_uint4(v, v, v, v);
   }
   __syncthreads();
+}
+
+// The header fields of the record at p (p + 26 <= size): record_len, the stored CRC, key and value
+// lengths (wal.cpp:14-18). Two dword-aligned 16-byte loads cover [p & ~3, + 32) and the fields are
+// realigned in registers; within 32 bytes of the image's end (where those loads could cross into
+// the next page) the fields are read as separate dwords.
+__device__ __forceinline__ void header_fields(const WalArgs& a, std::uint64_t p, std::uint32_t* rlen,
+                                              std::uint32_t* stored, std::uint64_t* klen, std::uint64_t* vlen) {
+  const std::uintptr_t q = reinterpret_cast<std::uintptr_t>(a.w) + p;
+  const std::uintptr_t b = q & ~static_cast<std::uintptr_t>(3);
+  if (b + 32 > reinterpret_cast<std::uintptr_t>(a.w) + a.size) {
+    *rlen = ld32(a.w, p, a.size);
+    *stored = ld32(a.w, p + 4, a.size);
+    *klen = ld32(a.w, p + 18, a.size);
+    *vlen = ld32(a.w, p + 22, a.size);
+    return;
+  }
+  const uint4 u = *reinterpret_cast<const uint4*>(b), v = *reinterpret_cast<const uint4*>(b + 16);
+  const std::uint32_t t = static_cast<std::uint32_t>(q & 3u);
+  const std::uint32_t d[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+  auto at = [&](std::uint32_t lo, std::uint32_t hi) { return t ? __builtin_amdgcn_alignbyte(hi, lo, t) : lo; };
+  *rlen = at(d[0], d[1]);
+  *stored = at(d[1], d[2]);
+  // bytes p+18.. and p+22.. start in dword (t + 18) / 4 = 4 or 5 and (t + 22) / 4 = 5 or 6 of the
+  // window, at byte (t + 2) & 3 of it
+  const bool up = t >= 2u;
+  const std::uint32_t o = (t + 2u) & 3u;
+  auto at2 = [&](std::uint32_t lo, std::uint32_t hi) { return o ? __builtin_amdgcn_alignbyte(hi, lo, o) : lo; };
+  *klen = up ? at2(d[5], d[6]) : at2(d[4], d[5]);
+  *vlen = up ? at2(d[6], d[7]) : at2(d[5], d[6]);
 }
 
 // Walk piece k from `start` over the records that start in the piece (wal.cpp:63-87: header size,
@@ -256,13 +296,13 @@ __device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::
       bad_hdr = true;
       break;
     }
-    const std::uint32_t rlen = ld32(a.w, p, a.size);
+    std::uint32_t rlen, stored;
+    std::uint64_t klen, vlen;
+    header_fields(a, p, &rlen, &stored, &klen, &vlen);
     if (static_cast<std::uint64_t>(rlen) + 8 > a.size - p) {
       bad_hdr = true;
       break;
     }
-    const std::uint32_t stored = ld32(a.w, p + 4, a.size);
-    const std::uint64_t klen = ld32(a.w, p + 18, a.size), vlen = ld32(a.w, p + 22, a.size);
     bool bad = kWalMeta + klen + vlen > 8ull + rlen;
     if (rlen <= kWalLaneMax) {
       bad = bad || lane_crc(lds, kc, a, p + 8, rlen) != stored;
@@ -324,14 +364,23 @@ __global__ void wal_jump_init(WalArgs a) {
   a.bad_at[k] = kNone;
 }
 
-// 3. One doubling round: marks J(k) for every marked k (J = next^(2^t)), then J <- J o J. Marks set
-// during the round by other threads are pieces of the true path too, so reading them early is safe.
+// 3. One quadrupling round (J = next^(4^t)): every marked k marks J(k), J(J(k)) and J(J(J(k))), then
+// J <- J o J o J o J. After round t the marks hold next^i(0) for every i < 4^(t+1), so
+// ceil(log4 K) rounds mark the whole path: half the launches of doubling, for two more dependent
+// loads per round. Marks set during the round by other threads are pieces of the true path too,
+// so reading them early is safe. K is the end of the path.
 __global__ void wal_jump(const std::uint32_t* J, std::uint32_t* J2, std::uint8_t* on, std::uint32_t K) {
   const std::uint64_t k = gid();
   if (k >= K) return;
-  const std::uint32_t j = J[k];
-  if (j < K && on[k]) on[j] = 1;
-  J2[k] = j < K ? J[j] : K;
+  const std::uint32_t j1 = J[k];
+  const std::uint32_t j2 = j1 < K ? J[j1] : K;
+  const std::uint32_t j3 = j2 < K ? J[j2] : K;
+  J2[k] = j3 < K ? J[j3] : K;
+  if (on[k]) {
+    if (j1 < K) on[j1] = 1;
+    if (j2 < K) on[j2] = 1;
+    if (j3 < K) on[j3] = 1;
+  }
 }
 
 // Entry points: each on-path piece hands its exit to the piece that holds it (one writer each:
@@ -597,9 +646,10 @@ void pass_front(const WalArgs& a, std::uint64_t k_lo, std::uint64_t k_hi, hipStr
   const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
   const std::uint64_t off0 = w0 & 15u;
   const std::uint64_t plo = k_lo * kWalPiece, phi = std::min<std::uint64_t>(k_hi * kWalPiece, a.size);
-  const std::uint64_t t0 = ((plo + off0) / 16) & ~63ull;  // whole waves (the kernel's piece arithmetic)
+  const std::uint64_t t0 = (plo + off0) / 16;  // the chunk holding plo
   const std::uint64_t t1 = (phi + off0 + 15) / 16;
-  hipLaunchKernelGGL(wal_scan, dim3(blocks(t1 - t0, kScanThreads)), dim3(kScanThreads), 0, st, a, t0, plo, phi);
+  const std::uint64_t threads = (t1 - t0 + kScanChunks - 1) / kScanChunks * 64;  // kScanChunks chunks per wave
+  hipLaunchKernelGGL(wal_scan, dim3(blocks(threads, kScanThreads)), dim3(kScanThreads), 0, st, a, t0, plo, phi);
   hipLaunchKernelGGL(wal_spec, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
 }
 
@@ -612,7 +662,7 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
   hipLaunchKernelGGL(wal_jump_init, dim3(blocks(K, 256)), dim3(256), 0, st, a);
   std::uint32_t* J = a.Ja;
   std::uint32_t* J2 = a.Jb;
-  for (std::uint64_t reach = 1; reach < K; reach <<= 1) {
+  for (std::uint64_t reach = 1; reach < K; reach <<= 2) {
     hipLaunchKernelGGL(wal_jump, dim3(blocks(K, 256)), dim3(256), 0, st, J, J2, a.on, K);
     std::swap(J, J2);
   }
