@@ -251,23 +251,37 @@ __device__ __forceinline__ void fill_slices(const DeviceTables* tabs, std::uint3
 }
 
 // The header fields of the record at p (p + 26 <= size): record_len, the stored CRC, key and value
-// lengths (wal.cpp:14-18). Two dword-aligned 16-byte loads cover [p & ~3, + 32) and the fields are
-// realigned in registers; within 32 bytes of the image's end (where those loads could cross into
-// the next page) the fields are read as separate dwords.
-__device__ __forceinline__ void header_fields(const WalArgs& a, std::uint64_t p, std::uint32_t* rlen,
+// lengths (wal.cpp:14-18). header_load issues two dword-aligned 16-byte loads over [p & ~3, + 32),
+// so the walk can put the next record's header in flight before it folds the current payload;
+// header_fields realigns the fields in registers. Within 32 bytes of the image's end (where those
+// loads could cross into the next page) nothing is loaded and the fields are read as dwords.
+struct HdrRaw {
+  uint4 u, v;
+};
+__device__ __forceinline__ bool header_window_ok(const WalArgs& a, std::uint64_t p) {
+  const std::uintptr_t b = (reinterpret_cast<std::uintptr_t>(a.w) + p) & ~static_cast<std::uintptr_t>(3);
+  return b + 32 <= reinterpret_cast<std::uintptr_t>(a.w) + a.size;
+}
+__device__ __forceinline__ HdrRaw header_load(const WalArgs& a, std::uint64_t p) {
+  HdrRaw h{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+  if (header_window_ok(a, p)) {
+    const std::uintptr_t b = (reinterpret_cast<std::uintptr_t>(a.w) + p) & ~static_cast<std::uintptr_t>(3);
+    h.u = *reinterpret_cast<const uint4*>(b);
+    h.v = *reinterpret_cast<const uint4*>(b + 16);
+  }
+  return h;
+}
+__device__ __forceinline__ void header_fields(const WalArgs& a, std::uint64_t p, const HdrRaw& h, std::uint32_t* rlen,
                                               std::uint32_t* stored, std::uint64_t* klen, std::uint64_t* vlen) {
-  const std::uintptr_t q = reinterpret_cast<std::uintptr_t>(a.w) + p;
-  const std::uintptr_t b = q & ~static_cast<std::uintptr_t>(3);
-  if (b + 32 > reinterpret_cast<std::uintptr_t>(a.w) + a.size) {
+  if (!header_window_ok(a, p)) {
     *rlen = ld32(a.w, p, a.size);
     *stored = ld32(a.w, p + 4, a.size);
     *klen = ld32(a.w, p + 18, a.size);
     *vlen = ld32(a.w, p + 22, a.size);
     return;
   }
-  const uint4 u = *reinterpret_cast<const uint4*>(b), v = *reinterpret_cast<const uint4*>(b + 16);
-  const std::uint32_t t = static_cast<std::uint32_t>(q & 3u);
-  const std::uint32_t d[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+  const std::uint32_t t = static_cast<std::uint32_t>((reinterpret_cast<std::uintptr_t>(a.w) + p) & 3u);
+  const std::uint32_t d[8] = {h.u.x, h.u.y, h.u.z, h.u.w, h.v.x, h.v.y, h.v.z, h.v.w};
   auto at = [&](std::uint32_t lo, std::uint32_t hi) { return t ? __builtin_amdgcn_alignbyte(hi, lo, t) : lo; };
   *rlen = at(d[0], d[1]);
   *stored = at(d[1], d[2]);
@@ -291,6 +305,7 @@ __device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::
   const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
   std::uint64_t p = start, n_all = 0, n_big = 0, first = kNone, first_pos = 0;
   bool bad_hdr = false;
+  HdrRaw h = header_load(a, p);
   while (p < limit) {
     if (a.size - p < kWalMeta) {
       bad_hdr = true;
@@ -298,11 +313,13 @@ __device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::
     }
     std::uint32_t rlen, stored;
     std::uint64_t klen, vlen;
-    header_fields(a, p, &rlen, &stored, &klen, &vlen);
+    header_fields(a, p, h, &rlen, &stored, &klen, &vlen);
     if (static_cast<std::uint64_t>(rlen) + 8 > a.size - p) {
       bad_hdr = true;
       break;
     }
+    const std::uint64_t np = p + 8 + static_cast<std::uint64_t>(rlen);
+    if (np < limit && a.size - np >= kWalMeta) h = header_load(a, np);  // next header in flight during the fold
     bool bad = kWalMeta + klen + vlen > 8ull + rlen;
     if (rlen <= kWalLaneMax) {
       bad = bad || lane_crc(lds, kc, a, p + 8, rlen) != stored;
@@ -319,7 +336,7 @@ __device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::
       first_pos = p;
     }
     ++n_all;
-    p += 8 + static_cast<std::uint64_t>(rlen);
+    p = np;
   }
   *exit_out = p;
   *broke_out = bad_hdr ? 1 : 0;
