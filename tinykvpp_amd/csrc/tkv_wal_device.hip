@@ -51,7 +51,7 @@ constexpr std::uint64_t kWalPiece = 2048;     // bytes of image per speculative 
 constexpr std::uint64_t kWalMeta = 26;        // wal.hpp:21-27 kMetadataSize
 constexpr std::uint32_t kWalLaneMax = 1024;   // payloads up to this size are checked by their lane
 constexpr std::uint64_t kNone = ~0ull;
-constexpr unsigned kScanThreads = 256;        // wal_scan: 16 positions per lane, 62 chunks per wave
+constexpr unsigned kScanThreads = 256;        // wal_scan: 32 positions per lane, 126 chunks per wave
 constexpr unsigned kCheckThreads = 1024;      // wal_spec/wal_recheck: one workgroup per CU (128 KiB of LDS)
 
 struct WalArgs {
@@ -111,16 +111,16 @@ __device__ __forceinline__ std::uint64_t gid() {
 }
 
 // 1. First plausible header per piece, one coalesced pass over the image. Lane l of a wave holds
-// the 16 bytes of absolute chunk t = t_wave + l (one 16-byte load) and reports the 16 positions of
-// that chunk, for l < kScanChunks; the last two lanes only lend their bytes. A header at position p
-// has its op and tombstone bytes (p+8, p+17) at 0 or 1 (wal.cpp:30-52). Each lane marks which of
-// its 16 bytes are 0 or 1 with byte-parallel arithmetic, takes its two right neighbours' marks by
-// cross-lane shifts, and so tests all 16 positions at once; only positions that pass get the full
-// check (record_len = 18 + klen + vlen, fitting the image; re-read through L1). The kernel is
+// the 32 bytes of absolute chunks t = t_wave + 2l and t + 1 (two 16-byte loads) and reports their
+// 32 positions, for l < 63; the last lane only lends its bytes. A header at position p has its op
+// and tombstone bytes (p+8, p+17) at 0 or 1 (wal.cpp:30-52). Each lane marks which of its 32 bytes
+// are 0 or 1 with byte-parallel arithmetic, takes its right neighbour's marks by a cross-lane shift,
+// and so tests all 32 positions at once; only positions that pass get the full check
+// (record_len = 18 + klen + vlen, fitting the image; re-read through L1). The kernel is
 // VALU-issue-bound, so each chunk is read and marked once (it was three times, by the chunk's own
-// lane and its two left neighbours). A wave covers 992 bytes, i.e. at most two pieces: wave
-// minimum per piece, one atomic per piece and wave.
-constexpr unsigned kScanChunks = 62;
+// lane and its two left neighbours), and a lane's fixed costs cover 32 positions. A wave covers
+// 2016 bytes, i.e. at most two pieces: one ballot per piece and wave, one atomic per piece and wave.
+constexpr unsigned kScanChunks = 126;  // chunks reported per wave: two per lane, lanes 0..62
 // 64-bit value of lane l (wave-uniform l), read with every lane active.
 __device__ __forceinline__ std::uint64_t readlane64_u(std::uint64_t v, std::uint32_t l) {
   return dev::readlane64(v, l);
@@ -140,26 +140,28 @@ __global__ __launch_bounds__(kScanThreads) void wal_scan(WalArgs a, std::uint64_
   const std::uint64_t off0 = w0 - al;
   const std::uint32_t lane = threadIdx.x & 63u;
   const std::uint64_t t_wave = t0 + (gid() >> 6) * kScanChunks;
-  const std::uint64_t t = t_wave + lane;
-  const std::uintptr_t c0 = al + 16 * t;  // this lane's chunk
-  uint4 v = make_uint4(0, 0, 0, 0);
-  if (c0 < w0 + a.size) v = *reinterpret_cast<const uint4*>(c0);
-  const std::uint32_t f = le1_bytes4(v.x) | le1_bytes4(v.y) << 4 | le1_bytes4(v.z) << 8 | le1_bytes4(v.w) << 12;
+  const std::uint64_t t = t_wave + 2 * lane;  // this lane's two chunks: 32 bytes from 16t
+  const std::uintptr_t c0 = al + 16 * t;
+  const std::uintptr_t end = w0 + a.size;
+  uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+  if (c0 < end) v0 = *reinterpret_cast<const uint4*>(c0);
+  if (c0 + 16 < end) v1 = *reinterpret_cast<const uint4*>(c0 + 16);
+  const std::uint32_t f = le1_bytes4(v0.x) | le1_bytes4(v0.y) << 4 | le1_bytes4(v0.z) << 8 | le1_bytes4(v0.w) << 12 |
+                          le1_bytes4(v1.x) << 16 | le1_bytes4(v1.y) << 20 | le1_bytes4(v1.z) << 24 | le1_bytes4(v1.w) << 28;
   const std::uint32_t f1 = static_cast<std::uint32_t>(__shfl_down(static_cast<int>(f), 1, 64));
-  const std::uint32_t f2 = static_cast<std::uint32_t>(__shfl_down(static_cast<int>(f), 2, 64));
-  const std::uint32_t M = (f >> 8) | (f1 << 8) | (f2 << 24);  // bit b: byte 8 + b of [16t, 16t + 48) is 0/1
-  std::uint32_t cand = M & (M >> 9) & 0xFFFFu;               // bit j: bytes j+8 and j+17 are 0/1
+  const std::uint64_t F = f | static_cast<std::uint64_t>(f1) << 32;  // bit b: byte b of [16t, 16t + 64) is 0/1
+  std::uint32_t cand = static_cast<std::uint32_t>((F >> 8) & (F >> 17));  // bit j: bytes j+8 and j+17 are 0/1
   // positions inside [plo, phi) with a full header left: j in [lo, hi]
   const std::int64_t p0 = static_cast<std::int64_t>(16 * t) - static_cast<std::int64_t>(off0);
   const std::int64_t last = std::min<std::int64_t>(static_cast<std::int64_t>(a.size) - static_cast<std::int64_t>(kWalMeta),
                                                     static_cast<std::int64_t>(phi) - 1);
   const std::int64_t lo = static_cast<std::int64_t>(plo) - p0, hi = last - p0;
-  if (lane >= kScanChunks || hi < 0 || lo > 15) {
+  if (2 * lane >= kScanChunks || hi < 0 || lo > 31) {
     cand = 0;
   } else {
     const std::uint32_t jlo = lo < 0 ? 0u : static_cast<std::uint32_t>(lo);
-    const std::uint32_t jhi = hi > 15 ? 15u : static_cast<std::uint32_t>(hi);
-    cand &= ((2u << jhi) - 1u) & ~((1u << jlo) - 1u);
+    const std::uint32_t jhi = hi > 31 ? 31u : static_cast<std::uint32_t>(hi);
+    cand &= (jhi == 31u ? 0xFFFFFFFFu : (2u << jhi) - 1u) & ~((1u << jlo) - 1u);
   }
   std::uint64_t best = kNone;
   while (cand) {
