@@ -220,23 +220,32 @@ __device__ __forceinline__ std::uint32_t lane_crc(const std::uint32_t* lds, cons
   };
   dev::Reg r{0, 0};
   uint4 c0 = G(0), c1 = G(1);
-  for (std::uint32_t m = 0; 4u * m <= nd; m += 2) {
-    const uint4 n0 = G(m + 2), n1 = G(m + 3);  // the next two granules, in flight
-    const std::uint32_t d[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  // Granule pairs [m, m + 2): the first one masks the head dwords, the ones wholly inside the
+  // payload fold unguarded, the last one (<= 8 dwords left) is guarded and takes the tail bytes.
+  auto pair = [&](std::uint32_t m, const uint4& x0, const uint4& x1, bool head, bool guarded) {
+    const std::uint32_t d[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
     for (std::uint32_t i = 0; i < 8; ++i) {
       const std::uint32_t k = 4u * m + i;
-      if (k < nd) {
-        wal_fold(lds, r, m == 0 ? d[i] & mask(k) : d[i], kc);
+      const std::uint32_t w = head ? d[i] & mask(k) : d[i];
+      if (!guarded || k < nd) {
+        wal_fold(lds, r, w, kc);
       } else if (k == nd && tb) {  // the last 1-3 bytes
-        std::uint32_t x = r.value(), b = m == 0 ? d[i] & mask(k) : d[i];
+        std::uint32_t x = r.value(), b = w;
         for (std::uint32_t t = 0; t < tb; ++t, b >>= 8) x = (x >> 8) ^ dev::lds_at(lds, (((x ^ b) & 0xFFu) << 8) | kc.L0);
         r = dev::Reg{x, 0};
       }
     }
+  };
+  std::uint32_t m = 0;
+  for (; 4u * m + 8u <= nd; m += 2) {  // pairs whose 8 dwords are all whole payload dwords
+    const uint4 n0 = G(m + 2), n1 = G(m + 3);  // the next two granules, in flight
+    if (m == 0) pair(0, c0, c1, true, false);
+    else pair(m, c0, c1, false, false);
     c0 = n0;
     c1 = n1;
   }
+  pair(m, c0, c1, m == 0, true);  // the last 0-7 whole dwords and the tail bytes
   return r.value() ^ a.inj[L] ^ 0xFFFFFFFFu;
 }
 
