@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """In-process comparison of builds of libtkv_crc32.so on the host-memory batch paths (not product
 code): tkv_crc32_batch_host over a pageable 430 MB WAL image's payloads, tkv_wal_stamp over the same
-records, tkv_sst_stamp_blocks over a pageable 1 GB SSTable image, and a pageable 4 GiB batch of
-64 KiB blocks; libraries rotate round by round, results must agree.
+records, tkv_sst_stamp_blocks over a pageable 1 GB SSTable image, a pageable 4 GiB batch of
+64 KiB blocks, and tkv_wal_verify of pageable WAL images (the 430 MB Zipf records, 1 GiB of small
+records); libraries rotate round by round, results must agree.
 
     python tools/ab_host.py lib1.so lib2.so ... [--rounds 4]
 """
@@ -17,6 +18,19 @@ import numpy as np
 VP, U64 = ctypes.c_void_p, ctypes.c_uint64
 
 
+def wal_image(n_rec, klen, vlen, rng):
+    """Records the reference encoder would write (wal.cpp:19-61), CRC fields left for tkv_wal_stamp."""
+    size = 26 + klen + vlen
+    offs = np.concatenate([[0], np.cumsum(size[:-1], dtype=np.uint64)]).astype(np.uint64)
+    w = rng.integers(0, 256, int(size.sum()), dtype=np.uint8)
+    for col, vals in ((0, size - 8), (18, klen), (22, vlen)):
+        for b in range(4):
+            w[offs.astype(np.int64) + col + b] = ((vals >> (8 * b)) & 0xFF).astype(np.uint8)
+    for col in (8, 17):
+        w[offs.astype(np.int64) + col] = 0
+    return w, offs, size.astype(np.uint32)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
@@ -28,6 +42,7 @@ def main():
         lib.tkv_crc32_batch_host.argtypes = [VP, VP, VP, VP, VP, U64]
         lib.tkv_wal_stamp.argtypes = [VP, VP, VP, U64]
         lib.tkv_sst_stamp_blocks.argtypes = [VP, VP, VP, U64]
+        lib.tkv_wal_verify.argtypes = [VP, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)]
         assert lib.tkv_set_device(0) == 0
         libs.append(lib)
     rng = np.random.default_rng(1)
@@ -47,6 +62,19 @@ def main():
     big = rng.integers(0, 256, n64 * 65536, dtype=np.uint8)
     boff = np.arange(n64, dtype=np.uint64) * 65536
     blen = np.full(n64, 65536, np.uint32)
+    wz, oz, sz = wal_image(n, klen, vlen, rng)
+    ns = 18_199_191
+    ws, os_, ss = wal_image(ns, rng.integers(4, 24, ns).astype(np.uint32), rng.integers(0, 40, ns).astype(np.uint32), rng)
+    for w, o, z in ((wz, oz, sz), (ws, os_, ss)):
+        assert libs[0].tkv_wal_stamp(VP(w.ctypes.data), VP(o.ctypes.data), VP(z.ctypes.data), o.size) == 0
+
+    def verify(w):
+        def call(lib, out):
+            g, s_ = U64(0), U64(0)
+            rc = lib.tkv_wal_verify(VP(w.ctypes.data), w.nbytes, ctypes.byref(g), ctypes.byref(s_))
+            out[0], out[1] = g.value & 0xFFFFFFFF, s_.value & 0xFFFFFFFF
+            return rc
+        return call
     work = [
         ("batch_host WAL payloads 430 MB", wal.nbytes, lambda lib, out: lib.tkv_crc32_batch_host(
             VP(wal.ctypes.data), VP(poff.ctypes.data), VP(plen.ctypes.data), None, VP(out.ctypes.data), n), n),
@@ -56,6 +84,8 @@ def main():
             VP(sst.ctypes.data), VP(soff.ctypes.data), VP(ssz.ctypes.data), nblk), None),
         ("batch_host 64 K x 64 KiB (4 GiB)", big.nbytes, lambda lib, out: lib.tkv_crc32_batch_host(
             VP(big.ctypes.data), VP(boff.ctypes.data), VP(blen.ctypes.data), None, VP(out.ctypes.data), n64), n64),
+        ("wal_verify Zipf 430 MB", wz.nbytes, verify(wz), 2),
+        ("wal_verify small records 1 GiB", ws.nbytes, verify(ws), 2),
     ]
     for name, nbytes, call, nout in work:
         outs = [np.zeros(nout or 1, np.uint32) for _ in libs]
