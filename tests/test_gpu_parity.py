@@ -451,6 +451,23 @@ def test_host_batch_block_larger_than_slab(gpu, oracle):
     assert [int(x) for x in got] == want
 
 
+@pytest.mark.parametrize("stride", [None, 4096])
+def test_host_batch_dense_run_longer_than_slab(gpu, oracle, stride):
+    """Pageable blocks 8 bytes apart (WAL payloads) whose covering range exceeds a 256 MiB staging
+    slab: each slab ends at the block that would push its range past 256 MiB and goes over as one
+    range. Random lengths, and 4088-byte blocks on a 4096-byte stride, whose first slab's range
+    ends 8 bytes short of 256 MiB. Against the oracle."""
+    rng = np.random.default_rng(29)
+    if stride is None:
+        lens = rng.integers(1, 16 << 10, 40_000).astype(np.uint32)
+    else:
+        lens = np.full(70_000, stride - 8, np.uint32)
+    offs = np.concatenate([[8], np.cumsum(lens.astype(np.uint64) + 8)[:-1] + 8]).astype(np.uint64)
+    host = rng.integers(0, 256, int(offs[-1]) + int(lens[-1]), dtype=np.uint8)
+    assert host.size > (256 << 20)
+    assert np.array_equal(tk.crc32_batch_host(host, offs, lens), oracle.batch(host, offs, lens))
+
+
 @pytest.mark.parametrize("ndev", [2, 3, 4])
 def test_host_multi_splits_large_blocks(gpu, oracle, ndev):
     """Blocks of >= 1 MiB that straddle a device share are cut at the share boundary and their
