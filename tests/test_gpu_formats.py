@@ -116,6 +116,27 @@ def test_sst_device_stamp_equals_host_stamp(gpu):
     assert sst.verify_blocks(d.cpu().numpy(), offs, sizes)[0] == "ok"
 
 
+def test_sst_device_checks_its_tensors(gpu):
+    """block_crcs_device checks shapes, dtypes and devices before any launch: a short `out`, a
+    length mismatch or a non-uint8 file would otherwise become an out-of-bounds device access."""
+    rng = np.random.default_rng(24)
+    f, offs, sizes = make_file(rng, 16)
+    d = torch.from_numpy(f).to(gpu)
+    o = torch.from_numpy(offs.astype(np.int64)).to(gpu)
+    sz = torch.from_numpy(sizes.astype(np.int32)).to(gpu)
+    for kw in ({"out": torch.empty(15, dtype=torch.int32, device=gpu)},
+               {"out": torch.empty(16, dtype=torch.int64, device=gpu)}):
+        with pytest.raises(ValueError):
+            sst.block_crcs_device(d, o, sz, **kw)
+    with pytest.raises(ValueError):
+        sst.block_crcs_device(d, o, sz[:15])
+    with pytest.raises(ValueError):
+        sst.block_crcs_device(d.view(torch.int8), o, sz)
+    with pytest.raises(ValueError):
+        sst.block_crcs_device(d, o.to(torch.int32), sz)
+    assert u32(sst.block_crcs_device(d, o, sz)).size == 16
+
+
 def test_sst_rejects_short_images(gpu):
     f = np.zeros(100, np.uint8)
     with pytest.raises(tk.TkvError):

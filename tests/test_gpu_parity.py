@@ -143,6 +143,8 @@ def test_odd_prefixes(gpu, oracle):
 # ---- WAL call sites (wal.cpp:54-58, 89-96; wal_test.cpp, engine_test.cpp:437-459) ----------------
 
 def test_wal_records_stamped_identically(gpu):
+    """The stamp equals the reference encoder's bytes for every golden record, including
+    {put,7,"test","data",0}, whose stored CRC wal_test.cpp:507-541 recomputes over [8, size)."""
     recs = golden("wal.json")["records"]
     unstamped = [tk.wal.encode_unstamped(r["op"], r["seq"], r["key"].encode(), r["value"].encode(),
                                          r["tombstone"]) for r in recs]
@@ -168,6 +170,15 @@ def test_wal_verify_and_first_corruption(gpu):
     # truncated tail (wal.cpp:68-70 / 82-87)
     st, good, stop = tk.wal.verify(image[:-3])
     assert st == "corrupted" and good == len(recs) - 1
+
+
+def test_wal_single_record_crc_byte_flip(gpu):
+    """wal_test.cpp:341-364: {put,1,"k","v",0} with its first CRC byte inverted fails, and the view
+    stays where it was (no good records, stop at byte 0)."""
+    rec = bytearray(bytes.fromhex(golden("wal.json")["records"][2]["hex"]))
+    rec[4] = ~rec[4] & 0xFF
+    assert tk.wal.verify(bytes(rec)) == ("corrupted", 0, 0)
+    assert tk.wal.verify(bytes(rec) + bytes.fromhex(golden("wal.json")["records"][0]["hex"])) == ("corrupted", 0, 0)
 
 
 def test_wal_key_value_overflow_detected_after_crc(gpu):

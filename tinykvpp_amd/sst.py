@@ -81,15 +81,19 @@ def block_crcs_device(file, offsets, sizes, store=False, out=None, stream=None):
     """Device-resident images (torch uint8 CUDA tensor, int64 offsets, int32 sizes): the stamp value
     of every image (its CRC with the field read as zero); store=True also writes it into the field."""
     import torch
-    from .crc32 import _stream_ptr
+    from .crc32 import _check_data, _check_vec, _out_vec, _stream_ptr
+    n = offsets.numel()
+    if sizes.numel() != n:
+        raise ValueError("offsets and sizes differ in length")
+    if file.dtype != torch.uint8:
+        raise ValueError("file must be a uint8 tensor")
+    _check_data(file)
     for name, t, dt in (("offsets", offsets, torch.int64), ("sizes", sizes, torch.int32)):
-        if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
-            raise ValueError(f"{name} must be a contiguous CUDA {dt} tensor")
-    if out is None:
-        out = torch.empty(offsets.numel(), dtype=torch.int32, device=file.device)
+        _check_vec(name, t, dt, n, file.device)
+    out = _out_vec(out, n, file.device, stream)
     check(load_library().tkv_sst_block_crcs_device(
         ctypes.c_void_p(file.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), ctypes.c_void_p(sizes.data_ptr()),
-        ctypes.c_void_p(out.data_ptr()), offsets.numel(), int(bool(store)), _stream_ptr(stream)))
+        ctypes.c_void_p(out.data_ptr()), n, int(bool(store)), _stream_ptr(stream)))
     return out
 
 
