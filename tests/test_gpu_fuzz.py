@@ -1,0 +1,121 @@
+"""Seeded randomized parity sweep of every device entry point against the oracle (TEST
+INFRASTRUCTURE: oracle/liboracle.so is the checker). Each case draws a batch shape the targeted tests
+cover one at a time, mixed: lengths 0-3, around the 64-byte lane segment, the 1 KiB small-block
+bound and the 4 KiB row, up to 300 KiB; base misalignment 0-4105; back-to-back layouts (stream mode
+when every block is >= 64 bytes), overlapping and gapped layouts (general walk), optional per-block
+initial registers, both polynomials. The reference's semantics per block: crc32.cpp:9-16 from the
+given raw register, finalize() = crc32.cpp:19."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import tinykvpp_amd as tk
+
+pytestmark = pytest.mark.gpu
+
+ALGOS = ("crc32", "crc32c")
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def draw_lengths(rng, n):
+    """A mixture over the decomposition's boundaries (segment 64 B, small 1 KiB, row 4 KiB)."""
+    kind = rng.integers(0, 6, n)
+    edges = np.array([0, 1, 2, 3, 63, 64, 65, 1023, 1024, 1025, 4095, 4096, 4097, 8192, 65536])
+    lens = np.where(kind == 0, rng.choice(edges, n),
+           np.where(kind == 1, rng.integers(0, 64, n),
+           np.where(kind == 2, rng.integers(64, 1025, n),
+           np.where(kind == 3, rng.integers(1025, 9000, n),
+           np.where(kind == 4, rng.integers(9000, 70000, n), rng.integers(70000, 300000, n))))))
+    # keep the case's payload bounded so the oracle finishes quickly
+    while lens.sum() > (24 << 20):
+        lens = lens // 2
+    return lens.astype(np.int64)
+
+
+def oracle_batch(oracle, algo, host, offs, lens, init):
+    if algo == "crc32":
+        return oracle.batch(host, offs, lens, init)
+    out = np.zeros(offs.size, np.uint32)
+    for i, (o, n) in enumerate(zip(offs.tolist(), lens.tolist())):
+        raw = 0xFFFFFFFF if init is None else int(init[i])
+        out[i] = oracle.update_c(raw, host[o:o + n].tobytes()) ^ 0xFFFFFFFF
+    return out
+
+
+def irregular_mode():
+    return tk.load_library().tkv_debug_irregular_mode(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_irregular_random(gpu, oracle, seed):
+    rng = np.random.default_rng(1000 + seed)
+    algo = ALGOS[seed % 2]
+    n = int(rng.choice([1, 2, 3, 17, 300, 2000, 9000]))
+    lens = draw_lengths(rng, n)
+    layout = ("back_to_back", "back_to_back_min64", "gapped", "overlapping")[seed // 2 % 4]
+    if layout == "back_to_back_min64":
+        lens = np.maximum(lens, 64)
+    start = int(rng.integers(0, 4106))
+    if layout.startswith("back_to_back"):
+        offs = start + np.concatenate([[0], np.cumsum(lens)[:-1]])
+    elif layout == "gapped":
+        offs = start + np.concatenate([[0], np.cumsum(lens + rng.integers(0, 40, n))[:-1]])
+    else:
+        offs = rng.integers(0, max(1, int(lens.sum()) // 2 + 1), n) + start
+    size = int((offs + lens).max()) + 64
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if rng.random() < 0.5 else None
+    d = torch.from_numpy(host).to(gpu)
+    o = torch.from_numpy(offs.astype(np.int64)).to(gpu)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    ini = None if init is None else torch.from_numpy(init.view(np.int32)).to(gpu)
+    got = u32(tk.crc32_batch(d, o, ln, init_raw=ini, algo=algo))
+    want = oracle_batch(oracle, algo, host, offs, lens, init)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, (f"{layout} n={n} start={start} algo={algo} mode={irregular_mode()}: "
+                           f"{bad.size} blocks differ, first {bad[:5]} (lens {lens[bad[:5]]})")
+    if layout == "back_to_back_min64" and n > 1:
+        assert irregular_mode() == 1, "a back-to-back batch of blocks >= 64 B takes stream mode"
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_uniform_random(gpu, oracle, seed):
+    rng = np.random.default_rng(2000 + seed)
+    algo = ALGOS[seed % 2]
+    length = int(rng.choice([0, 1, 3, 64, 1000, 4096, 4097, 8192, 12288, 65536, int(rng.integers(0, 70000))]))
+    stride = length + int(rng.choice([0, 0, 0, 1, 16, 4096, int(rng.integers(0, 5000))]))
+    stride = max(stride, 1)
+    n = int(rng.choice([1, 5, 4095, 4096, 5000, 20000]))
+    while n * stride > (48 << 20) and n > 1:
+        n //= 2
+    offset = int(rng.choice([0, 0, 16, int(rng.integers(0, 4106))]))
+    size = offset + (n - 1) * stride + length + 64
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if rng.random() < 0.4 else None
+    d = torch.from_numpy(host).to(gpu)
+    ini = None if init is None else torch.from_numpy(init.view(np.int32)).to(gpu)
+    got = u32(tk.crc32_batch_uniform(d, length, n, stride=stride, init_raw=ini, offset=offset, algo=algo))
+    offs = offset + np.arange(n, dtype=np.int64) * stride
+    want = oracle_batch(oracle, algo, host, offs, np.full(n, length, np.int64), init)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, f"len={length} stride={stride} n={n} offset={offset} algo={algo}: {bad[:5]}"
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_update_chain_random(gpu, oracle, seed):
+    """crc32::update chained over random pieces (host spans and device tensors) equals one pass."""
+    rng = np.random.default_rng(3000 + seed)
+    algo = ALGOS[seed % 2]
+    pieces = [rng.integers(0, 256, int(rng.choice([0, 1, 5, 36, 700, 4096, 20000, 300000])), dtype=np.uint8)
+              for _ in range(int(rng.integers(1, 12)))]
+    c = tk.crc32() if algo == "crc32" else tk.crc32c()
+    raw = 0xFFFFFFFF
+    for i, p in enumerate(pieces):
+        c.update(torch.from_numpy(p).to(gpu) if i % 2 else p.tobytes())
+        raw = oracle.update(raw, p.tobytes()) if algo == "crc32" else oracle.update_c(raw, p.tobytes())
+    assert c.finalize() == raw ^ 0xFFFFFFFF
