@@ -5,9 +5,9 @@
 //
 // The record chain is a linked list through the image (record i+1 starts 8 + record_len bytes after
 // record i), so it is walked speculatively in parallel and stitched exactly:
-//  1. wal_scan (one streaming pass): the image is cut into pieces of kWalPiece bytes, and the first
-//     plausible header of every piece (one the reference encoder could have written,
-//     wal.cpp:19-61) becomes its speculative start S_k; piece 0 starts at 0.
+//  1. wal_scan_head: the image is cut into pieces of kWalPiece bytes, and the first plausible header
+//     of every piece (one the reference encoder could have written, wal.cpp:19-61), searched from
+//     the piece's front, becomes its speculative start S_k; piece 0 starts at 0.
 //  2. wal_spec: one lane per piece walks the chain from S_k over the records that start in the
 //     piece (X_k = the first record start at or past the piece's end, or the header that broke),
 //     and checks them as it goes: key/value bounds, and the CRC of every payload of at most
@@ -51,7 +51,7 @@ constexpr std::uint64_t kWalPiece = 2048;     // bytes of image per speculative 
 constexpr std::uint64_t kWalMeta = 26;        // wal.hpp:21-27 kMetadataSize
 constexpr std::uint32_t kWalLaneMax = 1024;   // payloads up to this size are checked by their lane
 constexpr std::uint64_t kNone = ~0ull;
-constexpr unsigned kScanThreads = 256;        // wal_scan: 32 positions per lane, 126 chunks per wave
+constexpr unsigned kScanThreads = 256;        // wal_scan_head: 8 lanes per piece, 8 pieces per wave
 constexpr unsigned kCheckThreads = 1024;      // wal_spec/wal_recheck: one workgroup per CU (128 KiB of LDS)
 
 struct WalArgs {
@@ -110,21 +110,6 @@ __device__ __forceinline__ std::uint64_t gid() {
   return blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
 }
 
-// 1. First plausible header per piece, one coalesced pass over the image. Lane l of a wave holds
-// the 32 bytes of absolute chunks t = t_wave + 2l and t + 1 (two 16-byte loads) and reports their
-// 32 positions, for l < 63; the last lane only lends its bytes. A header at position p has its op
-// and tombstone bytes (p+8, p+17) at 0 or 1 (wal.cpp:30-52). Each lane marks which of its 32 bytes
-// are 0 or 1 with byte-parallel arithmetic, takes its right neighbour's marks by a cross-lane shift,
-// and so tests all 32 positions at once; only positions that pass get the full check
-// (record_len = 18 + klen + vlen, fitting the image; re-read through L1). The kernel is
-// VALU-issue-bound, so each chunk is read and marked once (it was three times, by the chunk's own
-// lane and its two left neighbours), and a lane's fixed costs cover 32 positions. A wave covers
-// 2016 bytes, i.e. at most two pieces: one ballot per piece and wave, one atomic per piece and wave.
-constexpr unsigned kScanChunks = 126;  // chunks reported per wave: two per lane, lanes 0..62
-// 64-bit value of lane l (wave-uniform l), read with every lane active.
-__device__ __forceinline__ std::uint64_t readlane64_u(std::uint64_t v, std::uint32_t l) {
-  return dev::readlane64(v, l);
-}
 __device__ __forceinline__ std::uint32_t le1_bytes4(std::uint32_t d) {
   // 4-bit mask: bit i set iff byte i of d is 0 or 1
   const std::uint32_t x = d & 0xFEFEFEFEu;
@@ -132,62 +117,79 @@ __device__ __forceinline__ std::uint32_t le1_bytes4(std::uint32_t d) {
   return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
 }
 
-// Positions [plo, phi) only (pieces [plo, phi) / kWalPiece; t0 = the chunk holding plo).
-__global__ __launch_bounds__(kScanThreads) void wal_scan(WalArgs a, std::uint64_t t0, std::uint64_t plo,
-                                                          std::uint64_t phi) {
+// 1. The first plausible header of every piece, searched from the piece's front with an early exit.
+// A group of 8 lanes owns one piece and tests 224 positions per step. Lanes 0-6 each hold 32 bytes
+// (two 16-byte loads) and report their 32 positions; lane 7 only lends its bytes. A header at p has
+// its op and tombstone bytes (p+8, p+17) at 0 or 1 (wal.cpp:30-52): each lane marks which of its
+// bytes are 0 or 1 with byte-parallel arithmetic, takes its right neighbour's marks by a cross-lane
+// shift and so tests all 32 positions at once; only positions that pass get the full check
+// (record_len = 18 + klen + vlen, fitting the image; re-read through L1). The group moves on only
+// while no position of its piece passed. In a WAL of small records the first step finds the
+// header, so about 256 bytes of every 2 KiB piece are read; a piece inside a large value is scanned
+// whole. The earlier kernel scanned every position of the image in one coalesced pass: 1.11 ->
+// 0.85 ms on 1 GiB of 59-byte records, Zipf image unchanged (profiles/r2/wal_head_scan/). Each
+// piece has one owner, so the result is a plain store (S is preset to kNone; piece 0 starts at 0).
+constexpr unsigned kHeadLanes = 8;                   // lanes per piece
+constexpr unsigned kHeadChunks = 2 * (kHeadLanes - 1);  // 16-byte chunks reported per group and step
+__global__ __launch_bounds__(kScanThreads) void wal_scan_head(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
   const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
   const std::uintptr_t al = w0 & ~static_cast<std::uintptr_t>(15);
   const std::uint64_t off0 = w0 - al;
-  const std::uint32_t lane = threadIdx.x & 63u;
-  const std::uint64_t t_wave = t0 + (gid() >> 6) * kScanChunks;
-  const std::uint64_t t = t_wave + 2 * lane;  // this lane's two chunks: 32 bytes from 16t
-  const std::uintptr_t c0 = al + 16 * t;
   const std::uintptr_t end = w0 + a.size;
-  uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
-  if (c0 < end) v0 = *reinterpret_cast<const uint4*>(c0);
-  if (c0 + 16 < end) v1 = *reinterpret_cast<const uint4*>(c0 + 16);
-  const std::uint32_t f = le1_bytes4(v0.x) | le1_bytes4(v0.y) << 4 | le1_bytes4(v0.z) << 8 | le1_bytes4(v0.w) << 12 |
-                          le1_bytes4(v1.x) << 16 | le1_bytes4(v1.y) << 20 | le1_bytes4(v1.z) << 24 | le1_bytes4(v1.w) << 28;
-  const std::uint32_t f1 = static_cast<std::uint32_t>(__shfl_down(static_cast<int>(f), 1, 64));
-  const std::uint64_t F = f | static_cast<std::uint64_t>(f1) << 32;  // bit b: byte b of [16t, 16t + 64) is 0/1
-  std::uint32_t cand = static_cast<std::uint32_t>((F >> 8) & (F >> 17));  // bit j: bytes j+8 and j+17 are 0/1
-  // positions inside [plo, phi) with a full header left: j in [lo, hi]
-  const std::int64_t p0 = static_cast<std::int64_t>(16 * t) - static_cast<std::int64_t>(off0);
-  const std::int64_t last = std::min<std::int64_t>(static_cast<std::int64_t>(a.size) - static_cast<std::int64_t>(kWalMeta),
-                                                    static_cast<std::int64_t>(phi) - 1);
-  const std::int64_t lo = static_cast<std::int64_t>(plo) - p0, hi = last - p0;
-  if (2 * lane >= kScanChunks || hi < 0 || lo > 31) {
-    cand = 0;
-  } else {
-    const std::uint32_t jlo = lo < 0 ? 0u : static_cast<std::uint32_t>(lo);
-    const std::uint32_t jhi = hi > 31 ? 31u : static_cast<std::uint32_t>(hi);
-    cand &= (jhi == 31u ? 0xFFFFFFFFu : (2u << jhi) - 1u) & ~((1u << jlo) - 1u);
-  }
-  std::uint64_t best = kNone;
-  while (cand) {
-    const int j = __builtin_ctz(cand);
-    const std::uint64_t p = static_cast<std::uint64_t>(p0 + j);
-    const std::uint64_t rlen = ld32(a.w, p, a.size), klen = ld32(a.w, p + 18, a.size), vlen = ld32(a.w, p + 22, a.size);
-    if (rlen == 18u + klen + vlen && rlen + 8 <= a.size - p) {
-      best = p;
-      break;
+  const std::uint32_t lane = threadIdx.x & 63u, g = lane / kHeadLanes, i = lane % kHeadLanes;
+  const std::uint64_t k = k_lo + (gid() >> 6) * (64 / kHeadLanes) + g;
+  const std::uint64_t ps = k * kWalPiece;
+  // positions with a whole header inside the image and inside the piece: [ps, pe)
+  const std::uint64_t pe = a.size < kWalMeta ? 0 : std::min<std::uint64_t>(ps + kWalPiece, a.size - kWalMeta + 1);
+  bool active = k < k_hi && k != 0 && ps < pe;  // uniform within a group
+  const std::uint64_t tg = (ps + off0) / 16;   // the chunk holding ps
+  std::uint64_t found_at = kNone;
+  for (std::uint64_t step = 0; __ballot(active) != 0; ++step) {
+    const std::uint64_t t = tg + step * kHeadChunks + 2 * i;
+    const std::uintptr_t c0 = al + 16 * t;
+    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+    if (active && c0 < end) v0 = *reinterpret_cast<const uint4*>(c0);
+    if (active && c0 + 16 < end) v1 = *reinterpret_cast<const uint4*>(c0 + 16);
+    const std::uint32_t f = le1_bytes4(v0.x) | le1_bytes4(v0.y) << 4 | le1_bytes4(v0.z) << 8 | le1_bytes4(v0.w) << 12 |
+                            le1_bytes4(v1.x) << 16 | le1_bytes4(v1.y) << 20 | le1_bytes4(v1.z) << 24 |
+                            le1_bytes4(v1.w) << 28;
+    const std::uint32_t f1 = static_cast<std::uint32_t>(__shfl_down(static_cast<int>(f), 1, 64));
+    const std::uint64_t F = f | static_cast<std::uint64_t>(f1) << 32;
+    std::uint32_t cand = static_cast<std::uint32_t>((F >> 8) & (F >> 17));  // bytes j+8, j+17 are 0/1
+    const std::int64_t p0 = static_cast<std::int64_t>(16 * t) - static_cast<std::int64_t>(off0);
+    const std::int64_t lo = static_cast<std::int64_t>(ps) - p0, hi = static_cast<std::int64_t>(pe) - 1 - p0;
+    if (!active || i + 1 == kHeadLanes || hi < 0 || lo > 31) {
+      cand = 0;
+    } else {
+      const std::uint32_t jlo = lo < 0 ? 0u : static_cast<std::uint32_t>(lo);
+      const std::uint32_t jhi = hi > 31 ? 31u : static_cast<std::uint32_t>(hi);
+      cand &= (jhi == 31u ? 0xFFFFFFFFu : (2u << jhi) - 1u) & ~((1u << jlo) - 1u);
     }
-    cand &= cand - 1;
+    std::uint64_t best = kNone;
+    while (cand) {
+      const int j = __builtin_ctz(cand);
+      const std::uint64_t p = static_cast<std::uint64_t>(p0 + j);
+      const std::uint64_t rlen = ld32(a.w, p, a.size), klen = ld32(a.w, p + 18, a.size), vlen = ld32(a.w, p + 22, a.size);
+      if (rlen == 18u + klen + vlen && rlen + 8 <= a.size - p) {
+        best = p;
+        break;
+      }
+      cand &= cand - 1;
+    }
+    // positions grow with the lane index inside a group: its first header is its lowest finder's
+    const std::uint64_t bal = __ballot(best != kNone);
+    const std::uint32_t gb = static_cast<std::uint32_t>(bal >> (g * kHeadLanes)) & ((1u << (kHeadLanes - 1)) - 1u);
+    const std::uint32_t src = g * kHeadLanes + (gb ? static_cast<std::uint32_t>(__builtin_ctz(gb)) : 0u);
+    const std::uint64_t first = __shfl(best, static_cast<int>(src), 64);
+    const std::int64_t next_p0 = static_cast<std::int64_t>(16 * (tg + (step + 1) * kHeadChunks)) - static_cast<std::int64_t>(off0);
+    if (active && gb) {
+      found_at = first;
+      active = false;
+    } else if (next_p0 >= static_cast<std::int64_t>(pe)) {
+      active = false;
+    }
   }
-  // the wave's positions span pieces pa and pa + 1
-  const std::int64_t wave_p0 = static_cast<std::int64_t>(16 * t_wave) - static_cast<std::int64_t>(off0);
-  const std::uint64_t pa = wave_p0 < 0 ? 0 : static_cast<std::uint64_t>(wave_p0) / kWalPiece;
-  // Positions grow with the lane index, so a piece's first header in this wave is the one of the
-  // lowest lane that found one there: a ballot and a lane read, not a shuffle reduction.
-  const bool found = best != kNone;
-  const bool inA = found && best / kWalPiece == pa;
-  const std::uint64_t balA = __ballot(inA), balB = __ballot(found && !inA);
-  const std::uint64_t mA = readlane64_u(best, balA ? static_cast<std::uint32_t>(__builtin_ctzll(balA)) : 0u);
-  const std::uint64_t mB = readlane64_u(best, balB ? static_cast<std::uint32_t>(__builtin_ctzll(balB)) : 0u);
-  if (lane == 0) {
-    if (balA && pa != 0) atomicMin(reinterpret_cast<unsigned long long*>(&a.S[pa]), mA);
-    if (balB && pa + 1 < a.K) atomicMin(reinterpret_cast<unsigned long long*>(&a.S[pa + 1]), mB);
-  }
+  if (i == 0 && found_at != kNone) a.S[k] = found_at;
 }
 
 // One slicing-by-4 step of the lane's register over dword w (the engine's replicated LDS tables).
@@ -671,13 +673,8 @@ int pass_begin(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStre
 
 void pass_front(const WalArgs& a, std::uint64_t k_lo, std::uint64_t k_hi, hipStream_t st) {
   if (k_hi <= k_lo) return;
-  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
-  const std::uint64_t off0 = w0 & 15u;
-  const std::uint64_t plo = k_lo * kWalPiece, phi = std::min<std::uint64_t>(k_hi * kWalPiece, a.size);
-  const std::uint64_t t0 = (plo + off0) / 16;  // the chunk holding plo
-  const std::uint64_t t1 = (phi + off0 + 15) / 16;
-  const std::uint64_t threads = (t1 - t0 + kScanChunks - 1) / kScanChunks * 64;  // kScanChunks chunks per wave
-  hipLaunchKernelGGL(wal_scan, dim3(blocks(threads, kScanThreads)), dim3(kScanThreads), 0, st, a, t0, plo, phi);
+  const std::uint64_t threads = (k_hi - k_lo + 64 / kHeadLanes - 1) / (64 / kHeadLanes) * 64;  // 8 pieces per wave
+  hipLaunchKernelGGL(wal_scan_head, dim3(blocks(threads, kScanThreads)), dim3(kScanThreads), 0, st, a, k_lo, k_hi);
   hipLaunchKernelGGL(wal_spec, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
 }
 
