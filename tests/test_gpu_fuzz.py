@@ -47,11 +47,19 @@ def oracle_batch(oracle, algo, host, offs, lens, init):
     return out
 
 
+def on_device(host, gpu, shift):
+    """host bytes on the GPU at `shift` bytes past a 256-byte aligned allocation (the batch APIs take
+    any base pointer; stream mode's row 0 may then start before it)."""
+    d = torch.zeros(host.size + shift, dtype=torch.uint8, device=gpu)
+    d[shift:] = torch.from_numpy(host).to(gpu)
+    return d[shift:]
+
+
 def irregular_mode():
     return tk.load_library().tkv_debug_irregular_mode(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
 
 
-@pytest.mark.parametrize("seed", range(48))
+@pytest.mark.parametrize("seed", range(96))
 def test_irregular_random(gpu, oracle, seed):
     rng = np.random.default_rng(1000 + seed)
     algo = ALGOS[seed % 2]
@@ -70,20 +78,21 @@ def test_irregular_random(gpu, oracle, seed):
     size = int((offs + lens).max()) + 64
     host = rng.integers(0, 256, size, dtype=np.uint8)
     init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if rng.random() < 0.5 else None
-    d = torch.from_numpy(host).to(gpu)
+    shift = int(rng.integers(0, 16)) if seed % 3 else 0
+    d = on_device(host, gpu, shift)
     o = torch.from_numpy(offs.astype(np.int64)).to(gpu)
     ln = torch.from_numpy(lens.astype(np.int32)).to(gpu)
     ini = None if init is None else torch.from_numpy(init.view(np.int32)).to(gpu)
     got = u32(tk.crc32_batch(d, o, ln, init_raw=ini, algo=algo))
     want = oracle_batch(oracle, algo, host, offs, lens, init)
     bad = np.flatnonzero(got != want)
-    assert bad.size == 0, (f"{layout} n={n} start={start} algo={algo} mode={irregular_mode()}: "
+    assert bad.size == 0, (f"{layout} n={n} start={start} shift={shift} algo={algo} mode={irregular_mode()}: "
                            f"{bad.size} blocks differ, first {bad[:5]} (lens {lens[bad[:5]]})")
     if layout == "back_to_back_min64" and n > 1:
         assert irregular_mode() == 1, "a back-to-back batch of blocks >= 64 B takes stream mode"
 
 
-@pytest.mark.parametrize("seed", range(32))
+@pytest.mark.parametrize("seed", range(64))
 def test_uniform_random(gpu, oracle, seed):
     rng = np.random.default_rng(2000 + seed)
     algo = ALGOS[seed % 2]
@@ -97,16 +106,17 @@ def test_uniform_random(gpu, oracle, seed):
     size = offset + (n - 1) * stride + length + 64
     host = rng.integers(0, 256, size, dtype=np.uint8)
     init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if rng.random() < 0.4 else None
-    d = torch.from_numpy(host).to(gpu)
+    shift = int(rng.integers(0, 16)) if seed % 3 else 0
+    d = on_device(host, gpu, shift)
     ini = None if init is None else torch.from_numpy(init.view(np.int32)).to(gpu)
     got = u32(tk.crc32_batch_uniform(d, length, n, stride=stride, init_raw=ini, offset=offset, algo=algo))
     offs = offset + np.arange(n, dtype=np.int64) * stride
     want = oracle_batch(oracle, algo, host, offs, np.full(n, length, np.int64), init)
     bad = np.flatnonzero(got != want)
-    assert bad.size == 0, f"len={length} stride={stride} n={n} offset={offset} algo={algo}: {bad[:5]}"
+    assert bad.size == 0, f"len={length} stride={stride} n={n} offset={offset} shift={shift} algo={algo}: {bad[:5]}"
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", range(16))
 def test_update_chain_random(gpu, oracle, seed):
     """crc32::update chained over random pieces (host spans and device tensors) equals one pass."""
     rng = np.random.default_rng(3000 + seed)
@@ -116,6 +126,45 @@ def test_update_chain_random(gpu, oracle, seed):
     c = tk.crc32() if algo == "crc32" else tk.crc32c()
     raw = 0xFFFFFFFF
     for i, p in enumerate(pieces):
-        c.update(torch.from_numpy(p).to(gpu) if i % 2 else p.tobytes())
+        c.update(on_device(p, gpu, int(rng.integers(0, 16))) if i % 2 else p.tobytes())
         raw = oracle.update(raw, p.tobytes()) if algo == "crc32" else oracle.update_c(raw, p.tobytes())
     assert c.finalize() == raw ^ 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("seed", range(96))
+def test_wal_verify_random(gpu, oracle, seed):
+    """Device WAL recovery verify (host-image and device-image paths) on random WAL images against
+    the sequential decode of wal.cpp:63-130 (test_gpu_wal_device.sequential_decode): random record
+    counts and value sizes, values holding fake headers, torn tails, an unaligned device image, and
+    one random corruption: a payload bit, the stored CRC, a lying record_len, a key/value length that
+    overruns the record under a valid CRC (caught after the CRC, wal.cpp:118-121), or any byte."""
+    from test_gpu_wal_device import both, make_wal, sequential_decode
+    rng = np.random.default_rng(4000 + seed)
+    n_rec = int(rng.choice([1, 2, 7, 300, 5000, 20000, 120000]))
+    vmax = int(rng.choice([64, 600, 5000, 16000])) if n_rec < 100000 else 600
+    img, offs, size = make_wal(rng, n_rec, vmax=vmax, fake_headers=float(rng.choice([0.0, 0.0, 0.3])))
+    kind = ("none", "payload", "crc", "record_len", "kv_overflow", "any")[seed % 6]
+    r = int(rng.integers(0, n_rec))
+    o = int(offs[r])
+    if kind == "payload":
+        img[o + 8 + int(rng.integers(0, int(size[r]) - 8))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    elif kind == "crc":
+        img[o + 4 + int(rng.integers(0, 4))] ^= np.uint8(0x10)
+    elif kind == "record_len":
+        delta = int(rng.choice([-9, -1, 1, 5, 4096, 1 << 20]))
+        img[o:o + 4] = np.frombuffer(((int(size[r]) - 8 + delta) & 0xFFFFFFFF).to_bytes(4, "little"), np.uint8)
+    elif kind == "kv_overflow":
+        img[o + 22:o + 26] = np.frombuffer((int(size[r])).to_bytes(4, "little"), np.uint8)  # vlen > what fits
+        lib = tk.load_library()
+        one_off = np.array([o], np.uint64)
+        one_len = np.array([int(size[r])], np.uint32)
+        tk.check(lib.tkv_wal_stamp(ctypes.c_void_p(img.ctypes.data), ctypes.c_void_p(one_off.ctypes.data),
+                                   ctypes.c_void_p(one_len.ctypes.data), 1))  # a valid CRC over the bad lengths
+    elif kind == "any":
+        img[int(rng.integers(0, img.size))] ^= np.uint8(int(rng.integers(1, 256)))
+    n = img.size if rng.random() < 0.6 else int(rng.integers(0, img.size + 1))  # torn tail
+    want = sequential_decode(oracle, img, n)
+    if kind == "kv_overflow" and o + int(size[r]) <= n:
+        assert want[0] == "corrupted" and want[2] <= o
+    got = both(img, n, shift=int(rng.integers(0, 16)))
+    assert got == (want, want), f"kind={kind} record={r} n_rec={n_rec} vmax={vmax} n={n}"

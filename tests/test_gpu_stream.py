@@ -111,3 +111,25 @@ def test_stream_then_general_on_same_scratch(gpu, oracle):
         assert run(gpu, oracle, lens, start=k, seed=20 + k) == 1
         lens[7] = 10
         assert run(gpu, oracle, lens, start=k, seed=30 + k) == 0
+
+
+@pytest.mark.parametrize("nblocks", [1, 2, 300])
+def test_stream_row0_before_a_misaligned_base(gpu, oracle, nblocks):
+    """A base pointer that is not 16-byte aligned, with the stream starting in its first bytes: row 0
+    (the stream start rounded down to 16 bytes) then starts before the base pointer. Its offset from
+    base wraps as a u64; the row count must still come out right (it read 0 rows, and every CRC was
+    wrong, for base shifts 1-7 with the stream at offset 8, before the fix)."""
+    rng = np.random.default_rng(nblocks)
+    lens = rng.integers(64, 9000, nblocks)
+    for shift in range(16):
+        for first in (0, 3, 8, 15):
+            offs = (first + np.concatenate([[0], np.cumsum(lens[:-1])])).astype(np.int64)
+            size = int(offs[-1] + lens[-1]) + 64
+            host = rng.integers(0, 256, size, dtype=np.uint8)
+            d = torch.zeros(size + shift, dtype=torch.uint8, device=gpu)
+            d[shift:] = torch.from_numpy(host).to(gpu)
+            got = u32(tk.crc32_batch(d[shift:], torch.from_numpy(offs).to(gpu),
+                                     torch.from_numpy(lens.astype(np.int32)).to(gpu)))
+            assert mode() == 1
+            want = oracle.batch(host, offs, lens)
+            assert np.array_equal(got, want), (shift, first)

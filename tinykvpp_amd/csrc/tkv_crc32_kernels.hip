@@ -152,9 +152,12 @@ __device__ __forceinline__ StreamGeom stream_geometry(const std::uint8_t* base, 
                                                       const std::uint32_t* lengths, std::uint32_t n) {
   const std::uint64_t off0 = offsets[0];
   const std::uint64_t s0rel = (reinterpret_cast<std::uintptr_t>(base) + off0) & 15u;
+  // zoff may lie up to 15 bytes before base (a base that is not 16-byte aligned, with the stream
+  // starting in its first bytes): it wraps as a u64, and base + zoff is still row 0's address, so
+  // the row count is taken from the stream's own extent, never by comparing with zoff.
   const std::uint64_t zoff = off0 - s0rel;
   const std::uint64_t end = offsets[n - 1] + lengths[n - 1];
-  return {zoff, s0rel, end > zoff ? (end - zoff + kRow - 1) / kRow : 0};
+  return {zoff, s0rel, end >= off0 ? (end - off0 + s0rel + kRow - 1) / kRow : 0};
 }
 
 __global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase, const std::uint64_t* offsets,
