@@ -250,3 +250,27 @@ def test_wal_stamp_random(gpu, oracle, seed):
         assert s[:4] == r[:4] and s[8:] == r[8:]
         assert int.from_bytes(s[4:8], "little") == oracle.crc(r[8:])
     assert wal.verify(b"".join(stamped)) == ("ok", n, sum(len(s) for s in stamped))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_stream_many_blocks_random(gpu, oracle, seed):
+    """Stream mode over 50 K-200 K back-to-back blocks (several block ends per row and lane segment
+    boundary, every wave holding ends), any base alignment and stream start, per-block initial
+    registers, both polynomials."""
+    rng = np.random.default_rng(8000 + seed)
+    algo = ALGOS[seed % 2]
+    n = int(rng.integers(50_000, 200_000))
+    lens = rng.integers(64, int(rng.choice([65, 128, 600, 3000])), n).astype(np.int64)
+    start = int(rng.integers(0, 64))
+    offs = start + np.concatenate([[0], np.cumsum(lens)[:-1]])
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if seed % 3 == 0 else None
+    shift = int(rng.integers(0, 16))
+    d = on_device(host, gpu, shift)
+    ini = None if init is None else torch.from_numpy(init.view(np.int32)).to(gpu)
+    got = u32(tk.crc32_batch(d, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu),
+                             init_raw=ini, algo=algo))
+    assert irregular_mode() == 1
+    want = oracle_batch(oracle, algo, host, offs, lens, init)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, f"n={n} start={start} shift={shift} algo={algo}: {bad.size} differ, first {bad[:5]}"
