@@ -172,9 +172,9 @@ def test_wal_verify_random(gpu, oracle, seed):
 
 @pytest.mark.parametrize("seed", range(48))
 def test_host_batch_random(gpu, oracle, seed):
-    """tkv_crc32[c]_batch_host[_multi] over pageable host memory at any alignment (the staged
-    pipeline; dense runs, gathers, blocks longer than a slab cut across devices), random layouts and
-    initial registers, against the oracle."""
+    """tkv_crc32[c]_batch_host[_multi] over pageable host memory (the staged pipeline: dense runs,
+    gathers, blocks cut across devices) and pinned host memory (read in place) at any alignment,
+    random layouts and initial registers, against the oracle."""
     rng = np.random.default_rng(5000 + seed)
     algo = ALGOS[seed % 2]
     n = int(rng.choice([1, 3, 40, 256, 257, 3000]))
@@ -191,14 +191,19 @@ def test_host_batch_random(gpu, oracle, seed):
     shift = int(rng.integers(0, 16))
     size = int((offs + lens).max()) + 64
     raw = rng.integers(0, 256, size + shift, dtype=np.uint8)
-    host = raw[shift:]  # a pageable source at any alignment
+    pinned = seed % 2 == 1
+    if pinned:  # a pinned source: the kernels read it in place over PCIe (mapped_batch)
+        pin = torch.empty(size + shift, dtype=torch.uint8, pin_memory=True)
+        pin.numpy()[:] = raw
+        raw = pin.numpy()
+    host = raw[shift:]  # a source at any alignment
     init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if rng.random() < 0.4 else None
     devices = (None, [0], [0, 0], [0, 0, 0, 0])[seed % 4]
     got = tk.crc32_batch_host(host, offs.astype(np.uint64), lens.astype(np.uint32), init_raw=init,
                               devices=devices, algo=algo)
     want = oracle_batch(oracle, algo, host, offs.astype(np.int64), lens, init)
     bad = np.flatnonzero(got != want)
-    assert bad.size == 0, f"{layout} n={n} shift={shift} devices={devices} algo={algo}: {bad[:5]}"
+    assert bad.size == 0, f"{layout} n={n} shift={shift} pinned={pinned} devices={devices} algo={algo}: {bad[:5]}"
 
 
 @pytest.mark.parametrize("seed", range(24))
