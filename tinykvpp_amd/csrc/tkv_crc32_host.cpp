@@ -922,7 +922,6 @@ int update_impl(int algo, uint32_t raw_state, const void* data, size_t len, uint
     std::memcpy(c->h_small, data, len);
     const SpanDesc one{0, static_cast<std::uint32_t>(len), raw_state, 0};
     return run_spans(c, algo, one, 1, 0u, out_raw);
-    return TKV_OK;
   }
   const std::size_t want = std::min<std::size_t>(std::max<std::size_t>(len, 1 << 16), kSlab);
   if (want > c->stage_cap) {
