@@ -168,6 +168,11 @@ def test_wal_verify_random(gpu, oracle, seed):
         assert want[0] == "corrupted" and want[2] <= o
     got = both(img, n, shift=int(rng.integers(0, 16)))
     assert got == (want, want), f"kind={kind} record={r} n_rec={n_rec} vmax={vmax} n={n}"
+    if seed % 3 == 0:  # the host image in pinned memory at any alignment (read in place)
+        pshift = int(rng.integers(0, 16))
+        pin = torch.empty(n + pshift, dtype=torch.uint8, pin_memory=True)
+        pin.numpy()[pshift:] = img[:n]
+        assert tk.wal.verify(pin.numpy()[pshift:]) == want, f"pinned shift {pshift}"
 
 
 @pytest.mark.parametrize("seed", range(48))
@@ -254,7 +259,19 @@ def test_wal_stamp_random(gpu, oracle, seed):
     for r, s in zip(recs, stamped):
         assert s[:4] == r[:4] and s[8:] == r[8:]
         assert int.from_bytes(s[4:8], "little") == oracle.crc(r[8:])
-    assert wal.verify(b"".join(stamped)) == ("ok", n, sum(len(s) for s in stamped))
+    image = b"".join(stamped)
+    assert wal.verify(image) == ("ok", n, len(image))
+    # the same group commit in place in a pinned append buffer at any alignment
+    shift = int(rng.integers(0, 16))
+    pin = torch.empty(len(image) + shift, dtype=torch.uint8, pin_memory=True)
+    buf = pin.numpy()[shift:]
+    buf[:] = np.frombuffer(b"".join(recs), np.uint8)
+    sizes = np.array([len(r) for r in recs], np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    tk.check(tk.load_library().tkv_wal_stamp(ctypes.c_void_p(buf.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                                             ctypes.c_void_p(sizes.ctypes.data), n))
+    assert buf.tobytes() == image, f"pinned stamp differs (shift {shift})"
 
 
 @pytest.mark.parametrize("seed", range(12))
