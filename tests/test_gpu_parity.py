@@ -657,3 +657,22 @@ def test_rank_shards_full_size(gpu, oracle, cfg):
             got = u32(tk.crc32_batch_uniform(d, blen, n))
         del d
         assert aggregates(got) == (sh["xor"], sh["sum32"]), f"{cfg} shard at block {first}"
+
+
+@pytest.mark.parametrize("blen", [64, 128, 256, 512, 1024, 2048])
+def test_packed_small_blocks(gpu, oracle, blen):
+    """Uniform batches of 64*G-byte blocks packed back to back (G-lane groups, 64/G blocks per 4 KiB
+    row): batches ending in a partial row, single blocks, and a batch large enough
+    for every wave, against the oracle; raw registers through update_device."""
+    rng = np.random.default_rng(blen)
+    bpr = 4096 // blen
+    for n in (1, 2, bpr - 1, bpr, bpr + 1, 4096 * bpr + 3, 300_000 // max(1, blen // 64)):
+        host = rng.integers(0, 256, n * blen + 64, dtype=np.uint8)
+        d = torch.from_numpy(host).to(gpu)
+        got = u32(tk.crc32_batch_uniform(d, blen, n))
+        offs = np.arange(n, dtype=np.uint64) * blen
+        want = oracle.batch(host, offs, np.full(n, blen, np.uint32))
+        bad = np.flatnonzero(got != want)
+        assert bad.size == 0, (n, bad[:5])
+    c = tk.crc32().update(torch.from_numpy(host[:blen].copy()).to(gpu))
+    assert c.finalize() == oracle.crc(host[:blen].tobytes())

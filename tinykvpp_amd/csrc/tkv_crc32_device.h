@@ -1065,6 +1065,122 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
 }
 
 
+// ---- packed small blocks: uniform batches of len = 64*G bytes (G = 1, 2, 4, ..., 32), stride == len,
+// 16-byte aligned base. A 4 KiB row holds 64/G whole blocks; lane l folds its 64
+// bytes as in crc_packed_body, its G-lane group (the lanes of one block) moves the partials to the
+// block's end and XORs them together, so no row carries padding. The generic kernel gave every such
+// block a whole zero-padded 4 KiB row (8x the table lookups of its bytes at 512 B).
+
+// LDS image for G-lane groups: the slicing tables as fill_lds stores them, and in lane-shift column
+// l the shift of lane l%G of a G-lane block, Shift_{(G-1-l%G)*64}, which is column 64-G+l%G of the
+// device tables (LS[j][v][c] = Shift_{(63-c)*64}); every lane keeps a column of its own, so the
+// lookups stay free of bank conflicts. G = 1 needs no lane shift.
+template <int G>
+__device__ __forceinline__ void fill_lds_group(const DeviceTables* tabs, std::uint32_t* lds) {
+  for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
+    const std::uint32_t pair = u >> 9, e = (u >> 1) & 255u, t = u & 1u;
+    const std::uint32_t v = tabs->slice[2 * pair + t][e];
+    uint4* dst = reinterpret_cast<uint4*>(lds + pair * 16384u + e * 64u + t * 32u);
+#pragma unroll
+    for (std::uint32_t k = 0; k < 8u; ++k) dst[(k + u) & 7u] = make_uint4(v, v, v, v);
+  }
+  if constexpr (G >= 4) {
+    const uint4* ls = reinterpret_cast<const uint4*>(&tabs->lane_shift[0][0][0]);
+    uint4* lds_ls = reinterpret_cast<uint4*>(lds + kLdsSliceWords);
+    for (std::uint32_t i = threadIdx.x; i < kLdsLaneWords / 4u; i += blockDim.x)
+      lds_ls[i] = ls[(i & ~15u) + (64u - G + (4u * (i & 15u)) % G) / 4u];
+  } else if constexpr (G == 2) {
+    const std::uint32_t* ls = &tabs->lane_shift[0][0][0];
+    std::uint32_t* lds_ls = lds + kLdsSliceWords;
+    for (std::uint32_t i = threadIdx.x; i < static_cast<std::uint32_t>(kLdsLaneWords); i += blockDim.x)
+      lds_ls[i] = ls[(i & ~63u) + 62u + (i & 1u)];
+  }
+}
+
+// XOR over each G-lane group (G <= 32) with the first steps of wave_xor_to_lane63: for G <= 16 every
+// lane of a group ends with the group's sum; for G = 32 lanes 16-31 and 48-63 do.
+template <int G>
+__device__ __forceinline__ std::uint32_t group_xor(std::uint32_t v) {
+  if constexpr (G >= 2) v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  if constexpr (G >= 4) v ^= __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  if constexpr (G >= 8) v ^= __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  if constexpr (G >= 16) v ^= __builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, false); // row_mirror
+  if constexpr (G >= 32) v ^= __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1,3
+  return v;
+}
+
+// Batch rows (4 KiB each, 64/G blocks) are split over the waves in contiguous ranges, with the
+// packed kernel's pipeline and issue priority. Every block starts from init_default (per-block
+// initial registers take the generic kernel): raw = Shift_len(init) ^ crc_0(block), with
+// Shift_len(init) = head_z * init (head_z = x^(8 len)) added by the lane that stores the block.
+template <int G, int DEPTH, int ILP, int PRIO = 0>
+__device__ __forceinline__ void crc_packed_small_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(G >= 1 && G <= 32 && (G & (G - 1)) == 0, "G-lane groups of a power of two up to 32");
+  static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
+  constexpr std::uint32_t kBpr = 64u / G;  // blocks per row
+  fill_lds_group<G>(a.tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const LaneConst kc = lane_const(lane);
+  const std::uint32_t K = multmodp(a.head_z, a.init_default, a.tabs->poly) ^ a.out_xor;
+  const bool stores = (lane % G) == G - 1u;
+  __syncthreads();
+
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves, TR = a.total_rows;
+  const std::uint32_t r0 = static_cast<std::uint32_t>(wave * TR / W);
+  const std::uint32_t nrows = static_cast<std::uint32_t>((wave + 1) * TR / W) - r0;
+  if (nrows == 0) return;
+  // lane's block in row j of the range: (r0 + j) * kBpr + lane / G; in the batch's last row the
+  // lanes past its last block read that row's first segment instead (their results are not stored)
+  const std::uint64_t row_base = reinterpret_cast<std::uintptr_t>(a.base) + static_cast<std::uint64_t>(r0) * kRow;
+  const std::uint32_t lane_blk = lane / G;
+
+  uint4 buf[DEPTH][4];
+  auto issue = [&](std::uint32_t j, uint4 (&q)[4]) {
+    const std::uint32_t jc = j < nrows ? j : nrows - 1;  // rows past the range reload the last one
+    const bool live = static_cast<std::uint64_t>(r0 + jc) * kBpr + lane_blk < a.nblocks;
+    const std::uintptr_t p = row_base + static_cast<std::uint64_t>(jc) * kRow + (live ? lane * kSeg : 0u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i);
+  };
+  auto finish = [&](std::uint32_t j, std::uint32_t p) {
+    std::uint32_t v = p;
+    if constexpr (G > 1) v = group_xor<G>(lane_shift(lds, v, kc));
+    const std::uint64_t blk = static_cast<std::uint64_t>(r0 + j) * kBpr + lane_blk;
+    if (stores && blk < a.nblocks) a.out[blk] = v ^ K;
+  };
+
+#pragma unroll
+  for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
+  for (std::uint32_t j = 0; j < nrows; j += DEPTH) {
+    if constexpr (PRIO != 0) set_prio_from_left<PRIO>(nrows - j, nrows);
+#pragma unroll
+    for (int q = 0; q < DEPTH; q += ILP) {
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) issue(j + q + DEPTH - ILP + i, buf[(q + DEPTH - ILP + i) % DEPTH]);
+      const std::uint32_t jq = j + q;
+      if (jq >= nrows) break;
+      Reg p[ILP];
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) p[i] = Reg{0, 0};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].x, kc);
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].y, kc);
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].z, kc);
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) slice4(lds, p[i], buf[q + i][t].w, kc);
+      }
+#pragma unroll
+      for (int i = 0; i < ILP; ++i)
+        if (jq + i < nrows) finish(jq + i, p[i].value());
+    }
+  }
+}
+
 // Combine the partials of blocks that were split between waves: one thread per seam record (two
 // per wave) shifts its piece's partial past the rows that follow it in the block and XORs it into
 // the block's result, which the head piece seeded with xorout. All pieces of a block combine in

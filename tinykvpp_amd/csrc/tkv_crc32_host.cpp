@@ -28,6 +28,8 @@ namespace tkv {
 hipError_t launch_rows(const RowsArgs& a, bool aligned, bool uniform, unsigned grid, hipStream_t st);
 hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
 hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st);
+bool packed_small_len(std::uint32_t len);
+hipError_t launch_packed_small(const RowsArgs& a, unsigned grid, hipStream_t st);
 hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
                           std::uint32_t n, std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* tile_ok,
                           std::uint32_t* counts, std::uint64_t* sinfo, std::uint64_t* ends, const PrepassOut& o,
@@ -444,6 +446,16 @@ int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t s
     a.nwaves = static_cast<std::uint32_t>(packed_waves);
     a.snap_blocks = 1;
     TKV_HIP(launch_packed(a, static_cast<unsigned>(c->ncu), st));  // whole blocks per wave, no seams
+    return TKV_OK;
+  }
+  if (aligned && !d_init && stride == len && packed_small_len(a.len)) {
+    // 4 KiB rows of 64/G whole blocks; as many workgroups as there are rows to give
+    const std::uint64_t bpr = kRow / len;
+    a.total_rows = static_cast<std::uint32_t>((n + bpr - 1) / bpr);
+    const std::uint64_t grid = std::max<std::uint64_t>(
+        1, std::min<std::uint64_t>(c->ncu, (a.total_rows + kWavesPerWG - 1) / kWavesPerWG));
+    a.nwaves = static_cast<std::uint32_t>(grid * kWavesPerWG);
+    TKV_HIP(launch_packed_small(a, static_cast<unsigned>(grid), st));
     return TKV_OK;
   }
   // Launch only as many workgroups as there are rows to give them (small batches).

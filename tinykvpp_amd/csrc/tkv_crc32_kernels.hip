@@ -123,6 +123,13 @@ __global__ __launch_bounds__(kThreads) void crc_packed(RowsArgs a) {
   dev::crc_packed_body<kPackedDepth, kPackedIlp, R1, R1 ? 0 : kPackedSkew, kPackedPrio>(a, lds);
 }
 
+// Packed small blocks (len = 64*G < 4 KiB, stride == len, 16-byte aligned, default init): DESIGN.md §4.4.
+template <int G>
+__global__ __launch_bounds__(kThreads) void crc_packed_small(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  dev::crc_packed_small_body<G, kPackedDepth, kPackedIlp, kPackedPrio>(a, lds);
+}
+
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 
 }  // namespace
@@ -518,6 +525,23 @@ hipError_t launch_rows(const RowsArgs& a, bool aligned, bool uniform, unsigned g
 hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st) {
   if (a.len == kRow) hipLaunchKernelGGL(crc_packed<true>, dim3(grid), dim3(kThreads), 0, st, a);
   else hipLaunchKernelGGL(crc_packed<false>, dim3(grid), dim3(kThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+bool packed_small_len(std::uint32_t len) {
+  return len == 64u || len == 128u || len == 256u || len == 512u || len == 1024u || len == 2048u;
+}
+
+hipError_t launch_packed_small(const RowsArgs& a, unsigned grid, hipStream_t st) {
+  switch (a.len) {
+    case 64: hipLaunchKernelGGL(crc_packed_small<1>, dim3(grid), dim3(kThreads), 0, st, a); break;
+    case 128: hipLaunchKernelGGL(crc_packed_small<2>, dim3(grid), dim3(kThreads), 0, st, a); break;
+    case 256: hipLaunchKernelGGL(crc_packed_small<4>, dim3(grid), dim3(kThreads), 0, st, a); break;
+    case 512: hipLaunchKernelGGL(crc_packed_small<8>, dim3(grid), dim3(kThreads), 0, st, a); break;
+    case 1024: hipLaunchKernelGGL(crc_packed_small<16>, dim3(grid), dim3(kThreads), 0, st, a); break;
+    case 2048: hipLaunchKernelGGL(crc_packed_small<32>, dim3(grid), dim3(kThreads), 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
