@@ -368,6 +368,47 @@ __global__ __launch_bounds__(1024) void k_pat(const std::uint8_t* base, std::uin
 }
 
 
+// Block-per-lane probe (memory only): lane l of a wave walks 4 KiB block (64 t + l) of its tile t
+// in steps of QB bytes (QB/16 loads of 16 bytes), DEPTH steps in flight; waves own contiguous tile
+// ranges. A CRC kernel on this layout needs no lane shift and no wave reduction (each lane's chain
+// is its block's CRC); the question is whether loads that touch 64 lines each keep the stream rate.
+template <int QB, int DEPTH>
+__global__ __launch_bounds__(1024) void k_blk(const std::uint8_t* base, std::uint32_t nrows, std::uint32_t W,
+                                              std::uint32_t* out) {
+  constexpr int NL = QB / 16;
+  constexpr std::uint32_t SPT = 4096u / QB;  // steps per tile
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint32_t wave = blockIdx.x * 16 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t ntiles = (nrows + 1) / 64u;
+  const std::uint32_t t0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(ntiles) / W);
+  const std::uint32_t t1 = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(ntiles) / W);
+  const std::uint32_t S = (t1 - t0) * SPT;
+  if (S == 0) return;
+  auto addr = [&](std::uint32_t s, int i) -> std::uintptr_t {
+    const std::uint32_t sc = s < S ? s : S - 1;
+    const std::uint64_t blk = static_cast<std::uint64_t>(t0 + sc / SPT) * 64u + lane;
+    return reinterpret_cast<std::uintptr_t>(base) + blk * 4096u + (sc % SPT) * QB + 16u * i;
+  };
+  uint4 buf[DEPTH][NL];
+  std::uint32_t acc = 0;
+#pragma unroll
+  for (int s = 0; s < DEPTH - 1; ++s)
+#pragma unroll
+    for (int i = 0; i < NL; ++i) buf[s][i] = dev::gload16(addr(s, i));
+  for (std::uint32_t g = 0; g < S; g += DEPTH) {
+#pragma unroll
+    for (int k = 0; k < DEPTH; ++k) {
+      const int sl = (k + DEPTH - 1) % DEPTH;
+#pragma unroll
+      for (int i = 0; i < NL; ++i) buf[sl][i] = dev::gload16(addr(g + k + DEPTH - 1, i));
+      if (g + k >= S) break;
+#pragma unroll
+      for (int i = 0; i < NL; ++i) acc ^= buf[k][i].x ^ buf[k][i].y ^ buf[k][i].z ^ buf[k][i].w;
+    }
+  }
+  if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
 // Interference probe: the packed kernel's loads and pipeline (D4, seg64, batched stores), plus
 // per row NLDS conflict-free ds_read_b32 in 4-wide dependent steps and/or NVALU dependent VALU
 // ops, to see which pipe's activity slows the memory stream.
@@ -544,6 +585,11 @@ template <int PAT, int D, int F, int MIS = 0, int STR = 0>
 void P(XArgs a, hipStream_t s) {
   hipLaunchKernelGGL((k_pat<PAT, D, F, MIS, STR>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows - 1, a.nwaves,
                      a.out);
+}
+
+template <int QB, int D>
+void BL(XArgs a, hipStream_t s) {
+  hipLaunchKernelGGL((k_blk<QB, D>), dim3(g_ncu), dim3(1024), 0, s, a.base, a.total_rows - 1, a.nwaves, a.out);
 }
 
 template <int D, int I, bool R1, int T, bool SP, std::uint32_t ROT = 0, int CHK = 0>
@@ -795,6 +841,8 @@ const V kVariants[] = {
     {"crc D4 I2", L<4, 2, 0>}, {"crc D6 I2", L<6, 2, 0>},
     {"mem D2 I1", L<2, 1, 1>}, {"mem D4 I1", L<4, 1, 1>}, {"mem D4 I2", L<4, 2, 1>},
     {"mem D8 I1", L<8, 1, 1>},
+    {"blk q64 D4", BL<64, 4>}, {"blk q128 D2", BL<128, 2>}, {"blk q128 D3", BL<128, 3>},
+    {"blk q128 D4", BL<128, 4>}, {"blk q256 D2", BL<256, 2>},
     {"pat seg64 D4 fin0 strided", P<0, 4, 0, 0, 1>}, {"pat coal D4 fin0 strided", P<1, 4, 0, 0, 1>},
     {"pat seg64 D4 fin2 strided", P<0, 4, 2, 0, 1>}, {"stream T1024 ncu", nullptr},
     {"pat seg64 D4 fin2 mis0", P<0, 4, 2, 0>}, {"pat seg64 D4 fin2 mis4", P<0, 4, 2, 4>},
