@@ -1122,7 +1122,6 @@ __device__ __forceinline__ void crc_packed_small_body(const RowsArgs& a, std::ui
   const std::uint32_t lane = threadIdx.x & 63u;
   const LaneConst kc = lane_const(lane);
   const std::uint32_t K = multmodp(a.head_z, a.init_default, a.tabs->poly) ^ a.out_xor;
-  const bool stores = (lane % G) == G - 1u;
   __syncthreads();
 
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1143,11 +1142,27 @@ __device__ __forceinline__ void crc_packed_small_body(const RowsArgs& a, std::ui
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i);
   };
+  // G >= 2: the kBpr results of a row move into keep lanes ((j % G) * kBpr + block of the row), so
+  // G rows fill all 64 and leave in one coalesced store; a store per row would sit in the same vmcnt
+  // queue as the row loads issued after it. G = 1: each row's 64 results are one store already.
+  std::uint32_t keep = 0;
+  const std::uint32_t keep_src = ((lane % kBpr) * G + (G - 1u)) * 4u;  // byte address for ds_bpermute
   auto finish = [&](std::uint32_t j, std::uint32_t p) {
     std::uint32_t v = p;
-    if constexpr (G > 1) v = group_xor<G>(lane_shift(lds, v, kc));
-    const std::uint64_t blk = static_cast<std::uint64_t>(r0 + j) * kBpr + lane_blk;
-    if (stores && blk < a.nblocks) a.out[blk] = v ^ K;
+    if constexpr (G > 1) {
+      v = group_xor<G>(lane_shift(lds, v, kc)) ^ K;
+      const std::uint32_t pulled = static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(keep_src),
+                                                                                          static_cast<int>(v)));
+      const std::uint32_t slot = j % G;
+      keep = lane / kBpr == slot ? pulled : keep;
+      if (slot == G - 1u || j + 1u == nrows) {
+        const std::uint64_t blk = static_cast<std::uint64_t>(r0 + j - slot) * kBpr + lane;
+        if (lane < (slot + 1u) * kBpr && blk < a.nblocks) a.out[blk] = keep;
+      }
+    } else {
+      const std::uint64_t blk = static_cast<std::uint64_t>(r0 + j) * kBpr + lane_blk;
+      if (blk < a.nblocks) a.out[blk] = v ^ K;
+    }
   };
 
 #pragma unroll

@@ -8,6 +8,7 @@
   sst_stamp    tkv_sst_stamp_blocks over a host SSTable image of ~4 KiB data blocks
   sst_device   tkv_sst_block_crcs_device over the same images resident in HBM (kernel + fix-up)
   crc32c_cfg2  CRC-32C over 1 M x 4 KiB device-resident blocks (cfg2 shape)
+  uniform_512B, uniform_64B  the same 4 GiB as 8 M x 512 B and 64 M x 64 B blocks (crc_packed_small)
 
 Host-memory rows include the PCIe copies (pageable source: host memcpy into pinned staging). Beside
 each row, "cpu_reference" times the reference's own path on one host core over the same bytes: its
@@ -277,6 +278,23 @@ probe = data[:64 * 4096].cpu().numpy()
 ok = all(ora.crc_c(probe[i * 4096:(i + 1) * 4096].tobytes()) == int(outc[i:i + 1].cpu().numpy().view(np.uint32)[0])
          for i in range(0, 64, 7))
 emit("crc32c_cfg2", n * 4096, t, n, {"frac_of_8TB/s": round(n * 4096 / t / 8e12, 4), "bit_exact_sample": ok})
+
+# ---- small uniform blocks (sector-sized checksums, crc_packed_small) --------------------
+for blen in (512, 64):
+    nb = (n * 4096) // blen
+    outs = torch.empty(nb, dtype=torch.int32, device="cuda")
+    for _ in range(20):
+        tk.crc32_batch_uniform(data, blen, nb, out=outs)
+    e0.record(st)
+    for _ in range(50):
+        tk.crc32_batch_uniform(data, blen, nb, out=outs)
+    e1.record(st)
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 50 / 1e3
+    ok = all(ora.crc(probe[i * blen:(i + 1) * blen].tobytes()) == int(outs[i:i + 1].cpu().numpy().view(np.uint32)[0])
+             for i in range(0, 64 * 4096 // blen, 7))
+    emit(f"uniform_{blen}B", nb * blen, t, nb, {"frac_of_8TB/s": round(nb * blen / t / 8e12, 4),
+                                               "bit_exact_sample": ok})
 
 # ---- latency of small calls (the per-record drop-in path and small group commits) ----------------------
 def lat(fn, reps=200):
