@@ -53,6 +53,7 @@ def main():
     data = torch.empty(cap, dtype=torch.uint8, device="cuda")
     D = VP(data.data_ptr())
     dz_o, dz_l = torch.from_numpy(offs).to("cuda"), torch.from_numpy(lens.astype(np.int32)).to("cuda")
+    dz_g = torch.from_numpy((lens - 1).astype(np.int32)).to("cuda")  # 1-byte gaps: the general walk
     d64_o = torch.arange(n64, dtype=torch.int64, device="cuda") * 65536
     d64_l = torch.full((n64,), 65536, dtype=torch.int32, device="cuda")
     outs = [torch.empty(1 << 17, dtype=torch.int32, device="cuda") for _ in libs]
@@ -70,6 +71,9 @@ def main():
          lambda lib, o: lib.tkv_crc32_batch_device(D, VP(d64_o.data_ptr()), VP(d64_l.data_ptr()), None, o, n64, sp)),
         ("cfg4 Zipf 128K", fill_zipf, int(lens.sum()), lens.size,
          lambda lib, o: lib.tkv_crc32_batch_device(D, VP(dz_o.data_ptr()), VP(dz_l.data_ptr()), None, o, lens.size,
+                                                   sp)),
+        ("cfg4 Zipf general (1-byte gaps)", fill_zipf, int(lens.sum()) - lens.size, lens.size,
+         lambda lib, o: lib.tkv_crc32_batch_device(D, VP(dz_o.data_ptr()), VP(dz_g.data_ptr()), None, o, lens.size,
                                                    sp)),
     ]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

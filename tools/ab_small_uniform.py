@@ -30,7 +30,7 @@ buf = torch.empty(total, dtype=torch.uint8, device="cuda")
 st = VP(torch.cuda.current_stream().cuda_stream)
 assert libs[0].tkv_fill_synthetic_uniform(VP(buf.data_ptr()), 4096, 4096, 0, total // 4096, 1, st) == 0
 K = 20
-for L in (64, 128, 512, 1024, 2048):
+for L in [int(x) for x in os.environ.get("AB_LENS", "64,128,512,1024,2048").split(",")]:
     n = total // L
     outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in libs]
     times = [[] for _ in libs]

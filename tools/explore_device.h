@@ -94,6 +94,7 @@ __device__ __forceinline__ void x_rows_body(const XArgs& a, std::uint32_t* lds) 
   WaveState st;
   st.B = 0;
   st.first_piece = true;
+  st.k_val = st.k_idx = st.k_n = 0;
 #pragma unroll
   for (int s = 0; s < 2; ++s) st.s_block[s] = st.s_part[s] = st.s_after[s] = st.s_flags[s] = 0;
 
@@ -172,6 +173,7 @@ __device__ __forceinline__ void x_rows_body(const XArgs& a, std::uint32_t* lds) 
         }
       }
     }
+    if (UNIFORM && lane < st.k_n) a.out[st.k_idx] = st.k_val;  // the last gathered results
   }
 
   if constexpr (!UNIFORM && MODE == 0) {
