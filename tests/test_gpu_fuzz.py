@@ -96,8 +96,8 @@ def test_irregular_random(gpu, oracle, seed):
 def test_uniform_random(gpu, oracle, seed):
     rng = np.random.default_rng(2000 + seed)
     algo = ALGOS[seed % 2]
-    length = int(rng.choice([0, 1, 3, 64, 128, 256, 512, 1000, 1024, 2048, 4096, 4097, 8192, 12288, 65536,
-                             int(rng.integers(0, 70000))]))
+    length = int(rng.choice([0, 1, 3, 16, 48, 64, 128, 256, 512, 1000, 1024, 1040, 2048, 3008, 4080, 4096, 4097,
+                             8192, 12288, 65536, int(rng.integers(0, 70000)), 16 * int(rng.integers(1, 256))]))
     stride = length + int(rng.choice([0, 0, 0, 0, 1, 16, 4096, int(rng.integers(0, 5000))]))
     stride = max(stride, 1)
     n = int(rng.choice([1, 5, 4095, 4096, 5000, 20000]))

@@ -659,13 +659,17 @@ def test_rank_shards_full_size(gpu, oracle, cfg):
         assert aggregates(got) == (sh["xor"], sh["sum32"]), f"{cfg} shard at block {first}"
 
 
-@pytest.mark.parametrize("blen", [64, 128, 256, 512, 1024, 2048])
+@pytest.mark.parametrize("blen", [16, 48, 64, 80, 128, 144, 256, 512, 1024, 1040, 2048, 2064, 3008, 4080])
 def test_packed_small_blocks(gpu, oracle, blen):
-    """Uniform batches of 64*G-byte blocks packed back to back (G-lane groups, 64/G blocks per 4 KiB
-    row): batches ending in a partial row, single blocks, and a batch large enough
-    for every wave, against the oracle; raw registers through update_device."""
+    """Uniform batches of small blocks packed back to back (G-lane groups, each block right-aligned
+    in a 64*G-byte slot, 64/G blocks per wave row): batches ending in a partial row,
+    single blocks, and a batch large enough for every wave, against the oracle; raw registers
+    through update_device."""
     rng = np.random.default_rng(blen)
-    bpr = 4096 // blen
+    g = 1
+    while 64 * g < blen:
+        g *= 2
+    bpr = 64 // g
     for n in (1, 2, bpr - 1, bpr, bpr + 1, 4096 * bpr + 3, 300_000 // max(1, blen // 64)):
         host = rng.integers(0, 256, n * blen + 64, dtype=np.uint8)
         d = torch.from_numpy(host).to(gpu)

@@ -28,7 +28,7 @@ namespace tkv {
 hipError_t launch_rows(const RowsArgs& a, bool aligned, bool uniform, unsigned grid, hipStream_t st);
 hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
 hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st);
-bool packed_small_len(std::uint32_t len);
+std::uint32_t packed_small_group(std::uint32_t len);
 hipError_t launch_packed_small(const RowsArgs& a, unsigned grid, hipStream_t st);
 hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
                           std::uint32_t n, std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* tile_ok,
@@ -448,9 +448,9 @@ int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t s
     TKV_HIP(launch_packed(a, static_cast<unsigned>(c->ncu), st));  // whole blocks per wave, no seams
     return TKV_OK;
   }
-  if (aligned && !d_init && stride == len && packed_small_len(a.len)) {
-    // 4 KiB rows of 64/G whole blocks; as many workgroups as there are rows to give
-    const std::uint64_t bpr = kRow / len;
+  if (aligned && !d_init && stride == len && packed_small_group(a.len)) {
+    // wave rows of 64/G blocks; as many workgroups as there are rows to give
+    const std::uint64_t bpr = 64u / packed_small_group(a.len);
     a.total_rows = static_cast<std::uint32_t>((n + bpr - 1) / bpr);
     const std::uint64_t grid = std::max<std::uint64_t>(
         1, std::min<std::uint64_t>(c->ncu, (a.total_rows + kWavesPerWG - 1) / kWavesPerWG));

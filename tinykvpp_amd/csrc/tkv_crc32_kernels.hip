@@ -123,11 +123,12 @@ __global__ __launch_bounds__(kThreads) void crc_packed(RowsArgs a) {
   dev::crc_packed_body<kPackedDepth, kPackedIlp, R1, R1 ? 0 : kPackedSkew, kPackedPrio>(a, lds);
 }
 
-// Packed small blocks (len = 64*G < 4 KiB, stride == len, 16-byte aligned, default init): DESIGN.md §4.4.
-template <int G>
+// Packed small blocks (len <= 2 KiB a multiple of 16, stride == len, 16-byte aligned, default init):
+// DESIGN.md §4.4. EXACT: len = 64 G.
+template <int G, bool EXACT>
 __global__ __launch_bounds__(kThreads) void crc_packed_small(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_small_body<G, kPackedDepth, kPackedIlp, kPackedPrio>(a, lds);
+  dev::crc_packed_small_body<G, EXACT, kPackedDepth, kPackedIlp, kPackedPrio>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
@@ -528,18 +529,30 @@ hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-bool packed_small_len(std::uint32_t len) {
-  return len == 64u || len == 128u || len == 256u || len == 512u || len == 1024u || len == 2048u;
+// Lanes per block of crc_packed_small: the smallest power of two G with 64 G >= len, for len <= 2 KiB
+// a multiple of 16 (0: not this kernel's batch; between 2 and 4 KiB a slot is a whole 4 KiB row, and
+// the generic kernel measured faster, profiles/r2/packed_small/ab_slots.jsonl).
+std::uint32_t packed_small_group(std::uint32_t len) {
+  if (len == 0 || len > 2048u || len % 16u != 0) return 0;
+  std::uint32_t g = 1;
+  while (64u * g < len) g <<= 1;
+  return g;
+}
+
+template <int G>
+void launch_small_g(const RowsArgs& a, unsigned grid, hipStream_t st) {
+  if (a.len == 64u * G) hipLaunchKernelGGL((crc_packed_small<G, true>), dim3(grid), dim3(kThreads), 0, st, a);
+  else hipLaunchKernelGGL((crc_packed_small<G, false>), dim3(grid), dim3(kThreads), 0, st, a);
 }
 
 hipError_t launch_packed_small(const RowsArgs& a, unsigned grid, hipStream_t st) {
-  switch (a.len) {
-    case 64: hipLaunchKernelGGL(crc_packed_small<1>, dim3(grid), dim3(kThreads), 0, st, a); break;
-    case 128: hipLaunchKernelGGL(crc_packed_small<2>, dim3(grid), dim3(kThreads), 0, st, a); break;
-    case 256: hipLaunchKernelGGL(crc_packed_small<4>, dim3(grid), dim3(kThreads), 0, st, a); break;
-    case 512: hipLaunchKernelGGL(crc_packed_small<8>, dim3(grid), dim3(kThreads), 0, st, a); break;
-    case 1024: hipLaunchKernelGGL(crc_packed_small<16>, dim3(grid), dim3(kThreads), 0, st, a); break;
-    case 2048: hipLaunchKernelGGL(crc_packed_small<32>, dim3(grid), dim3(kThreads), 0, st, a); break;
+  switch (packed_small_group(a.len)) {
+    case 1: launch_small_g<1>(a, grid, st); break;
+    case 2: launch_small_g<2>(a, grid, st); break;
+    case 4: launch_small_g<4>(a, grid, st); break;
+    case 8: launch_small_g<8>(a, grid, st); break;
+    case 16: launch_small_g<16>(a, grid, st); break;
+    case 32: launch_small_g<32>(a, grid, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
