@@ -285,6 +285,44 @@ def test_model_small_block_groups(model, oracle):
         assert v ^ 0xFFFFFFFF == oracle.update(init, data.tobytes()) ^ 0xFFFFFFFF
 
 
+def packed_small_group(n):
+    """crc_packed_small's G: the smallest power of two with 64 G >= n (n <= 2048, a multiple of 16)."""
+    g = 1
+    while 64 * g < n:
+        g *= 2
+    return g
+
+
+@pytest.mark.parametrize("n", [16, 48, 64, 80, 96, 128, 144, 256, 512, 1024, 1040, 2048])
+def test_model_packed_small_slots(model, oracle, n):
+    """crc_packed_small's arithmetic on a wave row of 64/G uniform blocks of n bytes packed back to
+    back (DESIGN.md §4.4): lane l of block l // G reads the 64 bytes at n - 64 G + 64 (l % G) of its
+    block (pieces in front of the block read zeros), folds them, and moves the partial with the
+    lane-shift column the workgroup copies into column l (device column 64 - G + l % G); the group's
+    XOR plus Shift_n(init) is the raw register."""
+    G = packed_small_group(n)
+    bpr = 64 // G
+    rng = np.random.default_rng(n)
+    blocks = rng.integers(0, 256, (bpr, n), dtype=np.uint8)
+    row = np.zeros(ROW, np.uint8)
+    for lane in range(64):
+        b, g = lane // G, lane % G
+        off = n - 64 * G + 64 * g
+        for i in range(4):  # the kernel's four 16-byte pieces: in front of the block -> zeros
+            if off + 16 * i >= 0:
+                row[64 * lane + 16 * i:64 * lane + 16 * i + 16] = blocks[b][off + 16 * i:off + 16 * i + 16]
+    p = model.slice_lanes(row)
+    col = np.array([64 - G + (lane % G) for lane in range(64)])  # fill_lds_group's column remap
+    v = np.zeros(64, np.uint32)
+    for j in range(8):
+        v ^= model.lane[j][(p >> (4 * j)) & 15, col]
+    init = 0xFFFFFFFF
+    K = bits_dot(init, model.head[n])  # Shift_n(init): head_shift[n][i] = Shift_n(1 << i)
+    for b in range(bpr):
+        raw = int(np.bitwise_xor.reduce(v[b * G:(b + 1) * G])) ^ K
+        assert raw ^ 0xFFFFFFFF == oracle.crc(blocks[b].tobytes()), (n, b)
+
+
 def test_combine_matches_concatenation(lib, oracle):
     """tkv_crc32_combine / tkv_crc32c_combine (host arithmetic on 4-byte values, no device): the CRC
     of A || B from CRC(A), CRC(B), |B|, against zlib.crc32 and the oracle's CRC-32C of the
