@@ -15,6 +15,11 @@ import tinykvpp_amd as tk
 
 pytestmark = pytest.mark.gpu
 
+# TKV_FUZZ_OFFSET shifts every case's seed, so the same sweep can explore other cases (the default,
+# 0, is the committed set).
+import os  # noqa: E402
+OFFSET = int(os.environ.get("TKV_FUZZ_OFFSET", "0"))
+
 ALGOS = ("crc32", "crc32c")
 
 
@@ -61,7 +66,7 @@ def irregular_mode():
 
 @pytest.mark.parametrize("seed", range(96))
 def test_irregular_random(gpu, oracle, seed):
-    rng = np.random.default_rng(1000 + seed)
+    rng = np.random.default_rng(1000 + seed + OFFSET)
     algo = ALGOS[seed % 2]
     n = int(rng.choice([1, 2, 3, 17, 300, 2000, 9000]))
     lens = draw_lengths(rng, n)
@@ -94,7 +99,7 @@ def test_irregular_random(gpu, oracle, seed):
 
 @pytest.mark.parametrize("seed", range(64))
 def test_uniform_random(gpu, oracle, seed):
-    rng = np.random.default_rng(2000 + seed)
+    rng = np.random.default_rng(2000 + seed + OFFSET)
     algo = ALGOS[seed % 2]
     length = int(rng.choice([0, 1, 3, 16, 48, 64, 128, 256, 512, 1000, 1024, 1040, 2048, 3008, 4080, 4096, 4097,
                              8192, 12288, 65536, int(rng.integers(0, 70000)), 16 * int(rng.integers(1, 256))]))
@@ -120,7 +125,7 @@ def test_uniform_random(gpu, oracle, seed):
 @pytest.mark.parametrize("seed", range(16))
 def test_update_chain_random(gpu, oracle, seed):
     """crc32::update chained over random pieces (host spans and device tensors) equals one pass."""
-    rng = np.random.default_rng(3000 + seed)
+    rng = np.random.default_rng(3000 + seed + OFFSET)
     algo = ALGOS[seed % 2]
     pieces = [rng.integers(0, 256, int(rng.choice([0, 1, 5, 36, 700, 4096, 20000, 300000])), dtype=np.uint8)
               for _ in range(int(rng.integers(1, 12)))]
@@ -140,7 +145,7 @@ def test_wal_verify_random(gpu, oracle, seed):
     one random corruption: a payload bit, the stored CRC, a lying record_len, a key/value length that
     overruns the record under a valid CRC (caught after the CRC, wal.cpp:118-121), or any byte."""
     from test_gpu_wal_device import both, make_wal, sequential_decode
-    rng = np.random.default_rng(4000 + seed)
+    rng = np.random.default_rng(4000 + seed + OFFSET)
     n_rec = int(rng.choice([1, 2, 7, 300, 5000, 20000, 120000]))
     vmax = int(rng.choice([64, 600, 5000, 16000])) if n_rec < 100000 else 600
     img, offs, size = make_wal(rng, n_rec, vmax=vmax, fake_headers=float(rng.choice([0.0, 0.0, 0.3])))
@@ -181,7 +186,7 @@ def test_host_batch_random(gpu, oracle, seed):
     """tkv_crc32[c]_batch_host[_multi] over pageable host memory (the staged pipeline: dense runs,
     gathers, blocks cut across devices) and pinned host memory (read in place) at any alignment,
     random layouts and initial registers, against the oracle."""
-    rng = np.random.default_rng(5000 + seed)
+    rng = np.random.default_rng(5000 + seed + OFFSET)
     algo = ALGOS[seed % 2]
     n = int(rng.choice([1, 3, 40, 256, 257, 3000]))
     lens = draw_lengths(rng, n)
@@ -219,7 +224,7 @@ def test_sst_random(gpu, oracle, seed):
     device stamp (block_crcs_device, store) against the host stamp, verify of a random corruption."""
     from test_gpu_formats import make_file
     from tinykvpp_amd import sst
-    rng = np.random.default_rng(6000 + seed)
+    rng = np.random.default_rng(6000 + seed + OFFSET)
     f, offs, sizes = make_file(rng, int(rng.choice([1, 2, 30, 400])))
     shift = int(rng.integers(0, 16))
     buf = np.zeros(f.size + shift, np.uint8)
@@ -250,7 +255,7 @@ def test_wal_stamp_random(gpu, oracle, seed):
     CRC over [8, 8 + record_len) of each, stored at offset 4, against the oracle; the stamped batch
     verifies clean."""
     from tinykvpp_amd import wal
-    rng = np.random.default_rng(7000 + seed)
+    rng = np.random.default_rng(7000 + seed + OFFSET)
     n = int(rng.choice([1, 2, 16, 255, 256, 257, 5000]))
     recs = [wal.encode_unstamped(int(rng.integers(0, 2)), int(rng.integers(0, 2**63)),
                                  rng.bytes(int(rng.integers(0, 64))),
@@ -280,7 +285,7 @@ def test_stream_many_blocks_random(gpu, oracle, seed):
     """Stream mode over 50 K-200 K back-to-back blocks (several block ends per row and lane segment
     boundary, every wave holding ends), any base alignment and stream start, per-block initial
     registers, both polynomials."""
-    rng = np.random.default_rng(8000 + seed)
+    rng = np.random.default_rng(8000 + seed + OFFSET)
     algo = ALGOS[seed % 2]
     n = int(rng.integers(50_000, 200_000))
     lens = rng.integers(64, int(rng.choice([65, 128, 600, 3000])), n).astype(np.int64)
