@@ -707,7 +707,7 @@ __device__ __forceinline__ std::uint32_t stream_first_wave(const std::uint32_t* 
 // lane values gives Y = Shift_4096(B) ^ (lanes before l, moved to the row end). Then
 // crc_0(wave bytes up to E) = Shift_(rowend - E)^-1 (Y) ^ Q, which stream_finish turns into each
 // block's CRC. Each wave stores (Y, Q) per block end it meets and its own B at the end of its range.
-template <int PRIO>
+template <int PRIO, bool MANY = false>
 __device__ __forceinline__ void crc_stream_body(const RowsArgs& a, std::uint32_t* lds) {
   constexpr int DEPTH = 4, ILP = 2;
   fill_lds(a.tabs, lds);
@@ -764,12 +764,66 @@ __device__ __forceinline__ void crc_stream_body(const RowsArgs& a, std::uint32_t
 
   // Block ends in the row [rs, rs + 4096): the lane whose segment holds one learns (r, block), and
   // keep lane b - kb learns which lane that is (src; rmask: keep lanes fed by this row).
+  // MANY (probe): a row with many ends takes them all at once (lane-parallel capture).
   auto take_ends = [&](std::uint64_t rs, std::uint32_t& my_r, std::uint32_t& my_b, std::uint32_t& src,
                        std::uint64_t& rmask) -> bool {
-    bool any = false;
     my_r = 0xFFu;  // no end in this lane's segment
     rmask = 0;
-    while (e_next <= rs + kRow) {
+    const std::uint64_t lim = rs + kRow;
+    if (e_next > lim) return false;
+    // more than kManyEnds ends in the row (E[b + kManyEnds] inside it): take them all at once
+    constexpr std::uint32_t kManyEnds = 8;
+    const std::uint32_t probe = ci + kManyEnds;
+    if (MANY && b + kManyEnds < n &&
+        (probe < 64u ? readlane64(win, probe) : readlane64(win2, probe - 64u)) <= lim) {
+      const bool in1 = lane >= ci && win <= lim;
+      const std::uint32_t c1 = static_cast<std::uint32_t>(__popcll(__ballot(in1)));
+      bool in2 = false;
+      std::uint32_t cnt = c1;
+      if (c1 == 64u - ci) {
+        in2 = win2 <= lim;
+        cnt += static_cast<std::uint32_t>(__popcll(__ballot(in2)));
+      }
+      {
+        const std::uint32_t rel1 = static_cast<std::uint32_t>(win - rs), rel2 = static_cast<std::uint32_t>(win2 - rs);
+        const std::uint32_t l1 = (rel1 + 63u) / 64u - 1u, r1 = rel1 - 64u * l1;
+        const std::uint32_t l2 = (rel2 + 63u) / 64u - 1u, r2 = rel2 - 64u * l2;
+        const std::uint64_t bit = (in1 ? 1ull << (l1 & 63u) : 0ull) | (in2 ? 1ull << (l2 & 63u) : 0ull);
+        std::uint64_t S = bit;
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) S |= __shfl_xor(S, m, 64);
+        const std::uint32_t kr = static_cast<std::uint32_t>(__popcll(S & ((1ull << lane) - 1ull)));
+        const std::uint32_t pos = ci + kr;
+        const int pfrom = static_cast<int>((pos & 63u) << 2);
+        const std::uint32_t pr1 = static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(pfrom, static_cast<int>(r1)));
+        const std::uint32_t pr2 = static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(pfrom, static_cast<int>(r2)));
+        if ((S >> lane) & 1u) {
+          my_r = pos < 64u ? pr1 : pr2;
+          my_b = b + kr;
+        }
+        const std::uint32_t kp = kb + lane - bw;
+        const int kfrom = static_cast<int>((kp & 63u) << 2);
+        const std::uint32_t pl1 = static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(kfrom, static_cast<int>(l1)));
+        const std::uint32_t pl2 = static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(kfrom, static_cast<int>(l2)));
+        const std::uint32_t k0 = b - kb;
+        if (lane >= k0 && lane < k0 + cnt) src = kp < 64u ? pl1 : pl2;
+        if (k0 < 64u) {
+          const std::uint32_t k1 = k0 + cnt < 64u ? k0 + cnt : 64u;
+          rmask = (k1 == 64u ? ~0ull : (1ull << k1) - 1ull) & ~((1ull << k0) - 1ull);
+        }
+        b += cnt;
+        ci += cnt;
+        if (ci >= 64u) {
+          bw += 64u;
+          win = win2;
+          win2 = load_win(bw + 64u);
+          ci -= 64u;
+        }
+        e_next = b < n ? readlane64(win, ci) : ~0ull;
+        return true;
+      }
+    }
+    while (e_next <= lim) {
       const std::uint32_t rel = static_cast<std::uint32_t>(e_next - rs);  // 1..4096
       const std::uint32_t l = (rel + 63u) / 64u - 1u;
       my_r = lane == l ? rel - 64u * l : my_r;
@@ -779,7 +833,6 @@ __device__ __forceinline__ void crc_stream_body(const RowsArgs& a, std::uint32_t
         src = lane == k ? l : src;
         rmask |= 1ull << k;
       }
-      any = true;
       ++b;
       if (++ci == 64u) {
         bw += 64u;
@@ -789,7 +842,7 @@ __device__ __forceinline__ void crc_stream_body(const RowsArgs& a, std::uint32_t
       }
       e_next = b < n ? readlane64(win, ci) : ~0ull;
     }
-    return any;
+    return true;
   };
 
   uint4 buf[DEPTH][4];

@@ -103,7 +103,22 @@ constexpr int kStreamSkew = 154;
 __global__ __launch_bounds__(kStreamThreads) void crc_stream(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   if (dev::sload32(a.counts, 3) != kModeStream) return;
-  dev::crc_stream_body<3>(a, lds);  // issue priority from the rows left: +0.8 % on cfg4 (in-process A/B)
+  // issue priority from the rows left: +0.8 % on cfg4 (in-process A/B). A wave whose rows hold more
+  // than 8 block ends per row on average (blocks under ~500 bytes) takes them a row at a time
+  // (MANY); the others keep the per-end loop, whose code the MANY path slows by up to 10 % when it
+  // shares the loop (4 KiB blocks, profiles/r2/stream_many/). Both paths end in the one barrier of
+  // crc_stream_body's table fill, so a workgroup may mix them.
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t g0 = dev::sload32(a.s_row0, wave), g1 = dev::sload32(a.s_row0, wave + 1);
+  const std::uint32_t e0 = dev::sload32(a.wave_start, wave);
+  const std::uint32_t e1 = wave + 1 < a.nwaves ? dev::sload32(a.wave_start, wave + 1) : a.nblocks;
+#ifdef TKV_PROBE_STREAM_SCALAR
+  const bool many = false;
+#else
+  const bool many = g1 > g0 && e1 > e0 && e1 - e0 > 8u * (g1 - g0);
+#endif
+  if (many) dev::crc_stream_body<3, true>(a, lds);
+  else dev::crc_stream_body<3, false>(a, lds);
 }
 
 // Packed uniform batches (len % 4 KiB == 0, stride == len, 16-byte aligned): DESIGN.md §4.
