@@ -51,6 +51,10 @@ int tkv_set_device(int device);
 /* Human-readable text of the last error on this thread ("" if none). */
 const char *tkv_last_error(void);
 
+/* Build identity: 16 hex digits of sha256 over the library's sources and Makefile, baked in at build
+ * time (tinykvpp_amd/build_id.py); tests and bench.py check it against the tree they run in. */
+const char *tkv_build_id(void);
+
 /* ---- crc32::update replacement ---------------------------------------------------------------- */
 
 /* Continue raw register `raw_state` over `len` bytes of HOST memory; writes the new raw register.

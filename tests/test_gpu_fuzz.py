@@ -72,7 +72,7 @@ def test_irregular_random(gpu, oracle, seed):
     lens = draw_lengths(rng, n)
     layout = ("back_to_back", "back_to_back_min64", "gapped", "overlapping")[seed // 2 % 4]
     if layout == "back_to_back_min64":
-        lens = np.maximum(lens, 64)
+        lens = np.maximum(lens, 65)
     start = int(rng.integers(0, 4106))
     if layout.startswith("back_to_back"):
         offs = start + np.concatenate([[0], np.cumsum(lens)[:-1]])
@@ -94,7 +94,7 @@ def test_irregular_random(gpu, oracle, seed):
     assert bad.size == 0, (f"{layout} n={n} start={start} shift={shift} algo={algo} mode={irregular_mode()}: "
                            f"{bad.size} blocks differ, first {bad[:5]} (lens {lens[bad[:5]]})")
     if layout == "back_to_back_min64" and n > 1:
-        assert irregular_mode() == 1, "a back-to-back batch of blocks >= 64 B takes stream mode"
+        assert irregular_mode() == 1, "a back-to-back batch of blocks > 64 B (kLaneMax) takes stream mode"
 
 
 @pytest.mark.parametrize("seed", range(64))
@@ -288,7 +288,7 @@ def test_stream_many_blocks_random(gpu, oracle, seed):
     rng = np.random.default_rng(8000 + seed + OFFSET)
     algo = ALGOS[seed % 2]
     n = int(rng.integers(50_000, 200_000))
-    lens = rng.integers(64, int(rng.choice([65, 128, 600, 3000])), n).astype(np.int64)
+    lens = rng.integers(65, int(rng.choice([66, 128, 600, 3000])), n).astype(np.int64)
     start = int(rng.integers(0, 64))
     offs = start + np.concatenate([[0], np.cumsum(lens)[:-1]])
     host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)

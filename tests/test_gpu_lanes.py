@@ -1,0 +1,182 @@
+"""GPU parity of the lane-block kernels: blocks of at most kLaneMax = 64 bytes, each
+folded whole by one lane from its own initial register.
+
+Uniform batches take crc_lanes (any stride, alignment and per-block init); irregular batches fold
+their lane blocks in crc_stream's launch (general path) while the prepass lists only the rest. The
+shapes are the reference's WAL records: 26 + |k| + |v| bytes (/root/reference/src/engine/wal.cpp:25,
+kMetadataSize in wal.hpp:21-27), stamped one per put (wal.cpp:54-57), whose payloads lie 8 header
+bytes apart in an image. Everything is compared block by block with the oracle.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import tinykvpp_amd as tk
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+WAL_SIZES = (26, 28, 33, 36, 59)
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def mode():
+    """Path the last irregular batch on the current stream took: 0 general, 1 stream mode."""
+    return tk.load_library().tkv_debug_irregular_mode(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+
+def i32(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.uint32).view(np.int32))
+
+
+def oracle_c(oracle, host, offs, lens, init=None):
+    """CRC-32C finalize() values of the blocks (the oracle's restatement, one call per block)."""
+    out = np.zeros(len(offs), np.uint32)
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        raw = 0xFFFFFFFF if init is None else int(init[i])
+        out[i] = oracle.update_c(raw, host[int(o):int(o) + int(n)].tobytes()) ^ 0xFFFFFFFF
+    return out
+
+
+@pytest.fixture(scope="module")
+def buf(gpu):
+    rng = np.random.default_rng(64)
+    host = rng.integers(0, 256, (64 << 20) + 4096, dtype=np.uint8)
+    return host, torch.from_numpy(host).to(gpu)
+
+
+@pytest.mark.parametrize("blen", list(range(0, 65)))
+def test_uniform_every_length(gpu, oracle, buf, blen):
+    """Every length 0..64 with strides equal to, past (a WAL header's 8 bytes) and below the length
+    (overlapping blocks), base pointers at every alignment class, batches ending inside a 64-block
+    step, and per-block initial registers."""
+    host, d = buf
+    rng = np.random.default_rng(1000 + blen)
+    cases = [(blen, 0, 1), (blen, 0, 64), (blen + 8, 5, 65), (max(blen, 1) + 3, 13, 1000),
+             (blen + 8, 4, 4097), (max(blen - 7, 0), 1, 300), (59, 7, 2000), (blen, 8, 70_001)]
+    for stride, offset, n in cases:
+        offs = offset + np.arange(n, dtype=np.int64) * stride
+        lens = np.full(n, blen, np.int32)
+        want = oracle.batch(host, offs, lens)
+        got = u32(tk.crc32_batch_uniform(d, blen, n, stride=stride, offset=offset))
+        bad = np.flatnonzero(got != want)
+        assert bad.size == 0, (stride, offset, n, bad[:5])
+        init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        got = u32(tk.crc32_batch_uniform(d, blen, n, stride=stride, offset=offset, init_raw=i32(init).to(gpu)))
+        assert np.array_equal(got, oracle.batch(host, offs, lens, init)), (stride, offset, n)
+
+
+@pytest.mark.parametrize("blen", WAL_SIZES + (64,))
+def test_uniform_full_waves(gpu, oracle, buf, blen):
+    """1 M WAL-record-sized blocks back to back (every wave of every workgroup busy), aligned and at
+    an odd base."""
+    host, d = buf
+    n = 1 << 20
+    for offset in (0, 3):
+        offs = offset + np.arange(n, dtype=np.int64) * blen
+        want = oracle.batch(host, offs, np.full(n, blen, np.int32))
+        got = u32(tk.crc32_batch_uniform(d, blen, n, offset=offset))
+        assert np.array_equal(got, want), offset
+
+
+def test_uniform_crc32c(gpu, oracle, buf):
+    host, d = buf
+    for blen, stride, offset, n in ((36, 44, 0, 3000), (59, 59, 5, 1999), (0, 4, 0, 10), (64, 64, 16, 700)):
+        offs = offset + np.arange(n, dtype=np.int64) * stride
+        got = u32(tk.crc32_batch_uniform(d, blen, n, stride=stride, offset=offset, algo="crc32c"))
+        assert np.array_equal(got, oracle_c(oracle, host, offs, np.full(n, blen))), (blen, stride)
+        init = np.random.default_rng(n).integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        got = u32(tk.crc32_batch_uniform(d, blen, n, stride=stride, offset=offset, init_raw=i32(init).to(gpu),
+                                         algo="crc32c"))
+        assert np.array_equal(got, oracle_c(oracle, host, offs, np.full(n, blen), init)), (blen, stride)
+
+
+def wal_payloads(rng, n, sizes, base):
+    """Payload offsets/lengths of a WAL image: each record is an 8-byte header (length, CRC) followed
+    by its payload, so consecutive payloads lie 8 bytes apart."""
+    lens = rng.choice(np.asarray(sizes), n).astype(np.int64)
+    starts = base + 8 + np.concatenate([[0], np.cumsum(lens[:-1] + 8)])
+    return starts.astype(np.int64), lens.astype(np.int32)
+
+
+@pytest.mark.parametrize("sizes", [(36,), WAL_SIZES, tuple(range(0, 65))])
+@pytest.mark.parametrize("base", [0, 1, 6, 11])
+def test_irregular_wal_payloads(gpu, oracle, buf, sizes, base):
+    """A device batch of WAL payloads: lane blocks only, gapped, at every base alignment; the prepass
+    takes the general path and crc_stream's launch folds every block."""
+    host, d = buf
+    rng = np.random.default_rng(len(sizes) * 16 + base)
+    offs, lens = wal_payloads(rng, 120_000, sizes, base)
+    o, ln = torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu)
+    got = u32(tk.crc32_batch(d, o, ln))
+    assert mode() == 0
+    assert np.array_equal(got, oracle.batch(host, offs, lens))
+    init = rng.integers(0, 2**32, offs.size, dtype=np.uint64).astype(np.uint32)
+    got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))
+    assert np.array_equal(got, oracle.batch(host, offs, lens, init))
+
+
+@pytest.mark.parametrize("mix", ["lane_small_large", "lane_then_large", "random_offsets", "lane_at_buffer_end"])
+def test_irregular_mixed_classes(gpu, oracle, mix):
+    """Lane blocks (<= 64 B), small blocks (<= 1 KiB) and large ones in one batch: each class goes to
+    its own phase and every result lands at its batch index; CRC-32C on the same batch."""
+    rng = np.random.default_rng(len(mix))
+    n = 30_000
+    if mix == "lane_small_large":
+        lens = rng.choice(np.array([rng.integers(0, 65), 200, 1024, 1025, 5000, 64, 65, 0]), n)
+        lens = np.where(rng.random(n) < 0.5, rng.integers(0, 65, n), lens)
+    elif mix == "lane_then_large":
+        lens = np.concatenate([rng.integers(0, 65, n // 2), rng.integers(65, 20000, n - n // 2)])
+    elif mix == "random_offsets":
+        lens = rng.integers(0, 3000, n)
+    else:
+        lens = rng.integers(0, 65, n)
+    if mix == "random_offsets":
+        offs = rng.integers(0, int(lens.sum()), n)
+    else:
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])]) + rng.integers(0, 9, n).cumsum()
+    size = int((offs + lens).max()) + (0 if mix == "lane_at_buffer_end" else 24)
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    d = torch.from_numpy(host).to(gpu)
+    o = torch.from_numpy(offs.astype(np.int64)).to(gpu)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    want = oracle.batch(host, offs, lens.astype(np.int32))
+    assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), want)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))
+    assert np.array_equal(got, oracle.batch(host, offs, lens.astype(np.int32), init))
+    m = 3000
+    got = u32(tk.crc32_batch(d, o[:m].contiguous(), ln[:m].contiguous(), algo="crc32c"))
+    assert np.array_equal(got, oracle_c(oracle, host, offs[:m], lens[:m]))
+
+
+def test_stream_mode_needs_blocks_longer_than_lanes(gpu, oracle, buf):
+    """Back-to-back 64-byte blocks are lane blocks (general path); 65-byte blocks still take stream
+    mode; both bit-exact."""
+    host, d = buf
+    for blen, want_mode in ((64, 0), (65, 1), (40, 0)):
+        n = 50_000
+        offs = 7 + np.arange(n, dtype=np.int64) * blen
+        lens = np.full(n, blen, np.int32)
+        got = u32(tk.crc32_batch(d, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu)))
+        assert mode() == want_mode, blen
+        assert np.array_equal(got, oracle.batch(host, offs, lens)), blen
+
+
+def test_lane_blocks_then_stream_batch_same_scratch(gpu, oracle, buf):
+    """A lane-only batch, a stream-mode batch and a mixed general batch one after the other on one
+    stream: the lane count of one batch never leaks into the next."""
+    host, d = buf
+    rng = np.random.default_rng(77)
+    batches = [wal_payloads(rng, 5000, WAL_SIZES, 0),
+               (np.arange(3000, dtype=np.int64) * 1000, np.full(3000, 1000, np.int32)),
+               (np.arange(4000, dtype=np.int64) * 300, rng.integers(0, 300, 4000).astype(np.int32)),
+               wal_payloads(rng, 3, (36,), 5)]
+    for offs, lens in batches * 2:
+        got = u32(tk.crc32_batch(d, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu)))
+        assert np.array_equal(got, oracle.batch(host, offs, lens))

@@ -1,4 +1,4 @@
-"""Irregular batches whose blocks lie back to back (each at least 64 bytes) take the byte-stream row
+"""Irregular batches whose blocks lie back to back (each longer than kLaneMax = 64 bytes) take the byte-stream row
 walk: the prepass chooses it on the device, the row kernel walks full 4 KiB rows of
 the stream and records a (Y, Q) pair at every block end and a register per wave, and the general row
 kernel's launch (which has no rows to walk then) turns those into block CRCs. Every case is compared block by block with the oracle (crc32.cpp:9-16 restated),
@@ -51,7 +51,7 @@ def run(gpu, oracle, lens, start=0, init=False, algo="crc32", seed=0):
 @pytest.mark.parametrize("start", [0, 1, 7, 15, 16, 4095, 4096 + 9])
 def test_stream_alignments(gpu, oracle, start):
     rng = np.random.default_rng(start)
-    lens = rng.integers(64, 20000, 3000)
+    lens = rng.integers(65, 20000, 3000)
     assert run(gpu, oracle, lens, start=start, seed=start) == 1
 
 
@@ -59,29 +59,29 @@ def test_stream_alignments(gpu, oracle, start):
                                   "many_small", "span_waves"])
 def test_stream_shapes(gpu, oracle, case):
     rng = np.random.default_rng(hash(case) & 0xFFFF)
-    if case == "exact64":  # a block end in every lane segment
-        lens = np.full(20000, 64)
+    if case == "exact64":  # a block end in 64 of every 65 lane segments (64-byte blocks are lane blocks)
+        lens = np.full(20000, 65)
     elif case == "seg_ends":  # ends on 64-byte segment boundaries, some at r = 64, some mid-dword
-        lens = rng.choice([64, 128, 192, 65, 67, 127], 20000)
+        lens = rng.choice([129, 128, 192, 65, 67, 127], 20000)
     elif case == "row_ends":  # ends on 4 KiB row boundaries
-        lens = np.tile([4096, 8192, 4032, 64, 4096 * 3], 500)
+        lens = np.tile([4096, 8192, 4031, 65, 4096 * 3], 500)
     elif case == "one_block":
         lens = np.array([(5 << 20) + 3])
     elif case == "two_blocks":
-        lens = np.array([64, 100])
+        lens = np.array([65, 100])
     elif case == "mixed_huge":  # Zipf-like: 256 B to 1 MiB (cfg4's classes)
         lens = np.maximum(256, (256 * 2 ** rng.integers(0, 13, 4000)) - rng.integers(0, 128, 4000))
     elif case == "span_waves":  # blocks that span many waves' row ranges, between small ones
-        lens = np.concatenate([rng.integers(64, 5000, 3000), [(40 << 20) + 17], rng.integers(64, 300, 500),
-                               [(24 << 20) + 4096], rng.integers(64, 5000, 3000)])
+        lens = np.concatenate([rng.integers(65, 5000, 3000), [(40 << 20) + 17], rng.integers(65, 300, 500),
+                               [(24 << 20) + 4096], rng.integers(65, 5000, 3000)])
     else:  # many small blocks: several ends per row in consecutive lanes
-        lens = rng.integers(64, 200, 200000)
+        lens = rng.integers(65, 200, 200000)
     assert run(gpu, oracle, lens, start=5, seed=1) == 1
 
 
 def test_stream_init_and_crc32c(gpu, oracle):
     rng = np.random.default_rng(11)
-    lens = rng.integers(64, 9000, 5000)
+    lens = rng.integers(65, 9000, 5000)
     assert run(gpu, oracle, lens, start=3, init=True, seed=2) == 1
     assert run(gpu, oracle, lens, start=3, algo="crc32c", seed=3) == 1
     assert run(gpu, oracle, lens, start=3, init=True, algo="crc32c", seed=4) == 1
@@ -90,10 +90,10 @@ def test_stream_init_and_crc32c(gpu, oracle):
 def test_general_path_when_not_back_to_back(gpu, oracle):
     """A short block, or a gap between blocks, keeps the general row walk (and stays exact)."""
     rng = np.random.default_rng(12)
-    lens = rng.integers(64, 9000, 3000)
+    lens = rng.integers(65, 9000, 3000)
     lens[1234] = 63
     assert run(gpu, oracle, lens, seed=5) == 0
-    lens = rng.integers(64, 9000, 3000)
+    lens = rng.integers(65, 9000, 3000)
     offs = (np.concatenate([[0], np.cumsum(lens[:-1])])).astype(np.int64)
     offs[2000:] += 1  # one byte gap
     host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
@@ -107,7 +107,7 @@ def test_stream_then_general_on_same_scratch(gpu, oracle):
     """The stream and general paths share the stream's prepass scratch: alternate them."""
     rng = np.random.default_rng(13)
     for k in range(3):
-        lens = rng.integers(64, 30000, 2000)
+        lens = rng.integers(65, 30000, 2000)
         assert run(gpu, oracle, lens, start=k, seed=20 + k) == 1
         lens[7] = 10
         assert run(gpu, oracle, lens, start=k, seed=30 + k) == 0
@@ -120,7 +120,7 @@ def test_stream_row0_before_a_misaligned_base(gpu, oracle, nblocks):
     base wraps as a u64; the row count must still come out right (it read 0 rows, and every CRC was
     wrong, for base shifts 1-7 with the stream at offset 8, before the fix)."""
     rng = np.random.default_rng(nblocks)
-    lens = rng.integers(64, 9000, nblocks)
+    lens = rng.integers(65, 9000, nblocks)
     for shift in range(16):
         for first in (0, 3, 8, 15):
             offs = (first + np.concatenate([[0], np.cumsum(lens[:-1])])).astype(np.int64)

@@ -36,6 +36,7 @@ SIGNATURES = {
     "tkv_device_count": (_int, []),
     "tkv_set_device": (_int, [_int]),
     "tkv_last_error": (ctypes.c_char_p, []),
+    "tkv_build_id": (ctypes.c_char_p, []),
     "tkv_crc32_update": (_int, [_u32, _vp, _sz, ctypes.POINTER(_u32)]),
     "tkv_crc32_update_host": (_int, [_u32, _vp, _sz, ctypes.POINTER(_u32)]),
     "tkv_crc32c_update_host": (_int, [_u32, _vp, _sz, ctypes.POINTER(_u32)]),
@@ -74,6 +75,9 @@ SIGNATURES = {
     "tkv_debug_multi_combine": (_int, [_u32, _int, _vp, _vp, _vp, _u64, _vp, _vp]),
 }
 
+# symbols an older build may lack (tools/ab_lib.py loads earlier builds for A/B runs)
+OPTIONAL = {"tkv_build_id"}
+
 _lib = None
 
 
@@ -87,6 +91,8 @@ def load_library(path=LIB_PATH):
                           "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if name in OPTIONAL and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

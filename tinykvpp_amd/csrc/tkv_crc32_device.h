@@ -357,7 +357,7 @@ __device__ __forceinline__ void small_phase(const RowsArgs& a, std::uint32_t* ld
 // stores the 32 copies as eight 16-byte LDS writes, rotated by u so that a wave's writes spread over
 // the banks; the lane-shift tables move as 16-byte pieces. Against one dword load and store per LDS
 // word: +1.0 % on 1 M x 4 KiB, +0.2 to +0.4 % on 64 KiB blocks (profiles/r1/explore_wide_fill.txt).
-__device__ __forceinline__ void fill_lds(const DeviceTables* tabs, std::uint32_t* lds) {
+__device__ __forceinline__ void fill_lds_slicing(const DeviceTables* tabs, std::uint32_t* lds) {
   for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
     const std::uint32_t pair = u >> 9, e = (u >> 1) & 255u, t = u & 1u;
     const std::uint32_t v = tabs->slice[2 * pair + t][e];
@@ -365,6 +365,10 @@ __device__ __forceinline__ void fill_lds(const DeviceTables* tabs, std::uint32_t
 #pragma unroll
     for (std::uint32_t k = 0; k < 8u; ++k) dst[(k + u) & 7u] = make_uint4(v, v, v, v);
   }
+}
+
+__device__ __forceinline__ void fill_lds(const DeviceTables* tabs, std::uint32_t* lds) {
+  fill_lds_slicing(tabs, lds);
   const uint4* ls = reinterpret_cast<const uint4*>(&tabs->lane_shift[0][0][0]);
   uint4* lds_ls = reinterpret_cast<uint4*>(lds + kLdsSliceWords);
   for (std::uint32_t i = threadIdx.x; i < kLdsLaneWords / 4u; i += blockDim.x) lds_ls[i] = ls[i];
@@ -707,15 +711,15 @@ __device__ __forceinline__ std::uint32_t stream_first_wave(const std::uint32_t* 
 // lane values gives Y = Shift_4096(B) ^ (lanes before l, moved to the row end). Then
 // crc_0(wave bytes up to E) = Shift_(rowend - E)^-1 (Y) ^ Q, which stream_finish turns into each
 // block's CRC. Each wave stores (Y, Q) per block end it meets and its own B at the end of its range.
+// The caller has filled the LDS tables (fill_lds + barrier): the body holds no barrier, so the waves
+// of one workgroup may run different instantiations of it.
 template <int PRIO, bool MANY = false>
 __device__ __forceinline__ void crc_stream_body(const RowsArgs& a, std::uint32_t* lds) {
   constexpr int DEPTH = 4, ILP = 2;
-  fill_lds(a.tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
   const LaneConst kc = lane_const(lane);
   const std::uint32_t hcon = a.tabs->horner[lane];  // Shift_4096(1 << l) for l < 32, else 0
   const bool lo_half = lane < 32u;
-  __syncthreads();
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint64_t TR = sload32(a.counts, 2);
   const std::uint32_t g0 = sload32(a.s_row0, wave);
@@ -1147,13 +1151,7 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
 // lookups stay free of bank conflicts. G = 1 needs no lane shift.
 template <int G>
 __device__ __forceinline__ void fill_lds_group(const DeviceTables* tabs, std::uint32_t* lds) {
-  for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
-    const std::uint32_t pair = u >> 9, e = (u >> 1) & 255u, t = u & 1u;
-    const std::uint32_t v = tabs->slice[2 * pair + t][e];
-    uint4* dst = reinterpret_cast<uint4*>(lds + pair * 16384u + e * 64u + t * 32u);
-#pragma unroll
-    for (std::uint32_t k = 0; k < 8u; ++k) dst[(k + u) & 7u] = make_uint4(v, v, v, v);
-  }
+  fill_lds_slicing(tabs, lds);
   if constexpr (G >= 4) {
     const uint4* ls = reinterpret_cast<const uint4*>(&tabs->lane_shift[0][0][0]);
     uint4* lds_ls = reinterpret_cast<uint4*>(lds + kLdsSliceWords);
@@ -1279,6 +1277,237 @@ __device__ __forceinline__ void crc_packed_small_body(const RowsArgs& a, std::ui
 #pragma unroll
       for (int i = 0; i < ILP; ++i)
         if (jq + i < nrows) finish(jq + i, p[i].value());
+    }
+  }
+}
+
+// ---- lane blocks ------------------------------------------------------------------
+// One lane folds one whole block of at most kLaneMax = 64 bytes. It starts from the block's own initial
+// register and takes the bytes in the reference's order (crc32.cpp:9-16): whole dwords by slicing-by-4,
+// the last len % 4 bytes by Sarwate steps. There is no GF(2) shift, no lane shift and no reduction, so
+// a WAL record (26 + |k| + |v| bytes, wal.cpp:25) costs the lookups of its own bytes. The bytes come in
+// as the 16-byte aligned granules that cover the block: a granule holding one of the block's bytes
+// lies in a page the block maps, so no load can fault whatever the block's alignment. They are
+// realigned in registers: two bitwise selects by the start's dword offset within its granule, then
+// v_alignbyte by its byte offset. ALIGN 16 (every block start 16-byte aligned) needs neither, ALIGN 4
+// (dword aligned) only the selects.
+constexpr int kLaneGran = 5;  // granules covering 64 bytes at any alignment
+
+template <int ALIGN>
+__device__ __forceinline__ void lane_issue(std::uintptr_t blk, std::uint32_t n, std::uintptr_t dmy,
+                                           uint4 (&g)[kLaneGran]) {
+  constexpr int NG = ALIGN == 16 ? 4 : kLaneGran;
+  const std::uintptr_t al = blk & ~static_cast<std::uintptr_t>(15);
+  const std::uintptr_t last = (blk + n - 1u) & ~static_cast<std::uintptr_t>(15);  // used when n >= 1
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const std::uintptr_t p = al + 16u * i;
+    // past the block's last granule: that granule again (an L1 hit); an empty block reads `dummy`
+    g[i] = gload16(n == 0 ? dmy : (p < last ? p : last));
+  }
+}
+
+// The 16 little-endian dwords d[k] = bytes [blk + 4k, blk + 4k + 4) from the granules (o = blk & 15).
+template <int ALIGN>
+__device__ __forceinline__ void lane_dwords(const uint4 (&g)[kLaneGran], std::uint32_t o, std::uint32_t (&d)[16]) {
+  constexpr int NG = ALIGN == 16 ? 4 : kLaneGran;
+  std::uint32_t raw[4 * kLaneGran];
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    raw[4 * i + 0] = g[i].x;
+    raw[4 * i + 1] = g[i].y;
+    raw[4 * i + 2] = g[i].z;
+    raw[4 * i + 3] = g[i].w;
+  }
+  if constexpr (ALIGN == 16) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = raw[k];
+  } else {
+    // bitwise selects: a ternary on a per-lane condition here becomes a dynamically indexed array
+    const std::uint32_t m8 = 0u - ((o >> 3) & 1u), m4 = 0u - ((o >> 2) & 1u);
+#pragma unroll
+    for (int i = 0; i < 18; ++i) raw[i] ^= (raw[i] ^ raw[i + 2]) & m8;
+#pragma unroll
+    for (int i = 0; i < 17; ++i) raw[i] ^= (raw[i] ^ raw[i + 1]) & m4;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = ALIGN == 4 ? raw[k] : __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], o & 3u);
+  }
+}
+
+// Sarwate steps (crc32.cpp:12-14) over the low m <= 3 bytes of w, with T0 from the LDS image.
+__device__ __forceinline__ std::uint32_t sarwate_bytes(const std::uint32_t* lds, const LaneConst& kc, std::uint32_t c,
+                                                       std::uint32_t w, std::uint32_t m) {
+#pragma unroll
+  for (std::uint32_t j = 0; j < 3u; ++j)
+    if (j < m) c = (c >> 8) ^ lds_at(lds, (((c ^ (w >> (8 * j))) & 0xFFu) << 8) | kc.L0);
+  return c;
+}
+
+// Folds NB blocks (dwords d[i], lengths n[i] <= 64, registers r[i] holding their initial values on
+// entry and their final raw registers on return) with their chains interleaved. UNI: every block has
+// the same length (uniform batches), so the bounds are wave-uniform and the branches scalar.
+template <int NB, bool UNI>
+__device__ __forceinline__ void lane_fold(const std::uint32_t* lds, const LaneConst& kc, const std::uint32_t (*d)[16],
+                                          const std::uint32_t* n, std::uint32_t* r) {
+  std::uint32_t nf[NB], tb[NB];
+  Reg p[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const std::uint32_t len = UNI ? __builtin_amdgcn_readfirstlane(n[0]) : n[i];
+    nf[i] = len >> 2;
+    tb[i] = len & 3u;
+    p[i] = Reg{r[i], 0};
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      if (static_cast<std::uint32_t>(k) < nf[i]) {
+        slice4(lds, p[i], d[i][k], kc);
+      } else if (static_cast<std::uint32_t>(k) == nf[i] && tb[i] != 0u) {
+        p[i] = Reg{sarwate_bytes(lds, kc, p[i].value(), d[i][k], tb[i]), 0};
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) r[i] = p[i].value();
+}
+
+// Uniform batches of blocks of at most kLaneMax bytes, any stride, alignment and initial registers:
+// lane l of wave step s folds block 64 s + l. Waves own contiguous ranges of steps; DEPTH steps of
+// loads are in flight and ILP steps fold with interleaved chains (crc_packed_body's pipeline and issue
+// priority); each step's 64 results leave in one coalesced store.
+template <int ALIGN, int DEPTH, int ILP, int PRIO = 0>
+__device__ __forceinline__ void crc_lanes_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
+  fill_lds_slicing(a.tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const LaneConst kc = lane_const(lane);
+  __syncthreads();
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves, nb = a.nblocks;
+  const std::uint64_t TS = (nb + 63u) / 64u;
+  const std::uint64_t s0 = wave * TS / W;
+  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
+  if (ns == 0) return;
+  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
+  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
+  const std::uint32_t len = a.len;
+  const std::uint64_t blk0 = s0 * 64u + lane;                        // this lane's block in step 0
+  const std::uintptr_t lane_base = base + blk0 * a.stride;
+  const std::uint64_t step_bytes = 64u * a.stride;
+  const std::uintptr_t last_blk = base + (nb - 1u) * a.stride;  // lanes past the batch reload it, store nothing
+
+  uint4 buf[DEPTH][kLaneGran];
+  std::uint32_t ini[DEPTH], o16[DEPTH];
+  auto issue = [&](std::uint32_t j, int slot) {
+    const std::uint32_t jc = j < ns ? j : ns - 1;  // steps past the range reload the last one
+    const std::uint64_t b = blk0 + 64ull * jc;
+    const std::uintptr_t blk = b < nb ? lane_base + jc * step_bytes : last_blk;
+    lane_issue<ALIGN>(blk, len, dmy, buf[slot]);
+    o16[slot] = static_cast<std::uint32_t>(blk & 15u);
+    ini[slot] = a.init_raw ? a.init_raw[b < nb ? b : nb - 1u] : a.init_default;
+  };
+  auto fold = [&](auto nb_const, int q, std::uint32_t j) {
+    constexpr int NB = decltype(nb_const)::value;
+    std::uint32_t d[NB][16], n[NB], r[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      lane_dwords<ALIGN>(buf[q + i], o16[q + i], d[i]);
+      n[i] = len;
+      r[i] = ini[q + i];
+    }
+    lane_fold<NB, true>(lds, kc, d, n, r);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const std::uint64_t b = blk0 + 64ull * (j + i);
+      if (b < nb) a.out[b] = r[i] ^ a.out_xor;
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < DEPTH - ILP; ++s) issue(s, s);
+  for (std::uint32_t j = 0; j < ns; j += DEPTH) {
+    if constexpr (PRIO != 0) set_prio_from_left<PRIO>(ns - j, ns);
+#pragma unroll
+    for (int q = 0; q < DEPTH; q += ILP) {
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) issue(j + q + DEPTH - ILP + i, (q + DEPTH - ILP + i) % DEPTH);
+      const std::uint32_t jq = j + q;
+      if (jq >= ns) break;
+      if (jq + ILP <= ns) {
+        fold(std::integral_constant<int, ILP>{}, q, jq);
+      } else {
+#pragma unroll
+        for (int i = 0; i < ILP; ++i)  // tail: fewer than ILP steps left
+          if (jq + i < ns) fold(std::integral_constant<int, 1>{}, q + i, jq + i);
+      }
+    }
+  }
+}
+
+// Lane blocks of an irregular batch (len <= kLaneMax), walked straight from the caller's offsets and
+// lengths (the prepass lists them nowhere): wave w takes the blocks [w n / W, (w + 1) n / W) 64 at a
+// time, lane l of step j the block b0 + 64 j + l, and folds it if it is a lane block; other lanes idle.
+// Runs in crc_stream's launch when the prepass chose the general path and counted lane blocks, with
+// the slicing tables already in LDS. Descriptors are fetched four steps ahead of their data, data two
+// steps ahead of the fold, and no loaded value is touched before use (small_phase's pipeline).
+__device__ __forceinline__ void lane_phase(const RowsArgs& a, const std::uint32_t* lds) {
+  constexpr int RING = 4;
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const LaneConst kc = lane_const(lane);
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves, n = a.nblocks;
+  const std::uint64_t b0 = wave * n / W, b1 = (wave + 1) * n / W;
+  if (b0 >= b1) return;
+  const std::uint32_t ns = static_cast<std::uint32_t>((b1 - b0 + 63u) / 64u);
+  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
+  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
+
+  std::uint64_t d_off[RING];
+  std::uint32_t d_len[RING];
+  auto fetch = [&](std::uint32_t j, int slot) {
+    const std::uint64_t b = b0 + 64ull * j + lane;
+    const std::uint64_t bc = b < b1 ? b : b1 - 1u;  // clamped: every load stays inside the arrays
+    d_off[slot] = a.l_off[bc];
+    d_len[slot] = a.l_len[bc];
+  };
+  uint4 q[RING][kLaneGran];
+  std::uint32_t m_len[RING], m_o[RING], m_init[RING];
+  auto issue = [&](int slot, std::uint32_t j) {
+    const std::uint64_t b = b0 + 64ull * j + lane;
+    const bool live = j < ns && b < b1 && d_len[slot] <= kLaneMax;
+    const std::uint32_t len = live ? d_len[slot] : 0u;
+    const std::uintptr_t blk = base + d_off[slot];
+    lane_issue<1>(blk, len, dmy, q[slot]);
+    m_len[slot] = live ? len : 0xFFFFFFFFu;  // 0xFFFFFFFF: nothing to store
+    m_o[slot] = static_cast<std::uint32_t>(blk & 15u);
+    m_init[slot] = a.init_raw ? a.init_raw[live ? b : b0] : a.init_default;
+  };
+  auto fold = [&](int slot, std::uint32_t j) {
+    const std::uint32_t len = m_len[slot];
+    const bool live = len != 0xFFFFFFFFu;
+    if (__ballot(live) == 0) return;  // no lane block in this step
+    std::uint32_t d[1][16], nn[1] = {live ? len : 0u}, r[1] = {m_init[slot]};
+    lane_dwords<1>(q[slot], m_o[slot], d[0]);
+    lane_fold<1, false>(lds, kc, d, nn, r);
+    if (live) a.out[b0 + 64ull * j + lane] = r[0] ^ a.out_xor;
+  };
+
+#pragma unroll
+  for (int k = 0; k < RING; ++k) fetch(k, k);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    issue(k, k);
+    fetch(k + RING, k);
+  }
+  for (std::uint32_t t = 0; t < ns; t += RING) {
+#pragma unroll
+    for (int k = 0; k < RING; ++k) {
+      const int ahead = (k + 2) % RING;  // step t+k+2: its descriptor arrived RING steps ago
+      issue(ahead, t + k + 2);
+      fetch(t + k + 2 + RING, ahead);
+      if (t + k < ns) fold(k, t + k);
     }
   }
 }

@@ -30,6 +30,7 @@ hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
 hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st);
 std::uint32_t packed_small_group(std::uint32_t len);
 hipError_t launch_packed_small(const RowsArgs& a, unsigned grid, hipStream_t st);
+hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st);
 hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
                           std::uint32_t n, std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* tile_ok,
                           std::uint32_t* counts, std::uint64_t* sinfo, std::uint64_t* ends, const PrepassOut& o,
@@ -385,7 +386,7 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     }
     const std::uint64_t ntiles = prepass_tiles(cap) + 1;
     // 8-byte arrays first: scan, tiles, s_off, big_off; then the 4-byte ones
-    const std::uint64_t bytes = 8 * (cap + ntiles + 2 * cap) + 4 * (5 * cap + 1) + 4 * ntiles;
+    const std::uint64_t bytes = 8 * (cap + ntiles + 2 * cap) + 4 * (6 * cap + 1) + 4 * 2 * ntiles;
     TKV_HIP(hipMalloc(&s->blob, bytes));
     auto* p8 = static_cast<std::uint64_t*>(s->blob);
     s->scan = p8;
@@ -399,6 +400,8 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     s->po.big_idx = p4 + 3 * cap;
     s->po.row_scan = p4 + 4 * cap;  // cap + 1 entries
     s->tile_ok = p4 + 5 * cap + 1;
+    s->po.tile_lanes = s->tile_ok + ntiles;
+    s->po.lscan = s->po.tile_lanes + ntiles;  // cap entries
     s->cap_blocks = cap;
   }
   s->po.wave_start = s->wave_start;
@@ -417,6 +420,17 @@ RowsArgs base_args(DevCtx* c, StreamScratch* s, int algo) {
   a.out_xor = kInit;
   a.nwaves = c->W;
   return a;
+}
+
+// Uniform batches with len <= lane_max() take crc_lanes: kLaneMax; TKV_LANE_MAX lowers it (-1 turns
+// the kernel off; for A/B measurements against the kernels that served these lengths before).
+long long lane_max() {
+  static const long long v = [] {
+    const char* e = std::getenv("TKV_LANE_MAX");
+    const long long x = e ? std::atoll(e) : static_cast<long long>(kLaneMax);
+    return std::max(-1LL, std::min<long long>(x, kLaneMax));
+  }();
+  return v;
 }
 
 // Uniform-length batch (also used for single spans).
@@ -446,6 +460,15 @@ int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t s
     a.nwaves = static_cast<std::uint32_t>(packed_waves);
     a.snap_blocks = 1;
     TKV_HIP(launch_packed(a, static_cast<unsigned>(c->ncu), st));  // whole blocks per wave, no seams
+    return TKV_OK;
+  }
+  if (static_cast<long long>(len) <= lane_max()) {
+    // one lane per block: any stride, alignment and initial registers
+    const std::uint64_t steps = (n + 63) / 64;
+    const std::uint64_t grid =
+        std::max<std::uint64_t>(1, std::min<std::uint64_t>(c->ncu, (steps + kWavesPerWG - 1) / kWavesPerWG));
+    a.nwaves = static_cast<std::uint32_t>(grid * kWavesPerWG);
+    TKV_HIP(launch_lanes(a, static_cast<unsigned>(grid), st));
     return TKV_OK;
   }
   if (aligned && !d_init && stride == len && packed_small_group(a.len)) {
@@ -499,6 +522,8 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   auto* row0 = a.s_wtot + c->W;                             // (the seam records hold 16 words per wave)
   a.s_row0 = row0;
   a.s_wv = s->po.big_idx;
+  a.l_off = d_off;  // the lane phase walks the caller's own arrays
+  a.l_len = d_len;
   TKV_HIP(launch_prepass(d_base, d_off, d_len, a.nblocks, s->scan, s->tiles, s->tile_ok, s->counts, sinfo, s->po.big_off,
                          s->po, a.nwaves, static_cast<std::uint32_t>(c->ncu), d_out, row0, st));
   // stream mode: crc_stream walks the rows and crc_rows finishes the block CRCs; general path:

@@ -103,15 +103,27 @@ struct RowsArgs {
   std::uint32_t* s_wtot;             // per wave: crc_0 of its rows alone (crc_stream_body)
   const std::uint32_t* s_row0;       // [w] = first row of wave w, [nwaves] = rows (rows_tile_scan)
   std::uint32_t* s_wv;               // per block: the wave that met its end (crc_stream_body)
+  // irregular batches: the caller's own arrays, which the lane phase walks (blocks of at most kLaneMax
+  // bytes are in no prepass list; counts[kCountLanes] says how many there are)
+  const std::uint64_t* l_off;
+  const std::uint32_t* l_len;
 };
 constexpr std::uint32_t kModeStream = 1;
+// counts[] of an irregular batch: [0] large blocks, [1] small blocks, [2] rows of the large blocks,
+// [3] mode, [4..7] stream-mode info (two u64), [8] lane blocks (len <= kLaneMax)
+constexpr int kCountLanes = 8;
+
+// Blocks of at most kLaneMax bytes are folded whole by one lane each, from their own initial register
+// (DESIGN.md §4.5): uniform batches by crc_lanes, irregular ones by the lane phase in crc_stream's
+// launch. The prepass lists them nowhere, and stream mode needs every block to be longer.
+constexpr std::uint32_t kLaneMax = 64;
 
 // One short host span for crc_span: `len` bytes at byte `pos` (16-byte aligned) of the mapped
 // staging buffer, folded on from raw register `init`.
 struct SpanDesc {
   std::uint32_t pos, len, init, pad;
 };
-constexpr std::uint32_t kStreamMinLen = 64;  // at most one block end per 64-byte lane segment
+constexpr std::uint32_t kStreamMinLen = kLaneMax + 1;  // at most one block end per 64-byte lane segment
 
 // Outputs of the irregular prepass (scratch of one stream).
 struct PrepassOut {
@@ -123,6 +135,8 @@ struct PrepassOut {
   std::uint32_t* big_idx;
   std::uint32_t* row_scan;
   std::uint32_t* wave_start;
+  std::uint32_t* lscan;       // per block: lane blocks in front of it (exclusive, within its tile)
+  std::uint32_t* tile_lanes;  // per scan tile: its lane blocks (then their exclusive scan)
 };
 
 // Blocks of at most kSmallMax bytes are folded four to a wave (16 lanes x 64 B each) by the

@@ -102,12 +102,23 @@ constexpr unsigned kStreamThreads = kThreads;
 constexpr int kStreamSkew = 154;
 __global__ __launch_bounds__(kStreamThreads) void crc_stream(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  if (dev::sload32(a.counts, 3) != kModeStream) return;
+  const bool stream = dev::sload32(a.counts, 3) == kModeStream;
+  // General path: this launch folds the batch's lane blocks (len <= kLaneMax), if the
+  // prepass counted any; crc_rows follows with the rest.
+  if (!stream && dev::sload32(a.counts, kCountLanes) == 0) return;
+  // The one barrier of the kernel, in front of every branch (the mode is the same for the whole grid).
+  if (stream) dev::fill_lds(a.tabs, lds);
+  else dev::fill_lds_slicing(a.tabs, lds);
+  __syncthreads();
+  if (!stream) {
+    dev::lane_phase(a, lds);
+    return;
+  }
   // issue priority from the rows left: +0.8 % on cfg4 (in-process A/B). A wave whose rows hold more
   // than 8 block ends per row on average (blocks under ~500 bytes) takes them a row at a time
   // (MANY); the others keep the per-end loop, whose code the MANY path slows by up to 10 % when it
-  // shares the loop (4 KiB blocks, profiles/r2/stream_many/). Both paths end in the one barrier of
-  // crc_stream_body's table fill, so a workgroup may mix them.
+  // shares the loop (4 KiB blocks, profiles/r2/stream_many/). Neither body holds a barrier, so the
+  // waves of a workgroup may mix them.
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint32_t g0 = dev::sload32(a.s_row0, wave), g1 = dev::sload32(a.s_row0, wave + 1);
   const std::uint32_t e0 = dev::sload32(a.wave_start, wave);
@@ -144,6 +155,14 @@ template <int G, bool EXACT>
 __global__ __launch_bounds__(kThreads) void crc_packed_small(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   dev::crc_packed_small_body<G, EXACT, kPackedDepth, kPackedIlp, kPackedPrio>(a, lds);
+}
+
+// Uniform batches of blocks of at most kLaneMax bytes (any stride, alignment, initial registers): one
+// lane per block. Only the slicing tables go to LDS (128 KiB).
+template <int ALIGN>
+__global__ __launch_bounds__(kThreads) void crc_lanes(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  dev::crc_lanes_body<ALIGN, kPackedDepth, kPackedIlp, kPackedPrio>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
@@ -186,8 +205,10 @@ __device__ __forceinline__ StreamGeom stream_geometry(const std::uint8_t* base, 
 __global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase, const std::uint64_t* offsets,
                                                       const std::uint32_t* lengths, std::uint32_t n,
                                                       std::uint64_t* scan, std::uint64_t* tile_sums,
-                                                      std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws) {
+                                                      std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
+                                                      std::uint32_t* lscan, std::uint32_t* tile_lanes) {
   __shared__ std::uint64_t wsum[16];
+  __shared__ std::uint32_t lsum[16];
   // stream mode's wave partition (used only if the prepass picks stream mode): row0[0..Ws], grid-stride
   for (std::uint32_t w = blockIdx.x * 1024u + threadIdx.x; w <= Ws; w += gridDim.x * 1024u) {
     const std::uint64_t TR = stream_geometry(sbase, offsets, lengths, n).rows;
@@ -196,79 +217,113 @@ __global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase
   const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * 4u;
   const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   std::uint64_t v[4], s = 0;
+  std::uint32_t lv[4], ls = 0;  // lane blocks (len <= kLaneMax): in no list, folded by the lane phase
   bool ok = true;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const std::uint64_t b = base + i;
     const std::uint32_t len = b < n ? lengths[b] : 0u;
-    v[i] = b < n ? scan_item(len) : 0ull;
+    lv[i] = b < n && len <= kLaneMax ? 1u : 0u;
+    v[i] = b < n && !lv[i] ? scan_item(len) : 0ull;
     s += v[i];
+    ls += lv[i];
+    // (a lane block is shorter than kStreamMinLen: its offsets are never read here)
     if (b < n) ok = ok && len >= kStreamMinLen && (b + 1 >= n || offsets[b] + len == offsets[b + 1]);
   }
   const bool tile_all_ok = __syncthreads_and(ok ? 1 : 0) != 0;
   if (threadIdx.x == 0) tile_ok[blockIdx.x] = tile_all_ok ? 1u : 0u;
-  // Inclusive scan of the thread sums inside the wave (cross-lane shifts, no barriers), then the
+  // Inclusive scans of the thread sums inside the wave (cross-lane shifts, no barriers), then the
   // 16 wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
   std::uint64_t inc = s;
+  std::uint32_t linc = ls;
 #pragma unroll
   for (unsigned off = 1; off < 64; off <<= 1) {
     const std::uint64_t y = __shfl_up(inc, off, 64);
+    const std::uint32_t ly = __shfl_up(linc, off, 64);
     inc += lane >= off ? y : 0ull;
+    linc += lane >= off ? ly : 0u;
   }
-  if (lane == 63u) wsum[wid] = inc;
+  if (lane == 63u) {
+    wsum[wid] = inc;
+    lsum[wid] = linc;
+  }
   __syncthreads();
   std::uint64_t wpre = 0, tot = 0;
+  std::uint32_t lpre = 0, ltot = 0;
 #pragma unroll
   for (unsigned w = 0; w < 16; ++w) {
     const std::uint64_t t = wsum[w];
+    const std::uint32_t lt = lsum[w];
     wpre += w < wid ? t : 0ull;
     tot += t;
+    lpre += w < wid ? lt : 0u;
+    ltot += lt;
   }
   std::uint64_t run = wpre + inc - s;  // exclusive
+  std::uint32_t lrun = lpre + linc - ls;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    if (base + i < n) scan[base + i] = run;
+    if (base + i < n && !lv[i]) {  // the scatter reads these for listed blocks only
+      scan[base + i] = run;
+      lscan[base + i] = lrun;
+    }
     run += v[i];
+    lrun += lv[i];
   }
-  if (threadIdx.x == 1023) tile_sums[blockIdx.x] = tot;
+  if (threadIdx.x == 1023) {
+    tile_sums[blockIdx.x] = tot;
+    tile_lanes[blockIdx.x] = ltot;
+  }
 }
 
-__global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums, std::uint32_t ntiles,
-                                                       std::uint32_t n, std::uint32_t* counts) {
+__global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums, std::uint32_t* tile_lanes,
+                                                       std::uint32_t ntiles, std::uint32_t n, std::uint32_t* counts) {
   __shared__ std::uint64_t part[1024];
-  std::uint64_t carry = 0;
+  __shared__ std::uint32_t lpart[1024];
+  std::uint64_t carry = 0, lcarry = 0;
   for (std::uint32_t t0 = 0; t0 < ntiles; t0 += 1024) {
     const std::uint32_t i = t0 + threadIdx.x;
     const std::uint64_t x = i < ntiles ? tile_sums[i] : 0ull;
+    const std::uint32_t lx = i < ntiles ? tile_lanes[i] : 0u;
     part[threadIdx.x] = x;
+    lpart[threadIdx.x] = lx;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {
       const std::uint64_t y = threadIdx.x >= static_cast<unsigned>(off) ? part[threadIdx.x - off] : 0ull;
+      const std::uint32_t ly = threadIdx.x >= static_cast<unsigned>(off) ? lpart[threadIdx.x - off] : 0u;
       __syncthreads();
       part[threadIdx.x] += y;
+      lpart[threadIdx.x] += ly;
       __syncthreads();
     }
-    if (i < ntiles) tile_sums[i] = carry + part[threadIdx.x] - x;  // exclusive tile offset
+    if (i < ntiles) {
+      tile_sums[i] = carry + part[threadIdx.x] - x;  // exclusive tile offsets
+      tile_lanes[i] = static_cast<std::uint32_t>(lcarry + lpart[threadIdx.x] - lx);
+    }
     const std::uint64_t tot = part[1023];
+    const std::uint32_t ltot = lpart[1023];
     __syncthreads();
     carry += tot;
+    lcarry += ltot;
   }
   if (threadIdx.x == 0) {
-    const std::uint32_t ns = static_cast<std::uint32_t>(carry);
-    counts[0] = n - ns;                                // large blocks
-    counts[1] = ns;                                    // small blocks
+    const std::uint32_t ns = static_cast<std::uint32_t>(carry), nl = static_cast<std::uint32_t>(lcarry);
+    counts[0] = n - ns - nl;                               // large blocks
+    counts[1] = ns;                                        // small blocks
     counts[2] = static_cast<std::uint32_t>(carry >> 32);  // rows of the large blocks
     counts[3] = 0;                                         // general path (no stream mode here)
+    counts[kCountLanes] = nl;                              // lane blocks
   }
 }
 
-// Scatter of one block (rows_finish): e = its exclusive (small count, rows) pair, TR = rows of all
-// large blocks. A large block cut between row-kernel waves gets its result zeroed here, since the
-// row kernel XORs every piece of it into the result (crc_rows_body, irregular batches).
-// len and off are the block's length and offset (loaded by the caller).
+// Scatter of one block (rows_finish): e = its exclusive (small count, rows) pair, nlane = lane blocks
+// in front of it, TR = rows of all large blocks. A large block cut between row-kernel waves gets its
+// result zeroed here, since the row kernel XORs every piece of it into the result (crc_rows_body,
+// irregular batches). len and off are the block's length and offset (loaded by the caller).
 __device__ __forceinline__ void finish_block(std::uint64_t off, std::uint32_t len, std::uint64_t b, std::uint64_t e,
-                                             std::uint64_t TR, const PrepassOut& o, std::uint32_t W,
-                                             std::uint32_t* out) {
+                                             std::uint64_t nlane, std::uint64_t TR, const PrepassOut& o,
+                                             std::uint32_t W, std::uint32_t* out) {
+  if (len <= kLaneMax) return;  // the lane phase's
   const std::uint32_t nsmall = static_cast<std::uint32_t>(e);
   if (len <= kSmallMax) {
     o.s_off[nsmall] = off;
@@ -276,7 +331,7 @@ __device__ __forceinline__ void finish_block(std::uint64_t off, std::uint32_t le
     o.s_idx[nsmall] = static_cast<std::uint32_t>(b);
     return;
   }
-  const std::uint32_t k = static_cast<std::uint32_t>(b) - nsmall;  // compacted index
+  const std::uint32_t k = static_cast<std::uint32_t>(b - nsmall - nlane);  // compacted index
   const std::uint64_t lo = e >> 32;
   o.big_off[k] = off;
   o.big_len[k] = len;
@@ -296,7 +351,10 @@ __global__ void rows_finish(const std::uint64_t* offsets, const std::uint32_t* l
                             PrepassOut o, std::uint32_t W, std::uint32_t* out) {
   const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
   if (b >= n) return;
-  finish_block(offsets[b], lengths[b], b, scan[b] + tile_offs[b / kScanTile], counts[2], o, W, out);
+  const std::uint32_t len = lengths[b];
+  if (len <= kLaneMax) return;  // the lane phase's
+  const std::uint64_t t = b / kScanTile;
+  finish_block(offsets[b], len, b, scan[b] + tile_offs[t], o.lscan[b] + o.tile_lanes[t], counts[2], o, W, out);
 }
 
 // rows_finish with the scan of the tile sums folded in (ntiles <= kFusedTiles): every workgroup sums
@@ -320,6 +378,7 @@ __device__ __forceinline__ void stream_block(const std::uint8_t* base, const std
     counts[1] = 0;
     counts[2] = static_cast<std::uint32_t>(g.rows);
     counts[3] = kModeStream;
+    counts[kCountLanes] = 0;  // every block is longer than kLaneMax in stream mode
     sinfo[0] = g.zoff;
     sinfo[1] = g.s0rel;
   }
@@ -338,19 +397,24 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     std::uint32_t* counts, PrepassOut o, std::uint32_t W, std::uint32_t* out, std::uint64_t* ends,
     std::uint64_t* sinfo, std::uint32_t Ws, const std::uint32_t* row0) {
   constexpr std::uint32_t kWaves = kFinishThreads / 64;
-  __shared__ std::uint64_t red[3][kWaves];
+  __shared__ std::uint64_t red[5][kWaves];
   const std::uint32_t my_tile = blockIdx.x * kFinishThreads / kScanTile;  // kScanTile % 256 == 0
-  // The block's own operands are loaded first, so their latency overlaps the tile-sum reduction.
+  // The block's own operands are loaded first, so their latency overlaps the tile-sum reduction (the
+  // scan values of a lane block were never written and are not used).
   const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(kFinishThreads) + threadIdx.x;
   const bool live = b < n;
   const std::uint32_t len = live ? lengths[b] : 0u;
   const std::uint64_t off = live ? offsets[b] : 0ull;
   const std::uint64_t sc = live ? scan[b] : 0ull;
-  std::uint64_t before = 0, all = 0, bad = 0;
+  const std::uint32_t lsc = live ? o.lscan[b] : 0u;
+  std::uint64_t before = 0, all = 0, bad = 0, lbefore = 0, lall = 0;
   for (std::uint32_t i = threadIdx.x; i < ntiles; i += kFinishThreads) {
     const std::uint64_t v = tile_sums[i];
+    const std::uint64_t lv = o.tile_lanes[i];
     all += v;
     before += i < my_tile ? v : 0ull;
+    lall += lv;
+    lbefore += i < my_tile ? lv : 0ull;
     bad += tile_ok[i] ? 0u : 1u;
   }
   // Wave sums by cross-lane exchange, then the kWaves partial sums through LDS (one barrier).
@@ -359,34 +423,41 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     before += __shfl_xor(before, m, 64);
     all += __shfl_xor(all, m, 64);
     bad += __shfl_xor(bad, m, 64);
+    lbefore += __shfl_xor(lbefore, m, 64);
+    lall += __shfl_xor(lall, m, 64);
   }
   const unsigned wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63u) == 0) {
     red[0][wid] = before;
     red[1][wid] = all;
     red[2][wid] = bad;
+    red[3][wid] = lbefore;
+    red[4][wid] = lall;
   }
   __syncthreads();
-  std::uint64_t tile_off = 0, total = 0, nbad = 0;
+  std::uint64_t tile_off = 0, total = 0, nbad = 0, tile_loff = 0, ltotal = 0;
 #pragma unroll
   for (unsigned w = 0; w < kWaves; ++w) {
     tile_off += red[0][w];
     total += red[1][w];
     nbad += red[2][w];
+    tile_loff += red[3][w];
+    ltotal += red[4][w];
   }
   if (nbad == 0) {  // every block qualifies: stream mode
     if (live) stream_block(base, offsets, lengths, n, b, off, len, Ws, row0, counts, ends, sinfo, o.wave_start);
     return;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const std::uint32_t ns = static_cast<std::uint32_t>(total);
-    counts[0] = n - ns;                                    // large blocks
+    const std::uint32_t ns = static_cast<std::uint32_t>(total), nl = static_cast<std::uint32_t>(ltotal);
+    counts[0] = n - ns - nl;                               // large blocks
     counts[1] = ns;                                        // small blocks
     counts[2] = static_cast<std::uint32_t>(total >> 32);  // rows of the large blocks
     counts[3] = 0;                                         // general path
+    counts[kCountLanes] = nl;                              // lane blocks (crc_stream's lane phase)
   }
   if (!live) return;
-  finish_block(off, len, b, sc + tile_off, total >> 32, o, W, out);
+  finish_block(off, len, b, sc + tile_off, lsc + tile_loff, total >> 32, o, W, out);
 }
 
 
@@ -573,6 +644,16 @@ hipError_t launch_packed_small(const RowsArgs& a, unsigned grid, hipStream_t st)
   return hipGetLastError();
 }
 
+// Uniform lane-block batch (a.len <= kLaneMax): ALIGN from the base pointer and the stride.
+hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st) {
+  if (a.len > kLaneMax) return hipErrorInvalidValue;
+  const std::uintptr_t m = reinterpret_cast<std::uintptr_t>(a.base) | static_cast<std::uintptr_t>(a.stride);
+  if ((m & 15u) == 0) hipLaunchKernelGGL(crc_lanes<16>, dim3(grid), dim3(kThreads), 0, st, a);
+  else if ((m & 3u) == 0) hipLaunchKernelGGL(crc_lanes<4>, dim3(grid), dim3(kThreads), 0, st, a);
+  else hipLaunchKernelGGL(crc_lanes<1>, dim3(grid), dim3(kThreads), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_fixup(const RowsArgs& a, hipStream_t st) {
   const unsigned grid = (2u * a.nwaves + 255u) / 256u;  // one thread per seam record
   hipLaunchKernelGGL(crc_fixup, dim3(grid), dim3(256), 0, st, a);
@@ -590,14 +671,14 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
   const std::uint64_t nfused = (static_cast<std::uint64_t>(n) + kFinishThreads - 1) / kFinishThreads;
   const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
   hipLaunchKernelGGL(rows_tile_scan, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets, lengths,
-                     n, scan, tile_sums, tile_ok, row0, Ws);
+                     n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes);
   if (ntiles <= kFusedTiles) {
     hipLaunchKernelGGL(rows_finish_fused, dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
                        offsets, lengths, n, scan, tile_sums, tile_ok, static_cast<std::uint32_t>(ntiles), counts, o,
                        W, out, ends, sinfo, Ws, row0);
   } else {
-    hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, static_cast<std::uint32_t>(ntiles), n,
-                       counts);
+    hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, o.tile_lanes,
+                       static_cast<std::uint32_t>(ntiles), n, counts);
     hipLaunchKernelGGL(rows_finish, dim3(static_cast<unsigned>(nfinish)), dim3(256), 0, st, offsets, lengths, n, scan,
                        tile_sums, counts, o, W, out);
   }

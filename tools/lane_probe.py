@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""WAL-record-sized blocks (not product code): several builds of libtkv_crc32.so in one process,
+rotated round by round on one stream and the same device buffers. GB/s of payload from HIP events
+around K launches (median over rounds); every library's results are checked against the first's.
+
+    python tools/lane_probe.py lib1.so [lib2.so ...] [--rounds 5] [--reps 5] [--gib 1] [--only 36]
+
+Workloads: uniform batches of 26-64 B blocks (the reference's records are
+26 + |k| + |v| bytes, wal.cpp:25), the same at the WAL payload pitch (8-byte header between payloads)
+and at an odd base, and irregular batches of WAL payloads (8-byte gaps), back-to-back small blocks
+and a mixed 0-4 KiB batch.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+VP = ctypes.c_void_p
+U64 = ctypes.c_uint64
+
+
+def load(path):
+    lib = ctypes.CDLL(os.path.abspath(path))
+    lib.tkv_crc32_batch_uniform_device.argtypes = [VP, U64, U64, VP, VP, U64, VP]
+    lib.tkv_crc32_batch_device.argtypes = [VP, VP, VP, VP, VP, U64, VP]
+    lib.tkv_last_error.restype = ctypes.c_char_p
+    assert lib.tkv_set_device(0) == 0
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--gib", type=float, default=1.0)
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    libs = [load(p) for p in args.libs]
+    st = torch.cuda.current_stream()
+    sp = VP(st.cuda_stream)
+    total = int(args.gib * (1 << 30))
+    data = torch.randint(0, 256, (total + (total // 4) + 8192,), dtype=torch.uint8, device="cuda")
+    D = data.data_ptr()
+    rng = np.random.default_rng(0)
+
+    def uniform(L, stride=None, off=0):
+        stride = stride or L
+        n = total // stride
+        return (f"uniform {L} B stride {stride} base+{off}", n * L, n,
+                lambda lib, o: lib.tkv_crc32_batch_uniform_device(VP(D + off), stride, L, None, o, n, sp))
+
+    def irregular(name, lens, gaps, off=0):
+        lens = np.asarray(lens, np.int64)
+        offs = off + np.concatenate([[0], np.cumsum(lens[:-1] + gaps[:-1])])
+        d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
+        d_l = torch.from_numpy(lens.astype(np.int32)).cuda()
+        n = lens.size
+        return (name, int(lens.sum()), n,
+                lambda lib, o: lib.tkv_crc32_batch_device(VP(D), VP(d_o.data_ptr()), VP(d_l.data_ptr()), None, o, n, sp),
+                (d_o, d_l))
+
+    def count(L, pitch):
+        return total // pitch
+
+    work = []
+    for L in (26, 28, 33, 36, 59, 64):
+        work.append(uniform(L))
+    work.append(uniform(36, 44, 8))   # WAL payload pitch: 8-byte header in front of every 36-byte payload
+    work.append(uniform(36, 36, 3))   # odd base
+    work.append(uniform(59, 67, 8))
+    n36 = count(36, 44)
+    work.append(irregular("irregular WAL payloads 36 B, 8 B gaps", np.full(n36, 36), np.full(n36, 8), 8))
+    nm = count(42, 50)
+    lm = rng.choice([26, 28, 33, 36, 59], nm)
+    work.append(irregular("irregular WAL payloads 26-59 B, 8 B gaps", lm, np.full(nm, 8), 8))
+    n = count(36, 36)
+    work.append(irregular("irregular back to back 36 B", np.full(n, 36), np.zeros(n, np.int64), 0))
+    n = count(64, 64)
+    work.append(irregular("irregular back to back 64 B", np.full(n, 64), np.zeros(n, np.int64), 0))
+    n = count(128, 128)
+    work.append(irregular("irregular back to back 128 B", np.full(n, 128), np.zeros(n, np.int64), 0))
+    n = count(2048, 2056)
+    lr = rng.integers(0, 4097, n)
+    work.append(irregular("irregular 0-4 KiB, 8 B gaps", lr, np.full(n, 8), 8))
+
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for w in work:
+        name, nbytes, n, call = w[0], w[1], w[2], w[3]
+        if args.only and args.only not in name:
+            continue
+        outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in libs]
+        times = [[] for _ in libs]
+        for r in range(args.rounds):
+            for k in range(len(libs)):
+                i = (k + r) % len(libs)
+                call(libs[i], VP(outs[i].data_ptr()))
+                torch.cuda.synchronize()
+                e0.record(st)
+                for _ in range(args.reps):
+                    rc = call(libs[i], VP(outs[i].data_ptr()))
+                e1.record(st)
+                torch.cuda.synchronize()
+                if rc != 0:
+                    raise SystemExit(f"{args.libs[i]}: {name}: rc {rc}: {libs[i].tkv_last_error()}")
+                times[i].append(e0.elapsed_time(e1) / args.reps)
+        for i, p in enumerate(args.libs):
+            ms = float(np.median(times[i]))
+            same = bool(torch.equal(outs[i], outs[0]))
+            print(json.dumps({"work": name, "lib": os.path.basename(p), "blocks": n, "payload_bytes": nbytes,
+                              "ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1), "same_as_first": same}),
+                  flush=True)
+        del outs
+
+
+if __name__ == "__main__":
+    main()
