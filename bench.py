@@ -235,6 +235,110 @@ def cpu_baseline(host, nblocks, blen, seconds_target=16.0, total_blocks=None, of
             "one_core_gibs": round(one_core_gibs, 4), "slicing_by_8": slicing8}, out[:sample]
 
 
+def prepare(cfg, first, nblocks, dev, ora):
+    """Synthetic batch of `cfg` (rank shard [first, first + nblocks)) resident in HBM, and one step
+    over it: (step(stream, out), bytes per step, blen, lens, offs, data)."""
+    import torch
+    import tinykvpp_amd as tk
+    _, blen, _ = CONFIGS[cfg]
+    if blen is None:  # cfg4: Zipf lengths computed on the host (SURVEY §8d), packed, unaligned
+        lens = np.zeros(nblocks, np.uint64)
+        ora.oracle_zipf_lengths.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p]
+        ora.oracle_zipf_lengths(1, first, nblocks, lens.ctypes.data)
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+        total = int(lens.sum())
+        data = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+        d_off = torch.from_numpy(offs).to(dev)
+        d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+        tk.fill_synthetic_blocks(data, d_off, d_len, first_block=first)
+
+        def step(strm, o):
+            tk.crc32_batch(data, d_off, d_len, out=o, stream=strm)
+        keep = (d_off, d_len)
+    else:
+        lens, offs, keep = None, None, ()
+        total = nblocks * blen
+        data = torch.empty(total, dtype=torch.uint8, device=dev)
+        tk.fill_synthetic_uniform(data, blen, nblocks, first_block=first)
+
+        def step(strm, o):
+            tk.crc32_batch_uniform(data, blen, nblocks, out=o, stream=strm)
+    torch.cuda.synchronize()
+    return {"step": step, "total": total, "blen": blen, "lens": lens, "offs": offs, "data": data, "keep": keep}
+
+
+def time_steps(step, out, stream, steps, barrier=None):
+    """K back-to-back steps on one stream between one HIP event pair, bracketed by barrier() (ranks)
+    and a device sync on both sides: (wall s, device ms per step)."""
+    import torch
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if barrier is not None:
+        barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        step(stream, out)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if barrier is not None:
+        barrier()
+    return time.perf_counter() - t0, ev0.elapsed_time(ev1) / steps
+
+
+def roofline(total, kernel_ms, cfg, traffic_csv=None):
+    traffic, traffic_src = pmc_traffic(traffic_csv, cfg)
+    achieved = total / (kernel_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+            "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": total}
+
+
+def host_legs(cfg_ctx, crcs):
+    """cfg3 "+ H2D/D2H timed" (BASELINE configs[2]): the same blocks starting and ending in pinned host
+    memory, through tkv_crc32_batch_host, two ways: staged (hipMemcpyAsync of 256 MiB slabs to HBM on
+    two streams, the kernel there, results back) and zero-copy (the kernels read the pinned buffer in
+    place over PCIe). Never `value`."""
+    import torch
+    import tinykvpp_amd as tk
+    lib = tk.load_library()
+    total, blen = cfg_ctx["total"], cfg_ctx["blen"]
+    nblocks = total // blen
+    host_p = torch.empty(total, dtype=torch.uint8).pin_memory()
+    host_p.copy_(cfg_ctx["data"])
+    hp = host_p.numpy()
+    offs_h = np.arange(nblocks, dtype=np.uint64) * blen
+    lens_h = np.full(nblocks, blen, np.uint32)
+    legs = {}
+    for name, mapped in (("staged_hipMemcpyAsync", 0), ("zero_copy", 1)):
+        prev = lib.tkv_debug_set_host_mapped(mapped)
+        try:
+            got = tk.crc32_batch_host(hp, offs_h, lens_h)
+            t0 = time.perf_counter()
+            for _ in range(2):
+                tk.crc32_batch_host(hp, offs_h, lens_h)
+            dt = (time.perf_counter() - t0) / 2
+        finally:
+            lib.tkv_debug_set_host_mapped(prev)
+        legs[name] = {"value": round(total / (1 << 30) / dt, 2), "unit": "GiB/s", "GB_per_s": round(total / 1e9 / dt, 2),
+                      "bit_exact": bool(np.array_equal(got, crcs))}
+    legs["source"] = "pinned host memory in, host results out, whole batch per call, mean of 2 calls after one untimed"
+    del host_p, hp
+    return legs
+
+
+def build_identity():
+    """The build id baked into the loaded library against the hash of this tree's sources."""
+    from tinykvpp_amd import build_id
+    try:
+        lib_id, tree, same = build_id.check()
+    except AttributeError:  # a library built before tkv_build_id existed
+        lib_id, tree, same = None, build_id.source_hash(), False
+    if not same:
+        print(f"bench.py: WARNING: libtkv_crc32.so build id {lib_id} != tree source hash {tree}", file=sys.stderr)
+    return {"library": lib_id, "tree": tree, "match": same}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -246,6 +350,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="cfg3: skip the host-memory end-to-end measurement")
     ap.add_argument("--no-pipelined", action="store_true", help="skip the two-stream pipelined rate (extra field)")
+    ap.add_argument("--no-more-configs", action="store_true",
+                    help="cfg2 at N=1: skip timing cfg3 and cfg4 in the same run (more_configs)")
     ap.add_argument("--traffic-csv", default=None,
                     help="rocprofv3 --pmc counter_collection.csv (FETCH_SIZE) of this command, for roofline.traffic")
     args = ap.parse_args()
@@ -281,27 +387,8 @@ def main():
     ora = load_oracle()
     stream = torch.cuda.current_stream()
     out = torch.empty(nblocks, dtype=torch.int32, device=dev)
-    if blen is None:  # cfg4: Zipf lengths computed on the host, packed, unaligned
-        lens = np.zeros(nblocks, np.uint64)
-        ora.oracle_zipf_lengths.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_void_p]
-        ora.oracle_zipf_lengths(1, first, nblocks, lens.ctypes.data)
-        offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
-        total = int(lens.sum())
-        data = torch.empty(total + 64, dtype=torch.uint8, device=dev)
-        d_off = torch.from_numpy(offs).to(dev)
-        d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
-        tk.fill_synthetic_blocks(data, d_off, d_len, first_block=first)
-
-        def step(strm=None, o=out):
-            tk.crc32_batch(data, d_off, d_len, out=o, stream=strm)
-    else:
-        total = nblocks * blen
-        data = torch.empty(total, dtype=torch.uint8, device=dev)
-        tk.fill_synthetic_uniform(data, blen, nblocks, first_block=first)
-
-        def step(strm=None, o=out):
-            tk.crc32_batch_uniform(data, blen, nblocks, out=o, stream=strm)
-    torch.cuda.synchronize()
+    ctx = prepare(args.config, first, nblocks, dev, ora)
+    step, total, lens, offs, data = ctx["step"], ctx["total"], ctx["lens"], ctx["offs"], ctx["data"]
 
     if use_dist:
         # The first collective builds the communicator (RCCL: hundreds of ms). Paid here, before the
@@ -310,26 +397,13 @@ def main():
         # (profiles/r2/dist/bench_nccl_ws1_lazy.json).
         dist.barrier()
         reduce_timing(0.0, 0.0, True, dist, dev if backend == "nccl" else None)
-    warm_steps, warm_ms = warm_up(step, args.warmup, args.min_warmup_ms)
+    warm_steps, warm_ms = warm_up(lambda: step(None, out), args.warmup, args.min_warmup_ms)
 
     # One HIP event pair on the launch stream brackets the K steps; the average launch duration is
     # their span / K. Event markers between steps would each hold the next launch back by ~10 us
     # (rocprofv3 kernel trace: back-to-back launches start 0 us after their predecessor ends,
     # 10.4 us with two markers between them), a cost no caller pays.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        step(stream)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if use_dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    elapsed, kernel_ms = time_steps(step, out, stream, args.steps, dist.barrier if use_dist else None)
 
     # correctness of this exact buffer, from the last timed step (checked after the timed region so
     # no CPU pause lets the clocks fall between warmup and timing)
@@ -348,9 +422,6 @@ def main():
     bytes_per_step = total
     total_bytes = bytes_per_step * args.steps * world
     value = total_bytes / (1 << 30) / elapsed
-    achieved = bytes_per_step / (kernel_ms * 1e-3) / 1e9
-
-    traffic, traffic_src = pmc_traffic(args.traffic_csv, args.config)
 
     line = {
         "metric": "GiB/s CRC32 over device-resident blocks (4 KiB & 64 KiB) on 1 MI355X",
@@ -372,11 +443,9 @@ def main():
         "bit_exact": bit_exact,
         "bit_exact_scope": scope,
         "ranks_seen": ranks_seen,
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "traffic_source": traffic_src, "kernel_ms": round(kernel_ms, 4),
-                     "algorithmic_bytes_per_launch": bytes_per_step},
+        "roofline": roofline(bytes_per_step, kernel_ms, args.config, args.traffic_csv),
         "cpu_baseline": None,
+        "build": build_identity(),
     }
     if world == 1 and not args.no_pipelined:
         # A caller checksumming a stream of batches may alternate two HIP streams: each launch's
@@ -396,23 +465,9 @@ def main():
         line["pipelined_two_streams"] = {"value": round(total * args.steps / (1 << 30) / dt2, 2), "unit": "GiB/s",
                                          "ms_per_step": round(dt2 * 1e3 / args.steps, 4), "bit_exact": same,
                                          "note": "consecutive steps alternate two streams; not `value`"}
+        del outs, strms
     if args.config == "cfg3" and not args.no_e2e:
-        # BASELINE cfg3 "+ H2D/D2H timed": the same blocks starting and ending in host memory (pinned,
-        # read in place by the kernels over PCIe; results copied back), per rank; never `value`.
-        host_p = torch.empty(total, dtype=torch.uint8).pin_memory()
-        host_p.copy_(data)
-        hp = host_p.numpy()
-        offs_h = np.arange(nblocks, dtype=np.uint64) * blen
-        lens_h = np.full(nblocks, blen, np.uint32)
-        got = tk.crc32_batch_host(hp, offs_h, lens_h)
-        t0 = time.perf_counter()
-        for _ in range(2):
-            tk.crc32_batch_host(hp, offs_h, lens_h)
-        dt_e2e = (time.perf_counter() - t0) / 2
-        line["e2e_host"] = {"value": round(total / (1 << 30) / dt_e2e, 2), "unit": "GiB/s",
-                            "GB_per_s": round(total / 1e9 / dt_e2e, 2), "source": "pinned host memory, read in place",
-                            "bit_exact": bool(np.array_equal(got, crcs))}
-        del host_p, hp
+        line["e2e_host"] = host_legs(ctx, crcs)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if blen is not None:
             nb_host = min(nblocks, (4 << 30) // blen)  # at most 4 GiB of the batch goes to host memory
@@ -425,6 +480,33 @@ def main():
                                         offs=offs[:nb_host], lens=lens[:nb_host])
         cb["agrees_with_gpu"] = bool(np.array_equal(cpu_crcs, crcs[:cpu_crcs.size]))
         line["cpu_baseline"] = cb
+        del host
+    if world == 1 and args.config == "cfg2" and not args.no_more_configs:
+        # The metric's other half (64 KiB blocks, cfg3, with its host legs) and the irregular path (cfg4),
+        # timed in this same run exactly as the main line is: warm-up with the clock floor, K steps between
+        # one event pair, every block checked against the golden aggregates. Never `value`.
+        del ctx, step, data, out
+        torch.cuda.empty_cache()
+        more = {}
+        for cfg in ("cfg3", "cfg4"):
+            nb, bl, dsc = CONFIGS[cfg]
+            c = prepare(cfg, 0, nb, dev, ora)
+            o = torch.empty(nb, dtype=torch.int32, device=dev)
+            warm_up(lambda: c["step"](None, o), args.warmup, args.min_warmup_ms)
+            el, kms = time_steps(c["step"], o, stream, args.steps)
+            cr = o.cpu().numpy().view(np.uint32).copy()
+            ok, fl = verify_rank(ora, cfg, 0, cr, bl, None if bl else c["lens"])
+            entry = {"workload": f"{cfg}: {dsc}", "value": round(c["total"] * args.steps / (1 << 30) / el, 2),
+                     "unit": "GiB/s", "ms_per_step": round(el * 1e3 / args.steps, 4),
+                     "roofline": roofline(c["total"], kms, cfg), "bit_exact": ok,
+                     "bit_exact_scope": "every block (golden XOR/SUM32) and the first 64 against the oracle" if fl
+                     else "first 64 blocks against the oracle"}
+            if cfg == "cfg3" and not args.no_e2e:
+                entry["e2e_host"] = host_legs(c, cr)
+            more[cfg] = entry
+            del c, o
+            torch.cuda.empty_cache()
+        line["more_configs"] = more
     if rank == 0:
         print(json.dumps(line), flush=True)
     if use_dist:

@@ -36,9 +36,15 @@ def pytest_collection_finish(session):
     say = tr.write_line if tr is not None else print
     import torch
     import tinykvpp_amd
+    from tinykvpp_amd import build_id
     tinykvpp_amd.load_library()
     libs = _loaded_objects("libtkv_crc32")
     say(f"[tkv] product library loaded: {', '.join(libs) or 'NOT MAPPED'}")
+    lib_id, tree, same = build_id.check()
+    say(f"[tkv] build id: library {lib_id}, tree sources {tree}: {'match' if same else 'MISMATCH'}")
+    if not same:
+        pytest.exit(f"libtkv_crc32.so (build {lib_id}) was not built from this tree's sources ({tree}); rebuild it",
+                    returncode=3)
     if torch.cuda.is_available():
         p = torch.cuda.get_device_properties(0)
         say(f"[tkv] device 0: {p.name}, arch {getattr(p, 'gcnArchName', '?')}, "

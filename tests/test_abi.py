@@ -408,3 +408,49 @@ def test_stream_partition(TR, W):
         if 0 < r <= TR:  # the wave holding row r-1 is the last one starting at or before it
             w = lo - 1
             assert r0[w] <= r - 1 < r0[w + 1]
+
+
+def test_library_build_id_matches_tree(lib):
+    """libtkv_crc32.so carries the hash of the sources it was built from (tinykvpp_amd/build_id.py,
+    baked in by the Makefile); the in-tree library must be this tree's build."""
+    from tinykvpp_amd import build_id
+    lib_id, tree, same = build_id.check()
+    assert len(tree) == 16 and same, f"library {lib_id} vs tree {tree}: rebuild with make -C tinykvpp_amd/csrc"
+
+
+def lane_model(slice_, host, blk, n, init):
+    """The lane kernels' arithmetic (lane_issue / lane_dwords / lane_fold): the 16-byte
+    granules covering the block (clamped to its last granule), two selects by the start's dword offset,
+    v_alignbyte by its byte offset, then slicing-by-4 from the block's own register over the whole
+    dwords and Sarwate steps over the last n % 4 bytes."""
+    al = blk & ~15
+    last = (blk + n - 1) & ~15
+    raw = []
+    for i in range(5):
+        p = al + 16 * i
+        src = p if (n and p < last) else last
+        raw += [int.from_bytes(bytes(host[src + 4 * j:src + 4 * j + 4]), "little") if n else 0 for j in range(4)]
+    o = blk & 15
+    if o & 8:
+        raw = raw[2:] + [0, 0]
+    if o & 4:
+        raw = raw[1:] + [0]
+    t = o & 3
+    d = [((raw[k + 1] << 32 | raw[k]) >> (8 * t)) & 0xFFFFFFFF for k in range(16)]
+    c = init
+    for k in range(n >> 2):
+        x = c ^ d[k]
+        c = int(slice_[3][x & 255] ^ slice_[2][(x >> 8) & 255] ^ slice_[1][(x >> 16) & 255] ^ slice_[0][x >> 24])
+    for j in range(n & 3):
+        c = (c >> 8) ^ int(slice_[0][(c ^ (d[n >> 2] >> (8 * j))) & 255])
+    return c
+
+
+def test_model_lane_blocks(tables, oracle):
+    rng = np.random.default_rng(45)
+    host = rng.integers(0, 256, 4096, dtype=np.uint8)
+    for n in list(range(0, 65)) + [36, 59, 26]:
+        for blk in rng.integers(16, 4096 - 96, 6):
+            init = int(rng.integers(0, 2**32))
+            want = oracle.update(init, host[blk:blk + n].tobytes())
+            assert lane_model(tables[0], host, int(blk), n, init) == want, (n, int(blk))

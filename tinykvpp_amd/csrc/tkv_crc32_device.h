@@ -1293,9 +1293,10 @@ __device__ __forceinline__ void crc_packed_small_body(const RowsArgs& a, std::ui
 // (dword aligned) only the selects.
 constexpr int kLaneGran = 5;  // granules covering 64 bytes at any alignment
 
+// ngr: granules worth loading (a wave-uniform bound; the granules past it are never read).
 template <int ALIGN>
 __device__ __forceinline__ void lane_issue(std::uintptr_t blk, std::uint32_t n, std::uintptr_t dmy,
-                                           uint4 (&g)[kLaneGran]) {
+                                           uint4 (&g)[kLaneGran], std::uint32_t ngr = kLaneGran) {
   constexpr int NG = ALIGN == 16 ? 4 : kLaneGran;
   const std::uintptr_t al = blk & ~static_cast<std::uintptr_t>(15);
   const std::uintptr_t last = (blk + n - 1u) & ~static_cast<std::uintptr_t>(15);  // used when n >= 1
@@ -1303,7 +1304,8 @@ __device__ __forceinline__ void lane_issue(std::uintptr_t blk, std::uint32_t n, 
   for (int i = 0; i < NG; ++i) {
     const std::uintptr_t p = al + 16u * i;
     // past the block's last granule: that granule again (an L1 hit); an empty block reads `dummy`
-    g[i] = gload16(n == 0 ? dmy : (p < last ? p : last));
+    if (static_cast<std::uint32_t>(i) < ngr) g[i] = gload16(n == 0 ? dmy : (p < last ? p : last));
+    else g[i] = make_uint4(0, 0, 0, 0);
   }
 }
 
@@ -1349,23 +1351,42 @@ __device__ __forceinline__ std::uint32_t sarwate_bytes(const std::uint32_t* lds,
 template <int NB, bool UNI>
 __device__ __forceinline__ void lane_fold(const std::uint32_t* lds, const LaneConst& kc, const std::uint32_t (*d)[16],
                                           const std::uint32_t* n, std::uint32_t* r) {
-  std::uint32_t nf[NB], tb[NB];
   Reg p[NB];
 #pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const std::uint32_t len = UNI ? __builtin_amdgcn_readfirstlane(n[0]) : n[i];
-    nf[i] = len >> 2;
-    tb[i] = len & 3u;
-    p[i] = Reg{r[i], 0};
-  }
+  for (int i = 0; i < NB; ++i) p[i] = Reg{r[i], 0};
+  if constexpr (UNI) {
+    // one scalar branch per dword for all NB chains, so their lookups stay interleaved
+    const std::uint32_t len = __builtin_amdgcn_readfirstlane(n[0]);
+    const std::uint32_t nf = len >> 2, tb = len & 3u;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < 16; ++k) {
+      if (static_cast<std::uint32_t>(k) < nf) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) slice4(lds, p[i], d[i][k], kc);
+      } else {
+        if (static_cast<std::uint32_t>(k) == nf && tb != 0u) {
+#pragma unroll
+          for (int i = 0; i < NB; ++i) p[i] = Reg{sarwate_bytes(lds, kc, p[i].value(), d[i][k], tb), 0};
+        }
+        break;
+      }
+    }
+  } else {
+    std::uint32_t nf[NB], tb[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      if (static_cast<std::uint32_t>(k) < nf[i]) {
-        slice4(lds, p[i], d[i][k], kc);
-      } else if (static_cast<std::uint32_t>(k) == nf[i] && tb[i] != 0u) {
-        p[i] = Reg{sarwate_bytes(lds, kc, p[i].value(), d[i][k], tb[i]), 0};
+      nf[i] = n[i] >> 2;
+      tb[i] = n[i] & 3u;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        if (static_cast<std::uint32_t>(k) < nf[i]) {
+          slice4(lds, p[i], d[i][k], kc);
+        } else if (static_cast<std::uint32_t>(k) == nf[i] && tb[i] != 0u) {
+          p[i] = Reg{sarwate_bytes(lds, kc, p[i].value(), d[i][k], tb[i]), 0};
+        }
       }
     }
   }
@@ -1397,6 +1418,8 @@ __device__ __forceinline__ void crc_lanes_body(const RowsArgs& a, std::uint32_t*
   const std::uintptr_t lane_base = base + blk0 * a.stride;
   const std::uint64_t step_bytes = 64u * a.stride;
   const std::uintptr_t last_blk = base + (nb - 1u) * a.stride;  // lanes past the batch reload it, store nothing
+  // granules that can hold a block byte: the start lies at most 0 / 12 / 15 bytes into its granule
+  const std::uint32_t ngr = (len + (ALIGN == 16 ? 0u : ALIGN == 4 ? 12u : 15u) + 15u) / 16u;
 
   uint4 buf[DEPTH][kLaneGran];
   std::uint32_t ini[DEPTH], o16[DEPTH];
@@ -1404,7 +1427,7 @@ __device__ __forceinline__ void crc_lanes_body(const RowsArgs& a, std::uint32_t*
     const std::uint32_t jc = j < ns ? j : ns - 1;  // steps past the range reload the last one
     const std::uint64_t b = blk0 + 64ull * jc;
     const std::uintptr_t blk = b < nb ? lane_base + jc * step_bytes : last_blk;
-    lane_issue<ALIGN>(blk, len, dmy, buf[slot]);
+    lane_issue<ALIGN>(blk, len, dmy, buf[slot], ngr);
     o16[slot] = static_cast<std::uint32_t>(blk & 15u);
     ini[slot] = a.init_raw ? a.init_raw[b < nb ? b : nb - 1u] : a.init_default;
   };
@@ -1446,9 +1469,10 @@ __device__ __forceinline__ void crc_lanes_body(const RowsArgs& a, std::uint32_t*
   }
 }
 
-// Lane blocks of an irregular batch (len <= kLaneMax), walked straight from the caller's offsets and
-// lengths (the prepass lists them nowhere): wave w takes the blocks [w n / W, (w + 1) n / W) 64 at a
-// time, lane l of step j the block b0 + 64 j + l, and folds it if it is a lane block; other lanes idle.
+// Lane blocks of an irregular batch (len <= kLaneMax, in a scan tile the prepass marked dense), walked
+// straight from the caller's offsets and lengths (the prepass lists them nowhere): wave w takes the
+// blocks [w n / W, (w + 1) n / W) 64 at a time, lane l of step j the block b0 + 64 j + l, and folds it
+// if it is such a lane block; other lanes idle.
 // Runs in crc_stream's launch when the prepass chose the general path and counted lane blocks, with
 // the slicing tables already in LDS. Descriptors are fetched four steps ahead of their data, data two
 // steps ahead of the fold, and no loaded value is touched before use (small_phase's pipeline).
@@ -1476,7 +1500,7 @@ __device__ __forceinline__ void lane_phase(const RowsArgs& a, const std::uint32_
   std::uint32_t m_len[RING], m_o[RING], m_init[RING];
   auto issue = [&](int slot, std::uint32_t j) {
     const std::uint64_t b = b0 + 64ull * j + lane;
-    const bool live = j < ns && b < b1 && d_len[slot] <= kLaneMax;
+    const bool live = j < ns && b < b1 && d_len[slot] <= kLaneMax && (a.l_tile[b / 4096u] & kTileLanes);
     const std::uint32_t len = live ? d_len[slot] : 0u;
     const std::uintptr_t blk = base + d_off[slot];
     lane_issue<1>(blk, len, dmy, q[slot]);

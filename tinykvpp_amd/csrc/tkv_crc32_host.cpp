@@ -462,7 +462,10 @@ int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t s
     TKV_HIP(launch_packed(a, static_cast<unsigned>(c->ncu), st));  // whole blocks per wave, no seams
     return TKV_OK;
   }
-  if (static_cast<long long>(len) <= lane_max()) {
+  // (aligned back-to-back 64-byte blocks: crc_packed_small's exact G = 1 kernel is faster, 4477 vs
+  // 4108 GB/s, profiles/r3/lanes/ab_shapes.jsonl)
+  const bool small_exact64 = aligned && !d_init && stride == len && len == 64;
+  if (static_cast<long long>(len) <= lane_max() && !small_exact64) {
     // one lane per block: any stride, alignment and initial registers
     const std::uint64_t steps = (n + 63) / 64;
     const std::uint64_t grid =
@@ -524,6 +527,7 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   a.s_wv = s->po.big_idx;
   a.l_off = d_off;  // the lane phase walks the caller's own arrays
   a.l_len = d_len;
+  a.l_tile = s->tile_ok;
   TKV_HIP(launch_prepass(d_base, d_off, d_len, a.nblocks, s->scan, s->tiles, s->tile_ok, s->counts, sinfo, s->po.big_off,
                          s->po, a.nwaves, static_cast<std::uint32_t>(c->ncu), d_out, row0, st));
   // stream mode: crc_stream walks the rows and crc_rows finishes the block CRCs; general path:

@@ -107,16 +107,22 @@ struct RowsArgs {
   // bytes are in no prepass list; counts[kCountLanes] says how many there are)
   const std::uint64_t* l_off;
   const std::uint32_t* l_len;
+  const std::uint32_t* l_tile;  // per scan tile of 4096 blocks: kTileLanes when its lane blocks are ours
 };
 constexpr std::uint32_t kModeStream = 1;
 // counts[] of an irregular batch: [0] large blocks, [1] small blocks, [2] rows of the large blocks,
-// [3] mode, [4..7] stream-mode info (two u64), [8] lane blocks (len <= kLaneMax)
+// [3] mode, [4..7] stream-mode info (two u64), [8] lane blocks (len <= kLaneMax) of dense tiles
 constexpr int kCountLanes = 8;
 
 // Blocks of at most kLaneMax bytes are folded whole by one lane each, from their own initial register
 // (DESIGN.md §4.5): uniform batches by crc_lanes, irregular ones by the lane phase in crc_stream's
 // launch. The prepass lists them nowhere, and stream mode needs every block to be longer.
 constexpr std::uint32_t kLaneMax = 64;
+// The prepass leaves a scan tile's lane blocks to the lane phase only when the tile holds at least this
+// many (of its 4096); in a sparser tile they are listed as small blocks. Per-tile flags (tile_ok):
+constexpr std::uint32_t kLaneDenseTile = 256;
+constexpr std::uint32_t kTileStream = 1u;  // the tile's blocks qualify for stream mode
+constexpr std::uint32_t kTileLanes = 2u;   // the tile's lane blocks are the lane phase's
 
 // One short host span for crc_span: `len` bytes at byte `pos` (16-byte aligned) of the mapped
 // staging buffer, folded on from raw register `init`.

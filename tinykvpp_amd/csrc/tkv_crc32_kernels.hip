@@ -159,11 +159,15 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small(RowsArgs a) {
 
 // Uniform batches of blocks of at most kLaneMax bytes (any stride, alignment, initial registers): one
 // lane per block. Only the slicing tables go to LDS (128 KiB).
-template <int ALIGN>
+// Pipeline shapes (in-process A/B over 16-64 B blocks, profiles/r3/lanes/ab_shapes.jsonl): aligned
+// blocks DEPTH 4 / ILP 2; unaligned ones of at most 48 bytes DEPTH 3 / ILP 1 (ILP 2 spills there: 26 B
+// 3445 -> 3917 GB/s), longer unaligned ones DEPTH 4 / ILP 2 (59 B 3806 -> 4082 GB/s).
+template <int ALIGN, int DEPTH, int ILP>
 __global__ __launch_bounds__(kThreads) void crc_lanes(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsSliceWords];
-  dev::crc_lanes_body<ALIGN, kPackedDepth, kPackedIlp, kPackedPrio>(a, lds);
+  dev::crc_lanes_body<ALIGN, DEPTH, ILP, kPackedPrio>(a, lds);
 }
+constexpr std::uint32_t kLanesShortMax = 48;
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase
                                                       std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
                                                       std::uint32_t* lscan, std::uint32_t* tile_lanes) {
   __shared__ std::uint64_t wsum[16];
-  __shared__ std::uint32_t lsum[16];
+  __shared__ std::uint32_t lsum[16], lcnt[16];
   // stream mode's wave partition (used only if the prepass picks stream mode): row0[0..Ws], grid-stride
   for (std::uint32_t w = blockIdx.x * 1024u + threadIdx.x; w <= Ws; w += gridDim.x * 1024u) {
     const std::uint64_t TR = stream_geometry(sbase, offsets, lengths, n).rows;
@@ -216,22 +220,37 @@ __global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase
   }
   const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * 4u;
   const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  std::uint64_t v[4], s = 0;
-  std::uint32_t lv[4], ls = 0;  // lane blocks (len <= kLaneMax): in no list, folded by the lane phase
+  std::uint32_t len[4], lv[4];
   bool ok = true;
+  unsigned nlw = 0;  // lane blocks (len <= kLaneMax) of this wave
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const std::uint64_t b = base + i;
-    const std::uint32_t len = b < n ? lengths[b] : 0u;
-    lv[i] = b < n && len <= kLaneMax ? 1u : 0u;
-    v[i] = b < n && !lv[i] ? scan_item(len) : 0ull;
+    len[i] = b < n ? lengths[b] : 0u;
+    lv[i] = b < n && len[i] <= kLaneMax ? 1u : 0u;
+    nlw += static_cast<unsigned>(__popcll(__ballot(lv[i] != 0u)));
+    // (a lane block is shorter than kStreamMinLen: its offsets are never read here)
+    if (b < n) ok = ok && len[i] >= kStreamMinLen && (b + 1 >= n || offsets[b] + len[i] == offsets[b + 1]);
+  }
+  if (lane == 0) lcnt[wid] = nlw;
+  const bool tile_all_ok = __syncthreads_and(ok ? 1 : 0) != 0;
+  // A tile with at least kLaneDenseTile lane blocks leaves them to the lane phase (in no list); in a
+  // sparser tile they are listed as small blocks, so a batch with a few of them scattered about pays no
+  // lane-phase walk over its metadata.
+  std::uint32_t nlt = 0;
+#pragma unroll
+  for (unsigned w = 0; w < 16; ++w) nlt += lcnt[w];
+  const bool dense = nlt >= kLaneDenseTile;
+  if (threadIdx.x == 0) tile_ok[blockIdx.x] = (tile_all_ok ? kTileStream : 0u) | (dense ? kTileLanes : 0u);
+  std::uint64_t v[4], s = 0;
+  std::uint32_t ls = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    lv[i] = dense ? lv[i] : 0u;
+    v[i] = base + i < n && !lv[i] ? scan_item(len[i]) : 0ull;
     s += v[i];
     ls += lv[i];
-    // (a lane block is shorter than kStreamMinLen: its offsets are never read here)
-    if (b < n) ok = ok && len >= kStreamMinLen && (b + 1 >= n || offsets[b] + len == offsets[b + 1]);
   }
-  const bool tile_all_ok = __syncthreads_and(ok ? 1 : 0) != 0;
-  if (threadIdx.x == 0) tile_ok[blockIdx.x] = tile_all_ok ? 1u : 0u;
   // Inclusive scans of the thread sums inside the wave (cross-lane shifts, no barriers), then the
   // 16 wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
   std::uint64_t inc = s;
@@ -317,13 +336,14 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
 }
 
 // Scatter of one block (rows_finish): e = its exclusive (small count, rows) pair, nlane = lane blocks
-// in front of it, TR = rows of all large blocks. A large block cut between row-kernel waves gets its
+// in front of it that the lane phase folds, dense = its tile's lane blocks are the lane phase's,
+// TR = rows of all large blocks. A large block cut between row-kernel waves gets its
 // result zeroed here, since the row kernel XORs every piece of it into the result (crc_rows_body,
 // irregular batches). len and off are the block's length and offset (loaded by the caller).
 __device__ __forceinline__ void finish_block(std::uint64_t off, std::uint32_t len, std::uint64_t b, std::uint64_t e,
                                              std::uint64_t nlane, std::uint64_t TR, const PrepassOut& o,
-                                             std::uint32_t W, std::uint32_t* out) {
-  if (len <= kLaneMax) return;  // the lane phase's
+                                             std::uint32_t W, std::uint32_t* out, bool dense) {
+  if (len <= kLaneMax && dense) return;  // the lane phase's (a lane block of a sparse tile is small)
   const std::uint32_t nsmall = static_cast<std::uint32_t>(e);
   if (len <= kSmallMax) {
     o.s_off[nsmall] = off;
@@ -348,13 +368,15 @@ __device__ __forceinline__ void finish_block(std::uint64_t off, std::uint32_t le
 
 __global__ void rows_finish(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
                             const std::uint64_t* scan, const std::uint64_t* tile_offs, const std::uint32_t* counts,
-                            PrepassOut o, std::uint32_t W, std::uint32_t* out) {
+                            const std::uint32_t* tile_ok, PrepassOut o, std::uint32_t W, std::uint32_t* out) {
   const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
   if (b >= n) return;
   const std::uint32_t len = lengths[b];
-  if (len <= kLaneMax) return;  // the lane phase's
   const std::uint64_t t = b / kScanTile;
-  finish_block(offsets[b], len, b, scan[b] + tile_offs[t], o.lscan[b] + o.tile_lanes[t], counts[2], o, W, out);
+  const bool dense = (tile_ok[t] & kTileLanes) != 0;
+  if (len <= kLaneMax && dense) return;  // the lane phase's
+  finish_block(offsets[b], len, b, scan[b] + tile_offs[t], o.lscan[b] + o.tile_lanes[t], counts[2], o, W, out,
+               dense);
 }
 
 // rows_finish with the scan of the tile sums folded in (ntiles <= kFusedTiles): every workgroup sums
@@ -407,6 +429,7 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
   const std::uint64_t off = live ? offsets[b] : 0ull;
   const std::uint64_t sc = live ? scan[b] : 0ull;
   const std::uint32_t lsc = live ? o.lscan[b] : 0u;
+  const bool dense = (tile_ok[my_tile] & kTileLanes) != 0;
   std::uint64_t before = 0, all = 0, bad = 0, lbefore = 0, lall = 0;
   for (std::uint32_t i = threadIdx.x; i < ntiles; i += kFinishThreads) {
     const std::uint64_t v = tile_sums[i];
@@ -415,7 +438,7 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     before += i < my_tile ? v : 0ull;
     lall += lv;
     lbefore += i < my_tile ? lv : 0ull;
-    bad += tile_ok[i] ? 0u : 1u;
+    bad += (tile_ok[i] & kTileStream) ? 0u : 1u;
   }
   // Wave sums by cross-lane exchange, then the kWaves partial sums through LDS (one barrier).
 #pragma unroll
@@ -457,7 +480,7 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     counts[kCountLanes] = nl;                              // lane blocks (crc_stream's lane phase)
   }
   if (!live) return;
-  finish_block(off, len, b, sc + tile_off, lsc + tile_loff, total >> 32, o, W, out);
+  finish_block(off, len, b, sc + tile_off, lsc + tile_loff, total >> 32, o, W, out, dense);
 }
 
 
@@ -648,9 +671,12 @@ hipError_t launch_packed_small(const RowsArgs& a, unsigned grid, hipStream_t st)
 hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st) {
   if (a.len > kLaneMax) return hipErrorInvalidValue;
   const std::uintptr_t m = reinterpret_cast<std::uintptr_t>(a.base) | static_cast<std::uintptr_t>(a.stride);
-  if ((m & 15u) == 0) hipLaunchKernelGGL(crc_lanes<16>, dim3(grid), dim3(kThreads), 0, st, a);
-  else if ((m & 3u) == 0) hipLaunchKernelGGL(crc_lanes<4>, dim3(grid), dim3(kThreads), 0, st, a);
-  else hipLaunchKernelGGL(crc_lanes<1>, dim3(grid), dim3(kThreads), 0, st, a);
+  const bool shrt = a.len <= kLanesShortMax;
+  if ((m & 15u) == 0) hipLaunchKernelGGL((crc_lanes<16, 4, 2>), dim3(grid), dim3(kThreads), 0, st, a);
+  else if ((m & 3u) == 0 && shrt) hipLaunchKernelGGL((crc_lanes<4, 3, 1>), dim3(grid), dim3(kThreads), 0, st, a);
+  else if ((m & 3u) == 0) hipLaunchKernelGGL((crc_lanes<4, 4, 2>), dim3(grid), dim3(kThreads), 0, st, a);
+  else if (shrt) hipLaunchKernelGGL((crc_lanes<1, 3, 1>), dim3(grid), dim3(kThreads), 0, st, a);
+  else hipLaunchKernelGGL((crc_lanes<1, 4, 2>), dim3(grid), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 
@@ -680,7 +706,7 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
     hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, o.tile_lanes,
                        static_cast<std::uint32_t>(ntiles), n, counts);
     hipLaunchKernelGGL(rows_finish, dim3(static_cast<unsigned>(nfinish)), dim3(256), 0, st, offsets, lengths, n, scan,
-                       tile_sums, counts, o, W, out);
+                       tile_sums, counts, tile_ok, o, W, out);
   }
   return hipGetLastError();
 }

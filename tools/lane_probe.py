@@ -69,7 +69,7 @@ def main():
         return total // pitch
 
     work = []
-    for L in (26, 28, 33, 36, 59, 64):
+    for L in (16, 26, 28, 32, 33, 36, 48, 59, 64):
         work.append(uniform(L))
     work.append(uniform(36, 44, 8))   # WAL payload pitch: 8-byte header in front of every 36-byte payload
     work.append(uniform(36, 36, 3))   # odd base
