@@ -6,15 +6,19 @@
 // [[nodiscard]] uint32_t finalize() const noexcept and void reset() noexcept — so wal.cpp's
 // `core::crc32{}.update({...}).finalize()` (wal.cpp:54-57, 89-92) and test/crc32_test.cpp compile
 // unchanged. update() forwards to the C ABI (tkv_crc32_update, include/tkv_crc32.h), which runs the
-// gfx950 HIP kernel. The reference's update is noexcept with no error path, so a device failure is
-// reported on stderr and aborts (a wrong checksum would be worse than a crash for an integrity
-// routine).
+// gfx950 HIP kernel, except for short spans (below).
 //
-// Opt-in host path for short spans: compile with -DTKV_DROPIN_HOST_MAX=N and spans of at most N
-// bytes go to tkv_crc32_update_host (slicing-by-8 on the calling core, no device involved) instead
-// of a GPU round trip: the reference's per-put record stamp (wal.cpp:54-57) then costs what it
-// costs in the reference (INTEGRATION.md §1 has the numbers). The default, 0, keeps every span on
-// the GPU. Spans above N still abort on a device failure; nothing falls back to the host.
+// Short spans run on the calling core: spans of at most TKV_DROPIN_HOST_MAX bytes (default 65536) go
+// to tkv_crc32_update_host (slicing-by-8 over tables built from the polynomial, product code with its
+// own parity tests; not the oracle). That is the measured crossover of one call
+// (profiles/r3/put_latency.jsonl): up to 64 KiB the host path is faster (36 B: 0.011 us against the
+// reference's 0.040 us and 11 us for a GPU round trip; 64 KiB: 23 us against 31 us), from 128 KiB the
+// GPU is (35 us against 46 us). So the reference's per-put record stamp (wal.cpp:54-57) costs less
+// than in the reference, and its contract holds: update is noexcept and cannot fail, with or without
+// a device. Longer spans go to the GPU; the reference's update has no error path, so a device failure
+// there is reported on stderr and aborts (a wrong checksum would be worse than a crash for an
+// integrity routine). -DTKV_DROPIN_HOST_MAX=0 sends every span to the GPU. tkv_debug_update_counts
+// says which path the calling thread's calls took.
 //
 // Build: add include/ to the include path and link libtkv_crc32.so.
 #pragma once
@@ -29,7 +33,7 @@
 #include "tkv_crc32.h"
 
 #ifndef TKV_DROPIN_HOST_MAX
-#define TKV_DROPIN_HOST_MAX 0
+#define TKV_DROPIN_HOST_MAX 65536
 #endif
 
 namespace frankie::core {
@@ -79,7 +83,7 @@ class crc32 final {
 
  private:
   static constexpr const auto TABLE{generate_crc32_table()};  // crc32.hpp:46 (kept for layout parity)
-  // Spans up to this many bytes take the host path (TKV_DROPIN_HOST_MAX; 0 = none).
+  // Spans up to this many bytes take the host path (TKV_DROPIN_HOST_MAX; 0 = none, every span on the GPU).
   static constexpr std::size_t kHostSpanMax{TKV_DROPIN_HOST_MAX};
 
   std::uint32_t crc_{kCRC32DefaultValue};

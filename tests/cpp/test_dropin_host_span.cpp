@@ -1,7 +1,12 @@
-// The drop-in header with the opt-in host path for short spans (built with -DTKV_DROPIN_HOST_MAX,
-// by tests/test_host_span.py): the reference's crc32_test.cpp known answers (:81-124) and
-// wal_entry::encode's record CRC (wal.cpp:54-57, tests/golden/wal.json) through
-// frankie::core::crc32, every span at or below the threshold, so no GPU is touched.
+// The drop-in header as a maintainer gets it (default TKV_DROPIN_HOST_MAX = 64 KiB, built by
+// tests/test_host_span.py with no -D flag): the reference's crc32_test.cpp known answers (:81-124)
+// and wal_entry::encode's record CRC (wal.cpp:54-57, tests/golden/wal.json) through
+// frankie::core::crc32, every length up to the threshold, and the reference's contract: update never
+// fails and touches no GPU for these spans (this runs on a machine without one; the per-thread
+// counters of tkv_debug_update_counts show every call on the host path). It also times a 36-byte put
+// (wal_entry::encode's {put, 42, "hello", "world"}) against the reference's byte loop
+// (crc32.cpp:9-16, restated inline) on the same core.
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -11,8 +16,8 @@
 
 #include "frankie_crc32.hpp"
 
-#if TKV_DROPIN_HOST_MAX < 64
-#error "build with -DTKV_DROPIN_HOST_MAX=N, N >= 64"
+#if TKV_DROPIN_HOST_MAX < 65536
+#error "this test checks the default threshold (64 KiB)"
 #endif
 
 using namespace frankie::core;
@@ -69,12 +74,39 @@ void wal_record_crc() {
   CHECK_EQ(crc, 0x593B861Au);  // tests/golden/wal.json (the reference's crc32 over the same bytes)
 }
 
+// A 36-byte put through the default header against the reference's byte loop, same bytes, same core.
+void put_cost() {
+  constexpr auto T = generate_crc32_table();
+  std::vector<std::byte> rec(36 + 256);
+  for (std::size_t i = 0; i < rec.size(); ++i) rec[i] = static_cast<std::byte>((i * 40503u) >> 3);
+  using clk = std::chrono::steady_clock;
+  constexpr int reps = 2000000;
+  std::uint32_t sink = 0;
+  auto t0 = clk::now();
+  for (int i = 0; i < reps; ++i) sink ^= crc32{}.update({rec.data() + (i & 255), 36}).finalize();
+  const double ours = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / reps;
+  t0 = clk::now();
+  for (int i = 0; i < reps; ++i) {
+    std::uint32_t r = 0xFFFFFFFFu;  // crc32.cpp:9-16, one byte per step
+    const std::byte* p = rec.data() + (i & 255);
+    for (std::size_t k = 0; k < 36; ++k) r = (r >> 8) ^ T[(r ^ static_cast<std::uint32_t>(p[k])) & 0xFFu];
+    sink ^= r ^ 0xFFFFFFFFu;
+  }
+  const double ref = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / reps;
+  std::printf("put_cost_36B: drop-in %.4f us, reference byte loop %.4f us (sink %u)\n", ours, ref, sink & 1u);
+  if (!(ours <= ref)) {
+    std::fprintf(stderr, "a 36-byte put through the drop-in (%.4f us) is slower than the reference loop (%.4f us)\n",
+                 ours, ref);
+    ++g_fail;
+  }
+}
+
 // Every length up to the threshold against the byte-at-a-time definition (crc32.cpp:9-16).
 void all_lengths() {
   constexpr auto T = generate_crc32_table();
   std::vector<std::byte> d(TKV_DROPIN_HOST_MAX);
   for (std::size_t i = 0; i < d.size(); ++i) d[i] = static_cast<std::byte>((i * 2654435761u) >> 11);
-  for (std::size_t n = 0; n <= d.size(); n += (n < 130 ? 1 : 61)) {
+  for (std::size_t n = 0; n <= d.size(); n += (n < 130 ? 1 : 611)) {
     std::uint32_t r = 0xFFFFFFFFu;
     for (std::size_t i = 0; i < n; ++i) r = (r >> 8) ^ T[(r ^ static_cast<std::uint32_t>(d[i])) & 0xFFu];
     CHECK_EQ(crc32{}.update({d.data(), n}).finalize(), r ^ 0xFFFFFFFFu);
@@ -83,10 +115,23 @@ void all_lengths() {
 }  // namespace
 
 int main() {
+  std::uint64_t c0[2], c1[2];
+  tkv_debug_update_counts(c0);
   known_values();
   incremental_equals_single();
   wal_record_crc();
   all_lengths();
+  {  // the threshold itself: a 64 KiB span is still a host span
+    std::vector<std::byte> big(TKV_DROPIN_HOST_MAX, std::byte{7});
+    (void)crc32{}.update({big.data(), big.size()}).finalize();
+  }
+  tkv_debug_update_counts(c1);
+  CHECK_EQ(c1[1] - c0[1], 0u);   // no call took the GPU path
+  if (c1[0] - c0[0] < 200) {      // every update above was a host span
+    std::fprintf(stderr, "only %llu host span calls counted\n", (unsigned long long)(c1[0] - c0[0]));
+    ++g_fail;
+  }
+  put_cost();
   std::printf("%s\n", g_fail ? "FAILED" : "ALL PASSED");
   return g_fail ? 1 : 0;
 }

@@ -84,6 +84,26 @@ def test_batch_on_side_stream(gpu, oracle):
     assert np.array_equal(u32(out), want) and np.array_equal(u32(out2), want)
 
 
+def test_batch_on_side_stream_orders_itself(gpu, oracle):
+    """No caller-side wait_stream: the batch entry points order the side stream after the current
+    stream's prior work themselves, so bytes written there just before (and an `out` block the
+    caching allocator reuses) are seen by the kernels on the side stream."""
+    s = torch.cuda.Stream(device=gpu)
+    n, blen = 2000, 4096
+    base = torch.arange(n * blen // 8, dtype=torch.int64, device=gpu)
+    for k in range(3):
+        data = ((base * (2 * k + 3)) ^ (base >> 5)).view(torch.uint8)  # written on the current stream
+        out = tk.crc32_batch_uniform(data, blen, n, stream=s)
+        offs = torch.arange(n, dtype=torch.int64, device=gpu) * blen + 1
+        lens = torch.full((n,), blen - 1, dtype=torch.int32, device=gpu)
+        out2 = tk.crc32_batch(data, offs, lens, stream=s)
+        s.synchronize()
+        host = data.cpu().numpy()
+        assert np.array_equal(u32(out), oracle.batch(host, np.arange(n) * blen, np.full(n, blen))), k
+        assert np.array_equal(u32(out2), oracle.batch(host, offs.cpu().numpy(), lens.cpu().numpy())), k
+        del out, out2  # freed blocks go back to the pool for the next round's allocations
+
+
 def test_batch_argument_checks(gpu):
     data = torch.zeros(1 << 16, dtype=torch.uint8, device=gpu)
     offs = torch.zeros(4, dtype=torch.int64, device=gpu)

@@ -40,6 +40,17 @@ def _stream_ptr(stream):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+def _launch_stream(stream, device):
+    """The stream a batch launches on, ordered after the current stream's prior work: the inputs were
+    written there, and the caching allocator may hand out an `out` block whose previous owner's
+    kernels are still queued there (record_stream only guards the later free)."""
+    import torch
+    cur = torch.cuda.current_stream(device)
+    if stream is not None and stream != cur:
+        stream.wait_stream(cur)
+    return ctypes.c_void_p((stream if stream is not None else cur).cuda_stream)
+
+
 def _host_view(data):
     """(pointer, nbytes, keepalive) for a bytes-like or numpy host buffer."""
     if isinstance(data, np.ndarray):
@@ -82,6 +93,7 @@ class crc32:  # noqa: N801 - reference class name (crc32.hpp:32)
         except ImportError:  # pragma: no cover - torch is part of the image
             is_dev = False
         if is_dev:
+            _check_data(data)  # the library launches on the current device: the tensor must be there
             cur = torch.cuda.current_stream(data.device)
             t = data.contiguous().view(torch.uint8)  # any copy runs on the current stream
             out = torch.empty(1, dtype=torch.int32, device=t.device)
@@ -179,7 +191,7 @@ def crc32_batch(data, offsets, lengths, init_raw=None, out=None, stream=None, al
     check(_fn(algo, "batch_device")(
         ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
         ctypes.c_void_p(lengths.data_ptr()), initp, ctypes.c_void_p(out.data_ptr()), n,
-        _stream_ptr(stream)))
+        _launch_stream(stream, data.device)))
     return out
 
 
@@ -197,7 +209,7 @@ def crc32_batch_uniform(data, length, n, stride=None, init_raw=None, out=None, s
     initp = ctypes.c_void_p(init_raw.data_ptr()) if init_raw is not None else None
     check(_fn(algo, "batch_uniform_device")(
         ctypes.c_void_p(data.data_ptr() + offset), stride, length, initp,
-        ctypes.c_void_p(out.data_ptr()), n, _stream_ptr(stream)))
+        ctypes.c_void_p(out.data_ptr()), n, _launch_stream(stream, data.device)))
     return out
 
 

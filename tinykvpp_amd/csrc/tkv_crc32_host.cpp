@@ -945,8 +945,11 @@ int span_batch(DevCtx* c, int algo, const uint8_t* h_base, const uint64_t* h_off
   return run_spans(c, algo, c->h_desc[0], static_cast<std::uint32_t>(n), kInit, h_out_final);
 }
 
+extern thread_local std::uint64_t g_update_calls[2];  // tkv_crc32_span.cpp
+
 int update_impl(int algo, uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
   if (!ptr_ok(out_raw) || (len && !ptr_ok(data))) return fail(TKV_INVALID_ARGUMENT, "null pointer");
+  ++g_update_calls[1];
   DevCtx* c = nullptr;
   if (int rc = get_ctx(&c)) return rc;
   std::lock_guard<std::mutex> lk(c->upd_mu);

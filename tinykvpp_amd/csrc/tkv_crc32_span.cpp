@@ -1,18 +1,24 @@
-// Host latency path for one short span (opt-in).
+// Host latency path for one short span.
 //
 // tinykvpp's only live caller checksums one ~36-byte WAL record per put (wal_entry::encode,
 // /root/reference/src/engine/wal.cpp:54-57). Through the GPU every such call is a launch and a
 // round trip (~20 us); on the host core that already holds the record it is a few table lookups.
 // This file is that host path: slicing-by-8 over tables built from the polynomial, the same
 // register semantics as crc32::update (crc32.cpp:9-16: no init or xorout applied here). Nothing in
-// the library calls it; the drop-in header uses it only for spans up to TKV_DROPIN_HOST_MAX bytes
-// when the integrator defines that macro (default 0: every span goes to the GPU), and the C ABI
-// exposes it as the separately named tkv_crc32[c]_update_host. It is not a fallback: the GPU entry
-// points never route here, with or without a device.
+// the library calls it; the drop-in header uses it for spans up to TKV_DROPIN_HOST_MAX bytes
+// (default 64 KiB, the measured crossover with the GPU round trip), and the C ABI exposes it as the
+// separately named tkv_crc32[c]_update_host. It is not a fallback: the GPU entry points never route
+// here, with or without a device. Each call is counted per thread (tkv_debug_update_counts).
 #include <cstdint>
 #include <cstring>
 
 #include "tkv_crc32.h"
+
+namespace tkv {
+// Calls of this thread: [0] host span path (this file), [1] GPU update path (tkv_crc32_host.cpp).
+// Thread-local plain counters: an atomic add would cost a third of a 36-byte span.
+thread_local std::uint64_t g_update_calls[2] = {0, 0};
+}  // namespace tkv
 
 namespace {
 
@@ -52,6 +58,7 @@ std::uint32_t span_update(const SpanTables& T, std::uint32_t r, const unsigned c
 
 int update_host(std::uint32_t poly, std::uint32_t raw, const void* data, std::size_t len, std::uint32_t* out_raw) {
   if (out_raw == nullptr || (data == nullptr && len != 0)) return TKV_INVALID_ARGUMENT;
+  ++tkv::g_update_calls[0];
   *out_raw = len ? span_update(tables(poly), raw, static_cast<const unsigned char*>(data), len) : raw;
   return TKV_OK;
 }
@@ -66,6 +73,11 @@ int tkv_crc32_update_host(uint32_t raw_state, const void* data, size_t len, uint
 
 int tkv_crc32c_update_host(uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
   return update_host(0x82F63B78u, raw_state, data, len, out_raw);
+}
+
+void tkv_debug_update_counts(uint64_t out[2]) {
+  out[0] = tkv::g_update_calls[0];
+  out[1] = tkv::g_update_calls[1];
 }
 
 }  // extern "C"

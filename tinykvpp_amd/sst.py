@@ -81,7 +81,7 @@ def block_crcs_device(file, offsets, sizes, store=False, out=None, stream=None):
     """Device-resident images (torch uint8 CUDA tensor, int64 offsets, int32 sizes): the stamp value
     of every image (its CRC with the field read as zero); store=True also writes it into the field."""
     import torch
-    from .crc32 import _check_data, _check_vec, _out_vec, _stream_ptr
+    from .crc32 import _check_data, _check_vec, _launch_stream, _out_vec
     n = offsets.numel()
     if sizes.numel() != n:
         raise ValueError("offsets and sizes differ in length")
@@ -93,7 +93,7 @@ def block_crcs_device(file, offsets, sizes, store=False, out=None, stream=None):
     out = _out_vec(out, n, file.device, stream)
     check(load_library().tkv_sst_block_crcs_device(
         ctypes.c_void_p(file.data_ptr()), ctypes.c_void_p(offsets.data_ptr()), ctypes.c_void_p(sizes.data_ptr()),
-        ctypes.c_void_p(out.data_ptr()), n, int(bool(store)), _stream_ptr(stream)))
+        ctypes.c_void_p(out.data_ptr()), n, int(bool(store)), _launch_stream(stream, file.device)))
     return out
 
 

@@ -76,10 +76,12 @@ def verify_device(image, size=None, stream=None):
     n = image.numel() if size is None else int(size)
     if n > image.numel():
         raise ValueError("size exceeds the tensor")
-    st = torch.cuda.current_stream(image.device) if stream is None else stream
+    from .crc32 import _check_data, _launch_stream
+    _check_data(image)  # the library's WAL scratch and tables are the current device's
+    st = _launch_stream(stream, image.device)
     good, stop = ctypes.c_uint64(0), ctypes.c_uint64(0)
     rc = load_library().tkv_wal_verify_device(ctypes.c_void_p(image.data_ptr()), n, ctypes.byref(good),
-                                              ctypes.byref(stop), ctypes.c_void_p(st.cuda_stream))
+                                              ctypes.byref(stop), st)
     if rc not in (OK, CORRUPTED):
         check(rc)
     return ("ok" if rc == OK else "corrupted"), good.value, stop.value

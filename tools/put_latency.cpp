@@ -6,6 +6,7 @@
 // Build: make -C tools put_latency (needs oracle/_ref built from /root/reference).
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -28,35 +29,47 @@ int main(int argc, char** argv) {
   auto ref_crc32 = reinterpret_cast<ref_fn>(dlsym(h, "ref_crc32"));
   if (!ref_crc32 || tkv_set_device(0) != TKV_OK) return 1;
   std::mt19937_64 rng(1);
-  std::vector<unsigned char> buf(1 << 20);
+  std::vector<unsigned char> buf((2 << 20) + 256);
   for (auto& b : buf) b = static_cast<unsigned char>(rng());
-  for (std::size_t n : {28ul, 36ul, 128ul, 1024ul, 4096ul}) {
+  auto us_per = [](auto&& fn, int reps) {
+    auto t0 = clk::now();
+    for (int i = 0; i < reps; ++i) fn(i);
+    return std::chrono::duration<double, std::micro>(clk::now() - t0).count() / reps;
+  };
+  for (std::size_t n : {28ul, 36ul, 128ul, 1024ul, 4096ul, 16384ul, 65536ul, 131072ul, 262144ul, 1048576ul, 2097152ul}) {
     const auto* p = reinterpret_cast<const std::byte*>(buf.data());
     std::uint32_t sink = 0;
-    for (int i = 0; i < 50; ++i) sink ^= frankie::core::crc32{}.update({p, n}).finalize();
-    const int reps = 2000;
-    auto t0 = clk::now();
-    for (int i = 0; i < reps; ++i) sink ^= frankie::core::crc32{}.update({p + (i & 255), n}).finalize();
-    const double gpu_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / reps;
-    t0 = clk::now();
-    const int rreps = 200000;
-    for (int i = 0; i < rreps; ++i) sink ^= ref_crc32(buf.data() + (i & 255), n);
-    const double ref_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / rreps;
-    // the opt-in host span path (what the drop-in runs for spans <= TKV_DROPIN_HOST_MAX)
-    t0 = clk::now();
-    for (int i = 0; i < rreps; ++i) {
+    // the GPU path itself (C ABI tkv_crc32_update), whatever the drop-in's threshold
+    auto gpu = [&](int i) {
+      std::uint32_t r = 0;
+      (void)tkv_crc32_update(0xFFFFFFFFu, buf.data() + (i & 255), n, &r);
+      sink ^= r;
+    };
+    for (int i = 0; i < 20; ++i) gpu(i);
+    const int greps = n <= 16384 ? 2000 : 300;
+    const double gpu_us = us_per(gpu, greps);
+    const int rreps = static_cast<int>(std::max<std::size_t>(50, (std::size_t(200) << 20) / (n + 64)));
+    const double ref_us = us_per([&](int i) { sink ^= ref_crc32(buf.data() + (i & 255), n); }, rreps);
+    // the host span path (what the drop-in runs for spans <= TKV_DROPIN_HOST_MAX)
+    const double host_us = us_per([&](int i) {
       std::uint32_t r = 0;
       (void)tkv_crc32_update_host(0xFFFFFFFFu, buf.data() + (i & 255), n, &r);
       sink ^= r;
-    }
-    const double host_us = std::chrono::duration<double, std::micro>(clk::now() - t0).count() / rreps;
-    std::uint32_t hr = 0;
+    }, rreps);
+    // the drop-in header as built (default threshold)
+    const double dropin_us = us_per([&](int i) { sink ^= frankie::core::crc32{}.update({p + (i & 255), n}).finalize(); },
+                                    n <= TKV_DROPIN_HOST_MAX ? rreps : greps);
+    std::uint32_t hr = 0, gr = 0;
     (void)tkv_crc32_update_host(0xFFFFFFFFu, buf.data(), n, &hr);
-    const bool same = frankie::core::crc32{}.update({p, n}).finalize() == ref_crc32(buf.data(), n) &&
-                      (hr ^ 0xFFFFFFFFu) == ref_crc32(buf.data(), n);
-    std::printf("{\"row\": \"drop_in_update\", \"bytes\": %zu, \"gpu_us_per_call\": %.2f, \"host_span_us_per_call\": %.3f, "
-                "\"reference_cpu_us_per_call\": %.3f, \"bit_exact\": %s, \"sink\": %u}\n", n, gpu_us, host_us, ref_us,
+    (void)tkv_crc32_update(0xFFFFFFFFu, buf.data(), n, &gr);
+    const std::uint32_t want = ref_crc32(buf.data(), n);
+    const bool same = frankie::core::crc32{}.update({p, n}).finalize() == want && (hr ^ 0xFFFFFFFFu) == want &&
+                      (gr ^ 0xFFFFFFFFu) == want;
+    std::printf("{\"row\": \"drop_in_update\", \"bytes\": %zu, \"gpu_us_per_call\": %.3f, \"host_span_us_per_call\": %.3f, "
+                "\"drop_in_default_us_per_call\": %.3f, \"drop_in_host_max\": %d, \"reference_cpu_us_per_call\": %.3f, "
+                "\"bit_exact\": %s, \"sink\": %u}\n", n, gpu_us, host_us, dropin_us, TKV_DROPIN_HOST_MAX, ref_us,
                 same ? "true" : "false", sink & 1u);
+    std::fflush(stdout);
   }
   // group commit: N records of 36 bytes stamped in one call (wal.cpp:54-58 per record)
   for (std::size_t nrec : {1ul, 16ul, 256ul, 4096ul}) {
