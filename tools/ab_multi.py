@@ -56,7 +56,7 @@ def main():
     dz_g = torch.from_numpy((lens - 1).astype(np.int32)).to("cuda")  # 1-byte gaps: the general walk
     d64_o = torch.arange(n64, dtype=torch.int64, device="cuda") * 65536
     d64_l = torch.full((n64,), 65536, dtype=torch.int32, device="cuda")
-    outs = [torch.empty(1 << 17, dtype=torch.int32, device="cuda") for _ in libs]
+    outs = [torch.empty(1 << 20, dtype=torch.int32, device="cuda") for _ in libs]
 
     def fill_uniform():
         libs[0].tkv_fill_synthetic_uniform(D, 65536, 65536, 0, n64, 1, sp)
@@ -64,7 +64,14 @@ def main():
     def fill_zipf():
         libs[0].tkv_fill_synthetic_blocks(D, VP(dz_o.data_ptr()), VP(dz_l.data_ptr()), 0, lens.size, 1, sp)
 
+    n4k = 1 << 20
+
+    def fill_4k():
+        libs[0].tkv_fill_synthetic_uniform(D, 4096, 4096, 0, n4k, 1, sp)
+
     work = [
+        ("packed 1M x 4 KiB (cfg2)", fill_4k, n4k * 4096, n4k,
+         lambda lib, o: lib.tkv_crc32_batch_uniform_device(D, 4096, 4096, None, o, n4k, sp)),
         ("packed 64K x 64 KiB", fill_uniform, n64 * 65536, n64,
          lambda lib, o: lib.tkv_crc32_batch_uniform_device(D, 65536, 65536, None, o, n64, sp)),
         ("stream 64K x 64 KiB", fill_uniform, n64 * 65536, n64,
