@@ -725,10 +725,7 @@ __device__ __forceinline__ void crc_stream_body(const RowsArgs& a, std::uint32_t
   const std::uint32_t g0 = sload32(a.s_row0, wave);
   const std::uint32_t g1 = sload32(a.s_row0, wave + 1);
   if (g0 >= g1) {
-    if (lane == 0) {
-      a.s_wtot[wave] = 0u;
-      a.s_span[wave] = 0xFFFFFFFFu;
-    }
+    if (lane == 0) a.s_wtot[wave] = 0u;
     return;
   }
   const std::uint32_t n = a.nblocks;
@@ -741,7 +738,6 @@ __device__ __forceinline__ void crc_stream_body(const RowsArgs& a, std::uint32_t
 
   // block ends, 64 at a time: lane i of `win` holds E[bw + i]
   std::uint32_t b = sload32(a.wave_start, wave);  // first block ending in or after row g0
-  const std::uint32_t bfirst = b;
   std::uint32_t bw = b;
   auto load_win = [&](std::uint32_t from) -> std::uint64_t {
     const std::uint32_t i = from + lane;
@@ -996,43 +992,6 @@ __device__ __forceinline__ void crc_stream_body(const RowsArgs& a, std::uint32_t
   }
   flush();
   if (lane == 0) a.s_wtot[wave] = B;
-
-  // Finish here every block whose start lies in this wave's bytes (its end does too: the walk met it).
-  // With L(e) = crc_0 of this wave's bytes up to e, such a block's crc_0 is L(end) ^ Shift_len(L(start))
-  // (L = 0 at the wave's first byte and at the stream start). The block that starts in an earlier wave
-  // and ends here, if any, needs the earlier waves' totals: crc_rows finishes it (s_span[wave]).
-  const std::uint64_t wstart = static_cast<std::uint64_t>(g0) * kRow;
-  const std::uint64_t s0 = s0rel;
-  std::uint32_t span = 0xFFFFFFFFu;
-  if (bfirst < b) {
-    const std::uint64_t ep0 = bfirst ? sload64(a.s_ends, bfirst - 1) : s0;
-    if (ep0 < wstart) span = bfirst;
-  }
-  if (lane == 0) a.s_span[wave] = span;
-  const std::uint32_t blo = span == 0xFFFFFFFFu ? bfirst : bfirst + 1;
-  if (blo < b) {
-    // this wave's own (Y, Q) stores, read back by other lanes of the wave
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const DeviceTables* t = a.tabs;
-    const std::uint32_t poly = t->poly;
-    auto L = [&](std::uint64_t e, std::uint64_t yq) -> std::uint32_t {
-      const std::uint64_t rowend = ((e - 1) / kRow + 1) * kRow;
-      return multmodp(t->inv_shift[rowend - e], static_cast<std::uint32_t>(yq), poly) ^
-             static_cast<std::uint32_t>(yq >> 32);
-    };
-    for (std::uint32_t bb = blo + lane; bb < b; bb += 64u) {
-      const std::uint64_t e = a.s_ends[bb];
-      const std::uint64_t ep = bb ? a.s_ends[bb - 1] : s0;
-      const std::uint32_t le = L(e, a.s_yq[bb]);
-      const std::uint32_t lp = (bb == 0 || ep == wstart) ? 0u : L(ep, a.s_yq[bb - 1]);
-      const std::uint64_t len = e - ep;  // < 2^32
-      const std::uint32_t x8 = multmodp(shift_rows_tab(t, 0x80000000u, static_cast<std::uint32_t>(len >> 12)),
-                                        t->head_shift[len & 4095u][31], poly);  // x^(8 len)
-      const std::uint32_t init = a.init_raw ? a.init_raw[bb] : a.init_default;
-      a.out[bb] = (multmodp(x8, init ^ lp, poly) ^ le) ^ a.out_xor;
-    }
-  }
 }
 
 // Packed uniform fast path: block b = [base + b*len, +len) with len a multiple of kRow (4 KiB) and

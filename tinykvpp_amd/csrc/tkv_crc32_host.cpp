@@ -521,11 +521,9 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   a.s_ends = s->po.big_off;
   a.s_info = sinfo;
   a.s_yq = s->po.s_off;
-  a.s_wtot = reinterpret_cast<std::uint32_t*>(s->seams);  // c->W entries, then the row table (c->W + 1),
-  auto* row0 = a.s_wtot + c->W;                             // then the spanning blocks (c->W): the seam
-  a.s_row0 = row0;                                          // records hold 16 words per wave
-  a.s_span = row0 + c->W + 1;
-  a.s_nwaves = c->W;
+  a.s_wtot = reinterpret_cast<std::uint32_t*>(s->seams);  // c->W entries, then the row table (c->W + 1)
+  auto* row0 = a.s_wtot + c->W;                             // (the seam records hold 16 words per wave)
+  a.s_row0 = row0;
   a.s_wv = s->po.big_idx;
   a.l_off = d_off;  // the lane phase walks the caller's own arrays
   a.l_len = d_len;

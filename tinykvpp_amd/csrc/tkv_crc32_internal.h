@@ -103,9 +103,6 @@ struct RowsArgs {
   std::uint32_t* s_wtot;             // per wave: crc_0 of its rows alone (crc_stream_body)
   const std::uint32_t* s_row0;       // [w] = first row of wave w, [nwaves] = rows (rows_tile_scan)
   std::uint32_t* s_wv;               // per block: the wave that met its end (crc_stream_body)
-  std::uint32_t* s_span;             // per crc_stream wave: the block that ends in it but starts in an
-                                     // earlier wave (0xFFFFFFFF: none); crc_rows finishes those
-  std::uint32_t s_nwaves;            // crc_stream's waves
   // irregular batches: the caller's own arrays, which the lane phase walks (blocks of at most kLaneMax
   // bytes are in no prepass list; counts[kCountLanes] says how many there are)
   const std::uint64_t* l_off;

@@ -81,16 +81,13 @@ template <bool ALIGNED, bool UNIFORM>
 __global__ __launch_bounds__(kRowsThreads) void crc_rows(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   if constexpr (!UNIFORM) {
-    // irregular batch whose blocks lie back to back: the prepass chose the byte-stream row walk and
-    // crc_stream (launched just before) has walked it and finished every block that starts and ends
-    // in one of its waves; this launch finishes the blocks that span waves (at most one ends in each
-    // crc_stream wave), from the registers of every wave they cross
+    // irregular batch whose blocks lie back to back: the prepass chose the byte-stream row walk,
+    // crc_stream (launched just before) has walked it, and this launch turns its registers into
+    // block CRCs
     if (dev::sload32(a.counts, 3) == kModeStream) {
-      const std::uint32_t step = gridDim.x * blockDim.x;
-      for (std::uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < a.s_nwaves; w += step) {
-        const std::uint32_t b = a.s_span[w];
-        if (b != 0xFFFFFFFFu) stream_finish_block(a, b);
-      }
+      const std::uint64_t step = static_cast<std::uint64_t>(gridDim.x) * blockDim.x;
+      for (std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x; b < a.nblocks; b += step)
+        stream_finish_block(a, b);
       return;
     }
   }
