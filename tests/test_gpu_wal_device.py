@@ -80,15 +80,36 @@ def make_wal(rng, n_rec, vmax=16000, giant=(), fake_headers=0.0):
     return img, offs, size
 
 
+def wal_last():
+    """What this thread's last WAL verify did (tkv_debug_wal_last): passes, whether the exact host
+    walk had to finish it, whether a host image was copied, pieces of the first pass."""
+    out = (ctypes.c_uint64 * 4)()
+    tk.load_library().tkv_debug_wal_last(out)
+    return {"passes": out[0], "host_walk": out[1], "copied": out[2], "pieces": out[3]}
+
+
+LAST = {}
+
+
 def both(img, size, shift=0):
-    """(host-image path, device-image path at byte offset `shift` of its allocation)."""
+    """(host-image path, device-image path at byte offset `shift` of its allocation); LAST holds
+    which path each took."""
     h = tk.wal.verify(img[:size].tobytes())
+    LAST["host_image"] = wal_last()
     d = torch.zeros(size + shift, dtype=torch.uint8, device="cuda")
     if size:
         d[shift:] = torch.from_numpy(img[:size].copy()).cuda()
     dv = tk.wal.verify_device(d[shift:], size)
     torch.cuda.synchronize()
+    LAST["device_image"] = wal_last()
     return h, dv
+
+
+def device_walk_only(max_passes=1):
+    """Both verifies of the last `both` call ran on the device, in at most max_passes passes."""
+    for path, r in LAST.items():
+        assert r["host_walk"] == 0, (path, r)
+        assert 1 <= r["passes"] <= max_passes, (path, r)
 
 
 @pytest.mark.parametrize("shift", [0, 3])
@@ -99,12 +120,15 @@ def test_small_records_clean_and_corrupted(gpu, oracle, shift):
     want = sequential_decode(oracle, img, n)
     assert want == ("ok", offs.size, n)
     assert both(img, n, shift) == (want, want)
+    device_walk_only()
+    assert LAST["host_image"]["copied"] == 1 and LAST["device_image"]["copied"] == 0
     for bad in (0, 1, 777, 60000, 119999):  # payload flips: CRC mismatch at that record
         o = int(offs[bad]) + int(size[bad]) - 1
         img[o] ^= 0x01
         want = sequential_decode(oracle, img, n)
         assert want == ("corrupted", bad, int(offs[bad]))
         assert both(img, n, shift) == (want, want)
+        device_walk_only()
         img[o] ^= 0x01
 
 
@@ -114,6 +138,7 @@ def test_giant_records_and_torn_tail(gpu, oracle):
     for n in (img.size, img.size - 5, int(offs[11]) + 30, int(offs[20000]) + 26 + 4096):
         want = sequential_decode(oracle, img, n)
         assert both(img, n) == (want, want), n
+        device_walk_only(max_passes=8)
 
 
 def test_corrupted_record_len_and_overrun(gpu, oracle):
@@ -145,10 +170,12 @@ def test_fake_headers_inside_values(gpu, oracle):
     want = sequential_decode(oracle, img, n)
     assert want == ("ok", offs.size, n)
     assert both(img, n) == (want, want)
+    print("fake headers, clean image:", LAST)  # which path ran: passes, host walk
     o = int(offs[39000]) + 26
     img[o] ^= 0x80
     want = sequential_decode(oracle, img, n)
     assert both(img, n) == (want, want)
+    print("fake headers, corrupted image:", LAST)
 
 
 @pytest.mark.parametrize("n", [0, 1, 25, 26, 27, 33, 34, 35, 2047, 2048, 2049, 4096 + 17])

@@ -8,25 +8,25 @@
 //  1. wal_scan_head: the image is cut into pieces of kWalPiece bytes, and the first plausible header
 //     of every piece (one the reference encoder could have written, wal.cpp:19-61), searched from
 //     the piece's front, becomes its speculative start S_k; piece 0 starts at 0.
-//  2. wal_spec: one lane per piece walks the chain from S_k over the records that start in the
-//     piece (X_k = the first record start at or past the piece's end, or the header that broke),
-//     and checks them as it goes: key/value bounds, and the CRC of every payload of at most
-//     kWalLaneMax bytes folded by the lane itself (slicing-by-4 lookups into the engine's tables in
-//     LDS, the payload zero-padded in front to whole dwords). Larger records (at most two start in a
-//     piece) wait in the piece's slots for one CRC batch through the engine's irregular path.
+//  2. wal_walk: one lane per piece walks the chain of headers from S_k over the records that start
+//     in the piece (X_k = the first record start at or past the piece's end, or the header that
+//     broke), checks key/value bounds, and writes every record's start into the piece's slots. It
+//     folds no payload: with no LDS tables it runs at full occupancy, and its only loads are the
+//     header windows.
 //  3. wal_jump: next(k) = the piece holding X_k. The true chain visits the pieces 0, next(0),
 //     next(next(0)), ...; pointer jumping (x4 per round) marks exactly those pieces in
 //     log4(#pieces) rounds, and wal_link hands every on-path piece its entry E = X of its predecessor.
-//  4. wal_count: an on-path piece whose entry is its speculative start keeps its speculative walk
-//     and checks; otherwise it walks again from E (and wal_recheck checks it again). Its speculative
-//     exit was right when the exact walk leaves at the same X (and breaks, or not, the same way).
-//     Entries are exact up to and including the first piece k* whose speculative exit was wrong (a
-//     corrupted record_len, or a fake header in a key or value that led the speculation astray):
-//     later pieces are dropped, and when no record up to k*'s exact exit fails, the next pass
-//     resumes there (a true record start) as a new image.
-//  5. one exclusive scan numbers the records; wal_gather turns each piece's first failing record
-//     into a record index and moves the big-record slots into a dense list for the CRC batch;
-//     wal_check_big checks those. The first bad record is an atomic minimum of record indices.
+//  4. wal_count: an on-path piece whose entry is its speculative start keeps its speculative walk;
+//     otherwise it walks again from E (rewriting its slots). Its speculative exit was right when the
+//     exact walk leaves at the same X (and breaks, or not, the same way). Entries are exact up to and
+//     including the first piece k* whose speculative exit was wrong (a corrupted record_len, or a fake
+//     header in a key or value that led the speculation astray): later pieces are dropped, and when
+//     no record up to k*'s exact exit fails, the next pass resumes there (a true record start).
+//  5. one exclusive scan numbers the records; wal_crc checks the CRC of every record whose payload is
+//     at most kWalFold bytes with one lane per record and consecutive lanes on consecutive records (the
+//     lane-block fold of the batch engine), and lists the larger ones for one CRC batch
+//     through the engine's irregular path (wal_check_big). The first bad record is an atomic minimum
+//     of record indices.
 // Every step reads the image in HBM; the host only reads back a few counters.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -49,10 +49,17 @@ namespace {
 
 constexpr std::uint64_t kWalPiece = 2048;     // bytes of image per speculative walker
 constexpr std::uint64_t kWalMeta = 26;        // wal.hpp:21-27 kMetadataSize
-constexpr std::uint32_t kWalLaneMax = 1024;   // payloads up to this size are checked by their lane
+constexpr std::uint32_t kWalFold = 256;       // payloads up to this size are checked by wal_crc's lanes
 constexpr std::uint64_t kNone = ~0ull;
 constexpr unsigned kScanThreads = 256;        // wal_scan_head: 8 lanes per piece, 8 pieces per wave
-constexpr unsigned kCheckThreads = 1024;      // wal_spec/wal_recheck: one workgroup per CU (128 KiB of LDS)
+constexpr unsigned kWalkThreads = 256;        // wal_walk: one lane per piece, no LDS
+constexpr unsigned kCrcThreads = 1024;        // wal_crc: one workgroup per CU (128 KiB of LDS tables)
+// Record starts a piece can hold: every record before a piece's first bad one is at least kWalMeta
+// bytes long (a shorter one fails the key/value bounds), so at most ceil(2048 / 26) = 79 matter.
+// Slot word: bits 0-11 the start within the piece, bit 12 payload > kWalFold, bits 13-19 the number
+// of such larger records before it in the piece (its place in the piece's part of the big list).
+constexpr std::uint32_t kWalSlots = 80;
+constexpr std::uint32_t kSlotBig = 1u << 12;
 
 struct WalArgs {
   const std::uint8_t* w;
@@ -61,21 +68,20 @@ struct WalArgs {
   // per piece
   std::uint64_t* S;          // speculative start (kNone: no plausible header)
   std::uint64_t* X;          // exit of its speculative chain, or the start of the header that broke it
-  std::uint64_t* spec_cnt;   // records of the speculative chain: (all << 32) | (larger than kWalLaneMax)
+  std::uint64_t* spec_cnt;   // records of the speculative chain: (all << 32) | (larger than kWalFold)
   std::uint32_t* next;       // piece of X (K: end of image, broken chain or no start)
   std::uint8_t* broke;       // the speculative chain hit a header that does not fit (at X)
-  std::uint64_t* first_loc;  // first failing record of the piece's checked walk (local index, kNone)
-  std::uint64_t* first_pos;  // and its start
-  std::uint64_t* slot_off;   // two slots per piece: records larger than kWalLaneMax (payload offset,
-  std::uint32_t* slot_len;   //   length, stored CRC, local index)
-  std::uint32_t* slot_crc;
-  std::uint32_t* slot_loc;
+  std::uint64_t* first_loc;  // first record of the piece's walk that fails its key/value bounds (local
+  std::uint64_t* first_pos;  //   index, kNone) and its start
+  std::uint32_t* slots;      // kWalSlots per piece: its records' starts (slot words, above)
+  std::uint32_t* crc_bad;    // first record of the piece whose CRC fails (local index, 0xFFFFFFFF)
   std::uint32_t* Ja;         // pointer-jumping tables
   std::uint32_t* Jb;
   std::uint8_t* on;          // piece is on the true chain
   std::uint8_t* recheck;     // entered off its speculative start: walked and checked again
   std::uint64_t* entry;      // true entry point of an on-path piece
-  std::uint64_t* cnt;        // records of an on-path piece from its entry, packed as spec_cnt
+  std::uint64_t* cnt;        // records of an on-path piece from its entry, packed as spec_cnt (the
+                             //   second count: records > kWalFold before its first bounds failure)
   std::uint64_t* base;       // exclusive scan of cnt: first record index (high), first big record (low)
   std::uint64_t* Xe;         // exit of its exact walk from the entry (or the header that broke it)
   std::uint8_t* Be;          // the exact walk broke
@@ -86,7 +92,6 @@ struct WalArgs {
   std::uint64_t* big_idx;
   std::uint32_t* big_crc;
   std::uint32_t* got;        // engine CRC of each big payload (finalized)
-  const std::uint32_t* inj;  // inj[L] = Shift_L(0xFFFFFFFF), L <= kWalLaneMax: the init term
   const DeviceTables* tabs;
   std::uint64_t* res;        // [0] first piece with a wrong speculative exit, [1] chain end and
                              // [2] chain broke (from the path's last piece), [3] first bad record,
@@ -192,65 +197,6 @@ __global__ __launch_bounds__(kScanThreads) void wal_scan_head(WalArgs a, std::ui
   if (i == 0 && found_at != kNone) a.S[k] = found_at;
 }
 
-// One slicing-by-4 step of the lane's register over dword w (the engine's replicated LDS tables).
-__device__ __forceinline__ void wal_fold(const std::uint32_t* lds, dev::Reg& r, std::uint32_t w, const dev::LaneConst& kc) {
-  dev::slice4(lds, r, w, kc);
-}
-
-// CRC-32 (finalized) of the payload [q, q + L) in image bytes, L <= kWalLaneMax, folded by this
-// lane alone with slicing-by-4 lookups into the LDS tables; the init register enters as
-// inj[L] = Shift_L(0xFFFFFFFF) (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). The payload is read as the
-// 16-byte aligned granules that hold it, two at a time with the next two in flight: the bytes in
-// front of the payload in its first granule are zeroed (leading zeros leave an init-0 register at
-// 0), whole dwords are folded, and the last 0-3 bytes take Sarwate steps. A granule never crosses a
-// page, so reading the whole of one that holds payload bytes cannot fault. Each lane reads its own
-// part of the image, so a CU's lanes touch far more lines than its L1 holds; 16-byte reads take a
-// quarter of the requests of the dword reads they replace (profiles/r2/wal_pmc/).
-__device__ __forceinline__ std::uint32_t lane_crc(const std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
-                                                  std::uint64_t q, std::uint32_t L) {
-  if (L == 0) return 0u;  // crc32 of nothing
-  const std::uintptr_t s = reinterpret_cast<std::uintptr_t>(a.w) + q;
-  const std::uintptr_t g0 = s & ~static_cast<std::uintptr_t>(15);
-  const std::uint32_t h = static_cast<std::uint32_t>(s - g0);  // bytes in front, zeroed
-  const std::uint32_t span = h + L;
-  const std::uint32_t nd = span >> 2, tb = span & 3u;          // whole dwords, then tail bytes
-  const std::uint32_t glast = (span - 1u) >> 4;                 // last granule with payload bytes
-  auto G = [&](std::uint32_t m) { return *reinterpret_cast<const uint4*>(g0 + 16u * (m < glast ? m : glast)); };
-  auto mask = [&](std::uint32_t k) -> std::uint32_t {  // bytes of dword k at or after the payload start
-    const std::int32_t lead = static_cast<std::int32_t>(h) - static_cast<std::int32_t>(4u * k);
-    return lead <= 0 ? 0xFFFFFFFFu : (lead >= 4 ? 0u : 0xFFFFFFFFu << (8 * lead));
-  };
-  dev::Reg r{0, 0};
-  uint4 c0 = G(0), c1 = G(1);
-  // Granule pairs [m, m + 2): the first one masks the head dwords, the ones wholly inside the
-  // payload fold unguarded, the last one (<= 8 dwords left) is guarded and takes the tail bytes.
-  auto pair = [&](std::uint32_t m, const uint4& x0, const uint4& x1, bool head, bool guarded) {
-    const std::uint32_t d[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-    for (std::uint32_t i = 0; i < 8; ++i) {
-      const std::uint32_t k = 4u * m + i;
-      const std::uint32_t w = head ? d[i] & mask(k) : d[i];
-      if (!guarded || k < nd) {
-        wal_fold(lds, r, w, kc);
-      } else if (k == nd && tb) {  // the last 1-3 bytes
-        std::uint32_t x = r.value(), b = w;
-        for (std::uint32_t t = 0; t < tb; ++t, b >>= 8) x = (x >> 8) ^ dev::lds_at(lds, (((x ^ b) & 0xFFu) << 8) | kc.L0);
-        r = dev::Reg{x, 0};
-      }
-    }
-  };
-  std::uint32_t m = 0;
-  for (; 4u * m + 8u <= nd; m += 2) {  // pairs whose 8 dwords are all whole payload dwords
-    const uint4 n0 = G(m + 2), n1 = G(m + 3);  // the next two granules, in flight
-    if (m == 0) pair(0, c0, c1, true, false);
-    else pair(m, c0, c1, false, false);
-    c0 = n0;
-    c1 = n1;
-  }
-  pair(m, c0, c1, m == 0, true);  // the last 0-7 whole dwords and the tail bytes
-  return r.value() ^ a.inj[L] ^ 0xFFFFFFFFu;
-}
-
 // Slicing tables into LDS (the row kernels' lane-shift tables are not needed here).
 __device__ __forceinline__ void fill_slices(const DeviceTables* tabs, std::uint32_t* lds) {
   for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
@@ -308,15 +254,19 @@ __device__ __forceinline__ void header_fields(const WalArgs& a, std::uint64_t p,
 }
 
 // Walk piece k from `start` over the records that start in the piece (wal.cpp:63-87: header size,
-// then record_len against what is left) and check each one: key/value bounds (wal.cpp:118-121) and,
-// for payloads up to kWalLaneMax bytes, the CRC (wal.cpp:89-96) in this lane. Larger records (at most
-// two start in a piece) are kept in the piece's two slots for the CRC batch. Writes the piece's exit,
-// break, counts, first failing record (local index) and slots.
-__device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
-                                           std::uint64_t k, std::uint64_t start, std::uint64_t* exit_out,
-                                           std::uint8_t* broke_out, std::uint64_t* cnt_out) {
-  const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
-  std::uint64_t p = start, n_all = 0, n_big = 0, first = kNone, first_pos = 0;
+// then record_len against what is left), checking each one's key/value bounds (wal.cpp:118-121), and
+// write each record's start into the piece's slots, four slot words to a 16-byte store. Records after
+// the piece's first bounds failure get no slot (they cannot be the first corruption) and no place in
+// the big list. Writes the piece's exit, break, counts and first bounds failure.
+__device__ __forceinline__ void walk_headers(const WalArgs& a, std::uint64_t k, std::uint64_t start,
+                                             std::uint64_t* exit_out, std::uint8_t* broke_out,
+                                             std::uint64_t* cnt_out) {
+  const std::uint64_t pbase = k * kWalPiece;
+  const std::uint64_t limit = pbase + kWalPiece < a.size ? pbase + kWalPiece : a.size;
+  std::uint32_t* slots = a.slots + k * kWalSlots;
+  std::uint64_t p = start, first = kNone, first_pos = 0;
+  std::uint32_t n_all = 0, n_big = 0;
+  std::uint32_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
   bool bad_hdr = false;
   HdrRaw h = header_load(a, p);
   while (p < limit) {
@@ -332,37 +282,38 @@ __device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::
       break;
     }
     const std::uint64_t np = p + 8 + static_cast<std::uint64_t>(rlen);
-    if (np < limit && a.size - np >= kWalMeta) h = header_load(a, np);  // next header in flight during the fold
-    bool bad = kWalMeta + klen + vlen > 8ull + rlen;
-    if (rlen <= kWalLaneMax) {
-      bad = bad || lane_crc(lds, kc, a, p + 8, rlen) != stored;
-    } else {
-      const std::uint64_t sl = 2 * k + (n_big & 1u);
-      a.slot_off[sl] = p + 8;
-      a.slot_len[sl] = rlen;
-      a.slot_crc[sl] = stored;
-      a.slot_loc[sl] = static_cast<std::uint32_t>(n_all);
-      ++n_big;
-    }
-    if (bad && first == kNone) {
-      first = n_all;
-      first_pos = p;
+    if (np < limit && a.size - np >= kWalMeta) h = header_load(a, np);  // next header in flight
+    if (first == kNone) {
+      if (kWalMeta + klen + vlen > 8ull + rlen) {
+        first = n_all;
+        first_pos = p;
+      } else if (n_all < kWalSlots) {
+        const bool big = rlen > kWalFold;
+        const std::uint32_t word = static_cast<std::uint32_t>(p - pbase) | (big ? kSlotBig : 0u) | (n_big << 13);
+        const std::uint32_t j = n_all & 3u;
+        acc0 = j == 0 ? word : acc0;
+        acc1 = j == 1 ? word : acc1;
+        acc2 = j == 2 ? word : acc2;
+        acc3 = j == 3 ? word : acc3;
+        if (j == 3) *reinterpret_cast<uint4*>(slots + (n_all - 3)) = make_uint4(acc0, acc1, acc2, acc3);
+        n_big += big ? 1u : 0u;
+      }
     }
     ++n_all;
     p = np;
   }
+  const std::uint32_t kept = first == kNone ? n_all : static_cast<std::uint32_t>(first);
+  if ((kept & 3u) && kept <= kWalSlots)
+    *reinterpret_cast<uint4*>(slots + (kept & ~3u)) = make_uint4(acc0, acc1, acc2, acc3);
   *exit_out = p;
   *broke_out = bad_hdr ? 1 : 0;
-  *cnt_out = (n_all << 32) | n_big;
+  *cnt_out = (static_cast<std::uint64_t>(n_all) << 32) | n_big;
   a.first_loc[k] = first;
   a.first_pos[k] = first_pos;
 }
 
-// 2. Speculative walk and check of pieces [k_lo, k_hi) from their first plausible header (piece 0
-// from 0).
-__global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
-  __shared__ std::uint32_t lds[kLdsSliceWords];
-  fill_slices(a.tabs, lds);
+// 2. Speculative walk of pieces [k_lo, k_hi) from their first plausible header (piece 0 from 0).
+__global__ __launch_bounds__(kWalkThreads) void wal_walk(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
   const std::uint64_t k = k_lo + gid();
   if (k >= k_hi) return;
   const std::uint64_t s = k == 0 ? 0 : a.S[k];
@@ -375,10 +326,9 @@ __global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64
     a.first_loc[k] = kNone;
     return;
   }
-  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
   std::uint64_t x, c;
   std::uint8_t br;
-  walk_check(lds, kc, a, k, s, &x, &br, &c);
+  walk_headers(a, k, s, &x, &br, &c);
   a.X[k] = x;
   a.broke[k] = br;
   a.spec_cnt[k] = c;
@@ -392,6 +342,7 @@ __global__ void wal_jump_init(WalArgs a) {
   a.on[k] = k == 0 ? 1 : 0;
   a.recheck[k] = 0;
   a.bad_at[k] = kNone;
+  a.crc_bad[k] = 0xFFFFFFFFu;
 }
 
 // 3. One quadrupling round (J = next^(4^t)): every marked k marks J(k), J(J(k)) and J(J(J(k))), then
@@ -424,8 +375,9 @@ __global__ void wal_link(WalArgs a) {
 }
 
 // 4. Records of an on-path piece from its entry: the speculative walk's when it started there;
-// otherwise an exact walk (the records are checked again by wal_recheck). res[0] = the first piece
-// whose speculative exit was wrong; res[5] counts re-checked pieces. Off-path pieces count 0.
+// otherwise an exact walk from the entry, which rewrites the piece's slots and counts. res[0] = the
+// first piece whose speculative exit was wrong; res[5] counts re-walked pieces. Off-path pieces
+// count 0.
 __global__ void wal_count(WalArgs a) {
   const std::uint64_t k = gid();
   if (k >= a.K) return;
@@ -441,25 +393,9 @@ __global__ void wal_count(WalArgs a) {
     bad = a.broke[k] != 0;
     packed = a.spec_cnt[k];
   } else {
-    const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
-    std::uint64_t n_all = 0, n_big = 0;
-    p = e;
-    bad = false;
-    while (p < limit) {  // wal.cpp:63-87
-      if (a.size - p < kWalMeta) {
-        bad = true;
-        break;
-      }
-      const std::uint64_t rlen = ld32(a.w, p, a.size);
-      if (rlen + 8 > a.size - p) {
-        bad = true;
-        break;
-      }
-      ++n_all;
-      n_big += rlen > kWalLaneMax ? 1u : 0u;
-      p += 8 + rlen;
-    }
-    packed = (n_all << 32) | n_big;
+    std::uint8_t br;
+    walk_headers(a, k, e, &p, &br, &packed);
+    bad = br != 0;
     a.recheck[k] = 1;
     atomicAdd(reinterpret_cast<unsigned long long*>(&a.res[5]), 1ull);
     if (p != a.X[k] || bad != (a.broke[k] != 0)) atomicMin(reinterpret_cast<unsigned long long*>(&a.res[0]), k);
@@ -473,18 +409,6 @@ __global__ void wal_count(WalArgs a) {
   }
 }
 
-// Pieces entered off their speculative start: check their records from the true entry.
-__global__ __launch_bounds__(kCheckThreads) void wal_recheck(WalArgs a) {
-  __shared__ std::uint32_t lds[kLdsSliceWords];
-  fill_slices(a.tabs, lds);
-  const std::uint64_t k = gid();
-  if (k >= a.K || !a.recheck[k]) return;
-  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
-  std::uint64_t x, c;
-  std::uint8_t br;
-  walk_check(lds, kc, a, k, a.entry[k], &x, &br, &c);
-}
-
 // Records past the first piece with a wrong speculative exit are not on the true chain (or not
 // known to be): drop them.
 __global__ void wal_trim(WalArgs a, std::uint64_t kstar) {
@@ -492,23 +416,153 @@ __global__ void wal_trim(WalArgs a, std::uint64_t kstar) {
   if (k < a.K && k > kstar) a.cnt[k] = 0;
 }
 
-// 5. Record numbering: the first failing record of each counted piece becomes a record index, and
-// the big-record slots move to the dense list the CRC batch reads.
+// 5. CRC of every counted record (one lane per record, consecutive lanes on consecutive records).
+// Each wave takes 64 pieces at a time: lane p holds piece 64 g + p's record count (records before its
+// first bounds failure, at most kWalSlots) and the wave's inclusive scan of those counts, so record j
+// of the group belongs to the piece whose range of the scan holds j (a 6-step search over the lanes).
+// The lane reads the record's slot, then the 16-byte aligned granules from its start: header and
+// payload realigned in registers (lane_dwords' selects and v_alignbyte). A payload of at most kWalFold
+// bytes is folded from 0xFFFFFFFF (slicing-by-4, Sarwate tail), 64 bytes at a time, and compared with
+// the stored CRC (wal.cpp:89-96); a larger one goes to its place in the big list for the CRC batch.
+constexpr int kCrcGran = 6;  // granules covering the 8-byte header and a payload of kWalFold bytes
+__global__ __launch_bounds__(kCrcThreads) void wal_crc(WalArgs a) {
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  fill_slices(a.tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const dev::LaneConst kc = dev::lane_const(lane);
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t W = gridDim.x * (blockDim.x >> 6);
+  const std::uint64_t G = (static_cast<std::uint64_t>(a.K) + 63u) / 64u;
+  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
+  const std::uintptr_t glast = (w0 + a.size - 1) & ~static_cast<std::uintptr_t>(15);  // last granule
+  for (std::uint64_t g = wave; g < G; g += W) {
+    const std::uint64_t k = 64u * g + lane;
+    std::uint32_t nf = 0;
+    std::uint64_t b_all = 0, b_big = 0;
+    if (k < a.K && a.cnt[k] != 0) {
+      const std::uint64_t n_all = a.cnt[k] >> 32, fl = a.first_loc[k];
+      nf = static_cast<std::uint32_t>(std::min<std::uint64_t>(std::min<std::uint64_t>(n_all, fl), kWalSlots));
+      b_all = a.base[k] >> 32;
+      b_big = a.base[k] & 0xFFFFFFFFull;
+    }
+    std::uint32_t incl = nf;
+#pragma unroll
+    for (unsigned off = 1; off < 64; off <<= 1) {
+      const std::uint32_t y = __shfl_up(incl, off, 64);
+      incl += lane >= off ? y : 0u;
+    }
+    const std::uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+    // Two rounds of 64 records at a time: their slot loads, then their granule loads, go out together.
+    for (std::uint32_t r = 0; r < T; r += 128u) {
+      std::uint32_t word[2], ri[2];
+      std::uint64_t kk[2], pall[2], pbig[2];
+      bool live[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const std::uint32_t j = r + 64u * h + lane;
+        live[h] = j < T;
+        // the piece lane p: the smallest p with incl[p] > j
+        std::uint32_t pl = 0;
+#pragma unroll
+        for (std::uint32_t st = 32; st >= 1; st >>= 1) {
+          const std::uint32_t v = __shfl(incl, static_cast<int>(pl + st - 1), 64);
+          pl += v <= j ? st : 0u;
+        }
+        pl = pl > 63u ? 63u : pl;
+        const std::uint32_t pincl = __shfl(incl, static_cast<int>(pl), 64);
+        const std::uint32_t pn = __shfl(nf, static_cast<int>(pl), 64);
+        pall[h] = __shfl(b_all, static_cast<int>(pl), 64);
+        pbig[h] = __shfl(b_big, static_cast<int>(pl), 64);
+        ri[h] = j - (pincl - pn);
+        kk[h] = 64u * g + pl;
+        word[h] = live[h] ? a.slots[kk[h] * kWalSlots + ri[h]] : 0u;
+      }
+      std::uint32_t raw[2][4 * kCrcGran];
+      std::uintptr_t blk[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const std::uint64_t pos = kk[h] * kWalPiece + (word[h] & 0xFFFu);
+        blk[h] = live[h] ? w0 + pos : w0;
+        const std::uintptr_t al = blk[h] & ~static_cast<std::uintptr_t>(15);
+#pragma unroll
+        for (int q = 0; q < kCrcGran; ++q) {
+          const std::uintptr_t gp = al + 16u * q;
+          const uint4 v = *reinterpret_cast<const uint4*>(gp < glast ? gp : glast);  // inside the image's pages
+          raw[h][4 * q + 0] = v.x;
+          raw[h][4 * q + 1] = v.y;
+          raw[h][4 * q + 2] = v.z;
+          raw[h][4 * q + 3] = v.w;
+        }
+      }
+      std::uint32_t d[2][16], n[2], c[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, rlen[2], stored[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const std::uint32_t o = static_cast<std::uint32_t>(blk[h] & 15u);
+        const std::uint32_t m8 = 0u - ((o >> 3) & 1u), m4 = 0u - ((o >> 2) & 1u);
+#pragma unroll
+        for (int x = 0; x < 4 * kCrcGran - 2; ++x) raw[h][x] ^= (raw[h][x] ^ raw[h][x + 2]) & m8;
+#pragma unroll
+        for (int x = 0; x < 4 * kCrcGran - 3; ++x) raw[h][x] ^= (raw[h][x] ^ raw[h][x + 1]) & m4;
+        rlen[h] = __builtin_amdgcn_alignbyte(raw[h][1], raw[h][0], o & 3u);
+        stored[h] = __builtin_amdgcn_alignbyte(raw[h][2], raw[h][1], o & 3u);
+#pragma unroll
+        for (int x = 0; x < 16; ++x) d[h][x] = __builtin_amdgcn_alignbyte(raw[h][x + 3], raw[h][x + 2], o & 3u);
+        n[h] = live[h] && !(word[h] & kSlotBig) ? (rlen[h] < 64u ? rlen[h] : 64u) : 0u;
+      }
+      dev::lane_fold<2, false>(lds, kc, d, n, c);
+      // payloads of 65..kWalFold bytes: the next 64 bytes at a time, the chain carried over (the piece
+      // starts 64 q bytes into the payload, so its realignment is the payload start's)
+      for (std::uint32_t q = 1; q < kWalFold / 64u; ++q) {
+        bool more = false;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          n[h] = live[h] && !(word[h] & kSlotBig) && rlen[h] > 64u * q ? std::min(rlen[h] - 64u * q, 64u) : 0u;
+          more = more || n[h] != 0u;
+        }
+        if (__ballot(more) == 0) break;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const std::uintptr_t ps = blk[h] + 8u + 64u * q;
+          const std::uintptr_t al = ps & ~static_cast<std::uintptr_t>(15);
+          uint4 gr[dev::kLaneGran];
+#pragma unroll
+          for (int x = 0; x < dev::kLaneGran; ++x) {
+            const std::uintptr_t gp = al + 16u * x;
+            gr[x] = *reinterpret_cast<const uint4*>(gp < glast ? gp : glast);
+          }
+          dev::lane_dwords<1>(gr, static_cast<std::uint32_t>(ps & 15u), d[h]);
+        }
+        dev::lane_fold<2, false>(lds, kc, d, n, c);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (!live[h]) continue;
+        if (word[h] & kSlotBig) {
+          const std::uint64_t bi = pbig[h] + (word[h] >> 13);
+          a.big_off[bi] = kk[h] * kWalPiece + (word[h] & 0xFFFu) + 8;
+          a.big_len[bi] = rlen[h];
+          a.big_crc[bi] = stored[h];
+          a.big_idx[bi] = pall[h] + ri[h];
+        } else if ((c[h] ^ 0xFFFFFFFFu) != stored[h]) {
+          atomicMin(&a.crc_bad[kk[h]], ri[h]);
+        }
+      }
+    }
+  }
+}
+
+// The first failing record of each counted piece (key/value bounds or CRC) as a record index.
 __global__ void wal_gather(WalArgs a) {
   const std::uint64_t k = gid();
   if (k >= a.K || a.cnt[k] == 0) return;
-  const std::uint64_t b_all = a.base[k] >> 32, b_big = a.base[k] & 0xFFFFFFFFull;
-  const std::uint64_t n_big = a.cnt[k] & 0xFFFFFFFFull;
-  if (a.first_loc[k] != kNone) {
-    a.bad_at[k] = b_all + a.first_loc[k];
-    atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), b_all + a.first_loc[k]);
-  }
-  for (std::uint64_t j = 0; j < n_big; ++j) {
-    const std::uint64_t sl = 2 * k + j;
-    a.big_off[b_big + j] = a.slot_off[sl];
-    a.big_len[b_big + j] = a.slot_len[sl];
-    a.big_crc[b_big + j] = a.slot_crc[sl];
-    a.big_idx[b_big + j] = b_all + a.slot_loc[sl];
+  const std::uint64_t b_all = a.base[k] >> 32;
+  const std::uint64_t cb = a.crc_bad[k] == 0xFFFFFFFFu ? kNone : a.crc_bad[k];
+  const std::uint64_t fl = a.first_loc[k];
+  const std::uint64_t f = cb < fl ? cb : fl;
+  if (f != kNone) {
+    if (cb < fl) a.first_pos[k] = k * kWalPiece + (a.slots[k * kWalSlots + cb] & 0xFFFu);
+    a.bad_at[k] = b_all + f;
+    atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), b_all + f);
   }
 }
 
@@ -529,13 +583,13 @@ __global__ void wal_bad_pos(WalArgs a, std::uint64_t n_big) {
 struct WalScratch {
   std::mutex mu;
   std::uint64_t cap_pieces = 0, cap_big = 0;
-  void* pieces = nullptr;  // per piece: 13 u64, 9 u32, 4 u8 (carve)
+  void* pieces = nullptr;  // per piece: 10 u64, 4 + kWalSlots u32, 4 u8 (carve)
   void* bigs = nullptr;    // per big record: 2 u64, 3 u32
   void* cub = nullptr;
   std::size_t cub_bytes = 0;
   std::uint64_t* res = nullptr;
   std::uint64_t* h_res = nullptr;
-  std::uint32_t* inj = nullptr;  // Shift_L(0xFFFFFFFF), L = 0..kWalLaneMax
+  unsigned ncu = 0;              // the device's compute units (wal_crc's grid)
   // host images: device copy, pinned staging slabs for pageable sources, own stream
   std::uint8_t* d_img = nullptr;
   std::uint64_t cap_img = 0;
@@ -560,7 +614,6 @@ struct WalScratch {
     (void)hipFree(bigs);
     (void)hipFree(cub);
     (void)hipFree(res);
-    (void)hipFree(inj);
     (void)hipHostFree(h_res);
   }
 };
@@ -583,7 +636,7 @@ int grow_pieces(WalScratch& s, std::uint64_t K) {
   WAL_HIP(hipFree(s.pieces));
   s.pieces = nullptr;
   s.cap_pieces = 0;
-  WAL_HIP(hipMalloc(&s.pieces, cap * (13 * 8 + 9 * 4 + 4)));
+  WAL_HIP(hipMalloc(&s.pieces, cap * (10 * 8 + (4 + kWalSlots) * 4 + 4)));
   s.cap_pieces = cap;
   return TKV_OK;
 }
@@ -609,15 +662,13 @@ WalArgs carve(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std::uin
   std::uint64_t** u64s[] = {&a.S, &a.X, &a.spec_cnt, &a.first_loc, &a.first_pos, &a.entry, &a.cnt, &a.base, &a.Xe,
                             &a.bad_at};
   for (std::size_t i = 0; i < sizeof(u64s) / sizeof(u64s[0]); ++i) *u64s[i] = p8 + i * C;
-  a.slot_off = p8 + 10 * C;  // 2C
-  auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 13 * C);
-  a.next = p4;
-  a.Ja = p4 + C;
-  a.Jb = p4 + 2 * C;
-  a.slot_len = p4 + 3 * C;  // 2C each
-  a.slot_crc = p4 + 5 * C;
-  a.slot_loc = p4 + 7 * C;
-  auto* p1 = reinterpret_cast<std::uint8_t*>(p4 + 9 * C);
+  auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 10 * C);
+  a.slots = p4;  // kWalSlots * C (16-byte aligned: C * 80 u64 in front, kWalSlots * 4 = 320 bytes per piece)
+  a.next = p4 + kWalSlots * C;
+  a.Ja = a.next + C;
+  a.Jb = a.next + 2 * C;
+  a.crc_bad = a.next + 3 * C;
+  auto* p1 = reinterpret_cast<std::uint8_t*>(a.next + 4 * C);
   a.broke = p1;
   a.on = p1 + C;
   a.Be = p1 + 2 * C;
@@ -632,7 +683,6 @@ WalArgs carve(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std::uin
     a.big_crc = b4 + B;
     a.got = b4 + 2 * B;
   }
-  a.inj = s.inj;
   a.tabs = tabs;
   a.res = s.res;
   return a;
@@ -675,7 +725,7 @@ void pass_front(const WalArgs& a, std::uint64_t k_lo, std::uint64_t k_hi, hipStr
   if (k_hi <= k_lo) return;
   const std::uint64_t threads = (k_hi - k_lo + 64 / kHeadLanes - 1) / (64 / kHeadLanes) * 64;  // 8 pieces per wave
   hipLaunchKernelGGL(wal_scan_head, dim3(blocks(threads, kScanThreads)), dim3(kScanThreads), 0, st, a, k_lo, k_hi);
-  hipLaunchKernelGGL(wal_spec, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
+  hipLaunchKernelGGL(wal_walk, dim3(blocks(k_hi - k_lo, kWalkThreads)), dim3(kWalkThreads), 0, st, a, k_lo, k_hi);
 }
 
 int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
@@ -701,7 +751,6 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
   std::uint64_t chain_end = s.h_res[1];
   bool broke = s.h_res[2] != 0;
   const bool partial = kstar < K;
-  if (s.h_res[5]) hipLaunchKernelGGL(wal_recheck, dim3(blocks(K, kCheckThreads)), dim3(kCheckThreads), 0, st, a);
   if (partial) {
     hipLaunchKernelGGL(wal_trim, dim3(blocks(K, 256)), dim3(256), 0, st, a, kstar);
     std::uint8_t be = 0;
@@ -711,7 +760,7 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
     chain_end = s.h_res[1];
     broke = be != 0;
   }
-  // 5: record numbering, first failing in-lane record, the CRC batch of the big ones
+  // 5: record numbering, the CRC of every record (in wal_crc, or the batch of the big ones)
   std::size_t need = 0;
   WAL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, a.cnt, a.base, K, st));
   if (need > s.cub_bytes) {
@@ -732,6 +781,10 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
   if (n) {
     if (int rc = grow_big(s, std::max<std::uint64_t>(n_big, 1))) return rc;
     a = carve(s, w, size, K, tabs);
+    const std::uint64_t groups = (K + 63) / 64;  // wal_crc: 64 pieces per wave at a time
+    const unsigned crc_grid = static_cast<unsigned>(
+        std::max<std::uint64_t>(1, std::min<std::uint64_t>(s.ncu, (groups + kCrcThreads / 64 - 1) / (kCrcThreads / 64))));
+    hipLaunchKernelGGL(wal_crc, dim3(crc_grid), dim3(kCrcThreads), 0, st, a);
     hipLaunchKernelGGL(wal_gather, dim3(blocks(K, 256)), dim3(256), 0, st, a);
     WAL_HIP(hipGetLastError());
     for (std::uint64_t i = 0; i < n_big; i += kWalCrcChunk) {
@@ -779,10 +832,7 @@ int scratch(WalScratch** out) {
     WAL_HIP(hipStreamCreateWithFlags(&sp->st, hipStreamNonBlocking));
     WAL_HIP(hipStreamCreateWithFlags(&sp->stc, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) WAL_HIP(hipEventCreateWithFlags(&sp->landed[i], hipEventDisableTiming));
-    std::vector<std::uint32_t> inj(kWalLaneMax + 1);
-    for (std::uint32_t L = 0; L <= kWalLaneMax; ++L) inj[L] = shift_bytes(kInit, L, kPoly);
-    WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->inj), inj.size() * 4));
-    WAL_HIP(hipMemcpy(sp->inj, inj.data(), inj.size() * 4, hipMemcpyHostToDevice));
+    WAL_HIP(hipDeviceGetAttribute(reinterpret_cast<int*>(&sp->ncu), hipDeviceAttributeMultiprocessorCount, dev));
   }
   *out = sp;
   return TKV_OK;
@@ -852,6 +902,13 @@ int wal_verify_device_impl(const std::uint8_t* d_wal, std::uint64_t size, std::u
   return verify_locked(s, d_wal, size, n_good, stop_offset, st, needs_host_walk);
 }
 
+int wal_verify_host_image_body(WalScratch& s, const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
+                               std::uint64_t* stop_offset, bool* needs_host_walk);
+
+// Device copies of host images above this size are freed after the verify (a multi-GiB recovery must
+// not hold that much HBM for the rest of the process); smaller ones are kept for the next call.
+constexpr std::uint64_t kKeepImage = std::uint64_t(1) << 30;
+
 int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
                                std::uint64_t* stop_offset, bool* needs_host_walk) {
   *needs_host_walk = false;
@@ -867,6 +924,21 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
   if (int rc = scratch(&sp)) return rc;
   WalScratch& s = *sp;
   std::lock_guard<std::mutex> lk(s.mu);
+  const int rc = wal_verify_host_image_body(s, h_wal, size, n_good, stop_offset, needs_host_walk);
+  // Whatever happened, no copy that reads the caller's buffer or writes d_img is left in flight.
+  const hipError_t e0 = hipStreamSynchronize(s.st), e1 = hipStreamSynchronize(s.stc);
+  if (s.cap_img > kKeepImage) {
+    (void)hipFree(s.d_img);
+    s.d_img = nullptr;
+    s.cap_img = 0;
+  }
+  if (rc == TKV_OK && (e0 != hipSuccess || e1 != hipSuccess))
+    return set_error(TKV_IO_ERROR, hipGetErrorString(e0 != hipSuccess ? e0 : e1));
+  return rc;
+}
+
+int wal_verify_host_image_body(WalScratch& s, const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
+                               std::uint64_t* stop_offset, bool* needs_host_walk) {
   g_last[2] = 1;
   if (size > s.cap_img) {
     (void)hipStreamSynchronize(s.st);
@@ -897,7 +969,7 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
   // stream scans and speculatively walks the pieces before it whose records' bytes are all resident
   // (pieces ending at least kFrontMargin bytes before the end of what has landed), so only the last
   // chunk's pieces and the stitching remain once the copy is done.
-  constexpr std::uint64_t kFrontMargin = kWalPiece + kWalLaneMax + 64;
+  constexpr std::uint64_t kFrontMargin = kWalPiece + 64;  // the walk reads header windows only
   WalArgs a;
   if (int rc = pass_begin(s, s.d_img, size, s.stc, &a)) return rc;
   std::uint64_t fronted = 0;
