@@ -235,14 +235,16 @@ size_t tkv_debug_multi_plan(int ndev, const uint64_t *h_offsets, const uint32_t 
 int tkv_debug_multi_combine(uint32_t poly, int ndev, const uint64_t *h_offsets, const uint32_t *h_lengths,
                             const uint32_t *h_init_raw, uint64_t n, const uint32_t *piece_final,
                             uint32_t *h_out_final);
-/* What the calling thread's last tkv_wal_verify / tkv_wal_verify_device did: out[0] = device walk
- * passes, out[1] = 1 when it handed the image to the exact host-thread walk, out[2] = 1 when a
- * host image was copied to the device, out[3] = pieces of the last pass's image. */
 /* Update calls of the calling thread so far: out[0] through tkv_crc32[c]_update_host (the drop-in's
  * short-span host path), out[1] through tkv_crc32[c]_update (the GPU). */
 void tkv_debug_update_counts(uint64_t out[2]);
-
+/* What the calling thread's last tkv_wal_verify / tkv_wal_verify_device did: out[0] = device walk
+ * passes, out[1] = 1 when it handed the image to the exact host-thread walk, out[2] = 1 when a
+ * host image was copied to the device, out[3] = regions (one wave each) of the first pass. */
 void tkv_debug_wal_last(uint64_t out[4]);
+/* Forces the device WAL walk's region size (rounded up to 2 KiB; 0 = sized from the image and the
+ * device, 16 KiB - 1 MiB) for every later verify in the process; returns the previous setting. */
+uint64_t tkv_debug_wal_region(uint64_t bytes);
 /* Which path the last irregular batch on `stream` took: 1 = byte-stream row walk (blocks back to
  * back, each at least 64 bytes), 0 = general row walk; -1 on error. Synchronizes
  * the stream. */

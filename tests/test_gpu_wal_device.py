@@ -82,13 +82,24 @@ def make_wal(rng, n_rec, vmax=16000, giant=(), fake_headers=0.0):
 
 def wal_last():
     """What this thread's last WAL verify did (tkv_debug_wal_last): passes, whether the exact host
-    walk had to finish it, whether a host image was copied, pieces of the first pass."""
+    walk had to finish it, whether a host image was copied, regions of the first pass."""
     out = (ctypes.c_uint64 * 4)()
     tk.load_library().tkv_debug_wal_last(out)
-    return {"passes": out[0], "host_walk": out[1], "copied": out[2], "pieces": out[3]}
+    return {"passes": out[0], "host_walk": out[1], "copied": out[2], "regions": out[3]}
 
 
 LAST = {}
+
+
+@pytest.fixture(params=[0, 2048], ids=["auto_region", "region2k"])
+def region(request):
+    """Region size of the device walk (tkv_debug_wal_region): 0 sizes it from the image and the device
+    (16 KiB - 1 MiB); 2048 gives every 2 KiB chunk a wave of its own, so records straddle region
+    boundaries everywhere and the stitch and the exact re-walk run on every image."""
+    lib = tk.load_library()
+    old = lib.tkv_debug_wal_region(request.param)
+    yield request.param
+    lib.tkv_debug_wal_region(old)
 
 
 def both(img, size, shift=0):
@@ -113,7 +124,7 @@ def device_walk_only(max_passes=1):
 
 
 @pytest.mark.parametrize("shift", [0, 3])
-def test_small_records_clean_and_corrupted(gpu, oracle, shift):
+def test_small_records_clean_and_corrupted(gpu, oracle, shift, region):
     rng = np.random.default_rng(5)
     img, offs, size = make_wal(rng, 120000, vmax=600)
     n = img.size
@@ -132,7 +143,7 @@ def test_small_records_clean_and_corrupted(gpu, oracle, shift):
         img[o] ^= 0x01
 
 
-def test_giant_records_and_torn_tail(gpu, oracle):
+def test_giant_records_and_torn_tail(gpu, oracle, region):
     rng = np.random.default_rng(6)
     img, offs, size = make_wal(rng, 30000, giant=(10, 11, 20000, 29999))
     for n in (img.size, img.size - 5, int(offs[11]) + 30, int(offs[20000]) + 26 + 4096):
@@ -141,8 +152,8 @@ def test_giant_records_and_torn_tail(gpu, oracle):
         device_walk_only(max_passes=8)
 
 
-def test_corrupted_record_len_and_overrun(gpu, oracle):
-    """A record_len that lies sends the chain through garbage (the speculative pieces after it
+def test_corrupted_record_len_and_overrun(gpu, oracle, region):
+    """A record_len that lies sends the chain through garbage (the speculative regions after it
     disagree, the walk resumes or stops exactly where the sequential decode does)."""
     rng = np.random.default_rng(7)
     img, offs, size = make_wal(rng, 50000, vmax=2000)
@@ -161,7 +172,7 @@ def test_corrupted_record_len_and_overrun(gpu, oracle):
         img[o:o + 4] = old
 
 
-def test_fake_headers_inside_values(gpu, oracle):
+def test_fake_headers_inside_values(gpu, oracle, region):
     """Values full of well-formed records: speculative starts land off the true chain and must be
     discarded by the stitch (exact result, clean and with a late corruption)."""
     rng = np.random.default_rng(8)
@@ -178,8 +189,8 @@ def test_fake_headers_inside_values(gpu, oracle):
     print("fake headers, corrupted image:", LAST)
 
 
-@pytest.mark.parametrize("n", [0, 1, 25, 26, 27, 33, 34, 35, 2047, 2048, 2049, 4096 + 17])
-def test_tiny_and_piece_boundary_images(gpu, oracle, n):
+@pytest.mark.parametrize("n", [0, 1, 25, 26, 27, 33, 34, 35, 2047, 2048, 2049, 4096 + 17, 16384 + 5, 40000])
+def test_tiny_and_region_boundary_images(gpu, oracle, n, region):
     rng = np.random.default_rng(9)
     img, offs, size = make_wal(rng, 400, vmax=200)
     want = sequential_decode(oracle, img, n)
