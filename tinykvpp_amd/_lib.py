@@ -70,7 +70,6 @@ SIGNATURES = {
     "tkv_debug_set_host_mapped": (_int, [_int]),
     "tkv_debug_wal_chain": (_sz, [_u8p, _u64, _vp, _sz, ctypes.POINTER(_u64), ctypes.POINTER(_int)]),
     "tkv_debug_wal_last": (None, [_vp]),
-    "tkv_debug_wal_region": (_u64, [_u64]),
     "tkv_debug_update_counts": (None, [_vp]),
     "tkv_debug_irregular_mode": (_int, [_vp]),
     "tkv_debug_multi_plan": (_sz, [_int, _vp, _vp, _vp, _u64, _vp, _sz]),

@@ -206,44 +206,31 @@ __device__ __forceinline__ StreamGeom stream_geometry(const std::uint8_t* base, 
   return {zoff, s0rel, end >= off0 ? (end - off0 + s0rel + kRow - 1) / kRow : 0};
 }
 
-// One scan tile (kScanTile blocks, 4 per thread of a 1024-thread workgroup) of the prepass: the
-// tile's stream-mode verdict and lane density, and the exclusive scans inside the tile of the
-// (small count, rows) items and of the lane blocks. Also writes this workgroup's share of stream
-// mode's wave partition row0[0..Ws] (grid-stride).
-struct TileScan {
-  std::uint64_t off[4];
-  std::uint32_t len[4];
-  std::uint64_t v[4];   // scan items (0 for a lane block of a dense tile)
-  std::uint32_t lv[4];  // 1: lane block of a dense tile (the lane phase's)
-  std::uint64_t run;    // exclusive scan of the items inside the tile, at this thread's first block
-  std::uint32_t lrun;   // same for lane blocks
-  std::uint64_t tot;    // the tile's totals
-  std::uint32_t ltot;
-  std::uint32_t flags;  // kTileStream | kTileLanes
-};
-__device__ __forceinline__ TileScan tile_scan(const std::uint8_t* sbase, const std::uint64_t* offsets,
-                                             const std::uint32_t* lengths, std::uint32_t n, std::uint32_t* row0,
-                                             std::uint32_t Ws, std::uint32_t tile, bool need_off) {
+__global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase, const std::uint64_t* offsets,
+                                                      const std::uint32_t* lengths, std::uint32_t n,
+                                                      std::uint64_t* scan, std::uint64_t* tile_sums,
+                                                      std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
+                                                      std::uint32_t* lscan, std::uint32_t* tile_lanes) {
   __shared__ std::uint64_t wsum[16];
   __shared__ std::uint32_t lsum[16], lcnt[16];
+  // stream mode's wave partition (used only if the prepass picks stream mode): row0[0..Ws], grid-stride
   for (std::uint32_t w = blockIdx.x * 1024u + threadIdx.x; w <= Ws; w += gridDim.x * 1024u) {
     const std::uint64_t TR = stream_geometry(sbase, offsets, lengths, n).rows;
     row0[w] = static_cast<std::uint32_t>(dev::stream_row0<kStreamSkew>(w, TR, Ws));
   }
-  TileScan t;
-  const std::uint64_t base = static_cast<std::uint64_t>(tile) * kScanTile + threadIdx.x * 4u;
+  const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * 4u;
   const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  std::uint32_t len[4], lv[4];
   bool ok = true;
   unsigned nlw = 0;  // lane blocks (len <= kLaneMax) of this wave
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const std::uint64_t b = base + i;
-    t.len[i] = b < n ? lengths[b] : 0u;
-    t.off[i] = need_off && b < n ? offsets[b] : 0ull;
-    t.lv[i] = b < n && t.len[i] <= kLaneMax ? 1u : 0u;
-    nlw += static_cast<unsigned>(__popcll(__ballot(t.lv[i] != 0u)));
+    len[i] = b < n ? lengths[b] : 0u;
+    lv[i] = b < n && len[i] <= kLaneMax ? 1u : 0u;
+    nlw += static_cast<unsigned>(__popcll(__ballot(lv[i] != 0u)));
     // (a lane block is shorter than kStreamMinLen: its offsets are never read here)
-    if (b < n) ok = ok && t.len[i] >= kStreamMinLen && (b + 1 >= n || offsets[b] + t.len[i] == offsets[b + 1]);
+    if (b < n) ok = ok && len[i] >= kStreamMinLen && (b + 1 >= n || offsets[b] + len[i] == offsets[b + 1]);
   }
   if (lane == 0) lcnt[wid] = nlw;
   const bool tile_all_ok = __syncthreads_and(ok ? 1 : 0) != 0;
@@ -254,15 +241,15 @@ __device__ __forceinline__ TileScan tile_scan(const std::uint8_t* sbase, const s
 #pragma unroll
   for (unsigned w = 0; w < 16; ++w) nlt += lcnt[w];
   const bool dense = nlt >= kLaneDenseTile;
-  t.flags = (tile_all_ok ? kTileStream : 0u) | (dense ? kTileLanes : 0u);
-  std::uint64_t s = 0;
+  if (threadIdx.x == 0) tile_ok[blockIdx.x] = (tile_all_ok ? kTileStream : 0u) | (dense ? kTileLanes : 0u);
+  std::uint64_t v[4], s = 0;
   std::uint32_t ls = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    t.lv[i] = dense ? t.lv[i] : 0u;
-    t.v[i] = base + i < n && !t.lv[i] ? scan_item(t.len[i]) : 0ull;
-    s += t.v[i];
-    ls += t.lv[i];
+    lv[i] = dense ? lv[i] : 0u;
+    v[i] = base + i < n && !lv[i] ? scan_item(len[i]) : 0ull;
+    s += v[i];
+    ls += lv[i];
   }
   // Inclusive scans of the thread sums inside the wave (cross-lane shifts, no barriers), then the
   // 16 wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
@@ -280,46 +267,31 @@ __device__ __forceinline__ TileScan tile_scan(const std::uint8_t* sbase, const s
     lsum[wid] = linc;
   }
   __syncthreads();
-  std::uint64_t wpre = 0;
-  std::uint32_t lpre = 0;
-  t.tot = 0;
-  t.ltot = 0;
+  std::uint64_t wpre = 0, tot = 0;
+  std::uint32_t lpre = 0, ltot = 0;
 #pragma unroll
   for (unsigned w = 0; w < 16; ++w) {
-    const std::uint64_t x = wsum[w];
-    const std::uint32_t lx = lsum[w];
-    wpre += w < wid ? x : 0ull;
-    t.tot += x;
-    lpre += w < wid ? lx : 0u;
-    t.ltot += lx;
+    const std::uint64_t t = wsum[w];
+    const std::uint32_t lt = lsum[w];
+    wpre += w < wid ? t : 0ull;
+    tot += t;
+    lpre += w < wid ? lt : 0u;
+    ltot += lt;
   }
-  t.run = wpre + inc - s;  // exclusive
-  t.lrun = lpre + linc - ls;
-  return t;
-}
-
-__global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase, const std::uint64_t* offsets,
-                                                      const std::uint32_t* lengths, std::uint32_t n,
-                                                      std::uint64_t* scan, std::uint64_t* tile_sums,
-                                                      std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
-                                                      std::uint32_t* lscan, std::uint32_t* tile_lanes) {
-  const TileScan t = tile_scan(sbase, offsets, lengths, n, row0, Ws, blockIdx.x, false);
-  if (threadIdx.x == 0) tile_ok[blockIdx.x] = t.flags;
-  const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * 4u;
-  std::uint64_t run = t.run;
-  std::uint32_t lrun = t.lrun;
+  std::uint64_t run = wpre + inc - s;  // exclusive
+  std::uint32_t lrun = lpre + linc - ls;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    if (base + i < n && !t.lv[i]) {  // the scatter reads these for listed blocks only
+    if (base + i < n && !lv[i]) {  // the scatter reads these for listed blocks only
       scan[base + i] = run;
       lscan[base + i] = lrun;
     }
-    run += t.v[i];
-    lrun += t.lv[i];
+    run += v[i];
+    lrun += lv[i];
   }
   if (threadIdx.x == 1023) {
-    tile_sums[blockIdx.x] = t.tot;
-    tile_lanes[blockIdx.x] = t.ltot;
+    tile_sums[blockIdx.x] = tot;
+    tile_lanes[blockIdx.x] = ltot;
   }
 }
 

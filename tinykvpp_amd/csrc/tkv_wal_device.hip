@@ -4,35 +4,34 @@
 // ending in the first corruption - without walking the chain on the host.
 //
 // The record chain is a linked list through the image (record i+1 starts 8 + record_len bytes after
-// record i). The image is cut into regions of RS bytes (16 KiB - 1 MiB, about two per wave slot of
-// the device), one wave per region (wal_region):
-//  1. The wave streams its region in 2 KiB chunks, 32 bytes per lane, three chunks in flight. In each
-//     chunk every lane takes the first plausible header of its 32 bytes (one the reference encoder
-//     could have written, wal.cpp:19-61: op and tombstone bytes 0/1 found byte-parallel in registers,
-//     then record_len = 18 + klen + vlen) and walks the one to three headers that start there (L2-hot
-//     loads). The lane that holds the chain's current position starts there instead. Ballots then
-//     check that every lane's exit is the next lane's start; when they all agree (every WAL without
-//     fake headers in its values) the chain through the chunk is those lanes' records, otherwise a
-//     scalar loop follows it lane by lane and re-walks a lane from its true entry. The region's first
-//     record is its first plausible header (region 0: byte 0).
-//  2. Records of at most kWalFold payload bytes queue in LDS and are folded 128 at a time, one lane
-//     per record, with the slicing tables in LDS (the lane-block fold of the batch engine, DESIGN.md
-//     §4.5); larger ones are appended to a big list for one CRC batch through the irregular path. A
-//     region's walk stops at its first failing record (bounds or CRC).
-//  3. wal_jump: next(k) = the region holding the exit of region k's walk. The true chain visits
-//     regions 0, next(0), ...; pointer jumping (x4 per round) marks exactly those regions and
-//     wal_link hands every one its entry E. A region whose entry is not its speculative start is
-//     walked again from E (wal_region in exact mode). Entries are exact up to and including the first
-//     region k* whose speculative exit was wrong; later regions are dropped, and when no record up to
-//     k*'s exact exit fails, the next pass resumes there (a true record start).
-//  4. One exclusive scan numbers the records; the first bad record is an atomic minimum of record
-//     indices over the regions and the big list.
+// record i), so it is walked speculatively in parallel and stitched exactly:
+//  1. wal_scan_head: the image is cut into pieces of kWalPiece bytes, and the first plausible header
+//     of every piece (one the reference encoder could have written, wal.cpp:19-61), searched from
+//     the piece's front, becomes its speculative start S_k; piece 0 starts at 0.
+//  2. wal_spec: one lane per piece walks the chain from S_k over the records that start in the
+//     piece (X_k = the first record start at or past the piece's end, or the header that broke),
+//     and checks them as it goes: key/value bounds, and the CRC of every payload of at most
+//     kWalLaneMax bytes folded by the lane itself (slicing-by-4 lookups into the engine's tables in
+//     LDS, the payload zero-padded in front to whole dwords). Larger records (at most two start in a
+//     piece) wait in the piece's slots for one CRC batch through the engine's irregular path.
+//  3. wal_jump: next(k) = the piece holding X_k. The true chain visits the pieces 0, next(0),
+//     next(next(0)), ...; pointer jumping (x4 per round) marks exactly those pieces in
+//     log4(#pieces) rounds, and wal_link hands every on-path piece its entry E = X of its predecessor.
+//  4. wal_count: an on-path piece whose entry is its speculative start keeps its speculative walk
+//     and checks; otherwise it walks again from E (and wal_recheck checks it again). Its speculative
+//     exit was right when the exact walk leaves at the same X (and breaks, or not, the same way).
+//     Entries are exact up to and including the first piece k* whose speculative exit was wrong (a
+//     corrupted record_len, or a fake header in a key or value that led the speculation astray):
+//     later pieces are dropped, and when no record up to k*'s exact exit fails, the next pass
+//     resumes there (a true record start) as a new image.
+//  5. one exclusive scan numbers the records; wal_gather turns each piece's first failing record
+//     into a record index and moves the big-record slots into a dense list for the CRC batch;
+//     wal_check_big checks those. The first bad record is an atomic minimum of record indices.
 // Every step reads the image in HBM; the host only reads back a few counters.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
-#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -48,59 +47,64 @@
 namespace tkv {
 namespace {
 
-constexpr std::uint64_t kWalMeta = 26;      // wal.hpp:21-27 kMetadataSize
-constexpr std::uint32_t kWalFold = 256;     // payloads up to this size are folded by wal_region's lanes
+constexpr std::uint64_t kWalPiece = 2048;     // bytes of image per speculative walker
+constexpr std::uint64_t kWalMeta = 26;        // wal.hpp:21-27 kMetadataSize
+constexpr std::uint32_t kWalLaneMax = 1024;   // payloads up to this size are checked by their lane
 constexpr std::uint64_t kNone = ~0ull;
-constexpr unsigned kRegThreads = 768;       // wal_region: 12 waves (LDS: tables + 12 chunk copies), one region each
-constexpr unsigned kRegWaves = kRegThreads / 64;
-constexpr std::uint64_t kChunk = 2048;      // bytes per wave step: 32 per lane (two 16-byte granules)
-// A wave's LDS copy of its chunk carries the first kHalo bytes of the next one: every header that
-// starts in the chunk, and every record with a payload of at most kWalFold bytes, lies whole in it.
-constexpr std::uint32_t kHalo = 8 + kWalFold + 32;
-constexpr std::uint32_t kHaloGran = kHalo / 16;   // 18 granules, loaded by lanes 0-17
-// Good records (at least kWalMeta bytes each) that can start in one chunk.
-constexpr std::uint32_t kChunkRecs = (kChunk + kWalMeta - 1) / kWalMeta + 1;
-constexpr std::uint64_t kRegionMin = 16 << 10, kRegionMax = 1 << 20;
-constexpr std::uint32_t kBigReserve = 64;   // big-list slots a wave reserves at a time
+constexpr unsigned kScanThreads = 256;        // wal_scan_head: 8 lanes per piece, 8 pieces per wave
+constexpr unsigned kCheckThreads = 1024;      // wal_spec/wal_recheck: one workgroup per CU (128 KiB of LDS)
 
 struct WalArgs {
   const std::uint8_t* w;
   std::uint64_t size;
-  std::uint64_t RS;          // region size (a multiple of kChunk)
-  std::uint32_t K;           // regions
-  // per region: the speculative walk
+  std::uint32_t K;           // pieces
+  // per piece
   std::uint64_t* S;          // speculative start (kNone: no plausible header)
-  std::uint64_t* X;          // exit: the first record start at or past the region's end, or where the walk
-                             //   stopped (a header that does not fit, or a failing record)
-  std::uint8_t* broke;       // 0: ran to its exit, 1: a header that does not fit at X, 2: stopped at a failure
-  std::uint64_t* spec_cnt;   // good records walked
-  std::uint32_t* next;       // region of X (K: end of image, stopped, or no start)
-  // per region: the walk the results come from (speculative, or exact from the entry)
-  std::uint64_t* first_loc;  // first failing record (bounds or CRC of a folded payload): local index, kNone
-  std::uint64_t* first_pos;  //   and its start
+  std::uint64_t* X;          // exit of its speculative chain, or the start of the header that broke it
+  std::uint64_t* spec_cnt;   // records of the speculative chain: (all << 32) | (larger than kWalLaneMax)
+  std::uint32_t* next;       // piece of X (K: end of image, broken chain or no start)
+  std::uint8_t* broke;       // the speculative chain hit a header that does not fit (at X)
+  std::uint64_t* first_loc;  // first failing record of the piece's checked walk (local index, kNone)
+  std::uint64_t* first_pos;  // and its start
+  std::uint64_t* slot_off;   // two slots per piece: records larger than kWalLaneMax (payload offset,
+  std::uint32_t* slot_len;   //   length, stored CRC, local index)
+  std::uint32_t* slot_crc;
+  std::uint32_t* slot_loc;
   std::uint32_t* Ja;         // pointer-jumping tables
   std::uint32_t* Jb;
-  std::uint8_t* on;          // region is on the true chain
-  std::uint8_t* recheck;     // entered off its speculative start: walked again in exact mode
-  std::uint64_t* entry;      // true entry point of an on-path region
-  std::uint64_t* cnt;        // good records of an on-path region from its entry (0 off the path)
-  std::uint64_t* base;       // exclusive scan of cnt: index of the region's first record
-  std::uint64_t* Xe;         // exit and break of the walk from the entry
-  std::uint8_t* Be;
-  std::uint64_t* bad_at;     // index of the region's first failing record
-  // big list (payloads above kWalFold), appended in any order
-  std::uint64_t cap_big;
-  std::uint64_t* big_off;    // payload offset in the image
-  std::uint64_t* big_key;    // (region << 32) | local record index
+  std::uint8_t* on;          // piece is on the true chain
+  std::uint8_t* recheck;     // entered off its speculative start: walked and checked again
+  std::uint64_t* entry;      // true entry point of an on-path piece
+  std::uint64_t* cnt;        // records of an on-path piece from its entry, packed as spec_cnt
+  std::uint64_t* base;       // exclusive scan of cnt: first record index (high), first big record (low)
+  std::uint64_t* Xe;         // exit of its exact walk from the entry (or the header that broke it)
+  std::uint8_t* Be;          // the exact walk broke
+  std::uint64_t* bad_at;     // index of the piece's first failing record
+  // per big record (dense, in record order)
+  std::uint64_t* big_off;
   std::uint32_t* big_len;
-  std::uint32_t* big_crc;    // stored CRC
+  std::uint64_t* big_idx;
+  std::uint32_t* big_crc;
   std::uint32_t* got;        // engine CRC of each big payload (finalized)
-  std::uint8_t* big_tag;     // 0: appended by the speculative walk, 1: by the exact walk
+  const std::uint32_t* inj;  // inj[L] = Shift_L(0xFFFFFFFF), L <= kWalLaneMax: the init term
   const DeviceTables* tabs;
-  std::uint64_t* res;        // [0] first region with a wrong speculative exit, [1] chain end and
-                             // [2] chain broke (from the path's last region), [3] first bad record,
-                             // [4] its start, [5] regions re-walked, [6] big records appended
+  std::uint64_t* res;        // [0] first piece with a wrong speculative exit, [1] chain end and
+                             // [2] chain broke (from the path's last piece), [3] first bad record,
+                             // [4] its start, [5] pieces re-checked
 };
+
+// Little-endian u32 at byte p of the image, p + 4 <= size: dword loads aligned to the absolute
+// address, realigned with v_alignbyte. The second dword is read only when it starts inside the
+// image, so no load touches a dword past the image's last byte (nor a page past its allocation);
+// the first may start up to 3 bytes before w, inside the same aligned dword as w itself.
+__device__ __forceinline__ std::uint32_t ld32(const std::uint8_t* w, std::uint64_t p, std::uint64_t size) {
+  const std::uintptr_t q = reinterpret_cast<std::uintptr_t>(w) + p;
+  const std::uintptr_t a = q & ~static_cast<std::uintptr_t>(3);
+  const std::uintptr_t end = reinterpret_cast<std::uintptr_t>(w) + size;
+  const std::uint32_t lo = *reinterpret_cast<const std::uint32_t*>(a);
+  const std::uint32_t hi = (q & 3u) && a + 4 < end ? *reinterpret_cast<const std::uint32_t*>(a + 4) : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, static_cast<std::uint32_t>(q & 3u));
+}
 
 __device__ __forceinline__ std::uint64_t gid() {
   return blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
@@ -111,6 +115,140 @@ __device__ __forceinline__ std::uint32_t le1_bytes4(std::uint32_t d) {
   const std::uint32_t x = d & 0xFEFEFEFEu;
   const std::uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu) & 0x80808080u;
   return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+
+// 1. The first plausible header of every piece, searched from the piece's front with an early exit.
+// A group of 8 lanes owns one piece and tests 224 positions per step. Lanes 0-6 each hold 32 bytes
+// (two 16-byte loads) and report their 32 positions; lane 7 only lends its bytes. A header at p has
+// its op and tombstone bytes (p+8, p+17) at 0 or 1 (wal.cpp:30-52): each lane marks which of its
+// bytes are 0 or 1 with byte-parallel arithmetic, takes its right neighbour's marks by a cross-lane
+// shift and so tests all 32 positions at once; only positions that pass get the full check
+// (record_len = 18 + klen + vlen, fitting the image; re-read through L1). The group moves on only
+// while no position of its piece passed. In a WAL of small records the first step finds the
+// header, so about 256 bytes of every 2 KiB piece are read; a piece inside a large value is scanned
+// whole. The earlier kernel scanned every position of the image in one coalesced pass: 1.11 ->
+// 0.85 ms on 1 GiB of 59-byte records, Zipf image unchanged (profiles/r2/wal_head_scan/). Each
+// piece has one owner, so the result is a plain store (S is preset to kNone; piece 0 starts at 0).
+constexpr unsigned kHeadLanes = 8;                   // lanes per piece
+constexpr unsigned kHeadChunks = 2 * (kHeadLanes - 1);  // 16-byte chunks reported per group and step
+__global__ __launch_bounds__(kScanThreads) void wal_scan_head(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
+  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
+  const std::uintptr_t al = w0 & ~static_cast<std::uintptr_t>(15);
+  const std::uint64_t off0 = w0 - al;
+  const std::uintptr_t end = w0 + a.size;
+  const std::uint32_t lane = threadIdx.x & 63u, g = lane / kHeadLanes, i = lane % kHeadLanes;
+  const std::uint64_t k = k_lo + (gid() >> 6) * (64 / kHeadLanes) + g;
+  const std::uint64_t ps = k * kWalPiece;
+  // positions with a whole header inside the image and inside the piece: [ps, pe)
+  const std::uint64_t pe = a.size < kWalMeta ? 0 : std::min<std::uint64_t>(ps + kWalPiece, a.size - kWalMeta + 1);
+  bool active = k < k_hi && k != 0 && ps < pe;  // uniform within a group
+  const std::uint64_t tg = (ps + off0) / 16;   // the chunk holding ps
+  std::uint64_t found_at = kNone;
+  for (std::uint64_t step = 0; __ballot(active) != 0; ++step) {
+    const std::uint64_t t = tg + step * kHeadChunks + 2 * i;
+    const std::uintptr_t c0 = al + 16 * t;
+    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+    if (active && c0 < end) v0 = *reinterpret_cast<const uint4*>(c0);
+    if (active && c0 + 16 < end) v1 = *reinterpret_cast<const uint4*>(c0 + 16);
+    const std::uint32_t f = le1_bytes4(v0.x) | le1_bytes4(v0.y) << 4 | le1_bytes4(v0.z) << 8 | le1_bytes4(v0.w) << 12 |
+                            le1_bytes4(v1.x) << 16 | le1_bytes4(v1.y) << 20 | le1_bytes4(v1.z) << 24 |
+                            le1_bytes4(v1.w) << 28;
+    const std::uint32_t f1 = static_cast<std::uint32_t>(__shfl_down(static_cast<int>(f), 1, 64));
+    const std::uint64_t F = f | static_cast<std::uint64_t>(f1) << 32;
+    std::uint32_t cand = static_cast<std::uint32_t>((F >> 8) & (F >> 17));  // bytes j+8, j+17 are 0/1
+    const std::int64_t p0 = static_cast<std::int64_t>(16 * t) - static_cast<std::int64_t>(off0);
+    const std::int64_t lo = static_cast<std::int64_t>(ps) - p0, hi = static_cast<std::int64_t>(pe) - 1 - p0;
+    if (!active || i + 1 == kHeadLanes || hi < 0 || lo > 31) {
+      cand = 0;
+    } else {
+      const std::uint32_t jlo = lo < 0 ? 0u : static_cast<std::uint32_t>(lo);
+      const std::uint32_t jhi = hi > 31 ? 31u : static_cast<std::uint32_t>(hi);
+      cand &= (jhi == 31u ? 0xFFFFFFFFu : (2u << jhi) - 1u) & ~((1u << jlo) - 1u);
+    }
+    std::uint64_t best = kNone;
+    while (cand) {
+      const int j = __builtin_ctz(cand);
+      const std::uint64_t p = static_cast<std::uint64_t>(p0 + j);
+      const std::uint64_t rlen = ld32(a.w, p, a.size), klen = ld32(a.w, p + 18, a.size), vlen = ld32(a.w, p + 22, a.size);
+      if (rlen == 18u + klen + vlen && rlen + 8 <= a.size - p) {
+        best = p;
+        break;
+      }
+      cand &= cand - 1;
+    }
+    // positions grow with the lane index inside a group: its first header is its lowest finder's
+    const std::uint64_t bal = __ballot(best != kNone);
+    const std::uint32_t gb = static_cast<std::uint32_t>(bal >> (g * kHeadLanes)) & ((1u << (kHeadLanes - 1)) - 1u);
+    const std::uint32_t src = g * kHeadLanes + (gb ? static_cast<std::uint32_t>(__builtin_ctz(gb)) : 0u);
+    const std::uint64_t first = __shfl(best, static_cast<int>(src), 64);
+    const std::int64_t next_p0 = static_cast<std::int64_t>(16 * (tg + (step + 1) * kHeadChunks)) - static_cast<std::int64_t>(off0);
+    if (active && gb) {
+      found_at = first;
+      active = false;
+    } else if (next_p0 >= static_cast<std::int64_t>(pe)) {
+      active = false;
+    }
+  }
+  if (i == 0 && found_at != kNone) a.S[k] = found_at;
+}
+
+// One slicing-by-4 step of the lane's register over dword w (the engine's replicated LDS tables).
+__device__ __forceinline__ void wal_fold(const std::uint32_t* lds, dev::Reg& r, std::uint32_t w, const dev::LaneConst& kc) {
+  dev::slice4(lds, r, w, kc);
+}
+
+// CRC-32 (finalized) of the payload [q, q + L) in image bytes, L <= kWalLaneMax, folded by this
+// lane alone with slicing-by-4 lookups into the LDS tables; the init register enters as
+// inj[L] = Shift_L(0xFFFFFFFF) (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). The payload is read as the
+// 16-byte aligned granules that hold it, two at a time with the next two in flight: the bytes in
+// front of the payload in its first granule are zeroed (leading zeros leave an init-0 register at
+// 0), whole dwords are folded, and the last 0-3 bytes take Sarwate steps. A granule never crosses a
+// page, so reading the whole of one that holds payload bytes cannot fault. Each lane reads its own
+// part of the image, so a CU's lanes touch far more lines than its L1 holds; 16-byte reads take a
+// quarter of the requests of the dword reads they replace (profiles/r2/wal_pmc/).
+__device__ __forceinline__ std::uint32_t lane_crc(const std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
+                                                  std::uint64_t q, std::uint32_t L) {
+  if (L == 0) return 0u;  // crc32 of nothing
+  const std::uintptr_t s = reinterpret_cast<std::uintptr_t>(a.w) + q;
+  const std::uintptr_t g0 = s & ~static_cast<std::uintptr_t>(15);
+  const std::uint32_t h = static_cast<std::uint32_t>(s - g0);  // bytes in front, zeroed
+  const std::uint32_t span = h + L;
+  const std::uint32_t nd = span >> 2, tb = span & 3u;          // whole dwords, then tail bytes
+  const std::uint32_t glast = (span - 1u) >> 4;                 // last granule with payload bytes
+  auto G = [&](std::uint32_t m) { return *reinterpret_cast<const uint4*>(g0 + 16u * (m < glast ? m : glast)); };
+  auto mask = [&](std::uint32_t k) -> std::uint32_t {  // bytes of dword k at or after the payload start
+    const std::int32_t lead = static_cast<std::int32_t>(h) - static_cast<std::int32_t>(4u * k);
+    return lead <= 0 ? 0xFFFFFFFFu : (lead >= 4 ? 0u : 0xFFFFFFFFu << (8 * lead));
+  };
+  dev::Reg r{0, 0};
+  uint4 c0 = G(0), c1 = G(1);
+  // Granule pairs [m, m + 2): the first one masks the head dwords, the ones wholly inside the
+  // payload fold unguarded, the last one (<= 8 dwords left) is guarded and takes the tail bytes.
+  auto pair = [&](std::uint32_t m, const uint4& x0, const uint4& x1, bool head, bool guarded) {
+    const std::uint32_t d[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+    for (std::uint32_t i = 0; i < 8; ++i) {
+      const std::uint32_t k = 4u * m + i;
+      const std::uint32_t w = head ? d[i] & mask(k) : d[i];
+      if (!guarded || k < nd) {
+        wal_fold(lds, r, w, kc);
+      } else if (k == nd && tb) {  // the last 1-3 bytes
+        std::uint32_t x = r.value(), b = w;
+        for (std::uint32_t t = 0; t < tb; ++t, b >>= 8) x = (x >> 8) ^ dev::lds_at(lds, (((x ^ b) & 0xFFu) << 8) | kc.L0);
+        r = dev::Reg{x, 0};
+      }
+    }
+  };
+  std::uint32_t m = 0;
+  for (; 4u * m + 8u <= nd; m += 2) {  // pairs whose 8 dwords are all whole payload dwords
+    const uint4 n0 = G(m + 2), n1 = G(m + 3);  // the next two granules, in flight
+    if (m == 0) pair(0, c0, c1, true, false);
+    else pair(m, c0, c1, false, false);
+    c0 = n0;
+    c1 = n1;
+  }
+  pair(m, c0, c1, m == 0, true);  // the last 0-7 whole dwords and the tail bytes
+  return r.value() ^ a.inj[L] ^ 0xFFFFFFFFu;
 }
 
 // Slicing tables into LDS (the row kernels' lane-shift tables are not needed here).
@@ -125,425 +263,126 @@ __device__ __forceinline__ void fill_slices(const DeviceTables* tabs, std::uint3
   __syncthreads();
 }
 
-// The header fields of a record: record_len, the stored CRC, key and value lengths (wal.cpp:14-18).
-struct Hdr {
-  std::uint32_t rlen, stored;
-  std::uint64_t klen, vlen;
+// The header fields of the record at p (p + 26 <= size): record_len, the stored CRC, key and value
+// lengths (wal.cpp:14-18). header_load issues two dword-aligned 16-byte loads over [p & ~3, + 32),
+// so the walk can put the next record's header in flight before it folds the current payload;
+// header_fields realigns the fields in registers. Within 32 bytes of the image's end (where those
+// loads could cross into the next page) nothing is loaded and the fields are read as dwords.
+struct HdrRaw {
+  uint4 u, v;
 };
-
-// The fields from the wave's LDS copy of its chunk (byte b of the copy, b < kChunk; the copy holds
-// the 32 bytes after the chunk too, so a header that starts in the chunk is whole in it), realigned
-// with v_alignbyte.
-__device__ __forceinline__ Hdr header_lds(const std::uint32_t* cb, std::uint32_t b) {
-  const std::uint32_t* d = cb + (b >> 2);
-  const std::uint32_t t = b & 3u;
-  const std::uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x4 = d[4], x5 = d[5], x6 = d[6], x7 = d[7];
+__device__ __forceinline__ bool header_window_ok(const WalArgs& a, std::uint64_t p) {
+  const std::uintptr_t b = (reinterpret_cast<std::uintptr_t>(a.w) + p) & ~static_cast<std::uintptr_t>(3);
+  return b + 32 <= reinterpret_cast<std::uintptr_t>(a.w) + a.size;
+}
+__device__ __forceinline__ HdrRaw header_load(const WalArgs& a, std::uint64_t p) {
+  HdrRaw h{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+  if (header_window_ok(a, p)) {
+    const std::uintptr_t b = (reinterpret_cast<std::uintptr_t>(a.w) + p) & ~static_cast<std::uintptr_t>(3);
+    h.u = *reinterpret_cast<const uint4*>(b);
+    h.v = *reinterpret_cast<const uint4*>(b + 16);
+  }
+  return h;
+}
+__device__ __forceinline__ void header_fields(const WalArgs& a, std::uint64_t p, const HdrRaw& h, std::uint32_t* rlen,
+                                              std::uint32_t* stored, std::uint64_t* klen, std::uint64_t* vlen) {
+  if (!header_window_ok(a, p)) {
+    *rlen = ld32(a.w, p, a.size);
+    *stored = ld32(a.w, p + 4, a.size);
+    *klen = ld32(a.w, p + 18, a.size);
+    *vlen = ld32(a.w, p + 22, a.size);
+    return;
+  }
+  const std::uint32_t t = static_cast<std::uint32_t>((reinterpret_cast<std::uintptr_t>(a.w) + p) & 3u);
+  const std::uint32_t d[8] = {h.u.x, h.u.y, h.u.z, h.u.w, h.v.x, h.v.y, h.v.z, h.v.w};
   auto at = [&](std::uint32_t lo, std::uint32_t hi) { return t ? __builtin_amdgcn_alignbyte(hi, lo, t) : lo; };
-  Hdr f;
-  f.rlen = at(x0, x1);
-  f.stored = at(x1, x2);
+  *rlen = at(d[0], d[1]);
+  *stored = at(d[1], d[2]);
+  // bytes p+18.. and p+22.. start in dword (t + 18) / 4 = 4 or 5 and (t + 22) / 4 = 5 or 6 of the
+  // window, at byte (t + 2) & 3 of it
   const bool up = t >= 2u;
   const std::uint32_t o = (t + 2u) & 3u;
   auto at2 = [&](std::uint32_t lo, std::uint32_t hi) { return o ? __builtin_amdgcn_alignbyte(hi, lo, o) : lo; };
-  f.klen = up ? at2(x5, x6) : at2(x4, x5);
-  f.vlen = up ? at2(x6, x7) : at2(x5, x6);
-  return f;
+  *klen = up ? at2(d[5], d[6]) : at2(d[4], d[5]);
+  *vlen = up ? at2(d[6], d[7]) : at2(d[5], d[6]);
 }
 
-// The records that start in a lane's 32 bytes [.., hi) from s (wal.cpp:63-87: header size, then
-// record_len against what is left; then the key/value bounds, wal.cpp:118-121). A good record is at
-// least kWalMeta bytes long, so at most two start there, and a third step can only find a header
-// that does not fit (status 1) or a failing record (status 2). X: the start after the last good
-// record (or of the one that broke or failed).
-struct LaneWalk {
-  std::uint64_t X, p0, p1;
-  std::uint32_t n, status, r0, r1, c0, c1;
-};
-__device__ __forceinline__ LaneWalk lane_walk(const WalArgs& a, const std::uint32_t* cb, std::int64_t cs, std::uint64_t s,
-                                              std::uint64_t hi) {
-  LaneWalk L{s, 0, 0, 0, 0, 0, 0, 0, 0};
-  std::uint64_t p = s;
-#pragma unroll
-  for (int it = 0; it < 3; ++it) {
-    if (p >= hi || L.status != 0u) break;
+// Walk piece k from `start` over the records that start in the piece (wal.cpp:63-87: header size,
+// then record_len against what is left) and check each one: key/value bounds (wal.cpp:118-121) and,
+// for payloads up to kWalLaneMax bytes, the CRC (wal.cpp:89-96) in this lane. Larger records (at most
+// two start in a piece) are kept in the piece's two slots for the CRC batch. Writes the piece's exit,
+// break, counts, first failing record (local index) and slots.
+__device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
+                                           std::uint64_t k, std::uint64_t start, std::uint64_t* exit_out,
+                                           std::uint8_t* broke_out, std::uint64_t* cnt_out) {
+  const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
+  std::uint64_t p = start, n_all = 0, n_big = 0, first = kNone, first_pos = 0;
+  bool bad_hdr = false;
+  HdrRaw h = header_load(a, p);
+  while (p < limit) {
     if (a.size - p < kWalMeta) {
-      L.status = 1;
+      bad_hdr = true;
       break;
     }
-    const Hdr f = header_lds(cb, static_cast<std::uint32_t>(static_cast<std::int64_t>(p) - cs));
-    if (static_cast<std::uint64_t>(f.rlen) + 8 > a.size - p) {
-      L.status = 1;
+    std::uint32_t rlen, stored;
+    std::uint64_t klen, vlen;
+    header_fields(a, p, h, &rlen, &stored, &klen, &vlen);
+    if (static_cast<std::uint64_t>(rlen) + 8 > a.size - p) {
+      bad_hdr = true;
       break;
     }
-    if (kWalMeta + f.klen + f.vlen > 8ull + f.rlen) {
-      L.status = 2;
-      break;
-    }
-    if (L.n == 0) {
-      L.p0 = p;
-      L.r0 = f.rlen;
-      L.c0 = f.stored;
+    const std::uint64_t np = p + 8 + static_cast<std::uint64_t>(rlen);
+    if (np < limit && a.size - np >= kWalMeta) h = header_load(a, np);  // next header in flight during the fold
+    bool bad = kWalMeta + klen + vlen > 8ull + rlen;
+    if (rlen <= kWalLaneMax) {
+      bad = bad || lane_crc(lds, kc, a, p + 8, rlen) != stored;
     } else {
-      L.p1 = p;
-      L.r1 = f.rlen;
-      L.c1 = f.stored;
+      const std::uint64_t sl = 2 * k + (n_big & 1u);
+      a.slot_off[sl] = p + 8;
+      a.slot_len[sl] = rlen;
+      a.slot_crc[sl] = stored;
+      a.slot_loc[sl] = static_cast<std::uint32_t>(n_all);
+      ++n_big;
     }
-    ++L.n;
-    p += 8 + static_cast<std::uint64_t>(f.rlen);
+    if (bad && first == kNone) {
+      first = n_all;
+      first_pos = p;
+    }
+    ++n_all;
+    p = np;
   }
-  L.X = p;
-  return L;
+  *exit_out = p;
+  *broke_out = bad_hdr ? 1 : 0;
+  *cnt_out = (n_all << 32) | n_big;
+  a.first_loc[k] = first;
+  a.first_pos[k] = first_pos;
 }
 
-__device__ __forceinline__ std::uint64_t readlane64(std::uint64_t v, std::uint32_t l) {
-  const std::uint32_t lo = __builtin_amdgcn_readlane(static_cast<std::uint32_t>(v), l);
-  const std::uint32_t hi = __builtin_amdgcn_readlane(static_cast<std::uint32_t>(v >> 32), l);
-  return static_cast<std::uint64_t>(hi) << 32 | lo;
-}
-
-// The CRC of record k of a chunk's small records, one per lane (slot word: byte b of the record in
-// the wave's LDS copy of its chunk | rlen << 11), from that copy: the payload [b + 8, b + 8 + rlen)
-// folded from 0xFFFFFFFF a dword at a time with slicing-by-4 (read aligned and realigned with
-// v_alignbyte) for as many dwords as the wave's longest payload has, then its last 1-3 bytes with
-// Sarwate steps, and compared with the stored CRC at b + 4. Every step is predicated with selects
-// rather than branched on: lanes differ in length, and per-lane branches cost more scalar
-// instructions than the fold itself. live: the lane has a record. Returns whether it matches (true
-// for a lane without one).
-__device__ __forceinline__ bool fold_lds(const std::uint32_t* lds, const dev::LaneConst& kc, const std::uint32_t* cb,
-                                         std::uint32_t word, bool live) {
-  const std::uint32_t b = live ? word & 2047u : 0u, rl = live ? (word >> 11) & 511u : 0u;
-  auto dw = [&](std::uint32_t byte) {  // little-endian u32 at any byte of the copy
-    const std::uint32_t* d = cb + (byte >> 2);
-    const std::uint32_t t = byte & 3u;
-    return t ? __builtin_amdgcn_alignbyte(d[1], d[0], t) : d[0];
-  };
-  const std::uint32_t stored = dw(b + 4u);
-  const std::uint32_t nf = rl >> 2;
-  std::uint32_t mx = nf;  // the wave's longest payload, in whole dwords
-#pragma unroll
-  for (unsigned m = 32; m > 0; m >>= 1) mx = std::max(mx, static_cast<std::uint32_t>(__shfl_xor(static_cast<int>(mx), m, 64)));
-  const std::uint32_t kmax = __builtin_amdgcn_readfirstlane(mx);
-  const std::uint32_t s0 = b + 8u;
-  const std::uint32_t* d = cb + (s0 >> 2);
-  const std::uint32_t t = s0 & 3u;
-  dev::Reg p{0xFFFFFFFFu, 0u};
-  std::uint32_t lo = d[0];
-  for (std::uint32_t k = 0; k < kmax; ++k) {
-    const std::uint32_t hi = d[k + 1];
-    const std::uint32_t w = t ? __builtin_amdgcn_alignbyte(hi, lo, t) : lo;
-    lo = hi;
-    dev::Reg np = p;
-    dev::slice4(lds, np, w, kc);
-    const bool on = k < nf;
-    p.t = on ? np.t : p.t;
-    p.u = on ? np.u : p.u;
-  }
-  // the last rl & 3 bytes
-  const std::uint32_t tb = rl & 3u;
-  const std::uint32_t wt = dw(s0 + 4u * nf);
-  std::uint32_t c = p.value();
-#pragma unroll
-  for (std::uint32_t j = 0; j < 3u; ++j) {
-    const std::uint32_t cn = (c >> 8) ^ dev::lds_at(lds, (((c ^ (wt >> (8 * j))) & 0xFFu) << 8) | kc.L0);
-    c = j < tb ? cn : c;
-  }
-  return !live || (c ^ 0xFFFFFFFFu) == stored;
-}
-
-// A chunk's bytes in flight: lane l's 32 bytes, and for lanes 0-17 one granule of the next chunk's
-// first kHalo bytes.
-struct ChunkRegs {
-  uint4 v0, v1, h;
-};
-__device__ __forceinline__ void chunk_issue(std::uintptr_t al, std::uint64_t lim, std::uint64_t c, std::uint32_t lane,
-                                            ChunkRegs& k) {
-  // lim: end of the image from al (the image's start rounded down to 16 bytes); only granules that
-  // start before that end are read, so no load leaves the image's pages. A granule that does not
-  // loads the image's first granule instead; those bytes are never used (every header, candidate and
-  // record is bounded by the image's size), and no zeroing select may follow the loads here, or the
-  // compiler waits for them at once.
-  const std::uint64_t q = c * kChunk + 32u * lane;
-  const std::uint64_t h = (c + 1) * kChunk + 16u * lane;
-  k.v0 = dev::gload16(q < lim ? al + q : al);
-  k.v1 = dev::gload16(q + 16 < lim ? al + q + 16 : al);
-  k.h = dev::gload16(lane < kHaloGran && h < lim ? al + h : al);
-}
-
-// 1-2. One wave per region [k_lo, k_hi). exact = 0: every region from its first plausible header
-// (region 0 from byte 0); exact = 1: only the regions flagged `recheck`, from their entry.
-__global__ __launch_bounds__(kRegThreads) void wal_region(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi,
-                                                          int exact) {
+// 2. Speculative walk and check of pieces [k_lo, k_hi) from their first plausible header (piece 0
+// from 0).
+__global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
   __shared__ std::uint32_t lds[kLdsSliceWords];
-  __shared__ uint4 chunkbuf[kRegWaves][(kChunk + kHalo) / 16];  // the wave's chunk and the next kHalo bytes
-  __shared__ std::uint32_t slotbuf[kRegWaves][kChunkRecs];      // its small records, compacted
-  const std::uint32_t lane = threadIdx.x & 63u;
-  const std::uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const std::uint64_t r = k_lo + static_cast<std::uint64_t>(blockIdx.x) * kRegWaves + wid;
-  bool work = r < k_hi && (!exact || (a.on[r] && a.recheck[r]));
-  if (__syncthreads_or(work ? 1 : 0) == 0) return;  // (uniform per workgroup)
   fill_slices(a.tabs, lds);
-  if (!work) return;
-  const dev::LaneConst kc = dev::lane_const(lane);
-  uint4* cb4 = chunkbuf[wid];
-  const std::uint32_t* cb = reinterpret_cast<const std::uint32_t*>(cb4);
-  std::uint32_t* slots = slotbuf[wid];
-
-  const std::uint64_t size = a.size;
-  const std::uint64_t rb = r * a.RS;
-  const std::uint64_t re = std::min(rb + a.RS, size);
-  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
-  const std::uintptr_t al = w0 & ~static_cast<std::uintptr_t>(15);
-  const std::uint64_t off0 = w0 - al;
-  const std::uint64_t lim = off0 + size;
-  const std::int64_t size26 = static_cast<std::int64_t>(size) - static_cast<std::int64_t>(kWalMeta);
-
-  std::uint64_t P = exact ? a.entry[r] : (r == 0 ? 0 : kNone);  // the chain's next record start
-  std::uint64_t S = P;                                          // the region's first record start
-  std::uint64_t nrec = 0;                                       // good records so far
-  std::uint64_t fail_loc = kNone, fail_pos = 0;
-  std::uint32_t brk = 0;
-  bool done = false;
-
-  // chunks: from the one holding the region's start (or its entry) to the one holding re - 1
-  const std::uint64_t c_first = ((P == kNone ? rb : P) + off0) / kChunk;
-  const std::uint64_t c_last = (re - 1 + off0) / kChunk;
-
-  // Big-list slots are reserved kBigReserve at a time (one returning atomic per reservation, not per
-  // chunk); unused ones are written as empty entries of no region.
-  std::uint64_t res_base = 0;
-  std::uint32_t res_left = 0;
-  auto pad_big = [&](std::uint64_t b, std::uint32_t n) __attribute__((always_inline)) {
-    if (lane < n && b + lane < a.cap_big) {
-      a.big_off[b + lane] = 0;
-      a.big_len[b + lane] = 0;
-      a.big_crc[b + lane] = 0;
-      a.big_key[b + lane] = kNone;
-      a.big_tag[b + lane] = 0xFF;
-    }
-  };
-
-  // One chunk: returns with P advanced past it (or done set).
-  auto process = [&](std::uint64_t c, const ChunkRegs& k) __attribute__((always_inline)) {
-    const std::int64_t cs = static_cast<std::int64_t>(c * kChunk) - static_cast<std::int64_t>(off0);  // image pos
-    const std::int64_t ce = cs + static_cast<std::int64_t>(kChunk);
-    if (P != kNone && static_cast<std::int64_t>(P) >= ce) return;  // inside a record that spans the chunk
-    cb4[2 * lane] = k.v0;
-    cb4[2 * lane + 1] = k.v1;
-    if (lane < kHaloGran) cb4[kChunk / 16 + lane] = k.h;
-    __builtin_amdgcn_wave_barrier();
-    const std::int64_t sub = cs + 32 * static_cast<std::int64_t>(lane);
-    const std::uint64_t sub_hi = static_cast<std::uint64_t>(std::max<std::int64_t>(sub + 32, 0));
-    // lane e0 holds P; lanes before it take no part, lanes after it take their first plausible header
-    const std::uint32_t e0 = P == kNone ? 0u : static_cast<std::uint32_t>((static_cast<std::int64_t>(P) - cs) >> 5);
-    std::uint64_t start = kNone;
-    if (P != kNone && lane == e0) start = P;
-    if (lane > e0 || P == kNone) {
-      std::uint32_t dw[16];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint4 v = cb4[2 * lane + i];
-        dw[4 * i] = v.x;
-        dw[4 * i + 1] = v.y;
-        dw[4 * i + 2] = v.z;
-        dw[4 * i + 3] = v.w;
-      }
-      std::uint64_t F = 0;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) F |= static_cast<std::uint64_t>(le1_bytes4(dw[i])) << (4 * i);
-      std::uint32_t cand = static_cast<std::uint32_t>((F >> 8) & (F >> 17));  // bytes j+8, j+17 are 0/1
-      // positions: at or after the region's start (when searching for it), before re, header inside the image
-      const std::int64_t lo = P == kNone ? static_cast<std::int64_t>(rb) : 0;
-      const std::int64_t hi = std::min<std::int64_t>(static_cast<std::int64_t>(re), size26 + 1);
-      const std::int64_t jlo = std::max<std::int64_t>(lo - sub, 0), jhi = std::min<std::int64_t>(hi - sub, 32);
-      if (jhi <= jlo) {
-        cand = 0;
-      } else {
-        cand &= (jhi >= 32 ? 0xFFFFFFFFu : (1u << jhi) - 1u) & ~((1u << jlo) - 1u);
-      }
-      while (cand) {
-        const std::uint64_t p = static_cast<std::uint64_t>(sub + __builtin_ctz(cand));
-        const Hdr f = header_lds(cb, static_cast<std::uint32_t>(static_cast<std::int64_t>(p) - cs));
-        if (static_cast<std::uint64_t>(f.rlen) == 18ull + f.klen + f.vlen && f.rlen + 8ull <= size - p) {
-          start = p;
-          break;
-        }
-        cand &= cand - 1;
-      }
-    }
-    std::uint64_t H = __ballot(start != kNone);
-    if (P == kNone) {  // still looking for the region's first record
-      if (H == 0) return;
-      const std::uint32_t first = static_cast<std::uint32_t>(__builtin_ctzll(H));
-      P = readlane64(start, first);
-      S = P;
-    }
-    const std::uint64_t lane_hi = std::min<std::uint64_t>(sub_hi, re);
-    LaneWalk L{start, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (start != kNone) L = lane_walk(a, cb, cs, start, lane_hi);
-    // Fast path: every lane's exit is the start of the next lane with a start (or leaves the chunk,
-    // for the last one), so the chain is exactly those lanes.
-    const std::uint64_t above = lane == 63u ? 0ull : H & (~0ull << (lane + 1));
-    const std::uint32_t nh = above ? static_cast<std::uint32_t>(__builtin_ctzll(above)) : 64u;
-    const bool inside = L.status == 0u && L.X < static_cast<std::uint64_t>(ce) && L.X < re;
-    const std::uint32_t lnx = inside ? static_cast<std::uint32_t>((static_cast<std::int64_t>(L.X) - cs) >> 5) : 64u;
-    const std::uint64_t s_nh = __shfl(start, static_cast<int>(nh & 63u), 64);
-    const bool ok = start == kNone || (lnx == nh && (nh == 64u || s_nh == L.X));
-    std::uint64_t chain = H;
-    if (__ballot(!ok) != 0) {
-      // Slow path: follow the chain lane by lane from P, re-walking a lane whose start is not it.
-      chain = 0;
-      std::uint64_t pc = P;
-      while (pc < static_cast<std::uint64_t>(ce) && pc < re) {
-        const std::uint32_t l = __builtin_amdgcn_readfirstlane(
-            static_cast<std::uint32_t>((static_cast<std::int64_t>(pc) - cs) >> 5));
-        if (readlane64(start, l) != pc && lane == l) {
-          start = pc;
-          L = lane_walk(a, cb, cs, start, lane_hi);
-        }
-        chain |= 1ull << l;
-        const std::uint32_t st = __builtin_amdgcn_readlane(L.status, l);
-        pc = readlane64(L.X, l);
-        if (st != 0u) break;
-      }
-    }
-    const std::uint32_t lz = 63u - static_cast<std::uint32_t>(__builtin_clzll(chain));
-    const std::uint64_t pexit = readlane64(L.X, lz);
-    const std::uint32_t sexit = __builtin_amdgcn_readlane(L.status, lz);
-    // The chain's good records, numbered: small ones folded here from the LDS copy, big ones appended
-    // to the big list.
-    const bool on = (chain >> lane) & 1ull;
-    const bool g1 = on && L.n >= 1u, g2 = on && L.n >= 2u;
-    const bool s1 = g1 && L.r0 <= kWalFold, s2 = g2 && L.r1 <= kWalFold;
-    const bool b1 = g1 && !s1, b2 = g2 && !s2;
-    const std::uint64_t lt = (1ull << lane) - 1ull;
-    const std::uint64_t G1 = __ballot(g1), G2 = __ballot(g2);
-    const std::uint64_t B1 = __ballot(b1), B2 = __ballot(b2);
-    const std::uint64_t idx0 = nrec + __popcll(G1 & lt) + __popcll(G2 & lt);
-    // Small records, compacted into consecutive lanes in chain order (slot word: byte in the copy |
-    // rlen << 11 | rank among the chunk's good records << 20), folded one per lane.
-    const std::uint64_t S1 = __ballot(s1), S2 = __ballot(s2);
-    const std::uint32_t nsm = static_cast<std::uint32_t>(__popcll(S1) + __popcll(S2));
-#ifndef TKV_WAL_PROBE_NOFOLD  // probe builds only (tools/build_variant.sh): the walk without the fold
-    if (nsm != 0u) {
-#else
-    if (false) {
-#endif
-      const std::uint32_t sp = static_cast<std::uint32_t>(__popcll(S1 & lt) + __popcll(S2 & lt));
-      const std::uint32_t rk = static_cast<std::uint32_t>(idx0 - nrec);
-      if (s1)
-        slots[sp] = static_cast<std::uint32_t>(static_cast<std::int64_t>(L.p0) - cs) | L.r0 << 11 | rk << 20;
-      if (s2)
-        slots[sp + (s1 ? 1u : 0u)] =
-            static_cast<std::uint32_t>(static_cast<std::int64_t>(L.p1) - cs) | L.r1 << 11 | (rk + 1u) << 20;
-      __builtin_amdgcn_wave_barrier();
-      for (std::uint32_t k0 = 0; k0 < nsm; k0 += 64u) {
-        const bool live = k0 + lane < nsm;
-        const std::uint32_t word = live ? slots[k0 + lane] : 0u;
-        const std::uint64_t bad = __ballot(!fold_lds(lds, kc, cb, word, live));
-        if (bad) {  // the first failing record (slot order is record order)
-          const std::uint32_t w = __builtin_amdgcn_readlane(word, static_cast<std::uint32_t>(__builtin_ctzll(bad)));
-          const std::uint64_t loc = nrec + (w >> 20);
-          if (loc < fail_loc) {
-            fail_loc = loc;
-            fail_pos = static_cast<std::uint64_t>(cs + static_cast<std::int64_t>(w & 2047u));
-          }
-          done = true;
-          break;
-        }
-      }
-    }
-    const std::uint32_t nb = static_cast<std::uint32_t>(__popcll(B1) + __popcll(B2));
-    if (nb) {
-      if (nb > res_left) {  // a new reservation (the old one's unused slots become empty entries)
-        pad_big(res_base, res_left);
-        const std::uint32_t want = std::max(nb, kBigReserve);
-        std::uint64_t got_base = 0;
-        if (lane == 0)
-          got_base = atomicAdd(reinterpret_cast<unsigned long long*>(&a.res[6]), static_cast<unsigned long long>(want));
-        res_base = readlane64(got_base, 0);
-        res_left = want;
-      }
-      const std::uint64_t bbase = res_base + __popcll(B1 & lt) + __popcll(B2 & lt);
-      res_base += nb;
-      res_left -= nb;
-      const std::uint64_t key = r << 32;
-      if (b1 && bbase < a.cap_big) {
-        a.big_off[bbase] = L.p0 + 8;
-        a.big_len[bbase] = L.r0;
-        a.big_crc[bbase] = L.c0;
-        a.big_key[bbase] = key | idx0;
-        a.big_tag[bbase] = static_cast<std::uint8_t>(exact);
-      }
-      const std::uint64_t bb2 = bbase + (b1 ? 1u : 0u);
-      if (b2 && bb2 < a.cap_big) {
-        a.big_off[bb2] = L.p1 + 8;
-        a.big_len[bb2] = L.r1;
-        a.big_crc[bb2] = L.c1;
-        a.big_key[bb2] = key | (idx0 + 1);
-        a.big_tag[bb2] = static_cast<std::uint8_t>(exact);
-      }
-    }
-    nrec += static_cast<std::uint64_t>(__popcll(G1) + __popcll(G2));
-    P = pexit;
-    if (sexit == 2u) {  // a record that fails its key/value bounds: the region's last
-      if (nrec < fail_loc) {
-        fail_loc = nrec;
-        fail_pos = pexit;
-      }
-      done = true;
-    } else if (sexit == 1u) {
-      brk = 1;
-      done = true;
-    } else if (P >= re) {
-      done = true;
-    }
-    __builtin_amdgcn_wave_barrier();  // this chunk's LDS reads before the next chunk's writes
-  };
-
-  // Two chunk buffers: while one is processed the other's loads are in flight. Unrolled by hand (a
-  // buffer indexed at run time would live in scratch); two copies of the chunk step keep the kernel
-  // inside the instruction cache (six copies, 104 KB of code, ran at half the speed). The loads are
-  // issued unconditionally (clamped inside the image) so that the compiler's wait counting sees
-  // straight-line code and waits for a buffer only when it is used.
-  ChunkRegs ka, kb;
-  auto step = [&](std::uint64_t c, const ChunkRegs& k) __attribute__((always_inline)) {
-    if (c <= c_last && !done) process(c, k);
-  };
-  chunk_issue(al, lim, c_first, lane, ka);
-  for (std::uint64_t c = c_first; c <= c_last && !done; c += 2) {
-    chunk_issue(al, lim, c + 1, lane, kb);
-    step(c, ka);
-    chunk_issue(al, lim, c + 2, lane, ka);
-    step(c + 1, kb);
-  }
-  pad_big(res_base, res_left);
-  if (S == kNone) {  // no plausible header in the region
-    if (!exact) {
-      a.S[r] = kNone;
-      a.X[r] = kNone;
-      a.broke[r] = 0;
-      a.spec_cnt[r] = 0;
-      a.next[r] = a.K;
-      a.first_loc[r] = kNone;
-    }
+  const std::uint64_t k = k_lo + gid();
+  if (k >= k_hi) return;
+  const std::uint64_t s = k == 0 ? 0 : a.S[k];
+  if (k == 0) a.S[0] = 0;
+  if (s == kNone) {
+    a.X[k] = kNone;
+    a.next[k] = a.K;
+    a.broke[k] = 0;
+    a.spec_cnt[k] = 0;
+    a.first_loc[k] = kNone;
     return;
   }
-  if (fail_loc != kNone) brk = 2;
-  if (lane == 0) {
-    if (!exact) {
-      a.S[r] = S;
-      a.X[r] = P;
-      a.broke[r] = static_cast<std::uint8_t>(brk);
-      a.spec_cnt[r] = nrec;
-      a.next[r] = (brk != 0 || P >= size) ? a.K : static_cast<std::uint32_t>(P / a.RS);
-    } else {
-      a.Xe[r] = P;
-      a.Be[r] = static_cast<std::uint8_t>(brk);
-      a.cnt[r] = nrec;
-    }
-    a.first_loc[r] = fail_loc;
-    a.first_pos[r] = fail_pos;
-  }
+  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
+  std::uint64_t x, c;
+  std::uint8_t br;
+  walk_check(lds, kc, a, k, s, &x, &br, &c);
+  a.X[k] = x;
+  a.broke[k] = br;
+  a.spec_cnt[k] = c;
+  a.next[k] = (br || x >= a.size) ? a.K : static_cast<std::uint32_t>(x / kWalPiece);
 }
 
 __global__ void wal_jump_init(WalArgs a) {
@@ -558,7 +397,7 @@ __global__ void wal_jump_init(WalArgs a) {
 // 3. One quadrupling round (J = next^(4^t)): every marked k marks J(k), J(J(k)) and J(J(J(k))), then
 // J <- J o J o J o J. After round t the marks hold next^i(0) for every i < 4^(t+1), so
 // ceil(log4 K) rounds mark the whole path: half the launches of doubling, for two more dependent
-// loads per round. Marks set during the round by other threads are regions of the true path too,
+// loads per round. Marks set during the round by other threads are pieces of the true path too,
 // so reading them early is safe. K is the end of the path.
 __global__ void wal_jump(const std::uint32_t* J, std::uint32_t* J2, std::uint8_t* on, std::uint32_t K) {
   const std::uint64_t k = gid();
@@ -574,7 +413,7 @@ __global__ void wal_jump(const std::uint32_t* J, std::uint32_t* J2, std::uint8_t
   }
 }
 
-// Entry points: each on-path region hands its exit to the region that holds it (one writer each:
+// Entry points: each on-path piece hands its exit to the piece that holds it (one writer each:
 // the path is a simple chain).
 __global__ void wal_link(WalArgs a) {
   const std::uint64_t k = gid();
@@ -584,8 +423,9 @@ __global__ void wal_link(WalArgs a) {
   if (n < a.K) a.entry[n] = a.X[k];
 }
 
-// 3'. Records of an on-path region from its entry: the speculative walk's when it started there;
-// otherwise the region is flagged for the exact walk (res[5] counts them). Off-path regions count 0.
+// 4. Records of an on-path piece from its entry: the speculative walk's when it started there;
+// otherwise an exact walk (the records are checked again by wal_recheck). res[0] = the first piece
+// whose speculative exit was wrong; res[5] counts re-checked pieces. Off-path pieces count 0.
 __global__ void wal_count(WalArgs a) {
   const std::uint64_t k = gid();
   if (k >= a.K) return;
@@ -593,86 +433,109 @@ __global__ void wal_count(WalArgs a) {
     a.cnt[k] = 0;
     return;
   }
-  if (a.entry[k] == a.S[k]) {
-    a.cnt[k] = a.spec_cnt[k];
-    a.Xe[k] = a.X[k];
-    a.Be[k] = a.broke[k];
-    if (a.next[k] >= a.K) {
-      a.res[1] = a.X[k];
-      a.res[2] = a.broke[k] == 1 ? 1 : 0;
-    }
+  const std::uint64_t e = a.entry[k];
+  std::uint64_t p, packed;
+  bool bad;
+  if (e == a.S[k]) {
+    p = a.X[k];
+    bad = a.broke[k] != 0;
+    packed = a.spec_cnt[k];
   } else {
+    const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
+    std::uint64_t n_all = 0, n_big = 0;
+    p = e;
+    bad = false;
+    while (p < limit) {  // wal.cpp:63-87
+      if (a.size - p < kWalMeta) {
+        bad = true;
+        break;
+      }
+      const std::uint64_t rlen = ld32(a.w, p, a.size);
+      if (rlen + 8 > a.size - p) {
+        bad = true;
+        break;
+      }
+      ++n_all;
+      n_big += rlen > kWalLaneMax ? 1u : 0u;
+      p += 8 + rlen;
+    }
+    packed = (n_all << 32) | n_big;
     a.recheck[k] = 1;
     atomicAdd(reinterpret_cast<unsigned long long*>(&a.res[5]), 1ull);
+    if (p != a.X[k] || bad != (a.broke[k] != 0)) atomicMin(reinterpret_cast<unsigned long long*>(&a.res[0]), k);
   }
-}
-
-// After the exact walks: res[0] = the first region whose speculative exit was wrong.
-__global__ void wal_count_exact(WalArgs a) {
-  const std::uint64_t k = gid();
-  if (k >= a.K || !a.on[k] || !a.recheck[k]) return;
-  if (a.Xe[k] != a.X[k] || a.Be[k] != a.broke[k]) atomicMin(reinterpret_cast<unsigned long long*>(&a.res[0]), k);
+  a.cnt[k] = packed;
+  a.Xe[k] = p;
+  a.Be[k] = bad ? 1 : 0;
   if (a.next[k] >= a.K) {
-    a.res[1] = a.Xe[k];
-    a.res[2] = a.Be[k] == 1 ? 1 : 0;
+    a.res[1] = p;
+    a.res[2] = bad ? 1 : 0;
   }
 }
 
-// Regions past the first one with a wrong speculative exit are not on the true chain (or not known
-// to be): drop them.
+// Pieces entered off their speculative start: check their records from the true entry.
+__global__ __launch_bounds__(kCheckThreads) void wal_recheck(WalArgs a) {
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  fill_slices(a.tabs, lds);
+  const std::uint64_t k = gid();
+  if (k >= a.K || !a.recheck[k]) return;
+  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
+  std::uint64_t x, c;
+  std::uint8_t br;
+  walk_check(lds, kc, a, k, a.entry[k], &x, &br, &c);
+}
+
+// Records past the first piece with a wrong speculative exit are not on the true chain (or not
+// known to be): drop them.
 __global__ void wal_trim(WalArgs a, std::uint64_t kstar) {
   const std::uint64_t k = gid();
   if (k < a.K && k > kstar) a.cnt[k] = 0;
 }
 
-// 4. The first failing record of each counted region (bounds, or CRC of a folded payload), as a
-// record index.
-__global__ void wal_gather(WalArgs a, std::uint64_t kstar) {
+// 5. Record numbering: the first failing record of each counted piece becomes a record index, and
+// the big-record slots move to the dense list the CRC batch reads.
+__global__ void wal_gather(WalArgs a) {
   const std::uint64_t k = gid();
-  if (k >= a.K || !a.on[k] || k > kstar) return;
-  const std::uint64_t f = a.first_loc[k];
-  if (f != kNone) {
-    a.bad_at[k] = a.base[k] + f;
-    atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), a.base[k] + f);
+  if (k >= a.K || a.cnt[k] == 0) return;
+  const std::uint64_t b_all = a.base[k] >> 32, b_big = a.base[k] & 0xFFFFFFFFull;
+  const std::uint64_t n_big = a.cnt[k] & 0xFFFFFFFFull;
+  if (a.first_loc[k] != kNone) {
+    a.bad_at[k] = b_all + a.first_loc[k];
+    atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), b_all + a.first_loc[k]);
+  }
+  for (std::uint64_t j = 0; j < n_big; ++j) {
+    const std::uint64_t sl = 2 * k + j;
+    a.big_off[b_big + j] = a.slot_off[sl];
+    a.big_len[b_big + j] = a.slot_len[sl];
+    a.big_crc[b_big + j] = a.slot_crc[sl];
+    a.big_idx[b_big + j] = b_all + a.slot_loc[sl];
   }
 }
 
-// A big-list entry counts when its region is counted and it comes from that region's final walk.
-__device__ __forceinline__ bool big_valid(const WalArgs& a, std::uint64_t i, std::uint64_t kstar, std::uint64_t* idx) {
-  const std::uint64_t key = a.big_key[i];
-  const std::uint64_t k = key >> 32;
-  if (k >= a.K || !a.on[k] || k > kstar || a.big_tag[i] != a.recheck[k]) return false;
-  *idx = a.base[k] + (key & 0xFFFFFFFFull);
-  return true;
-}
-
-__global__ void wal_check_big(WalArgs a, std::uint64_t n, std::uint64_t kstar) {
+__global__ void wal_check_big(WalArgs a, std::uint64_t n) {
   const std::uint64_t i = gid();
-  std::uint64_t idx;
-  if (i < n && a.got[i] != a.big_crc[i] && big_valid(a, i, kstar, &idx))
-    atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), idx);
+  if (i < n && a.got[i] != a.big_crc[i]) atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), a.big_idx[i]);
 }
 
-// Start of the first bad record (res[3]): from the region that found it, or from the big list.
-__global__ void wal_bad_pos(WalArgs a, std::uint64_t n_big, std::uint64_t kstar) {
+// Start of the first bad record (res[3]): from the piece that found it, or from the big list.
+__global__ void wal_bad_pos(WalArgs a, std::uint64_t n_big) {
   const std::uint64_t i = gid();
   const std::uint64_t want = a.res[3];
-  if (i < a.K && a.on[i] && i <= kstar && a.bad_at[i] == want) a.res[4] = a.first_pos[i];
-  std::uint64_t idx;
-  if (i < n_big && a.got[i] != a.big_crc[i] && big_valid(a, i, kstar, &idx) && idx == want) a.res[4] = a.big_off[i] - 8;
+  if (i < a.K && a.cnt[i] != 0 && a.bad_at[i] == want) a.res[4] = a.first_pos[i];
+  if (i < n_big && a.big_idx[i] == want) a.res[4] = a.big_off[i] - 8;
 }
 
 // Per-device scratch, grown by doubling and kept between calls (guarded by mu).
 struct WalScratch {
   std::mutex mu;
-  std::uint64_t cap_regions = 0, cap_big = 0;
-  void* regions = nullptr;  // per region: 10 u64, 3 u32, 4 u8 (carve)
-  void* bigs = nullptr;     // per big record: 2 u64, 3 u32, 1 u8
+  std::uint64_t cap_pieces = 0, cap_big = 0;
+  void* pieces = nullptr;  // per piece: 13 u64, 9 u32, 4 u8 (carve)
+  void* bigs = nullptr;    // per big record: 2 u64, 3 u32
   void* cub = nullptr;
   std::size_t cub_bytes = 0;
   std::uint64_t* res = nullptr;
   std::uint64_t* h_res = nullptr;
-  unsigned ncu = 0;              // the device's compute units (region sizing)
+  std::uint32_t* inj = nullptr;  // Shift_L(0xFFFFFFFF), L = 0..kWalLaneMax
   // host images: device copy, pinned staging slabs for pageable sources, own stream
   std::uint8_t* d_img = nullptr;
   std::uint64_t cap_img = 0;
@@ -693,10 +556,11 @@ struct WalScratch {
       if (slab_free[i]) (void)hipEventDestroy(slab_free[i]);
     }
     if (st) (void)hipStreamDestroy(st);
-    (void)hipFree(regions);
+    (void)hipFree(pieces);
     (void)hipFree(bigs);
     (void)hipFree(cub);
     (void)hipFree(res);
+    (void)hipFree(inj);
     (void)hipHostFree(h_res);
   }
 };
@@ -705,9 +569,7 @@ std::mutex g_wal_mu;
 WalScratch* g_wal[64] = {};
 
 // What the calling thread's last WAL verify did (tkv_debug_wal_last).
-thread_local std::uint64_t g_last[4] = {0, 0, 0, 0};  // passes, host walk needed, image copied, regions
-// Region size forced by tkv_debug_wal_region (0: sized from the image and the device).
-std::atomic<std::uint64_t> g_region_force{0};
+thread_local std::uint64_t g_last[4] = {0, 0, 0, 0};  // passes, host walk needed, image copied, pieces
 
 #define WAL_HIP(call)                                                            \
   do {                                                                           \
@@ -715,25 +577,14 @@ std::atomic<std::uint64_t> g_region_force{0};
     if (e_ != hipSuccess) return set_error(TKV_IO_ERROR, hipGetErrorString(e_)); \
   } while (0)
 
-// About two regions per wave slot of the device (kRegWaves per CU), a power of two in
-// [kRegionMin, kRegionMax].
-std::uint64_t region_size(std::uint64_t size, unsigned ncu) {
-  const std::uint64_t forced = g_region_force.load(std::memory_order_relaxed);
-  if (forced) return forced;
-  const std::uint64_t slots = std::max<std::uint64_t>(1, 2ull * ncu * kRegWaves);
-  std::uint64_t rs = kRegionMin;
-  while (rs < kRegionMax && 2 * rs * slots <= size) rs *= 2;
-  return rs;
-}
-
-int grow_regions(WalScratch& s, std::uint64_t K) {
-  if (K <= s.cap_regions) return TKV_OK;
-  const std::uint64_t cap = std::max<std::uint64_t>(K, 2 * s.cap_regions);
-  WAL_HIP(hipFree(s.regions));
-  s.regions = nullptr;
-  s.cap_regions = 0;
-  WAL_HIP(hipMalloc(&s.regions, cap * (10 * 8 + 3 * 4 + 4)));
-  s.cap_regions = cap;
+int grow_pieces(WalScratch& s, std::uint64_t K) {
+  if (K <= s.cap_pieces) return TKV_OK;
+  const std::uint64_t cap = std::max<std::uint64_t>(K, 2 * s.cap_pieces);
+  WAL_HIP(hipFree(s.pieces));
+  s.pieces = nullptr;
+  s.cap_pieces = 0;
+  WAL_HIP(hipMalloc(&s.pieces, cap * (13 * 8 + 9 * 4 + 4)));
+  s.cap_pieces = cap;
   return TKV_OK;
 }
 
@@ -743,44 +594,45 @@ int grow_big(WalScratch& s, std::uint64_t n) {
   WAL_HIP(hipFree(s.bigs));
   s.bigs = nullptr;
   s.cap_big = 0;
-  WAL_HIP(hipMalloc(&s.bigs, cap * (2 * 8 + 3 * 4 + 1)));
+  WAL_HIP(hipMalloc(&s.bigs, cap * (2 * 8 + 3 * 4)));
   s.cap_big = cap;
   return TKV_OK;
 }
 
-WalArgs carve(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std::uint64_t RS, std::uint32_t K,
-              const DeviceTables* tabs) {
+WalArgs carve(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std::uint32_t K, const DeviceTables* tabs) {
   WalArgs a{};
   a.w = w;
   a.size = size;
-  a.RS = RS;
   a.K = K;
-  const std::uint64_t C = s.cap_regions;
-  auto* p8 = static_cast<std::uint64_t*>(s.regions);
+  const std::uint64_t C = s.cap_pieces;
+  auto* p8 = static_cast<std::uint64_t*>(s.pieces);
   std::uint64_t** u64s[] = {&a.S, &a.X, &a.spec_cnt, &a.first_loc, &a.first_pos, &a.entry, &a.cnt, &a.base, &a.Xe,
                             &a.bad_at};
   for (std::size_t i = 0; i < sizeof(u64s) / sizeof(u64s[0]); ++i) *u64s[i] = p8 + i * C;
-  auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 10 * C);
+  a.slot_off = p8 + 10 * C;  // 2C
+  auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 13 * C);
   a.next = p4;
   a.Ja = p4 + C;
   a.Jb = p4 + 2 * C;
-  auto* p1 = reinterpret_cast<std::uint8_t*>(p4 + 3 * C);
+  a.slot_len = p4 + 3 * C;  // 2C each
+  a.slot_crc = p4 + 5 * C;
+  a.slot_loc = p4 + 7 * C;
+  auto* p1 = reinterpret_cast<std::uint8_t*>(p4 + 9 * C);
   a.broke = p1;
   a.on = p1 + C;
   a.Be = p1 + 2 * C;
   a.recheck = p1 + 3 * C;
   const std::uint64_t B = s.cap_big;
-  a.cap_big = B;
   if (B) {
     auto* b8 = static_cast<std::uint64_t*>(s.bigs);
     a.big_off = b8;
-    a.big_key = b8 + B;
+    a.big_idx = b8 + B;
     auto* b4 = reinterpret_cast<std::uint32_t*>(b8 + 2 * B);
     a.big_len = b4;
     a.big_crc = b4 + B;
     a.got = b4 + 2 * B;
-    a.big_tag = reinterpret_cast<std::uint8_t*>(b4 + 3 * B);
   }
+  a.inj = s.inj;
   a.tabs = tabs;
   a.res = s.res;
   return a;
@@ -796,43 +648,42 @@ struct PassResult {
   std::uint64_t stop = 0;  // where decoding stopped (relative to the pass's start)
   bool corrupted = false;
   bool resume = false;     // the chain continues at `stop` (a true record start) beyond what was checked
-  bool retry = false;      // the big list overflowed its scratch (now grown): run the pass again
 };
 
 // A pass over the image [w, w + size), which starts with a record (or is empty), in three parts:
-// pass_begin (result words), pass_front over ranges of regions (the speculative walks; each range's
-// bytes and the next kFrontMargin bytes must be resident), pass_tail.
+// pass_begin (result words, speculative starts cleared), pass_front over ranges of pieces (scan and
+// speculative walk; each range's bytes and the next 1 KiB + 26 bytes must be resident), pass_tail.
 int pass_begin(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream_t st, WalArgs* out) {
-  const std::uint64_t RS = region_size(size, s.ncu);
-  const std::uint32_t K = static_cast<std::uint32_t>((size + RS - 1) / RS);
+  const std::uint32_t K = static_cast<std::uint32_t>((size + kWalPiece - 1) / kWalPiece);
   const DeviceTables* tabs = device_tables(kAlgoCrc32);
   if (!tabs) return TKV_IO_ERROR;
-  if (int rc = grow_regions(s, K)) return rc;
-  if (int rc = grow_big(s, std::max<std::uint64_t>(std::uint64_t(1) << 16, size >> 10))) return rc;
-  WalArgs a = carve(s, w, size, RS, K, tabs);
-  for (int i = 0; i < 8; ++i) s.h_res[i] = 0;
+  if (int rc = grow_pieces(s, K)) return rc;
+  WalArgs a = carve(s, w, size, K, tabs);
   s.h_res[0] = kNone;
   s.h_res[1] = size;
+  s.h_res[2] = 0;
   s.h_res[3] = kNone;
-  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 8 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
+  s.h_res[4] = 0;
+  s.h_res[5] = 0;
+  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 6 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
+  WAL_HIP(hipMemsetAsync(a.S, 0xFF, K * sizeof(std::uint64_t), st));
   *out = a;
   return TKV_OK;
 }
 
-// Bytes past a region that its walk may read: the halo of its last chunk and the payloads of at
-// most kWalFold bytes of its last records (header, 16-byte granules).
-constexpr std::uint64_t kFrontTail = 2 * kChunk + kWalFold + 64;
-
 void pass_front(const WalArgs& a, std::uint64_t k_lo, std::uint64_t k_hi, hipStream_t st) {
   if (k_hi <= k_lo) return;
-  hipLaunchKernelGGL(wal_region, dim3(blocks(k_hi - k_lo, kRegWaves)), dim3(kRegThreads), 0, st, a, k_lo, k_hi, 0);
+  const std::uint64_t threads = (k_hi - k_lo + 64 / kHeadLanes - 1) / (64 / kHeadLanes) * 64;  // 8 pieces per wave
+  hipLaunchKernelGGL(wal_scan_head, dim3(blocks(threads, kScanThreads)), dim3(kScanThreads), 0, st, a, k_lo, k_hi);
+  hipLaunchKernelGGL(wal_spec, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
 }
 
 int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
   const std::uint8_t* w = a.w;
   const std::uint64_t size = a.size;
   const std::uint32_t K = a.K;
-  // 3: the regions on the true chain and their entries
+  const DeviceTables* tabs = a.tabs;
+  // 3: the pieces on the true chain and their entries
   hipLaunchKernelGGL(wal_jump_init, dim3(blocks(K, 256)), dim3(256), 0, st, a);
   std::uint32_t* J = a.Ja;
   std::uint32_t* J2 = a.Jb;
@@ -841,24 +692,16 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
     std::swap(J, J2);
   }
   hipLaunchKernelGGL(wal_link, dim3(blocks(K, 256)), dim3(256), 0, st, a);
+  // 4: record counts from the entries
   hipLaunchKernelGGL(wal_count, dim3(blocks(K, 256)), dim3(256), 0, st, a);
-  // regions entered off their speculative start, walked again from the entry (most workgroups find
-  // no such region among their eight and end before filling their tables)
-  hipLaunchKernelGGL(wal_region, dim3(blocks(K, kRegWaves)), dim3(kRegThreads), 0, st, a, 0, K, 1);
-  hipLaunchKernelGGL(wal_count_exact, dim3(blocks(K, 256)), dim3(256), 0, st, a);
   WAL_HIP(hipGetLastError());
-  WAL_HIP(hipMemcpyAsync(s.h_res, s.res, 8 * sizeof(std::uint64_t), hipMemcpyDeviceToHost, st));
+  WAL_HIP(hipMemcpyAsync(s.h_res, s.res, 6 * sizeof(std::uint64_t), hipMemcpyDeviceToHost, st));
   WAL_HIP(hipStreamSynchronize(st));
-  if (s.h_res[6] > s.cap_big) {  // the big list did not fit: grow it and run the pass again
-    if (int rc = grow_big(s, s.h_res[6])) return rc;
-    r->retry = true;
-    return TKV_OK;
-  }
   const std::uint64_t kstar = s.h_res[0];
   std::uint64_t chain_end = s.h_res[1];
   bool broke = s.h_res[2] != 0;
-  const std::uint64_t n_big = s.h_res[6];
   const bool partial = kstar < K;
+  if (s.h_res[5]) hipLaunchKernelGGL(wal_recheck, dim3(blocks(K, kCheckThreads)), dim3(kCheckThreads), 0, st, a);
   if (partial) {
     hipLaunchKernelGGL(wal_trim, dim3(blocks(K, 256)), dim3(256), 0, st, a, kstar);
     std::uint8_t be = 0;
@@ -866,9 +709,9 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
     WAL_HIP(hipMemcpyAsync(&be, a.Be + kstar, 1, hipMemcpyDeviceToHost, st));
     WAL_HIP(hipStreamSynchronize(st));
     chain_end = s.h_res[1];
-    broke = be == 1;
+    broke = be != 0;
   }
-  // 4: record numbering, the first bad record (regions, then the CRC batch of the big ones)
+  // 5: record numbering, first failing in-lane record, the CRC batch of the big ones
   std::size_t need = 0;
   WAL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, a.cnt, a.base, K, st));
   if (need > s.cub_bytes) {
@@ -880,44 +723,45 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
     s.cub_bytes = need;
   }
   WAL_HIP(hipcub::DeviceScan::ExclusiveSum(s.cub, need, a.cnt, a.base, K, st));
-  const std::uint64_t ks = partial ? kstar : K;
-  hipLaunchKernelGGL(wal_gather, dim3(blocks(K, 256)), dim3(256), 0, st, a, ks);
-  WAL_HIP(hipGetLastError());
-  for (std::uint64_t i = 0; i < n_big; i += kWalCrcChunk) {
-    const std::uint64_t m = std::min(kWalCrcChunk, n_big - i);
-    if (int rc = batch_device_impl(kAlgoCrc32, w, a.big_off + i, a.big_len + i, nullptr, a.got + i, m, st)) return rc;
-  }
-  if (n_big) hipLaunchKernelGGL(wal_check_big, dim3(blocks(n_big, 256)), dim3(256), 0, st, a, n_big, ks);
-  hipLaunchKernelGGL(wal_bad_pos, dim3(blocks(std::max<std::uint64_t>(K, n_big), 256)), dim3(256), 0, st, a, n_big,
-                     ks);
-  WAL_HIP(hipGetLastError());
-  WAL_HIP(hipMemcpyAsync(s.h_res + 3, s.res + 3, 2 * sizeof(std::uint64_t), hipMemcpyDeviceToHost, st));
-  WAL_HIP(hipMemcpyAsync(s.h_res + 7, a.base + (K - 1), 8, hipMemcpyDeviceToHost, st));
+  WAL_HIP(hipMemcpyAsync(s.h_res + 5, a.base + (K - 1), 8, hipMemcpyDeviceToHost, st));
   WAL_HIP(hipMemcpyAsync(s.h_res + 6, a.cnt + (K - 1), 8, hipMemcpyDeviceToHost, st));
   WAL_HIP(hipStreamSynchronize(st));
-  const std::uint64_t n = s.h_res[7] + s.h_res[6];  // good records counted
-  const bool bad = s.h_res[3] != kNone;
-  r->good = bad ? std::min(s.h_res[3], n) : n;
-  r->corrupted = bad || broke;
-  r->stop = bad ? s.h_res[4] : chain_end;
+  const std::uint64_t tot = s.h_res[5] + s.h_res[6];  // (records << 32) | big records
+  const std::uint64_t n = tot >> 32, n_big = tot & 0xFFFFFFFFull;
+  std::uint64_t first = n;
+  if (n) {
+    if (int rc = grow_big(s, std::max<std::uint64_t>(n_big, 1))) return rc;
+    a = carve(s, w, size, K, tabs);
+    hipLaunchKernelGGL(wal_gather, dim3(blocks(K, 256)), dim3(256), 0, st, a);
+    WAL_HIP(hipGetLastError());
+    for (std::uint64_t i = 0; i < n_big; i += kWalCrcChunk) {
+      const std::uint64_t m = std::min(kWalCrcChunk, n_big - i);
+      if (int rc = batch_device_impl(kAlgoCrc32, w, a.big_off + i, a.big_len + i, nullptr, a.got + i, m, st)) return rc;
+    }
+    if (n_big) hipLaunchKernelGGL(wal_check_big, dim3(blocks(n_big, 256)), dim3(256), 0, st, a, n_big);
+    hipLaunchKernelGGL(wal_bad_pos, dim3(blocks(std::max<std::uint64_t>(K, n_big), 256)), dim3(256), 0, st, a, n_big);
+    WAL_HIP(hipGetLastError());
+    WAL_HIP(hipMemcpyAsync(s.h_res + 3, s.res + 3, 2 * sizeof(std::uint64_t), hipMemcpyDeviceToHost, st));
+    WAL_HIP(hipStreamSynchronize(st));
+    first = std::min<std::uint64_t>(s.h_res[3], n);
+  }
+  r->good = first;
+  r->corrupted = first < n || broke;
+  r->stop = first < n ? s.h_res[4] : chain_end;
   r->resume = !r->corrupted && partial && chain_end < size;
   return TKV_OK;
 }
 
 // A whole pass over a resident image.
 int wal_pass(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream_t st, PassResult* r) {
-  for (int attempt = 0; attempt < 3; ++attempt) {
-    WalArgs a;
-    if (int rc = pass_begin(s, w, size, st, &a)) return rc;
-    pass_front(a, 0, a.K, st);
-    *r = PassResult{};
-    if (int rc = pass_tail(s, a, st, r)) return rc;
-    if (!r->retry) return TKV_OK;
-  }
-  return set_error(TKV_IO_ERROR, "WAL verify: big-record list kept overflowing");
+  WalArgs a;
+  if (int rc = pass_begin(s, w, size, st, &a)) return rc;
+  pass_front(a, 0, a.K, st);
+  return pass_tail(s, a, st, r);
 }
 
-// The calling thread's device's scratch (created on first use, with its result words).
+// The calling thread's device's scratch (created on first use, with its result words and the
+// init-term table).
 int scratch(WalScratch** out) {
   int dev = 0;
   WAL_HIP(hipGetDevice(&dev));
@@ -935,7 +779,10 @@ int scratch(WalScratch** out) {
     WAL_HIP(hipStreamCreateWithFlags(&sp->st, hipStreamNonBlocking));
     WAL_HIP(hipStreamCreateWithFlags(&sp->stc, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) WAL_HIP(hipEventCreateWithFlags(&sp->landed[i], hipEventDisableTiming));
-    WAL_HIP(hipDeviceGetAttribute(reinterpret_cast<int*>(&sp->ncu), hipDeviceAttributeMultiprocessorCount, dev));
+    std::vector<std::uint32_t> inj(kWalLaneMax + 1);
+    for (std::uint32_t L = 0; L <= kWalLaneMax; ++L) inj[L] = shift_bytes(kInit, L, kPoly);
+    WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->inj), inj.size() * 4));
+    WAL_HIP(hipMemcpy(sp->inj, inj.data(), inj.size() * 4, hipMemcpyHostToDevice));
   }
   *out = sp;
   return TKV_OK;
@@ -944,20 +791,17 @@ int scratch(WalScratch** out) {
 int verify_locked(WalScratch& s, const std::uint8_t* d_wal, std::uint64_t size, std::uint64_t* n_good,
                   std::uint64_t* stop_offset, hipStream_t st, bool* needs_host_walk,
                   const PassResult* first_pass = nullptr) {
-  // Each pass checks the true chain at least through its first region; a pass that stops short of
+  // Each pass checks the true chain at least through its first piece; a pass that stops short of
   // the end without a verdict resumes at a true record start. Adversarial images that keep the
   // speculation wrong go to the exact host walk after kMaxPasses.
   constexpr int kMaxPasses = 8;
   std::uint64_t start = 0, good = 0;
   g_last[0] = g_last[1] = 0;
-  {
-    const std::uint64_t RS = region_size(size, s.ncu);
-    g_last[3] = (size + RS - 1) / RS;
-  }
+  g_last[3] = (size + kWalPiece - 1) / kWalPiece;
   for (int pass = 0; pass < kMaxPasses; ++pass) {
     PassResult r;
     g_last[0] = static_cast<std::uint64_t>(pass) + 1;
-    if (pass == 0 && first_pass && !first_pass->retry) r = *first_pass;
+    if (pass == 0 && first_pass) r = *first_pass;
     else if (int rc = wal_pass(s, d_wal + start, size - start, st, &r)) return rc;
     good += r.good;
     if (!r.resume) {
@@ -989,7 +833,6 @@ void stage_copy(std::uint8_t* dst, const std::uint8_t* src, std::uint64_t n) {
 }
 
 constexpr std::uint64_t kStageSlab = std::uint64_t(64) << 20;
-constexpr std::uint64_t kMaxImage = std::uint64_t(1) << 46;  // regions stay below 2^32
 
 }  // namespace
 
@@ -1000,20 +843,14 @@ int wal_verify_device_impl(const std::uint8_t* d_wal, std::uint64_t size, std::u
   *stop_offset = 0;
   g_last[0] = g_last[1] = g_last[2] = g_last[3] = 0;
   if (size == 0) return TKV_OK;
-  if (size >= kMaxImage) return set_error(TKV_INVALID_ARGUMENT, "WAL image too large for the device walk");
+  if ((size + kWalPiece - 1) / kWalPiece >= 0xFFFFFFFFull)
+    return set_error(TKV_INVALID_ARGUMENT, "WAL image too large for the device walk");
   WalScratch* sp = nullptr;
   if (int rc = scratch(&sp)) return rc;
   WalScratch& s = *sp;
   std::lock_guard<std::mutex> lk(s.mu);
   return verify_locked(s, d_wal, size, n_good, stop_offset, st, needs_host_walk);
 }
-
-int wal_verify_host_image_body(WalScratch& s, const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
-                               std::uint64_t* stop_offset, bool* needs_host_walk);
-
-// Device copies of host images above this size are freed after the verify (a multi-GiB recovery must
-// not hold that much HBM for the rest of the process); smaller ones are kept for the next call.
-constexpr std::uint64_t kKeepImage = std::uint64_t(1) << 30;
 
 int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
                                std::uint64_t* stop_offset, bool* needs_host_walk) {
@@ -1022,7 +859,7 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
   *stop_offset = 0;
   g_last[0] = g_last[1] = g_last[2] = g_last[3] = 0;
   if (size == 0) return TKV_OK;
-  if (size >= kMaxImage) {
+  if ((size + kWalPiece - 1) / kWalPiece >= 0xFFFFFFFFull) {
     *needs_host_walk = true;
     return TKV_OK;
   }
@@ -1030,21 +867,6 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
   if (int rc = scratch(&sp)) return rc;
   WalScratch& s = *sp;
   std::lock_guard<std::mutex> lk(s.mu);
-  const int rc = wal_verify_host_image_body(s, h_wal, size, n_good, stop_offset, needs_host_walk);
-  // Whatever happened, no copy that reads the caller's buffer or writes d_img is left in flight.
-  const hipError_t e0 = hipStreamSynchronize(s.st), e1 = hipStreamSynchronize(s.stc);
-  if (s.cap_img > kKeepImage) {
-    (void)hipFree(s.d_img);
-    s.d_img = nullptr;
-    s.cap_img = 0;
-  }
-  if (rc == TKV_OK && (e0 != hipSuccess || e1 != hipSuccess))
-    return set_error(TKV_IO_ERROR, hipGetErrorString(e0 != hipSuccess ? e0 : e1));
-  return rc;
-}
-
-int wal_verify_host_image_body(WalScratch& s, const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
-                               std::uint64_t* stop_offset, bool* needs_host_walk) {
   g_last[2] = 1;
   if (size > s.cap_img) {
     (void)hipStreamSynchronize(s.st);
@@ -1072,9 +894,10 @@ int wal_verify_host_image_body(WalScratch& s, const std::uint8_t* h_wal, std::ui
   }
   // The image goes over in chunks on the copy stream (pageable sources through two pinned slabs that
   // host threads fill while the copy engine drains the other). As each chunk lands, the compute
-  // stream walks the regions before it whose bytes are all resident (regions ending at least
-  // kFrontTail bytes before the end of what has landed), so only the last chunk's regions and the
-  // stitching remain once the copy is done.
+  // stream scans and speculatively walks the pieces before it whose records' bytes are all resident
+  // (pieces ending at least kFrontMargin bytes before the end of what has landed), so only the last
+  // chunk's pieces and the stitching remain once the copy is done.
+  constexpr std::uint64_t kFrontMargin = kWalPiece + kWalLaneMax + 64;
   WalArgs a;
   if (int rc = pass_begin(s, s.d_img, size, s.stc, &a)) return rc;
   std::uint64_t fronted = 0;
@@ -1092,7 +915,7 @@ int wal_verify_host_image_body(WalScratch& s, const std::uint8_t* h_wal, std::ui
     WAL_HIP(hipEventRecord(s.landed[k], s.st));
     WAL_HIP(hipStreamWaitEvent(s.stc, s.landed[k], 0));
     const bool last = off + m >= size;
-    const std::uint64_t k_hi = last ? a.K : (off + m > kFrontTail ? (off + m - kFrontTail) / a.RS : 0);
+    const std::uint64_t k_hi = last ? a.K : (off + m > kFrontMargin ? (off + m - kFrontMargin) / kWalPiece : 0);
     if (k_hi > fronted) {
       pass_front(a, fronted, k_hi, s.stc);
       fronted = k_hi;
@@ -1109,10 +932,4 @@ int wal_verify_host_image_body(WalScratch& s, const std::uint8_t* h_wal, std::ui
 
 extern "C" void tkv_debug_wal_last(uint64_t out[4]) {
   for (int i = 0; i < 4; ++i) out[i] = tkv::g_last[i];
-}
-
-extern "C" uint64_t tkv_debug_wal_region(uint64_t bytes) {
-  // rounded up to whole chunks; 0 restores the automatic size
-  const std::uint64_t rs = bytes ? (bytes + tkv::kChunk - 1) / tkv::kChunk * tkv::kChunk : 0;
-  return tkv::g_region_force.exchange(rs);
 }
