@@ -240,7 +240,8 @@ int tkv_debug_multi_combine(uint32_t poly, int ndev, const uint64_t *h_offsets, 
 void tkv_debug_update_counts(uint64_t out[2]);
 /* What the calling thread's last tkv_wal_verify / tkv_wal_verify_device did: out[0] = device walk
  * passes, out[1] = 1 when it handed the image to the exact host-thread walk, out[2] = 1 when a
- * host image was copied to the device, out[3] = pieces of the last pass's image. */
+ * host image was copied to the device, out[3] = 1 when every pass stitched its pieces by the fast
+ * path (no pointer jumping). */
 void tkv_debug_wal_last(uint64_t out[4]);
 /* Which path the last irregular batch on `stream` took: 1 = byte-stream row walk (blocks back to
  * back, each at least 64 bytes), 0 = general row walk; -1 on error. Synchronizes

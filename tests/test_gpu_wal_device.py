@@ -82,10 +82,11 @@ def make_wal(rng, n_rec, vmax=16000, giant=(), fake_headers=0.0):
 
 def wal_last():
     """What this thread's last WAL verify did (tkv_debug_wal_last): device passes, whether the exact
-    host-thread walk had to finish it, whether a host image was copied, pieces of the last pass."""
+    host-thread walk had to finish it, whether a host image was copied, whether every pass took the
+    fast stitch (no pointer jumping)."""
     out = (ctypes.c_uint64 * 4)()
     tk.load_library().tkv_debug_wal_last(out)
-    return {"passes": out[0], "host_walk": out[1], "copied": out[2], "pieces": out[3]}
+    return {"passes": out[0], "host_walk": out[1], "copied": out[2], "fast": out[3]}
 
 
 LAST = {}
@@ -105,11 +106,14 @@ def both(img, size, shift=0):
     return h, dv
 
 
-def device_walk_only(max_passes=1):
-    """Both verifies of the last `both` call finished on the device, in at most max_passes passes."""
+def device_walk_only(max_passes=1, fast=None):
+    """Both verifies of the last `both` call finished on the device, in at most max_passes passes
+    (and, if `fast` is given, with or without the pointer-jumping stitch)."""
     for path, r in LAST.items():
         assert r["host_walk"] == 0, (path, r)
         assert 1 <= r["passes"] <= max_passes, (path, r)
+        if fast is not None:
+            assert r["fast"] == fast, (path, r)
 
 
 @pytest.mark.parametrize("shift", [0, 3])
@@ -120,7 +124,7 @@ def test_small_records_clean_and_corrupted(gpu, oracle, shift):
     want = sequential_decode(oracle, img, n)
     assert want == ("ok", offs.size, n)
     assert both(img, n, shift) == (want, want)
-    device_walk_only()
+    device_walk_only(fast=1)
     assert LAST["host_image"]["copied"] == 1 and LAST["device_image"]["copied"] == 0
     for bad in (0, 1, 777, 60000, 119999):  # payload flips: CRC mismatch at that record
         o = int(offs[bad]) + int(size[bad]) - 1
@@ -158,6 +162,8 @@ def test_corrupted_record_len_and_overrun(gpu, oracle):
         want = sequential_decode(oracle, img, n)
         assert want == ("corrupted", bad, o)
         assert both(img, n) == (want, want)
+        # the chain breaks with pieces holding records after it: the fast stitch must refuse
+        device_walk_only(max_passes=8, fast=0)
         img[o:o + 4] = old
 
 

@@ -53,6 +53,7 @@ constexpr std::uint32_t kWalLaneMax = 1024;   // payloads up to this size are ch
 constexpr std::uint64_t kNone = ~0ull;
 constexpr unsigned kScanThreads = 256;        // wal_scan_head: 8 lanes per piece, 8 pieces per wave
 constexpr unsigned kCheckThreads = 1024;      // wal_spec/wal_recheck: one workgroup per CU (128 KiB of LDS)
+constexpr unsigned kHres = 16;                // words of the pinned result block
 
 struct WalArgs {
   const std::uint8_t* w;
@@ -394,6 +395,42 @@ __global__ void wal_jump_init(WalArgs a) {
   a.bad_at[k] = kNone;
 }
 
+// 3 (fast path). Takes every piece with a speculative start (S != kNone) as on the true chain and
+// entered at S, and checks that this holds: each such piece p must leave exactly into the next such
+// piece q (next(p) == q and X_p == S_q), and the last one must end the chain (next == K). Piece 0
+// is entered at 0, so by induction every such piece is then entered at S, and a piece with no
+// plausible header holds no record start of the chain (a header the encoder wrote is plausible; a
+// chain that reaches an implausible one breaks there, and next(p) == K contradicts a later piece
+// with a start). Pieces further than kFastScan pieces from the next start fail the check. When it
+// fails (res[6] = 1) the host runs the pointer-jumping stitch instead. Replaces wal_jump_init,
+// ceil(log4 K) wal_jump launches and wal_link on every image whose speculation was right.
+constexpr std::uint32_t kFastScan = 64;
+__global__ void wal_fast(WalArgs a) {
+  const std::uint64_t k = gid();
+  if (k >= a.K) return;
+  const std::uint64_t s = a.S[k];
+  const bool has = k == 0 || s != kNone;
+  a.on[k] = has ? 1 : 0;
+  a.entry[k] = k == 0 ? 0 : s;
+  a.recheck[k] = 0;
+  a.bad_at[k] = kNone;
+  if (!has) return;
+  std::uint64_t q = k + 1;
+  while (q < a.K && q - k <= kFastScan && a.S[q] == kNone) ++q;
+  bool ok;
+  if (q >= a.K) ok = a.next[k] >= a.K;
+  else ok = q - k <= kFastScan && a.next[k] == q && a.X[k] == a.S[q];
+  if (!ok) a.res[6] = 1;
+}
+
+// Result words (res[0..6]) and the record scan's last entries into the host's pinned block.
+__global__ void wal_publish(WalArgs a, std::uint64_t* h) {
+  const unsigned i = threadIdx.x;
+  if (i < 7) h[i] = a.res[i];
+  if (i == 7) h[7] = a.base[a.K - 1];
+  if (i == 8) h[8] = a.cnt[a.K - 1];
+}
+
 // 3. One quadrupling round (J = next^(4^t)): every marked k marks J(k), J(J(k)) and J(J(J(k))), then
 // J <- J o J o J o J. After round t the marks hold next^i(0) for every i < 4^(t+1), so
 // ceil(log4 K) rounds mark the whole path: half the launches of doubling, for two more dependent
@@ -534,7 +571,8 @@ struct WalScratch {
   void* cub = nullptr;
   std::size_t cub_bytes = 0;
   std::uint64_t* res = nullptr;
-  std::uint64_t* h_res = nullptr;
+  std::uint64_t* h_res = nullptr;  // pinned, kHres words
+  std::uint64_t* d_hres = nullptr;  // device view of h_res (wal_publish)
   std::uint32_t* inj = nullptr;  // Shift_L(0xFFFFFFFF), L = 0..kWalLaneMax
   // host images: device copy, pinned staging slabs for pageable sources, own stream
   std::uint8_t* d_img = nullptr;
@@ -569,7 +607,7 @@ std::mutex g_wal_mu;
 WalScratch* g_wal[64] = {};
 
 // What the calling thread's last WAL verify did (tkv_debug_wal_last).
-thread_local std::uint64_t g_last[4] = {0, 0, 0, 0};  // passes, host walk needed, image copied, pieces
+thread_local std::uint64_t g_last[4] = {0, 0, 0, 0};  // passes, host walk needed, image copied, fast stitch
 
 #define WAL_HIP(call)                                                            \
   do {                                                                           \
@@ -665,7 +703,8 @@ int pass_begin(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStre
   s.h_res[3] = kNone;
   s.h_res[4] = 0;
   s.h_res[5] = 0;
-  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 6 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
+  s.h_res[6] = 0;
+  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 7 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
   WAL_HIP(hipMemsetAsync(a.S, 0xFF, K * sizeof(std::uint64_t), st));
   *out = a;
   return TKV_OK;
@@ -683,35 +722,8 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
   const std::uint64_t size = a.size;
   const std::uint32_t K = a.K;
   const DeviceTables* tabs = a.tabs;
-  // 3: the pieces on the true chain and their entries
-  hipLaunchKernelGGL(wal_jump_init, dim3(blocks(K, 256)), dim3(256), 0, st, a);
-  std::uint32_t* J = a.Ja;
-  std::uint32_t* J2 = a.Jb;
-  for (std::uint64_t reach = 1; reach < K; reach <<= 2) {
-    hipLaunchKernelGGL(wal_jump, dim3(blocks(K, 256)), dim3(256), 0, st, J, J2, a.on, K);
-    std::swap(J, J2);
-  }
-  hipLaunchKernelGGL(wal_link, dim3(blocks(K, 256)), dim3(256), 0, st, a);
-  // 4: record counts from the entries
-  hipLaunchKernelGGL(wal_count, dim3(blocks(K, 256)), dim3(256), 0, st, a);
-  WAL_HIP(hipGetLastError());
-  WAL_HIP(hipMemcpyAsync(s.h_res, s.res, 6 * sizeof(std::uint64_t), hipMemcpyDeviceToHost, st));
-  WAL_HIP(hipStreamSynchronize(st));
-  const std::uint64_t kstar = s.h_res[0];
-  std::uint64_t chain_end = s.h_res[1];
-  bool broke = s.h_res[2] != 0;
-  const bool partial = kstar < K;
-  if (s.h_res[5]) hipLaunchKernelGGL(wal_recheck, dim3(blocks(K, kCheckThreads)), dim3(kCheckThreads), 0, st, a);
-  if (partial) {
-    hipLaunchKernelGGL(wal_trim, dim3(blocks(K, 256)), dim3(256), 0, st, a, kstar);
-    std::uint8_t be = 0;
-    WAL_HIP(hipMemcpyAsync(s.h_res + 1, a.Xe + kstar, 8, hipMemcpyDeviceToHost, st));
-    WAL_HIP(hipMemcpyAsync(&be, a.Be + kstar, 1, hipMemcpyDeviceToHost, st));
-    WAL_HIP(hipStreamSynchronize(st));
-    chain_end = s.h_res[1];
-    broke = be != 0;
-  }
-  // 5: record numbering, first failing in-lane record, the CRC batch of the big ones
+  // 3: the pieces on the true chain and their entries, first by the fast path (wal_fast), with
+  // record counts and their scan behind it, so one host sync reads the verdict and the totals
   std::size_t need = 0;
   WAL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, a.cnt, a.base, K, st));
   if (need > s.cub_bytes) {
@@ -722,11 +734,51 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
     WAL_HIP(hipMalloc(&s.cub, need));
     s.cub_bytes = need;
   }
-  WAL_HIP(hipcub::DeviceScan::ExclusiveSum(s.cub, need, a.cnt, a.base, K, st));
-  WAL_HIP(hipMemcpyAsync(s.h_res + 5, a.base + (K - 1), 8, hipMemcpyDeviceToHost, st));
-  WAL_HIP(hipMemcpyAsync(s.h_res + 6, a.cnt + (K - 1), 8, hipMemcpyDeviceToHost, st));
-  WAL_HIP(hipStreamSynchronize(st));
-  const std::uint64_t tot = s.h_res[5] + s.h_res[6];  // (records << 32) | big records
+  auto count_and_publish = [&]() -> int {
+    hipLaunchKernelGGL(wal_count, dim3(blocks(K, 256)), dim3(256), 0, st, a);
+    WAL_HIP(hipcub::DeviceScan::ExclusiveSum(s.cub, need, a.cnt, a.base, K, st));
+    hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
+    WAL_HIP(hipGetLastError());
+    WAL_HIP(hipStreamSynchronize(st));
+    return TKV_OK;
+  };
+  hipLaunchKernelGGL(wal_fast, dim3(blocks(K, 256)), dim3(256), 0, st, a);
+  if (int rc = count_and_publish()) return rc;
+  if (s.h_res[6]) g_last[3] = 0;
+  if (s.h_res[6]) {
+    // the speculation was wrong somewhere: pointer jumping marks the pieces on the true chain
+    // (wal_count above took the fast path's entries, which are speculative starts: it left res[0]
+    // and res[5] alone, and the exact count below rewrites res[1], res[2] from the true last piece)
+    hipLaunchKernelGGL(wal_jump_init, dim3(blocks(K, 256)), dim3(256), 0, st, a);
+    std::uint32_t* J = a.Ja;
+    std::uint32_t* J2 = a.Jb;
+    for (std::uint64_t reach = 1; reach < K; reach <<= 2) {
+      hipLaunchKernelGGL(wal_jump, dim3(blocks(K, 256)), dim3(256), 0, st, J, J2, a.on, K);
+      std::swap(J, J2);
+    }
+    hipLaunchKernelGGL(wal_link, dim3(blocks(K, 256)), dim3(256), 0, st, a);
+    // 4: record counts from the entries
+    if (int rc = count_and_publish()) return rc;
+  }
+  const std::uint64_t kstar = s.h_res[0];
+  std::uint64_t chain_end = s.h_res[1];
+  bool broke = s.h_res[2] != 0;
+  const bool partial = kstar < K;
+  std::uint64_t tot = s.h_res[7] + s.h_res[8];  // (records << 32) | big records
+  if (s.h_res[5]) hipLaunchKernelGGL(wal_recheck, dim3(blocks(K, kCheckThreads)), dim3(kCheckThreads), 0, st, a);
+  if (partial) {
+    hipLaunchKernelGGL(wal_trim, dim3(blocks(K, 256)), dim3(256), 0, st, a, kstar);
+    WAL_HIP(hipcub::DeviceScan::ExclusiveSum(s.cub, need, a.cnt, a.base, K, st));
+    hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
+    std::uint8_t be = 0;
+    WAL_HIP(hipMemcpyAsync(s.h_res + 1, a.Xe + kstar, 8, hipMemcpyDeviceToHost, st));
+    WAL_HIP(hipMemcpyAsync(&be, a.Be + kstar, 1, hipMemcpyDeviceToHost, st));
+    WAL_HIP(hipStreamSynchronize(st));
+    chain_end = s.h_res[1];
+    broke = be != 0;
+    tot = s.h_res[7] + s.h_res[8];
+  }
+  // 5: record numbering (the scan above), first failing in-lane record, the CRC batch of the big ones
   const std::uint64_t n = tot >> 32, n_big = tot & 0xFFFFFFFFull;
   std::uint64_t first = n;
   if (n) {
@@ -741,7 +793,8 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
     if (n_big) hipLaunchKernelGGL(wal_check_big, dim3(blocks(n_big, 256)), dim3(256), 0, st, a, n_big);
     hipLaunchKernelGGL(wal_bad_pos, dim3(blocks(std::max<std::uint64_t>(K, n_big), 256)), dim3(256), 0, st, a, n_big);
     WAL_HIP(hipGetLastError());
-    WAL_HIP(hipMemcpyAsync(s.h_res + 3, s.res + 3, 2 * sizeof(std::uint64_t), hipMemcpyDeviceToHost, st));
+    hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
+    WAL_HIP(hipGetLastError());
     WAL_HIP(hipStreamSynchronize(st));
     first = std::min<std::uint64_t>(s.h_res[3], n);
   }
@@ -775,7 +828,8 @@ int scratch(WalScratch** out) {
   std::lock_guard<std::mutex> lk(sp->mu);
   if (!sp->res) {
     WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->res), 8 * sizeof(std::uint64_t)));
-    WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&sp->h_res), 8 * sizeof(std::uint64_t), hipHostMallocDefault));
+    WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&sp->h_res), kHres * sizeof(std::uint64_t), hipHostMallocDefault));
+    WAL_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&sp->d_hres), sp->h_res, 0));
     WAL_HIP(hipStreamCreateWithFlags(&sp->st, hipStreamNonBlocking));
     WAL_HIP(hipStreamCreateWithFlags(&sp->stc, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) WAL_HIP(hipEventCreateWithFlags(&sp->landed[i], hipEventDisableTiming));
@@ -797,7 +851,6 @@ int verify_locked(WalScratch& s, const std::uint8_t* d_wal, std::uint64_t size, 
   constexpr int kMaxPasses = 8;
   std::uint64_t start = 0, good = 0;
   g_last[0] = g_last[1] = 0;
-  g_last[3] = (size + kWalPiece - 1) / kWalPiece;
   for (int pass = 0; pass < kMaxPasses; ++pass) {
     PassResult r;
     g_last[0] = static_cast<std::uint64_t>(pass) + 1;
@@ -833,6 +886,11 @@ void stage_copy(std::uint8_t* dst, const std::uint8_t* src, std::uint64_t n) {
 }
 
 constexpr std::uint64_t kStageSlab = std::uint64_t(64) << 20;
+// Device copies of host images up to this size stay allocated between verifies.
+constexpr std::uint64_t kKeepImg = std::uint64_t(256) << 20;
+
+int host_image_locked(WalScratch& s, const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
+                      std::uint64_t* stop_offset, bool* needs_host_walk);
 
 }  // namespace
 
@@ -843,6 +901,7 @@ int wal_verify_device_impl(const std::uint8_t* d_wal, std::uint64_t size, std::u
   *stop_offset = 0;
   g_last[0] = g_last[1] = g_last[2] = g_last[3] = 0;
   if (size == 0) return TKV_OK;
+  g_last[3] = 1;  // cleared by the first pass that needs the pointer-jumping stitch
   if ((size + kWalPiece - 1) / kWalPiece >= 0xFFFFFFFFull)
     return set_error(TKV_INVALID_ARGUMENT, "WAL image too large for the device walk");
   WalScratch* sp = nullptr;
@@ -859,6 +918,7 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
   *stop_offset = 0;
   g_last[0] = g_last[1] = g_last[2] = g_last[3] = 0;
   if (size == 0) return TKV_OK;
+  g_last[3] = 1;  // cleared by the first pass that needs the pointer-jumping stitch
   if ((size + kWalPiece - 1) / kWalPiece >= 0xFFFFFFFFull) {
     *needs_host_walk = true;
     return TKV_OK;
@@ -868,6 +928,23 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
   WalScratch& s = *sp;
   std::lock_guard<std::mutex> lk(s.mu);
   g_last[2] = 1;
+  const int rc = host_image_locked(s, h_wal, size, n_good, stop_offset, needs_host_walk);
+  // No copy that reads the caller's buffer, and no kernel on the device copy, may outlive the call
+  // (an error return included). A device copy larger than kKeepImg is released, so one large
+  // recovery does not keep its size of HBM from the caller's later allocations.
+  (void)hipStreamSynchronize(s.st);
+  (void)hipStreamSynchronize(s.stc);
+  if (s.cap_img > kKeepImg) {
+    (void)hipFree(s.d_img);
+    s.d_img = nullptr;
+    s.cap_img = 0;
+  }
+  return rc;
+}
+
+namespace {
+int host_image_locked(WalScratch& s, const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
+                      std::uint64_t* stop_offset, bool* needs_host_walk) {
   if (size > s.cap_img) {
     (void)hipStreamSynchronize(s.st);
     (void)hipFree(s.d_img);
@@ -927,6 +1004,7 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
   if (int rc = pass_tail(s, a, s.stc, &r)) return rc;
   return verify_locked(s, s.d_img, size, n_good, stop_offset, s.stc, needs_host_walk, &r);
 }
+}  // namespace
 
 }  // namespace tkv
 
