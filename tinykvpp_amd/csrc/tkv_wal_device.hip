@@ -359,186 +359,11 @@ __device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::
   a.first_pos[k] = first_pos;
 }
 
-// ---- the piece walk through a lane-private window ring in LDS ----------------------------------------
-// Each lane reads its piece as whole 64-byte windows (four 16-byte loads of one half line, a single
-// L1 miss) into a ring of two windows in LDS, and parses headers and folds payloads from there:
-// per-lane 16-byte reads at the record's own offsets made every CU's 1024 lanes re-miss lines the
-// L1 could not keep (3.2x the image in L1->L2 requests, the TA stalled on pending misses for 88 % of
-// wal_spec, profiles/r2/wal_head_scan/pmc_wal_spec.txt). The next window is in flight while the
-// lane works through the current two. The slicing tables are replicated 16 times (64 KiB; two lanes
-// share each copy) so that the rings of kWinThreads lanes fit beside them.
-constexpr unsigned kWinThreads = 640;              // 10 waves, one workgroup per CU
-constexpr std::uint32_t kWinTabBytes = 256u * 256u;  // entry e of table t, copy c: e*256 + t*64 + c*4
-constexpr std::uint32_t kWinStride = 144;          // ring bytes per lane (128 + 16 to spread the banks)
-constexpr std::uint32_t kWinLdsWords = (kWinTabBytes + kWinThreads * kWinStride) / 4;
-
-__device__ __forceinline__ void fill_slices16(const DeviceTables* tabs, std::uint32_t* lds) {
-  for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
-    const std::uint32_t t = u >> 8, e = u & 255u;
-    const std::uint32_t v = tabs->slice[t][e];
-    uint4* dst = reinterpret_cast<uint4*>(lds + e * 64u + t * 16u);
-#pragma unroll
-    for (std::uint32_t k = 0; k < 4u; ++k) dst[(k + u) & 3u] = make_uint4(v, v, v, v);
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ dev::LaneConst lane_const16(std::uint32_t lane) {
-  const std::uint32_t c4 = (lane & 15u) << 2;
-  return {c4, 64u + c4, 128u + c4, 192u + c4, 0u};
-}
-
-struct Ring {
-  std::uint32_t base;  // LDS byte address of this lane's ring
-  std::uintptr_t R0;   // memory address of the first resident window (64-aligned); [R0, R0 + 128) resident
-  std::uintptr_t mend; // end of the image (memory address)
-  uint4 pf0, pf1, pf2, pf3;  // window R0 + 128, in flight
-};
-
-__device__ __forceinline__ void win_load(const Ring& g, std::uintptr_t w, uint4& v0, uint4& v1, uint4& v2, uint4& v3) {
-  if (w < g.mend) {  // a 64-byte window with an image byte lies in that byte's page
-    v0 = dev::gload16(w);
-    v1 = dev::gload16(w + 16);
-    v2 = dev::gload16(w + 32);
-    v3 = dev::gload16(w + 48);
-  } else {
-    v0 = v1 = v2 = v3 = make_uint4(0, 0, 0, 0);
-  }
-}
-__device__ __forceinline__ void win_put(std::uint32_t* lds, const Ring& g, std::uintptr_t w, const uint4& v0,
-                                        const uint4& v1, const uint4& v2, const uint4& v3) {
-  uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + g.base + static_cast<std::uint32_t>(w & 64u));
-  d[0] = v0;
-  d[1] = v1;
-  d[2] = v2;
-  d[3] = v3;
-}
-// The ring from the window holding memory address m (its first two windows resident, the third in flight).
-__device__ __forceinline__ void ring_reset(std::uint32_t* lds, Ring& g, std::uintptr_t m) {
-  g.R0 = m & ~static_cast<std::uintptr_t>(63);
-  uint4 a0, a1, a2, a3, b0, b1, b2, b3;
-  win_load(g, g.R0, a0, a1, a2, a3);
-  win_load(g, g.R0 + 64, b0, b1, b2, b3);
-  win_load(g, g.R0 + 128, g.pf0, g.pf1, g.pf2, g.pf3);
-  win_put(lds, g, g.R0, a0, a1, a2, a3);
-  win_put(lds, g, g.R0 + 64, b0, b1, b2, b3);
-}
-// Bytes below memory address e resident (e <= R0 + 192 + 128 on every call site's path).
-__device__ __forceinline__ void ring_need(std::uint32_t* lds, Ring& g, std::uintptr_t e) {
-  while (e > g.R0 + 128) {
-    win_put(lds, g, g.R0 + 128, g.pf0, g.pf1, g.pf2, g.pf3);  // into the slot of window R0
-    g.R0 += 64;
-    win_load(g, g.R0 + 128, g.pf0, g.pf1, g.pf2, g.pf3);
-  }
-}
-// The aligned dword at memory address m (resident).
-__device__ __forceinline__ std::uint32_t ring_rd(const std::uint32_t* lds, const Ring& g, std::uintptr_t m) {
-  return dev::lds_at(lds, g.base + static_cast<std::uint32_t>(m & 124u));
-}
-
-// CRC-32 (finalized) of the payload at memory address m, L <= kWalLaneMax bytes, from the ring: the
-// aligned dwords that hold it, the bytes in front zeroed, the last 0-3 bytes by Sarwate steps; the
-// init register enters as inj[L] (as lane_crc).
-__device__ __forceinline__ std::uint32_t ring_crc(std::uint32_t* lds, Ring& g, const dev::LaneConst& kc,
-                                                  const WalArgs& a, std::uintptr_t m, std::uint32_t L) {
-  if (L == 0) return 0u;
-  const std::uintptr_t g0 = m & ~static_cast<std::uintptr_t>(3);
-  const std::uint32_t h = static_cast<std::uint32_t>(m - g0);
-  const std::uint32_t span = h + L;
-  const std::uint32_t nd = span >> 2, tb = span & 3u;
-  dev::Reg r{0, 0};
-  std::uint32_t k = 0;
-  if (nd) {
-    ring_need(lds, g, g0 + 4);
-    const std::uint32_t w = ring_rd(lds, g, g0) & (0xFFFFFFFFu << (8 * h));
-    dev::slice4(lds, r, w, kc);
-    k = 1;
-  }
-  for (; k < nd; ++k) {
-    const std::uintptr_t q = g0 + 4u * k;
-    ring_need(lds, g, q + 4);
-    dev::slice4(lds, r, ring_rd(lds, g, q), kc);
-  }
-  if (tb) {
-    const std::uintptr_t q = g0 + 4u * nd;
-    ring_need(lds, g, q + 4);
-    std::uint32_t b = ring_rd(lds, g, q);
-    if (nd == 0) b >>= 8 * h;  // the whole payload sits in this dword, after h bytes
-    std::uint32_t x = r.value();
-    const std::uint32_t n = nd == 0 ? L : tb;
-    for (std::uint32_t t = 0; t < n; ++t, b >>= 8) x = (x >> 8) ^ dev::lds_at(lds, (((x ^ b) & 0xFFu) << 8) | kc.L0);
-    r = dev::Reg{x, 0};
-  }
-  return r.value() ^ a.inj[L] ^ 0xFFFFFFFFu;
-}
-
-// walk_check through the ring (same walk, checks, slots and outputs).
-__device__ __forceinline__ void walk_check_win(std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
-                                               std::uint64_t k, std::uint64_t start, std::uint64_t* exit_out,
-                                               std::uint8_t* broke_out, std::uint64_t* cnt_out) {
-  const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
-  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
-  Ring g;
-  g.base = kWinTabBytes + threadIdx.x * kWinStride;
-  g.mend = w0 + a.size;
-  ring_reset(lds, g, w0 + start);
-  std::uint64_t p = start, n_all = 0, n_big = 0, first = kNone, first_pos = 0;
-  bool bad_hdr = false;
-  while (p < limit) {
-    if (a.size - p < kWalMeta) {
-      bad_hdr = true;
-      break;
-    }
-    const std::uintptr_t m = w0 + p;
-    const std::uintptr_t b = m & ~static_cast<std::uintptr_t>(3);
-    if (b >= g.R0 + 256) ring_reset(lds, g, m);  // past a record the walk did not fold
-    ring_need(lds, g, b + 32);
-    HdrRaw hr;
-    hr.u = make_uint4(ring_rd(lds, g, b), ring_rd(lds, g, b + 4), ring_rd(lds, g, b + 8), ring_rd(lds, g, b + 12));
-    hr.v = make_uint4(ring_rd(lds, g, b + 16), ring_rd(lds, g, b + 20), ring_rd(lds, g, b + 24), ring_rd(lds, g, b + 28));
-    const std::uint32_t t = static_cast<std::uint32_t>(m & 3u);
-    const std::uint32_t d[8] = {hr.u.x, hr.u.y, hr.u.z, hr.u.w, hr.v.x, hr.v.y, hr.v.z, hr.v.w};
-    auto at = [&](std::uint32_t lo, std::uint32_t hi, std::uint32_t o) { return o ? __builtin_amdgcn_alignbyte(hi, lo, o) : lo; };
-    const std::uint32_t rlen = at(d[0], d[1], t), stored = at(d[1], d[2], t);
-    const bool up = t >= 2u;
-    const std::uint32_t o = (t + 2u) & 3u;
-    const std::uint64_t klen = up ? at(d[5], d[6], o) : at(d[4], d[5], o);
-    const std::uint64_t vlen = up ? at(d[6], d[7], o) : at(d[5], d[6], o);
-    if (static_cast<std::uint64_t>(rlen) + 8 > a.size - p) {
-      bad_hdr = true;
-      break;
-    }
-    const std::uint64_t np = p + 8 + static_cast<std::uint64_t>(rlen);
-    bool bad = kWalMeta + klen + vlen > 8ull + rlen;
-    if (rlen <= kWalLaneMax) {
-      bad = bad || ring_crc(lds, g, kc, a, m + 8, rlen) != stored;
-    } else {
-      const std::uint64_t sl = 2 * k + (n_big & 1u);
-      a.slot_off[sl] = p + 8;
-      a.slot_len[sl] = rlen;
-      a.slot_crc[sl] = stored;
-      a.slot_loc[sl] = static_cast<std::uint32_t>(n_all);
-      ++n_big;
-    }
-    if (bad && first == kNone) {
-      first = n_all;
-      first_pos = p;
-    }
-    ++n_all;
-    p = np;
-  }
-  *exit_out = p;
-  *broke_out = bad_hdr ? 1 : 0;
-  *cnt_out = (n_all << 32) | n_big;
-  a.first_loc[k] = first;
-  a.first_pos[k] = first_pos;
-}
-
 // 2. Speculative walk and check of pieces [k_lo, k_hi) from their first plausible header (piece 0
 // from 0).
-__global__ __launch_bounds__(kWinThreads) void wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
-  __shared__ std::uint32_t lds[kWinLdsWords];
-  fill_slices16(a.tabs, lds);
+__global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  fill_slices(a.tabs, lds);
   const std::uint64_t k = k_lo + gid();
   if (k >= k_hi) return;
   const std::uint64_t s = k == 0 ? 0 : a.S[k];
@@ -551,10 +376,10 @@ __global__ __launch_bounds__(kWinThreads) void wal_spec(WalArgs a, std::uint64_t
     a.first_loc[k] = kNone;
     return;
   }
-  const dev::LaneConst kc = lane_const16(threadIdx.x & 63u);
+  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
   std::uint64_t x, c;
   std::uint8_t br;
-  walk_check_win(lds, kc, a, k, s, &x, &br, &c);
+  walk_check(lds, kc, a, k, s, &x, &br, &c);
   a.X[k] = x;
   a.broke[k] = br;
   a.spec_cnt[k] = c;
@@ -889,7 +714,7 @@ void pass_front(const WalArgs& a, std::uint64_t k_lo, std::uint64_t k_hi, hipStr
   if (k_hi <= k_lo) return;
   const std::uint64_t threads = (k_hi - k_lo + 64 / kHeadLanes - 1) / (64 / kHeadLanes) * 64;  // 8 pieces per wave
   hipLaunchKernelGGL(wal_scan_head, dim3(blocks(threads, kScanThreads)), dim3(kScanThreads), 0, st, a, k_lo, k_hi);
-  hipLaunchKernelGGL(wal_spec, dim3(blocks(k_hi - k_lo, kWinThreads)), dim3(kWinThreads), 0, st, a, k_lo, k_hi);
+  hipLaunchKernelGGL(wal_spec, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
 }
 
 int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
