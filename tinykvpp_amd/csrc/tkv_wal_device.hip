@@ -361,7 +361,7 @@ __device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::
 
 // 2. Speculative walk and check of pieces [k_lo, k_hi) from their first plausible header (piece 0
 // from 0).
-__global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
+[[maybe_unused]] __global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
   __shared__ std::uint32_t lds[kLdsSliceWords];
   fill_slices(a.tabs, lds);
   const std::uint64_t k = k_lo + gid();
@@ -384,6 +384,229 @@ __global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64
   a.broke[k] = br;
   a.spec_cnt[k] = c;
   a.next[k] = (br || x >= a.size) ? a.K : static_cast<std::uint32_t>(x / kWalPiece);
+}
+
+// ---- 2 (lockstep). The same walk and checks with every lane of a wave advancing through its piece
+// one 16-byte granule per step. The granule a lane reads at step j is loaded kLockSlots steps ahead
+// into a ring of registers, so no load waits on a header: the header fields come from the granule
+// holding the header and the two after it, and payload bytes are folded as their granule passes
+// (slicing-by-4, bytes outside the payload masked to zero; leading zeros leave an init-0 register
+// at 0, and the trailing ones are matched by shifting the expected register by the same zero
+// bytes). A record whose payload exceeds kWalLaneMax goes to the piece's slots as in walk_check, and
+// the lane re-aims its stream at the next header, idling while the new granules arrive. Outputs are
+// walk_check's, except that a record too short for its key/value lengths (record_len < 18) ends the
+// lane's walk there as a broken chain: it is the first failing record of the piece either way, and
+// no record after it can change the verdict.
+constexpr int kLockSlots = 6;  // granules in flight per lane (the ring)
+constexpr unsigned kInjWords = kWalLaneMax + 1;
+
+template <int LO, int N>
+__device__ __forceinline__ std::uint32_t sel_dword(std::uint32_t i, const std::uint32_t (&D)[12]) {
+  // D[i] for LO <= i < LO + N by a select tree on the bits of i - LO. (A chain of equality selects
+  // is turned back into an indexed load from a stack copy of D by the compiler.)
+  static_assert(N >= 2 && N <= 8, "select tree of up to 8");
+  const std::uint32_t t = i - LO;
+  auto at = [&](int j) { return D[LO + (j < N ? j : N - 1)]; };
+  const bool b0 = t & 1u, b1 = (t >> 1) & 1u, b2 = (t >> 2) & 1u;
+  const std::uint32_t l0 = b0 ? at(1) : at(0), l1 = b0 ? at(3) : at(2);
+  const std::uint32_t l2 = b0 ? at(5) : at(4), l3 = b0 ? at(7) : at(6);
+  const std::uint32_t m0 = b1 ? l1 : l0, m1 = b1 ? l3 : l2;
+  return N <= 4 ? m0 : (b2 ? m1 : m0);
+}
+// Little-endian u32 at byte q of the 48-byte window D, whose dword q/4 lies in [LO, LO + N).
+template <int LO, int N>
+__device__ __forceinline__ std::uint32_t win_u32(const std::uint32_t (&D)[12], std::uint32_t q) {
+  const std::uint32_t i = q >> 2, b = q & 3u;
+  const std::uint32_t lo = sel_dword<LO, N>(i, D), hi = sel_dword<LO + 1, N>(i + 1, D);
+  return b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
+}
+// Bytes [lo, hi) of the granule at g (image offsets) as a 16-bit mask.
+__device__ __forceinline__ std::uint32_t gran_mask(std::int64_t lo, std::int64_t hi, std::int64_t g) {
+  const std::int64_t l = lo - g < 0 ? 0 : (lo - g > 16 ? 16 : lo - g);
+  const std::int64_t h = hi - g < 0 ? 0 : (hi - g > 16 ? 16 : hi - g);
+  return ((1u << static_cast<std::uint32_t>(h)) - 1u) & ~((1u << static_cast<std::uint32_t>(l)) - 1u);
+}
+// Byte mask of dword i from a 16-bit granule mask.
+__device__ __forceinline__ std::uint32_t dword_mask(std::uint32_t m16, int i) {
+  const std::uint32_t nib = (m16 >> (4 * i)) & 0xFu;
+  const std::uint32_t spread = (nib * 0x00204081u) & 0x01010101u;
+  return __builtin_amdgcn_perm(0u, 0u, 0x0C0C0C0Cu + spread);  // selector 0x0D -> 0xFF, 0x0C -> 0x00
+}
+
+__global__ __launch_bounds__(kCheckThreads) void wal_lock(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
+  __shared__ std::uint32_t lds[kLdsSliceWords + kInjWords];
+  std::uint32_t* linj = lds + kLdsSliceWords;
+  for (std::uint32_t i = threadIdx.x; i < kInjWords; i += blockDim.x) linj[i] = a.inj[i];
+  fill_slices(a.tabs, lds);  // (its barrier covers linj too)
+  const std::uint64_t k = k_lo + gid();
+  if (k >= k_hi) return;
+  const std::uint64_t s0 = k == 0 ? 0 : a.S[k];
+  if (k == 0) a.S[0] = 0;
+  if (s0 == kNone) {
+    a.X[k] = kNone;
+    a.next[k] = a.K;
+    a.broke[k] = 0;
+    a.spec_cnt[k] = 0;
+    a.first_loc[k] = kNone;
+    return;
+  }
+  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
+  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
+  const std::int64_t size = static_cast<std::int64_t>(a.size);
+  const std::int64_t limit = static_cast<std::int64_t>((k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size);
+  auto galign = [&](std::int64_t p) -> std::int64_t {  // image offset of the 16-byte memory granule holding p
+    return static_cast<std::int64_t>(((w0 + static_cast<std::uintptr_t>(p)) & ~static_cast<std::uintptr_t>(15)) - w0);
+  };
+  // the stream: step j reads the granule at image offset gbase + 16 j
+  std::int64_t gbase = galign(static_cast<std::int64_t>(s0));
+  std::int64_t hs = static_cast<std::int64_t>(s0);  // next header start
+  bool has_cur = false;
+  std::int64_t cps = 0, cpe = 0;  // payload being folded: [cps, cpe)
+  std::uint32_t cE = 0;           // its expected register (see above)
+  std::uint64_t c_idx = 0, c_pos = 0;
+  dev::Reg r{0, 0};
+  int stall = 0;
+  bool done = false, bad_hdr = false;
+  std::int64_t X = 0;
+  std::uint64_t n_all = 0, n_big = 0, first = kNone, first_pos = 0;
+  auto note_bad = [&](std::uint64_t idx, std::uint64_t pos) {
+    if (idx < first) {
+      first = idx;
+      first_pos = pos;
+    }
+  };
+  const std::uintptr_t mend = w0 + a.size;
+  uint4 sl[kLockSlots];
+  // Loads are unconditional, so the compiler's wait counts stay exact (a load behind a branch makes
+  // every later use wait for all loads in flight): a granule past the image's end, or of a finished
+  // lane, re-reads the image's first granule, and its bytes are never used. A granule holding an
+  // image byte lies in that byte's page.
+  const std::uintptr_t safe = w0 & ~static_cast<std::uintptr_t>(15);
+  auto load_gran = [&](std::int64_t g) -> uint4 {
+    const std::uintptr_t m = w0 + static_cast<std::uintptr_t>(g);
+    return dev::gload16(!done && m < mend ? m : safe);
+  };
+#pragma unroll
+  for (int t = 0; t < kLockSlots; ++t) sl[t] = load_gran(gbase + 16 * t);
+
+  // One step: granule j in slot S0, the next two in S1, S2; then slot S0 takes granule j + kLockSlots.
+  auto step = [&](std::int64_t j, uint4& G0, const uint4& G1, const uint4& G2) {
+    if (!done) {
+      if (stall > 0) {
+        --stall;
+      } else {
+        const std::int64_t gp = gbase + 16 * j;
+        const std::uint32_t D[12] = {G0.x, G0.y, G0.z, G0.w, G1.x, G1.y, G1.z, G1.w, G2.x, G2.y, G2.z, G2.w};
+        bool has_new = false, fin_after = false;
+        std::int64_t nps = 0, npe = 0;
+        std::uint32_t nE = 0;
+        std::uint64_t n_idx = 0, n_pos = 0;
+        if (hs < gp + 16) {  // the next header starts in this granule
+          const std::uint64_t p = static_cast<std::uint64_t>(hs);
+          if (hs >= limit) {
+            X = hs;
+            fin_after = true;
+          } else if (size - hs < static_cast<std::int64_t>(kWalMeta)) {
+            X = hs;
+            bad_hdr = true;
+            fin_after = true;
+          } else {
+            const std::uint32_t o = static_cast<std::uint32_t>(hs - gp);
+            const std::uint32_t rlen = win_u32<0, 5>(D, o), stored = win_u32<1, 5>(D, o + 4);
+            const std::uint64_t klen = win_u32<4, 6>(D, o + 18), vlen = win_u32<5, 6>(D, o + 22);
+            if (static_cast<std::int64_t>(rlen) + 8 > size - hs) {
+              X = hs;
+              bad_hdr = true;
+              fin_after = true;
+            } else {
+              const std::uint64_t idx = n_all++;
+              const std::int64_t np = hs + 8 + static_cast<std::int64_t>(rlen);
+              if (kWalMeta + klen + vlen > 8ull + rlen) note_bad(idx, p);
+              if (rlen > kWalLaneMax) {
+                const std::uint64_t slt = 2 * k + (n_big & 1u);
+                a.slot_off[slt] = p + 8;
+                a.slot_len[slt] = rlen;
+                a.slot_crc[slt] = stored;
+                a.slot_loc[slt] = static_cast<std::uint32_t>(idx);
+                ++n_big;
+                hs = np;
+                if (np >= limit) {
+                  X = np;
+                  fin_after = true;
+                } else {  // re-aim the stream: step j + kLockSlots reads the granule holding np
+                  gbase = galign(np) - 16 * (j + kLockSlots);
+                  stall = kLockSlots - 1;
+                }
+              } else if (rlen < 18) {  // record_len < 18 fails the key/value bounds (noted above): stop
+                X = hs;
+                bad_hdr = true;
+                fin_after = true;
+              } else {
+                has_new = true;
+                nps = hs + 8;
+                npe = np;
+                n_idx = idx;
+                n_pos = p;
+                std::uint32_t e = stored ^ 0xFFFFFFFFu ^ linj[rlen];
+                const std::uint32_t pad = (4u - static_cast<std::uint32_t>((w0 + static_cast<std::uintptr_t>(np)) & 3u)) & 3u;
+                for (std::uint32_t t = 0; t < 3u; ++t)
+                  if (t < pad) e = (e >> 8) ^ dev::lds_at(lds, ((e & 0xFFu) << 8) | kc.L0);
+                nE = e;
+                hs = np;
+              }
+            }
+          }
+        }
+        // fold this granule's payload bytes: the end of the current payload, the start of the new one
+        const std::uint32_t m16 = (has_cur ? gran_mask(cps, cpe, gp) : 0u) | (has_new ? gran_mask(nps, npe, gp) : 0u);
+        std::int32_t rst = 4, fin = 4;
+        if (has_cur && cps >= gp) rst = static_cast<std::int32_t>((cps - gp) >> 2);
+        if (has_new && nps < gp + 16) rst = static_cast<std::int32_t>((nps - gp) >> 2);
+        if (has_cur && cpe - 1 < gp + 16) fin = static_cast<std::int32_t>((cpe - 1 - gp) >> 2);
+        if (m16) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (rst == i) r = dev::Reg{0, 0};
+            if ((m16 >> (4 * i)) & 0xFu) dev::slice4(lds, r, D[i] & dword_mask(m16, i), kc);
+            if (fin == i && r.value() != cE) note_bad(c_idx, c_pos);
+          }
+        }
+        if (fin < 4) has_cur = false;
+        if (has_new) {
+          has_cur = true;
+          cps = nps;
+          cpe = npe;
+          cE = nE;
+          c_idx = n_idx;
+          c_pos = n_pos;
+        }
+        if (fin_after) done = true;
+      }
+    }
+    G0 = load_gran(gbase + 16 * (j + kLockSlots));
+  };
+  // Every lane ends within (piece + overhang of its last folded record) / 16 steps plus kLockSlots
+  // per re-aim (at most two per piece); the cap is a guard that reports instead of spinning.
+  constexpr std::int64_t kMaxSteps = (kWalPiece + kWalLaneMax + 64) / 16 + 4 * kLockSlots + 64;
+  for (std::int64_t j = 0;; j += kLockSlots) {
+    if (j >= kMaxSteps) {
+      if (!done) a.res[7] = 1;
+      break;
+    }
+    step(j + 0, sl[0], sl[1], sl[2]);
+    step(j + 1, sl[1], sl[2], sl[3]);
+    step(j + 2, sl[2], sl[3], sl[4]);
+    step(j + 3, sl[3], sl[4], sl[5]);
+    step(j + 4, sl[4], sl[5], sl[0]);
+    step(j + 5, sl[5], sl[0], sl[1]);
+    if (__ballot(!done) == 0) break;
+  }
+  a.X[k] = static_cast<std::uint64_t>(X);
+  a.broke[k] = bad_hdr ? 1 : 0;
+  a.spec_cnt[k] = (n_all << 32) | n_big;
+  a.first_loc[k] = first;
+  a.first_pos[k] = first_pos;
+  a.next[k] = (bad_hdr || static_cast<std::uint64_t>(X) >= a.size) ? a.K : static_cast<std::uint32_t>(static_cast<std::uint64_t>(X) / kWalPiece);
 }
 
 __global__ void wal_jump_init(WalArgs a) {
@@ -429,6 +652,7 @@ __global__ void wal_publish(WalArgs a, std::uint64_t* h) {
   if (i < 7) h[i] = a.res[i];
   if (i == 7) h[7] = a.base[a.K - 1];
   if (i == 8) h[8] = a.cnt[a.K - 1];
+  if (i == 9) h[9] = a.res[7];
 }
 
 // 3. One quadrupling round (J = next^(4^t)): every marked k marks J(k), J(J(k)) and J(J(J(k))), then
@@ -704,7 +928,8 @@ int pass_begin(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStre
   s.h_res[4] = 0;
   s.h_res[5] = 0;
   s.h_res[6] = 0;
-  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 7 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
+  s.h_res[7] = 0;
+  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 8 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
   WAL_HIP(hipMemsetAsync(a.S, 0xFF, K * sizeof(std::uint64_t), st));
   *out = a;
   return TKV_OK;
@@ -714,7 +939,11 @@ void pass_front(const WalArgs& a, std::uint64_t k_lo, std::uint64_t k_hi, hipStr
   if (k_hi <= k_lo) return;
   const std::uint64_t threads = (k_hi - k_lo + 64 / kHeadLanes - 1) / (64 / kHeadLanes) * 64;  // 8 pieces per wave
   hipLaunchKernelGGL(wal_scan_head, dim3(blocks(threads, kScanThreads)), dim3(kScanThreads), 0, st, a, k_lo, k_hi);
+#ifdef TKV_WAL_SPEC_WALK
   hipLaunchKernelGGL(wal_spec, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
+#else
+  hipLaunchKernelGGL(wal_lock, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
+#endif
 }
 
 int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
@@ -744,6 +973,7 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
   };
   hipLaunchKernelGGL(wal_fast, dim3(blocks(K, 256)), dim3(256), 0, st, a);
   if (int rc = count_and_publish()) return rc;
+  if (s.h_res[9]) return set_error(TKV_IO_ERROR, "device WAL walk exceeded its step bound");
   if (s.h_res[6]) g_last[3] = 0;
   if (s.h_res[6]) {
     // the speculation was wrong somewhere: pointer jumping marks the pieces on the true chain
