@@ -398,6 +398,7 @@ __device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::
 // lane's walk there as a broken chain: it is the first failing record of the piece either way, and
 // no record after it can change the verdict.
 constexpr int kLockSlots = 6;  // granules in flight per lane (the ring)
+constexpr unsigned kLockThreads = 512;  // 8 waves (<= 256 VGPRs each), one workgroup per CU
 constexpr unsigned kInjWords = kWalLaneMax + 1;
 
 template <int LO, int N>
@@ -433,7 +434,7 @@ __device__ __forceinline__ std::uint32_t dword_mask(std::uint32_t m16, int i) {
   return __builtin_amdgcn_perm(0u, 0u, 0x0C0C0C0Cu + spread);  // selector 0x0D -> 0xFF, 0x0C -> 0x00
 }
 
-__global__ __launch_bounds__(kCheckThreads) void wal_lock(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
+__global__ __launch_bounds__(kLockThreads) void wal_lock(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
   __shared__ std::uint32_t lds[kLdsSliceWords + kInjWords];
   std::uint32_t* linj = lds + kLdsSliceWords;
   for (std::uint32_t i = threadIdx.x; i < kInjWords; i += blockDim.x) linj[i] = a.inj[i];
@@ -452,143 +453,144 @@ __global__ __launch_bounds__(kCheckThreads) void wal_lock(WalArgs a, std::uint64
   }
   const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
   const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
-  const std::int64_t size = static_cast<std::int64_t>(a.size);
-  const std::int64_t limit = static_cast<std::int64_t>((k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size);
-  auto galign = [&](std::int64_t p) -> std::int64_t {  // image offset of the 16-byte memory granule holding p
-    return static_cast<std::int64_t>(((w0 + static_cast<std::uintptr_t>(p)) & ~static_cast<std::uintptr_t>(15)) - w0);
-  };
-  // the stream: step j reads the granule at image offset gbase + 16 j
-  std::int64_t gbase = galign(static_cast<std::int64_t>(s0));
-  std::int64_t hs = static_cast<std::int64_t>(s0);  // next header start
+  // Positions are u32 offsets from the lane's first granule (image offset O, a 16-byte aligned
+  // address): everything a live lane touches lies within a piece plus one folded record of it.
+  const std::uintptr_t mO = (w0 + s0) & ~static_cast<std::uintptr_t>(15);
+  const std::int64_t O = static_cast<std::int64_t>(mO - w0);
+  const std::uint64_t szr = static_cast<std::uint64_t>(static_cast<std::int64_t>(a.size) - O);  // size, relative
+  const std::uint32_t szr32 = szr > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<std::uint32_t>(szr);
+  const std::uint64_t lim64 = ((k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size);
+  const std::uint32_t lim = static_cast<std::uint32_t>(static_cast<std::int64_t>(lim64) - O);
+  std::uint32_t gb = 0;  // step j reads the granule at gb + 16 j
+  std::uint32_t hs = static_cast<std::uint32_t>(static_cast<std::int64_t>(s0) - O);  // next header start
   bool has_cur = false;
-  std::int64_t cps = 0, cpe = 0;  // payload being folded: [cps, cpe)
-  std::uint32_t cE = 0;           // its expected register (see above)
-  std::uint64_t c_idx = 0, c_pos = 0;
-  dev::Reg r{0, 0};
-  int stall = 0;
+  std::uint32_t cps = 0, cpe = 0, cE = 0, c_idx = 0;  // payload being folded [cps, cpe), expected register
+  std::uint32_t t_reg = 0, u_reg = 0;                 // its CRC register (t ^ u)
+  std::uint32_t stall = 0;
   bool done = false, bad_hdr = false;
-  std::int64_t X = 0;
-  std::uint64_t n_all = 0, n_big = 0, first = kNone, first_pos = 0;
-  auto note_bad = [&](std::uint64_t idx, std::uint64_t pos) {
-    if (idx < first) {
-      first = idx;
-      first_pos = pos;
-    }
-  };
+  std::uint64_t X = 0;
+  std::uint32_t n_all = 0, n_big = 0, first = 0xFFFFFFFFu, first_pos = 0;
   const std::uintptr_t mend = w0 + a.size;
-  uint4 sl[kLockSlots];
+  const std::uintptr_t safe = w0 & ~static_cast<std::uintptr_t>(15);
   // Loads are unconditional, so the compiler's wait counts stay exact (a load behind a branch makes
   // every later use wait for all loads in flight): a granule past the image's end, or of a finished
   // lane, re-reads the image's first granule, and its bytes are never used. A granule holding an
   // image byte lies in that byte's page.
-  const std::uintptr_t safe = w0 & ~static_cast<std::uintptr_t>(15);
-  auto load_gran = [&](std::int64_t g) -> uint4 {
-    const std::uintptr_t m = w0 + static_cast<std::uintptr_t>(g);
+  auto load_gran = [&](std::uint32_t g) -> uint4 {
+    const std::uintptr_t m = mO + g;
     return dev::gload16(!done && m < mend ? m : safe);
   };
+  uint4 sl[kLockSlots];
 #pragma unroll
-  for (int t = 0; t < kLockSlots; ++t) sl[t] = load_gran(gbase + 16 * t);
+  for (int t = 0; t < kLockSlots; ++t) sl[t] = load_gran(16u * t);
 
-  // One step: granule j in slot S0, the next two in S1, S2; then slot S0 takes granule j + kLockSlots.
-  auto step = [&](std::int64_t j, uint4& G0, const uint4& G1, const uint4& G2) {
-    if (!done) {
-      if (stall > 0) {
-        --stall;
-      } else {
-        const std::int64_t gp = gbase + 16 * j;
-        const std::uint32_t D[12] = {G0.x, G0.y, G0.z, G0.w, G1.x, G1.y, G1.z, G1.w, G2.x, G2.y, G2.z, G2.w};
-        bool has_new = false, fin_after = false;
-        std::int64_t nps = 0, npe = 0;
-        std::uint32_t nE = 0;
-        std::uint64_t n_idx = 0, n_pos = 0;
-        if (hs < gp + 16) {  // the next header starts in this granule
-          const std::uint64_t p = static_cast<std::uint64_t>(hs);
-          if (hs >= limit) {
-            X = hs;
-            fin_after = true;
-          } else if (size - hs < static_cast<std::int64_t>(kWalMeta)) {
-            X = hs;
-            bad_hdr = true;
-            fin_after = true;
-          } else {
-            const std::uint32_t o = static_cast<std::uint32_t>(hs - gp);
-            const std::uint32_t rlen = win_u32<0, 5>(D, o), stored = win_u32<1, 5>(D, o + 4);
-            const std::uint64_t klen = win_u32<4, 6>(D, o + 18), vlen = win_u32<5, 6>(D, o + 22);
-            if (static_cast<std::int64_t>(rlen) + 8 > size - hs) {
-              X = hs;
-              bad_hdr = true;
-              fin_after = true;
-            } else {
-              const std::uint64_t idx = n_all++;
-              const std::int64_t np = hs + 8 + static_cast<std::int64_t>(rlen);
-              if (kWalMeta + klen + vlen > 8ull + rlen) note_bad(idx, p);
-              if (rlen > kWalLaneMax) {
-                const std::uint64_t slt = 2 * k + (n_big & 1u);
-                a.slot_off[slt] = p + 8;
-                a.slot_len[slt] = rlen;
-                a.slot_crc[slt] = stored;
-                a.slot_loc[slt] = static_cast<std::uint32_t>(idx);
-                ++n_big;
-                hs = np;
-                if (np >= limit) {
-                  X = np;
-                  fin_after = true;
-                } else {  // re-aim the stream: step j + kLockSlots reads the granule holding np
-                  gbase = galign(np) - 16 * (j + kLockSlots);
-                  stall = kLockSlots - 1;
-                }
-              } else if (rlen < 18) {  // record_len < 18 fails the key/value bounds (noted above): stop
-                X = hs;
-                bad_hdr = true;
-                fin_after = true;
-              } else {
-                has_new = true;
-                nps = hs + 8;
-                npe = np;
-                n_idx = idx;
-                n_pos = p;
-                std::uint32_t e = stored ^ 0xFFFFFFFFu ^ linj[rlen];
-                const std::uint32_t pad = (4u - static_cast<std::uint32_t>((w0 + static_cast<std::uintptr_t>(np)) & 3u)) & 3u;
-                for (std::uint32_t t = 0; t < 3u; ++t)
-                  if (t < pad) e = (e >> 8) ^ dev::lds_at(lds, ((e & 0xFFu) << 8) | kc.L0);
-                nE = e;
-                hs = np;
-              }
-            }
-          }
-        }
-        // fold this granule's payload bytes: the end of the current payload, the start of the new one
-        const std::uint32_t m16 = (has_cur ? gran_mask(cps, cpe, gp) : 0u) | (has_new ? gran_mask(nps, npe, gp) : 0u);
-        std::int32_t rst = 4, fin = 4;
-        if (has_cur && cps >= gp) rst = static_cast<std::int32_t>((cps - gp) >> 2);
-        if (has_new && nps < gp + 16) rst = static_cast<std::int32_t>((nps - gp) >> 2);
-        if (has_cur && cpe - 1 < gp + 16) fin = static_cast<std::int32_t>((cpe - 1 - gp) >> 2);
-        if (m16) {
+  auto step = [&](std::uint32_t j, uint4& G0, const uint4& G1, const uint4& G2) {
+    const std::uint32_t gp = gb + 16u * j;
+    const bool act = !done && stall == 0;
+    stall -= (!done && stall != 0) ? 1u : 0u;
+    const std::uint32_t D[12] = {G0.x, G0.y, G0.z, G0.w, G1.x, G1.y, G1.z, G1.w, G2.x, G2.y, G2.z, G2.w};
+    // ---- the header starting in this granule, if any: its fields through a funnel of selects
+    const std::uint32_t o = hs - gp;
+    const bool ev = act && o < 16u;
+    const bool q0 = (o >> 2) & 1u, q1 = (o >> 3) & 1u;
+    const std::uint32_t bo = o & 3u;
+    // dword shift of the window by o / 4 in two stages; each select is a v_perm (selector 0x07060504
+    // takes the high operand, 0x03020100 the low one), which the compiler cannot turn back into an
+    // indexed copy of D through scratch memory, as it does with plain selects over all elements
+    const std::uint32_t s0sel = q0 ? 0x07060504u : 0x03020100u, s1sel = q1 ? 0x07060504u : 0x03020100u;
+    std::uint32_t D1[10], D2[8];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (rst == i) r = dev::Reg{0, 0};
-            if ((m16 >> (4 * i)) & 0xFu) dev::slice4(lds, r, D[i] & dword_mask(m16, i), kc);
-            if (fin == i && r.value() != cE) note_bad(c_idx, c_pos);
-          }
-        }
-        if (fin < 4) has_cur = false;
-        if (has_new) {
-          has_cur = true;
-          cps = nps;
-          cpe = npe;
-          cE = nE;
-          c_idx = n_idx;
-          c_pos = n_pos;
-        }
-        if (fin_after) done = true;
+    for (int t = 0; t < 10; ++t) D1[t] = __builtin_amdgcn_perm(D[t + 1], D[t], s0sel);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) D2[t] = __builtin_amdgcn_perm(D1[t + 2], D1[t], s1sel);
+    auto E = [&](int t) { return __builtin_amdgcn_alignbyte(D2[t + 1], D2[t], bo); };
+    const std::uint32_t rlen = E(0), stored = E(1), e4 = E(4), e5 = E(5), e6 = E(6);
+    const std::uint32_t klen = __builtin_amdgcn_alignbyte(e5, e4, 2u), vlen = __builtin_amdgcn_alignbyte(e6, e5, 2u);
+    const bool c_lim = hs >= lim;
+    const bool c_sz = szr32 - hs < static_cast<std::uint32_t>(kWalMeta);
+    const bool c_len = static_cast<std::uint64_t>(rlen) + 8u > szr - hs;
+    const bool counted = ev && !c_lim && !c_sz && !c_len;
+    const bool big = rlen > kWalLaneMax, tiny = rlen < 18u;
+    const bool kvbad = static_cast<std::uint64_t>(klen) + vlen + kWalMeta > static_cast<std::uint64_t>(rlen) + 8u;
+    const std::uint32_t idx = n_all;
+    n_all += counted ? 1u : 0u;
+    if (counted && kvbad && idx < first) {
+      first = idx;
+      first_pos = hs;
+    }
+    const bool stop = ev && (c_lim || c_sz || c_len || tiny);  // tiny: fails the bounds (noted above)
+    bad_hdr = bad_hdr || (stop && !c_lim);
+    X = stop ? static_cast<std::uint64_t>(O + hs) : X;
+    const bool has_new = counted && !big && !tiny;
+    const std::uint32_t nps = hs + 8u, npe = hs + 8u + rlen;
+    // expected register of the new payload: crc_0 = stored ^ xorout ^ Shift_L(init), shifted by the
+    // zero bytes that pad its last dword
+    std::uint32_t e = stored ^ 0xFFFFFFFFu ^ linj[big ? 0u : rlen];
+    const std::uint32_t pad = (0u - npe) & 3u;
+#pragma unroll
+    for (std::uint32_t t = 0; t < 3u; ++t) {
+      const std::uint32_t e2 = (e >> 8) ^ dev::lds_at(lds, __builtin_amdgcn_perm(e, kc.L0, 0x0C020400u));
+      e = t < pad ? e2 : e;
+    }
+    if (counted && big) {  // rare: slot for the CRC batch, then re-aim the stream past the payload
+      const std::uint64_t p = static_cast<std::uint64_t>(O + hs);
+      const std::uint64_t slt = 2 * k + (n_big & 1u);
+      a.slot_off[slt] = p + 8;
+      a.slot_len[slt] = rlen;
+      a.slot_crc[slt] = stored;
+      a.slot_loc[slt] = idx;
+      ++n_big;
+      const std::uint64_t np = p + 8 + rlen;
+      if (np >= lim64) {
+        X = np;
+        done = true;
+      } else {
+        hs = static_cast<std::uint32_t>(static_cast<std::int64_t>(np) - O);
+        gb = (hs & ~15u) - 16u * (j + kLockSlots);
+        stall = kLockSlots - 1;
       }
     }
-    G0 = load_gran(gbase + 16 * (j + kLockSlots));
+    hs = has_new ? npe : hs;
+    // ---- fold this granule's payload bytes: the end of the current payload, the start of the new one
+    auto range16 = [&](std::uint32_t lo, std::uint32_t hi) {
+      const std::int32_t l = min(max(static_cast<std::int32_t>(lo - gp), 0), 16);  // v_med3_i32
+      const std::int32_t h = min(max(static_cast<std::int32_t>(hi - gp), 0), 16);
+      return h > l ? ((1u << h) - (1u << l)) : 0u;
+    };
+    const bool cur = act && has_cur;
+    const std::uint32_t m16 = (cur ? range16(cps, cpe) : 0u) | (has_new ? range16(nps, npe) : 0u);
+    const std::uint32_t rs = cur && static_cast<std::int32_t>(cps - gp) >= 0 ? (cps - gp) >> 2
+                                                                             : (has_new ? (nps - gp) >> 2 : 7u);
+    const std::uint32_t fi = cur && cpe - 1u - gp < 16u ? (cpe - 1u - gp) >> 2 : 7u;
+    std::uint32_t vf = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      t_reg = rs == static_cast<std::uint32_t>(i) ? 0u : t_reg;
+      u_reg = rs == static_cast<std::uint32_t>(i) ? 0u : u_reg;
+      const std::uint32_t nib = (m16 >> (4 * i)) & 0xFu;
+      const std::uint32_t msk = __builtin_amdgcn_perm(0u, 0u, 0x0C0C0C0Cu + ((nib * 0x00204081u) & 0x01010101u));
+      dev::Reg r{t_reg, u_reg};
+      dev::slice4(lds, r, D[i] & msk, kc);
+      t_reg = nib ? r.t : t_reg;
+      u_reg = nib ? r.u : u_reg;
+      vf = fi == static_cast<std::uint32_t>(i) ? (t_reg ^ u_reg) : vf;
+    }
+    if (fi < 4u && vf != cE && c_idx < first) {
+      first = c_idx;
+      first_pos = cps - 8u;
+    }
+    has_cur = act ? ((has_cur && fi >= 4u) || has_new) : has_cur;
+    cps = has_new ? nps : cps;
+    cpe = has_new ? npe : cpe;
+    cE = has_new ? e : cE;
+    c_idx = has_new ? idx : c_idx;
+    done = done || stop;
+    G0 = load_gran(gb + 16u * (j + kLockSlots));
   };
   // Every lane ends within (piece + overhang of its last folded record) / 16 steps plus kLockSlots
   // per re-aim (at most two per piece); the cap is a guard that reports instead of spinning.
-  constexpr std::int64_t kMaxSteps = (kWalPiece + kWalLaneMax + 64) / 16 + 4 * kLockSlots + 64;
-  for (std::int64_t j = 0;; j += kLockSlots) {
+  constexpr std::uint32_t kMaxSteps = (kWalPiece + kWalLaneMax + 64) / 16 + 4 * kLockSlots + 64;
+  for (std::uint32_t j = 0;; j += kLockSlots) {
     if (j >= kMaxSteps) {
       if (!done) a.res[7] = 1;
       break;
@@ -601,12 +603,12 @@ __global__ __launch_bounds__(kCheckThreads) void wal_lock(WalArgs a, std::uint64
     step(j + 5, sl[5], sl[0], sl[1]);
     if (__ballot(!done) == 0) break;
   }
-  a.X[k] = static_cast<std::uint64_t>(X);
+  a.X[k] = X;
   a.broke[k] = bad_hdr ? 1 : 0;
-  a.spec_cnt[k] = (n_all << 32) | n_big;
-  a.first_loc[k] = first;
-  a.first_pos[k] = first_pos;
-  a.next[k] = (bad_hdr || static_cast<std::uint64_t>(X) >= a.size) ? a.K : static_cast<std::uint32_t>(static_cast<std::uint64_t>(X) / kWalPiece);
+  a.spec_cnt[k] = (static_cast<std::uint64_t>(n_all) << 32) | n_big;
+  a.first_loc[k] = first == 0xFFFFFFFFu ? kNone : first;
+  a.first_pos[k] = static_cast<std::uint64_t>(O + first_pos);
+  a.next[k] = (bad_hdr || X >= a.size) ? a.K : static_cast<std::uint32_t>(X / kWalPiece);
 }
 
 __global__ void wal_jump_init(WalArgs a) {
@@ -942,7 +944,7 @@ void pass_front(const WalArgs& a, std::uint64_t k_lo, std::uint64_t k_hi, hipStr
 #ifdef TKV_WAL_SPEC_WALK
   hipLaunchKernelGGL(wal_spec, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
 #else
-  hipLaunchKernelGGL(wal_lock, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
+  hipLaunchKernelGGL(wal_lock, dim3(blocks(k_hi - k_lo, kLockThreads)), dim3(kLockThreads), 0, st, a, k_lo, k_hi);
 #endif
 }
 
