@@ -361,7 +361,7 @@ __device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::
 
 // 2. Speculative walk and check of pieces [k_lo, k_hi) from their first plausible header (piece 0
 // from 0).
-[[maybe_unused]] __global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
+__global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
   __shared__ std::uint32_t lds[kLdsSliceWords];
   fill_slices(a.tabs, lds);
   const std::uint64_t k = k_lo + gid();
@@ -384,231 +384,6 @@ __device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::
   a.broke[k] = br;
   a.spec_cnt[k] = c;
   a.next[k] = (br || x >= a.size) ? a.K : static_cast<std::uint32_t>(x / kWalPiece);
-}
-
-// ---- 2 (lockstep). The same walk and checks with every lane of a wave advancing through its piece
-// one 16-byte granule per step. The granule a lane reads at step j is loaded kLockSlots steps ahead
-// into a ring of registers, so no load waits on a header: the header fields come from the granule
-// holding the header and the two after it, and payload bytes are folded as their granule passes
-// (slicing-by-4, bytes outside the payload masked to zero; leading zeros leave an init-0 register
-// at 0, and the trailing ones are matched by shifting the expected register by the same zero
-// bytes). A record whose payload exceeds kWalLaneMax goes to the piece's slots as in walk_check, and
-// the lane re-aims its stream at the next header, idling while the new granules arrive. Outputs are
-// walk_check's, except that a record too short for its key/value lengths (record_len < 18) ends the
-// lane's walk there as a broken chain: it is the first failing record of the piece either way, and
-// no record after it can change the verdict.
-constexpr int kLockSlots = 6;  // granules in flight per lane (the ring)
-constexpr unsigned kLockThreads = 512;  // 8 waves (<= 256 VGPRs each), one workgroup per CU
-constexpr unsigned kInjWords = kWalLaneMax + 1;
-
-template <int LO, int N>
-__device__ __forceinline__ std::uint32_t sel_dword(std::uint32_t i, const std::uint32_t (&D)[12]) {
-  // D[i] for LO <= i < LO + N by a select tree on the bits of i - LO. (A chain of equality selects
-  // is turned back into an indexed load from a stack copy of D by the compiler.)
-  static_assert(N >= 2 && N <= 8, "select tree of up to 8");
-  const std::uint32_t t = i - LO;
-  auto at = [&](int j) { return D[LO + (j < N ? j : N - 1)]; };
-  const bool b0 = t & 1u, b1 = (t >> 1) & 1u, b2 = (t >> 2) & 1u;
-  const std::uint32_t l0 = b0 ? at(1) : at(0), l1 = b0 ? at(3) : at(2);
-  const std::uint32_t l2 = b0 ? at(5) : at(4), l3 = b0 ? at(7) : at(6);
-  const std::uint32_t m0 = b1 ? l1 : l0, m1 = b1 ? l3 : l2;
-  return N <= 4 ? m0 : (b2 ? m1 : m0);
-}
-// Little-endian u32 at byte q of the 48-byte window D, whose dword q/4 lies in [LO, LO + N).
-template <int LO, int N>
-__device__ __forceinline__ std::uint32_t win_u32(const std::uint32_t (&D)[12], std::uint32_t q) {
-  const std::uint32_t i = q >> 2, b = q & 3u;
-  const std::uint32_t lo = sel_dword<LO, N>(i, D), hi = sel_dword<LO + 1, N>(i + 1, D);
-  return b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
-}
-// Bytes [lo, hi) of the granule at g (image offsets) as a 16-bit mask.
-__device__ __forceinline__ std::uint32_t gran_mask(std::int64_t lo, std::int64_t hi, std::int64_t g) {
-  const std::int64_t l = lo - g < 0 ? 0 : (lo - g > 16 ? 16 : lo - g);
-  const std::int64_t h = hi - g < 0 ? 0 : (hi - g > 16 ? 16 : hi - g);
-  return ((1u << static_cast<std::uint32_t>(h)) - 1u) & ~((1u << static_cast<std::uint32_t>(l)) - 1u);
-}
-// Byte mask of dword i from a 16-bit granule mask.
-__device__ __forceinline__ std::uint32_t dword_mask(std::uint32_t m16, int i) {
-  const std::uint32_t nib = (m16 >> (4 * i)) & 0xFu;
-  const std::uint32_t spread = (nib * 0x00204081u) & 0x01010101u;
-  return __builtin_amdgcn_perm(0u, 0u, 0x0C0C0C0Cu + spread);  // selector 0x0D -> 0xFF, 0x0C -> 0x00
-}
-
-__global__ __launch_bounds__(kLockThreads) void wal_lock(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
-  __shared__ std::uint32_t lds[kLdsSliceWords + kInjWords];
-  std::uint32_t* linj = lds + kLdsSliceWords;
-  for (std::uint32_t i = threadIdx.x; i < kInjWords; i += blockDim.x) linj[i] = a.inj[i];
-  fill_slices(a.tabs, lds);  // (its barrier covers linj too)
-  const std::uint64_t k = k_lo + gid();
-  if (k >= k_hi) return;
-  const std::uint64_t s0 = k == 0 ? 0 : a.S[k];
-  if (k == 0) a.S[0] = 0;
-  if (s0 == kNone) {
-    a.X[k] = kNone;
-    a.next[k] = a.K;
-    a.broke[k] = 0;
-    a.spec_cnt[k] = 0;
-    a.first_loc[k] = kNone;
-    return;
-  }
-  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
-  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
-  // Positions are u32 offsets from the lane's first granule (image offset O, a 16-byte aligned
-  // address): everything a live lane touches lies within a piece plus one folded record of it.
-  const std::uintptr_t mO = (w0 + s0) & ~static_cast<std::uintptr_t>(15);
-  const std::int64_t O = static_cast<std::int64_t>(mO - w0);
-  const std::uint64_t szr = static_cast<std::uint64_t>(static_cast<std::int64_t>(a.size) - O);  // size, relative
-  const std::uint32_t szr32 = szr > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<std::uint32_t>(szr);
-  const std::uint64_t lim64 = ((k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size);
-  const std::uint32_t lim = static_cast<std::uint32_t>(static_cast<std::int64_t>(lim64) - O);
-  std::uint32_t gb = 0;  // step j reads the granule at gb + 16 j
-  std::uint32_t hs = static_cast<std::uint32_t>(static_cast<std::int64_t>(s0) - O);  // next header start
-  bool has_cur = false;
-  std::uint32_t cps = 0, cpe = 0, cE = 0, c_idx = 0;  // payload being folded [cps, cpe), expected register
-  std::uint32_t t_reg = 0, u_reg = 0;                 // its CRC register (t ^ u)
-  std::uint32_t stall = 0;
-  bool done = false, bad_hdr = false;
-  std::uint64_t X = 0;
-  std::uint32_t n_all = 0, n_big = 0, first = 0xFFFFFFFFu, first_pos = 0;
-  const std::uintptr_t mend = w0 + a.size;
-  const std::uintptr_t safe = w0 & ~static_cast<std::uintptr_t>(15);
-  // Loads are unconditional, so the compiler's wait counts stay exact (a load behind a branch makes
-  // every later use wait for all loads in flight): a granule past the image's end, or of a finished
-  // lane, re-reads the image's first granule, and its bytes are never used. A granule holding an
-  // image byte lies in that byte's page.
-  auto load_gran = [&](std::uint32_t g) -> uint4 {
-    const std::uintptr_t m = mO + g;
-    return dev::gload16(!done && m < mend ? m : safe);
-  };
-  uint4 sl[kLockSlots];
-#pragma unroll
-  for (int t = 0; t < kLockSlots; ++t) sl[t] = load_gran(16u * t);
-
-  auto step = [&](std::uint32_t j, uint4& G0, const uint4& G1, const uint4& G2) {
-    const std::uint32_t gp = gb + 16u * j;
-    const bool act = !done && stall == 0;
-    stall -= (!done && stall != 0) ? 1u : 0u;
-    const std::uint32_t D[12] = {G0.x, G0.y, G0.z, G0.w, G1.x, G1.y, G1.z, G1.w, G2.x, G2.y, G2.z, G2.w};
-    // ---- the header starting in this granule, if any: its fields through a funnel of selects
-    const std::uint32_t o = hs - gp;
-    const bool ev = act && o < 16u;
-    const bool q0 = (o >> 2) & 1u, q1 = (o >> 3) & 1u;
-    const std::uint32_t bo = o & 3u;
-    // dword shift of the window by o / 4 in two stages; each select is a v_perm (selector 0x07060504
-    // takes the high operand, 0x03020100 the low one), which the compiler cannot turn back into an
-    // indexed copy of D through scratch memory, as it does with plain selects over all elements
-    const std::uint32_t s0sel = q0 ? 0x07060504u : 0x03020100u, s1sel = q1 ? 0x07060504u : 0x03020100u;
-    std::uint32_t D1[10], D2[8];
-#pragma unroll
-    for (int t = 0; t < 10; ++t) D1[t] = __builtin_amdgcn_perm(D[t + 1], D[t], s0sel);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) D2[t] = __builtin_amdgcn_perm(D1[t + 2], D1[t], s1sel);
-    auto E = [&](int t) { return __builtin_amdgcn_alignbyte(D2[t + 1], D2[t], bo); };
-    const std::uint32_t rlen = E(0), stored = E(1), e4 = E(4), e5 = E(5), e6 = E(6);
-    const std::uint32_t klen = __builtin_amdgcn_alignbyte(e5, e4, 2u), vlen = __builtin_amdgcn_alignbyte(e6, e5, 2u);
-    const bool c_lim = hs >= lim;
-    const bool c_sz = szr32 - hs < static_cast<std::uint32_t>(kWalMeta);
-    const bool c_len = static_cast<std::uint64_t>(rlen) + 8u > szr - hs;
-    const bool counted = ev && !c_lim && !c_sz && !c_len;
-    const bool big = rlen > kWalLaneMax, tiny = rlen < 18u;
-    const bool kvbad = static_cast<std::uint64_t>(klen) + vlen + kWalMeta > static_cast<std::uint64_t>(rlen) + 8u;
-    const std::uint32_t idx = n_all;
-    n_all += counted ? 1u : 0u;
-    if (counted && kvbad && idx < first) {
-      first = idx;
-      first_pos = hs;
-    }
-    const bool stop = ev && (c_lim || c_sz || c_len || tiny);  // tiny: fails the bounds (noted above)
-    bad_hdr = bad_hdr || (stop && !c_lim);
-    X = stop ? static_cast<std::uint64_t>(O + hs) : X;
-    const bool has_new = counted && !big && !tiny;
-    const std::uint32_t nps = hs + 8u, npe = hs + 8u + rlen;
-    // expected register of the new payload: crc_0 = stored ^ xorout ^ Shift_L(init), shifted by the
-    // zero bytes that pad its last dword
-    std::uint32_t e = stored ^ 0xFFFFFFFFu ^ linj[big ? 0u : rlen];
-    const std::uint32_t pad = (0u - npe) & 3u;
-#pragma unroll
-    for (std::uint32_t t = 0; t < 3u; ++t) {
-      const std::uint32_t e2 = (e >> 8) ^ dev::lds_at(lds, __builtin_amdgcn_perm(e, kc.L0, 0x0C020400u));
-      e = t < pad ? e2 : e;
-    }
-    if (counted && big) {  // rare: slot for the CRC batch, then re-aim the stream past the payload
-      const std::uint64_t p = static_cast<std::uint64_t>(O + hs);
-      const std::uint64_t slt = 2 * k + (n_big & 1u);
-      a.slot_off[slt] = p + 8;
-      a.slot_len[slt] = rlen;
-      a.slot_crc[slt] = stored;
-      a.slot_loc[slt] = idx;
-      ++n_big;
-      const std::uint64_t np = p + 8 + rlen;
-      if (np >= lim64) {
-        X = np;
-        done = true;
-      } else {
-        hs = static_cast<std::uint32_t>(static_cast<std::int64_t>(np) - O);
-        gb = (hs & ~15u) - 16u * (j + kLockSlots);
-        stall = kLockSlots - 1;
-      }
-    }
-    hs = has_new ? npe : hs;
-    // ---- fold this granule's payload bytes: the end of the current payload, the start of the new one
-    auto range16 = [&](std::uint32_t lo, std::uint32_t hi) {
-      const std::int32_t l = min(max(static_cast<std::int32_t>(lo - gp), 0), 16);  // v_med3_i32
-      const std::int32_t h = min(max(static_cast<std::int32_t>(hi - gp), 0), 16);
-      return h > l ? ((1u << h) - (1u << l)) : 0u;
-    };
-    const bool cur = act && has_cur;
-    const std::uint32_t m16 = (cur ? range16(cps, cpe) : 0u) | (has_new ? range16(nps, npe) : 0u);
-    const std::uint32_t rs = cur && static_cast<std::int32_t>(cps - gp) >= 0 ? (cps - gp) >> 2
-                                                                             : (has_new ? (nps - gp) >> 2 : 7u);
-    const std::uint32_t fi = cur && cpe - 1u - gp < 16u ? (cpe - 1u - gp) >> 2 : 7u;
-    std::uint32_t vf = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      t_reg = rs == static_cast<std::uint32_t>(i) ? 0u : t_reg;
-      u_reg = rs == static_cast<std::uint32_t>(i) ? 0u : u_reg;
-      const std::uint32_t nib = (m16 >> (4 * i)) & 0xFu;
-      const std::uint32_t msk = __builtin_amdgcn_perm(0u, 0u, 0x0C0C0C0Cu + ((nib * 0x00204081u) & 0x01010101u));
-      dev::Reg r{t_reg, u_reg};
-      dev::slice4(lds, r, D[i] & msk, kc);
-      t_reg = nib ? r.t : t_reg;
-      u_reg = nib ? r.u : u_reg;
-      vf = fi == static_cast<std::uint32_t>(i) ? (t_reg ^ u_reg) : vf;
-    }
-    if (fi < 4u && vf != cE && c_idx < first) {
-      first = c_idx;
-      first_pos = cps - 8u;
-    }
-    has_cur = act ? ((has_cur && fi >= 4u) || has_new) : has_cur;
-    cps = has_new ? nps : cps;
-    cpe = has_new ? npe : cpe;
-    cE = has_new ? e : cE;
-    c_idx = has_new ? idx : c_idx;
-    done = done || stop;
-    G0 = load_gran(gb + 16u * (j + kLockSlots));
-  };
-  // Every lane ends within (piece + overhang of its last folded record) / 16 steps plus kLockSlots
-  // per re-aim (at most two per piece); the cap is a guard that reports instead of spinning.
-  constexpr std::uint32_t kMaxSteps = (kWalPiece + kWalLaneMax + 64) / 16 + 4 * kLockSlots + 64;
-  for (std::uint32_t j = 0;; j += kLockSlots) {
-    if (j >= kMaxSteps) {
-      if (!done) a.res[7] = 1;
-      break;
-    }
-    step(j + 0, sl[0], sl[1], sl[2]);
-    step(j + 1, sl[1], sl[2], sl[3]);
-    step(j + 2, sl[2], sl[3], sl[4]);
-    step(j + 3, sl[3], sl[4], sl[5]);
-    step(j + 4, sl[4], sl[5], sl[0]);
-    step(j + 5, sl[5], sl[0], sl[1]);
-    if (__ballot(!done) == 0) break;
-  }
-  a.X[k] = X;
-  a.broke[k] = bad_hdr ? 1 : 0;
-  a.spec_cnt[k] = (static_cast<std::uint64_t>(n_all) << 32) | n_big;
-  a.first_loc[k] = first == 0xFFFFFFFFu ? kNone : first;
-  a.first_pos[k] = static_cast<std::uint64_t>(O + first_pos);
-  a.next[k] = (bad_hdr || X >= a.size) ? a.K : static_cast<std::uint32_t>(X / kWalPiece);
 }
 
 __global__ void wal_jump_init(WalArgs a) {
@@ -654,7 +429,6 @@ __global__ void wal_publish(WalArgs a, std::uint64_t* h) {
   if (i < 7) h[i] = a.res[i];
   if (i == 7) h[7] = a.base[a.K - 1];
   if (i == 8) h[8] = a.cnt[a.K - 1];
-  if (i == 9) h[9] = a.res[7];
 }
 
 // 3. One quadrupling round (J = next^(4^t)): every marked k marks J(k), J(J(k)) and J(J(J(k))), then
@@ -930,8 +704,7 @@ int pass_begin(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStre
   s.h_res[4] = 0;
   s.h_res[5] = 0;
   s.h_res[6] = 0;
-  s.h_res[7] = 0;
-  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 8 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
+  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 7 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
   WAL_HIP(hipMemsetAsync(a.S, 0xFF, K * sizeof(std::uint64_t), st));
   *out = a;
   return TKV_OK;
@@ -941,11 +714,7 @@ void pass_front(const WalArgs& a, std::uint64_t k_lo, std::uint64_t k_hi, hipStr
   if (k_hi <= k_lo) return;
   const std::uint64_t threads = (k_hi - k_lo + 64 / kHeadLanes - 1) / (64 / kHeadLanes) * 64;  // 8 pieces per wave
   hipLaunchKernelGGL(wal_scan_head, dim3(blocks(threads, kScanThreads)), dim3(kScanThreads), 0, st, a, k_lo, k_hi);
-#ifdef TKV_WAL_SPEC_WALK
   hipLaunchKernelGGL(wal_spec, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
-#else
-  hipLaunchKernelGGL(wal_lock, dim3(blocks(k_hi - k_lo, kLockThreads)), dim3(kLockThreads), 0, st, a, k_lo, k_hi);
-#endif
 }
 
 int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
@@ -975,7 +744,6 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
   };
   hipLaunchKernelGGL(wal_fast, dim3(blocks(K, 256)), dim3(256), 0, st, a);
   if (int rc = count_and_publish()) return rc;
-  if (s.h_res[9]) return set_error(TKV_IO_ERROR, "device WAL walk exceeded its step bound");
   if (s.h_res[6]) g_last[3] = 0;
   if (s.h_res[6]) {
     // the speculation was wrong somewhere: pointer jumping marks the pieces on the true chain
