@@ -180,7 +180,7 @@ __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 //   * compacts large blocks into big_off/big_len/big_idx with their row offsets (row_scan) for the
 //     row kernel, and records the first large block of every row-kernel wave (wave_start),
 //   * leaves counts = {large blocks, small blocks, rows of large blocks}.
-constexpr int kScanTile = 4096;  // blocks per scan workgroup (1024 threads x 4)
+constexpr int kScanTile = 4096;  // blocks per scan workgroup (rows_tile_scan)
 
 __device__ __forceinline__ std::uint64_t scan_item(std::uint32_t len) {
   return len <= kSmallMax ? 1ull : static_cast<std::uint64_t>(rows_for_len(len)) << 32;
@@ -206,25 +206,34 @@ __device__ __forceinline__ StreamGeom stream_geometry(const std::uint8_t* base, 
   return {zoff, s0rel, end >= off0 ? (end - off0 + s0rel + kRow - 1) / kRow : 0};
 }
 
-__global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase, const std::uint64_t* offsets,
-                                                      const std::uint32_t* lengths, std::uint32_t n,
-                                                      std::uint64_t* scan, std::uint64_t* tile_sums,
-                                                      std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
-                                                      std::uint32_t* lscan, std::uint32_t* tile_lanes) {
-  __shared__ std::uint64_t wsum[16];
-  __shared__ std::uint32_t lsum[16], lcnt[16];
+// One workgroup per scan tile of kScanTile blocks, kTileThreads threads with kScanTile / kTileThreads
+// consecutive blocks each.
+#ifndef TKV_SCAN_THREADS
+#define TKV_SCAN_THREADS 1024
+#endif
+constexpr unsigned kTileThreads = TKV_SCAN_THREADS;
+constexpr unsigned kTileWaves = kTileThreads / 64;
+constexpr unsigned kTileBpt = kScanTile / kTileThreads;
+static_assert(kScanTile % kTileThreads == 0 && kTileWaves >= 1, "tile shape");
+__global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_t* sbase, const std::uint64_t* offsets,
+                                                              const std::uint32_t* lengths, std::uint32_t n,
+                                                              std::uint64_t* scan, std::uint64_t* tile_sums,
+                                                              std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
+                                                              std::uint32_t* lscan, std::uint32_t* tile_lanes) {
+  __shared__ std::uint64_t wsum[kTileWaves];
+  __shared__ std::uint32_t lsum[kTileWaves], lcnt[kTileWaves];
   // stream mode's wave partition (used only if the prepass picks stream mode): row0[0..Ws], grid-stride
-  for (std::uint32_t w = blockIdx.x * 1024u + threadIdx.x; w <= Ws; w += gridDim.x * 1024u) {
+  for (std::uint32_t w = blockIdx.x * kTileThreads + threadIdx.x; w <= Ws; w += gridDim.x * kTileThreads) {
     const std::uint64_t TR = stream_geometry(sbase, offsets, lengths, n).rows;
     row0[w] = static_cast<std::uint32_t>(dev::stream_row0<kStreamSkew>(w, TR, Ws));
   }
-  const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * 4u;
+  const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * kTileBpt;
   const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  std::uint32_t len[4], lv[4];
+  std::uint32_t len[kTileBpt], lv[kTileBpt];
   bool ok = true;
   unsigned nlw = 0;  // lane blocks (len <= kLaneMax) of this wave
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (unsigned i = 0; i < kTileBpt; ++i) {
     const std::uint64_t b = base + i;
     len[i] = b < n ? lengths[b] : 0u;
     lv[i] = b < n && len[i] <= kLaneMax ? 1u : 0u;
@@ -239,20 +248,20 @@ __global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase
   // lane-phase walk over its metadata.
   std::uint32_t nlt = 0;
 #pragma unroll
-  for (unsigned w = 0; w < 16; ++w) nlt += lcnt[w];
+  for (unsigned w = 0; w < kTileWaves; ++w) nlt += lcnt[w];
   const bool dense = nlt >= kLaneDenseTile;
   if (threadIdx.x == 0) tile_ok[blockIdx.x] = (tile_all_ok ? kTileStream : 0u) | (dense ? kTileLanes : 0u);
-  std::uint64_t v[4], s = 0;
+  std::uint64_t v[kTileBpt], s = 0;
   std::uint32_t ls = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (unsigned i = 0; i < kTileBpt; ++i) {
     lv[i] = dense ? lv[i] : 0u;
     v[i] = base + i < n && !lv[i] ? scan_item(len[i]) : 0ull;
     s += v[i];
     ls += lv[i];
   }
   // Inclusive scans of the thread sums inside the wave (cross-lane shifts, no barriers), then the
-  // 16 wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
+  // wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
   std::uint64_t inc = s;
   std::uint32_t linc = ls;
 #pragma unroll
@@ -270,7 +279,7 @@ __global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase
   std::uint64_t wpre = 0, tot = 0;
   std::uint32_t lpre = 0, ltot = 0;
 #pragma unroll
-  for (unsigned w = 0; w < 16; ++w) {
+  for (unsigned w = 0; w < kTileWaves; ++w) {
     const std::uint64_t t = wsum[w];
     const std::uint32_t lt = lsum[w];
     wpre += w < wid ? t : 0ull;
@@ -281,7 +290,7 @@ __global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase
   std::uint64_t run = wpre + inc - s;  // exclusive
   std::uint32_t lrun = lpre + linc - ls;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (unsigned i = 0; i < kTileBpt; ++i) {
     if (base + i < n && !lv[i]) {  // the scatter reads these for listed blocks only
       scan[base + i] = run;
       lscan[base + i] = lrun;
@@ -289,7 +298,7 @@ __global__ __launch_bounds__(1024) void rows_tile_scan(const std::uint8_t* sbase
     run += v[i];
     lrun += lv[i];
   }
-  if (threadIdx.x == 1023) {
+  if (threadIdx.x == kTileThreads - 1) {
     tile_sums[blockIdx.x] = tot;
     tile_lanes[blockIdx.x] = ltot;
   }
@@ -696,7 +705,7 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
   const std::uint64_t ntiles = prepass_tiles(n);
   const std::uint64_t nfused = (static_cast<std::uint64_t>(n) + kFinishThreads - 1) / kFinishThreads;
   const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
-  hipLaunchKernelGGL(rows_tile_scan, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets, lengths,
+  hipLaunchKernelGGL(rows_tile_scan, dim3(static_cast<unsigned>(ntiles)), dim3(kTileThreads), 0, st, base, offsets, lengths,
                      n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes);
   if (ntiles <= kFusedTiles) {
     hipLaunchKernelGGL(rows_finish_fused, dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
