@@ -180,3 +180,33 @@ def test_lane_blocks_then_stream_batch_same_scratch(gpu, oracle, buf):
     for offs, lens in batches * 2:
         got = u32(tk.crc32_batch(d, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu)))
         assert np.array_equal(got, oracle.batch(host, offs, lens))
+
+
+@pytest.mark.parametrize("shape", ["wal_payloads", "mixed_gaps", "back_to_back_128"])
+def test_irregular_more_than_1024_tiles(gpu, oracle, shape):
+    """Batches of more than 4 M blocks (over 1024 prepass tiles of 4096 blocks) take the 512-thread
+    tile scan: lane-dense tiles (WAL payloads), tiles mixing lane, small and large blocks with random
+    gaps, and sparse tiles whose scan entries are all written (128-byte blocks back to back); per-block
+    initial registers on the mixed batch."""
+    rng = np.random.default_rng({"wal_payloads": 1, "mixed_gaps": 2, "back_to_back_128": 3}[shape])
+    n = 4096 * 1025 + 777
+    if shape == "wal_payloads":
+        offs, lens = wal_payloads(rng, n, WAL_SIZES, 3)
+    elif shape == "mixed_gaps":
+        lens = np.where(rng.random(n) < 0.6, rng.integers(0, 65, n), rng.integers(65, 1025, n))
+        lens[rng.integers(0, n, 50)] = rng.integers(1025, 9000, 50)
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])]) + rng.integers(0, 5, n).cumsum()
+    else:
+        lens = np.full(n, 128)
+        offs = 5 + np.arange(n, dtype=np.int64) * 128
+    lens = lens.astype(np.int32)
+    size = int((offs + lens).max()) + 16
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    d = torch.from_numpy(host).to(gpu)
+    o = torch.from_numpy(offs.astype(np.int64)).to(gpu)
+    ln = torch.from_numpy(lens).to(gpu)
+    assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), oracle.batch(host, offs, lens))
+    if shape == "mixed_gaps":
+        init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))
+        assert np.array_equal(got, oracle.batch(host, offs, lens, init))

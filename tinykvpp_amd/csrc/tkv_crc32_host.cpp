@@ -386,7 +386,7 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     }
     const std::uint64_t ntiles = prepass_tiles(cap) + 1;
     // 8-byte arrays first: scan, tiles, s_off, big_off; then the 4-byte ones
-    const std::uint64_t bytes = 8 * (cap + ntiles + 2 * cap) + 4 * (6 * cap + 1) + 4 * 2 * ntiles;
+    const std::uint64_t bytes = 8 * (cap + ntiles + 2 * cap) + 4 * (6 * cap + 1) + 4 * 2 * ntiles + 16;
     TKV_HIP(hipMalloc(&s->blob, bytes));
     auto* p8 = static_cast<std::uint64_t*>(s->blob);
     s->scan = p8;
@@ -401,7 +401,9 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     s->po.row_scan = p4 + 4 * cap;  // cap + 1 entries
     s->tile_ok = p4 + 5 * cap + 1;
     s->po.tile_lanes = s->tile_ok + ntiles;
-    s->po.lscan = s->po.tile_lanes + ntiles;  // cap entries
+    // cap entries, 16-byte aligned (rows_tile_scan stores them 16 bytes at a time)
+    s->po.lscan = reinterpret_cast<std::uint32_t*>(
+        (reinterpret_cast<std::uintptr_t>(s->po.tile_lanes + ntiles) + 15) & ~static_cast<std::uintptr_t>(15));
     s->cap_blocks = cap;
   }
   s->po.wave_start = s->wave_start;

@@ -206,20 +206,22 @@ __device__ __forceinline__ StreamGeom stream_geometry(const std::uint8_t* base, 
   return {zoff, s0rel, end >= off0 ? (end - off0 + s0rel + kRow - 1) / kRow : 0};
 }
 
-// One workgroup per scan tile of kScanTile blocks, kTileThreads threads with kScanTile / kTileThreads
-// consecutive blocks each.
-#ifndef TKV_SCAN_THREADS
-#define TKV_SCAN_THREADS 1024
-#endif
-constexpr unsigned kTileThreads = TKV_SCAN_THREADS;
-constexpr unsigned kTileWaves = kTileThreads / 64;
-constexpr unsigned kTileBpt = kScanTile / kTileThreads;
-static_assert(kScanTile % kTileThreads == 0 && kTileWaves >= 1, "tile shape");
+// One workgroup per scan tile of kScanTile blocks, T threads with kScanTile / T consecutive blocks
+// each. Batches of more than kFusedTiles tiles (over 4 M blocks: WAL-record-sized batches) take
+// 512-thread tiles, which keep more tiles in flight per CU; fewer tiles keep 1024 threads (in one
+// process, 1 GiB batches, profiles/r3/scan_tiles/: WAL payloads of 36 B with 8-byte gaps 1820 ->
+// 1957 GB/s, back-to-back 36 B 1991 -> 2212, 64 B 2687 -> 2818, 128 B 730 -> 697 GB/s; cfg4 and
+// the 64 KiB stream batch unchanged either way).
+template <unsigned kTileThreads>
 __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_t* sbase, const std::uint64_t* offsets,
                                                               const std::uint32_t* lengths, std::uint32_t n,
                                                               std::uint64_t* scan, std::uint64_t* tile_sums,
                                                               std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
                                                               std::uint32_t* lscan, std::uint32_t* tile_lanes) {
+  constexpr unsigned kTileWaves = kTileThreads / 64;
+  constexpr unsigned kTileBpt = kScanTile / kTileThreads;
+  static_assert(kScanTile % kTileThreads == 0 && kTileWaves >= 1 && kTileBpt >= 4 && kTileBpt % 4 == 0,
+                "tile shape");
   __shared__ std::uint64_t wsum[kTileWaves];
   __shared__ std::uint32_t lsum[kTileWaves], lcnt[kTileWaves];
   // stream mode's wave partition (used only if the prepass picks stream mode): row0[0..Ws], grid-stride
@@ -289,14 +291,31 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   }
   std::uint64_t run = wpre + inc - s;  // exclusive
   std::uint32_t lrun = lpre + linc - ls;
+  if (!dense && base + kTileBpt <= n) {
+    // every block of a sparse tile is listed: this thread's entries as whole 16-byte stores
+    // (scan and lscan are 256-byte aligned scratch, base a multiple of kTileBpt >= 4)
+    std::uint64_t sc[kTileBpt];
 #pragma unroll
-  for (unsigned i = 0; i < kTileBpt; ++i) {
-    if (base + i < n && !lv[i]) {  // the scatter reads these for listed blocks only
-      scan[base + i] = run;
-      lscan[base + i] = lrun;
+    for (unsigned i = 0; i < kTileBpt; ++i) {
+      sc[i] = run;
+      run += v[i];
     }
-    run += v[i];
-    lrun += lv[i];
+#pragma unroll
+    for (unsigned i = 0; i < kTileBpt; i += 2)
+      *reinterpret_cast<ulonglong2*>(scan + base + i) = make_ulonglong2(sc[i], sc[i + 1]);
+#pragma unroll
+    for (unsigned i = 0; i < kTileBpt; i += 4)
+      *reinterpret_cast<uint4*>(lscan + base + i) = make_uint4(lrun, lrun, lrun, lrun);
+  } else {
+#pragma unroll
+    for (unsigned i = 0; i < kTileBpt; ++i) {
+      if (base + i < n && !lv[i]) {  // the scatter reads these for listed blocks only
+        scan[base + i] = run;
+        lscan[base + i] = lrun;
+      }
+      run += v[i];
+      lrun += lv[i];
+    }
   }
   if (threadIdx.x == kTileThreads - 1) {
     tile_sums[blockIdx.x] = tot;
@@ -705,8 +724,12 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
   const std::uint64_t ntiles = prepass_tiles(n);
   const std::uint64_t nfused = (static_cast<std::uint64_t>(n) + kFinishThreads - 1) / kFinishThreads;
   const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
-  hipLaunchKernelGGL(rows_tile_scan, dim3(static_cast<unsigned>(ntiles)), dim3(kTileThreads), 0, st, base, offsets, lengths,
-                     n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes);
+  if (ntiles <= kFusedTiles)
+    hipLaunchKernelGGL(rows_tile_scan<1024>, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets,
+                       lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes);
+  else
+    hipLaunchKernelGGL(rows_tile_scan<512>, dim3(static_cast<unsigned>(ntiles)), dim3(512), 0, st, base, offsets,
+                       lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes);
   if (ntiles <= kFusedTiles) {
     hipLaunchKernelGGL(rows_finish_fused, dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
                        offsets, lengths, n, scan, tile_sums, tile_ok, static_cast<std::uint32_t>(ntiles), counts, o,
