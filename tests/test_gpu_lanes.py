@@ -185,9 +185,9 @@ def test_lane_blocks_then_stream_batch_same_scratch(gpu, oracle, buf):
 @pytest.mark.parametrize("shape", ["wal_payloads", "mixed_gaps", "back_to_back_128"])
 def test_irregular_more_than_1024_tiles(gpu, oracle, shape):
     """Batches of more than 4 M blocks (over 1024 prepass tiles of 4096 blocks) take the 512-thread
-    tile scan: lane-dense tiles (WAL payloads), tiles mixing lane, small and large blocks with random
-    gaps, and sparse tiles whose scan entries are all written (128-byte blocks back to back); per-block
-    initial registers on the mixed batch."""
+    tile scan and the unfused scatter: lane-dense tiles (WAL payloads), tiles mixing lane, small and
+    large blocks with random gaps, and 128-byte blocks back to back, which take stream mode through
+    rows_scan_tiles' verdict; per-block initial registers on the mixed batch."""
     rng = np.random.default_rng({"wal_payloads": 1, "mixed_gaps": 2, "back_to_back_128": 3}[shape])
     n = 4096 * 1025 + 777
     if shape == "wal_payloads":
@@ -206,6 +206,8 @@ def test_irregular_more_than_1024_tiles(gpu, oracle, shape):
     o = torch.from_numpy(offs.astype(np.int64)).to(gpu)
     ln = torch.from_numpy(lens).to(gpu)
     assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), oracle.batch(host, offs, lens))
+    # back-to-back blocks longer than kLaneMax take stream mode at any batch size
+    assert mode() == (1 if shape == "back_to_back_128" else 0)
     if shape == "mixed_gaps":
         init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
         got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))

@@ -323,13 +323,23 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   }
 }
 
+// Scan of the tile sums for batches of more than kFusedTiles tiles (one workgroup), with the
+// stream-mode verdict over all tiles: when every tile qualified, counts and s_info take stream mode's
+// values (as stream_block does for fused batches) and rows_finish builds the block ends.
+__device__ __forceinline__ StreamGeom stream_geometry(const std::uint8_t* base, const std::uint64_t* offsets,
+                                                      const std::uint32_t* lengths, std::uint32_t n);
 __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums, std::uint32_t* tile_lanes,
-                                                       std::uint32_t ntiles, std::uint32_t n, std::uint32_t* counts) {
+                                                       std::uint32_t ntiles, std::uint32_t n, std::uint32_t* counts,
+                                                       const std::uint32_t* tile_ok, const std::uint8_t* base,
+                                                       const std::uint64_t* offsets, const std::uint32_t* lengths,
+                                                       std::uint64_t* sinfo) {
   __shared__ std::uint64_t part[1024];
   __shared__ std::uint32_t lpart[1024];
   std::uint64_t carry = 0, lcarry = 0;
+  bool all_stream = true;
   for (std::uint32_t t0 = 0; t0 < ntiles; t0 += 1024) {
     const std::uint32_t i = t0 + threadIdx.x;
+    all_stream = all_stream && (i >= ntiles || (tile_ok[i] & kTileStream) != 0);
     const std::uint64_t x = i < ntiles ? tile_sums[i] : 0ull;
     const std::uint32_t lx = i < ntiles ? tile_lanes[i] : 0u;
     part[threadIdx.x] = x;
@@ -353,12 +363,24 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
     carry += tot;
     lcarry += ltot;
   }
+  const bool stream = __syncthreads_and(all_stream ? 1 : 0) != 0;
   if (threadIdx.x == 0) {
+    if (stream) {
+      const StreamGeom g = stream_geometry(base, offsets, lengths, n);
+      counts[0] = 0;
+      counts[1] = 0;
+      counts[2] = static_cast<std::uint32_t>(g.rows);
+      counts[3] = kModeStream;
+      counts[kCountLanes] = 0;  // every block is longer than kLaneMax in stream mode
+      sinfo[0] = g.zoff;
+      sinfo[1] = g.s0rel;
+      return;
+    }
     const std::uint32_t ns = static_cast<std::uint32_t>(carry), nl = static_cast<std::uint32_t>(lcarry);
     counts[0] = n - ns - nl;                               // large blocks
     counts[1] = ns;                                        // small blocks
     counts[2] = static_cast<std::uint32_t>(carry >> 32);  // rows of the large blocks
-    counts[3] = 0;                                         // general path (no stream mode here)
+    counts[3] = 0;                                         // general path
     counts[kCountLanes] = nl;                              // lane blocks
   }
 }
@@ -394,12 +416,23 @@ __device__ __forceinline__ void finish_block(std::uint64_t off, std::uint32_t le
   if (whi > wlo && (whi - 1) * TR / W > lo) out[b] = 0u;
 }
 
-__global__ void rows_finish(const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
-                            const std::uint64_t* scan, const std::uint64_t* tile_offs, const std::uint32_t* counts,
-                            const std::uint32_t* tile_ok, PrepassOut o, std::uint32_t W, std::uint32_t* out) {
+__device__ __forceinline__ void stream_block(const std::uint8_t* base, const std::uint64_t* offsets,
+                                             const std::uint32_t* lengths, std::uint32_t n, std::uint64_t b,
+                                             std::uint64_t off, std::uint32_t len, std::uint32_t W,
+                                             const std::uint32_t* row0, std::uint32_t* counts, std::uint64_t* ends,
+                                             std::uint64_t* sinfo, std::uint32_t* wave_start);
+__global__ void rows_finish(const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
+                            std::uint32_t n, const std::uint64_t* scan, const std::uint64_t* tile_offs,
+                            std::uint32_t* counts, const std::uint32_t* tile_ok, PrepassOut o, std::uint32_t W,
+                            std::uint32_t* out, std::uint64_t* ends, std::uint64_t* sinfo, std::uint32_t Ws,
+                            const std::uint32_t* row0) {
   const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
   if (b >= n) return;
   const std::uint32_t len = lengths[b];
+  if (dev::sload32(counts, 3) == kModeStream) {  // rows_scan_tiles found every tile back to back
+    stream_block(base, offsets, lengths, n, b, offsets[b], len, Ws, row0, counts, ends, sinfo, o.wave_start);
+    return;
+  }
   const std::uint64_t t = b / kScanTile;
   const bool dense = (tile_ok[t] & kTileLanes) != 0;
   if (len <= kLaneMax && dense) return;  // the lane phase's
@@ -736,9 +769,9 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
                        W, out, ends, sinfo, Ws, row0);
   } else {
     hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, o.tile_lanes,
-                       static_cast<std::uint32_t>(ntiles), n, counts);
-    hipLaunchKernelGGL(rows_finish, dim3(static_cast<unsigned>(nfinish)), dim3(256), 0, st, offsets, lengths, n, scan,
-                       tile_sums, counts, tile_ok, o, W, out);
+                       static_cast<std::uint32_t>(ntiles), n, counts, tile_ok, base, offsets, lengths, sinfo);
+    hipLaunchKernelGGL(rows_finish, dim3(static_cast<unsigned>(nfinish)), dim3(256), 0, st, base, offsets, lengths,
+                       n, scan, tile_sums, counts, tile_ok, o, W, out, ends, sinfo, Ws, row0);
   }
   return hipGetLastError();
 }
