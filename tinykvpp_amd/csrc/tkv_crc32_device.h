@@ -1282,6 +1282,125 @@ __device__ __forceinline__ void crc_packed_small_body(const RowsArgs& a, std::ui
 }
 
 // ---- lane blocks ------------------------------------------------------------------
+// (declared here for crc_packed_small_gen_body below, defined with the lane kernels)
+constexpr int kLaneGran = 5;  // granules covering 64 bytes at any alignment
+template <int ALIGN>
+__device__ __forceinline__ void lane_dwords(const uint4 (&g)[kLaneGran], std::uint32_t o, std::uint32_t (&d)[16]);
+
+// ---- general small uniform blocks: 64 < L <= 64 G bytes (G = 2 .. 32 lanes per
+// block), any stride (overlapping or gapped), any base alignment, optional per-block initial
+// registers. The slot layout of crc_packed_small_body: block b sits right-aligned in a slot of 64 G
+// bytes, lane g of its group folds [start_b + L - 64 G + 64 g, + 64), a row holds 64/G blocks. Each
+// lane loads the five 16-byte granules covering its 64 bytes and realigns them in registers
+// (lane_dwords); a granule holding no byte of the block reads the zero buffer, so no load leaves the
+// block, and the bytes in front of the block in a straddling granule are masked (leading zeros leave
+// an init-0 register at 0). The init term is spread over the group: lane g adds
+// bit_i(init) * Shift_L(1 << i) for its 32/G bits i, before the group XOR.
+// INIT: the batch has per-block initial registers (a.init_raw); without, the init term is one constant.
+template <int G, bool INIT, int DEPTH, int ILP, int PRIO = 0>
+__device__ __forceinline__ void crc_packed_small_gen_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(G >= 2 && G <= 32 && (G & (G - 1)) == 0, "G-lane groups of a power of two, 2 to 32");
+  static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
+  constexpr std::uint32_t kBpr = 64u / G;   // blocks per row
+  constexpr int kBits = INIT ? 32 / G : 1;  // init bits per lane
+  fill_lds_group<G>(a.tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u, gl = lane % G, lane_blk = lane / G;
+  const LaneConst kc = lane_const(lane);
+  const std::uint32_t L = a.len;
+  std::uint32_t hsr[kBits];  // Shift_L(1 << i) for this lane's init bits
+#pragma unroll
+  for (int i = 0; i < kBits; ++i) hsr[i] = INIT ? a.tabs->head_shift[L][gl * kBits + i] : 0u;
+  const std::uint32_t K = multmodp(a.head_z, a.init_default, a.tabs->poly) ^ a.out_xor;
+  __syncthreads();
+
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves, TR = a.total_rows;
+  const std::uint32_t r0 = static_cast<std::uint32_t>(wave * TR / W);
+  const std::uint32_t nrows = static_cast<std::uint32_t>((wave + 1) * TR / W) - r0;
+  if (nrows == 0) return;
+  const std::uint64_t stride = a.stride;
+  const std::int64_t c_lane = static_cast<std::int64_t>(L) - 64 * G + 64 * static_cast<std::int64_t>(gl);
+  const std::uint64_t row_stride = static_cast<std::uint64_t>(kBpr) * stride;
+  const std::uintptr_t blk_base = reinterpret_cast<std::uintptr_t>(a.base) +
+                                  (static_cast<std::uint64_t>(r0) * kBpr + lane_blk) * stride;  // block of row 0
+  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
+  // bytes in front of the block, per dword k of the lane's 64: the low `before` bytes are zeroed
+  std::uint32_t zmask[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const std::int64_t before = -(c_lane + 4 * k);
+    const std::uint32_t sh = static_cast<std::uint32_t>(before < 0 ? 0 : (before > 4 ? 4 : before)) * 8u;
+    zmask[k] = static_cast<std::uint32_t>(0xFFFFFFFFull << sh);
+  }
+
+  uint4 buf[DEPTH][kLaneGran];
+  std::uint32_t o16[DEPTH];
+  auto issue = [&](std::uint32_t j, int slot) {
+    const std::uint32_t jc = j < nrows ? j : nrows - 1;  // rows past the range reload the last one
+    const bool live = static_cast<std::uint64_t>(r0 + jc) * kBpr + lane_blk < a.nblocks;
+    const std::uintptr_t blo = blk_base + static_cast<std::uint64_t>(jc) * row_stride, bhi = blo + L;
+    const std::uintptr_t p = static_cast<std::uintptr_t>(static_cast<std::int64_t>(blo) + c_lane);
+    const std::uintptr_t al = p & ~static_cast<std::uintptr_t>(15);
+#pragma unroll
+    for (int i = 0; i < kLaneGran; ++i) {
+      const std::uintptr_t q = al + 16u * i;
+      buf[slot][i] = gload16(live && q + 16u > blo && q < bhi ? q : dmy);
+    }
+    o16[slot] = static_cast<std::uint32_t>(p & 15u);
+  };
+  std::uint32_t keep = 0;
+  const std::uint32_t keep_src = ((lane % kBpr) * G + (G - 1u)) * 4u;  // byte address for ds_bpermute
+  auto finish = [&](std::uint32_t j, std::uint32_t p) {
+    std::uint32_t v = lane_shift(lds, p, kc);
+    const std::uint64_t blk = static_cast<std::uint64_t>(r0 + j) * kBpr + lane_blk;
+    if constexpr (INIT) {
+      const std::uint32_t init = a.init_raw[blk < a.nblocks ? blk : a.nblocks - 1u];
+#pragma unroll
+      for (int i = 0; i < kBits; ++i)
+        v ^= static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), gl * kBits + i, 1)) & hsr[i];
+      v = group_xor<G>(v) ^ a.out_xor;
+    } else {
+      v = group_xor<G>(v) ^ K;
+    }
+    const std::uint32_t pulled = static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(keep_src),
+                                                                                        static_cast<int>(v)));
+    const std::uint32_t slot = j % G;
+    keep = lane / kBpr == slot ? pulled : keep;
+    if (slot == G - 1u || j + 1u == nrows) {
+      const std::uint64_t ob = static_cast<std::uint64_t>(r0 + j - slot) * kBpr + lane;
+      if (lane < (slot + 1u) * kBpr && ob < a.nblocks) a.out[ob] = keep;
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < DEPTH - ILP; ++s) issue(s, s);
+  for (std::uint32_t j = 0; j < nrows; j += DEPTH) {
+    if constexpr (PRIO != 0) set_prio_from_left<PRIO>(nrows - j, nrows);
+#pragma unroll
+    for (int q = 0; q < DEPTH; q += ILP) {
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) issue(j + q + DEPTH - ILP + i, (q + DEPTH - ILP + i) % DEPTH);
+      const std::uint32_t jq = j + q;
+      if (jq >= nrows) break;
+      std::uint32_t d[ILP][16];
+      Reg p[ILP];
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) {
+        lane_dwords<1>(buf[q + i], o16[q + i], d[i]);
+        p[i] = Reg{0, 0};
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) slice4(lds, p[i], d[i][k] & zmask[k], kc);
+      }
+#pragma unroll
+      for (int i = 0; i < ILP; ++i)
+        if (jq + i < nrows) finish(jq + i, p[i].value());
+    }
+  }
+}
+
 // One lane folds one whole block of at most kLaneMax = 64 bytes. It starts from the block's own initial
 // register and takes the bytes in the reference's order (crc32.cpp:9-16): whole dwords by slicing-by-4,
 // the last len % 4 bytes by Sarwate steps. There is no GF(2) shift, no lane shift and no reduction, so
@@ -1290,8 +1409,7 @@ __device__ __forceinline__ void crc_packed_small_body(const RowsArgs& a, std::ui
 // lies in a page the block maps, so no load can fault whatever the block's alignment. They are
 // realigned in registers: two bitwise selects by the start's dword offset within its granule, then
 // v_alignbyte by its byte offset. ALIGN 16 (every block start 16-byte aligned) needs neither, ALIGN 4
-// (dword aligned) only the selects.
-constexpr int kLaneGran = 5;  // granules covering 64 bytes at any alignment
+// (dword aligned) only the selects. (kLaneGran and lane_dwords are declared above.)
 
 // ngr: granules worth loading (a wave-uniform bound; the granules past it are never read).
 template <int ALIGN>

@@ -31,6 +31,8 @@ hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st);
 std::uint32_t packed_small_group(std::uint32_t len);
 hipError_t launch_packed_small(const RowsArgs& a, unsigned grid, hipStream_t st);
 hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st);
+std::uint32_t packed_small_gen_group(std::uint32_t len);
+hipError_t launch_packed_small_gen(const RowsArgs& a, unsigned grid, hipStream_t st);
 hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
                           std::uint32_t n, std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* tile_ok,
                           std::uint32_t* counts, std::uint64_t* sinfo, std::uint64_t* ends, const PrepassOut& o,
@@ -484,6 +486,16 @@ int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t s
         1, std::min<std::uint64_t>(c->ncu, (a.total_rows + kWavesPerWG - 1) / kWavesPerWG));
     a.nwaves = static_cast<std::uint32_t>(grid * kWavesPerWG);
     TKV_HIP(launch_packed_small(a, static_cast<unsigned>(grid), st));
+    return TKV_OK;
+  }
+  if (packed_small_gen_group(a.len)) {
+    // the same slots for any other length of 65 B - 2 KiB, stride, alignment or initial registers
+    const std::uint64_t bpr = 64u / packed_small_gen_group(a.len);
+    a.total_rows = static_cast<std::uint32_t>((n + bpr - 1) / bpr);
+    const std::uint64_t grid = std::max<std::uint64_t>(
+        1, std::min<std::uint64_t>(c->ncu, (a.total_rows + kWavesPerWG - 1) / kWavesPerWG));
+    a.nwaves = static_cast<std::uint32_t>(grid * kWavesPerWG);
+    TKV_HIP(launch_packed_small_gen(a, static_cast<unsigned>(grid), st));
     return TKV_OK;
   }
   // Launch only as many workgroups as there are rows to give them (small batches).

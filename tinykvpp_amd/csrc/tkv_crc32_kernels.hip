@@ -157,6 +157,15 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small(RowsArgs a) {
   dev::crc_packed_small_body<G, EXACT, kPackedDepth, kPackedIlp, kPackedPrio>(a, lds);
 }
 
+// General small uniform blocks (64 < len <= 2 KiB, any stride, alignment, initial registers):
+// DESIGN.md §4.4. G-lane groups, the lanes kernel's load shape (DEPTH 4 / ILP 2 spills here: DEPTH 3 /
+// ILP 1).
+template <int G, bool INIT>
+__global__ __launch_bounds__(kThreads) void crc_packed_small_gen(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsWords];
+  dev::crc_packed_small_gen_body<G, INIT, 3, 1, kPackedPrio>(a, lds);
+}
+
 // Uniform batches of blocks of at most kLaneMax bytes (any stride, alignment, initial registers): one
 // lane per block. Only the slicing tables go to LDS (128 KiB).
 // Pipeline shapes (in-process A/B over 16-64 B blocks, profiles/r3/lanes/ab_shapes.jsonl): aligned
@@ -723,6 +732,33 @@ hipError_t launch_packed_small(const RowsArgs& a, unsigned grid, hipStream_t st)
     case 8: launch_small_g<8>(a, grid, st); break;
     case 16: launch_small_g<16>(a, grid, st); break;
     case 32: launch_small_g<32>(a, grid, st); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// Lanes per block of crc_packed_small_gen: the smallest power of two G >= 2 with 64 G >= len, for
+// 64 < len <= 2 KiB (0 otherwise).
+std::uint32_t packed_small_gen_group(std::uint32_t len) {
+  if (len <= kLaneMax || len > 2048u) return 0;
+  std::uint32_t g = 2;
+  while (64u * g < len) g <<= 1;
+  return g;
+}
+
+template <int G>
+void launch_small_gen_g(const RowsArgs& a, unsigned grid, hipStream_t st) {
+  if (a.init_raw) hipLaunchKernelGGL((crc_packed_small_gen<G, true>), dim3(grid), dim3(kThreads), 0, st, a);
+  else hipLaunchKernelGGL((crc_packed_small_gen<G, false>), dim3(grid), dim3(kThreads), 0, st, a);
+}
+
+hipError_t launch_packed_small_gen(const RowsArgs& a, unsigned grid, hipStream_t st) {
+  switch (packed_small_gen_group(a.len)) {
+    case 2: launch_small_gen_g<2>(a, grid, st); break;
+    case 4: launch_small_gen_g<4>(a, grid, st); break;
+    case 8: launch_small_gen_g<8>(a, grid, st); break;
+    case 16: launch_small_gen_g<16>(a, grid, st); break;
+    case 32: launch_small_gen_g<32>(a, grid, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

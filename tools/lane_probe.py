@@ -5,7 +5,7 @@ around K launches (median over rounds); every library's results are checked agai
 
     python tools/lane_probe.py lib1.so [lib2.so ...] [--rounds 5] [--reps 5] [--gib 1] [--only 36]
 
-Workloads: uniform batches of 26-64 B blocks (the reference's records are
+Workloads: uniform batches of 26-64 B blocks and of 65 B - 2 KiB blocks (the reference's records are
 26 + |k| + |v| bytes, wal.cpp:25), the same at the WAL payload pitch (8-byte header between payloads)
 and at an odd base, and irregular batches of WAL payloads (8-byte gaps), back-to-back small blocks
 and a mixed 0-4 KiB batch.
@@ -71,6 +71,10 @@ def main():
     work = []
     for L in (16, 26, 28, 32, 33, 36, 48, 59, 64):
         work.append(uniform(L))
+    for L in (100, 200, 300, 500, 1000, 1500, 2000):  # 65 B - 2 KiB, not multiples of 16 (crc_packed_small_gen)
+        work.append(uniform(L))
+    work.append(uniform(512, 512, 3))  # a multiple of 16 at an odd base
+    work.append(uniform(256, 264, 8))  # WAL payload pitch
     work.append(uniform(36, 44, 8))   # WAL payload pitch: 8-byte header in front of every 36-byte payload
     work.append(uniform(36, 36, 3))   # odd base
     work.append(uniform(59, 67, 8))
