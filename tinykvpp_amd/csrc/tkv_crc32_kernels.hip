@@ -158,12 +158,16 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small(RowsArgs a) {
 }
 
 // General small uniform blocks (64 < len <= 2 KiB, any stride, alignment, initial registers):
-// DESIGN.md §4.4. G-lane groups, the lanes kernel's load shape (DEPTH 4 / ILP 2 spills here: DEPTH 3 /
-// ILP 1).
+// DESIGN.md §4.4. G-lane groups, five granules per lane. DEPTH 4 spills here; DEPTH 2 / ILP 1 measured
+// 1-3 % faster than DEPTH 3 / ILP 1 in one process (profiles/r3/small_gen/ab_depth.jsonl).
+#ifndef TKV_GEN_DEPTH
+#define TKV_GEN_DEPTH 2
+#define TKV_GEN_ILP 1
+#endif
 template <int G, bool INIT>
 __global__ __launch_bounds__(kThreads) void crc_packed_small_gen(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_small_gen_body<G, INIT, 3, 1, kPackedPrio>(a, lds);
+  dev::crc_packed_small_gen_body<G, INIT, TKV_GEN_DEPTH, TKV_GEN_ILP, kPackedPrio>(a, lds);
 }
 
 // Uniform batches of blocks of at most kLaneMax bytes (any stride, alignment, initial registers): one
