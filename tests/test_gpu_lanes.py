@@ -212,3 +212,51 @@ def test_irregular_more_than_1024_tiles(gpu, oracle, shape):
         init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
         got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))
         assert np.array_equal(got, oracle.batch(host, offs, lens, init))
+
+
+@pytest.mark.parametrize("sizes", [(65,), (100, 128, 200), tuple(range(65, 257)), (256,)])
+@pytest.mark.parametrize("base", [0, 5, 8])
+def test_irregular_group_blocks(gpu, oracle, buf, sizes, base):
+    """Irregular blocks of 65-256 bytes in dense tiles (WAL records with short values: gapped payloads)
+    are folded by the group phase, a 4-lane group per block right-aligned in a 256-byte slot, at every
+    base alignment; per-block initial registers and CRC-32C on the same batch."""
+    host, d = buf
+    rng = np.random.default_rng(len(sizes) * 31 + base)
+    offs, lens = wal_payloads(rng, 100_000, sizes, base)
+    o, ln = torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu)
+    got = u32(tk.crc32_batch(d, o, ln))
+    assert mode() == 0
+    assert np.array_equal(got, oracle.batch(host, offs, lens))
+    init = rng.integers(0, 2**32, offs.size, dtype=np.uint64).astype(np.uint32)
+    got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))
+    assert np.array_equal(got, oracle.batch(host, offs, lens, init))
+    m = 2000
+    got = u32(tk.crc32_batch(d, o[:m].contiguous(), ln[:m].contiguous(), algo="crc32c"))
+    assert np.array_equal(got, oracle_c(oracle, host, offs[:m], lens[:m]))
+
+
+def test_irregular_lane_group_small_mix(gpu, oracle):
+    """Lane (<= 64 B), group (65-256 B), small (257 B - 1 KiB) and large blocks in one batch, dense and
+    sparse tiles (a sparse tile lists its group blocks as small blocks; a tile can be dense in lane
+    blocks and sparse in group blocks, or the reverse, or too large in bytes for the group phase),
+    random gaps and a batch that ends on the tensor's last byte."""
+    rng = np.random.default_rng(4242)
+    n = 4096 * 6 + 123
+    lens = rng.integers(0, 257, n)
+    lens[4096 * 2:4096 * 3] = rng.choice([300, 700, 1024, 5000, 100], 4096)  # a sparse tile
+    # dense lane blocks beside sparse group blocks, then the other way round
+    lens[4096 * 4:4096 * 5] = rng.choice([10, 100, 300, 700, 2000], 4096)
+    lens[4096 * 5:4096 * 6] = rng.choice([100, 150, 200, 300, 1500], 4096)
+    lens[4096 * 5 + rng.integers(0, 4096, 200)] = 5
+    lens[[4096 * 3 + 7, 4096 * 3 + 900]] = [3 << 20, 2 << 20]  # group-dense, but over kGroupTileBytes
+    lens[rng.integers(0, n, 40)] = rng.integers(1025, 20000, 40)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]) + rng.integers(0, 17, n).cumsum()
+    size = int((offs + lens).max())
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    d = torch.from_numpy(host).to(gpu)
+    o = torch.from_numpy(offs.astype(np.int64)).to(gpu)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), oracle.batch(host, offs, lens.astype(np.int32)))
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))
+    assert np.array_equal(got, oracle.batch(host, offs, lens.astype(np.int32), init))

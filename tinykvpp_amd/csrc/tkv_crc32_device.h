@@ -1654,6 +1654,112 @@ __device__ __forceinline__ void lane_phase(const RowsArgs& a, const std::uint32_
   }
 }
 
+// Group blocks of an irregular batch (kLaneMax < len <= kGroupMax, in a dense tile): a 4-lane group
+// folds one block right-aligned in a 256-byte slot (crc_packed_small_gen's layout at G = 4), 16 blocks
+// per wave step, walked straight from the caller's offsets and lengths over the same block range and
+// pipeline as lane_phase (other groups idle). Lane g loads the five granules covering its 64 bytes
+// and realigns them (lane_dwords); granules holding no byte of the block read the zero buffer and
+// the bytes in front of the block are masked. Lane shifts are column 60 + g of the LDS image
+// (Shift_{(3-g)*64}); the init term is Shift_len(init), from init_shift[len] for the default
+// register, or spread over the group (8 bits per lane, head_shift[len]) for per-block registers;
+// the group's sum comes from the first two DPP steps of the wave reduction.
+__device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32_t* lds) {
+  constexpr int RING = 4;
+  constexpr std::uint32_t G = 4, kSlot = 64u * G;
+  const std::uint32_t lane = threadIdx.x & 63u, gl = lane % G, grp = lane / G;
+  LaneConst kc = lane_const(lane);
+  kc.lsbase = kLdsLaneBase + (64u - G + gl) * 4u;
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves, n = a.nblocks;
+  const std::uint64_t b0 = wave * n / W, b1 = (wave + 1) * n / W;
+  if (b0 >= b1) return;
+  constexpr std::uint32_t kPer = 64u / G;  // blocks per step
+  const std::uint32_t ns = static_cast<std::uint32_t>((b1 - b0 + kPer - 1u) / kPer);
+  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
+  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
+
+  std::uint64_t d_off[RING];
+  std::uint32_t d_len[RING];
+  auto fetch = [&](std::uint32_t j, int slot) {
+    const std::uint64_t b = b0 + kPer * static_cast<std::uint64_t>(j) + grp;
+    const std::uint64_t bc = b < b1 ? b : b1 - 1u;  // clamped: every load stays inside the arrays
+    d_off[slot] = a.l_off[bc];
+    d_len[slot] = a.l_len[bc];
+  };
+  uint4 q[RING][kLaneGran];
+  std::uint32_t m_len[RING], m_o[RING], m_init[RING], m_ishift[RING];
+  std::int32_t m_lead[RING];
+  auto issue = [&](int slot, std::uint32_t j) {
+    const std::uint64_t b = b0 + kPer * static_cast<std::uint64_t>(j) + grp;
+    const std::uint32_t len0 = d_len[slot];
+    const bool live = j < ns && b < b1 && len0 > kLaneMax && len0 <= kGroupMax && (a.l_tile[b / 4096u] & kTileGroups);
+    const std::uint32_t len = live ? len0 : 0u;
+    const std::uintptr_t blo = base + d_off[slot], bhi = blo + len;
+    const std::int32_t c_lane = static_cast<std::int32_t>(len) - static_cast<std::int32_t>(kSlot) +
+                                64 * static_cast<std::int32_t>(gl);
+    const std::uintptr_t p = static_cast<std::uintptr_t>(static_cast<std::int64_t>(blo) + c_lane);
+    const std::uintptr_t al = p & ~static_cast<std::uintptr_t>(15);
+#pragma unroll
+    for (int i = 0; i < kLaneGran; ++i) {
+      const std::uintptr_t g = al + 16u * i;
+      q[slot][i] = gload16(live && g + 16u > blo && g < bhi ? g : dmy);
+    }
+    m_len[slot] = live ? len : 0xFFFFFFFFu;  // 0xFFFFFFFF: nothing to fold or store
+    m_o[slot] = static_cast<std::uint32_t>(p & 15u);
+    m_lead[slot] = -c_lane;  // bytes of the lane's window in front of the block
+    m_init[slot] = a.init_raw ? a.init_raw[live ? b : b0] : a.init_default;
+    m_ishift[slot] = a.tabs->init_shift[len];  // Shift_len(0xFFFFFFFF), the reference's init (crc32.hpp:39)
+  };
+  auto fold = [&](int slot, std::uint32_t j) {
+    const std::uint32_t len = m_len[slot];
+    const bool live = len != 0xFFFFFFFFu;
+    if (__ballot(live) == 0) return;  // no group block in this step
+    std::uint32_t d[16];
+    lane_dwords<1>(q[slot], m_o[slot], d);
+    const std::int32_t lead = m_lead[slot];
+    Reg p{0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const std::int32_t before = lead - 4 * k;
+      const std::uint32_t sh = static_cast<std::uint32_t>(before < 0 ? 0 : (before > 4 ? 4 : before)) * 8u;
+      slice4(lds, p, d[k] & static_cast<std::uint32_t>(0xFFFFFFFFull << sh), kc);
+    }
+    std::uint32_t v = lane_shift(lds, p.value(), kc);
+    const std::uint32_t L = live ? len : 0u;
+    if (a.init_raw) {
+      const std::uint32_t init = m_init[slot];
+#pragma unroll
+      for (std::uint32_t i = 0; i < 32u / G; ++i) {
+        const std::uint32_t bit = gl * (32u / G) + i;
+        v ^= static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), bit, 1)) &
+             a.tabs->head_shift[L][bit];
+      }
+    } else if (gl == 0u) {
+      v ^= m_ishift[slot];
+    }
+    v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    v ^= __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]: group sum
+    if (live && gl == G - 1u) a.out[b0 + kPer * static_cast<std::uint64_t>(j) + grp] = v ^ a.out_xor;
+  };
+
+#pragma unroll
+  for (int k = 0; k < RING; ++k) fetch(k, k);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    issue(k, k);
+    fetch(k + RING, k);
+  }
+  for (std::uint32_t t = 0; t < ns; t += RING) {
+#pragma unroll
+    for (int k = 0; k < RING; ++k) {
+      const int ahead = (k + 2) % RING;  // step t+k+2: its descriptor arrived RING steps ago
+      issue(ahead, t + k + 2);
+      fetch(t + k + 2 + RING, ahead);
+      if (t + k < ns) fold(k, t + k);
+    }
+  }
+}
+
 // Combine the partials of blocks that were split between waves: one thread per seam record (two
 // per wave) shifts its piece's partial past the rows that follow it in the block and XORs it into
 // the block's result, which the head piece seeded with xorout. All pieces of a block combine in

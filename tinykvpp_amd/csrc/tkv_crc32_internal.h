@@ -53,6 +53,7 @@ struct DeviceTables {
   std::uint32_t inv_shift[kRow + 1];    // [d] = x^(-8d) mod P: moves a register back by d bytes (stream)
   std::uint32_t poly;                   // reflected polynomial the tables were built for
   std::uint32_t pad_[2];
+  std::uint32_t init_shift[256 + 1];    // [h] = Shift_h(0xFFFFFFFF): the init term of a group-phase block
 };
 
 // One partial result of a block that was split between waves (irregular / huge-block path).
@@ -111,18 +112,42 @@ struct RowsArgs {
 };
 constexpr std::uint32_t kModeStream = 1;
 // counts[] of an irregular batch: [0] large blocks, [1] small blocks, [2] rows of the large blocks,
-// [3] mode, [4..7] stream-mode info (two u64), [8] lane blocks (len <= kLaneMax) of dense tiles
+// [3] mode, [4..7] stream-mode info (two u64), [8] lane and group blocks (len <= kGroupMax) of dense tiles
 constexpr int kCountLanes = 8;
+// counts[kCountPhases]: which of crc_stream's phases the general path needs (OR over the tiles'
+// kTileLanes / kTileGroups, shifted down by 1): 1 = lane blocks, 2 = group blocks
+constexpr int kCountPhases = 9;
 
 // Blocks of at most kLaneMax bytes are folded whole by one lane each, from their own initial register
 // (DESIGN.md §4.5): uniform batches by crc_lanes, irregular ones by the lane phase in crc_stream's
 // launch. The prepass lists them nowhere, and stream mode needs every block to be longer.
 constexpr std::uint32_t kLaneMax = 64;
-// The prepass leaves a scan tile's lane blocks to the lane phase only when the tile holds at least this
-// many (of its 4096); in a sparser tile they are listed as small blocks. Per-tile flags (tile_ok):
+// Irregular blocks of kLaneMax + 1 .. kGroupMax bytes in dense tiles are folded by 4-lane groups (one
+// block right-aligned in a 256-byte slot) in the group phase of crc_stream's launch, beside the lane
+// phase; the prepass lists them nowhere either.
+constexpr std::uint32_t kGroupMax = 256;
+// The prepass leaves a scan tile's lane blocks to the lane phase only when the tile holds at least
+// kLaneDenseTile of them (of its 4096), and its group blocks to the group phase only when it holds at
+// least kGroupDenseTile; in a sparser tile they are listed as small blocks. Either phase walks the
+// metadata of every block in its waves' ranges (64 blocks per lane-phase step, 16 per group-phase step)
+// where the small phase folds 4 listed blocks per step: the thresholds are those break-even points.
+// The group phase also needs a tile with at most kGroupTileRows rows of large blocks (4 MiB): where
+// large blocks carry the bytes, crc_rows folds the small blocks in the shadow of its row walk and the
+// group phase's own latency chain (descriptor, data, fold: ~10 us) would only add to the batch
+// (cfg4's general path: 1300 blocks of 255 bytes per tile, +1.2 % time with the group phase).
 constexpr std::uint32_t kLaneDenseTile = 256;
+constexpr std::uint32_t kGroupDenseTile = 1024;
+constexpr std::uint64_t kGroupTileRows = 1024;
+// Per-tile flags (tile_ok):
 constexpr std::uint32_t kTileStream = 1u;  // the tile's blocks qualify for stream mode
-constexpr std::uint32_t kTileLanes = 2u;   // the tile's lane blocks are the lane phase's
+constexpr std::uint32_t kTileLanes = 2u;   // the tile's lane blocks (len <= kLaneMax) are the lane phase's
+constexpr std::uint32_t kTileGroups = 4u;  // its group blocks (kLaneMax < len <= kGroupMax) the group phase's
+
+// Whether block of length len in a tile with flags tk is folded by the lane or group phase (and is
+// in no prepass list).
+__device__ __forceinline__ bool phase_block(std::uint32_t len, std::uint32_t tk) {
+  return len <= kLaneMax ? (tk & kTileLanes) != 0 : len <= kGroupMax && (tk & kTileGroups) != 0;
+}
 
 // One short host span for crc_span: `len` bytes at byte `pos` (16-byte aligned) of the mapped
 // staging buffer, folded on from raw register `init`.

@@ -102,18 +102,21 @@ constexpr unsigned kStreamThreads = kThreads;
 constexpr int kStreamSkew = 154;
 __global__ __launch_bounds__(kStreamThreads) void crc_stream(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  const bool stream = dev::sload32(a.counts, 3) == kModeStream;
-  // General path: this launch folds the batch's lane blocks (len <= kLaneMax), if the
-  // prepass counted any; crc_rows follows with the rest.
-  if (!stream && dev::sload32(a.counts, kCountLanes) == 0) return;
-  // The one barrier of the kernel, in front of every branch (the mode is the same for the whole grid).
-  if (stream) dev::fill_lds(a.tabs, lds);
-  else dev::fill_lds_slicing(a.tabs, lds);
-  __syncthreads();
-  if (!stream) {
-    dev::lane_phase(a, lds);
+  if (dev::sload32(a.counts, 3) != kModeStream) {
+    // General path: this launch folds the batch's lane and group blocks (len <= kGroupMax, DESIGN.md
+    // §4.5), each phase only if the prepass found its blocks; crc_rows follows with the rest. The
+    // group phase (column 60 + g) needs the lane-shift tables, the lane phase not.
+    const std::uint32_t ph = dev::sload32(a.counts, kCountPhases);
+    if (ph == 0) return;
+    if (ph & 2u) dev::fill_lds(a.tabs, lds);
+    else dev::fill_lds_slicing(a.tabs, lds);
+    __syncthreads();  // (the mode and ph are the same for the whole grid)
+    if (ph & 1u) dev::lane_phase(a, lds);
+    if (ph & 2u) dev::group_phase(a, lds);
     return;
   }
+  dev::fill_lds(a.tabs, lds);
+  __syncthreads();  // the one barrier of the stream walk
   // issue priority from the rows left: +0.8 % on cfg4 (in-process A/B). A wave whose rows hold more
   // than 8 block ends per row on average (blocks under ~500 bytes) takes them a row at a time
   // (MANY); the others keep the per-end loop, whose code the MANY path slows by up to 10 % when it
@@ -236,7 +239,7 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   static_assert(kScanTile % kTileThreads == 0 && kTileWaves >= 1 && kTileBpt >= 4 && kTileBpt % 4 == 0,
                 "tile shape");
   __shared__ std::uint64_t wsum[kTileWaves];
-  __shared__ std::uint32_t lsum[kTileWaves], lcnt[kTileWaves];
+  __shared__ std::uint32_t lsum[kTileWaves], wok[kTileWaves];
   // stream mode's wave partition (used only if the prepass picks stream mode): row0[0..Ws], grid-stride
   for (std::uint32_t w = blockIdx.x * kTileThreads + threadIdx.x; w <= Ws; w += gridDim.x * kTileThreads) {
     const std::uint64_t TR = stream_geometry(sbase, offsets, lengths, n).rows;
@@ -244,36 +247,23 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   }
   const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * kTileBpt;
   const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  std::uint32_t len[kTileBpt], lv[kTileBpt];
+  // Every block first counts as a small or large one (v); lane and group blocks are also counted in
+  // one packed u32 (lane blocks in the low 16 bits, group blocks in the high 16: a tile has at most
+  // 4096), so the one scan below yields both, and the tile's verdict on them (below) only subtracts.
+  std::uint32_t pk[kTileBpt];
+  std::uint64_t v[kTileBpt], s = 0;
+  std::uint32_t ls = 0;
   bool ok = true;
-  unsigned nlw = 0;  // lane blocks (len <= kLaneMax) of this wave
 #pragma unroll
   for (unsigned i = 0; i < kTileBpt; ++i) {
     const std::uint64_t b = base + i;
-    len[i] = b < n ? lengths[b] : 0u;
-    lv[i] = b < n && len[i] <= kLaneMax ? 1u : 0u;
-    nlw += static_cast<unsigned>(__popcll(__ballot(lv[i] != 0u)));
-    // (a lane block is shorter than kStreamMinLen: its offsets are never read here)
-    if (b < n) ok = ok && len[i] >= kStreamMinLen && (b + 1 >= n || offsets[b] + len[i] == offsets[b + 1]);
-  }
-  if (lane == 0) lcnt[wid] = nlw;
-  const bool tile_all_ok = __syncthreads_and(ok ? 1 : 0) != 0;
-  // A tile with at least kLaneDenseTile lane blocks leaves them to the lane phase (in no list); in a
-  // sparser tile they are listed as small blocks, so a batch with a few of them scattered about pays no
-  // lane-phase walk over its metadata.
-  std::uint32_t nlt = 0;
-#pragma unroll
-  for (unsigned w = 0; w < kTileWaves; ++w) nlt += lcnt[w];
-  const bool dense = nlt >= kLaneDenseTile;
-  if (threadIdx.x == 0) tile_ok[blockIdx.x] = (tile_all_ok ? kTileStream : 0u) | (dense ? kTileLanes : 0u);
-  std::uint64_t v[kTileBpt], s = 0;
-  std::uint32_t ls = 0;
-#pragma unroll
-  for (unsigned i = 0; i < kTileBpt; ++i) {
-    lv[i] = dense ? lv[i] : 0u;
-    v[i] = base + i < n && !lv[i] ? scan_item(len[i]) : 0ull;
+    const std::uint32_t len = b < n ? lengths[b] : 0u;
+    pk[i] = b >= n ? 0u : len <= kLaneMax ? 1u : len <= kGroupMax ? 0x10000u : 0u;
+    v[i] = b < n ? scan_item(len) : 0ull;
     s += v[i];
-    ls += lv[i];
+    ls += pk[i];
+    // (a lane block is shorter than kStreamMinLen: its offsets are never read here)
+    if (b < n) ok = ok && len >= kStreamMinLen && (b + 1 >= n || offsets[b] + len == offsets[b + 1]);
   }
   // Inclusive scans of the thread sums inside the wave (cross-lane shifts, no barriers), then the
   // wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
@@ -286,13 +276,15 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     inc += lane >= off ? y : 0ull;
     linc += lane >= off ? ly : 0u;
   }
+  const bool wave_ok = __ballot(!ok) == 0;
   if (lane == 63u) {
     wsum[wid] = inc;
     lsum[wid] = linc;
+    wok[wid] = wave_ok ? 1u : 0u;
   }
   __syncthreads();
   std::uint64_t wpre = 0, tot = 0;
-  std::uint32_t lpre = 0, ltot = 0;
+  std::uint32_t lpre = 0, ltot = 0, all_ok = 1;
 #pragma unroll
   for (unsigned w = 0; w < kTileWaves; ++w) {
     const std::uint64_t t = wsum[w];
@@ -301,11 +293,24 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     tot += t;
     lpre += w < wid ? lt : 0u;
     ltot += lt;
+    all_ok &= wok[w];
   }
-  std::uint64_t run = wpre + inc - s;  // exclusive
+  // A tile with at least kLaneDenseTile lane blocks leaves them to the lane phase (in no list), one
+  // with at least kGroupDenseTile group blocks and at most kGroupTileRows rows of large blocks those
+  // to the group phase; in other tiles they are listed as small blocks, so a batch with a few of them
+  // scattered about pays no phase walk over its metadata.
+  const std::uint32_t tph = ((ltot & 0xFFFFu) >= kLaneDenseTile ? kTileLanes : 0u) |
+                            ((ltot >> 16) >= kGroupDenseTile && (tot >> 32) <= kGroupTileRows ? kTileGroups : 0u);
+  const std::uint32_t tmask = ((tph & kTileLanes) ? 0xFFFFu : 0u) | ((tph & kTileGroups) ? 0xFFFF0000u : 0u);
+  auto taken = [&](std::uint32_t x) {  // the phase blocks among packed counts x
+    x &= tmask;
+    return (x & 0xFFFFu) + (x >> 16);
+  };
+  if (threadIdx.x == 0) tile_ok[blockIdx.x] = (all_ok ? kTileStream : 0u) | tph;
+  std::uint64_t run = wpre + inc - s;  // exclusive, lane and group blocks counted as small
   std::uint32_t lrun = lpre + linc - ls;
-  if (!dense && base + kTileBpt <= n) {
-    // every block of a sparse tile is listed: this thread's entries as whole 16-byte stores
+  if (tph == 0 && base + kTileBpt <= n) {
+    // every block of such a tile is listed: this thread's entries as whole 16-byte stores
     // (scan and lscan are 256-byte aligned scratch, base a multiple of kTileBpt >= 4)
     std::uint64_t sc[kTileBpt];
 #pragma unroll
@@ -317,22 +322,23 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     for (unsigned i = 0; i < kTileBpt; i += 2)
       *reinterpret_cast<ulonglong2*>(scan + base + i) = make_ulonglong2(sc[i], sc[i + 1]);
 #pragma unroll
-    for (unsigned i = 0; i < kTileBpt; i += 4)
-      *reinterpret_cast<uint4*>(lscan + base + i) = make_uint4(lrun, lrun, lrun, lrun);
+    for (unsigned i = 0; i < kTileBpt; i += 4) *reinterpret_cast<uint4*>(lscan + base + i) = make_uint4(0, 0, 0, 0);
   } else {
 #pragma unroll
     for (unsigned i = 0; i < kTileBpt; ++i) {
-      if (base + i < n && !lv[i]) {  // the scatter reads these for listed blocks only
-        scan[base + i] = run;
-        lscan[base + i] = lrun;
+      if (base + i < n && !taken(pk[i])) {  // the scatter reads these for listed blocks only
+        const std::uint32_t t = taken(lrun);
+        scan[base + i] = run - t;  // (t <= the small count in run's low half: no borrow)
+        lscan[base + i] = t;
       }
       run += v[i];
-      lrun += lv[i];
+      lrun += pk[i];
     }
   }
   if (threadIdx.x == kTileThreads - 1) {
-    tile_sums[blockIdx.x] = tot;
-    tile_lanes[blockIdx.x] = ltot;
+    const std::uint32_t tl = taken(ltot);
+    tile_sums[blockIdx.x] = tot - tl;
+    tile_lanes[blockIdx.x] = tl;
   }
 }
 
@@ -348,11 +354,15 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
                                                        std::uint64_t* sinfo) {
   __shared__ std::uint64_t part[1024];
   __shared__ std::uint32_t lpart[1024];
+  __shared__ std::uint32_t sph;
+  if (threadIdx.x == 0) sph = 0;  // (the loop's first barrier orders this before the ORs below)
   std::uint64_t carry = 0, lcarry = 0;
   bool all_stream = true;
+  std::uint32_t ph = 0;  // kTileLanes | kTileGroups over the tiles
   for (std::uint32_t t0 = 0; t0 < ntiles; t0 += 1024) {
     const std::uint32_t i = t0 + threadIdx.x;
     all_stream = all_stream && (i >= ntiles || (tile_ok[i] & kTileStream) != 0);
+    ph |= i < ntiles ? tile_ok[i] & (kTileLanes | kTileGroups) : 0u;
     const std::uint64_t x = i < ntiles ? tile_sums[i] : 0ull;
     const std::uint32_t lx = i < ntiles ? tile_lanes[i] : 0u;
     part[threadIdx.x] = x;
@@ -376,8 +386,12 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
     carry += tot;
     lcarry += ltot;
   }
+#pragma unroll
+  for (unsigned m = 32; m > 0; m >>= 1) ph |= __shfl_xor(ph, m, 64);
+  if ((threadIdx.x & 63u) == 0 && ph != 0) atomicOr(&sph, ph);
   const bool stream = __syncthreads_and(all_stream ? 1 : 0) != 0;
   if (threadIdx.x == 0) {
+    counts[kCountPhases] = stream ? 0u : sph >> 1;
     if (stream) {
       const StreamGeom g = stream_geometry(base, offsets, lengths, n);
       counts[0] = 0;
@@ -399,14 +413,14 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
 }
 
 // Scatter of one block (rows_finish): e = its exclusive (small count, rows) pair, nlane = lane blocks
-// in front of it that the lane phase folds, dense = its tile's lane blocks are the lane phase's,
+// and group blocks in front of it that those phases fold, tk = its tile's flags,
 // TR = rows of all large blocks. A large block cut between row-kernel waves gets its
 // result zeroed here, since the row kernel XORs every piece of it into the result (crc_rows_body,
 // irregular batches). len and off are the block's length and offset (loaded by the caller).
 __device__ __forceinline__ void finish_block(std::uint64_t off, std::uint32_t len, std::uint64_t b, std::uint64_t e,
                                              std::uint64_t nlane, std::uint64_t TR, const PrepassOut& o,
-                                             std::uint32_t W, std::uint32_t* out, bool dense) {
-  if (len <= kLaneMax && dense) return;  // the lane phase's (a lane block of a sparse tile is small)
+                                             std::uint32_t W, std::uint32_t* out, std::uint32_t tk) {
+  if (phase_block(len, tk)) return;  // the lane or group phase's (in a sparse tile it is small)
   const std::uint32_t nsmall = static_cast<std::uint32_t>(e);
   if (len <= kSmallMax) {
     o.s_off[nsmall] = off;
@@ -447,10 +461,9 @@ __global__ void rows_finish(const std::uint8_t* base, const std::uint64_t* offse
     return;
   }
   const std::uint64_t t = b / kScanTile;
-  const bool dense = (tile_ok[t] & kTileLanes) != 0;
-  if (len <= kLaneMax && dense) return;  // the lane phase's
-  finish_block(offsets[b], len, b, scan[b] + tile_offs[t], o.lscan[b] + o.tile_lanes[t], counts[2], o, W, out,
-               dense);
+  const std::uint32_t tk = tile_ok[t];
+  if (phase_block(len, tk)) return;  // the lane or group phase's
+  finish_block(offsets[b], len, b, scan[b] + tile_offs[t], o.lscan[b] + o.tile_lanes[t], counts[2], o, W, out, tk);
 }
 
 // rows_finish with the scan of the tile sums folded in (ntiles <= kFusedTiles): every workgroup sums
@@ -493,7 +506,7 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     std::uint32_t* counts, PrepassOut o, std::uint32_t W, std::uint32_t* out, std::uint64_t* ends,
     std::uint64_t* sinfo, std::uint32_t Ws, const std::uint32_t* row0) {
   constexpr std::uint32_t kWaves = kFinishThreads / 64;
-  __shared__ std::uint64_t red[5][kWaves];
+  __shared__ std::uint64_t red[6][kWaves];
   const std::uint32_t my_tile = blockIdx.x * kFinishThreads / kScanTile;  // kScanTile % 256 == 0
   // The block's own operands are loaded first, so their latency overlaps the tile-sum reduction (the
   // scan values of a lane block were never written and are not used).
@@ -503,16 +516,19 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
   const std::uint64_t off = live ? offsets[b] : 0ull;
   const std::uint64_t sc = live ? scan[b] : 0ull;
   const std::uint32_t lsc = live ? o.lscan[b] : 0u;
-  const bool dense = (tile_ok[my_tile] & kTileLanes) != 0;
+  const std::uint32_t mtk = tile_ok[my_tile];
   std::uint64_t before = 0, all = 0, bad = 0, lbefore = 0, lall = 0;
+  std::uint32_t ph = 0;  // kTileLanes | kTileGroups over the tiles
   for (std::uint32_t i = threadIdx.x; i < ntiles; i += kFinishThreads) {
     const std::uint64_t v = tile_sums[i];
     const std::uint64_t lv = o.tile_lanes[i];
+    const std::uint32_t tk = tile_ok[i];
     all += v;
     before += i < my_tile ? v : 0ull;
     lall += lv;
     lbefore += i < my_tile ? lv : 0ull;
-    bad += (tile_ok[i] & kTileStream) ? 0u : 1u;
+    bad += (tk & kTileStream) ? 0u : 1u;
+    ph |= tk & (kTileLanes | kTileGroups);
   }
   // Wave sums by cross-lane exchange, then the kWaves partial sums through LDS (one barrier).
 #pragma unroll
@@ -522,6 +538,7 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     bad += __shfl_xor(bad, m, 64);
     lbefore += __shfl_xor(lbefore, m, 64);
     lall += __shfl_xor(lall, m, 64);
+    ph |= __shfl_xor(ph, m, 64);
   }
   const unsigned wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63u) == 0) {
@@ -530,9 +547,10 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     red[2][wid] = bad;
     red[3][wid] = lbefore;
     red[4][wid] = lall;
+    red[5][wid] = ph;
   }
   __syncthreads();
-  std::uint64_t tile_off = 0, total = 0, nbad = 0, tile_loff = 0, ltotal = 0;
+  std::uint64_t tile_off = 0, total = 0, nbad = 0, tile_loff = 0, ltotal = 0, aph = 0;
 #pragma unroll
   for (unsigned w = 0; w < kWaves; ++w) {
     tile_off += red[0][w];
@@ -540,7 +558,9 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     nbad += red[2][w];
     tile_loff += red[3][w];
     ltotal += red[4][w];
+    aph |= red[5][w];
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) counts[kCountPhases] = nbad == 0 ? 0u : static_cast<std::uint32_t>(aph) >> 1;
   if (nbad == 0) {  // every block qualifies: stream mode
     if (live) stream_block(base, offsets, lengths, n, b, off, len, Ws, row0, counts, ends, sinfo, o.wave_start);
     return;
@@ -554,7 +574,7 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     counts[kCountLanes] = nl;                              // lane blocks (crc_stream's lane phase)
   }
   if (!live) return;
-  finish_block(off, len, b, sc + tile_off, lsc + tile_loff, total >> 32, o, W, out, dense);
+  finish_block(off, len, b, sc + tile_off, lsc + tile_loff, total >> 32, o, W, out, mtk);
 }
 
 

@@ -83,6 +83,12 @@ def main():
     nm = count(42, 50)
     lm = rng.choice([26, 28, 33, 36, 59], nm)
     work.append(irregular("irregular WAL payloads 26-59 B, 8 B gaps", lm, np.full(nm, 8), 8))
+    ng = count(150, 158)
+    work.append(irregular("irregular WAL payloads 100-200 B, 8 B gaps", rng.integers(100, 201, ng), np.full(ng, 8), 8))
+    ng = count(160, 168)
+    work.append(irregular("irregular WAL payloads 65-256 B, 8 B gaps", rng.integers(65, 257, ng), np.full(ng, 8), 8))
+    ng = count(128, 136)
+    work.append(irregular("irregular 128 B, 8 B gaps", np.full(ng, 128), np.full(ng, 8), 8))
     n = count(36, 36)
     work.append(irregular("irregular back to back 36 B", np.full(n, 36), np.zeros(n, np.int64), 0))
     n = count(64, 64)
