@@ -97,6 +97,43 @@ def test_irregular_random(gpu, oracle, seed):
         assert irregular_mode() == 1, "a back-to-back batch of blocks > 64 B (kLaneMax) takes stream mode"
 
 
+@pytest.mark.parametrize("seed", range(48))
+def test_irregular_dense_small_random(gpu, oracle, seed):
+    """Batches dense in blocks of at most 256 bytes (the lane and group phases): lane
+    and group shares around the prepass's per-tile thresholds (256 and 1024 of 4096 blocks), a few
+    large blocks that may push a tile over the group phase's row bound, gapped, back-to-back and
+    overlapping layouts, random base shifts, initial registers and algorithms."""
+    rng = np.random.default_rng(5000 + seed + OFFSET)
+    algo = ALGOS[seed % 2]
+    n = int(rng.choice([4096, 5000, 9000, 20000, 4096 * 3 + 17]))
+    p_lane = float(rng.choice([0.0, 0.05, 0.0625, 0.3, 0.9]))
+    p_group = float(rng.choice([0.0, 0.2, 0.25, 0.3, 0.9]))
+    u = rng.random(n)
+    lens = np.where(u < p_lane, rng.integers(0, 65, n),
+           np.where(u < p_lane + p_group, rng.integers(65, 257, n), rng.integers(257, 3000, n)))
+    nbig = int(rng.choice([0, 1, 3]))
+    lens[rng.integers(0, n, nbig)] = rng.integers(1 << 20, 6 << 20, nbig)
+    layout = ("gapped", "back_to_back", "overlapping")[seed % 3]
+    start = int(rng.integers(0, 300))
+    if layout == "back_to_back":
+        offs = start + np.concatenate([[0], np.cumsum(lens)[:-1]])
+    elif layout == "gapped":
+        offs = start + np.concatenate([[0], np.cumsum(lens + rng.integers(0, 20, n))[:-1]])
+    else:
+        offs = rng.integers(0, max(1, int(lens.sum()) // 2 + 1), n) + start
+    host = rng.integers(0, 256, int((offs + lens).max()) + 64, dtype=np.uint8)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if seed % 4 < 2 else None
+    shift = int(rng.integers(0, 16))
+    d = on_device(host, gpu, shift)
+    ini = None if init is None else torch.from_numpy(init.view(np.int32)).to(gpu)
+    got = u32(tk.crc32_batch(d, torch.from_numpy(offs.astype(np.int64)).to(gpu),
+                             torch.from_numpy(lens.astype(np.int32)).to(gpu), init_raw=ini, algo=algo))
+    want = oracle_batch(oracle, algo, host, offs, lens, init)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, (f"{layout} n={n} lane={p_lane} group={p_group} big={nbig} shift={shift} algo={algo} "
+                           f"mode={irregular_mode()}: {bad.size} blocks differ, first {bad[:5]} (lens {lens[bad[:5]]})")
+
+
 @pytest.mark.parametrize("seed", range(64))
 def test_uniform_random(gpu, oracle, seed):
     rng = np.random.default_rng(2000 + seed + OFFSET)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# The seeded random sweep (tests/test_gpu_fuzz.py, 372 cases) re-seeded with each TKV_FUZZ_OFFSET given;
+# The seeded random sweep (tests/test_gpu_fuzz.py) re-seeded with each TKV_FUZZ_OFFSET given;
 # one pytest process per offset, each under its own time limit; stops at the first failure.
 # Usage: tools/gpu_fuzz_offsets.sh <name> <offset> ...; logs in gpurun_out/<name>/.
 set -u
