@@ -253,17 +253,32 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   std::uint32_t pk[kTileBpt];
   std::uint64_t v[kTileBpt], s = 0;
   std::uint32_t ls = 0;
+  // Loads at clamped indices, all issued before any is used (n >= 1 here): one round trip for the
+  // lengths, one more for the offsets, which only a thread whose blocks are all long enough for stream
+  // mode reads (a lane-block batch never touches them).
+  std::uint32_t len[kTileBpt];
   bool ok = true;
 #pragma unroll
   for (unsigned i = 0; i < kTileBpt; ++i) {
     const std::uint64_t b = base + i;
-    const std::uint32_t len = b < n ? lengths[b] : 0u;
-    pk[i] = b >= n ? 0u : len <= kLaneMax ? 1u : len <= kGroupMax ? 0x10000u : 0u;
-    v[i] = b < n ? scan_item(len) : 0ull;
+    len[i] = lengths[b < n ? b : n - 1];
+  }
+#pragma unroll
+  for (unsigned i = 0; i < kTileBpt; ++i) {
+    const bool in = base + i < n;
+    len[i] = in ? len[i] : 0u;
+    pk[i] = !in ? 0u : len[i] <= kLaneMax ? 1u : len[i] <= kGroupMax ? 0x10000u : 0u;
+    v[i] = in ? scan_item(len[i]) : 0ull;
     s += v[i];
     ls += pk[i];
-    // (a lane block is shorter than kStreamMinLen: its offsets are never read here)
-    if (b < n) ok = ok && len >= kStreamMinLen && (b + 1 >= n || offsets[b] + len == offsets[b + 1]);
+    ok = ok && (!in || len[i] >= kStreamMinLen);
+  }
+  if (ok && base < n) {
+    std::uint64_t o[kTileBpt + 1];
+#pragma unroll
+    for (unsigned i = 0; i <= kTileBpt; ++i) o[i] = offsets[base + i < n ? base + i : n - 1];
+#pragma unroll
+    for (unsigned i = 0; i < kTileBpt; ++i) ok = ok && (base + i + 1 >= n || o[i] + len[i] == o[i + 1]);
   }
   // Inclusive scans of the thread sums inside the wave (cross-lane shifts, no barriers), then the
   // wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
