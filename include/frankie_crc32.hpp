@@ -14,11 +14,13 @@
 // (profiles/r3/put_latency.jsonl): up to 64 KiB the host path is faster (36 B: 0.011 us against the
 // reference's 0.040 us and 11 us for a GPU round trip; 64 KiB: 23 us against 31 us), from 128 KiB the
 // GPU is (35 us against 46 us). So the reference's per-put record stamp (wal.cpp:54-57) costs less
-// than in the reference, and its contract holds: update is noexcept and cannot fail, with or without
-// a device. Longer spans go to the GPU; the reference's update has no error path, so a device failure
-// there is reported on stderr and aborts (a wrong checksum would be worse than a crash for an
-// integrity routine). -DTKV_DROPIN_HOST_MAX=0 sends every span to the GPU. tkv_debug_update_counts
-// says which path the calling thread's calls took.
+// than in the reference. Longer spans go to the GPU (tkv_crc32_update). The reference's update is
+// noexcept and has no failure mode (crc32.cpp:9-16), so when the GPU call returns an error (no device
+// on this node, a HIP failure) the same span is recomputed on the host by tkv_crc32_update_fallback,
+// which warns once per process on stderr and counts the call. update therefore never fails, at any
+// span size, with or without a device. -DTKV_DROPIN_HOST_MAX=0 sends every span to the GPU first.
+// tkv_debug_update_counts says which path the calling thread's calls took: [0] host span, [1] GPU,
+// [2] host recompute after a GPU error.
 //
 // Build: add include/ to the include path and link libtkv_crc32.so.
 #pragma once
@@ -65,10 +67,11 @@ class crc32 final {
   [[nodiscard]] crc32 &update(std::span<const std::byte> data) noexcept {
     std::uint32_t next = crc_;
     const bool host = kHostSpanMax > 0 && data.size() <= kHostSpanMax;
-    const int rc = host ? tkv_crc32_update_host(crc_, data.data(), data.size(), &next)
-                        : tkv_crc32_update(crc_, data.data(), data.size(), &next);
-    if (rc != TKV_OK) {
-      std::fprintf(stderr, "frankie::core::crc32::update: GPU CRC failed (status %d): %s\n", rc, tkv_last_error());
+    int rc = host ? tkv_crc32_update_host(crc_, data.data(), data.size(), &next)
+                  : tkv_crc32_update(crc_, data.data(), data.size(), &next);
+    if (rc != TKV_OK && !host) rc = tkv_crc32_update_fallback(rc, crc_, data.data(), data.size(), &next);
+    if (rc != TKV_OK) {  // unreachable: the host path fails only on a null pointer, which a span cannot pass
+      std::fprintf(stderr, "frankie::core::crc32::update: host CRC failed (status %d)\n", rc);
       std::abort();
     }
     crc_ = next;

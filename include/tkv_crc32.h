@@ -4,9 +4,11 @@
  * Drop-in boundary for tinykvpp's integrity hot path: the CRC-32/ISO-HDLC routine
  * frankie::core::crc32 (/root/reference/src/core/crc32.hpp:32-49, crc32.cpp:9-22) and the call
  * sites that stamp/verify WAL records (/root/reference/src/engine/wal.cpp:54-58, 89-96).
- * Plain C: pointers, sizes and integer status codes only. Every checksum is computed by the HIP
- * kernels for gfx950; the library has no CPU implementation of the CRC and reports an error when
- * no GPU is usable.
+ * Plain C: pointers, sizes and integer status codes only. Every batch, device and host-pipeline
+ * entry point computes on the HIP kernels for gfx950 and reports TKV_IO_ERROR when no GPU is usable;
+ * none of them falls back to the CPU. The CPU computes only in the separately named single-span
+ * entry points tkv_crc32[c]_update_host and tkv_crc32[c]_update_fallback, which the drop-in header
+ * include/frankie_crc32.hpp uses to keep crc32::update's never-fail contract (crc32.cpp:9-16).
  *
  * State conventions (match crc32.hpp:37-46):
  *   "raw" register  = the value crc32::crc_ holds (init 0xFFFFFFFF, no xorout applied);
@@ -68,13 +70,22 @@ int tkv_crc32_update_device(uint32_t raw_state, const void *d_data, size_t len, 
                             void *stream);
 
 /* Host-CPU latency path for ONE short span (slicing-by-8; no device, never fails on valid
- * arguments): the same register semantics as tkv_crc32_update. No other entry point calls it: it is
- * not a fallback. The drop-in header include/frankie_crc32.hpp routes spans of at most
- * TKV_DROPIN_HOST_MAX bytes here when the integrator defines that macro (default 0: off), for the
- * reference's per-put record stamp (wal.cpp:54-57), where a GPU round trip costs ~20 us against
- * ~0.03 us on the host. */
+ * arguments): the same register semantics as tkv_crc32_update. No other entry point calls it. The
+ * drop-in header include/frankie_crc32.hpp routes spans of at most TKV_DROPIN_HOST_MAX bytes here
+ * (default 65536, the measured host/GPU crossover of one call), which covers the reference's per-put
+ * record stamp (wal.cpp:54-57): 0.011 us for 36 bytes against ~11 us for a GPU round trip
+ * (INTEGRATION.md §1). */
 int tkv_crc32_update_host(uint32_t raw_state, const void *data, size_t len, uint32_t *out_raw);
 int tkv_crc32c_update_host(uint32_t raw_state, const void *data, size_t len, uint32_t *out_raw);
+
+/* The drop-in header's recovery after tkv_crc32[c]_update returned `gpu_status` != TKV_OK: the same
+ * span recomputed on the host (the slicing-by-8 code of tkv_crc32_update_host), so crc32::update
+ * keeps the reference's never-fail contract (crc32.cpp:9-16) for spans of any size on a node without
+ * a usable GPU. Prints one warning per process on stderr (with gpu_status and tkv_last_error()) and
+ * counts the call in tkv_debug_update_counts slot 2. Fails only on null pointers. */
+int tkv_crc32_update_fallback(int gpu_status, uint32_t raw_state, const void *data, size_t len, uint32_t *out_raw);
+int tkv_crc32c_update_fallback(int gpu_status, uint32_t raw_state, const void *data, size_t len,
+                               uint32_t *out_raw);
 
 /* CRC of the concatenation A || B from crc1 = CRC(A), crc2 = CRC(B) (finalized values) and
  * len2 = |B| (zlib's crc32_combine): Shift_len2(crc1) ^ crc2, GF(2) arithmetic on the 4-byte
@@ -236,12 +247,14 @@ int tkv_debug_multi_combine(uint32_t poly, int ndev, const uint64_t *h_offsets, 
                             const uint32_t *h_init_raw, uint64_t n, const uint32_t *piece_final,
                             uint32_t *h_out_final);
 /* Update calls of the calling thread so far: out[0] through tkv_crc32[c]_update_host (the drop-in's
- * short-span host path), out[1] through tkv_crc32[c]_update (the GPU). */
-void tkv_debug_update_counts(uint64_t out[2]);
+ * short-span host path), out[1] through tkv_crc32[c]_update (the GPU), out[2] through
+ * tkv_crc32[c]_update_fallback (host recomputes after a failed GPU update). */
+void tkv_debug_update_counts(uint64_t out[3]);
 /* What the calling thread's last tkv_wal_verify / tkv_wal_verify_device did: out[0] = device walk
  * passes, out[1] = 1 when it handed the image to the exact host-thread walk, out[2] = 1 when a
- * host image was copied to the device, out[3] = 1 when every pass stitched its pieces by the fast
- * path (no pointer jumping). */
+ * host image was copied to the device, out[3] = 1 when at least one device pass ran and every pass
+ * stitched its pieces by the fast path (no pointer jumping); 0 when no device pass ran. (Before
+ * round 3, out[3] counted pieces; it is a flag since.) */
 void tkv_debug_wal_last(uint64_t out[4]);
 /* Which path the last irregular batch on `stream` took: 1 = byte-stream row walk (blocks back to
  * back, each at least 64 bytes), 0 = general row walk; -1 on error. Synchronizes

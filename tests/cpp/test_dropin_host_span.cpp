@@ -6,6 +6,13 @@
 // counters of tkv_debug_update_counts show every call on the host path). It also times a 36-byte put
 // (wal_entry::encode's {put, 42, "hello", "world"}) against the reference's byte loop
 // (crc32.cpp:9-16, restated inline) on the same core.
+//
+// Spans above the threshold go to the GPU. The reference's update cannot fail, so on a node without
+// a usable GPU (this container) the header recomputes them on the host after the GPU call's error
+// (tkv_crc32_update_fallback): a 1 MiB span and a 128 KiB WAL record (a put with a 128 KiB value,
+// wal.cpp:25) must return the byte loop's value without aborting, and the counters must show the GPU
+// attempt and the host recompute (slot 2). With a GPU (tests/test_gpu_parity.py runs this binary
+// too) the same spans take the GPU and slot 2 stays 0.
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -112,10 +119,47 @@ void all_lengths() {
     CHECK_EQ(crc32{}.update({d.data(), n}).finalize(), r ^ 0xFFFFFFFFu);
   }
 }
+std::uint32_t byte_loop(const std::byte* p, std::size_t n) {
+  constexpr auto T = generate_crc32_table();
+  std::uint32_t r = 0xFFFFFFFFu;  // crc32.cpp:9-16
+  for (std::size_t i = 0; i < n; ++i) r = (r >> 8) ^ T[(r ^ static_cast<std::uint32_t>(p[i])) & 0xFFu];
+  return r ^ 0xFFFFFFFFu;
+}
+
+// Spans longer than the threshold: the GPU, or the host recompute after its error.
+void long_spans() {
+  std::uint64_t c0[3], c1[3];
+  tkv_debug_update_counts(c0);
+  std::vector<std::byte> big(1u << 20);
+  for (std::size_t i = 0; i < big.size(); ++i) big[i] = static_cast<std::byte>((i * 2246822519u) >> 13);
+  CHECK_EQ(crc32{}.update({big.data(), big.size()}).finalize(), byte_loop(big.data(), big.size()));
+  // wal_entry::encode (wal.cpp:19-61) of {put, seq 7, 16-byte key, 128 KiB value}; CRC over [8, size).
+  const std::uint32_t klen = 16, vlen = 128u << 10, size = 26 + klen + vlen, record_len = size - 8;
+  const std::uint64_t seq = 7;
+  std::vector<std::byte> rec(size, std::byte{0});
+  std::memcpy(rec.data(), &record_len, 4);
+  std::memcpy(rec.data() + 9, &seq, 8);
+  std::memcpy(rec.data() + 18, &klen, 4);
+  std::memcpy(rec.data() + 22, &vlen, 4);
+  for (std::uint32_t i = 0; i < klen + vlen; ++i) rec[26 + i] = static_cast<std::byte>((i * 40503u) >> 5);
+  const std::uint32_t crc = crc32{}.update({rec.data() + 8, size - 8u}).finalize();
+  CHECK_EQ(crc, byte_loop(rec.data() + 8, size - 8u));
+  // chained: a short host span, then a long one, then a short one
+  crc32 chained;
+  (void)chained.update({rec.data() + 8, 100}).update({rec.data() + 108, 100000}).update({rec.data() + 100108, 7});
+  CHECK_EQ(chained.finalize(), byte_loop(rec.data() + 8, 100107));
+  tkv_debug_update_counts(c1);
+  const bool gpu = tkv_device_count() > 0;
+  std::printf("long_spans: %s; GPU calls %llu, host recomputes %llu\n", gpu ? "GPU present" : "no GPU",
+              (unsigned long long)(c1[1] - c0[1]), (unsigned long long)(c1[2] - c0[2]));
+  CHECK_EQ(c1[1] - c0[1], 3u);  // every long span went to the GPU first
+  CHECK_EQ(c1[2] - c0[2], gpu ? 0u : 3u);
+  CHECK_EQ(c1[0] - c0[0], 2u);  // the two short spans of the chain
+}
 }  // namespace
 
 int main() {
-  std::uint64_t c0[2], c1[2];
+  std::uint64_t c0[3], c1[3];
   tkv_debug_update_counts(c0);
   known_values();
   incremental_equals_single();
@@ -131,6 +175,7 @@ int main() {
     std::fprintf(stderr, "only %llu host span calls counted\n", (unsigned long long)(c1[0] - c0[0]));
     ++g_fail;
   }
+  long_spans();
   put_cost();
   std::printf("%s\n", g_fail ? "FAILED" : "ALL PASSED");
   return g_fail ? 1 : 0;

@@ -55,6 +55,22 @@ def test_update_device_tensor(gpu, oracle):
         assert tk.crc32().update(t).finalize() == oracle.crc(d.tobytes()), n
 
 
+def test_update_strided_device_views(gpu, oracle):
+    """update() over non-contiguous device views (every other byte, a column of a 2-D tensor, a
+    transposed int32 tensor): checksummed over the view's elements in order, as its contiguous copy
+    (ADVICE r3)."""
+    rng = np.random.default_rng(31)
+    d = rng.integers(0, 256, 1 << 18, dtype=np.uint8)
+    t = torch.from_numpy(d).to(gpu)
+    assert tk.crc32().update(t[::2]).finalize() == oracle.crc(d[::2].tobytes())
+    m = t.view(512, 512)
+    assert tk.crc32().update(m[:, 7]).finalize() == oracle.crc(np.ascontiguousarray(d.reshape(512, 512)[:, 7]).tobytes())
+    w = t.view(torch.int32).view(256, 256).t()
+    want = np.ascontiguousarray(d.view(np.int32).reshape(256, 256).T).tobytes()
+    assert tk.crc32().update(w).finalize() == oracle.crc(want)
+    assert tk.crc32c().update(t[1::3]).finalize() == oracle.crc_c(d[1::3].tobytes())
+
+
 def test_update_on_side_stream(gpu, oracle):
     """update(tensor, stream=s) with s not the current stream: the kernel on s must see bytes the
     current stream has just written, and the result must be read after the kernel on s."""

@@ -94,11 +94,7 @@ def test_null_arguments(lib, span):
     assert lib.tkv_crc32_update_host(0, None, 0, None) == 3
 
 
-def test_dropin_header_host_spans_on_cpu(tmp_path):
-    """The drop-in header with its default threshold (64 KiB): every span of the reference's usage
-    (crc32_test.cpp known answers, chained updates, wal_entry::encode's record CRC) runs on the host,
-    so this passes on a machine without a GPU, the per-thread counters show no GPU call, and a
-    36-byte put costs no more than the reference's byte loop on the same core."""
+def _run_dropin(tmp_path):
     exe = str(tmp_path / "test_dropin_host_span")
     lib = os.path.join(ROOT, "tinykvpp_amd")
     subprocess.run(["g++", "-std=c++20", "-O2", "-Wall", "-Wextra", "-Werror", "-Wconversion",
@@ -108,3 +104,24 @@ def test_dropin_header_host_spans_on_cpu(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
     assert "ALL PASSED" in r.stdout
+    return r
+
+
+def test_dropin_header_host_spans_on_cpu(tmp_path):
+    """The drop-in header with its default threshold (64 KiB): every span of the reference's usage
+    (crc32_test.cpp known answers, chained updates, wal_entry::encode's record CRC) runs on the host,
+    the per-thread counters show no GPU call, and a 36-byte put costs no more than the reference's
+    byte loop on the same core. Spans above the threshold (1 MiB, a 128 KiB WAL record) try the GPU;
+    on this GPU-less machine the header recomputes them on the host after the error, with one
+    warning, instead of aborting: crc32::update never fails (crc32.cpp:9-16)."""
+    r = _run_dropin(tmp_path)
+    if "no GPU" in r.stdout:
+        assert "GPU calls 3, host recomputes 3" in r.stdout
+        assert r.stderr.count("recomputed on the host") == 1  # one warning per process
+
+
+@pytest.mark.gpu
+def test_dropin_header_on_gpu(gpu, tmp_path):
+    """The same binary on the GPU box: the long spans take the GPU and nothing is recomputed."""
+    r = _run_dropin(tmp_path)
+    assert "GPU present; GPU calls 3, host recomputes 0" in r.stdout, r.stdout

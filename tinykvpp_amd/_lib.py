@@ -40,6 +40,8 @@ SIGNATURES = {
     "tkv_crc32_update": (_int, [_u32, _vp, _sz, ctypes.POINTER(_u32)]),
     "tkv_crc32_update_host": (_int, [_u32, _vp, _sz, ctypes.POINTER(_u32)]),
     "tkv_crc32c_update_host": (_int, [_u32, _vp, _sz, ctypes.POINTER(_u32)]),
+    "tkv_crc32_update_fallback": (_int, [_int, _u32, _vp, _sz, ctypes.POINTER(_u32)]),
+    "tkv_crc32c_update_fallback": (_int, [_int, _u32, _vp, _sz, ctypes.POINTER(_u32)]),
     "tkv_crc32_update_device": (_int, [_u32, _vp, _sz, _vp, _vp]),
     "tkv_crc32_batch_device": (_int, [_u8p, _vp, _vp, _vp, _vp, _u64, _vp]),
     "tkv_crc32_batch_uniform_device": (_int, [_u8p, _u64, _u64, _vp, _vp, _u64, _vp]),

@@ -93,9 +93,13 @@ class crc32:  # noqa: N801 - reference class name (crc32.hpp:32)
         except ImportError:  # pragma: no cover - torch is part of the image
             is_dev = False
         if is_dev:
-            _check_data(data)  # the library launches on the current device: the tensor must be there
+            # the library launches on the current device, so the tensor must be there; a strided view
+            # is checksummed over its elements in order, as a contiguous copy
+            if data.device.index != torch.cuda.current_device():
+                raise ValueError(f"data is on {data.device}, but the current device is "
+                                 f"cuda:{torch.cuda.current_device()}")
             cur = torch.cuda.current_stream(data.device)
-            t = data.contiguous().view(torch.uint8)  # any copy runs on the current stream
+            t = data.contiguous().view(-1).view(torch.uint8)  # any copy runs on the current stream
             out = torch.empty(1, dtype=torch.int32, device=t.device)
             s = stream if stream is not None else cur
             if s != cur:

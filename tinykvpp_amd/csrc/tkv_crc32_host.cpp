@@ -427,15 +427,21 @@ RowsArgs base_args(DevCtx* c, StreamScratch* s, int algo) {
   return a;
 }
 
-// Uniform batches with len <= lane_max() take crc_lanes: kLaneMax; TKV_LANE_MAX lowers it (-1 turns
-// the kernel off; for A/B measurements against the kernels that served these lengths before).
+// Uniform batches with len <= lane_max() take crc_lanes: kLaneMax. An A/B build
+// (-DTKV_AB_LANE_MAX_ENV, tools/build_variant.sh) lets the environment variable TKV_LANE_MAX lower it
+// (-1 turns the kernel off) to measure against the kernels that served these lengths before; the
+// product library has no such knob, so its kernel choice depends on the batch alone.
 long long lane_max() {
+#ifdef TKV_AB_LANE_MAX_ENV
   static const long long v = [] {
     const char* e = std::getenv("TKV_LANE_MAX");
     const long long x = e ? std::atoll(e) : static_cast<long long>(kLaneMax);
     return std::max(-1LL, std::min<long long>(x, kLaneMax));
   }();
   return v;
+#else
+  return static_cast<long long>(kLaneMax);
+#endif
 }
 
 // Uniform-length batch (also used for single spans).
@@ -527,6 +533,10 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   a.s_len = s->po.s_len;
   a.s_idx = s->po.s_idx;
   a.init_raw = d_init;
+  // The group phase takes the default register's init term from the init_shift table, which holds
+  // Shift_len(0xFFFFFFFF): an irregular batch without per-block registers must start from kInit
+  // (base_args sets it; this guards a future caller that changes it).
+  if (a.init_default != kInit) return fail(TKV_INVALID_ARGUMENT, "irregular batches start from 0xFFFFFFFF");
   a.out = d_out;
   a.nblocks = static_cast<std::uint32_t>(n);
   a.nwaves = static_cast<std::uint32_t>(c->ncu) * kRowsWavesPerWG;
@@ -960,7 +970,7 @@ int span_batch(DevCtx* c, int algo, const uint8_t* h_base, const uint64_t* h_off
   return run_spans(c, algo, c->h_desc[0], static_cast<std::uint32_t>(n), kInit, h_out_final);
 }
 
-extern thread_local std::uint64_t g_update_calls[2];  // tkv_crc32_span.cpp
+extern thread_local std::uint64_t g_update_calls[3];  // tkv_crc32_span.cpp
 
 int update_impl(int algo, uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
   if (!ptr_ok(out_raw) || (len && !ptr_ok(data))) return fail(TKV_INVALID_ARGUMENT, "null pointer");

@@ -165,8 +165,11 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small(RowsArgs a) {
 // 1-3 % faster than DEPTH 3 / ILP 1 in one process (profiles/r3/small_gen/ab_depth.jsonl).
 #ifndef TKV_GEN_DEPTH
 #define TKV_GEN_DEPTH 2
+#endif
+#ifndef TKV_GEN_ILP
 #define TKV_GEN_ILP 1
 #endif
+static_assert(TKV_GEN_ILP >= 1 && TKV_GEN_DEPTH > TKV_GEN_ILP, "crc_packed_small_gen: DEPTH - ILP rows stay in flight");
 template <int G, bool INIT>
 __global__ __launch_bounds__(kThreads) void crc_packed_small_gen(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];

@@ -7,17 +7,23 @@
 // register semantics as crc32::update (crc32.cpp:9-16: no init or xorout applied here). Nothing in
 // the library calls it; the drop-in header uses it for spans up to TKV_DROPIN_HOST_MAX bytes
 // (default 64 KiB, the measured crossover with the GPU round trip), and the C ABI exposes it as the
-// separately named tkv_crc32[c]_update_host. It is not a fallback: the GPU entry points never route
-// here, with or without a device. Each call is counted per thread (tkv_debug_update_counts).
+// separately named tkv_crc32[c]_update_host. The GPU entry points never route here, with or without
+// a device. The drop-in header alone calls tkv_crc32[c]_update_fallback after a GPU update of a
+// long span returned an error, because the reference's crc32::update cannot fail (crc32.cpp:9-16):
+// that call recomputes the span here, warns once per process and is counted in a slot of its own.
+// Each call is counted per thread (tkv_debug_update_counts).
+#include <atomic>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 
 #include "tkv_crc32.h"
 
 namespace tkv {
-// Calls of this thread: [0] host span path (this file), [1] GPU update path (tkv_crc32_host.cpp).
+// Calls of this thread: [0] host span path (this file), [1] GPU update path (tkv_crc32_host.cpp),
+// [2] host recomputes after a failed GPU update (tkv_crc32[c]_update_fallback).
 // Thread-local plain counters: an atomic add would cost a third of a 36-byte span.
-thread_local std::uint64_t g_update_calls[2] = {0, 0};
+thread_local std::uint64_t g_update_calls[3] = {0, 0, 0};
 }  // namespace tkv
 
 namespace {
@@ -63,6 +69,21 @@ int update_host(std::uint32_t poly, std::uint32_t raw, const void* data, std::si
   return TKV_OK;
 }
 
+std::atomic<bool> g_fallback_warned{false};
+
+int update_fallback(std::uint32_t poly, int gpu_status, std::uint32_t raw, const void* data, std::size_t len,
+                    std::uint32_t* out_raw) {
+  if (out_raw == nullptr || (data == nullptr && len != 0)) return TKV_INVALID_ARGUMENT;
+  ++tkv::g_update_calls[2];
+  if (!g_fallback_warned.exchange(true, std::memory_order_relaxed))
+    std::fprintf(stderr,
+                 "libtkv_crc32: a GPU update of %zu bytes failed (status %d: %s); this and later failed "
+                 "updates are recomputed on the host (warned once per process)\n",
+                 len, gpu_status, tkv_last_error());
+  *out_raw = len ? span_update(tables(poly), raw, static_cast<const unsigned char*>(data), len) : raw;
+  return TKV_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -75,9 +96,19 @@ int tkv_crc32c_update_host(uint32_t raw_state, const void* data, size_t len, uin
   return update_host(0x82F63B78u, raw_state, data, len, out_raw);
 }
 
-void tkv_debug_update_counts(uint64_t out[2]) {
+int tkv_crc32_update_fallback(int gpu_status, uint32_t raw_state, const void* data, size_t len, uint32_t* out_raw) {
+  return update_fallback(TKV_CRC32_POLYNOMIAL, gpu_status, raw_state, data, len, out_raw);
+}
+
+int tkv_crc32c_update_fallback(int gpu_status, uint32_t raw_state, const void* data, size_t len,
+                               uint32_t* out_raw) {
+  return update_fallback(0x82F63B78u, gpu_status, raw_state, data, len, out_raw);
+}
+
+void tkv_debug_update_counts(uint64_t out[3]) {
   out[0] = tkv::g_update_calls[0];
   out[1] = tkv::g_update_calls[1];
+  out[2] = tkv::g_update_calls[2];
 }
 
 }  // extern "C"

@@ -854,6 +854,7 @@ int verify_locked(WalScratch& s, const std::uint8_t* d_wal, std::uint64_t size, 
   for (int pass = 0; pass < kMaxPasses; ++pass) {
     PassResult r;
     g_last[0] = static_cast<std::uint64_t>(pass) + 1;
+    if (pass == 0 && !first_pass) g_last[3] = 1;  // cleared by the first pass that needs the pointer-jumping stitch
     if (pass == 0 && first_pass) r = *first_pass;
     else if (int rc = wal_pass(s, d_wal + start, size - start, st, &r)) return rc;
     good += r.good;
@@ -901,7 +902,6 @@ int wal_verify_device_impl(const std::uint8_t* d_wal, std::uint64_t size, std::u
   *stop_offset = 0;
   g_last[0] = g_last[1] = g_last[2] = g_last[3] = 0;
   if (size == 0) return TKV_OK;
-  g_last[3] = 1;  // cleared by the first pass that needs the pointer-jumping stitch
   if ((size + kWalPiece - 1) / kWalPiece >= 0xFFFFFFFFull)
     return set_error(TKV_INVALID_ARGUMENT, "WAL image too large for the device walk");
   WalScratch* sp = nullptr;
@@ -918,7 +918,6 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
   *stop_offset = 0;
   g_last[0] = g_last[1] = g_last[2] = g_last[3] = 0;
   if (size == 0) return TKV_OK;
-  g_last[3] = 1;  // cleared by the first pass that needs the pointer-jumping stitch
   if ((size + kWalPiece - 1) / kWalPiece >= 0xFFFFFFFFull) {
     *needs_host_walk = true;
     return TKV_OK;
@@ -1001,6 +1000,7 @@ int host_image_locked(WalScratch& s, const std::uint8_t* h_wal, std::uint64_t si
   WAL_HIP(hipGetLastError());
   PassResult r;
   g_last[0] = 1;
+  g_last[3] = 1;  // the first device pass starts here; cleared if it needs the pointer-jumping stitch
   if (int rc = pass_tail(s, a, s.stc, &r)) return rc;
   return verify_locked(s, s.d_img, size, n_good, stop_offset, s.stc, needs_host_walk, &r);
 }
