@@ -352,7 +352,7 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="cfg3: skip the host-memory end-to-end measurement")
     ap.add_argument("--no-pipelined", action="store_true", help="skip the two-stream pipelined rate (extra field)")
     ap.add_argument("--no-more-configs", action="store_true",
-                    help="cfg2 at N=1: skip timing cfg3 and cfg4 in the same run (more_configs)")
+                    help="cfg2: skip timing cfg3, cfg4 and cfg5 (N=1) or cfg5 (N>1) in the same run (more_configs)")
     ap.add_argument("--traffic-csv", default=None,
                     help="rocprofv3 --pmc counter_collection.csv (FETCH_SIZE) of this command, for roofline.traffic")
     args = ap.parse_args()
@@ -482,26 +482,37 @@ def main():
         cb["agrees_with_gpu"] = bool(np.array_equal(cpu_crcs, crcs[:cpu_crcs.size]))
         line["cpu_baseline"] = cb
         del host
-    if world == 1 and args.config == "cfg2" and not args.no_more_configs:
-        # The metric's other half (64 KiB blocks, cfg3, with its host legs) and the irregular path (cfg4),
-        # timed in this same run exactly as the main line is: warm-up with the clock floor, K steps between
-        # one event pair, every block checked against the golden aggregates. Never `value`.
+    if args.config == "cfg2" and not args.no_more_configs:
+        # The metric's other half (64 KiB blocks, cfg3, with its host legs), the irregular path (cfg4) and
+        # the 8-GPU shard config (cfg5: each rank its own 512 K x 64 KiB shard, rank r = global blocks
+        # [r * 512 K, (r + 1) * 512 K)), timed in this same run exactly as the main line is: warm-up with
+        # the clock floor, K steps between one event pair (bracketed by barriers across ranks), every
+        # block checked against the golden aggregates. At N > 1 only cfg5 runs (the scaling config), its
+        # aggregate = all ranks' bytes / the max over ranks of the wall time. Never `value`.
         del ctx, step, data, out
         torch.cuda.empty_cache()
         more = {}
-        for cfg in ("cfg3", "cfg4"):
+        for cfg in (("cfg3", "cfg4", "cfg5") if world == 1 else ("cfg5",)):
             nb, bl, dsc = CONFIGS[cfg]
-            c = prepare(cfg, 0, nb, dev, ora)
+            f0, nb = rank_shard(rank, nb) if cfg == "cfg5" else (0, nb)
+            c = prepare(cfg, f0, nb, dev, ora)
             o = torch.empty(nb, dtype=torch.int32, device=dev)
+            if use_dist:
+                dist.barrier()
             warm_up(lambda: c["step"](None, o), args.warmup, args.min_warmup_ms)
-            el, kms = time_steps(c["step"], o, stream, args.steps)
+            el, kms = time_steps(c["step"], o, stream, args.steps, dist.barrier if use_dist else None)
             cr = o.cpu().numpy().view(np.uint32).copy()
-            ok, fl = verify_rank(ora, cfg, 0, cr, bl, None if bl else c["lens"])
-            entry = {"workload": f"{cfg}: {dsc}", "value": round(c["total"] * args.steps / (1 << 30) / el, 2),
-                     "unit": "GiB/s", "ms_per_step": round(el * 1e3 / args.steps, 4),
-                     "roofline": roofline(c["total"], kms, cfg), "bit_exact": ok,
-                     "bit_exact_scope": "every block (golden XOR/SUM32) and the first 64 against the oracle" if fl
-                     else "first 64 blocks against the oracle"}
+            ok, fl = verify_rank(ora, cfg, f0, cr, bl, None if bl else c["lens"])
+            seen = 1
+            if use_dist:
+                el, kms, ok, seen, fl = reduce_timing(el, kms, ok, dist, dev if backend == "nccl" else None, fl)
+            entry = {"workload": f"{cfg}: {dsc}", "value": round(c["total"] * args.steps * world / (1 << 30) / el, 2),
+                     "unit": "GiB/s", "n_gpus": world, "ms_per_step": round(el * 1e3 / args.steps, 4),
+                     "roofline": roofline(c["total"], kms, cfg), "bit_exact": ok, "ranks_seen": seen,
+                     "bit_exact_scope": ("every block of every rank's shard (golden XOR/SUM32) and the first 64 "
+                                         "against the oracle") if fl else "first 64 blocks against the oracle"}
+            if cfg == "cfg5":
+                entry["shards"] = f"rank r: global blocks [r*{nb}, (r+1)*{nb}); value = {world} shards' bytes / max wall"
             if cfg == "cfg3" and not args.no_e2e:
                 entry["e2e_host"] = host_legs(c, cr)
             more[cfg] = entry
