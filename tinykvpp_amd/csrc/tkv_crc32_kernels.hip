@@ -41,10 +41,11 @@ struct Shape {
 // ---- stream mode: every block's CRC from crc_stream's per-end and per-wave registers -----------------
 // Run by crc_rows<false, false>, which is launched after crc_stream and has nothing else to do on a
 // stream-mode batch: the finish rides on that launch instead of a launch of its own.
-// x^(8d) mod P for any byte distance d.
+// x^(8d) mod P for any byte distance d: one table entry for d <= 4096, one GF(2) multiply more above.
 __device__ __forceinline__ std::uint32_t stream_x8n(const DeviceTables* t, std::uint64_t d) {
-  return dev::multmodp(dev::shift_rows_tab(t, 0x80000000u, static_cast<std::uint32_t>(d >> 12)),
-                       t->head_shift[d & 4095u][31], t->poly);
+  const std::uint32_t lo = t->head_shift[d & 4095u][31];
+  const std::uint32_t k = static_cast<std::uint32_t>(d >> 12);
+  return k == 0u ? lo : dev::shift_rows_tab(t, lo, k);
 }
 
 // Block b = [E[b-1], E[b]) of the stream (block 0 starts at the stream start s0; the bytes of row 0
@@ -53,28 +54,51 @@ __device__ __forceinline__ std::uint32_t stream_x8n(const DeviceTables* t, std::
 // L(e) = crc_0(bytes of e's wave up to e) = Shift_(rowend - e)^-1 (Y) ^ Q from the row kernel. Then
 // S(e) = Shift_(e - 4096 g0(w))(S(4096 g0(w))) ^ L(e), and S at a wave start is the sum of the earlier
 // waves' T_v each shifted to that point, so with e' = E[b-1] in wave w' and e = E[b] in wave w:
-//   crc_0(block) = S(e) ^ Shift_len(S(e')) = L(e) ^ Shift_len(L(e')) ^ sum_{w' <= v < w} Shift_(e - 4096 g1(v))(T_v)
+//   crc_0(block) = L(e) ^ Shift_len(L(e')) ^ sum_{w' <= v < w} Shift_(e - 4096 g1(v))(T_v)
 // (the wave sums before w' cancel). Most blocks lie in one wave and the last sum is empty. For
 // block 0, L(s0) = 0 and w' = 0. The register from init is Shift_len(init) ^ crc_0(block).
-__device__ __forceinline__ void stream_finish_block(const RowsArgs& a, std::uint64_t b) {
+//
+// Lane l of a wave takes block w0 + l - 1 and computes its L(E) and loads E and its wave; lanes 1-63
+// then finish their blocks with the predecessor's values pulled from the lane below (ds_bpermute), so
+// each L costs one GF(2) multiply per block instead of two, and a block under 4 KiB needs no multiply
+// for Shift_len: two multiplies per block in all (there were six, bitwise at 32 steps each). A wave
+// advances 63 blocks per step.
+__device__ __forceinline__ void stream_finish(const RowsArgs& a) {
   const DeviceTables* t = a.tabs;
   const std::uint32_t poly = t->poly;
-  auto L = [&](std::uint64_t e, std::uint64_t yq) -> std::uint32_t {
-    const std::uint64_t rowend = ((e - 1) / kRow + 1) * kRow;
-    return dev::multmodp(t->inv_shift[rowend - e], static_cast<std::uint32_t>(yq), poly) ^
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint64_t wave = (blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x) >> 6;
+  const std::uint64_t nw = (static_cast<std::uint64_t>(gridDim.x) * blockDim.x) >> 6;
+  const std::uint64_t n = a.nblocks;
+  for (std::uint64_t w0 = wave * 63u; w0 < n; w0 += nw * 63u) {
+    const std::uint64_t b = w0 + lane - 1u;  // lane 0 of the first step: b = ~0 (no block: L = 0)
+    const bool have = (w0 + lane) != 0u && b < n;
+    std::uint64_t e = a.s_info[1];  // the stream start, the end of "block -1"
+    std::uint32_t Le = 0, w = 0;
+    if (have) {
+      e = a.s_ends[b];
+      w = a.s_wv[b];
+      const std::uint64_t yq = a.s_yq[b];
+      const std::uint64_t rowend = ((e - 1) / kRow + 1) * kRow;
+      Le = dev::multmodp(t->inv_shift[rowend - e], static_cast<std::uint32_t>(yq), poly) ^
            static_cast<std::uint32_t>(yq >> 32);
-  };
-  const std::uint64_t e = a.s_ends[b];
-  const std::uint64_t ep = b ? a.s_ends[b - 1] : 0;
-  const std::uint64_t len = b ? e - ep : e - a.s_info[1];
-  std::uint32_t crc0 = L(e, a.s_yq[b]);
-  const std::uint32_t w = a.s_wv[b], wp = b ? a.s_wv[b - 1] : 0u;
-  for (std::uint32_t v = wp; v < w; ++v)
-    crc0 ^= dev::multmodp(stream_x8n(t, e - static_cast<std::uint64_t>(a.s_row0[v + 1]) * kRow), a.s_wtot[v], poly);
-  const std::uint32_t lp = b ? L(ep, a.s_yq[b - 1]) : 0u;
-  const std::uint32_t init = a.init_raw ? a.init_raw[b] : a.init_default;
-  const std::uint32_t raw = dev::multmodp(stream_x8n(t, len), init ^ lp, poly) ^ crc0;
-  a.out[b] = raw ^ a.out_xor;
+    }
+    const int src = static_cast<int>((lane == 0u ? 0u : lane - 1u) * 4u);
+    const std::uint32_t Lp = static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(Le)));
+    const std::uint32_t wp = static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(w)));
+    const std::uint64_t ep =
+        static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(static_cast<std::uint32_t>(e)))) |
+        (static_cast<std::uint64_t>(static_cast<std::uint32_t>(
+             __builtin_amdgcn_ds_bpermute(src, static_cast<int>(static_cast<std::uint32_t>(e >> 32)))))
+         << 32);
+    if (lane == 0u || b >= n) continue;
+    std::uint32_t crc0 = Le;
+    for (std::uint32_t v = wp; v < w; ++v)
+      crc0 ^= dev::multmodp(stream_x8n(t, e - static_cast<std::uint64_t>(a.s_row0[v + 1]) * kRow), a.s_wtot[v], poly);
+    const std::uint32_t init = a.init_raw ? a.init_raw[b] : a.init_default;
+    const std::uint32_t raw = dev::multmodp(stream_x8n(t, e - ep), init ^ Lp, poly) ^ crc0;
+    a.out[b] = raw ^ a.out_xor;
+  }
 }
 
 template <bool ALIGNED, bool UNIFORM>
@@ -85,9 +109,7 @@ __global__ __launch_bounds__(kRowsThreads) void crc_rows(RowsArgs a) {
     // crc_stream (launched just before) has walked it, and this launch turns its registers into
     // block CRCs
     if (dev::sload32(a.counts, 3) == kModeStream) {
-      const std::uint64_t step = static_cast<std::uint64_t>(gridDim.x) * blockDim.x;
-      for (std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x; b < a.nblocks; b += step)
-        stream_finish_block(a, b);
+      stream_finish(a);
       return;
     }
   }
