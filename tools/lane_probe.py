@@ -95,6 +95,12 @@ def main():
     work.append(irregular("irregular back to back 64 B", np.full(n, 64), np.zeros(n, np.int64), 0))
     n = count(128, 128)
     work.append(irregular("irregular back to back 128 B", np.full(n, 128), np.zeros(n, np.int64), 0))
+    # 257 B - 1 KiB: WAL payloads with mid-size values, gapped and back to back
+    for lo, hi in ((257, 512), (513, 1024), (300, 1000), (257, 1024)):
+        ng = count((lo + hi) // 2, (lo + hi) // 2 + 8)
+        work.append(irregular(f"irregular {lo}-{hi} B, 8 B gaps", rng.integers(lo, hi + 1, ng), np.full(ng, 8), 8))
+    ng = count(650, 650)
+    work.append(irregular("irregular back to back 300-1000 B", rng.integers(300, 1001, ng), np.zeros(ng, np.int64), 0))
     n = count(2048, 2056)
     lr = rng.integers(0, 4097, n)
     work.append(irregular("irregular 0-4 KiB, 8 B gaps", lr, np.full(n, 8), 8))
