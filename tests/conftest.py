@@ -171,3 +171,44 @@ def gpu():
     torch.cuda.set_device(0)
     tk.set_device(0)
     return torch.device("cuda:0")
+
+
+# ---- which path an irregular batch takes: the prepass's verdict restated --------
+LANE_MAX = 64        # kLaneMax
+GROUP_MAX = 256      # kGroupMax: blocks of LANE_MAX + 1 .. GROUP_MAX are group blocks
+SMALL_MAX = 1024     # kSmallMax
+SCAN_TILE = 4096     # kScanTile
+GROUP_DENSE_TILE = 1024  # kGroupDenseTile
+GROUP_TILE_ROWS = 1024   # kGroupTileRows
+
+
+def stream_expected(offs, lens, group_stream=False):
+    """1 when the prepass picks the byte-stream walk for this batch, else 0: every block at least
+    LANE_MAX + 1 bytes and starting where its predecessor ends, and (unless tkv_debug_set_stream_groups
+    is on) no scan tile dense in group blocks (at least GROUP_DENSE_TILE of them among its 4096 blocks,
+    with at most GROUP_TILE_ROWS rows of blocks over SMALL_MAX bytes)."""
+    offs = np.asarray(offs, np.int64)
+    lens = np.asarray(lens, np.int64)
+    if lens.size == 0 or lens.min() <= LANE_MAX or np.any(offs[:-1] + lens[:-1] != offs[1:]):
+        return 0
+    if group_stream:
+        return 1
+    for t in range(0, lens.size, SCAN_TILE):
+        tl = lens[t:t + SCAN_TILE]
+        groups = int(np.count_nonzero((tl > LANE_MAX) & (tl <= GROUP_MAX)))
+        big = tl[tl > SMALL_MAX]
+        rows = int(((big - 1) // 4096 + 1).sum())
+        if groups >= GROUP_DENSE_TILE and rows <= GROUP_TILE_ROWS:
+            return 0
+    return 1
+
+
+@pytest.fixture
+def stream_groups():
+    """Sets tkv_debug_set_stream_groups(1) for one test (group-dense back-to-back batches may take the
+    byte-stream walk, as before round 4), so the walk's many-ends-per-row shapes stay under test."""
+    import tinykvpp_amd as tk
+    lib = tk.load_library()
+    prev = lib.tkv_debug_set_stream_groups(1)
+    yield
+    lib.tkv_debug_set_stream_groups(prev)

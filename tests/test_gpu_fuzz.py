@@ -12,6 +12,7 @@ import pytest
 import torch
 
 import tinykvpp_amd as tk
+from conftest import stream_expected
 
 pytestmark = pytest.mark.gpu
 
@@ -94,7 +95,7 @@ def test_irregular_random(gpu, oracle, seed):
     assert bad.size == 0, (f"{layout} n={n} start={start} shift={shift} algo={algo} mode={irregular_mode()}: "
                            f"{bad.size} blocks differ, first {bad[:5]} (lens {lens[bad[:5]]})")
     if layout == "back_to_back_min64" and n > 1:
-        assert irregular_mode() == 1, "a back-to-back batch of blocks > 64 B (kLaneMax) takes stream mode"
+        assert irregular_mode() == stream_expected(offs, lens), "the prepass's stream verdict"
 
 
 @pytest.mark.parametrize("seed", range(48))
@@ -317,11 +318,22 @@ def test_wal_stamp_random(gpu, oracle, seed):
     assert buf.tobytes() == image, f"pinned stamp differs (shift {shift})"
 
 
+@pytest.mark.parametrize("group_stream", [True, False])
 @pytest.mark.parametrize("seed", range(12))
-def test_stream_many_blocks_random(gpu, oracle, seed):
+def test_stream_many_blocks_random(gpu, oracle, seed, group_stream):
     """Stream mode over 50 K-200 K back-to-back blocks (several block ends per row and lane segment
     boundary, every wave holding ends), any base alignment and stream start, per-block initial
-    registers, both polynomials."""
+    registers, both polynomials; with tkv_debug_set_stream_groups(1) every such batch takes the stream
+    walk, with the default policy those dense in 65-256-byte blocks take the general path."""
+    lib = tk.load_library()
+    prev = lib.tkv_debug_set_stream_groups(1 if group_stream else 0)
+    try:
+        stream_many_case(oracle, gpu, seed, group_stream)
+    finally:
+        lib.tkv_debug_set_stream_groups(prev)
+
+
+def stream_many_case(oracle, gpu, seed, group_stream):
     rng = np.random.default_rng(8000 + seed + OFFSET)
     algo = ALGOS[seed % 2]
     n = int(rng.integers(50_000, 200_000))
@@ -335,7 +347,7 @@ def test_stream_many_blocks_random(gpu, oracle, seed):
     ini = None if init is None else torch.from_numpy(init.view(np.int32)).to(gpu)
     got = u32(tk.crc32_batch(d, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu),
                              init_raw=ini, algo=algo))
-    assert irregular_mode() == 1
+    assert irregular_mode() == stream_expected(offs, lens, group_stream)
     want = oracle_batch(oracle, algo, host, offs, lens, init)
     bad = np.flatnonzero(got != want)
     assert bad.size == 0, f"n={n} start={start} shift={shift} algo={algo}: {bad.size} differ, first {bad[:5]}"

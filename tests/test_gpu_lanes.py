@@ -155,17 +155,25 @@ def test_irregular_mixed_classes(gpu, oracle, mix):
     assert np.array_equal(got, oracle_c(oracle, host, offs[:m], lens[:m]))
 
 
-def test_stream_mode_needs_blocks_longer_than_lanes(gpu, oracle, buf):
-    """Back-to-back 64-byte blocks are lane blocks (general path); 65-byte blocks still take stream
-    mode; both bit-exact."""
+@pytest.mark.parametrize("group_stream", [0, 1])
+def test_stream_mode_needs_blocks_longer_than_lanes(gpu, oracle, buf, group_stream):
+    """Back-to-back 64-byte blocks are lane blocks (general path). Back-to-back 65-byte blocks are group
+    blocks: by default their dense tiles take the general path and the group phase (round 4; it folds
+    them faster than the stream walk's rows of 63 block ends), with tkv_debug_set_stream_groups(1)
+    stream mode as before. 300-byte blocks take stream mode either way. All bit-exact."""
     host, d = buf
-    for blen, want_mode in ((64, 0), (65, 1), (40, 0)):
-        n = 50_000
-        offs = 7 + np.arange(n, dtype=np.int64) * blen
-        lens = np.full(n, blen, np.int32)
-        got = u32(tk.crc32_batch(d, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu)))
-        assert mode() == want_mode, blen
-        assert np.array_equal(got, oracle.batch(host, offs, lens)), blen
+    lib = tk.load_library()
+    prev = lib.tkv_debug_set_stream_groups(group_stream)
+    try:
+        for blen, want_mode in ((64, 0), (65, group_stream), (40, 0), (128, group_stream), (300, 1)):
+            n = 50_000
+            offs = 7 + np.arange(n, dtype=np.int64) * blen
+            lens = np.full(n, blen, np.int32)
+            got = u32(tk.crc32_batch(d, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu)))
+            assert mode() == want_mode, blen
+            assert np.array_equal(got, oracle.batch(host, offs, lens)), blen
+    finally:
+        lib.tkv_debug_set_stream_groups(prev)
 
 
 def test_lane_blocks_then_stream_batch_same_scratch(gpu, oracle, buf):
@@ -182,13 +190,15 @@ def test_lane_blocks_then_stream_batch_same_scratch(gpu, oracle, buf):
         assert np.array_equal(got, oracle.batch(host, offs, lens))
 
 
-@pytest.mark.parametrize("shape", ["wal_payloads", "mixed_gaps", "back_to_back_128"])
+@pytest.mark.parametrize("shape", ["wal_payloads", "mixed_gaps", "back_to_back_128", "back_to_back_128_stream",
+                                   "back_to_back_300"])
 def test_irregular_more_than_1024_tiles(gpu, oracle, shape):
     """Batches of more than 4 M blocks (over 1024 prepass tiles of 4096 blocks) take the 512-thread
     tile scan and the unfused scatter: lane-dense tiles (WAL payloads), tiles mixing lane, small and
     large blocks with random gaps, and 128-byte blocks back to back, which take stream mode through
     rows_scan_tiles' verdict; per-block initial registers on the mixed batch."""
-    rng = np.random.default_rng({"wal_payloads": 1, "mixed_gaps": 2, "back_to_back_128": 3}[shape])
+    rng = np.random.default_rng({"wal_payloads": 1, "mixed_gaps": 2, "back_to_back_128": 3, "back_to_back_128_stream": 3,
+                                 "back_to_back_300": 4}[shape])
     n = 4096 * 1025 + 777
     if shape == "wal_payloads":
         offs, lens = wal_payloads(rng, n, WAL_SIZES, 3)
@@ -197,17 +207,25 @@ def test_irregular_more_than_1024_tiles(gpu, oracle, shape):
         lens[rng.integers(0, n, 50)] = rng.integers(1025, 9000, 50)
         offs = np.concatenate([[0], np.cumsum(lens[:-1])]) + rng.integers(0, 5, n).cumsum()
     else:
-        lens = np.full(n, 128)
-        offs = 5 + np.arange(n, dtype=np.int64) * 128
+        blen = 300 if shape == "back_to_back_300" else 128
+        lens = np.full(n, blen)
+        offs = 5 + np.arange(n, dtype=np.int64) * blen
     lens = lens.astype(np.int32)
     size = int((offs + lens).max()) + 16
     host = rng.integers(0, 256, size, dtype=np.uint8)
     d = torch.from_numpy(host).to(gpu)
     o = torch.from_numpy(offs.astype(np.int64)).to(gpu)
     ln = torch.from_numpy(lens).to(gpu)
-    assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), oracle.batch(host, offs, lens))
-    # back-to-back blocks longer than kLaneMax take stream mode at any batch size
-    assert mode() == (1 if shape == "back_to_back_128" else 0)
+    lib = tk.load_library()
+    prev = lib.tkv_debug_set_stream_groups(1 if shape == "back_to_back_128_stream" else 0)
+    try:
+        assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), oracle.batch(host, offs, lens))
+        got_mode = mode()
+    finally:
+        lib.tkv_debug_set_stream_groups(prev)
+    # back-to-back blocks longer than kLaneMax take stream mode at any batch size, through
+    # rows_scan_tiles' verdict, unless their tiles are dense in group blocks (128 B, by default)
+    assert got_mode == (1 if shape in ("back_to_back_128_stream", "back_to_back_300") else 0)
     if shape == "mixed_gaps":
         init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
         got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))

@@ -10,6 +10,7 @@ import pytest
 import torch
 
 import tinykvpp_amd as tk
+from conftest import stream_expected
 
 pytestmark = pytest.mark.gpu
 
@@ -55,10 +56,8 @@ def test_stream_alignments(gpu, oracle, start):
     assert run(gpu, oracle, lens, start=start, seed=start) == 1
 
 
-@pytest.mark.parametrize("case", ["exact64", "seg_ends", "row_ends", "one_block", "two_blocks", "mixed_huge",
-                                  "many_small", "span_waves"])
-def test_stream_shapes(gpu, oracle, case):
-    rng = np.random.default_rng(hash(case) & 0xFFFF)
+def shape_lens(case):
+    rng = np.random.default_rng(sum(map(ord, case)))
     if case == "exact64":  # a block end in 64 of every 65 lane segments (64-byte blocks are lane blocks)
         lens = np.full(20000, 65)
     elif case == "seg_ends":  # ends on 64-byte segment boundaries, some at r = 64, some mid-dword
@@ -76,7 +75,28 @@ def test_stream_shapes(gpu, oracle, case):
                                [(24 << 20) + 4096], rng.integers(65, 5000, 3000)])
     else:  # many small blocks: several ends per row in consecutive lanes
         lens = rng.integers(65, 200, 200000)
-    assert run(gpu, oracle, lens, start=5, seed=1) == 1
+    return lens
+
+
+SHAPES = ["exact64", "seg_ends", "row_ends", "one_block", "two_blocks", "mixed_huge", "many_small", "span_waves"]
+
+
+@pytest.mark.parametrize("case", SHAPES)
+def test_stream_shapes(gpu, oracle, stream_groups, case):
+    """Every shape through the byte-stream walk (with tkv_debug_set_stream_groups(1), so the shapes
+    dense in 65-256-byte blocks, whose rows hold 16-64 block ends, take it too)."""
+    assert run(gpu, oracle, shape_lens(case), start=5, seed=1) == 1
+
+
+@pytest.mark.parametrize("case", SHAPES)
+def test_stream_shapes_default_policy(gpu, oracle, case):
+    """The same shapes with the default policy: back-to-back batches dense in 65-256-byte blocks take
+    the general path (their group phase, round 4), the others stream mode; bit-exact either way."""
+    lens = shape_lens(case)
+    offs = 5 + np.concatenate([[0], np.cumsum(lens[:-1])])
+    assert run(gpu, oracle, lens, start=5, seed=1) == stream_expected(offs, lens)
+    if case in ("exact64", "seg_ends", "many_small"):
+        assert stream_expected(offs, lens) == 0
 
 
 def test_stream_init_and_crc32c(gpu, oracle):

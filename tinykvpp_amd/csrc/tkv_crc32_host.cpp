@@ -37,7 +37,7 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
                           std::uint32_t n, std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* tile_ok,
                           std::uint32_t* counts, std::uint64_t* sinfo, std::uint64_t* ends, const PrepassOut& o,
                           std::uint32_t W, std::uint32_t ncu, std::uint32_t* out, std::uint32_t* row0,
-                          hipStream_t st);
+                          std::uint32_t group_stream, hipStream_t st);
 hipError_t launch_stream_rows(const RowsArgs& a, hipStream_t st, unsigned grid);
 std::uint64_t prepass_tiles(std::uint64_t n);
 hipError_t launch_span(const std::uint8_t* stage, const SpanDesc& one, const SpanDesc* desc, std::uint32_t n,
@@ -515,6 +515,11 @@ int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t s
   return TKV_OK;
 }
 
+// Whether a back-to-back batch whose scan tiles are dense in group blocks may still take stream mode
+// (tkv_debug_set_stream_groups; default 0: such tiles go to the general path, whose group phase folds
+// those blocks faster than the stream walk's many-ends rows).
+std::atomic<int> g_stream_groups{0};
+
 int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::uint64_t* d_off, const std::uint32_t* d_len,
                   const std::uint32_t* d_init, std::uint32_t* d_out, std::uint64_t n, hipStream_t st) {
   if (n == 0) return TKV_OK;
@@ -554,7 +559,8 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   a.l_len = d_len;
   a.l_tile = s->tile_ok;
   TKV_HIP(launch_prepass(d_base, d_off, d_len, a.nblocks, s->scan, s->tiles, s->tile_ok, s->counts, sinfo, s->po.big_off,
-                         s->po, a.nwaves, static_cast<std::uint32_t>(c->ncu), d_out, row0, st));
+                         s->po, a.nwaves, static_cast<std::uint32_t>(c->ncu), d_out, row0,
+                         static_cast<std::uint32_t>(g_stream_groups.load(std::memory_order_relaxed)), st));
   // stream mode: crc_stream walks the rows and crc_rows finishes the block CRCs; general path:
   // crc_stream returns at once and crc_rows walks the rows (and combines its own seams)
   TKV_HIP(launch_stream_rows(a, st, static_cast<unsigned>(c->ncu)));
@@ -1356,5 +1362,7 @@ int tkv_debug_irregular_mode(void* stream) {
 }
 
 int tkv_debug_set_host_mapped(int enable) { return tkv::g_host_mapped.exchange(enable ? 1 : 0); }
+
+int tkv_debug_set_stream_groups(int enable) { return tkv::g_stream_groups.exchange(enable ? 1 : 0); }
 
 }  // extern "C"

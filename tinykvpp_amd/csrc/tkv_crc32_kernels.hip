@@ -258,7 +258,8 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
                                                               const std::uint32_t* lengths, std::uint32_t n,
                                                               std::uint64_t* scan, std::uint64_t* tile_sums,
                                                               std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
-                                                              std::uint32_t* lscan, std::uint32_t* tile_lanes) {
+                                                              std::uint32_t* lscan, std::uint32_t* tile_lanes,
+                                                              std::uint32_t group_stream) {
   constexpr unsigned kTileWaves = kTileThreads / 64;
   constexpr unsigned kTileBpt = kScanTile / kTileThreads;
   static_assert(kScanTile % kTileThreads == 0 && kTileWaves >= 1 && kTileBpt >= 4 && kTileBpt % 4 == 0,
@@ -346,7 +347,12 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     x &= tmask;
     return (x & 0xFFFFu) + (x >> 16);
   };
-  if (threadIdx.x == 0) tile_ok[blockIdx.x] = (all_ok ? kTileStream : 0u) | tph;
+  // A tile dense in group blocks does not qualify for stream mode (unless group_stream, a debug
+  // setting): the group phase folds 65-256-byte blocks at the rate of gapped ones, where the stream
+  // walk's rows of 16-64 block ends ran at about 0.6 of it (back-to-back 128 B: 1404 against 2351
+  // GB/s, profiles/r3/group_phase/). Longer blocks keep stream mode, where it wins (cfg4, 64 KiB).
+  const bool stream_ok = all_ok && (group_stream != 0u || (tph & kTileGroups) == 0u);
+  if (threadIdx.x == 0) tile_ok[blockIdx.x] = (stream_ok ? kTileStream : 0u) | tph;
   std::uint64_t run = wpre + inc - s;  // exclusive, lane and group blocks counted as small
   std::uint32_t lrun = lpre + linc - ls;
   if (tph == 0 && base + kTileBpt <= n) {
@@ -851,7 +857,7 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
                           std::uint32_t n, std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* tile_ok,
                           std::uint32_t* counts, std::uint64_t* sinfo, std::uint64_t* ends, const PrepassOut& o,
                           std::uint32_t W, std::uint32_t ncu, std::uint32_t* out, std::uint32_t* row0,
-                          hipStream_t st) {
+                          std::uint32_t group_stream, hipStream_t st) {
   const std::uint32_t Ws = ncu * (kStreamThreads / 64);  // crc_stream's waves
   // Grid sizes in 64-bit arithmetic: n may be close to 2^32 (the host caps it at kMaxIrregularBlocks).
   const std::uint64_t ntiles = prepass_tiles(n);
@@ -859,10 +865,10 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
   const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
   if (ntiles <= kFusedTiles)
     hipLaunchKernelGGL(rows_tile_scan<1024>, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets,
-                       lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes);
+                       lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, group_stream);
   else
     hipLaunchKernelGGL(rows_tile_scan<512>, dim3(static_cast<unsigned>(ntiles)), dim3(512), 0, st, base, offsets,
-                       lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes);
+                       lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, group_stream);
   if (ntiles <= kFusedTiles) {
     hipLaunchKernelGGL(rows_finish_fused, dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
                        offsets, lengths, n, scan, tile_sums, tile_ok, static_cast<std::uint32_t>(ntiles), counts, o,
