@@ -140,6 +140,20 @@ int tkv_wal_verify(const uint8_t *h_wal, uint64_t size, uint64_t *n_good, uint64
 int tkv_wal_verify_device(const uint8_t *d_wal, uint64_t size, uint64_t *n_good, uint64_t *stop_offset,
                           void *stream);
 
+/* Check n records of a WAL image already in DEVICE memory whose start offsets are known - the record
+ * list of a walk, or the offsets a group-commit writer kept: record i starts at
+ * d_img + d_rec_off[i] (u32 offsets, images up to 4 GiB). Each record gets wal_entry::decode's checks
+ * (wal.cpp:63-127): at least 26 bytes left, record_len + 8 within the image, the CRC-32 of the
+ * record_len payload bytes equal to the stored CRC, key and value inside the payload. The payload
+ * length comes from the record's own header, read from the same 16-byte granules as its payload: no
+ * lengths array, no prepass. *d_first_bad (device memory) = the index of the first record failing a
+ * check, n when every record passes. d_crc (nullable, device): the computed finalized CRC of every
+ * payload (0 for a record whose length check failed). max_payload is a dispatch hint (the longest
+ * record_len the caller expects: up to 68 bytes one lane reads the record in 6 granules, above 8);
+ * longer payloads are still checked exactly. Asynchronous on `stream`. */
+int tkv_wal_check_records_device(const uint8_t *d_img, uint64_t size, const uint32_t *d_rec_off, uint64_t n,
+                                 uint32_t max_payload, uint32_t *d_crc, uint64_t *d_first_bad, void *stream);
+
 /* Stamp n records in place (host memory): for record i at h_buf + h_offsets[i] of total size
  * h_sizes[i] (>= 8), write crc32 of bytes [8, size) LE at offset 4 (wal.cpp:54-58). */
 int tkv_wal_stamp(uint8_t *h_buf, const uint64_t *h_offsets, const uint32_t *h_sizes, uint64_t n);

@@ -51,6 +51,7 @@ SIGNATURES = {
     "tkv_wal_verify": (_int, [_u8p, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "tkv_wal_verify_device": (_int, [_u8p, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64), _vp]),
     "tkv_wal_stamp": (_int, [_u8p, _vp, _vp, _u64]),
+    "tkv_wal_check_records_device": (_int, [_u8p, _u64, _vp, _u64, _u32, _vp, _vp, _vp]),
     "tkv_fill_synthetic_uniform": (_int, [_u8p, _u64, _u64, _u64, _u64, _u64, _vp]),
     "tkv_fill_synthetic_blocks": (_int, [_u8p, _vp, _vp, _u64, _u64, _u64, _vp]),
     "tkv_sst_stamp_blocks": (_int, [_u8p, _vp, _vp, _u64]),

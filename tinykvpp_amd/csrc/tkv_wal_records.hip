@@ -1,0 +1,224 @@
+// Record-list check of a WAL image in HBM (tkv_wal_check_records_device, include/tkv_crc32.h):
+// wal_entry::decode's per-record checks (/root/reference/src/engine/wal.cpp:63-127) for records whose
+// start offsets are already known - the record list a walk produced, or the offsets a group-commit
+// writer kept - with no lengths array and no prepass: each lane reads its record's header from the
+// same 16-byte granules that hold its payload.
+//
+// One lane folds one record. The lane loads the NG aligned granules that cover the record's first
+// 16 NG - 15 bytes at any alignment (the 8-byte header, key/value lengths at bytes 18-25, and the
+// first payload bytes), realigns them in registers (two bitwise selects by the start's dword offset in
+// its granule, then v_alignbyte by its byte offset, as the lane kernels do), and folds the payload
+// from 0xFFFFFFFF with slicing-by-4 lookups into the LDS tables and Sarwate steps for the last 1-3
+// bytes (crc32.cpp:9-16). A payload longer than the window continues 64 bytes at a time from fresh
+// granules, the register carried over (rare for WAL records; every length is exact). Loads are clamped
+// to the image's last granule, so no load leaves the image's pages whatever the offsets say.
+//
+// Per record (wal.cpp order): at least kMetadataSize = 26 bytes left (wal.cpp:68), record_len + 8
+// within the image (:80), CRC-32 of the record_len payload bytes equal to the stored CRC (:89-96), key
+// and value inside the payload (:118-121). A record failing any of them is corrupted; the first such
+// record index is an atomic minimum.
+//
+// Pipeline (lane_phase's): offsets are fetched four steps ahead of their granules, granules two steps
+// ahead of the fold, and nothing loaded is touched before use. Waves own contiguous ranges of records,
+// 64 per step, with the packed kernels' issue priority from the work left.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "tkv_crc32.h"
+#include "tkv_crc32_device.h"
+#include "tkv_engine.h"
+
+namespace tkv {
+namespace {
+
+constexpr std::uint32_t kRecMeta = 26;  // wal.hpp kMetadataSize: 8-byte header + op, seq, tombstone, key/value lengths
+constexpr unsigned kRecThreads = 1024;  // one workgroup per CU (128 KiB of LDS tables)
+
+struct RecArgs {
+  const std::uint8_t* w;
+  std::uint64_t size;
+  const std::uint32_t* off;
+  std::uint64_t n;
+  std::uint32_t* crc;                  // nullable: computed CRC per record (0 when its length is bad)
+  unsigned long long* first_bad;       // atomic minimum of bad record indices (preset to n)
+  std::uint32_t nwaves;
+};
+
+__global__ void rec_init(unsigned long long* first_bad, std::uint64_t n) { *first_bad = n; }
+
+// The 4 NG little-endian dwords from byte p of the granules g (o = p & 15): d[k] = bytes [p + 4k, +4).
+template <int NG>
+__device__ __forceinline__ void rec_dwords(const uint4 (&g)[NG], std::uint32_t o, std::uint32_t (&d)[4 * NG - 4]) {
+  std::uint32_t raw[4 * NG];
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    raw[4 * i + 0] = g[i].x;
+    raw[4 * i + 1] = g[i].y;
+    raw[4 * i + 2] = g[i].z;
+    raw[4 * i + 3] = g[i].w;
+  }
+  const std::uint32_t m8 = 0u - ((o >> 3) & 1u), m4 = 0u - ((o >> 2) & 1u);
+#pragma unroll
+  for (int i = 0; i < 4 * NG - 2; ++i) raw[i] ^= (raw[i] ^ raw[i + 2]) & m8;
+#pragma unroll
+  for (int i = 0; i < 4 * NG - 3; ++i) raw[i] ^= (raw[i] ^ raw[i + 1]) & m4;
+#pragma unroll
+  for (int k = 0; k < 4 * NG - 4; ++k) d[k] = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], o & 3u);
+}
+
+// Folds the payload bytes [0, n) of d (n <= 4 * ND) into register c (whole dwords, then Sarwate steps).
+template <int ND>
+__device__ __forceinline__ std::uint32_t rec_fold(const std::uint32_t* lds, const dev::LaneConst& kc, const std::uint32_t* d,
+                                                  std::uint32_t n, std::uint32_t c) {
+  dev::Reg r{c, 0};
+  const std::uint32_t nf = n >> 2, tb = n & 3u;
+#pragma unroll
+  for (int k = 0; k < ND; ++k) {
+    if (static_cast<std::uint32_t>(k) < nf) dev::slice4(lds, r, d[k], kc);
+    else if (static_cast<std::uint32_t>(k) == nf && tb != 0u) r = dev::Reg{dev::sarwate_bytes(lds, kc, r.value(), d[k], tb), 0};
+  }
+  if (nf == static_cast<std::uint32_t>(ND) && tb != 0u) r = dev::Reg{dev::sarwate_bytes(lds, kc, r.value(), d[ND], tb), 0};
+  return r.value();
+}
+
+// NG granules per record window; AHEAD steps of granules in flight (2, or 1 for the wide window,
+// whose three slots would spill at 16 waves per CU).
+template <int NG, int AHEAD>
+__global__ __launch_bounds__(kRecThreads) void wal_rec_lanes(RecArgs a, const DeviceTables* tabs) {
+  constexpr int ND = 4 * NG - 4;      // realigned dwords of the window
+  constexpr int NPAY = ND - 3;        // whole payload dwords folded from the window (payload at dword 2; one spare for the tail)
+  constexpr int RING = 4;             // offsets are fetched RING steps ahead of their granules
+  constexpr int DRING = AHEAD == 1 ? 2 : 4;
+  static_assert(AHEAD == 1 || AHEAD == 2, "granules one or two steps ahead");
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  dev::fill_lds_slicing(tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const dev::LaneConst kc = dev::lane_const(lane);
+  __syncthreads();
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves, n = a.n;
+  const std::uint64_t TS = (n + 63u) / 64u;
+  const std::uint64_t s0 = wave * TS / W;
+  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
+  if (ns == 0) return;
+  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
+  const std::uintptr_t glast = (w0 + a.size - 1u) & ~static_cast<std::uintptr_t>(15);  // the image's last granule
+  auto gran = [&](std::uintptr_t p) { return dev::gload16(p < glast ? p : glast); };
+
+  std::uint32_t d_off[RING];
+  auto fetch = [&](std::uint32_t j, int slot) {
+    const std::uint64_t b = (s0 + j) * 64u + lane;
+    d_off[slot] = a.off[b < n ? b : n - 1u];  // clamped: every load stays inside the array
+  };
+  uint4 q[DRING][NG];
+  std::uint32_t m_off[DRING];
+  auto issue = [&](int slot, int dslot) {
+    const std::uint32_t off = d_off[slot];
+    const std::uintptr_t al = (w0 + off) & ~static_cast<std::uintptr_t>(15);
+#pragma unroll
+    for (int i = 0; i < NG; ++i) q[dslot][i] = gran(al + 16u * i);
+    m_off[dslot] = off;
+  };
+  auto fold = [&](int slot, std::uint32_t j) {
+    const std::uint64_t b = (s0 + j) * 64u + lane;
+    const bool live = b < n;
+    const std::uint32_t off = m_off[slot];
+    const std::uintptr_t p = w0 + off;
+    std::uint32_t d[ND];
+    rec_dwords<NG>(q[slot], static_cast<std::uint32_t>(p & 15u), d);
+    const std::uint32_t rlen = d[0], stored = d[1];
+    const std::uint32_t klen = __builtin_amdgcn_alignbyte(d[5], d[4], 2u);
+    const std::uint32_t vlen = __builtin_amdgcn_alignbyte(d[6], d[5], 2u);
+    const std::uint64_t left = off < a.size ? a.size - off : 0u;
+    const bool len_ok = left >= kRecMeta && static_cast<std::uint64_t>(rlen) + 8u <= left;  // wal.cpp:68, :80
+    const std::uint32_t L = live && len_ok ? rlen : 0u;
+    std::uint32_t c = rec_fold<NPAY>(lds, kc, d + 2, L < 4u * NPAY ? L : 4u * NPAY, 0xFFFFFFFFu);
+    // payloads longer than the window: 64 bytes at a time from fresh granules, the register carried
+    for (std::uint32_t done = 4u * NPAY; __ballot(L > done) != 0; done += 64u) {
+      const std::uint32_t m = L > done ? std::min(L - done, 64u) : 0u;
+      const std::uintptr_t ps = p + 8u + done;
+      const std::uintptr_t al = ps & ~static_cast<std::uintptr_t>(15);
+      uint4 g[dev::kLaneGran];
+#pragma unroll
+      for (int i = 0; i < dev::kLaneGran; ++i) g[i] = gran(m ? al + 16u * i : glast);
+      std::uint32_t e[16];
+      dev::lane_dwords<1>(g, static_cast<std::uint32_t>(ps & 15u), e);
+      std::uint32_t e17[17];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) e17[k] = e[k];
+      e17[16] = 0u;
+      c = rec_fold<16>(lds, kc, e17, m, c);
+    }
+    const std::uint32_t crc = c ^ 0xFFFFFFFFu;
+    const bool kv_ok = static_cast<std::uint64_t>(klen) + vlen + (kRecMeta - 8u) <= rlen;  // wal.cpp:118-121
+    if (live && a.crc) a.crc[b] = len_ok ? crc : 0u;
+    if (live && (!len_ok || crc != stored || !kv_ok)) atomicMin(a.first_bad, static_cast<unsigned long long>(b));
+  };
+
+#pragma unroll
+  for (int k = 0; k < RING; ++k) fetch(k, k);
+#pragma unroll
+  for (int k = 0; k < AHEAD; ++k) {
+    issue(k, k % DRING);
+    fetch(k + RING, k);
+  }
+  for (std::uint32_t t = 0; t < ns; t += RING) {
+    dev::set_prio_from_left<3>(ns - t, ns);
+#pragma unroll
+    for (int k = 0; k < RING; ++k) {
+      const int ahead = (k + AHEAD) % RING;  // step t+k+AHEAD: its offset arrived RING steps ago
+      issue(ahead, (k + AHEAD) % DRING);
+      fetch(t + k + AHEAD + RING, ahead);
+      if (t + k < ns) fold(k % DRING, t + k);
+    }
+  }
+}
+
+int cu_count() {
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+}  // namespace
+}  // namespace tkv
+
+extern "C" int tkv_wal_check_records_device(const uint8_t* d_img, uint64_t size, const uint32_t* d_rec_off, uint64_t n,
+                                            uint32_t max_payload, uint32_t* d_crc, uint64_t* d_first_bad,
+                                            void* stream) {
+  using namespace tkv;
+  if (!d_first_bad || (n && (!d_img || !d_rec_off))) return set_error(TKV_INVALID_ARGUMENT, "null pointer");
+  if (size > 0xFFFFFFFFull + 1ull) return set_error(TKV_INVALID_ARGUMENT, "image larger than 4 GiB (u32 offsets)");
+  const DeviceTables* tabs = device_tables(kAlgoCrc32);
+  if (!tabs) return TKV_IO_ERROR;
+  const int ncu = cu_count();
+  if (ncu <= 0) return set_error(TKV_IO_ERROR, "no device");
+  auto st = static_cast<hipStream_t>(stream);
+  auto* fb = reinterpret_cast<unsigned long long*>(d_first_bad);
+  hipLaunchKernelGGL(rec_init, dim3(1), dim3(1), 0, st, fb, n);
+  if (n && size) {
+    const std::uint64_t steps = (n + 63) / 64;
+    const std::uint64_t grid = std::max<std::uint64_t>(
+        1, std::min<std::uint64_t>(static_cast<std::uint64_t>(ncu), (steps + 15) / 16));
+    RecArgs a{d_img, size, d_rec_off, n, d_crc, fb, static_cast<std::uint32_t>(grid * 16)};
+    // window: 6 granules hold the header and a payload of up to 64 bytes at any alignment, 8 up to 96
+    if (max_payload <= 64)
+      hipLaunchKernelGGL((wal_rec_lanes<6, 2>), dim3(static_cast<unsigned>(grid)), dim3(kRecThreads), 0, st, a, tabs);
+    else
+      hipLaunchKernelGGL((wal_rec_lanes<8, 1>), dim3(static_cast<unsigned>(grid)), dim3(kRecThreads), 0, st, a, tabs);
+  } else if (n) {
+    // an empty image: every record is corrupted (no header fits); the first is record 0
+    hipLaunchKernelGGL(rec_init, dim3(1), dim3(1), 0, st, fb, 0);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(TKV_IO_ERROR, hipGetErrorString(e));
+  return TKV_OK;
+}

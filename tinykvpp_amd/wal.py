@@ -87,6 +87,33 @@ def verify_device(image, size=None, stream=None):
     return ("ok" if rc == OK else "corrupted"), good.value, stop.value
 
 
+def check_records_device(image, rec_offsets, max_payload=64, crc_out=None, first_bad=None, stream=None):
+    """wal_entry::decode's per-record checks (wal.cpp:63-127) for records whose starts are known:
+    ``image`` a uint8 CUDA tensor, ``rec_offsets`` an int32/uint32 CUDA tensor of record start offsets
+    (u32; images up to 4 GiB). Returns (first_bad, crc): first_bad is a 1-element int64 CUDA tensor
+    holding the index of the first record that fails (len(rec_offsets) when none), crc an int32 CUDA
+    tensor of each payload's computed CRC (``crc_out`` if given). Asynchronous on ``stream``, like a
+    torch op issued there (tkv_wal_check_records_device)."""
+    import torch
+    from .crc32 import _check_data, _check_vec, _launch_stream
+    _check_data(image)
+    n = rec_offsets.numel()
+    if rec_offsets.dtype not in (torch.int32,):
+        raise ValueError("rec_offsets must be an int32 tensor (u32 offsets)")
+    _check_vec("rec_offsets", rec_offsets, torch.int32, n, image.device)
+    if crc_out is None:
+        crc_out = torch.empty(n, dtype=torch.int32, device=image.device)
+    _check_vec("crc_out", crc_out, torch.int32, n, image.device)
+    if first_bad is None:
+        first_bad = torch.empty(1, dtype=torch.int64, device=image.device)
+    _check_vec("first_bad", first_bad, torch.int64, 1, image.device)
+    check(load_library().tkv_wal_check_records_device(
+        ctypes.c_void_p(image.data_ptr()), image.numel(), ctypes.c_void_p(rec_offsets.data_ptr()), n,
+        int(max_payload), ctypes.c_void_p(crc_out.data_ptr()), ctypes.c_void_p(first_bad.data_ptr()),
+        _launch_stream(stream, image.device)))
+    return first_bad, crc_out
+
+
 def decode_fields(rec):
     """Header fields of one record (no checking): (record_len, crc, op, seq, tomb, key, value)."""
     record_len, crc = struct.unpack_from("<II", rec, 0)

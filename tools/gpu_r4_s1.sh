@@ -2,7 +2,7 @@ set -u
 O=$GRAFT_REPO_ROOT/gpurun_out/r4_s1
 mkdir -p $O
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -u -m pytest tests/test_gpu_stream.py tests/test_gpu_parity.py tests/test_gpu_lanes.py tests/test_gpu_fuzz.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_stream.py tests/test_gpu_parity.py tests/test_gpu_lanes.py tests/test_gpu_fuzz.py tests/test_gpu_wal_records.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u tools/ab_multi.py tools/ab/libtkv_r4base.so tinykvpp_amd/libtkv_crc32.so --rounds 10 --only cfg4 > $O/ab_finish.jsonl 2>&1
 rc=$?; echo "ab rc=$rc"; grep -v amdgpu $O/ab_finish.jsonl; [ $rc -eq 0 ] || exit $rc
