@@ -8,4 +8,6 @@ timeout -k 10 300 python -u tools/ab_multi.py tools/ab/libtkv_r4base.so tinykvpp
 rc=$?; echo "ab rc=$rc"; grep -v amdgpu $O/ab_finish.jsonl; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u tools/lane_probe.py tools/ab/libtkv_r4base.so tinykvpp_amd/libtkv_crc32.so --rounds 3 --reps 5 --only irregular > $O/probe_irregular.jsonl 2>&1
 rc=$?; echo "probe rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/rec_probe.py tinykvpp_amd/libtkv_crc32.so --rounds 3 --reps 5 > $O/rec_probe.jsonl 2>&1
+rc=$?; echo "rec rc=$rc"; grep -v amdgpu $O/rec_probe.jsonl | cut -c1-250; [ $rc -eq 0 ] || exit $rc
 bash tools/gpu_r4_lanepmc.sh r4_s1/lanepmc
