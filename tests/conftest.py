@@ -180,6 +180,27 @@ SMALL_MAX = 1024     # kSmallMax
 SCAN_TILE = 4096     # kScanTile
 GROUP_DENSE_TILE = 1024  # kGroupDenseTile
 GROUP_TILE_ROWS = 1024   # kGroupTileRows
+LANE_DENSE_TILE = 256    # kLaneDenseTile
+# group classes (lower bound exclusive, upper inclusive, tile threshold, phase bit): 4-, 8-, 16-lane passes
+GROUP_CLASSES = ((LANE_MAX, 256, 1024, 2), (256, 512, 1024, 4), (512, 1024, 2048, 8))
+
+
+def phases_expected(lens):
+    """The general path's phase bits the prepass publishes (tkv_debug_irregular_phases): per scan tile
+    of 4096 blocks, lane blocks (<= 64 B) when it holds at least 256 of them, and each group class when
+    it holds at least that class's threshold and at most GROUP_TILE_ROWS rows of blocks over SMALL_MAX."""
+    lens = np.asarray(lens, np.int64)
+    ph = 0
+    for t in range(0, lens.size, SCAN_TILE):
+        tl = lens[t:t + SCAN_TILE]
+        if np.count_nonzero(tl <= LANE_MAX) >= LANE_DENSE_TILE:
+            ph |= 1
+        big = tl[tl > SMALL_MAX]
+        if int(((big - 1) // 4096 + 1).sum()) <= GROUP_TILE_ROWS:
+            for lo, hi, thr, bit in GROUP_CLASSES:
+                if np.count_nonzero((tl > lo) & (tl <= hi)) >= thr:
+                    ph |= bit
+    return ph
 
 
 def stream_expected(offs, lens, group_stream=False):

@@ -12,7 +12,7 @@ import pytest
 import torch
 
 import tinykvpp_amd as tk
-from conftest import stream_expected
+from conftest import phases_expected, stream_expected
 
 pytestmark = pytest.mark.gpu
 
@@ -65,6 +65,10 @@ def irregular_mode():
     return tk.load_library().tkv_debug_irregular_mode(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
 
 
+def irregular_phases():
+    return tk.load_library().tkv_debug_irregular_phases(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+
 @pytest.mark.parametrize("seed", range(96))
 def test_irregular_random(gpu, oracle, seed):
     rng = np.random.default_rng(1000 + seed + OFFSET)
@@ -109,9 +113,15 @@ def test_irregular_dense_small_random(gpu, oracle, seed):
     n = int(rng.choice([4096, 5000, 9000, 20000, 4096 * 3 + 17]))
     p_lane = float(rng.choice([0.0, 0.05, 0.0625, 0.3, 0.9]))
     p_group = float(rng.choice([0.0, 0.2, 0.25, 0.3, 0.9]))
+    # the rest: 257-512 B (8-lane pass), 513-1024 B (16-lane pass) and 1025-3000 B, in shares around
+    # the passes' tile thresholds (1024 and 2048 of 4096)
+    mid = rng.choice([(0.0, 0.0), (0.25, 0.0), (0.3, 0.5), (0.0, 0.55), (0.45, 0.45)])
     u = rng.random(n)
+    v = rng.random(n)
+    rest = np.where(v < mid[0], rng.integers(257, 513, n),
+           np.where(v < mid[0] + mid[1], rng.integers(513, 1025, n), rng.integers(1025, 3000, n)))
     lens = np.where(u < p_lane, rng.integers(0, 65, n),
-           np.where(u < p_lane + p_group, rng.integers(65, 257, n), rng.integers(257, 3000, n)))
+           np.where(u < p_lane + p_group, rng.integers(65, 257, n), rest))
     nbig = int(rng.choice([0, 1, 3]))
     lens[rng.integers(0, n, nbig)] = rng.integers(1 << 20, 6 << 20, nbig)
     layout = ("gapped", "back_to_back", "overlapping")[seed % 3]
@@ -131,8 +141,11 @@ def test_irregular_dense_small_random(gpu, oracle, seed):
                              torch.from_numpy(lens.astype(np.int32)).to(gpu), init_raw=ini, algo=algo))
     want = oracle_batch(oracle, algo, host, offs, lens, init)
     bad = np.flatnonzero(got != want)
-    assert bad.size == 0, (f"{layout} n={n} lane={p_lane} group={p_group} big={nbig} shift={shift} algo={algo} "
-                           f"mode={irregular_mode()}: {bad.size} blocks differ, first {bad[:5]} (lens {lens[bad[:5]]})")
+    assert bad.size == 0, (f"{layout} n={n} lane={p_lane} group={p_group} mid={mid} big={nbig} shift={shift} "
+                           f"algo={algo} mode={irregular_mode()}: {bad.size} blocks differ, first {bad[:5]} "
+                           f"(lens {lens[bad[:5]]})")
+    if irregular_mode() == 0:
+        assert irregular_phases() == phases_expected(lens)
 
 
 @pytest.mark.parametrize("seed", range(64))

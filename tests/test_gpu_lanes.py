@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 import tinykvpp_amd as tk
+from conftest import phases_expected
 
 pytestmark = pytest.mark.gpu
 
@@ -230,6 +231,36 @@ def test_irregular_more_than_1024_tiles(gpu, oracle, shape):
         init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
         got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))
         assert np.array_equal(got, oracle.batch(host, offs, lens, init))
+
+
+def phases():
+    """General-path phases of the last irregular batch: 1 lane, 2/4/8 the 4/8/16-lane group passes."""
+    return tk.load_library().tkv_debug_irregular_phases(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+
+@pytest.mark.parametrize("sizes", [(257,), (300,), (512,), tuple(range(257, 513)), (513,), (700, 1000),
+                                   tuple(range(513, 1025)), (1024,), tuple(range(257, 1025))])
+@pytest.mark.parametrize("base", [0, 5, 8])
+def test_irregular_group8_16_blocks(gpu, oracle, buf, sizes, base):
+    """Irregular blocks of 257-1024 bytes in dense tiles (WAL payloads with mid-size values) are folded by
+    the 8-lane (257-512 B, 512-byte slots) and 16-lane (513-1024 B, 1 KiB slots) group passes: every
+    length at every base alignment, gapped, with per-block initial registers and CRC-32C."""
+    host, d = buf
+    rng = np.random.default_rng(sum(sizes) + base)
+    n = min(60_000, (host.size - 64) // (max(sizes) + 8))
+    offs, lens = wal_payloads(rng, n, sizes, base)
+    o, ln = torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu)
+    got = u32(tk.crc32_batch(d, o, ln))
+    assert mode() == 0
+    assert phases() == phases_expected(lens)
+    assert phases() & 12 != 0
+    assert np.array_equal(got, oracle.batch(host, offs, lens))
+    init = rng.integers(0, 2**32, offs.size, dtype=np.uint64).astype(np.uint32)
+    got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))
+    assert np.array_equal(got, oracle.batch(host, offs, lens, init))
+    m = 5000
+    got = u32(tk.crc32_batch(d, o[:m].contiguous(), ln[:m].contiguous(), algo="crc32c"))
+    assert np.array_equal(got, oracle_c(oracle, host, offs[:m], lens[:m]))
 
 
 @pytest.mark.parametrize("sizes", [(65,), (100, 128, 200), tuple(range(65, 257)), (256,)])

@@ -1654,18 +1654,24 @@ __device__ __forceinline__ void lane_phase(const RowsArgs& a, const std::uint32_
   }
 }
 
-// Group blocks of an irregular batch (kLaneMax < len <= kGroupMax, in a dense tile): a 4-lane group
-// folds one block right-aligned in a 256-byte slot (crc_packed_small_gen's layout at G = 4), 16 blocks
-// per wave step, walked straight from the caller's offsets and lengths over the same block range and
-// pipeline as lane_phase (other groups idle). Lane g loads the five granules covering its 64 bytes
-// and realigns them (lane_dwords); granules holding no byte of the block read the zero buffer and
-// the bytes in front of the block are masked. Lane shifts are column 60 + g of the LDS image
-// (Shift_{(3-g)*64}); the init term is Shift_len(init), from init_shift[len] for the default
-// register, or spread over the group (8 bits per lane, head_shift[len]) for per-block registers;
-// the group's sum comes from the first two DPP steps of the wave reduction.
+// Group blocks of an irregular batch (in tiles dense in their class): a G-lane group folds one block
+// right-aligned in a 64 G-byte slot (crc_packed_small_gen's layout), 64/G blocks per wave step, walked
+// straight from the caller's offsets and lengths over the same block range and pipeline as lane_phase
+// (other groups idle). G = 4 takes blocks of kLaneMax + 1 .. kGroupMax bytes, G = 8 up to kGroup8Max,
+// G = 16 up to kGroup16Max, each pass only the blocks of its class in tiles flagged for it. Lane g
+// loads the five granules covering its 64 bytes and realigns them (lane_dwords); granules holding no
+// byte of the block read the zero buffer and the bytes in front of the block are masked. Lane shifts
+// are column 64 - G + g of the LDS image (Shift_{(G-1-g)*64}); the init term is Shift_len(init), from
+// init_shift[len] for the default register, or spread over the group (32/G bits per lane,
+// head_shift[len]) for per-block registers; the group's sum comes from the first log2(G) DPP steps of
+// the wave reduction.
+template <int G>
 __device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32_t* lds) {
+  static_assert(G == 4 || G == 8 || G == 16, "4-, 8- or 16-lane groups");
   constexpr int RING = 4;
-  constexpr std::uint32_t G = 4, kSlot = 64u * G;
+  constexpr std::uint32_t kSlot = 64u * G;
+  constexpr std::uint32_t kLo = G == 4 ? kLaneMax : G == 8 ? kGroupMax : kGroup8Max;  // the class: (kLo, kSlot]
+  constexpr std::uint32_t kFlag = G == 4 ? kTileGroups : G == 8 ? kTileGroups8 : kTileGroups16;
   const std::uint32_t lane = threadIdx.x & 63u, gl = lane % G, grp = lane / G;
   LaneConst kc = lane_const(lane);
   kc.lsbase = kLdsLaneBase + (64u - G + gl) * 4u;
@@ -1692,7 +1698,7 @@ __device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32
   auto issue = [&](int slot, std::uint32_t j) {
     const std::uint64_t b = b0 + kPer * static_cast<std::uint64_t>(j) + grp;
     const std::uint32_t len0 = d_len[slot];
-    const bool live = j < ns && b < b1 && len0 > kLaneMax && len0 <= kGroupMax && (a.l_tile[b / 4096u] & kTileGroups);
+    const bool live = j < ns && b < b1 && len0 > kLo && len0 <= kSlot && (a.l_tile[b / 4096u] & kFlag);
     const std::uint32_t len = live ? len0 : 0u;
     const std::uintptr_t blo = base + d_off[slot], bhi = blo + len;
     const std::int32_t c_lane = static_cast<std::int32_t>(len) - static_cast<std::int32_t>(kSlot) +
@@ -1737,8 +1743,7 @@ __device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32
     } else if (gl == 0u) {
       v ^= m_ishift[slot];
     }
-    v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    v ^= __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]: group sum
+    v = group_xor<G>(v);  // every lane of the group holds the group's sum
     if (live && gl == G - 1u) a.out[b0 + kPer * static_cast<std::uint64_t>(j) + grp] = v ^ a.out_xor;
   };
 

@@ -81,7 +81,7 @@ void build_tables(DeviceTables* t, std::uint32_t poly) {
   const auto x8n = [poly](std::uint64_t n) { return x8nmodp(n, poly); };
   t->poly = poly;
   t->pad_[0] = t->pad_[1] = 0;
-  for (std::uint32_t h = 0; h <= kGroupMax; ++h) t->init_shift[h] = mm(x8n(h), 0xFFFFFFFFu);
+  for (std::uint32_t h = 0; h <= kGroup16Max; ++h) t->init_shift[h] = mm(x8n(h), 0xFFFFFFFFu);
   for (std::uint32_t i = 0; i < 256; ++i) {
     std::uint32_t c = i;
     for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? poly : 0u);
@@ -1349,17 +1349,23 @@ int tkv_debug_multi_combine(uint32_t poly, int ndev, const uint64_t* h_offsets, 
   return TKV_OK;
 }
 
-int tkv_debug_irregular_mode(void* stream) {
+namespace {
+int read_count_word(void* stream, int word) {
   DevCtx* c = nullptr;
   if (get_ctx(&c)) return -1;
   StreamScratch* s = nullptr;
   if (get_scratch(c, stream, 0, &s)) return -1;
-  std::uint32_t mode = 0;
+  std::uint32_t v = 0;
   if (hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess ||
-      hipMemcpy(&mode, s->counts + 3, 4, hipMemcpyDeviceToHost) != hipSuccess)
+      hipMemcpy(&v, s->counts + word, 4, hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
-  return static_cast<int>(mode);
+  return static_cast<int>(v);
 }
+}  // namespace
+
+int tkv_debug_irregular_mode(void* stream) { return read_count_word(stream, 3); }
+
+int tkv_debug_irregular_phases(void* stream) { return read_count_word(stream, kCountPhases); }
 
 int tkv_debug_set_host_mapped(int enable) { return tkv::g_host_mapped.exchange(enable ? 1 : 0); }
 

@@ -125,16 +125,18 @@ constexpr int kStreamSkew = 154;
 __global__ __launch_bounds__(kStreamThreads) void crc_stream(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   if (dev::sload32(a.counts, 3) != kModeStream) {
-    // General path: this launch folds the batch's lane and group blocks (len <= kGroupMax, DESIGN.md
+    // General path: this launch folds the batch's lane and group blocks (len <= kGroup16Max, DESIGN.md
     // §4.5), each phase only if the prepass found its blocks; crc_rows follows with the rest. The
-    // group phase (column 60 + g) needs the lane-shift tables, the lane phase not.
+    // group passes (lane-shift column 64 - G + g) need the lane-shift tables, the lane phase not.
     const std::uint32_t ph = dev::sload32(a.counts, kCountPhases);
     if (ph == 0) return;
-    if (ph & 2u) dev::fill_lds(a.tabs, lds);
+    if (ph & 14u) dev::fill_lds(a.tabs, lds);
     else dev::fill_lds_slicing(a.tabs, lds);
     __syncthreads();  // (the mode and ph are the same for the whole grid)
     if (ph & 1u) dev::lane_phase(a, lds);
-    if (ph & 2u) dev::group_phase(a, lds);
+    if (ph & 2u) dev::group_phase<4>(a, lds);
+    if (ph & 4u) dev::group_phase<8>(a, lds);
+    if (ph & 8u) dev::group_phase<16>(a, lds);
     return;
   }
   dev::fill_lds(a.tabs, lds);
@@ -264,8 +266,8 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   constexpr unsigned kTileBpt = kScanTile / kTileThreads;
   static_assert(kScanTile % kTileThreads == 0 && kTileWaves >= 1 && kTileBpt >= 4 && kTileBpt % 4 == 0,
                 "tile shape");
-  __shared__ std::uint64_t wsum[kTileWaves];
-  __shared__ std::uint32_t lsum[kTileWaves], wok[kTileWaves];
+  __shared__ std::uint64_t wsum[kTileWaves], lsum[kTileWaves];
+  __shared__ std::uint32_t wok[kTileWaves];
   // stream mode's wave partition (used only if the prepass picks stream mode): row0[0..Ws], grid-stride
   for (std::uint32_t w = blockIdx.x * kTileThreads + threadIdx.x; w <= Ws; w += gridDim.x * kTileThreads) {
     const std::uint64_t TR = stream_geometry(sbase, offsets, lengths, n).rows;
@@ -273,12 +275,13 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   }
   const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * kTileBpt;
   const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  // Every block first counts as a small or large one (v); lane and group blocks are also counted in
-  // one packed u32 (lane blocks in the low 16 bits, group blocks in the high 16: a tile has at most
-  // 4096), so the one scan below yields both, and the tile's verdict on them (below) only subtracts.
-  std::uint32_t pk[kTileBpt];
+  // Every block first counts as a small or large one (v); lane blocks and the three group classes
+  // are also counted in one packed u64 (16 bits each, lane blocks lowest, then 4-, 8- and 16-lane
+  // group blocks: a tile has at most 4096 of each), so the one scan below yields all of them, and
+  // the tile's verdict on them (below) only subtracts.
+  std::uint64_t pk[kTileBpt];
   std::uint64_t v[kTileBpt], s = 0;
-  std::uint32_t ls = 0;
+  std::uint64_t ls = 0;
   // Loads at clamped indices, all issued before any is used (n >= 1 here): one round trip for the
   // lengths, one more for the offsets, which only a thread whose blocks are all long enough for stream
   // mode reads (a lane-block batch never touches them).
@@ -293,7 +296,12 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   for (unsigned i = 0; i < kTileBpt; ++i) {
     const bool in = base + i < n;
     len[i] = in ? len[i] : 0u;
-    pk[i] = !in ? 0u : len[i] <= kLaneMax ? 1u : len[i] <= kGroupMax ? 0x10000u : 0u;
+    pk[i] = !in                    ? 0ull
+            : len[i] <= kLaneMax    ? 1ull
+            : len[i] <= kGroupMax   ? 1ull << 16
+            : len[i] <= kGroup8Max  ? 1ull << 32
+            : len[i] <= kGroup16Max ? 1ull << 48
+                                    : 0ull;
     v[i] = in ? scan_item(len[i]) : 0ull;
     s += v[i];
     ls += pk[i];
@@ -309,13 +317,13 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   // Inclusive scans of the thread sums inside the wave (cross-lane shifts, no barriers), then the
   // wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
   std::uint64_t inc = s;
-  std::uint32_t linc = ls;
+  std::uint64_t linc = ls;
 #pragma unroll
   for (unsigned off = 1; off < 64; off <<= 1) {
     const std::uint64_t y = __shfl_up(inc, off, 64);
-    const std::uint32_t ly = __shfl_up(linc, off, 64);
+    const std::uint64_t ly = __shfl_up(linc, off, 64);
     inc += lane >= off ? y : 0ull;
-    linc += lane >= off ? ly : 0u;
+    linc += lane >= off ? ly : 0ull;
   }
   const bool wave_ok = __ballot(!ok) == 0;
   if (lane == 63u) {
@@ -324,28 +332,34 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     wok[wid] = wave_ok ? 1u : 0u;
   }
   __syncthreads();
-  std::uint64_t wpre = 0, tot = 0;
-  std::uint32_t lpre = 0, ltot = 0, all_ok = 1;
+  std::uint64_t wpre = 0, tot = 0, lpre = 0, ltot = 0;
+  std::uint32_t all_ok = 1;
 #pragma unroll
   for (unsigned w = 0; w < kTileWaves; ++w) {
     const std::uint64_t t = wsum[w];
-    const std::uint32_t lt = lsum[w];
+    const std::uint64_t lt = lsum[w];
     wpre += w < wid ? t : 0ull;
     tot += t;
-    lpre += w < wid ? lt : 0u;
+    lpre += w < wid ? lt : 0ull;
     ltot += lt;
     all_ok &= wok[w];
   }
-  // A tile with at least kLaneDenseTile lane blocks leaves them to the lane phase (in no list), one
-  // with at least kGroupDenseTile group blocks and at most kGroupTileRows rows of large blocks those
-  // to the group phase; in other tiles they are listed as small blocks, so a batch with a few of them
-  // scattered about pays no phase walk over its metadata.
-  const std::uint32_t tph = ((ltot & 0xFFFFu) >= kLaneDenseTile ? kTileLanes : 0u) |
-                            ((ltot >> 16) >= kGroupDenseTile && (tot >> 32) <= kGroupTileRows ? kTileGroups : 0u);
-  const std::uint32_t tmask = ((tph & kTileLanes) ? 0xFFFFu : 0u) | ((tph & kTileGroups) ? 0xFFFF0000u : 0u);
-  auto taken = [&](std::uint32_t x) {  // the phase blocks among packed counts x
+  // A tile with at least kLaneDenseTile lane blocks leaves them to the lane phase (in no list); one
+  // with at most kGroupTileRows rows of large blocks leaves each group class of which it holds at
+  // least that class's threshold to that class's group pass; in other tiles they are listed as small
+  // blocks, so a batch with a few of them scattered about pays no phase walk over its metadata.
+  const bool few_rows = (tot >> 32) <= kGroupTileRows;
+  auto cls = [&](int c) { return static_cast<std::uint32_t>((ltot >> (16 * c)) & 0xFFFFu); };
+  const std::uint32_t tph = (cls(0) >= kLaneDenseTile ? kTileLanes : 0u) |
+                            (few_rows && cls(1) >= kGroupDenseTile ? kTileGroups : 0u) |
+                            (few_rows && cls(2) >= kGroup8DenseTile ? kTileGroups8 : 0u) |
+                            (few_rows && cls(3) >= kGroup16DenseTile ? kTileGroups16 : 0u);
+  const std::uint64_t tmask = ((tph & kTileLanes) ? 0xFFFFull : 0ull) | ((tph & kTileGroups) ? 0xFFFFull << 16 : 0ull) |
+                              ((tph & kTileGroups8) ? 0xFFFFull << 32 : 0ull) |
+                              ((tph & kTileGroups16) ? 0xFFFFull << 48 : 0ull);
+  auto taken = [&](std::uint64_t x) {  // the phase blocks among packed counts x
     x &= tmask;
-    return (x & 0xFFFFu) + (x >> 16);
+    return static_cast<std::uint32_t>((x & 0xFFFFu) + ((x >> 16) & 0xFFFFu) + ((x >> 32) & 0xFFFFu) + (x >> 48));
   };
   // A tile dense in group blocks does not qualify for stream mode (unless group_stream, a debug
   // setting): the group phase folds 65-256-byte blocks at the rate of gapped ones, where the stream
@@ -354,7 +368,7 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   const bool stream_ok = all_ok && (group_stream != 0u || (tph & kTileGroups) == 0u);
   if (threadIdx.x == 0) tile_ok[blockIdx.x] = (stream_ok ? kTileStream : 0u) | tph;
   std::uint64_t run = wpre + inc - s;  // exclusive, lane and group blocks counted as small
-  std::uint32_t lrun = lpre + linc - ls;
+  std::uint64_t lrun = lpre + linc - ls;
   if (tph == 0 && base + kTileBpt <= n) {
     // every block of such a tile is listed: this thread's entries as whole 16-byte stores
     // (scan and lscan are 256-byte aligned scratch, base a multiple of kTileBpt >= 4)
@@ -404,11 +418,11 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
   if (threadIdx.x == 0) sph = 0;  // (the loop's first barrier orders this before the ORs below)
   std::uint64_t carry = 0, lcarry = 0;
   bool all_stream = true;
-  std::uint32_t ph = 0;  // kTileLanes | kTileGroups over the tiles
+  std::uint32_t ph = 0;  // kTilePhases flags over the tiles
   for (std::uint32_t t0 = 0; t0 < ntiles; t0 += 1024) {
     const std::uint32_t i = t0 + threadIdx.x;
     all_stream = all_stream && (i >= ntiles || (tile_ok[i] & kTileStream) != 0);
-    ph |= i < ntiles ? tile_ok[i] & (kTileLanes | kTileGroups) : 0u;
+    ph |= i < ntiles ? tile_ok[i] & kTilePhases : 0u;
     const std::uint64_t x = i < ntiles ? tile_sums[i] : 0ull;
     const std::uint32_t lx = i < ntiles ? tile_lanes[i] : 0u;
     part[threadIdx.x] = x;
@@ -564,7 +578,7 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
   const std::uint32_t lsc = live ? o.lscan[b] : 0u;
   const std::uint32_t mtk = tile_ok[my_tile];
   std::uint64_t before = 0, all = 0, bad = 0, lbefore = 0, lall = 0;
-  std::uint32_t ph = 0;  // kTileLanes | kTileGroups over the tiles
+  std::uint32_t ph = 0;  // kTilePhases flags over the tiles
   for (std::uint32_t i = threadIdx.x; i < ntiles; i += kFinishThreads) {
     const std::uint64_t v = tile_sums[i];
     const std::uint64_t lv = o.tile_lanes[i];
@@ -574,7 +588,7 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     lall += lv;
     lbefore += i < my_tile ? lv : 0ull;
     bad += (tk & kTileStream) ? 0u : 1u;
-    ph |= tk & (kTileLanes | kTileGroups);
+    ph |= tk & kTilePhases;
   }
   // Wave sums by cross-lane exchange, then the kWaves partial sums through LDS (one barrier).
 #pragma unroll
