@@ -10,4 +10,6 @@ timeout -k 10 300 python -u tools/lane_probe.py tools/ab/libtkv_r4base.so tinykv
 rc=$?; echo "probe rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u tools/rec_probe.py tinykvpp_amd/libtkv_crc32.so --rounds 3 --reps 5 > $O/rec_probe.jsonl 2>&1
 rc=$?; echo "rec rc=$rc"; grep -v amdgpu $O/rec_probe.jsonl | cut -c1-250; [ $rc -eq 0 ] || exit $rc
-bash tools/gpu_r4_lanepmc.sh r4_s1/lanepmc
+timeout -k 10 300 python -u tools/walk_probe.py --rounds 3 > $O/walk_probe.jsonl 2>&1
+rc=$?; echo "walk rc=$rc"; grep -v amdgpu $O/walk_probe.jsonl | cut -c1-250
+exit $rc
