@@ -149,8 +149,9 @@ int tkv_wal_verify_device(const uint8_t *d_wal, uint64_t size, uint64_t *n_good,
  * lengths array, no prepass. *d_first_bad (device memory) = the index of the first record failing a
  * check, n when every record passes. d_crc (nullable, device): the computed finalized CRC of every
  * payload (0 for a record whose length check failed). max_payload is a dispatch hint (the longest
- * record_len the caller expects: up to 68 bytes one lane reads the record in 6 granules, above 8);
- * longer payloads are still checked exactly. Asynchronous on `stream`. */
+ * record_len the caller expects: one lane reads each record in a window of 4-8 16-byte granules sized
+ * for it, 36-byte payloads in 4, up to 102 bytes in 8); longer payloads are still checked exactly,
+ * 64 bytes at a time. Asynchronous on `stream`. */
 int tkv_wal_check_records_device(const uint8_t *d_img, uint64_t size, const uint32_t *d_rec_off, uint64_t n,
                                  uint32_t max_payload, uint32_t *d_crc, uint64_t *d_first_bad, void *stream);
 

@@ -102,7 +102,7 @@ def test_golden_records(gpu, oracle):
         assert crc.tolist() == [r["crc"] for r in golden("wal.json")["records"]]
 
 
-@pytest.mark.parametrize("max_payload", [64, 100, 1024])
+@pytest.mark.parametrize("max_payload", [36, 50, 64, 80, 100, 1024])
 @pytest.mark.parametrize("shift", [0, 3, 8, 13])
 def test_small_records_every_alignment(gpu, oracle, max_payload, shift):
     rng = np.random.default_rng(shift * 7 + max_payload)
@@ -138,7 +138,7 @@ def test_every_payload_length(gpu, oracle):
     s32 = sizes.astype(np.uint32)
     tk.check(tk.load_library().tkv_wal_stamp(ctypes.c_void_p(img.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
                                              ctypes.c_void_p(s32.ctypes.data), n))
-    for mp in (64, 100, 300):
+    for mp in (36, 64, 80, 100, 300):
         assert check(oracle, img, offs, mp, 1) == n
 
 

@@ -209,11 +209,18 @@ extern "C" int tkv_wal_check_records_device(const uint8_t* d_img, uint64_t size,
     const std::uint64_t grid = std::max<std::uint64_t>(
         1, std::min<std::uint64_t>(static_cast<std::uint64_t>(ncu), (steps + 15) / 16));
     RecArgs a{d_img, size, d_rec_off, n, d_crc, fb, static_cast<std::uint32_t>(grid * 16)};
-    // window: 6 granules hold the header and a payload of up to 64 bytes at any alignment, 8 up to 96
-    if (max_payload <= 64)
-      hipLaunchKernelGGL((wal_rec_lanes<6, 2>), dim3(static_cast<unsigned>(grid)), dim3(kRecThreads), 0, st, a, tabs);
-    else
-      hipLaunchKernelGGL((wal_rec_lanes<8, 1>), dim3(static_cast<unsigned>(grid)), dim3(kRecThreads), 0, st, a, tabs);
+    // window: NG granules hold the header, the key/value lengths and a payload of up to 16 NG - 26 bytes
+    // at any alignment (36-byte payloads: 4 granules; 64: 6; 100: 8); longer ones continue 64 bytes at
+    // a time. Wider windows keep one step of granules in flight instead of two (registers).
+    const std::uint32_t ng = std::min<std::uint32_t>(8u, std::max<std::uint32_t>(4u, (std::min<std::uint32_t>(max_payload, 1024u) + 26u + 15u) / 16u));
+    const dim3 g(static_cast<unsigned>(grid)), b(kRecThreads);
+    switch (ng) {
+      case 4: hipLaunchKernelGGL((wal_rec_lanes<4, 2>), g, b, 0, st, a, tabs); break;
+      case 5: hipLaunchKernelGGL((wal_rec_lanes<5, 2>), g, b, 0, st, a, tabs); break;
+      case 6: hipLaunchKernelGGL((wal_rec_lanes<6, 2>), g, b, 0, st, a, tabs); break;
+      case 7: hipLaunchKernelGGL((wal_rec_lanes<7, 1>), g, b, 0, st, a, tabs); break;
+      default: hipLaunchKernelGGL((wal_rec_lanes<8, 1>), g, b, 0, st, a, tabs); break;
+    }
   } else if (n) {
     // an empty image: every record is corrupted (no header fits); the first is record 0
     hipLaunchKernelGGL(rec_init, dim3(1), dim3(1), 0, st, fb, 0);
