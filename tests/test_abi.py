@@ -39,6 +39,20 @@ def test_no_gpu_is_an_error_not_a_fallback(lib):
     assert e.value.code == 2  # io_error: no device, and no CPU path to fall back to
 
 
+def test_record_check_arguments_without_a_gpu(lib):
+    """tkv_wal_check_records_device: null pointers and images over 4 GiB (u32 offsets) are invalid
+    arguments, checked before any device work; with valid arguments and no GPU it is an I/O error,
+    never a CPU fallback."""
+    import torch
+    f = lib.tkv_wal_check_records_device
+    dummy = ctypes.c_void_p(16)  # never dereferenced
+    assert f(dummy, 100, dummy, 5, 64, None, None, None) == 3          # no first_bad
+    assert f(None, 100, dummy, 5, 64, None, dummy, None) == 3          # no image
+    assert f(dummy, (1 << 32) + 2, dummy, 5, 64, None, dummy, None) == 3  # over 4 GiB
+    if not torch.cuda.is_available():
+        assert f(dummy, 100, dummy, 5, 64, None, dummy, None) == 2       # io_error: no device
+
+
 def test_oversize_irregular_batch_is_rejected(lib):
     """Irregular batches carry u32 block indices; a count the prepass cannot index (within one scan
     tile of 2^32) is an invalid argument, checked before any device work (no GPU needed)."""
