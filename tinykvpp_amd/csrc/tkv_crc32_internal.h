@@ -156,6 +156,7 @@ constexpr std::uint32_t kTileGroups = 4u;     // its blocks of kLaneMax + 1 .. k
 constexpr std::uint32_t kTileGroups8 = 8u;    // kGroupMax + 1 .. kGroup8Max: the 8-lane pass's
 constexpr std::uint32_t kTileGroups16 = 16u;  // kGroup8Max + 1 .. kGroup16Max: the 16-lane pass's
 constexpr std::uint32_t kTilePhases = kTileLanes | kTileGroups | kTileGroups8 | kTileGroups16;
+constexpr std::uint32_t kTileAllTaken = 32u;  // every block of the tile is a lane or group phase's: no scatter
 
 // Whether block of length len in a tile with flags tk is folded by the lane or a group pass (and is
 // in no prepass list).

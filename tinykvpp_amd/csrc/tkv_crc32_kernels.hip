@@ -366,7 +366,9 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   // walk's rows of 16-64 block ends ran at about 0.6 of it (back-to-back 128 B: 1404 against 2351
   // GB/s, profiles/r3/group_phase/). Longer blocks keep stream mode, where it wins (cfg4, 64 KiB).
   const bool stream_ok = all_ok && (group_stream != 0u || (tph & kTileGroups) == 0u);
-  if (threadIdx.x == 0) tile_ok[blockIdx.x] = (stream_ok ? kTileStream : 0u) | tph;
+  const std::uint64_t tile_n = n - static_cast<std::uint64_t>(blockIdx.x) * kScanTile;  // blocks in the tile
+  const bool all_taken = taken(ltot) == (tile_n < kScanTile ? tile_n : kScanTile);
+  if (threadIdx.x == 0) tile_ok[blockIdx.x] = (stream_ok ? kTileStream : 0u) | tph | (all_taken ? kTileAllTaken : 0u);
   std::uint64_t run = wpre + inc - s;  // exclusive, lane and group blocks counted as small
   std::uint64_t lrun = lpre + linc - ls;
   if (tph == 0 && base + kTileBpt <= n) {
@@ -515,13 +517,16 @@ __global__ void rows_finish(const std::uint8_t* base, const std::uint64_t* offse
                             const std::uint32_t* row0) {
   const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
   if (b >= n) return;
+  const bool stream = dev::sload32(counts, 3) == kModeStream;  // rows_scan_tiles found every tile back to back
+  // (launched with 256 threads: a workgroup lies in one scan tile, so its flags are one scalar load)
+  const std::uint64_t t = b / kScanTile;
+  const std::uint32_t tk = stream ? 0u : dev::sload32(tile_ok, static_cast<std::uint32_t>(blockIdx.x / (kScanTile / 256u)));
+  if (tk & kTileAllTaken) return;  // every block of the tile is the lane or a group phase's: nothing to list
   const std::uint32_t len = lengths[b];
-  if (dev::sload32(counts, 3) == kModeStream) {  // rows_scan_tiles found every tile back to back
+  if (stream) {
     stream_block(base, offsets, lengths, n, b, offsets[b], len, Ws, row0, counts, ends, sinfo, o.wave_start);
     return;
   }
-  const std::uint64_t t = b / kScanTile;
-  const std::uint32_t tk = tile_ok[t];
   if (phase_block(len, tk)) return;  // the lane or group phase's
   finish_block(offsets[b], len, b, scan[b] + tile_offs[t], o.lscan[b] + o.tile_lanes[t], counts[2], o, W, out, tk);
 }
