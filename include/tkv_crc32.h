@@ -277,8 +277,8 @@ void tkv_debug_wal_last(uint64_t out[4]);
  * the stream. */
 int tkv_debug_irregular_mode(void *stream);
 /* Which of crc_stream's general-path phases the last irregular batch on `stream` ran (0 in stream
- * mode): bit 0 the lane phase (blocks <= 64 B), bits 1 / 2 / 3 the 4- / 8- / 16-lane group passes
- * (65-256 / 257-512 / 513-1024 B); -1 on error. Synchronizes the stream. */
+ * mode): bit 0 the lane phase (blocks <= 64 B), bits 1 / 2 the 4- / 8-lane group passes (65-256 /
+ * 257-512 B); -1 on error. Synchronizes the stream. */
 int tkv_debug_irregular_phases(void *stream);
 /* Host batches from pinned host memory are read in place by the kernels (zero copy) unless this is
  * 0 (then they take the staged copy pipeline, as pageable memory does). Returns the previous

@@ -181,8 +181,8 @@ SCAN_TILE = 4096     # kScanTile
 GROUP_DENSE_TILE = 1024  # kGroupDenseTile
 GROUP_TILE_ROWS = 1024   # kGroupTileRows
 LANE_DENSE_TILE = 256    # kLaneDenseTile
-# group classes (lower bound exclusive, upper inclusive, tile threshold, phase bit): 4-, 8-, 16-lane passes
-GROUP_CLASSES = ((LANE_MAX, 256, 1024, 2), (256, 512, 1024, 4), (512, 1024, 2048, 8))
+# group classes (lower bound exclusive, upper inclusive, tile threshold, phase bit): 4- and 8-lane passes
+GROUP_CLASSES = ((LANE_MAX, 256, 1024, 2), (256, 512, 2048, 4))
 
 
 def phases_expected(lens):

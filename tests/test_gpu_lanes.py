@@ -241,10 +241,11 @@ def phases():
 @pytest.mark.parametrize("sizes", [(257,), (300,), (512,), tuple(range(257, 513)), (513,), (700, 1000),
                                    tuple(range(513, 1025)), (1024,), tuple(range(257, 1025))])
 @pytest.mark.parametrize("base", [0, 5, 8])
-def test_irregular_group8_16_blocks(gpu, oracle, buf, sizes, base):
-    """Irregular blocks of 257-1024 bytes in dense tiles (WAL payloads with mid-size values) are folded by
-    the 8-lane (257-512 B, 512-byte slots) and 16-lane (513-1024 B, 1 KiB slots) group passes: every
-    length at every base alignment, gapped, with per-block initial registers and CRC-32C."""
+def test_irregular_group8_and_small_blocks(gpu, oracle, buf, sizes, base):
+    """Irregular blocks of 257-1024 bytes (WAL payloads with mid-size values): the 8-lane group pass
+    (257-512 B, 512-byte slots) in tiles at least half of whose blocks are in its class, the listed
+    small phase (1 KiB slots) otherwise: every length at every base alignment, gapped, with per-block
+    initial registers and CRC-32C."""
     host, d = buf
     rng = np.random.default_rng(sum(sizes) + base)
     n = min(60_000, (host.size - 64) // (max(sizes) + 8))
@@ -253,7 +254,8 @@ def test_irregular_group8_16_blocks(gpu, oracle, buf, sizes, base):
     got = u32(tk.crc32_batch(d, o, ln))
     assert mode() == 0
     assert phases() == phases_expected(lens)
-    assert phases() & 12 != 0
+    if lens.max() <= 512:
+        assert phases() == 4  # the 8-lane pass ran
     assert np.array_equal(got, oracle.batch(host, offs, lens))
     init = rng.integers(0, 2**32, offs.size, dtype=np.uint64).astype(np.uint32)
     got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))

@@ -150,6 +150,7 @@ def test_corruptions(gpu, oracle, kind):
     rng = np.random.default_rng(sum(map(ord, kind)))
     img, offs, size = make_wal_small(rng, 30_000)
     offs = offs.astype(np.int64)
+    size = size.astype(np.int64)
     i = int(rng.integers(100, offs.size - 100))
     want = i
     if kind == "payload_bit":

@@ -1658,7 +1658,7 @@ __device__ __forceinline__ void lane_phase(const RowsArgs& a, const std::uint32_
 // right-aligned in a 64 G-byte slot (crc_packed_small_gen's layout), 64/G blocks per wave step, walked
 // straight from the caller's offsets and lengths over the same block range and pipeline as lane_phase
 // (other groups idle). G = 4 takes blocks of kLaneMax + 1 .. kGroupMax bytes, G = 8 up to kGroup8Max,
-// G = 16 up to kGroup16Max, each pass only the blocks of its class in tiles flagged for it. Lane g
+// each pass only the blocks of its class in tiles flagged for it. Lane g
 // loads the five granules covering its 64 bytes and realigns them (lane_dwords); granules holding no
 // byte of the block read the zero buffer and the bytes in front of the block are masked. Lane shifts
 // are column 64 - G + g of the LDS image (Shift_{(G-1-g)*64}); the init term is Shift_len(init), from
@@ -1667,11 +1667,11 @@ __device__ __forceinline__ void lane_phase(const RowsArgs& a, const std::uint32_
 // the wave reduction.
 template <int G>
 __device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32_t* lds) {
-  static_assert(G == 4 || G == 8 || G == 16, "4-, 8- or 16-lane groups");
+  static_assert(G == 4 || G == 8, "4- or 8-lane groups");
   constexpr int RING = 4;
   constexpr std::uint32_t kSlot = 64u * G;
-  constexpr std::uint32_t kLo = G == 4 ? kLaneMax : G == 8 ? kGroupMax : kGroup8Max;  // the class: (kLo, kSlot]
-  constexpr std::uint32_t kFlag = G == 4 ? kTileGroups : G == 8 ? kTileGroups8 : kTileGroups16;
+  constexpr std::uint32_t kLo = G == 4 ? kLaneMax : kGroupMax;  // the class: (kLo, kSlot]
+  constexpr std::uint32_t kFlag = G == 4 ? kTileGroups : kTileGroups8;
   const std::uint32_t lane = threadIdx.x & 63u, gl = lane % G, grp = lane / G;
   LaneConst kc = lane_const(lane);
   kc.lsbase = kLdsLaneBase + (64u - G + gl) * 4u;

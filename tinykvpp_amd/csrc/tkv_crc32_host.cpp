@@ -81,7 +81,7 @@ void build_tables(DeviceTables* t, std::uint32_t poly) {
   const auto x8n = [poly](std::uint64_t n) { return x8nmodp(n, poly); };
   t->poly = poly;
   t->pad_[0] = t->pad_[1] = 0;
-  for (std::uint32_t h = 0; h <= kGroup16Max; ++h) t->init_shift[h] = mm(x8n(h), 0xFFFFFFFFu);
+  for (std::uint32_t h = 0; h <= kGroup8Max; ++h) t->init_shift[h] = mm(x8n(h), 0xFFFFFFFFu);
   for (std::uint32_t i = 0; i < 256; ++i) {
     std::uint32_t c = i;
     for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? poly : 0u);

@@ -53,7 +53,7 @@ struct DeviceTables {
   std::uint32_t inv_shift[kRow + 1];    // [d] = x^(-8d) mod P: moves a register back by d bytes (stream)
   std::uint32_t poly;                   // reflected polynomial the tables were built for
   std::uint32_t pad_[2];
-  std::uint32_t init_shift[1024 + 1];   // [h] = Shift_h(0xFFFFFFFF): the init term of a group-phase block
+  std::uint32_t init_shift[512 + 1];    // [h] = Shift_h(0xFFFFFFFF): the init term of a group-phase block
 };
 
 // One partial result of a block that was split between waves (irregular / huge-block path).
@@ -115,8 +115,8 @@ constexpr std::uint32_t kModeStream = 1;
 // [3] mode, [4..7] stream-mode info (two u64), [8] lane and group blocks (len <= kGroupMax) of dense tiles
 constexpr int kCountLanes = 8;
 // counts[kCountPhases]: which of crc_stream's phases the general path needs (OR over the tiles'
-// kTileLanes / kTileGroups / kTileGroups8 / kTileGroups16, shifted down by 1): 1 = lane blocks,
-// 2 / 4 / 8 = group blocks of 4- / 8- / 16-lane groups
+// kTileLanes / kTileGroups / kTileGroups8, shifted down by 1): 1 = lane blocks, 2 / 4 = group blocks
+// of 4- / 8-lane groups
 constexpr int kCountPhases = 9;
 
 // Blocks of at most kLaneMax bytes are folded whole by one lane each, from their own initial register
@@ -126,13 +126,11 @@ constexpr std::uint32_t kLaneMax = 64;
 // Irregular blocks of kLaneMax + 1 .. kGroupMax bytes in dense tiles are folded by 4-lane groups (one
 // block right-aligned in a 256-byte slot) in the group phase of crc_stream's launch, beside the lane
 // phase; the prepass lists them nowhere either. Blocks of kGroupMax + 1 .. kGroup8Max
-// bytes take 8-lane groups (512-byte slots) and kGroup8Max + 1 .. kGroup16Max 16-lane groups (1 KiB
-// slots), each class in its own pass of the group phase, over the tiles dense in it.
+// bytes take 8-lane groups (512-byte slots) in a second pass of the group phase, over the tiles dense
+// in them. (A 16-lane pass for 513-1024 B measured below the listed small phase, which folds those
+// blocks in the same 1 KiB slots: 3292 against 3364 GB/s, profiles/r4/s1/probe_irregular.jsonl.)
 constexpr std::uint32_t kGroupMax = 256;
 constexpr std::uint32_t kGroup8Max = 512;
-constexpr std::uint32_t kGroup16Max = 1024;
-// Lane-group size of a group block of `len` bytes (kLaneMax < len <= kGroup16Max).
-TKV_HD constexpr std::uint32_t group_size(std::uint32_t len) { return len <= kGroupMax ? 4u : len <= kGroup8Max ? 8u : 16u; }
 // The prepass leaves a scan tile's lane blocks to the lane phase only when the tile holds at least
 // kLaneDenseTile of them (of its 4096), and its group blocks to the group phase only when it holds at
 // least kGroupDenseTile; in a sparser tile they are listed as small blocks. Either phase walks the
@@ -142,20 +140,20 @@ TKV_HD constexpr std::uint32_t group_size(std::uint32_t len) { return len <= kGr
 // large blocks carry the bytes, crc_rows folds the small blocks in the shadow of its row walk and the
 // group phase's own latency chain (descriptor, data, fold: ~10 us) would only add to the batch
 // (cfg4's general path: 1300 blocks of 255 bytes per tile, +1.2 % time with the group phase).
-// The 8- and 16-lane passes walk 8 and 4 blocks per step, the small phase 4 listed ones, so they need
-// denser tiles: kGroup8DenseTile and kGroup16DenseTile of their class among the tile's 4096 blocks.
+// The 8-lane pass walks 8 blocks per step where the small phase folds 4 listed ones (in 1 KiB
+// slots), so it needs a tile at least half of whose blocks are in its class: with both group passes
+// walking a tile of 257-1024-byte blocks, 300-1000 B payloads ran at 2270 against 3160 GB/s for the
+// small phase (profiles/r4/s1/probe_irregular.jsonl).
 constexpr std::uint32_t kLaneDenseTile = 256;
 constexpr std::uint32_t kGroupDenseTile = 1024;
-constexpr std::uint32_t kGroup8DenseTile = 1024;
-constexpr std::uint32_t kGroup16DenseTile = 2048;
+constexpr std::uint32_t kGroup8DenseTile = 2048;
 constexpr std::uint64_t kGroupTileRows = 1024;
 // Per-tile flags (tile_ok):
 constexpr std::uint32_t kTileStream = 1u;     // the tile's blocks qualify for stream mode
 constexpr std::uint32_t kTileLanes = 2u;      // the tile's lane blocks (len <= kLaneMax) are the lane phase's
 constexpr std::uint32_t kTileGroups = 4u;     // its blocks of kLaneMax + 1 .. kGroupMax bytes the 4-lane pass's
 constexpr std::uint32_t kTileGroups8 = 8u;    // kGroupMax + 1 .. kGroup8Max: the 8-lane pass's
-constexpr std::uint32_t kTileGroups16 = 16u;  // kGroup8Max + 1 .. kGroup16Max: the 16-lane pass's
-constexpr std::uint32_t kTilePhases = kTileLanes | kTileGroups | kTileGroups8 | kTileGroups16;
+constexpr std::uint32_t kTilePhases = kTileLanes | kTileGroups | kTileGroups8;
 constexpr std::uint32_t kTileAllTaken = 32u;  // every block of the tile is a lane or group phase's: no scatter
 
 // Whether block of length len in a tile with flags tk is folded by the lane or a group pass (and is
@@ -163,8 +161,7 @@ constexpr std::uint32_t kTileAllTaken = 32u;  // every block of the tile is a la
 __device__ __forceinline__ bool phase_block(std::uint32_t len, std::uint32_t tk) {
   return len <= kLaneMax     ? (tk & kTileLanes) != 0
          : len <= kGroupMax  ? (tk & kTileGroups) != 0
-         : len <= kGroup8Max ? (tk & kTileGroups8) != 0
-         : len <= kGroup16Max && (tk & kTileGroups16) != 0;
+         : len <= kGroup8Max && (tk & kTileGroups8) != 0;
 }
 
 // One short host span for crc_span: `len` bytes at byte `pos` (16-byte aligned) of the mapped

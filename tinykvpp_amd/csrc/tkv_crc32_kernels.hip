@@ -125,18 +125,17 @@ constexpr int kStreamSkew = 154;
 __global__ __launch_bounds__(kStreamThreads) void crc_stream(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   if (dev::sload32(a.counts, 3) != kModeStream) {
-    // General path: this launch folds the batch's lane and group blocks (len <= kGroup16Max, DESIGN.md
+    // General path: this launch folds the batch's lane and group blocks (len <= kGroup8Max, DESIGN.md
     // §4.5), each phase only if the prepass found its blocks; crc_rows follows with the rest. The
     // group passes (lane-shift column 64 - G + g) need the lane-shift tables, the lane phase not.
     const std::uint32_t ph = dev::sload32(a.counts, kCountPhases);
     if (ph == 0) return;
-    if (ph & 14u) dev::fill_lds(a.tabs, lds);
+    if (ph & 6u) dev::fill_lds(a.tabs, lds);
     else dev::fill_lds_slicing(a.tabs, lds);
     __syncthreads();  // (the mode and ph are the same for the whole grid)
     if (ph & 1u) dev::lane_phase(a, lds);
     if (ph & 2u) dev::group_phase<4>(a, lds);
     if (ph & 4u) dev::group_phase<8>(a, lds);
-    if (ph & 8u) dev::group_phase<16>(a, lds);
     return;
   }
   dev::fill_lds(a.tabs, lds);
@@ -275,10 +274,10 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   }
   const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * kTileBpt;
   const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  // Every block first counts as a small or large one (v); lane blocks and the three group classes
-  // are also counted in one packed u64 (16 bits each, lane blocks lowest, then 4-, 8- and 16-lane
-  // group blocks: a tile has at most 4096 of each), so the one scan below yields all of them, and
-  // the tile's verdict on them (below) only subtracts.
+  // Every block first counts as a small or large one (v); lane blocks and the two group classes are
+  // also counted in one packed u64 (16 bits each, lane blocks lowest, then 4- and 8-lane group blocks:
+  // a tile has at most 4096 of each), so the one scan below yields all of them, and the tile's verdict
+  // on them (below) only subtracts.
   std::uint64_t pk[kTileBpt];
   std::uint64_t v[kTileBpt], s = 0;
   std::uint64_t ls = 0;
@@ -300,7 +299,6 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
             : len[i] <= kLaneMax    ? 1ull
             : len[i] <= kGroupMax   ? 1ull << 16
             : len[i] <= kGroup8Max  ? 1ull << 32
-            : len[i] <= kGroup16Max ? 1ull << 48
                                     : 0ull;
     v[i] = in ? scan_item(len[i]) : 0ull;
     s += v[i];
@@ -352,11 +350,9 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   auto cls = [&](int c) { return static_cast<std::uint32_t>((ltot >> (16 * c)) & 0xFFFFu); };
   const std::uint32_t tph = (cls(0) >= kLaneDenseTile ? kTileLanes : 0u) |
                             (few_rows && cls(1) >= kGroupDenseTile ? kTileGroups : 0u) |
-                            (few_rows && cls(2) >= kGroup8DenseTile ? kTileGroups8 : 0u) |
-                            (few_rows && cls(3) >= kGroup16DenseTile ? kTileGroups16 : 0u);
+                            (few_rows && cls(2) >= kGroup8DenseTile ? kTileGroups8 : 0u);
   const std::uint64_t tmask = ((tph & kTileLanes) ? 0xFFFFull : 0ull) | ((tph & kTileGroups) ? 0xFFFFull << 16 : 0ull) |
-                              ((tph & kTileGroups8) ? 0xFFFFull << 32 : 0ull) |
-                              ((tph & kTileGroups16) ? 0xFFFFull << 48 : 0ull);
+                              ((tph & kTileGroups8) ? 0xFFFFull << 32 : 0ull);
   auto taken = [&](std::uint64_t x) {  // the phase blocks among packed counts x
     x &= tmask;
     return static_cast<std::uint32_t>((x & 0xFFFFu) + ((x >> 16) & 0xFFFFu) + ((x >> 32) & 0xFFFFu) + (x >> 48));

@@ -242,7 +242,7 @@ constexpr std::uint32_t kLdsRegion = kLdsPiece * 64;
 constexpr std::uint32_t kLdsBytes = kLdsRegion + 1024;
 constexpr std::uint32_t kLdsSlots = 12;
 constexpr std::uint32_t kLdsStitchSpan = 4096;      // pieces (1 MiB): a longer record fails the stitch
-constexpr std::uint32_t kLdsDefer = 64u << 10;      // payloads checked through the irregular batch path
+constexpr std::uint32_t kLdsDefer = 1024;           // longer payloads are checked through the irregular batch path
 constexpr std::uint16_t kNoStart = 0xFFFFu;
 constexpr std::uint8_t kBroke = 1, kOverflow = 2;
 
@@ -343,8 +343,8 @@ __global__ __launch_bounds__(64) void wal_walk_lds(LdsArgs a, std::uint32_t nreg
       if (start != kNoStart) {
         any_start = true;
         my_last = static_cast<std::uint32_t>(k);
-        const std::uint64_t lim = ps + kLdsPiece;
-        while (p < lim) {
+        const std::uint64_t lim = ps + kLdsPiece < size ? ps + kLdsPiece : size;  // a chain that ends at
+        while (p < lim) {                                                          // the image's end is clean
           if (size - p < kRecMeta) {
             fl |= kBroke;
             break;
