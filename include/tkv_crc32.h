@@ -267,10 +267,9 @@ int tkv_debug_multi_combine(uint32_t poly, int ndev, const uint64_t *h_offsets, 
 void tkv_debug_update_counts(uint64_t out[3]);
 /* What the calling thread's last tkv_wal_verify / tkv_wal_verify_device did: out[0] = device walk
  * passes, out[1] = 1 when it handed the image to the exact host-thread walk, out[2] = 1 when a
- * host image was copied to the device, out[3] bit 0 = 1 when at least one device pass ran and every
- * pass stitched its pieces by the fast path (no pointer jumping; 0 when no device pass ran), bit 1 =
- * 1 when a pass walked the image through LDS (round 4). (Before round 3, out[3]
- * counted pieces; it is flags since.) */
+ * host image was copied to the device, out[3] = 1 when at least one device pass ran and every pass
+ * stitched its pieces by the fast path (no pointer jumping); 0 when no device pass ran. (Before
+ * round 3, out[3] counted pieces; it is a flag since.) */
 void tkv_debug_wal_last(uint64_t out[4]);
 /* Which path the last irregular batch on `stream` took: 1 = byte-stream row walk (blocks back to
  * back, each at least 64 bytes), 0 = general row walk; -1 on error. Synchronizes
@@ -289,10 +288,7 @@ int tkv_debug_set_host_mapped(int enable);
  * then they may take the byte-stream walk as before round 4 (kept so its many-ends-per-row shapes
  * stay under test). Returns the previous setting. Default 0. */
 int tkv_debug_set_stream_groups(int enable);
-/* Device WAL verify passes first try the walk through LDS (1, default), falling back
- * to the round-3 pass when its fast stitch does not hold; 0: the round-3 pass only. Returns the
- * previous setting. */
-int tkv_debug_set_wal_lds_walk(int enable);
+
 
 #ifdef __cplusplus
 }

@@ -18,15 +18,6 @@ import tinykvpp_amd as tk
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=[1, 0], ids=["lds_walk", "round3_walk"])
-def walk_mode(request):
-    """Every case with the LDS-walk pass (default, round 4) and with the round-3 pass only."""
-    lib = tk.load_library()
-    prev = lib.tkv_debug_set_wal_lds_walk(request.param)
-    yield request.param
-    lib.tkv_debug_set_wal_lds_walk(prev)
-
-
 def sequential_decode(oracle, img, size):
     """wal_entry::decode applied record after record (engine.cpp:31-53 recovery loop)."""
     u32 = lambda p: int.from_bytes(img[p:p + 4].tobytes(), "little")  # noqa: E731
@@ -95,7 +86,7 @@ def wal_last():
     fast stitch (no pointer jumping)."""
     out = (ctypes.c_uint64 * 4)()
     tk.load_library().tkv_debug_wal_last(out)
-    return {"passes": out[0], "host_walk": out[1], "copied": out[2], "fast": out[3] & 1, "lds": out[3] >> 1 & 1}
+    return {"passes": out[0], "host_walk": out[1], "copied": out[2], "fast": out[3]}
 
 
 LAST = {}
@@ -126,7 +117,7 @@ def device_walk_only(max_passes=1, fast=None):
 
 
 @pytest.mark.parametrize("shift", [0, 3])
-def test_small_records_clean_and_corrupted(gpu, oracle, shift, walk_mode):
+def test_small_records_clean_and_corrupted(gpu, oracle, shift):
     rng = np.random.default_rng(5)
     img, offs, size = make_wal(rng, 120000, vmax=600)
     n = img.size
@@ -134,7 +125,6 @@ def test_small_records_clean_and_corrupted(gpu, oracle, shift, walk_mode):
     assert want == ("ok", offs.size, n)
     assert both(img, n, shift) == (want, want)
     device_walk_only(fast=1)
-    assert LAST["device_image"]["lds"] == walk_mode  # the image in HBM took the LDS walk (round 4)
     assert LAST["host_image"]["copied"] == 1 and LAST["device_image"]["copied"] == 0
     for bad in (0, 1, 777, 60000, 119999):  # payload flips: CRC mismatch at that record
         o = int(offs[bad]) + int(size[bad]) - 1

@@ -16,15 +16,6 @@ struct PassResult {
   bool resume = false;     // the chain continues at `stop` (a true record start) beyond what was checked
 };
 
-// The pass with the image streamed through LDS (tkv_wal_records.hip): the record
-// chain walked speculatively in 256-byte pieces from LDS copies of 16 KiB regions, checked by the fast
-// stitch, then every record checked from a dense record list (tkv_wal_check_records_device's kernel).
-// Sets *used = false, with nothing decided, when the fast stitch does not hold (a wrong speculation,
-// a record spanning more than 1 MiB of pieces) or the image is 4 GiB or larger: the caller then runs
-// the round-3 pass. Synchronous on `st`.
-int wal_pass_lds(const std::uint8_t* w, std::uint64_t size, hipStream_t st, PassResult* r, bool* used);
-// 1 (default): tkv_wal_verify_device passes try wal_pass_lds first; 0: the round-3 pass only.
-extern int g_wal_lds_walk;
 
 // Verify the WAL image [d_wal, d_wal + size) in device memory on `st` (synchronous): the record
 // chain walked on the device, one CRC batch, the first bad record. Same results as tkv_wal_verify.

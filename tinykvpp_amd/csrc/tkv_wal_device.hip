@@ -737,7 +737,7 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
   };
   hipLaunchKernelGGL(wal_fast, dim3(blocks(K, 256)), dim3(256), 0, st, a);
   if (int rc = count_and_publish()) return rc;
-  if (s.h_res[6]) g_last[3] &= ~1ull;  // the pointer-jumping stitch ran
+  if (s.h_res[6]) g_last[3] = 0;  // the pointer-jumping stitch ran
   if (s.h_res[6]) {
     // the speculation was wrong somewhere: pointer jumping marks the pieces on the true chain
     // (wal_count above took the fast path's entries, which are speculative starts: it left res[0]
@@ -798,17 +798,8 @@ int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
   return TKV_OK;
 }
 
-// A whole pass over a resident image: the LDS-walk pass when it settles the image (tkv_wal_records.hip),
-// else the round-3 pass.
+// A whole pass over a resident image.
 int wal_pass(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream_t st, PassResult* r) {
-  if (g_wal_lds_walk) {
-    bool used = false;
-    if (int rc = wal_pass_lds(w, size, st, r, &used)) return rc;
-    if (used) {
-      g_last[3] |= 2u;  // bit 1: a pass took the LDS walk (whose stitch is always the fast one)
-      return TKV_OK;
-    }
-  }
   WalArgs a;
   if (int rc = pass_begin(s, w, size, st, &a)) return rc;
   pass_front(a, 0, a.K, st);

@@ -4,9 +4,6 @@ the 1 GiB image of small records (tools/wal_dev_probe.py) and the formats bench'
 resident in HBM; every library verifies each image in rotation, results must agree.
 
     python tools/ab_wal.py lib1.so lib2.so ... [--rounds 6]
-
-A library given as PATH:walk=N calls tkv_debug_set_wal_lds_walk(N) before each of its verifies (the
-same build with the LDS-walk pass on or off).
 """
 import argparse
 import ctypes
@@ -40,10 +37,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     args = ap.parse_args()
     torch.cuda.set_device(0)
-    libs, knob = [], []
-    for spec in args.libs:
-        p, _, opt = spec.partition(":walk=")
-        knob.append(int(opt) if opt else None)
+    libs = []
+    for p in args.libs:
         lib = ctypes.CDLL(os.path.abspath(p))
         lib.tkv_wal_verify_device.argtypes = [VP, U64, ctypes.POINTER(U64), ctypes.POINTER(U64), VP]
         lib.tkv_wal_stamp.argtypes = [VP, VP, VP, U64]
@@ -65,8 +60,6 @@ def main():
         for r in range(args.rounds):
             for k in (list(range(len(libs)))[r % len(libs):] + list(range(len(libs)))[:r % len(libs)]):
                 good, stop = U64(0), U64(0)
-                if knob[k] is not None:
-                    libs[k].tkv_debug_set_wal_lds_walk(knob[k])
                 t0 = time.perf_counter()
                 rc = libs[k].tkv_wal_verify_device(VP(d.data_ptr()), w.size, ctypes.byref(good), ctypes.byref(stop), st)
                 dt = time.perf_counter() - t0
