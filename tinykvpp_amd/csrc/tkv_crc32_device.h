@@ -1587,6 +1587,136 @@ __device__ __forceinline__ void crc_lanes_body(const RowsArgs& a, std::uint32_t*
   }
 }
 
+// ---- uniform lane batches with an exact-size window (round 4) --------------------------------------
+// The lane kernel is latency-bound, not issue-bound: in uniform 36-byte batches its waves waited on
+// memory (SQ_WAIT_ANY) 64 % of their cycles and issued VALU 15 % (profiles/r4/lanes_pmc/summary.txt),
+// because a lane keeps only DEPTH - ILP blocks (72 bytes at 36 B) in flight where the packed kernel's
+// lanes keep 128. A uniform batch's block length is known at launch, so the window is exactly the NG
+// granules a block can touch (NG = ceil((len + worst misalignment) / 16)) and the registers that
+// five-granule windows spent go to more blocks in flight: DEPTH 8 at NG <= 2, 6 at 3, 5 at 4.
+template <int ALIGN, int NG>
+__device__ __forceinline__ void lane_issue_n(std::uintptr_t blk, std::uint32_t n, std::uintptr_t dmy, uint4 (&g)[NG]) {
+  const std::uintptr_t al = blk & ~static_cast<std::uintptr_t>(15);
+  const std::uintptr_t last = (blk + n - 1u) & ~static_cast<std::uintptr_t>(15);  // used when n >= 1
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const std::uintptr_t p = al + 16u * i;
+    // past the block's last granule: that granule again (an L1 hit); an empty block reads `dummy`
+    g[i] = gload16(n == 0 ? dmy : (p < last ? p : last));
+  }
+}
+
+// d[k] = bytes [blk + 4k, +4) for k < 4 NG - (ALIGN == 16 ? 0 : 1) from the granules (o = blk & 15);
+// the rest are don't-care.
+template <int ALIGN, int NG>
+__device__ __forceinline__ void lane_dwords_n(const uint4 (&g)[NG], std::uint32_t o, std::uint32_t (&d)[4 * NG]) {
+  std::uint32_t raw[4 * NG + 3];
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    raw[4 * i + 0] = g[i].x;
+    raw[4 * i + 1] = g[i].y;
+    raw[4 * i + 2] = g[i].z;
+    raw[4 * i + 3] = g[i].w;
+  }
+  raw[4 * NG] = raw[4 * NG + 1] = raw[4 * NG + 2] = 0u;
+  if constexpr (ALIGN == 16) {
+#pragma unroll
+    for (int k = 0; k < 4 * NG; ++k) d[k] = raw[k];
+  } else {
+    const std::uint32_t m8 = 0u - ((o >> 3) & 1u), m4 = 0u - ((o >> 2) & 1u);
+#pragma unroll
+    for (int i = 0; i < 4 * NG + 1; ++i) raw[i] ^= (raw[i] ^ raw[i + 2]) & m8;
+#pragma unroll
+    for (int i = 0; i < 4 * NG + 1; ++i) raw[i] ^= (raw[i] ^ raw[i + 1]) & m4;
+#pragma unroll
+    for (int k = 0; k < 4 * NG; ++k) d[k] = ALIGN == 4 ? raw[k] : __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], o & 3u);
+  }
+}
+
+template <int ALIGN, int NG, int DEPTH, int ILP, int PRIO = 0>
+__device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
+  constexpr int ND = 4 * NG;
+  fill_lds_slicing(a.tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const LaneConst kc = lane_const(lane);
+  __syncthreads();
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves, nb = a.nblocks;
+  const std::uint64_t TS = (nb + 63u) / 64u;
+  const std::uint64_t s0 = wave * TS / W;
+  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
+  if (ns == 0) return;
+  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
+  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
+  const std::uint32_t len = a.len;
+  const std::uint32_t nf = len >> 2, tb = len & 3u;  // whole dwords, tail bytes (uniform)
+  const std::uint64_t blk0 = s0 * 64u + lane;
+  const std::uintptr_t lane_base = base + blk0 * a.stride;
+  const std::uint64_t step_bytes = 64u * a.stride;
+  const std::uintptr_t last_blk = base + (nb - 1u) * a.stride;  // lanes past the batch reload it, store nothing
+
+  uint4 buf[DEPTH][NG];
+  std::uint32_t ini[DEPTH], o16[DEPTH];
+  auto issue = [&](std::uint32_t j, int slot) {
+    const std::uint32_t jc = j < ns ? j : ns - 1;  // steps past the range reload the last one
+    const std::uint64_t b = blk0 + 64ull * jc;
+    const std::uintptr_t blk = b < nb ? lane_base + jc * step_bytes : last_blk;
+    lane_issue_n<ALIGN, NG>(blk, len, dmy, buf[slot]);
+    o16[slot] = static_cast<std::uint32_t>(blk & 15u);
+    ini[slot] = a.init_raw ? a.init_raw[b < nb ? b : nb - 1u] : a.init_default;
+  };
+  auto fold = [&](auto nb_const, int q, std::uint32_t j) {
+    constexpr int NB = decltype(nb_const)::value;
+    std::uint32_t d[NB][ND];
+    Reg p[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      lane_dwords_n<ALIGN, NG>(buf[q + i], o16[q + i], d[i]);
+      p[i] = Reg{ini[q + i], 0};
+    }
+    // one scalar branch per dword for all NB chains (the length is uniform)
+#pragma unroll
+    for (int k = 0; k < ND; ++k) {
+      if (static_cast<std::uint32_t>(k) < nf) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) slice4(lds, p[i], d[i][k], kc);
+      } else {
+        if (static_cast<std::uint32_t>(k) == nf && tb != 0u) {
+#pragma unroll
+          for (int i = 0; i < NB; ++i) p[i] = Reg{sarwate_bytes(lds, kc, p[i].value(), d[i][k], tb), 0};
+        }
+        break;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const std::uint64_t b = blk0 + 64ull * (j + i);
+      if (b < nb) a.out[b] = p[i].value() ^ a.out_xor;
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < DEPTH - ILP; ++s) issue(s, s);
+  for (std::uint32_t j = 0; j < ns; j += DEPTH) {
+    if constexpr (PRIO != 0) set_prio_from_left<PRIO>(ns - j, ns);
+#pragma unroll
+    for (int q = 0; q < DEPTH; q += ILP) {
+#pragma unroll
+      for (int i = 0; i < ILP; ++i) issue(j + q + DEPTH - ILP + i, (q + DEPTH - ILP + i) % DEPTH);
+      const std::uint32_t jq = j + q;
+      if (jq >= ns) break;
+      if (jq + ILP <= ns) {
+        fold(std::integral_constant<int, ILP>{}, q, jq);
+      } else {
+#pragma unroll
+        for (int i = 0; i < ILP; ++i)  // tail: fewer than ILP steps left
+          if (jq + i < ns) fold(std::integral_constant<int, 1>{}, q + i, jq + i);
+      }
+    }
+  }
+}
+
 // Lane blocks of an irregular batch (len <= kLaneMax, in a scan tile the prepass marked dense), walked
 // straight from the caller's offsets and lengths (the prepass lists them nowhere): wave w takes the
 // blocks [w n / W, (w + 1) n / W) 64 at a time, lane l of step j the block b0 + 64 j + l, and folds it

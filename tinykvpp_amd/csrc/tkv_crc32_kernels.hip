@@ -211,6 +211,15 @@ __global__ __launch_bounds__(kThreads) void crc_lanes(RowsArgs a) {
 }
 constexpr std::uint32_t kLanesShortMax = 48;
 
+// Uniform lane batches with an exact-size window of NG granules and a deeper pipeline (round 4,
+// DESIGN.md §4.5): DEPTH 8 at NG <= 2, 6 at NG 3, 5 at NG 4, 4 at NG 5, ILP 1.
+template <int ALIGN, int NG>
+__global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
+  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? 5 : 4;
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  dev::crc_lanes_n_body<ALIGN, NG, DEPTH, 1, kPackedPrio>(a, lds);
+}
+
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 
 }  // namespace
@@ -853,12 +862,22 @@ hipError_t launch_packed_small_gen(const RowsArgs& a, unsigned grid, hipStream_t
 hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st) {
   if (a.len > kLaneMax) return hipErrorInvalidValue;
   const std::uintptr_t m = reinterpret_cast<std::uintptr_t>(a.base) | static_cast<std::uintptr_t>(a.stride);
-  const bool shrt = a.len <= kLanesShortMax;
-  if ((m & 15u) == 0) hipLaunchKernelGGL((crc_lanes<16, 4, 2>), dim3(grid), dim3(kThreads), 0, st, a);
-  else if ((m & 3u) == 0 && shrt) hipLaunchKernelGGL((crc_lanes<4, 3, 1>), dim3(grid), dim3(kThreads), 0, st, a);
-  else if ((m & 3u) == 0) hipLaunchKernelGGL((crc_lanes<4, 4, 2>), dim3(grid), dim3(kThreads), 0, st, a);
-  else if (shrt) hipLaunchKernelGGL((crc_lanes<1, 3, 1>), dim3(grid), dim3(kThreads), 0, st, a);
-  else hipLaunchKernelGGL((crc_lanes<1, 4, 2>), dim3(grid), dim3(kThreads), 0, st, a);
+  const int align = (m & 15u) == 0 ? 16 : (m & 3u) == 0 ? 4 : 1;
+  const std::uint32_t mis = align == 16 ? 0u : align == 4 ? 12u : 15u;  // worst start offset in a granule
+  const std::uint32_t ng = std::max<std::uint32_t>(1u, (a.len + mis + 15u) / 16u);  // granules a block can touch
+  const dim3 g(grid), b(kThreads);
+#define TKV_LANES_N(A)                                                                  \
+  switch (ng) {                                                                         \
+    case 1: hipLaunchKernelGGL((crc_lanes_n<A, 1>), g, b, 0, st, a); break;             \
+    case 2: hipLaunchKernelGGL((crc_lanes_n<A, 2>), g, b, 0, st, a); break;             \
+    case 3: hipLaunchKernelGGL((crc_lanes_n<A, 3>), g, b, 0, st, a); break;             \
+    case 4: hipLaunchKernelGGL((crc_lanes_n<A, 4>), g, b, 0, st, a); break;             \
+    default: hipLaunchKernelGGL((crc_lanes_n<A, 5>), g, b, 0, st, a); break;            \
+  }
+  if (align == 16) { TKV_LANES_N(16) }
+  else if (align == 4) { TKV_LANES_N(4) }
+  else { TKV_LANES_N(1) }
+#undef TKV_LANES_N
   return hipGetLastError();
 }
 

@@ -83,15 +83,15 @@ __device__ __forceinline__ std::uint32_t rec_fold(const std::uint32_t* lds, cons
   return r.value();
 }
 
-// NG granules per record window; AHEAD steps of granules in flight (2, or 1 for the wide window,
-// whose three slots would spill at 16 waves per CU).
+// NG granules per record window; AHEAD steps of granules in flight (3 for narrow windows, 2 at 6
+// granules, 1 for the wide ones, whose three slots would spill at 16 waves per CU).
 template <int NG, int AHEAD>
 __global__ __launch_bounds__(kRecThreads) void wal_rec_lanes(RecArgs a, const DeviceTables* tabs) {
   constexpr int ND = 4 * NG - 4;      // realigned dwords of the window
   constexpr int NPAY = ND - 3;        // whole payload dwords folded from the window (payload at dword 2; one spare for the tail)
   constexpr int RING = 4;             // offsets are fetched RING steps ahead of their granules
   constexpr int DRING = AHEAD == 1 ? 2 : 4;
-  static_assert(AHEAD == 1 || AHEAD == 2, "granules one or two steps ahead");
+  static_assert(AHEAD >= 1 && AHEAD <= 3, "granules one to three steps ahead");
   __shared__ std::uint32_t lds[kLdsSliceWords];
   dev::fill_lds_slicing(tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
@@ -196,13 +196,14 @@ void launch_records(RecArgs a, std::uint32_t max_payload, int ncu, const DeviceT
   a.nwaves = static_cast<std::uint32_t>(grid * 16);
   // window: NG granules hold the header, the key/value lengths and a payload of up to 16 NG - 26 bytes
   // at any alignment (36-byte payloads: 4 granules; 64: 6; 100: 8); longer ones continue 64 bytes at
-  // a time. Wider windows keep one step of granules in flight instead of two (registers).
+  // a time. Records are latency-bound like the lane kernel (profiles/r4/rec_check/): narrow windows keep
+  // three steps of granules in flight, 6 granules two, wider ones one (registers).
   const std::uint32_t ng =
       std::min<std::uint32_t>(8u, std::max<std::uint32_t>(4u, (std::min<std::uint32_t>(max_payload, 1024u) + 26u + 15u) / 16u));
   const dim3 g(static_cast<unsigned>(grid)), b(kRecThreads);
   switch (ng) {
-    case 4: hipLaunchKernelGGL((wal_rec_lanes<4, 2>), g, b, 0, st, a, tabs); break;
-    case 5: hipLaunchKernelGGL((wal_rec_lanes<5, 2>), g, b, 0, st, a, tabs); break;
+    case 4: hipLaunchKernelGGL((wal_rec_lanes<4, 3>), g, b, 0, st, a, tabs); break;
+    case 5: hipLaunchKernelGGL((wal_rec_lanes<5, 3>), g, b, 0, st, a, tabs); break;
     case 6: hipLaunchKernelGGL((wal_rec_lanes<6, 2>), g, b, 0, st, a, tabs); break;
     case 7: hipLaunchKernelGGL((wal_rec_lanes<7, 1>), g, b, 0, st, a, tabs); break;
     default: hipLaunchKernelGGL((wal_rec_lanes<8, 1>), g, b, 0, st, a, tabs); break;
