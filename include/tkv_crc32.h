@@ -279,6 +279,11 @@ int tkv_debug_irregular_mode(void *stream);
  * mode): bit 0 the lane phase (blocks <= 64 B), bits 1 / 2 the 4- / 8-lane group passes (65-256 /
  * 257-512 B); -1 on error. Synchronizes the stream. */
 int tkv_debug_irregular_phases(void *stream);
+/* The small-block lists of the last irregular batch on `stream` (all 0 in stream mode): out[0] =
+ * blocks of at most 1 KiB the small-block phase folds (those no lane or group pass took), out[1] =
+ * how many of them are at most 256 bytes (4-lane groups), out[2] = 257-512 bytes (8-lane groups; the
+ * rest take 16-lane groups). Returns 0, or -1 on error. Synchronizes the stream. */
+int tkv_debug_irregular_lists(void *stream, uint32_t out[3]);
 /* Host batches from pinned host memory are read in place by the kernels (zero copy) unless this is
  * 0 (then they take the staged copy pipeline, as pageable memory does). Returns the previous
  * setting. Default 1; the environment variable TKV_HOST_MAPPED=0 sets 0 at load time. */

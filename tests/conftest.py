@@ -203,6 +203,28 @@ def phases_expected(lens):
     return ph
 
 
+def lists_expected(lens):
+    """The small-block lists the prepass builds (tkv_debug_irregular_lists) for a general-path batch:
+    blocks of at most SMALL_MAX bytes that no lane or group pass takes (phases_expected's per-tile
+    verdicts), and how many of them are at most 256 and 257-512 bytes."""
+    lens = np.asarray(lens, np.int64)
+    listed = []
+    for t in range(0, lens.size, SCAN_TILE):
+        tl = lens[t:t + SCAN_TILE]
+        taken = np.zeros(tl.size, bool)
+        if np.count_nonzero(tl <= LANE_MAX) >= LANE_DENSE_TILE:
+            taken |= tl <= LANE_MAX
+        big = tl[tl > SMALL_MAX]
+        if int(((big - 1) // 4096 + 1).sum()) <= GROUP_TILE_ROWS:
+            for lo, hi, thr, _ in GROUP_CLASSES:
+                cls = (tl > lo) & (tl <= hi)
+                if np.count_nonzero(cls) >= thr:
+                    taken |= cls
+        listed.append(tl[(tl <= SMALL_MAX) & ~taken])
+    ls = np.concatenate(listed) if listed else np.zeros(0, np.int64)
+    return (int(ls.size), int(np.count_nonzero(ls <= 256)), int(np.count_nonzero((ls > 256) & (ls <= 512))))
+
+
 def stream_expected(offs, lens, group_stream=False):
     """1 when the prepass picks the byte-stream walk for this batch, else 0: every block at least
     LANE_MAX + 1 bytes and starting where its predecessor ends, and (unless tkv_debug_set_stream_groups

@@ -85,9 +85,9 @@ def load_tables(lib, poly=0xEDB88320):
     for k in range(12):
         assert int(rows_shift[1 << k]) == int(buf[1024 + 8 * 16 * 64 + 64 + k])
     built_for = int(buf[o]); o += 3  # poly + 2 pad words
-    init_shift = buf[o:o + 513]; o += 513  # [h] = Shift_h(0xFFFFFFFF): the group phase's init term
+    init_shift = buf[o:o + 1025]; o += 1025  # [h] = Shift_h(0xFFFFFFFF): the group walks' init term
     if poly == POLY:
-        for h in (0, 1, 65, 200, 256, 257, 300, 512):
+        for h in (0, 1, 65, 200, 256, 257, 300, 512, 513, 777, 1024):
             assert int(init_shift[h]) == lib.tkv_debug_multmodp(lib.tkv_debug_x8nmodp(h), 0xFFFFFFFF)
     # the group phase's result is init_shift[h] ^ crc_0(block) = crc_init(block) (affine start)
     assert o * 4 == n

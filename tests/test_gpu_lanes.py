@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import tinykvpp_amd as tk
-from conftest import phases_expected
+from conftest import lists_expected, phases_expected
 
 pytestmark = pytest.mark.gpu
 
@@ -263,6 +263,53 @@ def test_irregular_group8_and_small_blocks(gpu, oracle, buf, sizes, base):
     m = 5000
     got = u32(tk.crc32_batch(d, o[:m].contiguous(), ln[:m].contiguous(), algo="crc32c"))
     assert np.array_equal(got, oracle_c(oracle, host, offs[:m], lens[:m]))
+
+
+def lists():
+    """(listed small blocks, of which <= 256 B, of which 257-512 B) of the last irregular batch."""
+    out = (ctypes.c_uint32 * 3)()
+    assert tk.load_library().tkv_debug_irregular_lists(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream), out) == 0
+    return tuple(int(x) for x in out)
+
+
+@pytest.mark.parametrize("shape", ["sparse", "dense_g8", "dense_lanes", "tiny"])
+@pytest.mark.parametrize("base", [0, 5, 8])
+def test_irregular_small_lists_by_class(gpu, oracle, buf, shape, base):
+    """Small blocks the lane and group passes do not take are listed by class and folded by 4-, 8- or
+    16-lane groups (256-, 512- and 1024-byte slots): every length 0-1024 mixed with large blocks (tiles
+    with too many rows for the group passes), next to tiles dense in 257-512-byte blocks (the 8-lane
+    pass takes those, the rest stay listed) or in lane blocks; the list sizes the prepass publishes,
+    the results, per-block initial registers and CRC-32C."""
+    host, d = buf
+    rng = np.random.default_rng(700 + base + len(shape))
+    if shape == "tiny":  # fewer blocks than one step of each walk
+        lens = np.array([0, 1, 256, 257, 512, 513, 1024, 5000], np.int64)
+    else:
+        n = 24_000
+        lens = rng.integers(0, 1025, n)
+        big = rng.random(n) < 0.3
+        lens[big] = rng.integers(4097, 9000, int(big.sum()))
+        if shape == "dense_g8":  # the second and fourth tiles: 257-512-byte blocks only, no large ones
+            for t in (1, 3):
+                lens[t * 4096:(t + 1) * 4096] = rng.integers(257, 513, 4096)
+        if shape == "dense_lanes":  # the third tile: mostly lane blocks
+            lens[2 * 4096:3 * 4096] = np.where(rng.random(4096) < 0.5, rng.integers(0, 65, 4096), rng.integers(65, 1025, 4096))
+        lens[:1025] = np.arange(1025)  # every small length, all in the first tile
+        lens[1025:1025 + 200] = rng.integers(5000, 9000, 200)  # keeps the first tile out of the group passes
+    gaps = rng.integers(0, 9, lens.size)
+    offs = base + np.concatenate([[0], np.cumsum(lens[:-1] + gaps[:-1])])
+    assert offs[-1] + lens[-1] <= host.size
+    o, ln = torch.from_numpy(offs.astype(np.int64)).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    got = u32(tk.crc32_batch(d, o, ln))
+    assert mode() == 0
+    assert lists() == lists_expected(lens)
+    assert phases() == phases_expected(lens)
+    assert np.array_equal(got, oracle.batch(host, offs, lens))
+    init = rng.integers(0, 2**32, offs.size, dtype=np.uint64).astype(np.uint32)
+    got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))
+    assert np.array_equal(got, oracle.batch(host, offs, lens, init))
+    got = u32(tk.crc32_batch(d, o, ln, algo="crc32c"))
+    assert np.array_equal(got, oracle_c(oracle, host, offs, lens))
 
 
 @pytest.mark.parametrize("sizes", [(65,), (100, 128, 200), tuple(range(65, 257)), (256,)])

@@ -350,7 +350,7 @@ __device__ __forceinline__ void set_prio_from_left(std::uint32_t left, std::uint
 }
 
 // Small blocks of an irregular batch (defined below; runs inside the irregular row kernel).
-__device__ __forceinline__ void small_phase(const RowsArgs& a, std::uint32_t* lds);
+__device__ __forceinline__ void small_phase(const RowsArgs& a, const std::uint32_t* lds);
 
 // Fill the 160 KiB LDS table image (slicing tables replicated 32x, lane-shift nibble tables) with one
 // global load per slicing entry: thread u owns (pair, entry, table) of u = 512 pair + 2 e + t and
@@ -521,135 +521,6 @@ __device__ __forceinline__ void crc_rows_body(const RowsArgs& a, std::uint32_t* 
   }
 }
 
-
-// Small blocks of an irregular batch (len <= kSmallMax = 1 KiB, listed by the prepass in
-// s_off/s_len/s_idx): a 16-lane group folds one block, right-aligned in a 1 KiB mini-row (lane g
-// owns bytes [64 g, 64 g + 64) of it; bytes in front of the block are zero), so a wave folds four
-// blocks per step where the row kernel would spend a whole 4 KiB row on each. Lane shifts are the
-// LS entries of lane 48 + g (Shift_{(15-g)*64}), the init term is spread over the group (two bits
-// per lane: bit_i(init) * Shift_len(1 << i)), and the first four DPP steps of the wave reduction
-// sum each 16-lane row. Waves own contiguous ranges of steps (4 blocks per step). Pipeline: data of
-// step t+2 is issued while step t folds; descriptors are fetched 4 steps ahead of their data.
-// The tables must already be in LDS (fill_lds + barrier). Runs inside the irregular row kernel,
-// before its rows, on the same partition of waves.
-__device__ __forceinline__ void small_phase(const RowsArgs& a, std::uint32_t* lds) {
-  constexpr int RING = 4;
-  const std::uint32_t lane = threadIdx.x & 63u;
-  const std::uint32_t grp = lane >> 4, gl = lane & 15u;
-  LaneConst kc = lane_const(lane);
-  kc.lsbase = kLdsLaneBase + (48u + gl) * 4u;
-
-  const std::uint32_t NS = sload32(a.counts, 1);
-  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const std::uint64_t W = a.nwaves;
-  const std::uint64_t S = (NS + 3u) / 4u;
-  const std::uint32_t t0 = static_cast<std::uint32_t>(wave * S / W);
-  const std::uint32_t t1 = static_cast<std::uint32_t>((wave + 1) * S / W);
-  if (t0 >= t1) return;
-  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
-  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
-
-  // descriptor ring (slot = step % RING): byte offset, length, batch index; kept valid-masked
-  std::uint64_t d_off[RING];
-  std::uint32_t d_len[RING], d_idx[RING];
-  auto step_ok = [&](std::uint32_t t) { return t < t1 && 4u * t + grp < NS; };
-  auto fetch = [&](std::uint32_t t, int slot) {
-    // unconditional loads (index clamped), results left untouched until issue() uses them four
-    // steps later: any branch or select on them here would make the compiler wait for them now
-    const std::uint32_t jj = step_ok(t) ? 4u * t + grp : 0u;
-    d_off[slot] = a.s_off[jj];
-    d_len[slot] = a.s_len[jj];
-    d_idx[slot] = a.s_idx[jj];
-  };
-  // data ring: five 16-byte pieces covering the lane's segment, plus what the fold step needs
-  uint4 q[RING][5];
-  std::uint32_t m_len[RING], m_idx[RING], m_end[RING], m_hs0[RING], m_hs1[RING], m_init[RING];
-  auto issue = [&](int slot, std::uint32_t t) {
-    const bool ok = step_ok(t);
-    const std::uint32_t n = ok ? d_len[slot] : 0u;
-    const std::uintptr_t blo = base + d_off[slot];
-    const std::uintptr_t bhi = blo + n;
-    const std::uintptr_t seg = static_cast<std::uintptr_t>(static_cast<std::int64_t>(bhi) - static_cast<std::int64_t>(kSmallMax)) +
-                               gl * kSeg;
-    const std::uintptr_t al = seg & ~static_cast<std::uintptr_t>(15);
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      const std::uintptr_t p = al + 16u * i;
-      q[slot][i] = gload16(ok && (p + 16 > blo) && (p < bhi) ? p : dmy);
-    }
-    m_len[slot] = n;
-    m_idx[slot] = ok ? d_idx[slot] : 0xFFFFFFFFu;
-    m_end[slot] = static_cast<std::uint32_t>(bhi & 15u);
-    // init-term operands travel with the data (loaded now, used two steps later)
-    const std::uint32_t nn = ok ? n : 0u;
-    m_hs0[slot] = a.tabs->head_shift[nn][gl];
-    m_hs1[slot] = a.tabs->head_shift[nn][16u + gl];
-    m_init[slot] = a.init_default;
-    if (a.init_raw) m_init[slot] = a.init_raw[m_idx[slot] != 0xFFFFFFFFu ? m_idx[slot] : 0u];
-  };
-  auto fold = [&](int slot) {
-    const std::uint32_t n = m_len[slot];
-    std::uint32_t raw[20];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      raw[4 * i + 0] = q[slot][i].x;
-      raw[4 * i + 1] = q[slot][i].y;
-      raw[4 * i + 2] = q[slot][i].z;
-      raw[4 * i + 3] = q[slot][i].w;
-    }
-    // realign by the block end's offset within 16 bytes (per group: bitwise selects - a ternary
-    // here is turned into a dynamically indexed array, i.e. scratch memory)
-    const std::uint32_t sft = m_end[slot];
-    const std::uint32_t m8 = 0u - ((sft >> 3) & 1u), m4 = 0u - ((sft >> 2) & 1u);
-#pragma unroll
-    for (int i = 0; i < 18; ++i) raw[i] ^= (raw[i] ^ raw[i + 2]) & m8;
-#pragma unroll
-    for (int i = 0; i < 19; ++i) raw[i] ^= (raw[i] ^ raw[i + 1]) & m4;
-    std::uint32_t dw[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dw[k] = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sft & 3u);
-    // zero the bytes in front of the block (a straddling piece holds its neighbour's bytes)
-    const std::int32_t off0 = static_cast<std::int32_t>(n) - static_cast<std::int32_t>(kSmallMax) +
-                              static_cast<std::int32_t>(gl * kSeg);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const std::int32_t before = -(off0 + 4 * k);
-      const std::uint32_t sh = static_cast<std::uint32_t>(before < 0 ? 0 : (before > 4 ? 4 : before)) * 8u;
-      dw[k] &= static_cast<std::uint32_t>(0xFFFFFFFFull << sh);
-    }
-    Reg p{0, 0};
-#pragma unroll
-    for (int k = 0; k < 16; ++k) slice4(lds, p, dw[k], kc);
-    std::uint32_t v = lane_shift(lds, p.value(), kc);
-    const bool ok = m_idx[slot] != 0xFFFFFFFFu;
-    const std::uint32_t init = ok ? m_init[slot] : 0u;
-    v ^= (static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), gl, 1)) & m_hs0[slot]) ^
-         (static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), 16u + gl, 1)) & m_hs1[slot]);
-    v ^= __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    v ^= __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    v ^= __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-    v ^= __builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, false);  // row_mirror: row sum in all 16 lanes
-    if (ok && gl == 15u) a.out[m_idx[slot]] = v ^ a.out_xor;
-  };
-
-  // prologue: descriptors of steps t0..t0+3, data of steps t0, t0+1
-#pragma unroll
-  for (int k = 0; k < RING; ++k) fetch(t0 + k, k);
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    issue(k, t0 + k);
-    fetch(t0 + k + RING, k);
-  }
-  for (std::uint32_t t = t0; t < t1; t += RING) {
-#pragma unroll
-    for (int k = 0; k < RING; ++k) {
-      const int ahead = (k + 2) % RING;  // step t+k+2: its descriptor arrived RING steps ago
-      issue(ahead, t + k + 2);
-      fetch(t + k + 2 + RING, ahead);
-      if (t + k < t1) fold(k);
-    }
-  }
-}
 
 // Inclusive prefix XOR of v over the 64 lanes (DPP row shifts within rows of 16, then row
 // broadcasts across rows).
@@ -1512,88 +1383,18 @@ __device__ __forceinline__ void lane_fold(const std::uint32_t* lds, const LaneCo
   for (int i = 0; i < NB; ++i) r[i] = p[i].value();
 }
 
+// ---- uniform lane batches ---------------------------------------------------------------------------
 // Uniform batches of blocks of at most kLaneMax bytes, any stride, alignment and initial registers:
 // lane l of wave step s folds block 64 s + l. Waves own contiguous ranges of steps; DEPTH steps of
 // loads are in flight and ILP steps fold with interleaved chains (crc_packed_body's pipeline and issue
 // priority); each step's 64 results leave in one coalesced store.
-template <int ALIGN, int DEPTH, int ILP, int PRIO = 0>
-__device__ __forceinline__ void crc_lanes_body(const RowsArgs& a, std::uint32_t* lds) {
-  static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
-  fill_lds_slicing(a.tabs, lds);
-  const std::uint32_t lane = threadIdx.x & 63u;
-  const LaneConst kc = lane_const(lane);
-  __syncthreads();
-  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const std::uint64_t W = a.nwaves, nb = a.nblocks;
-  const std::uint64_t TS = (nb + 63u) / 64u;
-  const std::uint64_t s0 = wave * TS / W;
-  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
-  if (ns == 0) return;
-  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
-  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
-  const std::uint32_t len = a.len;
-  const std::uint64_t blk0 = s0 * 64u + lane;                        // this lane's block in step 0
-  const std::uintptr_t lane_base = base + blk0 * a.stride;
-  const std::uint64_t step_bytes = 64u * a.stride;
-  const std::uintptr_t last_blk = base + (nb - 1u) * a.stride;  // lanes past the batch reload it, store nothing
-  // granules that can hold a block byte: the start lies at most 0 / 12 / 15 bytes into its granule
-  const std::uint32_t ngr = (len + (ALIGN == 16 ? 0u : ALIGN == 4 ? 12u : 15u) + 15u) / 16u;
-
-  uint4 buf[DEPTH][kLaneGran];
-  std::uint32_t ini[DEPTH], o16[DEPTH];
-  auto issue = [&](std::uint32_t j, int slot) {
-    const std::uint32_t jc = j < ns ? j : ns - 1;  // steps past the range reload the last one
-    const std::uint64_t b = blk0 + 64ull * jc;
-    const std::uintptr_t blk = b < nb ? lane_base + jc * step_bytes : last_blk;
-    lane_issue<ALIGN>(blk, len, dmy, buf[slot], ngr);
-    o16[slot] = static_cast<std::uint32_t>(blk & 15u);
-    ini[slot] = a.init_raw ? a.init_raw[b < nb ? b : nb - 1u] : a.init_default;
-  };
-  auto fold = [&](auto nb_const, int q, std::uint32_t j) {
-    constexpr int NB = decltype(nb_const)::value;
-    std::uint32_t d[NB][16], n[NB], r[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      lane_dwords<ALIGN>(buf[q + i], o16[q + i], d[i]);
-      n[i] = len;
-      r[i] = ini[q + i];
-    }
-    lane_fold<NB, true>(lds, kc, d, n, r);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const std::uint64_t b = blk0 + 64ull * (j + i);
-      if (b < nb) a.out[b] = r[i] ^ a.out_xor;
-    }
-  };
-
-#pragma unroll
-  for (int s = 0; s < DEPTH - ILP; ++s) issue(s, s);
-  for (std::uint32_t j = 0; j < ns; j += DEPTH) {
-    if constexpr (PRIO != 0) set_prio_from_left<PRIO>(ns - j, ns);
-#pragma unroll
-    for (int q = 0; q < DEPTH; q += ILP) {
-#pragma unroll
-      for (int i = 0; i < ILP; ++i) issue(j + q + DEPTH - ILP + i, (q + DEPTH - ILP + i) % DEPTH);
-      const std::uint32_t jq = j + q;
-      if (jq >= ns) break;
-      if (jq + ILP <= ns) {
-        fold(std::integral_constant<int, ILP>{}, q, jq);
-      } else {
-#pragma unroll
-        for (int i = 0; i < ILP; ++i)  // tail: fewer than ILP steps left
-          if (jq + i < ns) fold(std::integral_constant<int, 1>{}, q + i, jq + i);
-      }
-    }
-  }
-}
-
-// ---- uniform lane batches with an exact-size window (round 4) --------------------------------------
-// The lane kernel is latency-bound, not issue-bound: in uniform 36-byte batches its waves waited on
-// memory (SQ_WAIT_ANY) 64 % of their cycles and issued VALU 15 % (profiles/r4/lanes_pmc/summary.txt),
-// because a lane keeps only DEPTH - ILP blocks (72 bytes at 36 B) in flight where the packed kernel's
-// lanes keep 128. A uniform batch's block length is known at launch, so the window is exactly the NG
-// granules a block can touch (NG = ceil((len + worst misalignment) / 16)) and the registers that
-// five-granule windows spent go to more blocks in flight: DEPTH 8 at NG <= 2, 6 at 3, 5 at 4.
+// Waves of the round-3 kernel waited on memory (SQ_WAIT_ANY) 64 % of their cycles in uniform 36-byte
+// batches and issued VALU 15 % (profiles/r4/lanes_pmc/summary.txt). A uniform batch's block length is
+// known at launch, so the window here is exactly the NG granules a block can touch (NG = ceil((len +
+// worst misalignment) / 16)) and the registers five-granule windows spent go to more blocks in flight:
+// DEPTH 8 at NG <= 2, 6 at 3, 5 at 4. That lifted short blocks (26 B +8 %) but not 36 B: with 16 waves
+// per CU (LDS-bound: one 1024-thread workgroup) the SIMDs' VALU is already ~52 % busy there, so more
+// loads in flight leave the same issue-latency bound.
 template <int ALIGN, int NG>
 __device__ __forceinline__ void lane_issue_n(std::uintptr_t blk, std::uint32_t n, std::uintptr_t dmy, uint4 (&g)[NG]) {
   const std::uintptr_t al = blk & ~static_cast<std::uintptr_t>(15);
@@ -1717,6 +1518,96 @@ __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_
   }
 }
 
+// Uniform lane batches loaded dword by dword (round 4): a block of len = 4 NF + tb bytes (4 <= len
+// <= kLaneMax) is read with exactly its own bytes, no 16-byte granules and no realignment: NF whole
+// dwords as ceil(NF / 4) dword-aligned or byte-aligned 16-byte loads (the last one anchored at the
+// last whole dword, overlapping its predecessor, so no load reaches past the block), and for tb > 0
+// the dword holding the tail bytes: the aligned dword at 4 NF when the blocks are dword aligned
+// (it cannot cross a page), else the dword ending at the block's end, shifted down. The 16-byte
+// granule window of crc_lanes_n spends ~2 selects per dword on realignment (26 of ~150 VALU
+// instructions per 36-byte step) and 12 registers per block for 9 dwords.
+template <int NF>
+__device__ __forceinline__ void lane_load_direct(std::uintptr_t blk, std::uint32_t (&d)[NF]) {
+  if constexpr (NF >= 4) {
+#pragma unroll
+    for (int k = 0; k < NF; k += 4) {
+      const int at = k + 4 <= NF ? k : NF - 4;  // the last load ends at dword NF
+      const v4u v = *reinterpret_cast<g_v4u*>(blk + 4u * at);
+      const std::uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (at + i >= k) d[at + i] = w[i];
+    }
+  } else {
+    typedef unsigned v2u __attribute__((ext_vector_type(2)));
+    typedef const v2u __attribute__((address_space(1))) g_v2u;
+    if constexpr (NF >= 2) {
+      const v2u v = *reinterpret_cast<g_v2u*>(blk);
+      d[0] = v.x;
+      d[1] = v.y;
+    }
+    if constexpr (NF == 1 || NF == 3) d[NF - 1] = *reinterpret_cast<g_u32*>(blk + 4u * (NF - 1));
+  }
+}
+
+template <int ALIGN, int NF, int DEPTH, int PRIO = 0>
+__device__ __forceinline__ void crc_lanes_d_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(ALIGN == 4 || ALIGN == 1, "dword-aligned or byte-aligned blocks");
+  static_assert(NF >= 1 && 4 * NF <= static_cast<int>(kLaneMax) && DEPTH >= 2, "block shape");
+  fill_lds_slicing(a.tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const LaneConst kc = lane_const(lane);
+  __syncthreads();
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves, nb = a.nblocks;
+  const std::uint64_t TS = (nb + 63u) / 64u;
+  const std::uint64_t s0 = wave * TS / W;
+  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
+  if (ns == 0) return;
+  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
+  const std::uint32_t len = a.len;
+  const std::uint32_t tb = len & 3u;  // tail bytes (uniform)
+  const std::uint64_t blk0 = s0 * 64u + lane;
+  const std::uintptr_t lane_base = base + blk0 * a.stride;
+  const std::uint64_t step_bytes = 64u * a.stride;
+  const std::uintptr_t last_blk = base + (nb - 1u) * a.stride;  // lanes past the batch reload it, store nothing
+  // tail dword: dword-aligned blocks read the aligned dword after the whole ones, others the dword
+  // ending at the block's end (its top tb bytes are the tail)
+  const std::uint32_t tail_at = ALIGN == 4 ? 4u * NF : len - 4u;
+  const std::uint32_t tail_sh = ALIGN == 4 ? 0u : 8u * (4u - tb);
+
+  std::uint32_t buf[DEPTH][NF], tail[DEPTH], ini[DEPTH];
+  auto issue = [&](std::uint32_t j, int slot) {
+    const std::uint32_t jc = j < ns ? j : ns - 1;  // steps past the range reload the last one
+    const std::uint64_t b = blk0 + 64ull * jc;
+    const std::uintptr_t blk = b < nb ? lane_base + jc * step_bytes : last_blk;
+    lane_load_direct<NF>(blk, buf[slot]);
+    if (tb != 0u) tail[slot] = *reinterpret_cast<g_u32*>(blk + tail_at);  // (a scalar branch)
+    ini[slot] = a.init_raw ? a.init_raw[b < nb ? b : nb - 1u] : a.init_default;
+  };
+  auto fold = [&](int q, std::uint32_t j) {
+    Reg p{ini[q], 0};
+#pragma unroll
+    for (int k = 0; k < NF; ++k) slice4(lds, p, buf[q][k], kc);
+    std::uint32_t r = p.value();
+    if (tb != 0u) r = sarwate_bytes(lds, kc, r, tail[q] >> tail_sh, tb);
+    const std::uint64_t b = blk0 + 64ull * j;
+    if (b < nb) a.out[b] = r ^ a.out_xor;
+  };
+
+#pragma unroll
+  for (int s = 0; s < DEPTH - 1; ++s) issue(s, s);
+  for (std::uint32_t j = 0; j < ns; j += DEPTH) {
+    if constexpr (PRIO != 0) set_prio_from_left<PRIO>(ns - j, ns);
+#pragma unroll
+    for (int q = 0; q < DEPTH; ++q) {
+      issue(j + q + DEPTH - 1, (q + DEPTH - 1) % DEPTH);
+      if (j + q >= ns) break;
+      fold(q, j + q);
+    }
+  }
+}
+
 // Lane blocks of an irregular batch (len <= kLaneMax, in a scan tile the prepass marked dense), walked
 // straight from the caller's offsets and lengths (the prepass lists them nowhere): wave w takes the
 // blocks [w n / W, (w + 1) n / W) 64 at a time, lane l of step j the block b0 + 64 j + l, and folds it
@@ -1784,20 +1675,26 @@ __device__ __forceinline__ void lane_phase(const RowsArgs& a, const std::uint32_
   }
 }
 
-// Group blocks of an irregular batch (in tiles dense in their class): a G-lane group folds one block
-// right-aligned in a 64 G-byte slot (crc_packed_small_gen's layout), 64/G blocks per wave step, walked
-// straight from the caller's offsets and lengths over the same block range and pipeline as lane_phase
-// (other groups idle). G = 4 takes blocks of kLaneMax + 1 .. kGroupMax bytes, G = 8 up to kGroup8Max,
-// each pass only the blocks of its class in tiles flagged for it. Lane g
-// loads the five granules covering its 64 bytes and realigns them (lane_dwords); granules holding no
-// byte of the block read the zero buffer and the bytes in front of the block are masked. Lane shifts
-// are column 64 - G + g of the LDS image (Shift_{(G-1-g)*64}); the init term is Shift_len(init), from
-// init_shift[len] for the default register, or spread over the group (32/G bits per lane,
-// head_shift[len]) for per-block registers; the group's sum comes from the first log2(G) DPP steps of
-// the wave reduction.
-template <int G>
-__device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32_t* lds) {
-  static_assert(G == 4 || G == 8, "4- or 8-lane groups");
+// Group blocks of an irregular batch: a G-lane group folds one block right-aligned in a 64 G-byte
+// slot (crc_packed_small_gen's layout), 64/G blocks per wave step. Two walks share the code:
+//  * LIST = false, the group phase (tiles dense in a class): straight from the caller's offsets and
+//    lengths over the same block range and pipeline as lane_phase (other groups idle). G = 4 takes
+//    blocks of kLaneMax + 1 .. kGroupMax bytes, G = 8 up to kGroup8Max, each pass only the blocks of
+//    its class in tiles flagged for it;
+//  * LIST = true, the small-block phase: entries [lo, lo + cnt) of the prepass lists s_off/s_len/s_idx
+//    (one class per list range, so every block but those of the shortest class fills over half its
+//    slot), waves owning contiguous ranges of entries.
+// Lane g loads the five granules covering its 64 bytes and realigns them (lane_dwords); granules
+// holding no byte of the block read the zero buffer and the bytes in front of the block are masked.
+// Lane shifts are column 64 - G + g of the LDS image (Shift_{(G-1-g)*64}); the init term is
+// Shift_len(init), from init_shift[len] for the default register, or spread over the group (32/G bits
+// per lane, head_shift[len]) for per-block registers; the group's sum comes from the first log2(G)
+// DPP steps of the wave reduction. Pipeline: data of step t+2 is issued while step t folds;
+// descriptors are fetched RING steps ahead of their data. The tables must already be in LDS.
+template <int G, bool LIST>
+__device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_t* lds, std::uint32_t lo,
+                                           std::uint32_t cnt) {
+  static_assert(G == 4 || G == 8 || (LIST && G == 16), "4- or 8-lane groups (16 for listed blocks)");
   constexpr int RING = 4;
   constexpr std::uint32_t kSlot = 64u * G;
   constexpr std::uint32_t kLo = G == 4 ? kLaneMax : kGroupMax;  // the class: (kLo, kSlot]
@@ -1806,8 +1703,8 @@ __device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32
   LaneConst kc = lane_const(lane);
   kc.lsbase = kLdsLaneBase + (64u - G + gl) * 4u;
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const std::uint64_t W = a.nwaves, n = a.nblocks;
-  const std::uint64_t b0 = wave * n / W, b1 = (wave + 1) * n / W;
+  const std::uint64_t W = a.nwaves, n = LIST ? cnt : a.nblocks, first = LIST ? lo : 0u;
+  const std::uint64_t b0 = first + wave * n / W, b1 = first + (wave + 1) * n / W;
   if (b0 >= b1) return;
   constexpr std::uint32_t kPer = 64u / G;  // blocks per step
   const std::uint32_t ns = static_cast<std::uint32_t>((b1 - b0 + kPer - 1u) / kPer);
@@ -1815,20 +1712,27 @@ __device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32
   const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
 
   std::uint64_t d_off[RING];
-  std::uint32_t d_len[RING];
+  std::uint32_t d_len[RING], d_idx[RING];
   auto fetch = [&](std::uint32_t j, int slot) {
     const std::uint64_t b = b0 + kPer * static_cast<std::uint64_t>(j) + grp;
     const std::uint64_t bc = b < b1 ? b : b1 - 1u;  // clamped: every load stays inside the arrays
-    d_off[slot] = a.l_off[bc];
-    d_len[slot] = a.l_len[bc];
+    if constexpr (LIST) {
+      d_off[slot] = a.s_off[bc];
+      d_len[slot] = a.s_len[bc];
+      d_idx[slot] = a.s_idx[bc];
+    } else {
+      d_off[slot] = a.l_off[bc];
+      d_len[slot] = a.l_len[bc];
+      d_idx[slot] = static_cast<std::uint32_t>(bc);
+    }
   };
   uint4 q[RING][kLaneGran];
-  std::uint32_t m_len[RING], m_o[RING], m_init[RING], m_ishift[RING];
+  std::uint32_t m_len[RING], m_o[RING], m_ishift[RING], m_idx[RING];
   std::int32_t m_lead[RING];
   auto issue = [&](int slot, std::uint32_t j) {
     const std::uint64_t b = b0 + kPer * static_cast<std::uint64_t>(j) + grp;
     const std::uint32_t len0 = d_len[slot];
-    const bool live = j < ns && b < b1 && len0 > kLo && len0 <= kSlot && (a.l_tile[b / 4096u] & kFlag);
+    const bool live = j < ns && b < b1 && len0 <= kSlot && (LIST || (len0 > kLo && (a.l_tile[b / 4096u] & kFlag)));
     const std::uint32_t len = live ? len0 : 0u;
     const std::uintptr_t blo = base + d_off[slot], bhi = blo + len;
     const std::int32_t c_lane = static_cast<std::int32_t>(len) - static_cast<std::int32_t>(kSlot) +
@@ -1842,9 +1746,13 @@ __device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32
     }
     m_len[slot] = live ? len : 0xFFFFFFFFu;  // 0xFFFFFFFF: nothing to fold or store
     m_o[slot] = static_cast<std::uint32_t>(p & 15u);
-    m_lead[slot] = -c_lane;  // bytes of the lane's window in front of the block
-    m_init[slot] = a.init_raw ? a.init_raw[live ? b : b0] : a.init_default;
+    m_lead[slot] = -c_lane;     // bytes of the lane's window in front of the block
+    if constexpr (LIST) m_idx[slot] = d_idx[slot];  // (a valid batch index even in a dead slot)
     m_ishift[slot] = a.tabs->init_shift[len];  // Shift_len(0xFFFFFFFF), the reference's init (crc32.hpp:39)
+  };
+  auto out_idx = [&](int slot, std::uint32_t j) -> std::uint64_t {  // the block's batch index (live slots)
+    if constexpr (LIST) return m_idx[slot];
+    return b0 + kPer * static_cast<std::uint64_t>(j) + grp;
   };
   auto fold = [&](int slot, std::uint32_t j) {
     const std::uint32_t len = m_len[slot];
@@ -1863,7 +1771,8 @@ __device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32
     std::uint32_t v = lane_shift(lds, p.value(), kc);
     const std::uint32_t L = live ? len : 0u;
     if (a.init_raw) {
-      const std::uint32_t init = m_init[slot];
+      // per-block registers (a rare path): loaded here rather than carried through the ring
+      const std::uint32_t init = a.init_raw[live || LIST ? out_idx(slot, j) : b0];
 #pragma unroll
       for (std::uint32_t i = 0; i < 32u / G; ++i) {
         const std::uint32_t bit = gl * (32u / G) + i;
@@ -1874,7 +1783,7 @@ __device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32
       v ^= m_ishift[slot];
     }
     v = group_xor<G>(v);  // every lane of the group holds the group's sum
-    if (live && gl == G - 1u) a.out[b0 + kPer * static_cast<std::uint64_t>(j) + grp] = v ^ a.out_xor;
+    if (live && gl == G - 1u) a.out[out_idx(slot, j)] = v ^ a.out_xor;
   };
 
 #pragma unroll
@@ -1893,6 +1802,23 @@ __device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32
       if (t + k < ns) fold(k, t + k);
     }
   }
+}
+
+template <int G>
+__device__ __forceinline__ void group_phase(const RowsArgs& a, const std::uint32_t* lds) {
+  group_walk<G, false>(a, lds, 0u, 0u);
+}
+
+// Small blocks of an irregular batch (len <= kSmallMax = 1 KiB, listed by the prepass in
+// s_off/s_len/s_idx by class): 4-lane groups for blocks of at most kGroupMax bytes, 8-lane groups up
+// to kGroup8Max, 16-lane groups for the rest. Runs inside the irregular row kernel, before its rows,
+// on the same partition of waves.
+__device__ __forceinline__ void small_phase(const RowsArgs& a, const std::uint32_t* lds) {
+  const std::uint32_t ns = sload32(a.counts, 1), n4 = sload32(a.counts, kCountSmall4);
+  const std::uint32_t n8 = sload32(a.counts, kCountSmall8);
+  if (n4) group_walk<4, true>(a, lds, 0u, n4);
+  if (n8) group_walk<8, true>(a, lds, n4, n8);
+  if (ns - n4 - n8) group_walk<16, true>(a, lds, n4 + n8, ns - n4 - n8);
 }
 
 // Combine the partials of blocks that were split between waves: one thread per seam record (two

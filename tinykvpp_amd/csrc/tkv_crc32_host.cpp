@@ -81,7 +81,7 @@ void build_tables(DeviceTables* t, std::uint32_t poly) {
   const auto x8n = [poly](std::uint64_t n) { return x8nmodp(n, poly); };
   t->poly = poly;
   t->pad_[0] = t->pad_[1] = 0;
-  for (std::uint32_t h = 0; h <= kGroup8Max; ++h) t->init_shift[h] = mm(x8n(h), 0xFFFFFFFFu);
+  for (std::uint32_t h = 0; h <= kSmallMax; ++h) t->init_shift[h] = mm(x8n(h), 0xFFFFFFFFu);
   for (std::uint32_t i = 0; i < 256; ++i) {
     std::uint32_t c = i;
     for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? poly : 0u);
@@ -388,15 +388,16 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
       s->cap_blocks = 0;
     }
     const std::uint64_t ntiles = prepass_tiles(cap) + 1;
-    // 8-byte arrays first: scan, tiles, s_off, big_off; then the 4-byte ones
-    const std::uint64_t bytes = 8 * (cap + ntiles + 2 * cap) + 4 * (6 * cap + 1) + 4 * 2 * ntiles + 16;
+    // 8-byte arrays first: scan, tiles, s_off, big_off, tile_cls; then the 4-byte ones
+    const std::uint64_t bytes = 8 * (cap + 2 * ntiles + 2 * cap) + 4 * (7 * cap + 1) + 4 * 2 * ntiles + 32;
     TKV_HIP(hipMalloc(&s->blob, bytes));
     auto* p8 = static_cast<std::uint64_t*>(s->blob);
     s->scan = p8;
     s->tiles = p8 + cap;
     s->po.s_off = p8 + cap + ntiles;
     s->po.big_off = p8 + 2 * cap + ntiles;
-    auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 3 * cap + ntiles);
+    s->po.tile_cls = p8 + 3 * cap + ntiles;
+    auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 3 * cap + 2 * ntiles);
     s->po.s_len = p4;
     s->po.s_idx = p4 + cap;
     s->po.big_len = p4 + 2 * cap;
@@ -407,6 +408,7 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     // cap entries, 16-byte aligned (rows_tile_scan stores them 16 bytes at a time)
     s->po.lscan = reinterpret_cast<std::uint32_t*>(
         (reinterpret_cast<std::uintptr_t>(s->po.tile_lanes + ntiles) + 15) & ~static_cast<std::uintptr_t>(15));
+    s->po.cscan = s->po.lscan + ((cap + 3) & ~static_cast<std::uint64_t>(3));  // also 16-byte aligned
     s->cap_blocks = cap;
   }
   s->po.wave_start = s->wave_start;
@@ -1366,6 +1368,16 @@ int read_count_word(void* stream, int word) {
 int tkv_debug_irregular_mode(void* stream) { return read_count_word(stream, 3); }
 
 int tkv_debug_irregular_phases(void* stream) { return read_count_word(stream, kCountPhases); }
+
+int tkv_debug_irregular_lists(void* stream, std::uint32_t out[3]) {
+  const int w[3] = {1, kCountSmall4, kCountSmall8};
+  for (int i = 0; i < 3; ++i) {
+    const int v = read_count_word(stream, w[i]);
+    if (v == -1) return -1;
+    out[i] = static_cast<std::uint32_t>(v);
+  }
+  return 0;
+}
 
 int tkv_debug_set_host_mapped(int enable) { return tkv::g_host_mapped.exchange(enable ? 1 : 0); }
 

@@ -53,7 +53,7 @@ struct DeviceTables {
   std::uint32_t inv_shift[kRow + 1];    // [d] = x^(-8d) mod P: moves a register back by d bytes (stream)
   std::uint32_t poly;                   // reflected polynomial the tables were built for
   std::uint32_t pad_[2];
-  std::uint32_t init_shift[512 + 1];    // [h] = Shift_h(0xFFFFFFFF): the init term of a group-phase block
+  std::uint32_t init_shift[1024 + 1];   // [h] = Shift_h(0xFFFFFFFF): the init term of a group-walk block
 };
 
 // One partial result of a block that was split between waves (irregular / huge-block path).
@@ -118,6 +118,12 @@ constexpr int kCountLanes = 8;
 // kTileLanes / kTileGroups / kTileGroups8, shifted down by 1): 1 = lane blocks, 2 / 4 = group blocks
 // of 4- / 8-lane groups
 constexpr int kCountPhases = 9;
+// counts[kCountSmall4], counts[kCountSmall8]: listed small blocks of at most kGroupMax bytes (the first
+// entries of s_off/s_len/s_idx) and of kGroupMax + 1 .. kGroup8Max bytes (the next ones); the rest of
+// the counts[1] listed blocks (kGroup8Max + 1 .. kSmallMax bytes) follow them. The small-block phase
+// folds each class with groups of 4, 8 or 16 lanes.
+constexpr int kCountSmall4 = 10;
+constexpr int kCountSmall8 = 11;
 
 // Blocks of at most kLaneMax bytes are folded whole by one lane each, from their own initial register
 // (DESIGN.md §4.5): uniform batches by crc_lanes, irregular ones by the lane phase in crc_stream's
@@ -145,8 +151,14 @@ constexpr std::uint32_t kGroup8Max = 512;
 // walking a tile of 257-1024-byte blocks, 300-1000 B payloads ran at 2270 against 3160 GB/s for the
 // small phase (profiles/r4/s1/probe_irregular.jsonl).
 constexpr std::uint32_t kLaneDenseTile = 256;
-constexpr std::uint32_t kGroupDenseTile = 1024;
-constexpr std::uint32_t kGroup8DenseTile = 2048;
+#ifndef TKV_AB_GROUP_DENSE  // (A/B builds only: tools/build_at.sh -DTKV_AB_GROUP_DENSE=...)
+#define TKV_AB_GROUP_DENSE 1024
+#endif
+#ifndef TKV_AB_GROUP8_DENSE
+#define TKV_AB_GROUP8_DENSE 2048
+#endif
+constexpr std::uint32_t kGroupDenseTile = TKV_AB_GROUP_DENSE;
+constexpr std::uint32_t kGroup8DenseTile = TKV_AB_GROUP8_DENSE;
 constexpr std::uint64_t kGroupTileRows = 1024;
 // Per-tile flags (tile_ok):
 constexpr std::uint32_t kTileStream = 1u;     // the tile's blocks qualify for stream mode
@@ -183,10 +195,14 @@ struct PrepassOut {
   std::uint32_t* wave_start;
   std::uint32_t* lscan;       // per block: lane blocks in front of it (exclusive, within its tile)
   std::uint32_t* tile_lanes;  // per scan tile: its lane blocks (then their exclusive scan)
+  // per block: listed blocks of kGroupMax + 1 .. kGroup8Max bytes in front of it (low half) and of
+  // kGroup8Max + 1 .. kSmallMax bytes (high half), exclusive, within its tile
+  std::uint32_t* cscan;
+  std::uint64_t* tile_cls;    // per scan tile: the same two counts over the tile (low, high word), then scanned
 };
 
-// Blocks of at most kSmallMax bytes are folded four to a wave (16 lanes x 64 B each) by the
-// small-block phase instead of occupying a whole 4 KiB row each.
+// Blocks of at most kSmallMax bytes are listed by class (kCountSmall4) and folded by the small-block
+// phase, a group of 4, 8 or 16 lanes (64 B each) per block, instead of occupying a whole 4 KiB row each.
 constexpr std::uint32_t kSmallMax = 1024;
 
 // Irregular batches carry u32 block indices (prepass scan, compacted lists, results): the host caps

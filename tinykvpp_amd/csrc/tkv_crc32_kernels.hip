@@ -21,6 +21,8 @@
 //    partials that crc_fixup combines with x^(8*4096*k) mod P products.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "tkv_crc32_device.h"
 
 namespace tkv {
@@ -200,24 +202,24 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small_gen(RowsArgs a) {
 }
 
 // Uniform batches of blocks of at most kLaneMax bytes (any stride, alignment, initial registers): one
-// lane per block. Only the slicing tables go to LDS (128 KiB).
-// Pipeline shapes (in-process A/B over 16-64 B blocks, profiles/r3/lanes/ab_shapes.jsonl): aligned
-// blocks DEPTH 4 / ILP 2; unaligned ones of at most 48 bytes DEPTH 3 / ILP 1 (ILP 2 spills there: 26 B
-// 3445 -> 3917 GB/s), longer unaligned ones DEPTH 4 / ILP 2 (59 B 3806 -> 4082 GB/s).
-template <int ALIGN, int DEPTH, int ILP>
-__global__ __launch_bounds__(kThreads) void crc_lanes(RowsArgs a) {
-  __shared__ std::uint32_t lds[kLdsSliceWords];
-  dev::crc_lanes_body<ALIGN, DEPTH, ILP, kPackedPrio>(a, lds);
-}
-constexpr std::uint32_t kLanesShortMax = 48;
-
-// Uniform lane batches with an exact-size window of NG granules and a deeper pipeline (round 4,
-// DESIGN.md §4.5): DEPTH 8 at NG <= 2, 6 at NG 3, 5 at NG 4, 4 at NG 5, ILP 1.
+// lane per block, a window of exactly the NG granules a block can touch and DEPTH 8 at NG <= 2, 6 at
+// NG 3, 5 at NG 4, 4 at NG 5, ILP 1. Only the slicing tables go to LDS (128 KiB).
+// In one process against the five-granule DEPTH 3-4 kernel of round 3 (profiles/r4/lanes_ab/):
+// 26 B 3544 -> 3825 GB/s, 16 B 3615 -> 3720, 28 B 3877 -> 4044, 36 B and 59 B unchanged.
 template <int ALIGN, int NG>
 __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
   constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? 5 : 4;
   __shared__ std::uint32_t lds[kLdsSliceWords];
   dev::crc_lanes_n_body<ALIGN, NG, DEPTH, 1, kPackedPrio>(a, lds);
+}
+
+// The same batches of 4..kLaneMax-byte blocks (dword-aligned or not) read dword by dword with no
+// realignment (crc_lanes_d_body): NF = len / 4 whole dwords; DEPTH by registers per block.
+template <int ALIGN, int NF>
+__global__ __launch_bounds__(kThreads) void crc_lanes_d(RowsArgs a) {
+  constexpr int DEPTH = NF <= 4 ? 8 : NF <= 8 ? 7 : NF <= 12 ? 6 : 5;
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  dev::crc_lanes_d_body<ALIGN, NF, DEPTH, kPackedPrio>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
@@ -269,6 +271,7 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
                                                               std::uint64_t* scan, std::uint64_t* tile_sums,
                                                               std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
                                                               std::uint32_t* lscan, std::uint32_t* tile_lanes,
+                                                              std::uint32_t* cscan, std::uint64_t* tile_cls,
                                                               std::uint32_t group_stream) {
   constexpr unsigned kTileWaves = kTileThreads / 64;
   constexpr unsigned kTileBpt = kScanTile / kTileThreads;
@@ -283,10 +286,11 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   }
   const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * kTileBpt;
   const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  // Every block first counts as a small or large one (v); lane blocks and the two group classes are
-  // also counted in one packed u64 (16 bits each, lane blocks lowest, then 4- and 8-lane group blocks:
-  // a tile has at most 4096 of each), so the one scan below yields all of them, and the tile's verdict
-  // on them (below) only subtracts.
+  // Every block first counts as a small or large one (v); lane blocks, the two group classes and the
+  // small blocks over kGroup8Max bytes are also counted in one packed u64 (16 bits each, lane blocks
+  // lowest, then 4- and 8-lane group blocks, then the rest up to kSmallMax: a tile has at most 4096 of
+  // each), so the one scan below yields all of them, and the tile's verdict on them (below) only
+  // subtracts. The last two fields also place listed small blocks in their class's list (cscan).
   std::uint64_t pk[kTileBpt];
   std::uint64_t v[kTileBpt], s = 0;
   std::uint64_t ls = 0;
@@ -308,6 +312,7 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
             : len[i] <= kLaneMax    ? 1ull
             : len[i] <= kGroupMax   ? 1ull << 16
             : len[i] <= kGroup8Max  ? 1ull << 32
+            : len[i] <= kSmallMax   ? 1ull << 48
                                     : 0ull;
     v[i] = in ? scan_item(len[i]) : 0ull;
     s += v[i];
@@ -364,7 +369,13 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
                               ((tph & kTileGroups8) ? 0xFFFFull << 32 : 0ull);
   auto taken = [&](std::uint64_t x) {  // the phase blocks among packed counts x
     x &= tmask;
-    return static_cast<std::uint32_t>((x & 0xFFFFu) + ((x >> 16) & 0xFFFFu) + ((x >> 32) & 0xFFFFu) + (x >> 48));
+    return static_cast<std::uint32_t>((x & 0xFFFFu) + ((x >> 16) & 0xFFFFu) + ((x >> 32) & 0xFFFFu));
+  };
+  // listed blocks of kGroupMax + 1 .. kGroup8Max bytes (none when the 8-lane pass takes them) and of
+  // kGroup8Max + 1 .. kSmallMax bytes among packed counts x, as the low and high half of a u32
+  const std::uint64_t c8mask = (tph & kTileGroups8) ? 0ull : 0xFFFFull << 32;
+  auto cls_pair = [&](std::uint64_t x) {
+    return static_cast<std::uint32_t>(((x & c8mask) >> 32) | ((x >> 48) << 16));
   };
   // A tile dense in group blocks does not qualify for stream mode (unless group_stream, a debug
   // setting): the group phase folds 65-256-byte blocks at the rate of gapped ones, where the stream
@@ -378,18 +389,24 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   std::uint64_t lrun = lpre + linc - ls;
   if (tph == 0 && base + kTileBpt <= n) {
     // every block of such a tile is listed: this thread's entries as whole 16-byte stores
-    // (scan and lscan are 256-byte aligned scratch, base a multiple of kTileBpt >= 4)
+    // (scan, lscan and cscan are 16-byte aligned scratch, base a multiple of kTileBpt >= 4)
     std::uint64_t sc[kTileBpt];
+    std::uint32_t cs[kTileBpt];
 #pragma unroll
     for (unsigned i = 0; i < kTileBpt; ++i) {
       sc[i] = run;
+      cs[i] = cls_pair(lrun);
       run += v[i];
+      lrun += pk[i];
     }
 #pragma unroll
     for (unsigned i = 0; i < kTileBpt; i += 2)
       *reinterpret_cast<ulonglong2*>(scan + base + i) = make_ulonglong2(sc[i], sc[i + 1]);
 #pragma unroll
-    for (unsigned i = 0; i < kTileBpt; i += 4) *reinterpret_cast<uint4*>(lscan + base + i) = make_uint4(0, 0, 0, 0);
+    for (unsigned i = 0; i < kTileBpt; i += 4) {
+      *reinterpret_cast<uint4*>(lscan + base + i) = make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(cscan + base + i) = make_uint4(cs[i], cs[i + 1], cs[i + 2], cs[i + 3]);
+    }
   } else {
 #pragma unroll
     for (unsigned i = 0; i < kTileBpt; ++i) {
@@ -397,6 +414,7 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
         const std::uint32_t t = taken(lrun);
         scan[base + i] = run - t;  // (t <= the small count in run's low half: no borrow)
         lscan[base + i] = t;
+        cscan[base + i] = cls_pair(lrun);
       }
       run += v[i];
       lrun += pk[i];
@@ -406,6 +424,8 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     const std::uint32_t tl = taken(ltot);
     tile_sums[blockIdx.x] = tot - tl;
     tile_lanes[blockIdx.x] = tl;
+    const std::uint32_t tc = cls_pair(ltot);
+    tile_cls[blockIdx.x] = (tc & 0xFFFFu) | (static_cast<std::uint64_t>(tc >> 16) << 32);
   }
 }
 
@@ -415,15 +435,15 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
 __device__ __forceinline__ StreamGeom stream_geometry(const std::uint8_t* base, const std::uint64_t* offsets,
                                                       const std::uint32_t* lengths, std::uint32_t n);
 __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums, std::uint32_t* tile_lanes,
-                                                       std::uint32_t ntiles, std::uint32_t n, std::uint32_t* counts,
+                                                       std::uint64_t* tile_cls, std::uint32_t ntiles, std::uint32_t n, std::uint32_t* counts,
                                                        const std::uint32_t* tile_ok, const std::uint8_t* base,
                                                        const std::uint64_t* offsets, const std::uint32_t* lengths,
                                                        std::uint64_t* sinfo) {
-  __shared__ std::uint64_t part[1024];
+  __shared__ std::uint64_t part[1024], cpart[1024];
   __shared__ std::uint32_t lpart[1024];
   __shared__ std::uint32_t sph;
   if (threadIdx.x == 0) sph = 0;  // (the loop's first barrier orders this before the ORs below)
-  std::uint64_t carry = 0, lcarry = 0;
+  std::uint64_t carry = 0, lcarry = 0, ccarry = 0;
   bool all_stream = true;
   std::uint32_t ph = 0;  // kTilePhases flags over the tiles
   for (std::uint32_t t0 = 0; t0 < ntiles; t0 += 1024) {
@@ -432,26 +452,33 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
     ph |= i < ntiles ? tile_ok[i] & kTilePhases : 0u;
     const std::uint64_t x = i < ntiles ? tile_sums[i] : 0ull;
     const std::uint32_t lx = i < ntiles ? tile_lanes[i] : 0u;
+    const std::uint64_t cx = i < ntiles ? tile_cls[i] : 0ull;
     part[threadIdx.x] = x;
     lpart[threadIdx.x] = lx;
+    cpart[threadIdx.x] = cx;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {
       const std::uint64_t y = threadIdx.x >= static_cast<unsigned>(off) ? part[threadIdx.x - off] : 0ull;
       const std::uint32_t ly = threadIdx.x >= static_cast<unsigned>(off) ? lpart[threadIdx.x - off] : 0u;
+      const std::uint64_t cy = threadIdx.x >= static_cast<unsigned>(off) ? cpart[threadIdx.x - off] : 0ull;
       __syncthreads();
       part[threadIdx.x] += y;
       lpart[threadIdx.x] += ly;
+      cpart[threadIdx.x] += cy;
       __syncthreads();
     }
     if (i < ntiles) {
       tile_sums[i] = carry + part[threadIdx.x] - x;  // exclusive tile offsets
       tile_lanes[i] = static_cast<std::uint32_t>(lcarry + lpart[threadIdx.x] - lx);
+      tile_cls[i] = ccarry + cpart[threadIdx.x] - cx;
     }
     const std::uint64_t tot = part[1023];
     const std::uint32_t ltot = lpart[1023];
+    const std::uint64_t ctot = cpart[1023];
     __syncthreads();
     carry += tot;
     lcarry += ltot;
+    ccarry += ctot;
   }
 #pragma unroll
   for (unsigned m = 32; m > 0; m >>= 1) ph |= __shfl_xor(ph, m, 64);
@@ -466,6 +493,8 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
       counts[2] = static_cast<std::uint32_t>(g.rows);
       counts[3] = kModeStream;
       counts[kCountLanes] = 0;  // every block is longer than kLaneMax in stream mode
+      counts[kCountSmall4] = 0;
+      counts[kCountSmall8] = 0;
       sinfo[0] = g.zoff;
       sinfo[1] = g.s0rel;
       return;
@@ -476,6 +505,8 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
     counts[2] = static_cast<std::uint32_t>(carry >> 32);  // rows of the large blocks
     counts[3] = 0;                                         // general path
     counts[kCountLanes] = nl;                              // lane blocks
+    counts[kCountSmall8] = static_cast<std::uint32_t>(ccarry);
+    counts[kCountSmall4] = ns - static_cast<std::uint32_t>(ccarry) - static_cast<std::uint32_t>(ccarry >> 32);
   }
 }
 
@@ -485,14 +516,18 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
 // result zeroed here, since the row kernel XORs every piece of it into the result (crc_rows_body,
 // irregular batches). len and off are the block's length and offset (loaded by the caller).
 __device__ __forceinline__ void finish_block(std::uint64_t off, std::uint32_t len, std::uint64_t b, std::uint64_t e,
-                                             std::uint64_t nlane, std::uint64_t TR, const PrepassOut& o,
+                                             std::uint64_t nlane, std::uint64_t cpre, std::uint32_t n4,
+                                             std::uint32_t n8, std::uint64_t TR, const PrepassOut& o,
                                              std::uint32_t W, std::uint32_t* out, std::uint32_t tk) {
   if (phase_block(len, tk)) return;  // the lane or group phase's (in a sparse tile it is small)
   const std::uint32_t nsmall = static_cast<std::uint32_t>(e);
   if (len <= kSmallMax) {
-    o.s_off[nsmall] = off;
-    o.s_len[nsmall] = len;
-    o.s_idx[nsmall] = static_cast<std::uint32_t>(b);
+    // class lists one after the other: [0, n4) up to kGroupMax bytes, then n8 up to kGroup8Max, then the rest
+    const std::uint32_t c8 = static_cast<std::uint32_t>(cpre), c16 = static_cast<std::uint32_t>(cpre >> 32);
+    const std::uint32_t pos = len <= kGroupMax ? nsmall - c8 - c16 : len <= kGroup8Max ? n4 + c8 : n4 + n8 + c16;
+    o.s_off[pos] = off;
+    o.s_len[pos] = len;
+    o.s_idx[pos] = static_cast<std::uint32_t>(b);
     return;
   }
   const std::uint32_t k = static_cast<std::uint32_t>(b - nsmall - nlane);  // compacted index
@@ -533,7 +568,10 @@ __global__ void rows_finish(const std::uint8_t* base, const std::uint64_t* offse
     return;
   }
   if (phase_block(len, tk)) return;  // the lane or group phase's
-  finish_block(offsets[b], len, b, scan[b] + tile_offs[t], o.lscan[b] + o.tile_lanes[t], counts[2], o, W, out, tk);
+  const std::uint32_t cs = o.cscan[b];
+  const std::uint64_t cpre = o.tile_cls[t] + (cs & 0xFFFFu) + (static_cast<std::uint64_t>(cs >> 16) << 32);
+  finish_block(offsets[b], len, b, scan[b] + tile_offs[t], o.lscan[b] + o.tile_lanes[t], cpre,
+               dev::sload32(counts, kCountSmall4), dev::sload32(counts, kCountSmall8), counts[2], o, W, out, tk);
 }
 
 // rows_finish with the scan of the tile sums folded in (ntiles <= kFusedTiles): every workgroup sums
@@ -558,6 +596,8 @@ __device__ __forceinline__ void stream_block(const std::uint8_t* base, const std
     counts[2] = static_cast<std::uint32_t>(g.rows);
     counts[3] = kModeStream;
     counts[kCountLanes] = 0;  // every block is longer than kLaneMax in stream mode
+    counts[kCountSmall4] = 0;
+    counts[kCountSmall8] = 0;
     sinfo[0] = g.zoff;
     sinfo[1] = g.s0rel;
   }
@@ -576,7 +616,7 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     std::uint32_t* counts, PrepassOut o, std::uint32_t W, std::uint32_t* out, std::uint64_t* ends,
     std::uint64_t* sinfo, std::uint32_t Ws, const std::uint32_t* row0) {
   constexpr std::uint32_t kWaves = kFinishThreads / 64;
-  __shared__ std::uint64_t red[6][kWaves];
+  __shared__ std::uint64_t red[8][kWaves];
   const std::uint32_t my_tile = blockIdx.x * kFinishThreads / kScanTile;  // kScanTile % 256 == 0
   // The block's own operands are loaded first, so their latency overlaps the tile-sum reduction (the
   // scan values of a lane block were never written and are not used).
@@ -586,17 +626,21 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
   const std::uint64_t off = live ? offsets[b] : 0ull;
   const std::uint64_t sc = live ? scan[b] : 0ull;
   const std::uint32_t lsc = live ? o.lscan[b] : 0u;
+  const std::uint32_t csc = live ? o.cscan[b] : 0u;
   const std::uint32_t mtk = tile_ok[my_tile];
-  std::uint64_t before = 0, all = 0, bad = 0, lbefore = 0, lall = 0;
+  std::uint64_t before = 0, all = 0, bad = 0, lbefore = 0, lall = 0, cbefore = 0, call = 0;
   std::uint32_t ph = 0;  // kTilePhases flags over the tiles
   for (std::uint32_t i = threadIdx.x; i < ntiles; i += kFinishThreads) {
     const std::uint64_t v = tile_sums[i];
     const std::uint64_t lv = o.tile_lanes[i];
+    const std::uint64_t cv = o.tile_cls[i];
     const std::uint32_t tk = tile_ok[i];
     all += v;
     before += i < my_tile ? v : 0ull;
     lall += lv;
     lbefore += i < my_tile ? lv : 0ull;
+    call += cv;
+    cbefore += i < my_tile ? cv : 0ull;
     bad += (tk & kTileStream) ? 0u : 1u;
     ph |= tk & kTilePhases;
   }
@@ -608,6 +652,8 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     bad += __shfl_xor(bad, m, 64);
     lbefore += __shfl_xor(lbefore, m, 64);
     lall += __shfl_xor(lall, m, 64);
+    cbefore += __shfl_xor(cbefore, m, 64);
+    call += __shfl_xor(call, m, 64);
     ph |= __shfl_xor(ph, m, 64);
   }
   const unsigned wid = threadIdx.x >> 6;
@@ -618,9 +664,11 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     red[3][wid] = lbefore;
     red[4][wid] = lall;
     red[5][wid] = ph;
+    red[6][wid] = cbefore;
+    red[7][wid] = call;
   }
   __syncthreads();
-  std::uint64_t tile_off = 0, total = 0, nbad = 0, tile_loff = 0, ltotal = 0, aph = 0;
+  std::uint64_t tile_off = 0, total = 0, nbad = 0, tile_loff = 0, ltotal = 0, aph = 0, tile_coff = 0, ctotal = 0;
 #pragma unroll
   for (unsigned w = 0; w < kWaves; ++w) {
     tile_off += red[0][w];
@@ -629,6 +677,8 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     tile_loff += red[3][w];
     ltotal += red[4][w];
     aph |= red[5][w];
+    tile_coff += red[6][w];
+    ctotal += red[7][w];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) counts[kCountPhases] = nbad == 0 ? 0u : static_cast<std::uint32_t>(aph) >> 1;
   if (nbad == 0) {  // every block qualifies: stream mode
@@ -643,8 +693,15 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     counts[3] = 0;                                         // general path
     counts[kCountLanes] = nl;                              // lane blocks (crc_stream's lane phase)
   }
+  const std::uint32_t n8 = static_cast<std::uint32_t>(ctotal);
+  const std::uint32_t n4 = static_cast<std::uint32_t>(total) - n8 - static_cast<std::uint32_t>(ctotal >> 32);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    counts[kCountSmall4] = n4;
+    counts[kCountSmall8] = n8;
+  }
   if (!live) return;
-  finish_block(off, len, b, sc + tile_off, lsc + tile_loff, total >> 32, o, W, out, mtk);
+  const std::uint64_t cpre = tile_coff + (csc & 0xFFFFu) + (static_cast<std::uint64_t>(csc >> 16) << 32);
+  finish_block(off, len, b, sc + tile_off, lsc + tile_loff, cpre, n4, n8, total >> 32, o, W, out, mtk);
 }
 
 
@@ -858,6 +915,16 @@ hipError_t launch_packed_small_gen(const RowsArgs& a, unsigned grid, hipStream_t
   return hipGetLastError();
 }
 
+// A/B switch for the dword-by-dword lane kernel (TKV_LANES_DIRECT: 0 off, 1 dword-aligned blocks
+// only, 2 also byte-aligned ones); read once.
+int lanes_direct() {
+  static const int v = [] {
+    const char* e = std::getenv("TKV_LANES_DIRECT");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
 // Uniform lane-block batch (a.len <= kLaneMax): ALIGN from the base pointer and the stride.
 hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st) {
   if (a.len > kLaneMax) return hipErrorInvalidValue;
@@ -874,10 +941,34 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st) {
     case 4: hipLaunchKernelGGL((crc_lanes_n<A, 4>), g, b, 0, st, a); break;             \
     default: hipLaunchKernelGGL((crc_lanes_n<A, 5>), g, b, 0, st, a); break;            \
   }
+#define TKV_LANES_D(A)                                                                                   \
+  switch (a.len >> 2) {                                                                                  \
+    case 1: hipLaunchKernelGGL((crc_lanes_d<A, 1>), g, b, 0, st, a); break;                              \
+    case 2: hipLaunchKernelGGL((crc_lanes_d<A, 2>), g, b, 0, st, a); break;                              \
+    case 3: hipLaunchKernelGGL((crc_lanes_d<A, 3>), g, b, 0, st, a); break;                              \
+    case 4: hipLaunchKernelGGL((crc_lanes_d<A, 4>), g, b, 0, st, a); break;                              \
+    case 5: hipLaunchKernelGGL((crc_lanes_d<A, 5>), g, b, 0, st, a); break;                              \
+    case 6: hipLaunchKernelGGL((crc_lanes_d<A, 6>), g, b, 0, st, a); break;                              \
+    case 7: hipLaunchKernelGGL((crc_lanes_d<A, 7>), g, b, 0, st, a); break;                              \
+    case 8: hipLaunchKernelGGL((crc_lanes_d<A, 8>), g, b, 0, st, a); break;                              \
+    case 9: hipLaunchKernelGGL((crc_lanes_d<A, 9>), g, b, 0, st, a); break;                              \
+    case 10: hipLaunchKernelGGL((crc_lanes_d<A, 10>), g, b, 0, st, a); break;                            \
+    case 11: hipLaunchKernelGGL((crc_lanes_d<A, 11>), g, b, 0, st, a); break;                            \
+    case 12: hipLaunchKernelGGL((crc_lanes_d<A, 12>), g, b, 0, st, a); break;                            \
+    case 13: hipLaunchKernelGGL((crc_lanes_d<A, 13>), g, b, 0, st, a); break;                            \
+    case 14: hipLaunchKernelGGL((crc_lanes_d<A, 14>), g, b, 0, st, a); break;                            \
+    case 15: hipLaunchKernelGGL((crc_lanes_d<A, 15>), g, b, 0, st, a); break;                            \
+    default: hipLaunchKernelGGL((crc_lanes_d<A, 16>), g, b, 0, st, a); break;                            \
+  }
   if (align == 16) { TKV_LANES_N(16) }
-  else if (align == 4) { TKV_LANES_N(4) }
+  else if (a.len < 4u || lanes_direct() == 0) {
+    if (align == 4) { TKV_LANES_N(4) }
+    else { TKV_LANES_N(1) }
+  } else if (align == 4) { TKV_LANES_D(4) }
+  else if (lanes_direct() == 2) { TKV_LANES_D(1) }
   else { TKV_LANES_N(1) }
 #undef TKV_LANES_N
+#undef TKV_LANES_D
   return hipGetLastError();
 }
 
@@ -899,16 +990,18 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
   const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
   if (ntiles <= kFusedTiles)
     hipLaunchKernelGGL(rows_tile_scan<1024>, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets,
-                       lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, group_stream);
+                       lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
+                       group_stream);
   else
     hipLaunchKernelGGL(rows_tile_scan<512>, dim3(static_cast<unsigned>(ntiles)), dim3(512), 0, st, base, offsets,
-                       lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, group_stream);
+                       lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
+                       group_stream);
   if (ntiles <= kFusedTiles) {
     hipLaunchKernelGGL(rows_finish_fused, dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
                        offsets, lengths, n, scan, tile_sums, tile_ok, static_cast<std::uint32_t>(ntiles), counts, o,
                        W, out, ends, sinfo, Ws, row0);
   } else {
-    hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, o.tile_lanes,
+    hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, o.tile_lanes, o.tile_cls,
                        static_cast<std::uint32_t>(ntiles), n, counts, tile_ok, base, offsets, lengths, sinfo);
     hipLaunchKernelGGL(rows_finish, dim3(static_cast<unsigned>(nfinish)), dim3(256), 0, st, base, offsets, lengths,
                        n, scan, tile_sums, counts, tile_ok, o, W, out, ends, sinfo, Ws, row0);

@@ -9,7 +9,7 @@ git archive "$REV" tinykvpp_amd/csrc include | tar -x -C "$T"
 H=$T/tinykvpp_amd/csrc
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$T/include -I$H"
 mkdir -p tools/ab
-for s in tkv_crc32_kernels.hip tkv_wal_device.hip; do /opt/rocm/bin/hipcc $F "$@" -c $H/$s -o $T/${s%.*}.o & done
+for f in $H/*.hip; do s=$(basename $f); /opt/rocm/bin/hipcc $F "$@" -c $H/$s -o $T/${s%.*}.o & done
 for s in tkv_crc32_host.cpp tkv_formats.cpp tkv_crc32_span.cpp; do /opt/rocm/bin/hipcc $F "$@" -x hip -c $H/$s -o $T/${s%.*}.o & done
 wait
 echo "extern \"C\" const char* tkv_build_id(void) { return \"rev-$REV\"; }" > $T/id.cpp

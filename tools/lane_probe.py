@@ -101,6 +101,10 @@ def main():
         work.append(irregular(f"irregular {lo}-{hi} B, 8 B gaps", rng.integers(lo, hi + 1, ng), np.full(ng, 8), 8))
     ng = count(650, 650)
     work.append(irregular("irregular back to back 300-1000 B", rng.integers(300, 1001, ng), np.zeros(ng, np.int64), 0))
+    ng = count(512, 520)
+    work.append(irregular("irregular 0-1024 B, 8 B gaps", rng.integers(0, 1025, ng), np.full(ng, 8), 8))
+    ng = count(450, 458)
+    work.append(irregular("irregular 200-700 B, 8 B gaps", rng.integers(200, 701, ng), np.full(ng, 8), 8))
     n = count(2048, 2056)
     lr = rng.integers(0, 4097, n)
     work.append(irregular("irregular 0-4 KiB, 8 B gaps", lr, np.full(n, 8), 8))
