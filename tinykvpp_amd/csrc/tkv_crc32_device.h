@@ -1518,96 +1518,6 @@ __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_
   }
 }
 
-// Uniform lane batches loaded dword by dword (round 4): a block of len = 4 NF + tb bytes (4 <= len
-// <= kLaneMax) is read with exactly its own bytes, no 16-byte granules and no realignment: NF whole
-// dwords as ceil(NF / 4) dword-aligned or byte-aligned 16-byte loads (the last one anchored at the
-// last whole dword, overlapping its predecessor, so no load reaches past the block), and for tb > 0
-// the dword holding the tail bytes: the aligned dword at 4 NF when the blocks are dword aligned
-// (it cannot cross a page), else the dword ending at the block's end, shifted down. The 16-byte
-// granule window of crc_lanes_n spends ~2 selects per dword on realignment (26 of ~150 VALU
-// instructions per 36-byte step) and 12 registers per block for 9 dwords.
-template <int NF>
-__device__ __forceinline__ void lane_load_direct(std::uintptr_t blk, std::uint32_t (&d)[NF]) {
-  if constexpr (NF >= 4) {
-#pragma unroll
-    for (int k = 0; k < NF; k += 4) {
-      const int at = k + 4 <= NF ? k : NF - 4;  // the last load ends at dword NF
-      const v4u v = *reinterpret_cast<g_v4u*>(blk + 4u * at);
-      const std::uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (at + i >= k) d[at + i] = w[i];
-    }
-  } else {
-    typedef unsigned v2u __attribute__((ext_vector_type(2)));
-    typedef const v2u __attribute__((address_space(1))) g_v2u;
-    if constexpr (NF >= 2) {
-      const v2u v = *reinterpret_cast<g_v2u*>(blk);
-      d[0] = v.x;
-      d[1] = v.y;
-    }
-    if constexpr (NF == 1 || NF == 3) d[NF - 1] = *reinterpret_cast<g_u32*>(blk + 4u * (NF - 1));
-  }
-}
-
-template <int ALIGN, int NF, int DEPTH, int PRIO = 0>
-__device__ __forceinline__ void crc_lanes_d_body(const RowsArgs& a, std::uint32_t* lds) {
-  static_assert(ALIGN == 4 || ALIGN == 1, "dword-aligned or byte-aligned blocks");
-  static_assert(NF >= 1 && 4 * NF <= static_cast<int>(kLaneMax) && DEPTH >= 2, "block shape");
-  fill_lds_slicing(a.tabs, lds);
-  const std::uint32_t lane = threadIdx.x & 63u;
-  const LaneConst kc = lane_const(lane);
-  __syncthreads();
-  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const std::uint64_t W = a.nwaves, nb = a.nblocks;
-  const std::uint64_t TS = (nb + 63u) / 64u;
-  const std::uint64_t s0 = wave * TS / W;
-  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
-  if (ns == 0) return;
-  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
-  const std::uint32_t len = a.len;
-  const std::uint32_t tb = len & 3u;  // tail bytes (uniform)
-  const std::uint64_t blk0 = s0 * 64u + lane;
-  const std::uintptr_t lane_base = base + blk0 * a.stride;
-  const std::uint64_t step_bytes = 64u * a.stride;
-  const std::uintptr_t last_blk = base + (nb - 1u) * a.stride;  // lanes past the batch reload it, store nothing
-  // tail dword: dword-aligned blocks read the aligned dword after the whole ones, others the dword
-  // ending at the block's end (its top tb bytes are the tail)
-  const std::uint32_t tail_at = ALIGN == 4 ? 4u * NF : len - 4u;
-  const std::uint32_t tail_sh = ALIGN == 4 ? 0u : 8u * (4u - tb);
-
-  std::uint32_t buf[DEPTH][NF], tail[DEPTH], ini[DEPTH];
-  auto issue = [&](std::uint32_t j, int slot) {
-    const std::uint32_t jc = j < ns ? j : ns - 1;  // steps past the range reload the last one
-    const std::uint64_t b = blk0 + 64ull * jc;
-    const std::uintptr_t blk = b < nb ? lane_base + jc * step_bytes : last_blk;
-    lane_load_direct<NF>(blk, buf[slot]);
-    if (tb != 0u) tail[slot] = *reinterpret_cast<g_u32*>(blk + tail_at);  // (a scalar branch)
-    ini[slot] = a.init_raw ? a.init_raw[b < nb ? b : nb - 1u] : a.init_default;
-  };
-  auto fold = [&](int q, std::uint32_t j) {
-    Reg p{ini[q], 0};
-#pragma unroll
-    for (int k = 0; k < NF; ++k) slice4(lds, p, buf[q][k], kc);
-    std::uint32_t r = p.value();
-    if (tb != 0u) r = sarwate_bytes(lds, kc, r, tail[q] >> tail_sh, tb);
-    const std::uint64_t b = blk0 + 64ull * j;
-    if (b < nb) a.out[b] = r ^ a.out_xor;
-  };
-
-#pragma unroll
-  for (int s = 0; s < DEPTH - 1; ++s) issue(s, s);
-  for (std::uint32_t j = 0; j < ns; j += DEPTH) {
-    if constexpr (PRIO != 0) set_prio_from_left<PRIO>(ns - j, ns);
-#pragma unroll
-    for (int q = 0; q < DEPTH; ++q) {
-      issue(j + q + DEPTH - 1, (q + DEPTH - 1) % DEPTH);
-      if (j + q >= ns) break;
-      fold(q, j + q);
-    }
-  }
-}
-
 // Lane blocks of an irregular batch (len <= kLaneMax, in a scan tile the prepass marked dense), walked
 // straight from the caller's offsets and lengths (the prepass lists them nowhere): wave w takes the
 // blocks [w n / W, (w + 1) n / W) 64 at a time, lane l of step j the block b0 + 64 j + l, and folds it

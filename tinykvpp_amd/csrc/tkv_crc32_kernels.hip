@@ -21,8 +21,6 @@
 //    partials that crc_fixup combines with x^(8*4096*k) mod P products.
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
-
 #include "tkv_crc32_device.h"
 
 namespace tkv {
@@ -211,15 +209,6 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
   constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? 5 : 4;
   __shared__ std::uint32_t lds[kLdsSliceWords];
   dev::crc_lanes_n_body<ALIGN, NG, DEPTH, 1, kPackedPrio>(a, lds);
-}
-
-// The same batches of 4..kLaneMax-byte blocks (dword-aligned or not) read dword by dword with no
-// realignment (crc_lanes_d_body): NF = len / 4 whole dwords; DEPTH by registers per block.
-template <int ALIGN, int NF>
-__global__ __launch_bounds__(kThreads) void crc_lanes_d(RowsArgs a) {
-  constexpr int DEPTH = NF <= 4 ? 8 : NF <= 8 ? 7 : NF <= 12 ? 6 : 5;
-  __shared__ std::uint32_t lds[kLdsSliceWords];
-  dev::crc_lanes_d_body<ALIGN, NF, DEPTH, kPackedPrio>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
@@ -915,16 +904,6 @@ hipError_t launch_packed_small_gen(const RowsArgs& a, unsigned grid, hipStream_t
   return hipGetLastError();
 }
 
-// A/B switch for the dword-by-dword lane kernel (TKV_LANES_DIRECT: 0 off, 1 dword-aligned blocks
-// only, 2 also byte-aligned ones); read once.
-int lanes_direct() {
-  static const int v = [] {
-    const char* e = std::getenv("TKV_LANES_DIRECT");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
-
 // Uniform lane-block batch (a.len <= kLaneMax): ALIGN from the base pointer and the stride.
 hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st) {
   if (a.len > kLaneMax) return hipErrorInvalidValue;
@@ -941,34 +920,10 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st) {
     case 4: hipLaunchKernelGGL((crc_lanes_n<A, 4>), g, b, 0, st, a); break;             \
     default: hipLaunchKernelGGL((crc_lanes_n<A, 5>), g, b, 0, st, a); break;            \
   }
-#define TKV_LANES_D(A)                                                                                   \
-  switch (a.len >> 2) {                                                                                  \
-    case 1: hipLaunchKernelGGL((crc_lanes_d<A, 1>), g, b, 0, st, a); break;                              \
-    case 2: hipLaunchKernelGGL((crc_lanes_d<A, 2>), g, b, 0, st, a); break;                              \
-    case 3: hipLaunchKernelGGL((crc_lanes_d<A, 3>), g, b, 0, st, a); break;                              \
-    case 4: hipLaunchKernelGGL((crc_lanes_d<A, 4>), g, b, 0, st, a); break;                              \
-    case 5: hipLaunchKernelGGL((crc_lanes_d<A, 5>), g, b, 0, st, a); break;                              \
-    case 6: hipLaunchKernelGGL((crc_lanes_d<A, 6>), g, b, 0, st, a); break;                              \
-    case 7: hipLaunchKernelGGL((crc_lanes_d<A, 7>), g, b, 0, st, a); break;                              \
-    case 8: hipLaunchKernelGGL((crc_lanes_d<A, 8>), g, b, 0, st, a); break;                              \
-    case 9: hipLaunchKernelGGL((crc_lanes_d<A, 9>), g, b, 0, st, a); break;                              \
-    case 10: hipLaunchKernelGGL((crc_lanes_d<A, 10>), g, b, 0, st, a); break;                            \
-    case 11: hipLaunchKernelGGL((crc_lanes_d<A, 11>), g, b, 0, st, a); break;                            \
-    case 12: hipLaunchKernelGGL((crc_lanes_d<A, 12>), g, b, 0, st, a); break;                            \
-    case 13: hipLaunchKernelGGL((crc_lanes_d<A, 13>), g, b, 0, st, a); break;                            \
-    case 14: hipLaunchKernelGGL((crc_lanes_d<A, 14>), g, b, 0, st, a); break;                            \
-    case 15: hipLaunchKernelGGL((crc_lanes_d<A, 15>), g, b, 0, st, a); break;                            \
-    default: hipLaunchKernelGGL((crc_lanes_d<A, 16>), g, b, 0, st, a); break;                            \
-  }
   if (align == 16) { TKV_LANES_N(16) }
-  else if (a.len < 4u || lanes_direct() == 0) {
-    if (align == 4) { TKV_LANES_N(4) }
-    else { TKV_LANES_N(1) }
-  } else if (align == 4) { TKV_LANES_D(4) }
-  else if (lanes_direct() == 2) { TKV_LANES_D(1) }
+  else if (align == 4) { TKV_LANES_N(4) }
   else { TKV_LANES_N(1) }
 #undef TKV_LANES_N
-#undef TKV_LANES_D
   return hipGetLastError();
 }
 
