@@ -105,6 +105,12 @@ def main():
     work.append(irregular("irregular 0-1024 B, 8 B gaps", rng.integers(0, 1025, ng), np.full(ng, 8), 8))
     ng = count(450, 458)
     work.append(irregular("irregular 200-700 B, 8 B gaps", rng.integers(200, 701, ng), np.full(ng, 8), 8))
+    ng = count(400, 408)  # group-pass densities between the thresholds: 65-256 B ~26 %, 257-512 B ~43 %
+    work.append(irregular("irregular 100-700 B, 8 B gaps", rng.integers(100, 701, ng), np.full(ng, 8), 8))
+    ng = count(290, 298)  # 65-256 B ~40 %, 257-512 B ~60 %
+    work.append(irregular("irregular 180-400 B, 8 B gaps", rng.integers(180, 401, ng), np.full(ng, 8), 8))
+    ng = count(545, 553)
+    work.append(irregular("irregular 65-1024 B, 8 B gaps", rng.integers(65, 1025, ng), np.full(ng, 8), 8))
     n = count(2048, 2056)
     lr = rng.integers(0, 4097, n)
     work.append(irregular("irregular 0-4 KiB, 8 B gaps", lr, np.full(n, 8), 8))
