@@ -288,10 +288,11 @@ int tkv_debug_irregular_lists(void *stream, uint32_t out[3]);
  * 0 (then they take the staged copy pipeline, as pageable memory does). Returns the previous
  * setting. Default 1; the environment variable TKV_HOST_MAPPED=0 sets 0 at load time. */
 int tkv_debug_set_host_mapped(int enable);
-/* Back-to-back irregular batches whose 4096-block scan tiles hold at least 1024 blocks of 65-256 bytes
- * take the general path, whose group phase folds those blocks, unless this is 1:
- * then they may take the byte-stream walk as before round 4 (kept so its many-ends-per-row shapes
- * stay under test). Returns the previous setting. Default 0. */
+/* Back-to-back irregular batches with a 4096-block scan tile of at least 1024 blocks of at most
+ * 1 KiB and at most 1024 rows (4 MiB) of larger blocks take the general path, whose group passes and
+ * small phase fold those blocks, unless this is 1: then they may take the byte-stream
+ * walk as before round 4 (kept so its many-ends-per-row shapes stay under test). Returns the previous
+ * setting. Default 0. */
 int tkv_debug_set_stream_groups(int enable);
 
 

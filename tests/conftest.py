@@ -178,11 +178,12 @@ LANE_MAX = 64        # kLaneMax
 GROUP_MAX = 256      # kGroupMax: blocks of LANE_MAX + 1 .. GROUP_MAX are group blocks
 SMALL_MAX = 1024     # kSmallMax
 SCAN_TILE = 4096     # kScanTile
-GROUP_DENSE_TILE = 1024  # kGroupDenseTile
+GROUP_DENSE_TILE = 3072  # kGroupDenseTile
 GROUP_TILE_ROWS = 1024   # kGroupTileRows
+STREAM_SMALL_TILE = 1024  # kStreamSmallTile
 LANE_DENSE_TILE = 256    # kLaneDenseTile
 # group classes (lower bound exclusive, upper inclusive, tile threshold, phase bit): 4- and 8-lane passes
-GROUP_CLASSES = ((LANE_MAX, 256, 1024, 2), (256, 512, 2048, 4))
+GROUP_CLASSES = ((LANE_MAX, 256, 3072, 2), (256, 512, 3968, 4))
 
 
 def phases_expected(lens):
@@ -228,8 +229,8 @@ def lists_expected(lens):
 def stream_expected(offs, lens, group_stream=False):
     """1 when the prepass picks the byte-stream walk for this batch, else 0: every block at least
     LANE_MAX + 1 bytes and starting where its predecessor ends, and (unless tkv_debug_set_stream_groups
-    is on) no scan tile dense in group blocks (at least GROUP_DENSE_TILE of them among its 4096 blocks,
-    with at most GROUP_TILE_ROWS rows of blocks over SMALL_MAX bytes)."""
+    is on) no scan tile whose bytes are mostly in small blocks (at least STREAM_SMALL_TILE blocks of at
+    most SMALL_MAX bytes among its 4096, with at most GROUP_TILE_ROWS rows of larger blocks)."""
     offs = np.asarray(offs, np.int64)
     lens = np.asarray(lens, np.int64)
     if lens.size == 0 or lens.min() <= LANE_MAX or np.any(offs[:-1] + lens[:-1] != offs[1:]):
@@ -238,10 +239,10 @@ def stream_expected(offs, lens, group_stream=False):
         return 1
     for t in range(0, lens.size, SCAN_TILE):
         tl = lens[t:t + SCAN_TILE]
-        groups = int(np.count_nonzero((tl > LANE_MAX) & (tl <= GROUP_MAX)))
+        small = int(np.count_nonzero(tl <= SMALL_MAX))
         big = tl[tl > SMALL_MAX]
         rows = int(((big - 1) // 4096 + 1).sum())
-        if groups >= GROUP_DENSE_TILE and rows <= GROUP_TILE_ROWS:
+        if small >= STREAM_SMALL_TILE and rows <= GROUP_TILE_ROWS:
             return 0
     return 1
 

@@ -105,17 +105,17 @@ def test_irregular_random(gpu, oracle, seed):
 @pytest.mark.parametrize("seed", range(48))
 def test_irregular_dense_small_random(gpu, oracle, seed):
     """Batches dense in blocks of at most 256 bytes (the lane and group phases): lane
-    and group shares around the prepass's per-tile thresholds (256 and 1024 of 4096 blocks), a few
+    and group shares around the prepass's per-tile thresholds (256 and 3072 of 4096 blocks), a few
     large blocks that may push a tile over the group phase's row bound, gapped, back-to-back and
     overlapping layouts, random base shifts, initial registers and algorithms."""
     rng = np.random.default_rng(5000 + seed + OFFSET)
     algo = ALGOS[seed % 2]
     n = int(rng.choice([4096, 5000, 9000, 20000, 4096 * 3 + 17]))
     p_lane = float(rng.choice([0.0, 0.05, 0.0625, 0.3, 0.9]))
-    p_group = float(rng.choice([0.0, 0.2, 0.25, 0.3, 0.9]))
-    # the rest: 257-512 B (8-lane pass), 513-1024 B (16-lane pass) and 1025-3000 B, in shares around
-    # the passes' tile thresholds (1024 and 2048 of 4096)
-    mid = rng.choice([(0.0, 0.0), (0.25, 0.0), (0.3, 0.5), (0.0, 0.55), (0.45, 0.45)])
+    p_group = float(rng.choice([0.0, 0.2, 0.3, 0.74, 0.76, 0.9]))
+    # the rest: 257-512 B (8-lane pass or listed), 513-1024 B (listed) and 1025-3000 B, in shares around
+    # the 8-lane pass's tile threshold (3968 of 4096)
+    mid = rng.choice([(0.0, 0.0), (0.25, 0.0), (0.3, 0.5), (0.0, 0.55), (0.45, 0.45), (0.96, 0.0), (0.995, 0.0)])
     u = rng.random(n)
     v = rng.random(n)
     rest = np.where(v < mid[0], rng.integers(257, 513, n),

@@ -159,15 +159,17 @@ def test_irregular_mixed_classes(gpu, oracle, mix):
 @pytest.mark.parametrize("group_stream", [0, 1])
 def test_stream_mode_needs_blocks_longer_than_lanes(gpu, oracle, buf, group_stream):
     """Back-to-back 64-byte blocks are lane blocks (general path). Back-to-back 65-byte blocks are group
-    blocks: by default their dense tiles take the general path and the group phase (round 4; it folds
-    them faster than the stream walk's rows of 63 block ends), with tkv_debug_set_stream_groups(1)
-    stream mode as before. 300-byte blocks take stream mode either way. All bit-exact."""
+    blocks: by default their tiles take the general path and the group phase (round 4; it folds them
+    faster than the stream walk's rows of 63 block ends), with tkv_debug_set_stream_groups(1) stream
+    mode as before; 300-byte blocks likewise (the small phase), 2000-byte ones stream mode either way.
+    All bit-exact."""
     host, d = buf
     lib = tk.load_library()
     prev = lib.tkv_debug_set_stream_groups(group_stream)
     try:
-        for blen, want_mode in ((64, 0), (65, group_stream), (40, 0), (128, group_stream), (300, 1)):
-            n = 50_000
+        for blen, want_mode in ((64, 0), (65, group_stream), (40, 0), (128, group_stream), (300, group_stream),
+                                (2000, 1)):
+            n = 50_000 if blen < 1000 else 20_000
             offs = 7 + np.arange(n, dtype=np.int64) * blen
             lens = np.full(n, blen, np.int32)
             got = u32(tk.crc32_batch(d, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu)))
@@ -197,7 +199,8 @@ def test_irregular_more_than_1024_tiles(gpu, oracle, shape):
     """Batches of more than 4 M blocks (over 1024 prepass tiles of 4096 blocks) take the 512-thread
     tile scan and the unfused scatter: lane-dense tiles (WAL payloads), tiles mixing lane, small and
     large blocks with random gaps, and 128-byte blocks back to back, which take stream mode through
-    rows_scan_tiles' verdict; per-block initial registers on the mixed batch."""
+    rows_scan_tiles' verdict with tkv_debug_set_stream_groups(1), the general path by default;
+    per-block initial registers on the mixed batch."""
     rng = np.random.default_rng({"wal_payloads": 1, "mixed_gaps": 2, "back_to_back_128": 3, "back_to_back_128_stream": 3,
                                  "back_to_back_300": 4}[shape])
     n = 4096 * 1025 + 777
@@ -225,8 +228,9 @@ def test_irregular_more_than_1024_tiles(gpu, oracle, shape):
     finally:
         lib.tkv_debug_set_stream_groups(prev)
     # back-to-back blocks longer than kLaneMax take stream mode at any batch size, through
-    # rows_scan_tiles' verdict, unless their tiles are dense in group blocks (128 B, by default)
-    assert got_mode == (1 if shape in ("back_to_back_128_stream", "back_to_back_300") else 0)
+    # rows_scan_tiles' verdict, unless their tiles' bytes are mostly in blocks of at most 1 KiB (128 and
+    # 300 B, by default: the group passes and the small phase)
+    assert got_mode == (1 if shape == "back_to_back_128_stream" else 0)
     if shape == "mixed_gaps":
         init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
         got = u32(tk.crc32_batch(d, o, ln, init_raw=i32(init).to(gpu)))

@@ -138,26 +138,30 @@ constexpr std::uint32_t kLaneMax = 64;
 constexpr std::uint32_t kGroupMax = 256;
 constexpr std::uint32_t kGroup8Max = 512;
 // The prepass leaves a scan tile's lane blocks to the lane phase only when the tile holds at least
-// kLaneDenseTile of them (of its 4096), and its group blocks to the group phase only when it holds at
-// least kGroupDenseTile; in a sparser tile they are listed as small blocks. Either phase walks the
-// metadata of every block in its waves' ranges (64 blocks per lane-phase step, 16 per group-phase step)
-// where the small phase folds 4 listed blocks per step: the thresholds are those break-even points.
+// kLaneDenseTile of them (of its 4096), its 65-256-byte blocks to the 4-lane pass only when it holds
+// at least kGroupDenseTile and its 257-512-byte blocks to the 8-lane pass only when nearly all its
+// blocks are of that class; in other tiles they are listed as small blocks by class (4-, 8- and
+// 16-lane groups in the small phase, the same slots). A pass walks the metadata of every block in its
+// waves' ranges with the lanes of other classes idle, while listing costs a scatter per block: since
+// the small phase folds each class at its own group size (round 4), a pass pays only in tiles almost
+// all of its class. One process, 1 GiB gapped batches, against the round-4 start's 1024 / 2048
+// (profiles/r4/group_policy/probe_thresholds.jsonl): 180-400 B 1832 -> 2612 GB/s, 100-700 B 2181 ->
+// 2774, 200-700 B 2211 -> 2881; pure classes within noise (65-256 B 2948 / 2879, 257-512 B 3218 / 3156).
 // The group phase also needs a tile with at most kGroupTileRows rows of large blocks (4 MiB): where
 // large blocks carry the bytes, crc_rows folds the small blocks in the shadow of its row walk and the
 // group phase's own latency chain (descriptor, data, fold: ~10 us) would only add to the batch
 // (cfg4's general path: 1300 blocks of 255 bytes per tile, +1.2 % time with the group phase).
-// The 8-lane pass walks 8 blocks per step where the small phase folds 4 listed ones (in 1 KiB
-// slots), so it needs a tile at least half of whose blocks are in its class: with both group passes
-// walking a tile of 257-1024-byte blocks, 300-1000 B payloads ran at 2270 against 3160 GB/s for the
-// small phase (profiles/r4/s1/probe_irregular.jsonl).
 constexpr std::uint32_t kLaneDenseTile = 256;
 #ifndef TKV_AB_GROUP_DENSE  // (A/B builds only: tools/build_at.sh -DTKV_AB_GROUP_DENSE=...)
-#define TKV_AB_GROUP_DENSE 1024
+#define TKV_AB_GROUP_DENSE 3072
 #endif
 #ifndef TKV_AB_GROUP8_DENSE
-#define TKV_AB_GROUP8_DENSE 2048
+#define TKV_AB_GROUP8_DENSE 3968
 #endif
 constexpr std::uint32_t kGroupDenseTile = TKV_AB_GROUP_DENSE;
+// A back-to-back tile with at least this many blocks of at most kSmallMax bytes and at most
+// kGroupTileRows rows of larger ones takes the general path, not stream mode (rows_tile_scan).
+constexpr std::uint32_t kStreamSmallTile = 1024;
 constexpr std::uint32_t kGroup8DenseTile = TKV_AB_GROUP8_DENSE;
 constexpr std::uint64_t kGroupTileRows = 1024;
 // Per-tile flags (tile_ok):

@@ -207,7 +207,7 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small_gen(RowsArgs a) {
 template <int ALIGN, int NG>
 __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
   constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? 5 : 4;
-  __shared__ std::uint32_t lds[kLdsSliceWords];
+  __shared__ std::uint32_t lds[kLdsSliceWords + 1024];  // slicing tables, then the two-chain shift table
   dev::crc_lanes_n_body<ALIGN, NG, DEPTH, 1, kPackedPrio>(a, lds);
 }
 
@@ -366,11 +366,15 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   auto cls_pair = [&](std::uint64_t x) {
     return static_cast<std::uint32_t>(((x & c8mask) >> 32) | ((x >> 48) << 16));
   };
-  // A tile dense in group blocks does not qualify for stream mode (unless group_stream, a debug
-  // setting): the group phase folds 65-256-byte blocks at the rate of gapped ones, where the stream
-  // walk's rows of 16-64 block ends ran at about 0.6 of it (back-to-back 128 B: 1404 against 2351
-  // GB/s, profiles/r3/group_phase/). Longer blocks keep stream mode, where it wins (cfg4, 64 KiB).
-  const bool stream_ok = all_ok && (group_stream != 0u || (tph & kTileGroups) == 0u);
+  // A tile whose bytes are mostly in small blocks (at least kStreamSmallTile blocks of at most
+  // kSmallMax bytes and at most kGroupTileRows rows of larger ones) does not qualify for stream mode
+  // (unless group_stream, a debug setting): the group passes and the small phase fold such blocks at
+  // the rate of gapped ones, where the stream walk's rows of many block ends ran slower (back-to-back
+  // 128 B: 1404 against 2351 GB/s, profiles/r3/group_phase/; 300-1000 B: 2893 against 3206,
+  // profiles/r4/s5/). Tiles whose bytes are in larger blocks keep stream mode, where it wins (cfg4,
+  // 64 KiB blocks, and short batches of any blocks).
+  const bool small_tile = few_rows && static_cast<std::uint32_t>(tot) >= kStreamSmallTile;
+  const bool stream_ok = all_ok && (group_stream != 0u || !small_tile);
   const std::uint64_t tile_n = n - static_cast<std::uint64_t>(blockIdx.x) * kScanTile;  // blocks in the tile
   const bool all_taken = taken(ltot) == (tile_n < kScanTile ? tile_n : kScanTile);
   if (threadIdx.x == 0) tile_ok[blockIdx.x] = (stream_ok ? kTileStream : 0u) | tph | (all_taken ? kTileAllTaken : 0u);
@@ -568,7 +572,14 @@ __global__ void rows_finish(const std::uint8_t* base, const std::uint64_t* offse
 // no single-workgroup tile-scan launch sits between the tile scan and the scatter. Workgroup 0
 // publishes counts for the row kernel.
 constexpr std::uint32_t kFusedTiles = 1024;
-constexpr std::uint32_t kFinishThreads = 256;
+// One workgroup of kFinishThreads threads and kFinishPer blocks each per scan tile (round 4; with a
+// 256-thread workgroup per 256 blocks every workgroup re-read all tile sums, ntiles^2 * 16 loads: 37 µs
+// of a 330 µs step at 400 tiles).
+#ifndef TKV_AB_FINISH_PER  // (A/B builds only)
+#define TKV_AB_FINISH_PER 4
+#endif
+constexpr std::uint32_t kFinishPer = TKV_AB_FINISH_PER;
+constexpr std::uint32_t kFinishThreads = kFinishPer == 1 ? 256 : kScanTile / kFinishPer;
 // Stream mode (every tile qualified): instead of the small/large lists, every block
 // gets its end E[b] in bytes from row 0 (the stream start rounded down to 16 bytes), and every
 // row-kernel wave the first block ending in or after its first row; counts = {0, 0, rows, 1} and
@@ -599,27 +610,35 @@ __device__ __forceinline__ void stream_block(const std::uint8_t* base, const std
     wave_start[w] = static_cast<std::uint32_t>(b);
 }
 
-__global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
+template <unsigned T, unsigned PER>
+__global__ __launch_bounds__(T) void rows_finish_fused(
     const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
     const std::uint64_t* scan, const std::uint64_t* tile_sums, const std::uint32_t* tile_ok, std::uint32_t ntiles,
     std::uint32_t* counts, PrepassOut o, std::uint32_t W, std::uint32_t* out, std::uint64_t* ends,
     std::uint64_t* sinfo, std::uint32_t Ws, const std::uint32_t* row0) {
-  constexpr std::uint32_t kWaves = kFinishThreads / 64;
+  static_assert(kScanTile % (T * PER) == 0 && T % 64 == 0, "a workgroup lies in one scan tile");
+  constexpr std::uint32_t kWaves = T / 64;
   __shared__ std::uint64_t red[8][kWaves];
-  const std::uint32_t my_tile = blockIdx.x * kFinishThreads / kScanTile;  // kScanTile % 256 == 0
-  // The block's own operands are loaded first, so their latency overlaps the tile-sum reduction (the
-  // scan values of a lane block were never written and are not used).
-  const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(kFinishThreads) + threadIdx.x;
-  const bool live = b < n;
-  const std::uint32_t len = live ? lengths[b] : 0u;
-  const std::uint64_t off = live ? offsets[b] : 0ull;
-  const std::uint64_t sc = live ? scan[b] : 0ull;
-  const std::uint32_t lsc = live ? o.lscan[b] : 0u;
-  const std::uint32_t csc = live ? o.cscan[b] : 0u;
+  const std::uint32_t my_tile = blockIdx.x * (T * PER) / kScanTile;
+  // The workgroup's own operands are loaded first, so their latency overlaps the tile-sum reduction
+  // (the scan values of a lane block were never written and are not used).
+  const std::uint64_t b0 = blockIdx.x * static_cast<std::uint64_t>(T * PER) + threadIdx.x;
+  std::uint32_t len[PER], lsc[PER], csc[PER];
+  std::uint64_t off[PER], sc[PER];
+#pragma unroll
+  for (unsigned r = 0; r < PER; ++r) {
+    const std::uint64_t b = b0 + r * T;
+    const bool live = b < n;
+    len[r] = live ? lengths[b] : 0u;
+    off[r] = live ? offsets[b] : 0ull;
+    sc[r] = live ? scan[b] : 0ull;
+    lsc[r] = live ? o.lscan[b] : 0u;
+    csc[r] = live ? o.cscan[b] : 0u;
+  }
   const std::uint32_t mtk = tile_ok[my_tile];
   std::uint64_t before = 0, all = 0, bad = 0, lbefore = 0, lall = 0, cbefore = 0, call = 0;
   std::uint32_t ph = 0;  // kTilePhases flags over the tiles
-  for (std::uint32_t i = threadIdx.x; i < ntiles; i += kFinishThreads) {
+  for (std::uint32_t i = threadIdx.x; i < ntiles; i += T) {
     const std::uint64_t v = tile_sums[i];
     const std::uint64_t lv = o.tile_lanes[i];
     const std::uint64_t cv = o.tile_cls[i];
@@ -671,9 +690,15 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) counts[kCountPhases] = nbad == 0 ? 0u : static_cast<std::uint32_t>(aph) >> 1;
   if (nbad == 0) {  // every block qualifies: stream mode
-    if (live) stream_block(base, offsets, lengths, n, b, off, len, Ws, row0, counts, ends, sinfo, o.wave_start);
+#pragma unroll
+    for (unsigned r = 0; r < PER; ++r) {
+      const std::uint64_t b = b0 + r * T;
+      if (b < n) stream_block(base, offsets, lengths, n, b, off[r], len[r], Ws, row0, counts, ends, sinfo, o.wave_start);
+    }
     return;
   }
+  const std::uint32_t n8 = static_cast<std::uint32_t>(ctotal);
+  const std::uint32_t n4 = static_cast<std::uint32_t>(total) - n8 - static_cast<std::uint32_t>(ctotal >> 32);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const std::uint32_t ns = static_cast<std::uint32_t>(total), nl = static_cast<std::uint32_t>(ltotal);
     counts[0] = n - ns - nl;                               // large blocks
@@ -681,18 +706,17 @@ __global__ __launch_bounds__(kFinishThreads) void rows_finish_fused(
     counts[2] = static_cast<std::uint32_t>(total >> 32);  // rows of the large blocks
     counts[3] = 0;                                         // general path
     counts[kCountLanes] = nl;                              // lane blocks (crc_stream's lane phase)
-  }
-  const std::uint32_t n8 = static_cast<std::uint32_t>(ctotal);
-  const std::uint32_t n4 = static_cast<std::uint32_t>(total) - n8 - static_cast<std::uint32_t>(ctotal >> 32);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
     counts[kCountSmall4] = n4;
     counts[kCountSmall8] = n8;
   }
-  if (!live) return;
-  const std::uint64_t cpre = tile_coff + (csc & 0xFFFFu) + (static_cast<std::uint64_t>(csc >> 16) << 32);
-  finish_block(off, len, b, sc + tile_off, lsc + tile_loff, cpre, n4, n8, total >> 32, o, W, out, mtk);
+#pragma unroll
+  for (unsigned r = 0; r < PER; ++r) {
+    const std::uint64_t b = b0 + r * T;
+    if (b >= n) break;
+    const std::uint64_t cpre = tile_coff + (csc[r] & 0xFFFFu) + (static_cast<std::uint64_t>(csc[r] >> 16) << 32);
+    finish_block(off[r], len[r], b, sc[r] + tile_off, lsc[r] + tile_loff, cpre, n4, n8, total >> 32, o, W, out, mtk);
+  }
 }
-
 
 // ---- synthetic data: byte j of block b = LE byte j%8 of
 //      splitmix64((b << 24) ^ (j >> 3) ^ (seed << 56)). Test/bench input generation only. ----------
@@ -941,7 +965,7 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
   const std::uint32_t Ws = ncu * (kStreamThreads / 64);  // crc_stream's waves
   // Grid sizes in 64-bit arithmetic: n may be close to 2^32 (the host caps it at kMaxIrregularBlocks).
   const std::uint64_t ntiles = prepass_tiles(n);
-  const std::uint64_t nfused = (static_cast<std::uint64_t>(n) + kFinishThreads - 1) / kFinishThreads;
+  const std::uint64_t nfused = (static_cast<std::uint64_t>(n) + kFinishThreads * kFinishPer - 1) / (kFinishThreads * kFinishPer);
   const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
   if (ntiles <= kFusedTiles)
     hipLaunchKernelGGL(rows_tile_scan<1024>, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets,
@@ -952,7 +976,7 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
                        lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
                        group_stream);
   if (ntiles <= kFusedTiles) {
-    hipLaunchKernelGGL(rows_finish_fused, dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
+    hipLaunchKernelGGL((rows_finish_fused<kFinishThreads, kFinishPer>), dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
                        offsets, lengths, n, scan, tile_sums, tile_ok, static_cast<std::uint32_t>(ntiles), counts, o,
                        W, out, ends, sinfo, Ws, row0);
   } else {
