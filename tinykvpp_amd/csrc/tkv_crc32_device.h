@@ -1434,35 +1434,11 @@ __device__ __forceinline__ void lane_dwords_n(const uint4 (&g)[NG], std::uint32_
   }
 }
 
-#ifndef LANES_TWO_CHAINS  // (A/B builds: -DLANES_TWO_CHAINS=0 keeps one chain per block)
-#define LANES_TWO_CHAINS 1
-#endif
 template <int ALIGN, int NG, int DEPTH, int ILP, int PRIO = 0>
 __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
   constexpr int ND = 4 * NG;
-  // Two chains per block: the lookups of one slicing step depend on the previous step's, so a block
-  // of nf dwords is nf LDS round trips deep. With H = half the most whole dwords this window holds,
-  // a block longer than 4 H bytes folds dwords [0, H) from its register (chain A) beside the rest
-  // from 0 (chain B), interleaved, and joins them as Shift_{len - 4H}(A) ^ B: the shift by the
-  // batch's one length is four lookups into a 4 KiB table built in LDS at launch
-  // (M_j[b] = Shift_n(b << 8j), from head_shift[n]).
-  constexpr int NFMAX = ALIGN == 16 ? 4 * NG : ALIGN == 4 ? 4 * NG - 3 : 4 * NG - 4;
-  constexpr int H = (NFMAX + 1) / 2;
-  constexpr bool kTwo = LANES_TWO_CHAINS && ILP == 1 && NFMAX >= 6;
-  const std::uint32_t len0 = a.len;
-  const bool two = kTwo && len0 > 4u * H;  // uniform
   fill_lds_slicing(a.tabs, lds);
-  if (two) {
-    const std::uint32_t sn = len0 - 4u * H;
-    for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
-      const std::uint32_t j = u >> 8, bb = u & 255u;
-      std::uint32_t v = 0;
-#pragma unroll
-      for (std::uint32_t i = 0; i < 8u; ++i) v ^= (bb >> i) & 1u ? a.tabs->head_shift[sn][8u * j + i] : 0u;
-      lds[kLdsSliceWords + u] = v;
-    }
-  }
   const std::uint32_t lane = threadIdx.x & 63u;
   const LaneConst kc = lane_const(lane);
   __syncthreads();
@@ -1490,27 +1466,6 @@ __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_
     lane_issue_n<ALIGN, NG>(blk, len, dmy, buf[slot]);
     o16[slot] = static_cast<std::uint32_t>(blk & 15u);
     ini[slot] = a.init_raw ? a.init_raw[b < nb ? b : nb - 1u] : a.init_default;
-  };
-  auto fold2 = [&](int q, std::uint32_t j) {  // kTwo: chains A and B interleaved
-    std::uint32_t d[ND];
-    lane_dwords_n<ALIGN, NG>(buf[q], o16[q], d);
-    Reg pa{ini[q], 0}, pb{0, 0};
-    constexpr int KB = ND - H;  // chain B: dwords H .. nf - 1, then the tail bytes in dword nf
-#pragma unroll
-    for (int k = 0; k < (H > KB ? H : KB); ++k) {
-      if (k < H) slice4(lds, pa, d[k], kc);
-      if (k < KB) {
-        if (static_cast<std::uint32_t>(H + k) < nf) slice4(lds, pb, d[H + k], kc);
-        else if (static_cast<std::uint32_t>(H + k) == nf && tb != 0u) pb = Reg{sarwate_bytes(lds, kc, pb.value(), d[H + k], tb), 0};
-      }
-    }
-    const std::uint32_t x = pa.value();
-    const std::uint32_t sh = lds_at(lds, kLdsSliceWords * 4u + ((x & 0xFFu) << 2)) ^
-                             lds_at(lds, kLdsSliceWords * 4u + 1024u + (((x >> 8) & 0xFFu) << 2)) ^
-                             lds_at(lds, kLdsSliceWords * 4u + 2048u + (((x >> 16) & 0xFFu) << 2)) ^
-                             lds_at(lds, kLdsSliceWords * 4u + 3072u + ((x >> 24) << 2));
-    const std::uint64_t b = blk0 + 64ull * j;
-    if (b < nb) a.out[b] = (sh ^ pb.value()) ^ a.out_xor;
   };
   auto fold = [&](auto nb_const, int q, std::uint32_t j) {
     constexpr int NB = decltype(nb_const)::value;
@@ -1552,9 +1507,7 @@ __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_
       for (int i = 0; i < ILP; ++i) issue(j + q + DEPTH - ILP + i, (q + DEPTH - ILP + i) % DEPTH);
       const std::uint32_t jq = j + q;
       if (jq >= ns) break;
-      if (kTwo && two) {
-        fold2(q, jq);
-      } else if (jq + ILP <= ns) {
+      if (jq + ILP <= ns) {
         fold(std::integral_constant<int, ILP>{}, q, jq);
       } else {
 #pragma unroll

@@ -207,7 +207,7 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small_gen(RowsArgs a) {
 template <int ALIGN, int NG>
 __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
   constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? 5 : 4;
-  __shared__ std::uint32_t lds[kLdsSliceWords + 1024];  // slicing tables, then the two-chain shift table
+  __shared__ std::uint32_t lds[kLdsSliceWords];
   dev::crc_lanes_n_body<ALIGN, NG, DEPTH, 1, kPackedPrio>(a, lds);
 }
 
@@ -572,11 +572,12 @@ __global__ void rows_finish(const std::uint8_t* base, const std::uint64_t* offse
 // no single-workgroup tile-scan launch sits between the tile scan and the scatter. Workgroup 0
 // publishes counts for the row kernel.
 constexpr std::uint32_t kFusedTiles = 1024;
-// One workgroup of kFinishThreads threads and kFinishPer blocks each per scan tile (round 4; with a
-// 256-thread workgroup per 256 blocks every workgroup re-read all tile sums, ntiles^2 * 16 loads: 37 µs
-// of a 330 µs step at 400 tiles).
+// A 256-thread workgroup per 256 blocks, each re-reading all tile sums. One 1024-thread workgroup per
+// scan tile with 4 blocks per thread (TKV_AB_FINISH_PER=4) cuts those re-reads by 16 but measured
+// slower: 300-1000 B gapped 3210 -> 2929 GB/s, 257-512 B 3210 -> 2748 (profiles/r4/s7/): the scatter's
+// latency, not the re-reads, is what the finish pays for.
 #ifndef TKV_AB_FINISH_PER  // (A/B builds only)
-#define TKV_AB_FINISH_PER 4
+#define TKV_AB_FINISH_PER 1
 #endif
 constexpr std::uint32_t kFinishPer = TKV_AB_FINISH_PER;
 constexpr std::uint32_t kFinishThreads = kFinishPer == 1 ? 256 : kScanTile / kFinishPer;
