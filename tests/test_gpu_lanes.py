@@ -316,6 +316,43 @@ def test_irregular_small_lists_by_class(gpu, oracle, buf, shape, base):
     assert np.array_equal(got, oracle_c(oracle, host, offs, lens))
 
 
+@pytest.mark.parametrize("pattern", ["all_1024", "empty_mix", "one_byte_mix", "16_lanes", "2_lanes", "ramp", "one"])
+def test_irregular_small_packed_lanes(gpu, oracle, buf, pattern):
+    """Listed small blocks of every lane count (ceil(len / 64) = 1..16) in the small-block phase's class
+    walks: whole 1 KiB slots, empty blocks, one-byte blocks among 1 KiB ones, blocks of exactly 16
+    lanes, 2-lane blocks, ramps of every length, and a single block; each beside large blocks so that
+    no group pass takes them, at base offsets 0-7. (Round 4 also built a walk that packed such blocks
+    back to back in lane space; this test was written for it, and it measured slower)"""
+    host, d = buf
+    rng = np.random.default_rng(len(pattern) * 7)
+    n = 9000
+    # (lane blocks stay under the lane phase's 256 per tile, so they are listed too)
+    small = {"all_1024": np.full(n, 1024),
+             "empty_mix": np.where(rng.random(n) < 0.1, 0, rng.integers(500, 1025, n)),
+             "one_byte_mix": np.tile([1] + [1024] * 9, n // 10), "16_lanes": rng.integers(961, 1025, n),
+             "2_lanes": rng.integers(65, 129, n), "ramp": np.arange(n) % 1025,
+             "one": np.array([777])}[pattern].astype(np.int64)
+    lens = np.empty(small.size * 2, np.int64)
+    lens[0::2] = small
+    lens[1::2] = 4097 + rng.integers(0, 3000, small.size)  # rows enough to keep every group pass off
+    for base in range(8):
+        gaps = rng.integers(1, 5, lens.size)  # (gapped: back-to-back pairs could take stream mode)
+        offs = base + np.concatenate([[0], np.cumsum(lens[:-1] + gaps[:-1])])
+        if offs[-1] + lens[-1] > host.size:
+            keep = int(np.searchsorted(offs + lens, host.size, side="right"))
+            offs, lens_b = offs[:keep], lens[:keep]
+        else:
+            lens_b = lens
+        o = torch.from_numpy(offs.astype(np.int64)).to(gpu)
+        ln = torch.from_numpy(lens_b.astype(np.int32)).to(gpu)
+        got = u32(tk.crc32_batch(d, o, ln))
+        assert mode() == 0 and phases() == phases_expected(lens_b) == 0, base
+        assert lists() == lists_expected(lens_b), base
+        want = oracle.batch(host, offs, lens_b)
+        bad = np.flatnonzero(got != want)
+        assert bad.size == 0, (base, bad[:5], lens_b[bad[:5]])
+
+
 @pytest.mark.parametrize("sizes", [(65,), (100, 128, 200), tuple(range(65, 257)), (256,)])
 @pytest.mark.parametrize("base", [0, 5, 8])
 def test_irregular_group_blocks(gpu, oracle, buf, sizes, base):
