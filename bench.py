@@ -128,7 +128,8 @@ def pmc_traffic(csv_path, config):
                      "rows_finish", "crc_fixup") if config == "cfg4" else ("crc_packed",))
     path = csv_path
     if path is None:
-        for cand in (os.path.join(ROOT, "profiles", "r3", "pmc", f"pmc_{config}_FETCH_SIZE.csv"),
+        for cand in (os.path.join(ROOT, "profiles", "r4", "final", f"pmc_{config}_FETCH_SIZE.csv"),
+                     os.path.join(ROOT, "profiles", "r3", "pmc", f"pmc_{config}_FETCH_SIZE.csv"),
                      os.path.join(ROOT, "profiles", "r2", f"pmc_{config}", "FETCH_SIZE_counters.csv"),
                      os.path.join(ROOT, "profiles", "r1", f"pmc_{config}", "p3_counters.csv")):
             if os.path.exists(cand):

@@ -1,0 +1,32 @@
+#!/bin/bash
+# Round-4 final evidence on the tree: the GPU suite, smoke(), the default bench line, kernel traces of
+# cfg2 (one stream, so the stats average is the per-launch duration) and cfg4, and one FETCH_SIZE
+# pass each for cfg2 and cfg4. Output: gpurun_out/r4final/.
+set -u
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r4final
+mkdir -p $O
+cd $R
+timeout -k 10 500 python -u -m pytest tests -m gpu -q --maxfail=30 --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest.log; grep -E "^FAILED|^ERROR" $O/pytest.log | head -20
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -1 $O/smoke.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err
+rc=$?; echo "bench rc=$rc"; tail -c 600 $O/bench.json; [ $rc -eq 0 ] || exit $rc
+cd /tmp && export TMPDIR=/tmp
+run() {  # name limit command...
+  local name=$1 t=$2
+  shift 2
+  timeout -k 10 -s KILL $t "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  return $rc
+}
+B="python3 $R/bench.py --no-cpu-baseline --no-pipelined --no-more-configs --no-e2e"
+run trace_cfg2 300 rocprofv3 --kernel-trace --stats -d $O/trace_cfg2 -o run --output-format csv -- $B || exit 1
+run trace_cfg4 300 rocprofv3 --kernel-trace --stats -d $O/trace_cfg4 -o run --output-format csv -- $B --config cfg4 || exit 1
+for cfg in cfg2 cfg4; do
+  run pmc_${cfg}_FETCH_SIZE 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_${cfg}_FETCH_SIZE -o pmc --output-format csv -- $B --config $cfg --steps 5 --warmup 3 --min-warmup-ms 0 || exit 1
+done
+echo done
