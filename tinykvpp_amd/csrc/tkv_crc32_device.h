@@ -46,6 +46,13 @@ __device__ __forceinline__ LaneConst lane_const(std::uint32_t lane) {
   const std::uint32_t c4 = (lane & 31u) << 2;
   return {c4, 128u + c4, 0x10000u + c4, 0x10080u + c4, kLdsLaneBase + lane * 4u};
 }
+// The 64 KiB image (fill_lds_slicing16): 16 replicas, all four tables in one 256-byte row per entry
+// (table t at bytes 64 t + 4 c), so the entry * 256 addressing of slice4 holds; lanes l and l + 16 of
+// a half-wave share a bank (2-way conflicts when their entries differ). Lane shifts are not in it.
+__device__ __forceinline__ LaneConst lane_const16(std::uint32_t lane) {
+  const std::uint32_t c4 = (lane & 15u) << 2;
+  return {c4, 64u + c4, 128u + c4, 192u + c4, 0u};
+}
 
 __device__ __forceinline__ std::uint32_t xor3(std::uint32_t a, std::uint32_t b, std::uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32 truth table 0x96 = a ^ b ^ c
@@ -364,6 +371,16 @@ __device__ __forceinline__ void fill_lds_slicing(const DeviceTables* tabs, std::
     uint4* dst = reinterpret_cast<uint4*>(lds + pair * 16384u + e * 64u + t * 32u);
 #pragma unroll
     for (std::uint32_t k = 0; k < 8u; ++k) dst[(k + u) & 7u] = make_uint4(v, v, v, v);
+  }
+}
+
+__device__ __forceinline__ void fill_lds_slicing16(const DeviceTables* tabs, std::uint32_t* lds) {
+  for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
+    const std::uint32_t e = u >> 2, t = u & 3u;
+    const std::uint32_t v = tabs->slice[t][e];
+    uint4* dst = reinterpret_cast<uint4*>(lds + e * 64u + t * 16u);
+#pragma unroll
+    for (std::uint32_t k = 0; k < 4u; ++k) dst[(k + u) & 3u] = make_uint4(v, v, v, v);
   }
 }
 
@@ -1434,13 +1451,15 @@ __device__ __forceinline__ void lane_dwords_n(const uint4 (&g)[NG], std::uint32_
   }
 }
 
-template <int ALIGN, int NG, int DEPTH, int ILP, int PRIO = 0>
+template <int ALIGN, int NG, int DEPTH, int ILP, int PRIO = 0, int R = 32>
 __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
   constexpr int ND = 4 * NG;
-  fill_lds_slicing(a.tabs, lds);
+  static_assert(R == 32 || R == 16, "32- or 16-replica table image");
+  if constexpr (R == 32) fill_lds_slicing(a.tabs, lds);
+  else fill_lds_slicing16(a.tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
-  const LaneConst kc = lane_const(lane);
+  const LaneConst kc = R == 32 ? lane_const(lane) : lane_const16(lane);
   __syncthreads();
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint64_t W = a.nwaves, nb = a.nblocks;

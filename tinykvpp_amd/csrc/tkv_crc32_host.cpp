@@ -481,9 +481,11 @@ int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t s
   if (static_cast<long long>(len) <= lane_max() && !small_exact64) {
     // one lane per block: any stride, alignment and initial registers
     const std::uint64_t steps = (n + 63) / 64;
+    constexpr std::uint64_t kLaneWaves = kLaneThreads / 64;
+    const std::uint64_t wgs = TKV_AB_LANES16 ? 2u * c->ncu : c->ncu;  // (A/B: two workgroups per CU)
     const std::uint64_t grid =
-        std::max<std::uint64_t>(1, std::min<std::uint64_t>(c->ncu, (steps + kWavesPerWG - 1) / kWavesPerWG));
-    a.nwaves = static_cast<std::uint32_t>(grid * kWavesPerWG);
+        std::max<std::uint64_t>(1, std::min<std::uint64_t>(wgs, (steps + kLaneWaves - 1) / kLaneWaves));
+    a.nwaves = static_cast<std::uint32_t>(grid * kLaneWaves);
     TKV_HIP(launch_lanes(a, static_cast<unsigned>(grid), st));
     return TKV_OK;
   }

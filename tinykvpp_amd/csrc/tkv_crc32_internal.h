@@ -29,6 +29,13 @@ constexpr int kSeg = 64;                 // contiguous bytes one lane folds per 
 constexpr int kRow = 64 * kSeg;          // bytes one wave folds per row (4 KiB)
 constexpr int kWavesPerWG = 16;          // packed kernel: 1024-thread workgroups, one per CU (LDS-bound)
 constexpr int kThreads = 64 * kWavesPerWG;
+#ifndef TKV_AB_LANES16  // (A/B builds only: the lane kernel on a 64 KiB table image, two workgroups per CU)
+#define TKV_AB_LANES16 0
+#endif
+#ifndef TKV_AB_LANES16_THREADS
+#define TKV_AB_LANES16_THREADS 1024
+#endif
+constexpr int kLaneThreads = TKV_AB_LANES16 ? TKV_AB_LANES16_THREADS : kThreads;  // crc_lanes_n's workgroup
 constexpr int kRowsWavesPerWG = 12;      // generic row kernels: 768 threads (162 VGPRs at ILP 2)
 constexpr int kRowsThreads = 64 * kRowsWavesPerWG;
 

@@ -204,12 +204,24 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small_gen(RowsArgs a) {
 // NG 3, 5 at NG 4, 4 at NG 5, ILP 1. Only the slicing tables go to LDS (128 KiB).
 // In one process against the five-granule DEPTH 3-4 kernel of round 3 (profiles/r4/lanes_ab/):
 // 26 B 3544 -> 3825 GB/s, 16 B 3615 -> 3720, 28 B 3877 -> 4044, 36 B and 59 B unchanged.
+#ifndef TKV_AB_LANES16_DEPTH
+#define TKV_AB_LANES16_DEPTH 3
+#endif
+#if TKV_AB_LANES16
+template <int ALIGN, int NG>
+__global__ __launch_bounds__(kLaneThreads, 2) void crc_lanes_n(RowsArgs a) {
+  constexpr int DEPTH = TKV_AB_LANES16_DEPTH;
+  __shared__ std::uint32_t lds[kLdsSliceWords / 2];
+  dev::crc_lanes_n_body<ALIGN, NG, DEPTH, 1, kPackedPrio, 16>(a, lds);
+}
+#else
 template <int ALIGN, int NG>
 __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
   constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? 5 : 4;
   __shared__ std::uint32_t lds[kLdsSliceWords];
   dev::crc_lanes_n_body<ALIGN, NG, DEPTH, 1, kPackedPrio>(a, lds);
 }
+#endif
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 
@@ -936,7 +948,7 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st) {
   const int align = (m & 15u) == 0 ? 16 : (m & 3u) == 0 ? 4 : 1;
   const std::uint32_t mis = align == 16 ? 0u : align == 4 ? 12u : 15u;  // worst start offset in a granule
   const std::uint32_t ng = std::max<std::uint32_t>(1u, (a.len + mis + 15u) / 16u);  // granules a block can touch
-  const dim3 g(grid), b(kThreads);
+  const dim3 g(grid), b(kLaneThreads);
 #define TKV_LANES_N(A)                                                                  \
   switch (ng) {                                                                         \
     case 1: hipLaunchKernelGGL((crc_lanes_n<A, 1>), g, b, 0, st, a); break;             \
