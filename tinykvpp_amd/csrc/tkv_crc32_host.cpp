@@ -30,7 +30,7 @@ hipError_t launch_fixup(const RowsArgs& a, hipStream_t st);
 hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st);
 std::uint32_t packed_small_group(std::uint32_t len);
 hipError_t launch_packed_small(const RowsArgs& a, unsigned grid, hipStream_t st);
-hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st);
+hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st);
 std::uint32_t packed_small_gen_group(std::uint32_t len);
 hipError_t launch_packed_small_gen(const RowsArgs& a, unsigned grid, hipStream_t st);
 hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
@@ -479,14 +479,9 @@ int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t s
   // 4108 GB/s, profiles/r3/lanes/ab_shapes.jsonl)
   const bool small_exact64 = aligned && !d_init && stride == len && len == 64;
   if (static_cast<long long>(len) <= lane_max() && !small_exact64) {
-    // one lane per block: any stride, alignment and initial registers
-    const std::uint64_t steps = (n + 63) / 64;
-    constexpr std::uint64_t kLaneWaves = kLaneThreads / 64;
-    const std::uint64_t wgs = TKV_AB_LANES16 ? 2u * c->ncu : c->ncu;  // (A/B: two workgroups per CU)
-    const std::uint64_t grid =
-        std::max<std::uint64_t>(1, std::min<std::uint64_t>(wgs, (steps + kLaneWaves - 1) / kLaneWaves));
-    a.nwaves = static_cast<std::uint32_t>(grid * kLaneWaves);
-    TKV_HIP(launch_lanes(a, static_cast<unsigned>(grid), st));
+    // one lane per block: any stride, alignment and initial registers; the launch
+    // sizes its own grid (and a.nwaves) by the window's workgroup shape
+    TKV_HIP(launch_lanes(a, static_cast<unsigned>(c->ncu), st));
     return TKV_OK;
   }
   if (aligned && !d_init && stride == len && packed_small_group(a.len)) {

@@ -29,13 +29,16 @@ constexpr int kSeg = 64;                 // contiguous bytes one lane folds per 
 constexpr int kRow = 64 * kSeg;          // bytes one wave folds per row (4 KiB)
 constexpr int kWavesPerWG = 16;          // packed kernel: 1024-thread workgroups, one per CU (LDS-bound)
 constexpr int kThreads = 64 * kWavesPerWG;
-#ifndef TKV_AB_LANES16  // (A/B builds only: the lane kernel on a 64 KiB table image, two workgroups per CU)
-#define TKV_AB_LANES16 0
+// The uniform lane kernel runs windows of up to 4 granules on the 64 KiB 16-replica table image with
+// two workgroups per CU (LaneShape in tkv_crc32_kernels.hip). TKV_AB_LANES16=0 builds
+// every window on the 128 KiB image with one 1024-thread workgroup per CU; windows of at most
+// TKV_AB_LANES16_NARROW granules take 1024-thread workgroups, wider ones 768 (A/B builds only).
+#ifndef TKV_AB_LANES16
+#define TKV_AB_LANES16 1
 #endif
-#ifndef TKV_AB_LANES16_THREADS
-#define TKV_AB_LANES16_THREADS 1024
+#ifndef TKV_AB_LANES16_NARROW
+#define TKV_AB_LANES16_NARROW 3
 #endif
-constexpr int kLaneThreads = TKV_AB_LANES16 ? TKV_AB_LANES16_THREADS : kThreads;  // crc_lanes_n's workgroup
 constexpr int kRowsWavesPerWG = 12;      // generic row kernels: 768 threads (162 VGPRs at ILP 2)
 constexpr int kRowsThreads = 64 * kRowsWavesPerWG;
 

@@ -204,15 +204,29 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small_gen(RowsArgs a) {
 // NG 3, 5 at NG 4, 4 at NG 5, ILP 1. Only the slicing tables go to LDS (128 KiB).
 // In one process against the five-granule DEPTH 3-4 kernel of round 3 (profiles/r4/lanes_ab/):
 // 26 B 3544 -> 3825 GB/s, 16 B 3615 -> 3720, 28 B 3877 -> 4044, 36 B and 59 B unchanged.
-#ifndef TKV_AB_LANES16_DEPTH
-#define TKV_AB_LANES16_DEPTH 3
-#endif
+// Per window size: threads per workgroup, workgroups per CU and pipeline depth. Narrow windows fit
+// two 1024-thread workgroups per CU (8 waves per SIMD: at most 64 VGPRs), 4 granules two 768-thread
+// ones (6 waves: 80 VGPRs); 5 granules keep the 128 KiB image's shape (one 1024-thread workgroup,
+// DEPTH 4), whose window does not fit 80 registers deep enough.
+template <int NG>
+struct LaneShape {
+  static constexpr bool kW16 = TKV_AB_LANES16 && NG <= 4;
+  static constexpr unsigned kThreads = !kW16 ? 1024u : NG <= TKV_AB_LANES16_NARROW ? 1024u : 768u;
+  static constexpr unsigned kWgPerCu = kW16 ? 2u : 1u;
+  static constexpr int kDepth = !kW16 ? 4 : 3;
+};
 #if TKV_AB_LANES16
 template <int ALIGN, int NG>
-__global__ __launch_bounds__(kLaneThreads, 2) void crc_lanes_n(RowsArgs a) {
-  constexpr int DEPTH = TKV_AB_LANES16_DEPTH;
-  __shared__ std::uint32_t lds[kLdsSliceWords / 2];
-  dev::crc_lanes_n_body<ALIGN, NG, DEPTH, 1, kPackedPrio, 16>(a, lds);
+__global__ __launch_bounds__(LaneShape<NG>::kThreads)
+__attribute__((amdgpu_waves_per_eu(LaneShape<NG>::kWgPerCu * LaneShape<NG>::kThreads / 256))) void
+crc_lanes_n(RowsArgs a) {
+  if constexpr (LaneShape<NG>::kW16) {
+    __shared__ std::uint32_t lds[kLdsSliceWords / 2];
+    dev::crc_lanes_n_body<ALIGN, NG, LaneShape<NG>::kDepth, 1, kPackedPrio, 16>(a, lds);
+  } else {
+    __shared__ std::uint32_t lds[kLdsSliceWords];
+    dev::crc_lanes_n_body<ALIGN, NG, LaneShape<NG>::kDepth, 1, kPackedPrio>(a, lds);
+  }
 }
 #else
 template <int ALIGN, int NG>
@@ -942,20 +956,32 @@ hipError_t launch_packed_small_gen(const RowsArgs& a, unsigned grid, hipStream_t
 }
 
 // Uniform lane-block batch (a.len <= kLaneMax): ALIGN from the base pointer and the stride.
-hipError_t launch_lanes(const RowsArgs& a, unsigned grid, hipStream_t st) {
+template <int ALIGN, int NG>
+void launch_lanes_shape(RowsArgs a, unsigned ncu, hipStream_t st) {
+  using S = LaneShape<NG>;
+  const std::uint64_t steps = (static_cast<std::uint64_t>(a.nblocks) + 63u) / 64u;
+  const std::uint64_t waves = S::kThreads / 64u;
+  const std::uint64_t grid =
+      std::max<std::uint64_t>(1, std::min<std::uint64_t>(static_cast<std::uint64_t>(ncu) * S::kWgPerCu, (steps + waves - 1) / waves));
+  a.nwaves = static_cast<std::uint32_t>(grid * waves);
+  hipLaunchKernelGGL((crc_lanes_n<ALIGN, NG>), dim3(static_cast<unsigned>(grid)), dim3(S::kThreads), 0, st, a);
+}
+
+// Uniform lane-block batch (a.len <= kLaneMax): ALIGN from the base pointer and the stride, the window
+// (NG granules) from the length; grid and waves from the window's LaneShape.
+hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   if (a.len > kLaneMax) return hipErrorInvalidValue;
   const std::uintptr_t m = reinterpret_cast<std::uintptr_t>(a.base) | static_cast<std::uintptr_t>(a.stride);
   const int align = (m & 15u) == 0 ? 16 : (m & 3u) == 0 ? 4 : 1;
   const std::uint32_t mis = align == 16 ? 0u : align == 4 ? 12u : 15u;  // worst start offset in a granule
   const std::uint32_t ng = std::max<std::uint32_t>(1u, (a.len + mis + 15u) / 16u);  // granules a block can touch
-  const dim3 g(grid), b(kLaneThreads);
-#define TKV_LANES_N(A)                                                                  \
-  switch (ng) {                                                                         \
-    case 1: hipLaunchKernelGGL((crc_lanes_n<A, 1>), g, b, 0, st, a); break;             \
-    case 2: hipLaunchKernelGGL((crc_lanes_n<A, 2>), g, b, 0, st, a); break;             \
-    case 3: hipLaunchKernelGGL((crc_lanes_n<A, 3>), g, b, 0, st, a); break;             \
-    case 4: hipLaunchKernelGGL((crc_lanes_n<A, 4>), g, b, 0, st, a); break;             \
-    default: hipLaunchKernelGGL((crc_lanes_n<A, 5>), g, b, 0, st, a); break;            \
+#define TKV_LANES_N(A)                                           \
+  switch (ng) {                                                  \
+    case 1: launch_lanes_shape<A, 1>(a, ncu, st); break;         \
+    case 2: launch_lanes_shape<A, 2>(a, ncu, st); break;         \
+    case 3: launch_lanes_shape<A, 3>(a, ncu, st); break;         \
+    case 4: launch_lanes_shape<A, 4>(a, ncu, st); break;         \
+    default: launch_lanes_shape<A, 5>(a, ncu, st); break;        \
   }
   if (align == 16) { TKV_LANES_N(16) }
   else if (align == 4) { TKV_LANES_N(4) }

@@ -34,7 +34,21 @@ namespace tkv {
 namespace {
 
 constexpr std::uint32_t kRecMeta = 26;  // wal.hpp kMetadataSize: 8-byte header + op, seq, tombstone, key/value lengths
-constexpr unsigned kRecThreads = 1024;  // one workgroup per CU (128 KiB of LDS tables)
+// Narrow windows (4-5 granules, payloads up to 54 bytes) run on the 64 KiB 16-replica table image
+// with two 768-thread workgroups per CU (24 waves, at most 80 VGPRs), as the lane kernel does;
+// wider ones keep the 128 KiB image and one 1024-thread workgroup per CU (their windows need the
+// registers). TKV_AB_REC16=0 builds every window the wide way (A/B builds only).
+#ifndef TKV_AB_REC16
+#define TKV_AB_REC16 1
+#endif
+#ifndef TKV_AB_REC16_AHEAD
+#define TKV_AB_REC16_AHEAD 1
+#endif
+template <bool W16>
+struct RecShape {
+  static constexpr unsigned kThreads = W16 ? 768 : 1024;
+  static constexpr unsigned kWgPerCu = W16 ? 2 : 1;
+};
 
 struct RecArgs {
   const std::uint8_t* w;
@@ -85,17 +99,20 @@ __device__ __forceinline__ std::uint32_t rec_fold(const std::uint32_t* lds, cons
 
 // NG granules per record window; AHEAD steps of granules in flight (3 for narrow windows, 2 at 6
 // granules, 1 for the wide ones, whose three slots would spill at 16 waves per CU).
-template <int NG, int AHEAD>
-__global__ __launch_bounds__(kRecThreads) void wal_rec_lanes(RecArgs a, const DeviceTables* tabs) {
+template <int NG, int AHEAD, bool W16>
+__global__ __launch_bounds__(RecShape<W16>::kThreads)
+__attribute__((amdgpu_waves_per_eu(RecShape<W16>::kWgPerCu * RecShape<W16>::kThreads / 256))) void
+wal_rec_lanes(RecArgs a, const DeviceTables* tabs) {
   constexpr int ND = 4 * NG - 4;      // realigned dwords of the window
   constexpr int NPAY = ND - 3;        // whole payload dwords folded from the window (payload at dword 2; one spare for the tail)
   constexpr int RING = 4;             // offsets are fetched RING steps ahead of their granules
   constexpr int DRING = AHEAD == 1 ? 2 : 4;
   static_assert(AHEAD >= 1 && AHEAD <= 3, "granules one to three steps ahead");
-  __shared__ std::uint32_t lds[kLdsSliceWords];
-  dev::fill_lds_slicing(tabs, lds);
+  __shared__ std::uint32_t lds[W16 ? kLdsSliceWords / 2 : kLdsSliceWords];
+  if constexpr (W16) dev::fill_lds_slicing16(tabs, lds);
+  else dev::fill_lds_slicing(tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
-  const dev::LaneConst kc = dev::lane_const(lane);
+  const dev::LaneConst kc = W16 ? dev::lane_const16(lane) : dev::lane_const(lane);
   __syncthreads();
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint64_t W = a.nwaves, n = a.n;
@@ -191,22 +208,28 @@ int cu_count() {
 // The record check over n records (first_bad preset to n by the caller's stream order).
 void launch_records(RecArgs a, std::uint32_t max_payload, int ncu, const DeviceTables* tabs, hipStream_t st) {
   const std::uint64_t steps = (a.n + 63) / 64;
-  const std::uint64_t grid =
-      std::max<std::uint64_t>(1, std::min<std::uint64_t>(static_cast<std::uint64_t>(ncu), (steps + 15) / 16));
-  a.nwaves = static_cast<std::uint32_t>(grid * 16);
   // window: NG granules hold the header, the key/value lengths and a payload of up to 16 NG - 26 bytes
   // at any alignment (36-byte payloads: 4 granules; 64: 6; 100: 8); longer ones continue 64 bytes at
   // a time. Records are latency-bound like the lane kernel (profiles/r4/rec_check/): narrow windows keep
   // three steps of granules in flight, 6 granules two, wider ones one (registers).
   const std::uint32_t ng =
       std::min<std::uint32_t>(8u, std::max<std::uint32_t>(4u, (std::min<std::uint32_t>(max_payload, 1024u) + 26u + 15u) / 16u));
-  const dim3 g(static_cast<unsigned>(grid)), b(kRecThreads);
-  switch (ng) {
-    case 4: hipLaunchKernelGGL((wal_rec_lanes<4, 3>), g, b, 0, st, a, tabs); break;
-    case 5: hipLaunchKernelGGL((wal_rec_lanes<5, 3>), g, b, 0, st, a, tabs); break;
-    case 6: hipLaunchKernelGGL((wal_rec_lanes<6, 2>), g, b, 0, st, a, tabs); break;
-    case 7: hipLaunchKernelGGL((wal_rec_lanes<7, 1>), g, b, 0, st, a, tabs); break;
-    default: hipLaunchKernelGGL((wal_rec_lanes<8, 1>), g, b, 0, st, a, tabs); break;
+  const bool w16 = TKV_AB_REC16 && ng <= 5;
+  const std::uint64_t threads = w16 ? RecShape<true>::kThreads : RecShape<false>::kThreads;
+  const std::uint64_t per_cu = w16 ? RecShape<true>::kWgPerCu : RecShape<false>::kWgPerCu;
+  const std::uint64_t waves = threads / 64;
+  const std::uint64_t grid = std::max<std::uint64_t>(
+      1, std::min<std::uint64_t>(static_cast<std::uint64_t>(ncu) * per_cu, (steps + waves - 1) / waves));
+  a.nwaves = static_cast<std::uint32_t>(grid * waves);
+  const dim3 g(static_cast<unsigned>(grid)), b(static_cast<unsigned>(threads));
+  switch (w16 ? ng : ng + 16u) {
+    case 4: hipLaunchKernelGGL((wal_rec_lanes<4, TKV_AB_REC16_AHEAD, true>), g, b, 0, st, a, tabs); break;
+    case 5: hipLaunchKernelGGL((wal_rec_lanes<5, TKV_AB_REC16_AHEAD, true>), g, b, 0, st, a, tabs); break;
+    case 20: hipLaunchKernelGGL((wal_rec_lanes<4, 3, false>), g, b, 0, st, a, tabs); break;
+    case 21: hipLaunchKernelGGL((wal_rec_lanes<5, 3, false>), g, b, 0, st, a, tabs); break;
+    case 22: hipLaunchKernelGGL((wal_rec_lanes<6, 2, false>), g, b, 0, st, a, tabs); break;
+    case 23: hipLaunchKernelGGL((wal_rec_lanes<7, 1, false>), g, b, 0, st, a, tabs); break;
+    default: hipLaunchKernelGGL((wal_rec_lanes<8, 1, false>), g, b, 0, st, a, tabs); break;
   }
 }
 
