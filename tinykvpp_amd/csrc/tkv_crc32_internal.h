@@ -29,12 +29,13 @@ constexpr int kSeg = 64;                 // contiguous bytes one lane folds per 
 constexpr int kRow = 64 * kSeg;          // bytes one wave folds per row (4 KiB)
 constexpr int kWavesPerWG = 16;          // packed kernel: 1024-thread workgroups, one per CU (LDS-bound)
 constexpr int kThreads = 64 * kWavesPerWG;
-// The uniform lane kernel runs windows of up to 4 granules on the 64 KiB 16-replica table image with
-// two workgroups per CU (LaneShape in tkv_crc32_kernels.hip). TKV_AB_LANES16=0 builds
-// every window on the 128 KiB image with one 1024-thread workgroup per CU; windows of at most
-// TKV_AB_LANES16_NARROW granules take 1024-thread workgroups, wider ones 768 (A/B builds only).
+// A/B builds only (TKV_AB_LANES16=1): the uniform lane kernel's windows of up to 4 granules on the
+// 64 KiB 16-replica table image with two workgroups per CU (LaneShape in tkv_crc32_kernels.hip;
+// 1024 threads for windows of at most TKV_AB_LANES16_NARROW granules, 768 for wider ones). Measured
+// against the 128 KiB image with one 1024-thread workgroup per CU, in one process: within -5..+2 %
+// (profiles/r4/lanes16/), so the product keeps the 128 KiB image.
 #ifndef TKV_AB_LANES16
-#define TKV_AB_LANES16 1
+#define TKV_AB_LANES16 0
 #endif
 #ifndef TKV_AB_LANES16_NARROW
 #define TKV_AB_LANES16_NARROW 3

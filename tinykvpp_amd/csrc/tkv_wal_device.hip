@@ -52,7 +52,14 @@ constexpr std::uint64_t kWalMeta = 26;        // wal.hpp:21-27 kMetadataSize
 constexpr std::uint32_t kWalLaneMax = 1024;   // payloads up to this size are checked by their lane
 constexpr std::uint64_t kNone = ~0ull;
 constexpr unsigned kScanThreads = 256;        // wal_scan_head: 8 lanes per piece, 8 pieces per wave
-constexpr unsigned kCheckThreads = 1024;      // wal_spec/wal_recheck: one workgroup per CU (128 KiB of LDS)
+constexpr unsigned kCheckThreads = 1024;      // wal_spec/wal_recheck
+// A/B builds only (TKV_AB_WAL16=1): wal_spec/wal_recheck on the 64 KiB 16-replica table image with two
+// workgroups per CU (32 waves, at most 64 VGPRs) where the 128 KiB image allows one: the walk is
+// latency-bound (8 or 4 waves per CU instead of 16 were 15 % and 66 % slower).
+#ifndef TKV_AB_WAL16
+#define TKV_AB_WAL16 0
+#endif
+constexpr unsigned kCheckWgPerCu = TKV_AB_WAL16 ? 2 : 1;
 constexpr unsigned kHres = 16;                // words of the pinned result block
 
 struct WalArgs {
@@ -254,12 +261,16 @@ __device__ __forceinline__ std::uint32_t lane_crc(const std::uint32_t* lds, cons
 
 // Slicing tables into LDS (the row kernels' lane-shift tables are not needed here).
 __device__ __forceinline__ void fill_slices(const DeviceTables* tabs, std::uint32_t* lds) {
-  for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
-    const std::uint32_t pair = u >> 9, e = (u >> 1) & 255u, tt = u & 1u;
-    const std::uint32_t v = tabs->slice[2 * pair + tt][e];
-    uint4* dst = reinterpret_cast<uint4*>(lds + pair * 16384u + e * 64u + tt * 32u);
+  if constexpr (TKV_AB_WAL16) {
+    dev::fill_lds_slicing16(tabs, lds);
+  } else {
+    for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
+      const std::uint32_t pair = u >> 9, e = (u >> 1) & 255u, tt = u & 1u;
+      const std::uint32_t v = tabs->slice[2 * pair + tt][e];
+      uint4* dst = reinterpret_cast<uint4*>(lds + pair * 16384u + e * 64u + tt * 32u);
 #pragma unroll
-    for (std::uint32_t k = 0; k < 8u; ++k) dst[(k + u) & 7u] = make_uint4(v, v, v, v);
+      for (std::uint32_t k = 0; k < 8u; ++k) dst[(k + u) & 7u] = make_uint4(v, v, v, v);
+    }
   }
   __syncthreads();
 }
@@ -361,8 +372,9 @@ __device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::
 
 // 2. Speculative walk and check of pieces [k_lo, k_hi) from their first plausible header (piece 0
 // from 0).
-__global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
-  __shared__ std::uint32_t lds[kLdsSliceWords];
+__global__ __launch_bounds__(kCheckThreads) __attribute__((amdgpu_waves_per_eu(kCheckWgPerCu * kCheckThreads / 256))) void
+wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
+  __shared__ std::uint32_t lds[TKV_AB_WAL16 ? kLdsSliceWords / 2 : kLdsSliceWords];
   fill_slices(a.tabs, lds);
   const std::uint64_t k = k_lo + gid();
   if (k >= k_hi) return;
@@ -376,7 +388,7 @@ __global__ __launch_bounds__(kCheckThreads) void wal_spec(WalArgs a, std::uint64
     a.first_loc[k] = kNone;
     return;
   }
-  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
+  const dev::LaneConst kc = TKV_AB_WAL16 ? dev::lane_const16(threadIdx.x & 63u) : dev::lane_const(threadIdx.x & 63u);
   std::uint64_t x, c;
   std::uint8_t br;
   walk_check(lds, kc, a, k, s, &x, &br, &c);
@@ -511,12 +523,13 @@ __global__ void wal_count(WalArgs a) {
 }
 
 // Pieces entered off their speculative start: check their records from the true entry.
-__global__ __launch_bounds__(kCheckThreads) void wal_recheck(WalArgs a) {
-  __shared__ std::uint32_t lds[kLdsSliceWords];
+__global__ __launch_bounds__(kCheckThreads) __attribute__((amdgpu_waves_per_eu(kCheckWgPerCu * kCheckThreads / 256))) void
+wal_recheck(WalArgs a) {
+  __shared__ std::uint32_t lds[TKV_AB_WAL16 ? kLdsSliceWords / 2 : kLdsSliceWords];
   fill_slices(a.tabs, lds);
   const std::uint64_t k = gid();
   if (k >= a.K || !a.recheck[k]) return;
-  const dev::LaneConst kc = dev::lane_const(threadIdx.x & 63u);
+  const dev::LaneConst kc = TKV_AB_WAL16 ? dev::lane_const16(threadIdx.x & 63u) : dev::lane_const(threadIdx.x & 63u);
   std::uint64_t x, c;
   std::uint8_t br;
   walk_check(lds, kc, a, k, a.entry[k], &x, &br, &c);

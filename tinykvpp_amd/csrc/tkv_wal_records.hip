@@ -34,12 +34,12 @@ namespace tkv {
 namespace {
 
 constexpr std::uint32_t kRecMeta = 26;  // wal.hpp kMetadataSize: 8-byte header + op, seq, tombstone, key/value lengths
-// Narrow windows (4-5 granules, payloads up to 54 bytes) run on the 64 KiB 16-replica table image
-// with two 768-thread workgroups per CU (24 waves, at most 80 VGPRs), as the lane kernel does;
-// wider ones keep the 128 KiB image and one 1024-thread workgroup per CU (their windows need the
-// registers). TKV_AB_REC16=0 builds every window the wide way (A/B builds only).
+// A/B builds only (TKV_AB_REC16=1): narrow windows (4-5 granules, payloads up to 54 bytes) on the
+// 64 KiB 16-replica table image with two 768-thread workgroups per CU (24 waves, at most 80 VGPRs).
+// Measured 3 % slower than the 128 KiB image with one 1024-thread workgroup per CU
+// (profiles/r4/lanes16/rec_probe_rec16.jsonl), which every window keeps.
 #ifndef TKV_AB_REC16
-#define TKV_AB_REC16 1
+#define TKV_AB_REC16 0
 #endif
 #ifndef TKV_AB_REC16_AHEAD
 #define TKV_AB_REC16_AHEAD 1
