@@ -1537,6 +1537,19 @@ __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_
   }
 }
 
+// Steps of data in flight ahead of the fold in the lane phase and the group walks (the ring holds
+// four; A/B builds: -DTKV_AB_WALK_AHEAD=3).
+#ifndef TKV_AB_WALK_AHEAD
+#define TKV_AB_WALK_AHEAD 2
+#endif
+#ifndef TKV_AB_LIST_AHEAD  // (the small phase's list walks, in crc_rows: registers to spare)
+#define TKV_AB_LIST_AHEAD 2
+#endif
+constexpr int kWalkAhead = TKV_AB_WALK_AHEAD;
+constexpr int kListAhead = TKV_AB_LIST_AHEAD;
+static_assert(kWalkAhead >= 1 && kWalkAhead <= 3 && kListAhead >= 1 && kListAhead <= 3,
+              "at most three steps ahead of a four-slot ring");
+
 // Lane blocks of an irregular batch (len <= kLaneMax, in a scan tile the prepass marked dense), walked
 // straight from the caller's offsets and lengths (the prepass lists them nowhere): wave w takes the
 // blocks [w n / W, (w + 1) n / W) 64 at a time, lane l of step j the block b0 + 64 j + l, and folds it
@@ -1589,16 +1602,16 @@ __device__ __forceinline__ void lane_phase(const RowsArgs& a, const std::uint32_
 #pragma unroll
   for (int k = 0; k < RING; ++k) fetch(k, k);
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kWalkAhead; ++k) {
     issue(k, k);
     fetch(k + RING, k);
   }
   for (std::uint32_t t = 0; t < ns; t += RING) {
 #pragma unroll
     for (int k = 0; k < RING; ++k) {
-      const int ahead = (k + 2) % RING;  // step t+k+2: its descriptor arrived RING steps ago
-      issue(ahead, t + k + 2);
-      fetch(t + k + 2 + RING, ahead);
+      const int ahead = (k + kWalkAhead) % RING;  // step t+k+kWalkAhead: its descriptor arrived RING steps ago
+      issue(ahead, t + k + kWalkAhead);
+      fetch(t + k + kWalkAhead + RING, ahead);
       if (t + k < ns) fold(k, t + k);
     }
   }
@@ -1625,6 +1638,7 @@ __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_
                                            std::uint32_t cnt) {
   static_assert(G == 4 || G == 8 || (LIST && G == 16), "4- or 8-lane groups (16 for listed blocks)");
   constexpr int RING = 4;
+  constexpr int kAhead = LIST ? kListAhead : kWalkAhead;  // steps of data in flight
   constexpr std::uint32_t kSlot = 64u * G;
   constexpr std::uint32_t kLo = G == 4 ? kLaneMax : kGroupMax;  // the class: (kLo, kSlot]
   constexpr std::uint32_t kFlag = G == 4 ? kTileGroups : kTileGroups8;
@@ -1718,16 +1732,16 @@ __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_
 #pragma unroll
   for (int k = 0; k < RING; ++k) fetch(k, k);
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kAhead; ++k) {
     issue(k, k);
     fetch(k + RING, k);
   }
   for (std::uint32_t t = 0; t < ns; t += RING) {
 #pragma unroll
     for (int k = 0; k < RING; ++k) {
-      const int ahead = (k + 2) % RING;  // step t+k+2: its descriptor arrived RING steps ago
-      issue(ahead, t + k + 2);
-      fetch(t + k + 2 + RING, ahead);
+      const int ahead = (k + kAhead) % RING;  // step t+k+kAhead: its descriptor arrived RING steps ago
+      issue(ahead, t + k + kAhead);
+      fetch(t + k + kAhead + RING, ahead);
       if (t + k < ns) fold(k, t + k);
     }
   }
