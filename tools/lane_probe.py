@@ -95,6 +95,8 @@ def main():
     work.append(irregular("irregular back to back 64 B", np.full(n, 64), np.zeros(n, np.int64), 0))
     n = count(128, 128)
     work.append(irregular("irregular back to back 128 B", np.full(n, 128), np.zeros(n, np.int64), 0))
+    n = count(150, 150)
+    work.append(irregular("irregular back to back 100-200 B", rng.integers(100, 201, n), np.zeros(n, np.int64), 0))
     # 257 B - 1 KiB: WAL payloads with mid-size values, gapped and back to back
     for lo, hi in ((257, 512), (513, 1024), (300, 1000), (257, 1024)):
         ng = count((lo + hi) // 2, (lo + hi) // 2 + 8)

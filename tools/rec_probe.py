@@ -3,6 +3,7 @@
 
 Images of ~1 GiB in HBM laid out as wal.cpp:19-61 (stamped by tkv_wal_stamp):
   * "36 B payloads": uniform 44-byte records (payload 36 B, the verdict's gapped WAL payloads);
+  * "28 B payloads": uniform 36-byte records (the shape round 4's first probes ran under the 36 B label);
   * "small records": 26 + |k| + |v| bytes, |k| 4-23, |v| 0-39 (tools/ab_wal.py's image, payloads 22-80 B).
 For each: tkv_wal_check_records_device over the record offsets (u32) and tkv_crc32_batch_device over
 (payload offsets u64, lengths u32), HIP events around K calls, several libraries rotated in one
@@ -60,7 +61,11 @@ def main():
     total = int(args.gib * (1 << 30))
     n36 = total // 44
     n_small = total // 59
-    imgs = [("36 B payloads (44-byte records)", np.full(n36, 4, np.uint64), np.full(n36, 6, np.uint64), 36),
+    # (round 4's first probes used klen 4 / vlen 6, i.e. 36-byte records with 28-byte payloads, under
+    # the 36 B label; both shapes are measured now)
+    n28 = total // 36
+    imgs = [("36 B payloads (44-byte records)", np.full(n36, 8, np.uint64), np.full(n36, 10, np.uint64), 36),
+            ("28 B payloads (36-byte records)", np.full(n28, 4, np.uint64), np.full(n28, 6, np.uint64), 28),
             ("small records (payloads 22-80 B)", rng.integers(4, 24, n_small).astype(np.uint64),
              rng.integers(0, 40, n_small).astype(np.uint64), 80)]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
