@@ -375,6 +375,7 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->wave_start), sizeof(std::uint32_t) * c->W));
     // counts[0..3], then (u64) the stream-mode info at counts + 4
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->counts), sizeof(std::uint32_t) * 16));
+    TKV_HIP(hipMemset(slot->counts, 0, sizeof(std::uint32_t) * 16));  // (the tile scan's ticket starts at 0)
   }
   StreamScratch* s = slot.get();
   if (nblocks > s->cap_blocks) {

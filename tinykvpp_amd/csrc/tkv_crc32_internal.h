@@ -135,6 +135,9 @@ constexpr int kCountPhases = 9;
 // folds each class with groups of 4, 8 or 16 lanes.
 constexpr int kCountSmall4 = 10;
 constexpr int kCountSmall8 = 11;
+// counts[kCountTicket]: workgroups of the tile scan done so far (the last one scans the tile sums and
+// resets it to 0; zero when the scratch is allocated).
+constexpr int kCountTicket = 12;
 
 // Blocks of at most kLaneMax bytes are folded whole by one lane each, from their own initial register
 // (DESIGN.md §4.5): uniform batches by crc_lanes, irregular ones by the lane phase in crc_stream's

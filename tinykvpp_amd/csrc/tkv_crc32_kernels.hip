@@ -280,6 +280,17 @@ __device__ __forceinline__ StreamGeom stream_geometry(const std::uint8_t* base, 
 // process, 1 GiB batches, profiles/r3/scan_tiles/: WAL payloads of 36 B with 8-byte gaps 1820 ->
 // 1957 GB/s, back-to-back 36 B 1991 -> 2212, 64 B 2687 -> 2818, 128 B 730 -> 697 GB/s; cfg4 and
 // the 64 KiB stream batch unchanged either way).
+struct ScanLds {  // rows_scan_tiles_body's workspace (1024 threads)
+  std::uint64_t part[1024], cpart[1024];
+  std::uint32_t lpart[1024];
+  std::uint32_t sph;
+};
+__device__ __forceinline__ void rows_scan_tiles_body(ScanLds& L, std::uint64_t* tile_sums, std::uint32_t* tile_lanes,
+                                                     std::uint64_t* tile_cls, std::uint32_t ntiles, std::uint32_t n,
+                                                     std::uint32_t* counts, const std::uint32_t* tile_ok,
+                                                     const std::uint8_t* base, const std::uint64_t* offsets,
+                                                     const std::uint32_t* lengths, std::uint64_t* sinfo);
+
 template <unsigned kTileThreads>
 __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_t* sbase, const std::uint64_t* offsets,
                                                               const std::uint32_t* lengths, std::uint32_t n,
@@ -287,7 +298,8 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
                                                               std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
                                                               std::uint32_t* lscan, std::uint32_t* tile_lanes,
                                                               std::uint32_t* cscan, std::uint64_t* tile_cls,
-                                                              std::uint32_t group_stream) {
+                                                              std::uint32_t group_stream, std::uint32_t* counts,
+                                                              std::uint64_t* sinfo, std::uint32_t last_scans) {
   constexpr unsigned kTileWaves = kTileThreads / 64;
   constexpr unsigned kTileBpt = kScanTile / kTileThreads;
   static_assert(kScanTile % kTileThreads == 0 && kTileWaves >= 1 && kTileBpt >= 4 && kTileBpt % 4 == 0,
@@ -446,6 +458,26 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     const std::uint32_t tc = cls_pair(ltot);
     tile_cls[blockIdx.x] = (tc & 0xFFFFu) | (static_cast<std::uint64_t>(tc >> 16) << 32);
   }
+  // last_scans (batches of at most kFusedTiles tiles): the workgroup that finishes last scans the tile
+  // sums for all (rows_scan_tiles_body), so the scatter that follows reads its tile's offsets instead
+  // of every workgroup summing all tile sums again. Each workgroup's tile records are released by a
+  // device-scope fence before its ticket; the last one acquires them by another fence.
+  if constexpr (kTileThreads == 1024) {
+    if (last_scans) {  // (uniform)
+      __shared__ ScanLds L;
+      __shared__ std::uint32_t is_last;
+      __threadfence();
+      __syncthreads();
+      if (threadIdx.x == 0) is_last = atomicAdd(counts + kCountTicket, 1u) == gridDim.x - 1u ? 1u : 0u;
+      __syncthreads();
+      if (is_last) {
+        __threadfence();
+        rows_scan_tiles_body(L, tile_sums, tile_lanes, tile_cls, gridDim.x, n, counts, tile_ok, sbase, offsets,
+                             lengths, sinfo);
+        if (threadIdx.x == 0) counts[kCountTicket] = 0u;  // ready for the next batch on this stream
+      }
+    }
+  }
 }
 
 // Scan of the tile sums for batches of more than kFusedTiles tiles (one workgroup), with the
@@ -453,14 +485,15 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
 // values (as stream_block does for fused batches) and rows_finish builds the block ends.
 __device__ __forceinline__ StreamGeom stream_geometry(const std::uint8_t* base, const std::uint64_t* offsets,
                                                       const std::uint32_t* lengths, std::uint32_t n);
-__global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums, std::uint32_t* tile_lanes,
-                                                       std::uint64_t* tile_cls, std::uint32_t ntiles, std::uint32_t n, std::uint32_t* counts,
-                                                       const std::uint32_t* tile_ok, const std::uint8_t* base,
-                                                       const std::uint64_t* offsets, const std::uint32_t* lengths,
-                                                       std::uint64_t* sinfo) {
-  __shared__ std::uint64_t part[1024], cpart[1024];
-  __shared__ std::uint32_t lpart[1024];
-  __shared__ std::uint32_t sph;
+__device__ __forceinline__ void rows_scan_tiles_body(ScanLds& L, std::uint64_t* tile_sums, std::uint32_t* tile_lanes,
+                                                     std::uint64_t* tile_cls, std::uint32_t ntiles, std::uint32_t n,
+                                                     std::uint32_t* counts, const std::uint32_t* tile_ok,
+                                                     const std::uint8_t* base, const std::uint64_t* offsets,
+                                                     const std::uint32_t* lengths, std::uint64_t* sinfo) {
+  std::uint64_t* part = L.part;
+  std::uint64_t* cpart = L.cpart;
+  std::uint32_t* lpart = L.lpart;
+  std::uint32_t& sph = L.sph;
   if (threadIdx.x == 0) sph = 0;  // (the loop's first barrier orders this before the ORs below)
   std::uint64_t carry = 0, lcarry = 0, ccarry = 0;
   bool all_stream = true;
@@ -527,6 +560,14 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
     counts[kCountSmall8] = static_cast<std::uint32_t>(ccarry);
     counts[kCountSmall4] = ns - static_cast<std::uint32_t>(ccarry) - static_cast<std::uint32_t>(ccarry >> 32);
   }
+}
+__global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums, std::uint32_t* tile_lanes,
+                                                       std::uint64_t* tile_cls, std::uint32_t ntiles, std::uint32_t n, std::uint32_t* counts,
+                                                       const std::uint32_t* tile_ok, const std::uint8_t* base,
+                                                       const std::uint64_t* offsets, const std::uint32_t* lengths,
+                                                       std::uint64_t* sinfo) {
+  __shared__ ScanLds L;
+  rows_scan_tiles_body(L, tile_sums, tile_lanes, tile_cls, ntiles, n, counts, tile_ok, base, offsets, lengths, sinfo);
 }
 
 // Scatter of one block (rows_finish): e = its exclusive (small count, rows) pair, nlane = lane blocks
@@ -598,6 +639,11 @@ __global__ void rows_finish(const std::uint8_t* base, const std::uint64_t* offse
 // no single-workgroup tile-scan launch sits between the tile scan and the scatter. Workgroup 0
 // publishes counts for the row kernel.
 constexpr std::uint32_t kFusedTiles = 1024;
+// Batches of at most kFusedTiles tiles: the tile scan's last workgroup scans the tile sums and the
+// plain scatter follows (1), or every scatter workgroup sums the tile sums itself (0, A/B builds).
+#ifndef TKV_AB_LAST_SCANS
+#define TKV_AB_LAST_SCANS 1
+#endif
 // A 256-thread workgroup per 256 blocks, each re-reading all tile sums. One 1024-thread workgroup per
 // scan tile with 4 blocks per thread (TKV_AB_FINISH_PER=4) cuts those re-reads by 16 but measured
 // slower: 300-1000 B gapped 3210 -> 2929 GB/s, 257-512 B 3210 -> 2748 (profiles/r4/s7/): the scatter's
@@ -1006,15 +1052,19 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
   const std::uint64_t ntiles = prepass_tiles(n);
   const std::uint64_t nfused = (static_cast<std::uint64_t>(n) + kFinishThreads * kFinishPer - 1) / (kFinishThreads * kFinishPer);
   const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
+  const std::uint32_t last_scans = TKV_AB_LAST_SCANS && ntiles <= kFusedTiles ? 1u : 0u;
   if (ntiles <= kFusedTiles)
     hipLaunchKernelGGL(rows_tile_scan<1024>, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets,
                        lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
-                       group_stream);
+                       group_stream, counts, sinfo, last_scans);
   else
     hipLaunchKernelGGL(rows_tile_scan<512>, dim3(static_cast<unsigned>(ntiles)), dim3(512), 0, st, base, offsets,
                        lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
-                       group_stream);
-  if (ntiles <= kFusedTiles) {
+                       group_stream, counts, sinfo, 0u);
+  if (last_scans) {
+    hipLaunchKernelGGL(rows_finish, dim3(static_cast<unsigned>(nfinish)), dim3(256), 0, st, base, offsets, lengths,
+                       n, scan, tile_sums, counts, tile_ok, o, W, out, ends, sinfo, Ws, row0);
+  } else if (ntiles <= kFusedTiles) {
     hipLaunchKernelGGL((rows_finish_fused<kFinishThreads, kFinishPer>), dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
                        offsets, lengths, n, scan, tile_sums, tile_ok, static_cast<std::uint32_t>(ntiles), counts, o,
                        W, out, ends, sinfo, Ws, row0);
