@@ -462,6 +462,7 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
   // sums for all (rows_scan_tiles_body), so the scatter that follows reads its tile's offsets instead
   // of every workgroup summing all tile sums again. Each workgroup's tile records are released by a
   // device-scope fence before its ticket; the last one acquires them by another fence.
+#if TKV_AB_LAST_SCANS
   if constexpr (kTileThreads == 1024) {
     if (last_scans) {  // (uniform)
       __shared__ ScanLds L;
@@ -478,6 +479,11 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
       }
     }
   }
+#else
+  (void)counts;
+  (void)sinfo;
+  (void)last_scans;
+#endif
 }
 
 // Scan of the tile sums for batches of more than kFusedTiles tiles (one workgroup), with the
@@ -639,10 +645,13 @@ __global__ void rows_finish(const std::uint8_t* base, const std::uint64_t* offse
 // no single-workgroup tile-scan launch sits between the tile scan and the scatter. Workgroup 0
 // publishes counts for the row kernel.
 constexpr std::uint32_t kFusedTiles = 1024;
-// Batches of at most kFusedTiles tiles: the tile scan's last workgroup scans the tile sums and the
-// plain scatter follows (1), or every scatter workgroup sums the tile sums itself (0, A/B builds).
+// Batches of at most kFusedTiles tiles: every scatter workgroup sums the tile sums itself (the
+// product), or the tile scan's last workgroup scans them and the plain scatter follows
+// (TKV_AB_LAST_SCANS=1, A/B builds). The latter measured far slower in one process (300-1000 B gapped
+// 3041 -> 1934 GB/s, cfg4 -2 %, profiles/r4/s14/): the device-scope fence each tile-scan workgroup
+// needs before its ticket writes back its XCD's L2.
 #ifndef TKV_AB_LAST_SCANS
-#define TKV_AB_LAST_SCANS 1
+#define TKV_AB_LAST_SCANS 0
 #endif
 // A 256-thread workgroup per 256 blocks, each re-reading all tile sums. One 1024-thread workgroup per
 // scan tile with 4 blocks per thread (TKV_AB_FINISH_PER=4) cuts those re-reads by 16 but measured

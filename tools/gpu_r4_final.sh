@@ -29,4 +29,11 @@ run trace_cfg4 300 rocprofv3 --kernel-trace --stats -d $O/trace_cfg4 -o run --ou
 for cfg in cfg2 cfg4; do
   run pmc_${cfg}_FETCH_SIZE 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_${cfg}_FETCH_SIZE -o pmc --output-format csv -- $B --config $cfg --steps 5 --warmup 3 --min-warmup-ms 0 || exit 1
 done
+cd $R
+timeout -k 10 400 python -u tools/lane_probe.py tinykvpp_amd/libtkv_crc32.so --rounds 3 --reps 5 > $O/lane_probe.jsonl 2>&1
+rc=$?; echo "lane_probe rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/rec_probe.py tinykvpp_amd/libtkv_crc32.so --rounds 3 --reps 5 > $O/rec_probe.jsonl 2>&1
+rc=$?; echo "rec_probe rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/ab_wal.py tinykvpp_amd/libtkv_crc32.so --rounds 4 > $O/ab_wal.jsonl 2>&1
+rc=$?; echo "ab_wal rc=$rc"; [ $rc -eq 0 ] || exit $rc
 echo done
