@@ -648,8 +648,8 @@ constexpr std::uint32_t kFusedTiles = 1024;
 // Batches of at most kFusedTiles tiles: every scatter workgroup sums the tile sums itself (the
 // product), or the tile scan's last workgroup scans them and the plain scatter follows
 // (TKV_AB_LAST_SCANS=1, A/B builds). The latter measured far slower in one process (300-1000 B gapped
-// 3041 -> 1934 GB/s, cfg4 -2 %, profiles/r4/s14/): the device-scope fence each tile-scan workgroup
-// needs before its ticket writes back its XCD's L2.
+// 3041 -> 1934 GB/s, cfg4 -2 %, profiles/r4/s14/), most likely from the device-scope fence each
+// tile-scan workgroup needs before its ticket (on gfx950 it writes back the XCD's L2).
 #ifndef TKV_AB_LAST_SCANS
 #define TKV_AB_LAST_SCANS 0
 #endif
