@@ -231,7 +231,10 @@ crc_lanes_n(RowsArgs a) {
 #else
 template <int ALIGN, int NG>
 __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
-  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? 5 : 4;
+#ifndef TKV_AB_LANES_DEPTH3  // (A/B builds only: the 3-granule window's depth)
+#define TKV_AB_LANES_DEPTH3 6
+#endif
+  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? TKV_AB_LANES_DEPTH3 : NG == 4 ? 5 : 4;
   __shared__ std::uint32_t lds[kLdsSliceWords];
   dev::crc_lanes_n_body<ALIGN, NG, DEPTH, 1, kPackedPrio>(a, lds);
 }
