@@ -1537,6 +1537,98 @@ __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_
   }
 }
 
+// Uniform lane batches staged through LDS (round 4): a wave's 64 blocks of one step are 64 x stride
+// contiguous bytes, so the wave copies them to its own LDS buffer with coalesced LDS-DMA
+// (global_load_lds_dwordx4: lane l moves bytes [16 l, +16) of each KiB, no VGPRs) one step ahead of
+// the fold, and each lane then reads its block's dwords from LDS (dword-aligned blocks: one ds_read
+// per dword; others: two reads and v_alignbyte). Against crc_lanes_n this drops the per-lane 16-byte
+// granule loads (each wave load touched ~36 lines for 36-byte blocks, three times per step) and the
+// realignment selects. For strides up to kLanesLdsMaxStride (a step's bytes fit a 3 KiB buffer) and
+// default initial registers; the slicing tables are the 64 KiB 16-replica image, which leaves 96 KiB
+// for 16 waves x 2 buffers x 3 KiB.
+constexpr std::uint32_t kLanesLdsBuf = 3072;                              // bytes per step buffer
+constexpr std::uint32_t kLanesLdsMaxStride = (kLanesLdsBuf - 16u) / 64u;  // 47
+template <bool RA, int NW, int PRIO = 0>
+__device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(NW >= 1 && NW <= 16, "a block's dwords (ceil(len / 4) <= NW)");
+  constexpr std::uint32_t kTabWords = kLdsSliceWords / 2;  // the 64 KiB image
+  fill_lds_slicing16(a.tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const LaneConst kc = lane_const16(lane);
+  const std::uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __syncthreads();
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + wid;
+  const std::uint64_t W = a.nwaves, nb = a.nblocks;
+  const std::uint64_t TS = (nb + 63u) / 64u;
+  const std::uint64_t s0 = wave * TS / W;
+  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
+  if (ns == 0) return;
+  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
+  const std::uint64_t stride = a.stride;
+  const std::uint32_t len = a.len;
+  const std::uint32_t nf = len >> 2, tb = len & 3u;  // whole dwords, tail bytes (uniform)
+  // the batch's last byte's granule: no copy reads past it (bytes beyond the last block are never used)
+  const std::uintptr_t glast = (base + (nb - 1u) * stride + (len ? len : 1u) - 1u) & ~static_cast<std::uintptr_t>(15);
+  // this wave's two step buffers, byte offsets in LDS
+  const std::uint32_t buf0 = kTabWords * 4u + wid * 2u * kLanesLdsBuf;
+  auto copy = [&](std::uint32_t j, std::uint32_t buf) {  // step j's bytes into buf (3 DMA instructions)
+    const std::uint64_t b0 = (s0 + j) * 64u;
+    const std::uintptr_t al = (base + b0 * stride) & ~static_cast<std::uintptr_t>(15);
+#pragma unroll
+    for (std::uint32_t i = 0; i < kLanesLdsBuf / 1024u; ++i) {
+      std::uintptr_t g = al + 1024u * i + 16u * lane;
+      g = g < glast ? g : glast;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const __attribute__((address_space(1))) void*>(g),
+                                       reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                           reinterpret_cast<std::uintptr_t>(reinterpret_cast<std::uint8_t*>(lds) + buf + 1024u * i)),
+                                       16, 0, 0);
+    }
+  };
+  auto lds32 = [&](std::uint32_t byte) { return lds_at(lds, byte); };
+  copy(0, buf0);
+  for (std::uint32_t j = 0; j < ns; ++j) {
+    if constexpr (PRIO != 0) set_prio_from_left<PRIO>(ns - j, ns);
+    const std::uint32_t cur = buf0 + (j & 1u) * kLanesLdsBuf;
+    if (j + 1u < ns) {
+      copy(j + 1u, buf0 + ((j + 1u) & 1u) * kLanesLdsBuf);
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // step j's copy has landed; step j+1's stays in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const std::uint64_t b0 = (s0 + j) * 64u;
+    const std::uint32_t o = static_cast<std::uint32_t>((base + b0 * stride) & 15u);
+    const std::uint32_t q = cur + o + lane * static_cast<std::uint32_t>(stride);  // this lane's block in LDS
+    const std::uint32_t qa = q & ~3u, sh = q & 3u;
+    (void)qa;
+    (void)sh;
+    // all NW words first (unconditional reads inside this lane's buffer: the bytes after a block are
+    // don't-care), so one LDS round trip covers them before the lookup chain starts
+    std::uint32_t w[NW];
+    if constexpr (RA) {
+      std::uint32_t r[NW + 1];
+#pragma unroll
+      for (int k = 0; k <= NW; ++k) r[k] = lds32(qa + 4u * k);
+#pragma unroll
+      for (int k = 0; k < NW; ++k) w[k] = __builtin_amdgcn_alignbyte(r[k + 1], r[k], sh);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NW; ++k) w[k] = lds32(q + 4u * k);
+    }
+    Reg p{a.init_default, 0};
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      if (static_cast<std::uint32_t>(k) < nf) {
+        slice4(lds, p, w[k], kc);
+      } else {
+        if (static_cast<std::uint32_t>(k) == nf && tb != 0u) p = Reg{sarwate_bytes(lds, kc, p.value(), w[k], tb), 0};
+        break;
+      }
+    }
+    const std::uint64_t b = b0 + lane;
+    if (b < nb) a.out[b] = p.value() ^ a.out_xor;
+  }
+}
+
 // Steps of data in flight ahead of the fold in the lane phase and the group walks (the ring holds
 // four; A/B builds: -DTKV_AB_WALK_AHEAD=3).
 #ifndef TKV_AB_WALK_AHEAD

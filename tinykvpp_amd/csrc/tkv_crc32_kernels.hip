@@ -240,6 +240,14 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
 }
 #endif
 
+// Uniform lane batches staged through LDS by LDS-DMA (crc_lanes_lds_body): strides up to
+// kLanesLdsMaxStride, default initial registers. RA: blocks not dword-aligned (v_alignbyte reads).
+template <bool RA, int NW>
+__global__ __launch_bounds__(kThreads) void crc_lanes_lds(RowsArgs a) {
+  __shared__ std::uint32_t lds[kLdsSliceWords / 2 + kThreads / 64 * 2 * dev::kLanesLdsBuf / 4];
+  dev::crc_lanes_lds_body<RA, NW, kPackedPrio>(a, lds);
+}
+
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 
 }  // namespace
@@ -1014,6 +1022,9 @@ hipError_t launch_packed_small_gen(const RowsArgs& a, unsigned grid, hipStream_t
 }
 
 // Uniform lane-block batch (a.len <= kLaneMax): ALIGN from the base pointer and the stride.
+#ifndef TKV_AB_LANES_LDS  // (A/B builds: 0 keeps every uniform lane batch on crc_lanes_n)
+#define TKV_AB_LANES_LDS 1
+#endif
 template <int ALIGN, int NG>
 void launch_lanes_shape(RowsArgs a, unsigned ncu, hipStream_t st) {
   using S = LaneShape<NG>;
@@ -1033,6 +1044,26 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   const int align = (m & 15u) == 0 ? 16 : (m & 3u) == 0 ? 4 : 1;
   const std::uint32_t mis = align == 16 ? 0u : align == 4 ? 12u : 15u;  // worst start offset in a granule
   const std::uint32_t ng = std::max<std::uint32_t>(1u, (a.len + mis + 15u) / 16u);  // granules a block can touch
+  // a step's bytes fit one 3 KiB LDS buffer (the last lane's block, its alignment slack and the
+  // realigning read's extra dword included): stage through LDS
+  if (TKV_AB_LANES_LDS && a.init_raw == nullptr && a.stride <= dev::kLanesLdsMaxStride &&
+      15u + 63u * a.stride + a.len + 8u <= dev::kLanesLdsBuf) {
+    const std::uint64_t steps = (static_cast<std::uint64_t>(a.nblocks) + 63u) / 64u;
+    const std::uint64_t waves = kThreads / 64u;
+    const std::uint64_t grid = std::max<std::uint64_t>(1, std::min<std::uint64_t>(ncu, (steps + waves - 1) / waves));
+    RowsArgs b = a;
+    b.nwaves = static_cast<std::uint32_t>(grid * waves);
+    const dim3 g(static_cast<unsigned>(grid)), t(kThreads);
+    const std::uint32_t nw = (a.len + 3u) / 4u;  // words to read (the tail's included)
+#define TKV_LANES_LDS(RA)                                                                    \
+    if (nw <= 4) hipLaunchKernelGGL((crc_lanes_lds<RA, 4>), g, t, 0, st, b);                 \
+    else if (nw <= 8) hipLaunchKernelGGL((crc_lanes_lds<RA, 8>), g, t, 0, st, b);            \
+    else if (nw <= 12) hipLaunchKernelGGL((crc_lanes_lds<RA, 12>), g, t, 0, st, b);          \
+    else hipLaunchKernelGGL((crc_lanes_lds<RA, 16>), g, t, 0, st, b);
+    if (align == 1) { TKV_LANES_LDS(true) } else { TKV_LANES_LDS(false) }
+#undef TKV_LANES_LDS
+    return hipGetLastError();
+  }
 #define TKV_LANES_N(A)                                           \
   switch (ng) {                                                  \
     case 1: launch_lanes_shape<A, 1>(a, ncu, st); break;         \
