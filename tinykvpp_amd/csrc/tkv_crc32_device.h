@@ -1548,9 +1548,10 @@ __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_
 // for 16 waves x 2 buffers x 3 KiB.
 constexpr std::uint32_t kLanesLdsBuf = 3072;                              // bytes per step buffer
 constexpr std::uint32_t kLanesLdsMaxStride = (kLanesLdsBuf - 16u) / 64u;  // 47
-template <bool RA, int NW, int PRIO = 0>
+template <bool RA, int NW, int KB, int PRIO = 0>
 __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(NW >= 1 && NW <= 16, "a block's dwords (ceil(len / 4) <= NW)");
+  static_assert(KB >= 1 && KB <= static_cast<int>(kLanesLdsBuf / 1024u), "KiB copied per step");
   constexpr std::uint32_t kTabWords = kLdsSliceWords / 2;  // the 64 KiB image
   fill_lds_slicing16(a.tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
@@ -1575,7 +1576,7 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
     const std::uint64_t b0 = (s0 + j) * 64u;
     const std::uintptr_t al = (base + b0 * stride) & ~static_cast<std::uintptr_t>(15);
 #pragma unroll
-    for (std::uint32_t i = 0; i < kLanesLdsBuf / 1024u; ++i) {
+    for (std::uint32_t i = 0; i < static_cast<std::uint32_t>(KB); ++i) {  // KB KiB: the step's bytes and slack
       std::uintptr_t g = al + 1024u * i + 16u * lane;
       g = g < glast ? g : glast;
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const __attribute__((address_space(1))) void*>(g),
@@ -1591,7 +1592,10 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
     const std::uint32_t cur = buf0 + (j & 1u) * kLanesLdsBuf;
     if (j + 1u < ns) {
       copy(j + 1u, buf0 + ((j + 1u) & 1u) * kLanesLdsBuf);
-      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // step j's copy has landed; step j+1's stays in flight
+      // step j's copy has landed; step j+1's KB copies stay in flight
+      if constexpr (KB == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else if constexpr (KB == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }

@@ -242,10 +242,10 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
 
 // Uniform lane batches staged through LDS by LDS-DMA (crc_lanes_lds_body): strides up to
 // kLanesLdsMaxStride, default initial registers. RA: blocks not dword-aligned (v_alignbyte reads).
-template <bool RA, int NW>
+template <bool RA, int NW, int KB>
 __global__ __launch_bounds__(kThreads) void crc_lanes_lds(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsSliceWords / 2 + kThreads / 64 * 2 * dev::kLanesLdsBuf / 4];
-  dev::crc_lanes_lds_body<RA, NW, kPackedPrio>(a, lds);
+  dev::crc_lanes_lds_body<RA, NW, KB, kPackedPrio>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
@@ -1055,13 +1055,19 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
     b.nwaves = static_cast<std::uint32_t>(grid * waves);
     const dim3 g(static_cast<unsigned>(grid)), t(kThreads);
     const std::uint32_t nw = (a.len + 3u) / 4u;  // words to read (the tail's included)
+    const std::uint32_t kb = (15u + 63u * a.stride + a.len + 8u + 1023u) / 1024u;  // KiB a step copies
+#define TKV_LANES_LDS_KB(RA, NW)                                                             \
+    if (kb <= 1) hipLaunchKernelGGL((crc_lanes_lds<RA, NW, 1>), g, t, 0, st, b);             \
+    else if (kb == 2) hipLaunchKernelGGL((crc_lanes_lds<RA, NW, 2>), g, t, 0, st, b);        \
+    else hipLaunchKernelGGL((crc_lanes_lds<RA, NW, 3>), g, t, 0, st, b);
 #define TKV_LANES_LDS(RA)                                                                    \
-    if (nw <= 4) hipLaunchKernelGGL((crc_lanes_lds<RA, 4>), g, t, 0, st, b);                 \
-    else if (nw <= 8) hipLaunchKernelGGL((crc_lanes_lds<RA, 8>), g, t, 0, st, b);            \
-    else if (nw <= 12) hipLaunchKernelGGL((crc_lanes_lds<RA, 12>), g, t, 0, st, b);          \
-    else hipLaunchKernelGGL((crc_lanes_lds<RA, 16>), g, t, 0, st, b);
+    if (nw <= 4) { TKV_LANES_LDS_KB(RA, 4) }                                                \
+    else if (nw <= 8) { TKV_LANES_LDS_KB(RA, 8) }                                           \
+    else if (nw <= 12) { TKV_LANES_LDS_KB(RA, 12) }                                         \
+    else { TKV_LANES_LDS_KB(RA, 16) }
     if (align == 1) { TKV_LANES_LDS(true) } else { TKV_LANES_LDS(false) }
 #undef TKV_LANES_LDS
+#undef TKV_LANES_LDS_KB
     return hipGetLastError();
   }
 #define TKV_LANES_N(A)                                           \
