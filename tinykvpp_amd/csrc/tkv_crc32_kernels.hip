@@ -1045,8 +1045,11 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   const std::uint32_t mis = align == 16 ? 0u : align == 4 ? 12u : 15u;  // worst start offset in a granule
   const std::uint32_t ng = std::max<std::uint32_t>(1u, (a.len + mis + 15u) / 16u);  // granules a block can touch
   // a step's bytes fit one 3 KiB LDS buffer (the last lane's block, its alignment slack and the
-  // realigning read's extra dword included): stage through LDS
-  if (TKV_AB_LANES_LDS && a.init_raw == nullptr && a.stride <= dev::kLanesLdsMaxStride &&
+  // realigning read's extra dword included) and the granule path would realign: stage through LDS.
+  // In one process against crc_lanes_n (profiles/r4/lanes_lds/): 33 B +2.3 %, 36 B +0.7 %, 36 B at
+  // base + 3 +5.3 %, 36 B stride 44 +1.3 %; 16-byte aligned blocks (no realignment to save) and blocks
+  // under 28 bytes (a step copies more than it folds) measured slower and keep crc_lanes_n.
+  if (TKV_AB_LANES_LDS && a.init_raw == nullptr && align != 16 && a.len >= 28u && a.stride <= dev::kLanesLdsMaxStride &&
       15u + 63u * a.stride + a.len + 8u <= dev::kLanesLdsBuf) {
     const std::uint64_t steps = (static_cast<std::uint64_t>(a.nblocks) + 63u) / 64u;
     const std::uint64_t waves = kThreads / 64u;
