@@ -44,6 +44,9 @@ constexpr std::uint32_t kRecMeta = 26;  // wal.hpp kMetadataSize: 8-byte header 
 #ifndef TKV_AB_REC16_AHEAD
 #define TKV_AB_REC16_AHEAD 1
 #endif
+#ifndef TKV_AB_REC_LDS  // (A/B builds: 0 keeps narrow windows on wal_rec_lanes)
+#define TKV_AB_REC_LDS 1
+#endif
 template <bool W16>
 struct RecShape {
   static constexpr unsigned kThreads = W16 ? 768 : 1024;
@@ -193,6 +196,169 @@ wal_rec_lanes(RecArgs a, const DeviceTables* tabs) {
   }
 }
 
+// The record check for narrow windows (4-5 granules) staged through LDS (round 4): a WAL image's
+// records lie back to back, so the 64 records of a wave step span about 64 record lengths; the wave
+// copies that span (3 KiB at most, else the step loads its granules as wal_rec_lanes does) into its
+// own LDS buffer with coalesced LDS-DMA one step ahead, the step's offsets too (one 4-byte DMA per
+// lane, two steps ahead, so no ordinary load is pending while the copies fly), and each lane reads
+// its record's window from LDS (two reads per dword and v_alignbyte). Slicing tables: the 64 KiB
+// image; 12 waves x (2 x 3 KiB + 2 x 256 B) of buffers.
+constexpr unsigned kRecLdsThreads = 768;
+constexpr std::uint32_t kRecLdsBuf = 3072;
+__device__ __forceinline__ std::uint32_t wave_min_u32(std::uint32_t v) {
+  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0xB1, 0xF, 0xF, false)));
+  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x4E, 0xF, 0xF, false)));
+  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x141, 0xF, 0xF, false)));
+  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x140, 0xF, 0xF, false)));
+  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x142, 0xA, 0xF, false)));
+  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x143, 0xC, 0xF, false)));
+  return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ std::uint32_t wave_max_u32(std::uint32_t v) {
+  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false)));
+  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false)));
+  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, false)));
+  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, false)));
+  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false)));
+  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false)));
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
+template <int NG>
+__global__ __launch_bounds__(kRecLdsThreads) void wal_rec_lds(RecArgs a, const DeviceTables* tabs) {
+  constexpr int ND = 4 * NG - 4;  // realigned dwords of the window
+  constexpr int NPAY = ND - 3;
+  constexpr std::uint32_t kWaves = kRecLdsThreads / 64;
+  constexpr std::uint32_t kTabBytes = kLdsSliceWords * 2;  // the 64 KiB image
+  __shared__ std::uint32_t lds[(kTabBytes + kWaves * (2 * kRecLdsBuf + 2 * 256)) / 4];
+  dev::fill_lds_slicing16(tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const dev::LaneConst kc = dev::lane_const16(lane);
+  const std::uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __syncthreads();
+  const std::uint32_t wave = blockIdx.x * kWaves + wid;
+  const std::uint64_t W = a.nwaves, n = a.n;
+  const std::uint64_t TS = (n + 63u) / 64u;
+  const std::uint64_t s0 = wave * TS / W;
+  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
+  if (ns == 0) return;
+  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
+  const std::uintptr_t glast = (w0 + a.size - 1u) & ~static_cast<std::uintptr_t>(15);  // the image's last granule
+  auto gran = [&](std::uintptr_t p) { return dev::gload16(p < glast ? p : glast); };
+  std::uint8_t* l8 = reinterpret_cast<std::uint8_t*>(lds);
+  const std::uint32_t data0 = kTabBytes + wid * 2u * kRecLdsBuf;             // byte offsets in LDS
+  const std::uint32_t offs0 = kTabBytes + kWaves * 2u * kRecLdsBuf + wid * 512u;
+  auto lds_ptr = [&](std::uint32_t byte) {
+    return reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<std::uintptr_t>(l8 + byte));
+  };
+  auto copy_offs = [&](std::uint32_t j) {  // step j's 64 offsets into offset buffer j & 1
+    const std::uint64_t b = (s0 + j) * 64u + lane;
+    const std::uint32_t* src = a.off + (b < n ? b : n - 1u);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const __attribute__((address_space(1))) void*>(
+                                         reinterpret_cast<std::uintptr_t>(src)),
+                                     lds_ptr(offs0 + (j & 1u) * 256u), 4, 0, 0);
+  };
+  // per step (uniform): staged in LDS, the lowest offset and its place in the first granule
+  bool st_staged0 = false, st_staged1 = false;  // (two named slots: no dynamically indexed arrays)
+  std::uint32_t st_min0 = 0, st_min1 = 0, st_o0 = 0, st_o1 = 0;
+  auto plan = [&](std::uint32_t j) {  // step j's offsets have landed: copy its span if it fits
+    const std::uint32_t k = j & 1u;
+    const std::uint32_t off = dev::lds_at(lds, offs0 + k * 256u + 4u * lane);
+    const std::uint32_t mn = wave_min_u32(off), mx = wave_max_u32(off);
+    const std::uintptr_t al = (w0 + mn) & ~static_cast<std::uintptr_t>(15);
+    const std::uint32_t o = static_cast<std::uint32_t>(w0 + mn - al);
+    const bool staged = static_cast<std::uint64_t>(mx - mn) + o + 16u * NG <= kRecLdsBuf;
+    if (k) {
+      st_staged1 = staged;
+      st_min1 = mn;
+      st_o1 = o;
+    } else {
+      st_staged0 = staged;
+      st_min0 = mn;
+      st_o0 = o;
+    }
+    if (staged) {
+#pragma unroll
+      for (std::uint32_t i = 0; i < kRecLdsBuf / 1024u; ++i) {
+        std::uintptr_t g = al + 1024u * i + 16u * lane;
+        g = g < glast ? g : glast;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const __attribute__((address_space(1))) void*>(g),
+                                         lds_ptr(data0 + k * kRecLdsBuf + 1024u * i), 16, 0, 0);
+      }
+    }
+  };
+
+  copy_offs(0);
+  if (ns > 1) copy_offs(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  plan(0);
+  for (std::uint32_t j = 0; j < ns; ++j) {
+    dev::set_prio_from_left<3>(ns - j, ns);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step j's span and step j+1's offsets have landed
+    const std::uint32_t k = j & 1u;
+    const std::uint32_t off = dev::lds_at(lds, offs0 + k * 256u + 4u * lane);  // (read before its buffer is reused)
+    const bool staged = k ? st_staged1 : st_staged0;
+    const std::uint32_t mn = k ? st_min1 : st_min0, o = k ? st_o1 : st_o0;
+    if (j + 1u < ns) {
+      plan(j + 1u);
+      if (j + 2u < ns) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the offset read above is done with its buffer)
+        copy_offs(j + 2u);
+      }
+    }
+    const std::uint64_t b = (s0 + j) * 64u + lane;
+    const bool live = b < n;
+    const std::uintptr_t p = w0 + off;
+    std::uint32_t d[ND + 1];
+    if (staged) {
+      const std::uint32_t qb = data0 + k * kRecLdsBuf + o + (off - mn);
+      const std::uint32_t qa = qb & ~3u, sh = qb & 3u;
+      std::uint32_t r[ND + 1];
+#pragma unroll
+      for (int i = 0; i <= ND; ++i) r[i] = dev::lds_at(lds, qa + 4u * i);
+#pragma unroll
+      for (int i = 0; i < ND; ++i) d[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+    } else {
+      uint4 q[NG];
+      const std::uintptr_t al = p & ~static_cast<std::uintptr_t>(15);
+#pragma unroll
+      for (int i = 0; i < NG; ++i) q[i] = gran(al + 16u * i);
+      std::uint32_t e[4 * NG - 4];
+      rec_dwords<NG>(q, static_cast<std::uint32_t>(p & 15u), e);
+#pragma unroll
+      for (int i = 0; i < ND; ++i) d[i] = e[i];
+    }
+    d[ND] = 0u;
+    const std::uint32_t rlen = d[0], stored = d[1];
+    const std::uint32_t klen = __builtin_amdgcn_alignbyte(d[5], d[4], 2u);
+    const std::uint32_t vlen = __builtin_amdgcn_alignbyte(d[6], d[5], 2u);
+    const std::uint64_t left = off < a.size ? a.size - off : 0u;
+    const bool len_ok = left >= kRecMeta && static_cast<std::uint64_t>(rlen) + 8u <= left;  // wal.cpp:68, :80
+    const std::uint32_t L = live && len_ok ? rlen : 0u;
+    std::uint32_t c = rec_fold<NPAY>(lds, kc, d + 2, L < 4u * NPAY ? L : 4u * NPAY, 0xFFFFFFFFu);
+    // payloads longer than the window: 64 bytes at a time from fresh granules, the register carried
+    for (std::uint32_t done = 4u * NPAY; __ballot(L > done) != 0; done += 64u) {
+      const std::uint32_t m = L > done ? std::min(L - done, 64u) : 0u;
+      const std::uintptr_t ps = p + 8u + done;
+      const std::uintptr_t al = ps & ~static_cast<std::uintptr_t>(15);
+      uint4 g[dev::kLaneGran];
+#pragma unroll
+      for (int i = 0; i < dev::kLaneGran; ++i) g[i] = gran(m ? al + 16u * i : glast);
+      std::uint32_t e[16];
+      dev::lane_dwords<1>(g, static_cast<std::uint32_t>(ps & 15u), e);
+      std::uint32_t e17[17];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) e17[i] = e[i];
+      e17[16] = 0u;
+      c = rec_fold<16>(lds, kc, e17, m, c);
+    }
+    const std::uint32_t crc = c ^ 0xFFFFFFFFu;
+    const bool kv_ok = static_cast<std::uint64_t>(klen) + vlen + (kRecMeta - 8u) <= rlen;  // wal.cpp:118-121
+    if (live && a.crc) a.crc[b] = len_ok ? crc : 0u;
+    if (live && (!len_ok || crc != stored || !kv_ok)) atomicMin(a.first_bad, static_cast<unsigned long long>(b));
+  }
+}
+
 int cu_count() {
   static int cached[64] = {};
   int dev = 0;
@@ -214,6 +380,15 @@ void launch_records(RecArgs a, std::uint32_t max_payload, int ncu, const DeviceT
   // three steps of granules in flight, 6 granules two, wider ones one (registers).
   const std::uint32_t ng =
       std::min<std::uint32_t>(8u, std::max<std::uint32_t>(4u, (std::min<std::uint32_t>(max_payload, 1024u) + 26u + 15u) / 16u));
+  if (TKV_AB_REC_LDS && ng <= 5) {  // narrow windows: staged through LDS (wal_rec_lds)
+    constexpr std::uint64_t waves = kRecLdsThreads / 64;
+    const std::uint64_t grid =
+        std::max<std::uint64_t>(1, std::min<std::uint64_t>(static_cast<std::uint64_t>(ncu), (steps + waves - 1) / waves));
+    a.nwaves = static_cast<std::uint32_t>(grid * waves);
+    if (ng == 4) hipLaunchKernelGGL((wal_rec_lds<4>), dim3(static_cast<unsigned>(grid)), dim3(kRecLdsThreads), 0, st, a, tabs);
+    else hipLaunchKernelGGL((wal_rec_lds<5>), dim3(static_cast<unsigned>(grid)), dim3(kRecLdsThreads), 0, st, a, tabs);
+    return;
+  }
   const bool w16 = TKV_AB_REC16 && ng <= 5;
   const std::uint64_t threads = w16 ? RecShape<true>::kThreads : RecShape<false>::kThreads;
   const std::uint64_t per_cu = w16 ? RecShape<true>::kWgPerCu : RecShape<false>::kWgPerCu;
