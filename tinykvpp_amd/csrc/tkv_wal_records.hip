@@ -205,22 +205,24 @@ wal_rec_lanes(RecArgs a, const DeviceTables* tabs) {
 // image; 12 waves x (2 x 3 KiB + 2 x 256 B) of buffers.
 constexpr unsigned kRecLdsThreads = 768;
 constexpr std::uint32_t kRecLdsBuf = 3072;
+__device__ __forceinline__ std::uint32_t umin32(std::uint32_t x, std::uint32_t y) { return x < y ? x : y; }
+__device__ __forceinline__ std::uint32_t umax32(std::uint32_t x, std::uint32_t y) { return x > y ? x : y; }
 __device__ __forceinline__ std::uint32_t wave_min_u32(std::uint32_t v) {
-  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0xB1, 0xF, 0xF, false)));
-  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x4E, 0xF, 0xF, false)));
-  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x141, 0xF, 0xF, false)));
-  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x140, 0xF, 0xF, false)));
-  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x142, 0xA, 0xF, false)));
-  v = min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x143, 0xC, 0xF, false)));
+  v = umin32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0xB1, 0xF, 0xF, false)));
+  v = umin32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x4E, 0xF, 0xF, false)));
+  v = umin32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x141, 0xF, 0xF, false)));
+  v = umin32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x140, 0xF, 0xF, false)));
+  v = umin32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x142, 0xA, 0xF, false)));
+  v = umin32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(~0u, v, 0x143, 0xC, 0xF, false)));
   return __builtin_amdgcn_readlane(v, 63);
 }
 __device__ __forceinline__ std::uint32_t wave_max_u32(std::uint32_t v) {
-  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false)));
-  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false)));
-  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, false)));
-  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, false)));
-  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false)));
-  v = max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false)));
+  v = umax32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false)));
+  v = umax32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false)));
+  v = umax32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, false)));
+  v = umax32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, false)));
+  v = umax32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false)));
+  v = umax32(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false)));
   return __builtin_amdgcn_readlane(v, 63);
 }
 
@@ -248,15 +250,14 @@ __global__ __launch_bounds__(kRecLdsThreads) void wal_rec_lds(RecArgs a, const D
   std::uint8_t* l8 = reinterpret_cast<std::uint8_t*>(lds);
   const std::uint32_t data0 = kTabBytes + wid * 2u * kRecLdsBuf;             // byte offsets in LDS
   const std::uint32_t offs0 = kTabBytes + kWaves * 2u * kRecLdsBuf + wid * 512u;
-  auto lds_ptr = [&](std::uint32_t byte) {
-    return reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<std::uintptr_t>(l8 + byte));
-  };
   auto copy_offs = [&](std::uint32_t j) {  // step j's 64 offsets into offset buffer j & 1
     const std::uint64_t b = (s0 + j) * 64u + lane;
     const std::uint32_t* src = a.off + (b < n ? b : n - 1u);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const __attribute__((address_space(1))) void*>(
                                          reinterpret_cast<std::uintptr_t>(src)),
-                                     lds_ptr(offs0 + (j & 1u) * 256u), 4, 0, 0);
+                                     reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                         reinterpret_cast<std::uintptr_t>(l8 + offs0 + (j & 1u) * 256u)),
+                                     4, 0, 0);
   };
   // per step (uniform): staged in LDS, the lowest offset and its place in the first granule
   bool st_staged0 = false, st_staged1 = false;  // (two named slots: no dynamically indexed arrays)
@@ -283,7 +284,9 @@ __global__ __launch_bounds__(kRecLdsThreads) void wal_rec_lds(RecArgs a, const D
         std::uintptr_t g = al + 1024u * i + 16u * lane;
         g = g < glast ? g : glast;
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const __attribute__((address_space(1))) void*>(g),
-                                         lds_ptr(data0 + k * kRecLdsBuf + 1024u * i), 16, 0, 0);
+                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                             reinterpret_cast<std::uintptr_t>(l8 + data0 + k * kRecLdsBuf + 1024u * i)),
+                                         16, 0, 0);
       }
     }
   };
