@@ -383,7 +383,11 @@ void launch_records(RecArgs a, std::uint32_t max_payload, int ncu, const DeviceT
   // three steps of granules in flight, 6 granules two, wider ones one (registers).
   const std::uint32_t ng =
       std::min<std::uint32_t>(8u, std::max<std::uint32_t>(4u, (std::min<std::uint32_t>(max_payload, 1024u) + 26u + 15u) / 16u));
-  if (TKV_AB_REC_LDS && ng <= 5) {  // narrow windows: staged through LDS (wal_rec_lds)
+  // narrow windows with payloads of at least 32 bytes: staged through LDS (wal_rec_lds). One process
+  // against wal_rec_lanes (profiles/r4/rec_lds/): 44-byte records (36-byte payloads) 2957 -> 3099 GB/s
+  // of payload; 36-byte records (28-byte payloads) 2813 -> 2591, where the per-step cost (span
+  // reduction, copy, full wait) outweighs what the copy saves, so shorter payloads keep wal_rec_lanes.
+  if (TKV_AB_REC_LDS && ng <= 5 && max_payload >= 32u) {
     constexpr std::uint64_t waves = kRecLdsThreads / 64;
     const std::uint64_t grid =
         std::max<std::uint64_t>(1, std::min<std::uint64_t>(static_cast<std::uint64_t>(ncu), (steps + waves - 1) / waves));
