@@ -36,4 +36,6 @@ timeout -k 10 300 python -u tools/rec_probe.py tinykvpp_amd/libtkv_crc32.so --ro
 rc=$?; echo "rec_probe rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u tools/ab_wal.py tinykvpp_amd/libtkv_crc32.so --rounds 4 > $O/ab_wal.jsonl 2>&1
 rc=$?; echo "ab_wal rc=$rc"; [ $rc -eq 0 ] || exit $rc
+cd /tmp
+run pmc_rec_FETCH_SIZE 200 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_rec_FETCH_SIZE -o pmc --output-format csv -- python3 $R/tools/rec_probe.py $R/tinykvpp_amd/libtkv_crc32.so --rounds 1 --reps 2 || exit 1
 echo done
