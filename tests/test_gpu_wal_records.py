@@ -185,3 +185,50 @@ def test_empty_and_tiny(gpu, oracle):
     img, offs, _ = make_wal_small(np.random.default_rng(9), 1)
     assert check(oracle, img, offs, 64) == 1
     assert check(oracle, img[:-1].copy(), offs, 64) == 0  # record_len overruns the truncated image
+
+
+def make_wal_sized(rng, sizes):
+    """Stamped records of the given total sizes (26 + |k| + |v| each)."""
+    import ctypes
+    sizes = np.asarray(sizes, np.uint64)
+    n = sizes.size
+    klen = np.minimum(sizes - 26, rng.integers(0, 12, n).astype(np.uint64))
+    vlen = sizes - 26 - klen
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1])
+    img = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8)
+    hdr = np.zeros((n, 26), np.uint8)
+    hdr[:, 0:4] = (sizes - 8).astype("<u4").view(np.uint8).reshape(-1, 4)
+    hdr[:, 18:22] = klen.astype("<u4").view(np.uint8).reshape(-1, 4)
+    hdr[:, 22:26] = vlen.astype("<u4").view(np.uint8).reshape(-1, 4)
+    img[offs.astype(np.int64)[:, None] + np.arange(26)] = hdr
+    s32 = sizes.astype(np.uint32)
+    tk.check(tk.load_library().tkv_wal_stamp(ctypes.c_void_p(img.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                                             ctypes.c_void_p(s32.ctypes.data), n))
+    return img, offs
+
+
+@pytest.mark.parametrize("layout", ["uniform_44", "mixed_spans", "permuted", "to_the_end"])
+@pytest.mark.parametrize("shift", [0, 3, 8, 13])
+def test_lds_staged_windows(gpu, oracle, layout, shift):
+    """Windows of 4-5 granules with payloads of at least 32 bytes are staged through LDS a step at a
+    time: 44-byte records (every step staged); steps holding a long record next to
+    staged ones (its span over 3 KiB: that step loads granules); offsets out of order (spans over 3 KiB
+    everywhere); the last records ending on the image's last byte. Payload flips in staged steps must
+    report the first bad record."""
+    rng = np.random.default_rng(len(layout) * 31 + shift)
+    n = 20_000
+    sizes = np.full(n, 44, np.uint64)
+    if layout == "mixed_spans":
+        sizes[rng.integers(0, n, 60)] = rng.integers(1500, 5000, 60).astype(np.uint64)
+        sizes[rng.integers(0, n, 2000)] = rng.integers(40, 81, 2000).astype(np.uint64)
+    img, offs = make_wal_sized(rng, sizes)
+    if layout == "permuted":
+        offs = offs[rng.permutation(n)]
+    for mp in (36, 54):
+        assert check(oracle, img, offs, mp, shift) == n
+    if layout != "permuted":
+        o = offs.astype(np.int64)
+        for i in sorted(rng.integers(70, n - 70, 3), reverse=True):  # latest first: each becomes the first bad
+            img[o[i] + 8 + int(rng.integers(0, 36))] ^= 0x10
+            assert check(oracle, img, offs, 36, shift) == i
