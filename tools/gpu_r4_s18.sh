@@ -1,0 +1,7 @@
+set -u
+# Round-4 step 18: the whole GPU suite on the tree (new LDS-staged record-check tests included).
+O=$GRAFT_REPO_ROOT/gpurun_out/r4_s18
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+timeout -k 10 500 python -u -m pytest tests -m gpu -q --maxfail=30 --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest.log; grep -E "^FAILED|^ERROR" $O/pytest.log | head -30; exit $rc
