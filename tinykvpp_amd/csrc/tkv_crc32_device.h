@@ -1451,6 +1451,81 @@ __device__ __forceinline__ void lane_dwords_n(const uint4 (&g)[NG], std::uint32_
   }
 }
 
+// Right-aligned lane walk for the default initial register, the length's whole-dword count NF a
+// compile-time constant: each lane's window is the NF dwords that END at its block's end, starting
+// lead = 4 NF - len bytes in front of the block. Those lead bytes (whatever lies there) are masked to
+// zero in the first dword, and the NF dwords are folded from register 0, which leading zeros leave at
+// 0; so every lane folds the same whole dwords, with no Sarwate tail for the last 1-3 bytes and no
+// per-dword branch, and the initial register enters as one uniform term Shift_len(init) =
+// head_z * init (head_z = x^(8 len)). ALIGN is the window start's alignment class (the block's when
+// lead = 0, bytes otherwise); a window granule wholly in front of the block's own first granule reads
+// the zero buffer, so no load leaves the block's granules.
+template <int ALIGN, int NF, int NG, int DEPTH, int PRIO = 0>
+__device__ __forceinline__ void crc_lanes_r_body(const RowsArgs& a, std::uint32_t* lds) {
+  static_assert(NF >= 1 && NF <= 16 && 4 * NF + (ALIGN == 16 ? 0 : ALIGN == 4 ? 12 : 15) <= 16 * NG,
+                "the window's NG granules must cover NF dwords at the worst start offset");
+  fill_lds_slicing(a.tabs, lds);
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const LaneConst kc = lane_const(lane);
+  const std::uint32_t K = multmodp(a.head_z, a.init_default, a.tabs->poly) ^ a.out_xor;
+  __syncthreads();
+  const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint64_t W = a.nwaves, nb = a.nblocks;
+  const std::uint64_t TS = (nb + 63u) / 64u;
+  const std::uint64_t s0 = wave * TS / W;
+  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
+  if (ns == 0) return;
+  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
+  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
+  const std::uint32_t len = a.len;                 // 4 NF - 3 .. 4 NF
+  const std::uint32_t lead = 4u * NF - len;        // bytes in front of the block in the first dword
+  const std::uint32_t m0 = ~0u << (8u * lead);     // (lead <= 3)
+  const std::uint64_t blk0 = s0 * 64u + lane;
+  const std::uintptr_t lane_base = base + blk0 * a.stride;
+  const std::uint64_t step_bytes = 64u * a.stride;
+  const std::uintptr_t last_blk = base + (nb - 1u) * a.stride;  // lanes past the batch reload it, store nothing
+
+  uint4 buf[DEPTH][NG];
+  std::uint32_t o16[DEPTH];
+  auto issue = [&](std::uint32_t j, int slot) {
+    const std::uint32_t jc = j < ns ? j : ns - 1;  // steps past the range reload the last one
+    const std::uint64_t b = blk0 + 64ull * jc;
+    const std::uintptr_t blk = b < nb ? lane_base + jc * step_bytes : last_blk;
+    const std::uintptr_t s = blk - lead;
+    const std::uintptr_t al = s & ~static_cast<std::uintptr_t>(15);
+    const std::uintptr_t first = blk & ~static_cast<std::uintptr_t>(15);
+    const std::uintptr_t last = (blk + len - 1u) & ~static_cast<std::uintptr_t>(15);
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const std::uintptr_t p = al + 16u * i;
+      buf[slot][i] = gload16(p < first ? dmy : (p < last ? p : last));
+    }
+    o16[slot] = static_cast<std::uint32_t>(s & 15u);
+  };
+  auto fold = [&](int q, std::uint32_t j) {
+    std::uint32_t d[4 * NG];
+    lane_dwords_n<ALIGN, NG>(buf[q], o16[q], d);
+    Reg p{0u, 0u};
+    slice4(lds, p, d[0] & m0, kc);
+#pragma unroll
+    for (int k = 1; k < NF; ++k) slice4(lds, p, d[k], kc);
+    const std::uint64_t b = blk0 + 64ull * j;
+    if (b < nb) a.out[b] = p.value() ^ K;
+  };
+
+#pragma unroll
+  for (int s = 0; s < DEPTH - 1; ++s) issue(s, s);
+  for (std::uint32_t j = 0; j < ns; j += DEPTH) {
+    if constexpr (PRIO != 0) set_prio_from_left<PRIO>(ns - j, ns);
+#pragma unroll
+    for (int q = 0; q < DEPTH; ++q) {
+      issue(j + q + DEPTH - 1, (q + DEPTH - 1) % DEPTH);
+      if (j + q >= ns) break;
+      fold(q, j + q);
+    }
+  }
+}
+
 template <int ALIGN, int NG, int DEPTH, int ILP, int PRIO = 0, int R = 32>
 __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");

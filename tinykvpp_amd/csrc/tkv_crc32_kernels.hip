@@ -240,6 +240,17 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
 }
 #endif
 
+// Uniform lane batches with the default initial register, right-aligned windows of NF whole dwords
+// (crc_lanes_r_body); ALIGN is the window start's alignment class.
+template <int ALIGN, int NF>
+__global__ __launch_bounds__(kThreads) void crc_lanes_r(RowsArgs a) {
+  constexpr int kMis = ALIGN == 16 ? 0 : ALIGN == 4 ? 12 : 15;
+  constexpr int NG = (4 * NF + kMis + 15) / 16;
+  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? 5 : 4;
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  dev::crc_lanes_r_body<ALIGN, NF, NG, DEPTH, kPackedPrio>(a, lds);
+}
+
 // Uniform lane batches staged through LDS by LDS-DMA (crc_lanes_lds_body): strides up to
 // kLanesLdsMaxStride, default initial registers. RA: blocks not dword-aligned (v_alignbyte reads).
 template <bool RA, int NW, int KB>
@@ -1036,12 +1047,43 @@ void launch_lanes_shape(RowsArgs a, unsigned ncu, hipStream_t st) {
   hipLaunchKernelGGL((crc_lanes_n<ALIGN, NG>), dim3(static_cast<unsigned>(grid)), dim3(S::kThreads), 0, st, a);
 }
 
+#ifndef TKV_AB_LANES_R  // (A/B builds: 0 off, 1 right-aligned windows where crc_lanes_n would run, 2 also
+#define TKV_AB_LANES_R 1  // before the LDS-staged kernel)
+#endif
+template <int ALIGN, int NF>
+void launch_lanes_r_nf(RowsArgs a, unsigned ncu, hipStream_t st) {
+  const std::uint64_t steps = (static_cast<std::uint64_t>(a.nblocks) + 63u) / 64u;
+  const std::uint64_t waves = kThreads / 64u;
+  const std::uint64_t grid = std::max<std::uint64_t>(1, std::min<std::uint64_t>(ncu, (steps + waves - 1) / waves));
+  a.nwaves = static_cast<std::uint32_t>(grid * waves);
+  hipLaunchKernelGGL((crc_lanes_r<ALIGN, NF>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, st, a);
+}
+template <int ALIGN, int NF = 1>
+void launch_lanes_r(const RowsArgs& a, std::uint32_t nf, unsigned ncu, hipStream_t st) {
+  if constexpr (NF < 16) {
+    if (nf != NF) {
+      launch_lanes_r<ALIGN, NF + 1>(a, nf, ncu, st);
+      return;
+    }
+  }
+  launch_lanes_r_nf<ALIGN, NF>(a, ncu, st);
+}
+
 // Uniform lane-block batch (a.len <= kLaneMax): ALIGN from the base pointer and the stride, the window
 // (NG granules) from the length; grid and waves from the window's LaneShape.
 hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   if (a.len > kLaneMax) return hipErrorInvalidValue;
   const std::uintptr_t m = reinterpret_cast<std::uintptr_t>(a.base) | static_cast<std::uintptr_t>(a.stride);
   const int align = (m & 15u) == 0 ? 16 : (m & 3u) == 0 ? 4 : 1;
+  const bool lanes_r = TKV_AB_LANES_R != 0 && a.init_raw == nullptr && a.len >= 1u;
+  const std::uint32_t nf = (a.len + 3u) / 4u, lead = 4u * nf - a.len;
+  const int ralign = lead != 0u ? 1 : align;  // the window start's class
+  if (lanes_r && TKV_AB_LANES_R == 2) {
+    if (ralign == 16) launch_lanes_r<16>(a, nf, ncu, st);
+    else if (ralign == 4) launch_lanes_r<4>(a, nf, ncu, st);
+    else launch_lanes_r<1>(a, nf, ncu, st);
+    return hipGetLastError();
+  }
   const std::uint32_t mis = align == 16 ? 0u : align == 4 ? 12u : 15u;  // worst start offset in a granule
   const std::uint32_t ng = std::max<std::uint32_t>(1u, (a.len + mis + 15u) / 16u);  // granules a block can touch
   // a step's bytes fit one 3 KiB LDS buffer (the last lane's block, its alignment slack and the
@@ -1071,6 +1113,12 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
     if (align == 1) { TKV_LANES_LDS(true) } else { TKV_LANES_LDS(false) }
 #undef TKV_LANES_LDS
 #undef TKV_LANES_LDS_KB
+    return hipGetLastError();
+  }
+  if (lanes_r) {
+    if (ralign == 16) launch_lanes_r<16>(a, nf, ncu, st);
+    else if (ralign == 4) launch_lanes_r<4>(a, nf, ncu, st);
+    else launch_lanes_r<1>(a, nf, ncu, st);
     return hipGetLastError();
   }
 #define TKV_LANES_N(A)                                           \
