@@ -253,10 +253,11 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_r(RowsArgs a) {
 
 // Uniform lane batches staged through LDS by LDS-DMA (crc_lanes_lds_body): strides up to
 // kLanesLdsMaxStride, default initial registers. RA: blocks not dword-aligned (v_alignbyte reads).
-template <bool RA, int NW, int KB>
+// NF > 0: right-aligned windows of NF = NW dwords (crc_lanes_r_body's arithmetic).
+template <bool RA, int NW, int KB, int NF = 0>
 __global__ __launch_bounds__(kThreads) void crc_lanes_lds(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsSliceWords / 2 + kThreads / 64 * 2 * dev::kLanesLdsBuf / 4];
-  dev::crc_lanes_lds_body<RA, NW, KB, kPackedPrio>(a, lds);
+  dev::crc_lanes_lds_body<RA, NW, KB, kPackedPrio, NF>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
@@ -1050,6 +1051,9 @@ void launch_lanes_shape(RowsArgs a, unsigned ncu, hipStream_t st) {
 #ifndef TKV_AB_LANES_R  // (A/B builds: 0 off, 1 right-aligned windows where crc_lanes_n would run, 2 also
 #define TKV_AB_LANES_R 1  // before the LDS-staged kernel)
 #endif
+#ifndef TKV_AB_LANES_LDS_R  // (A/B builds: 1 = the LDS-staged kernel with right-aligned windows)
+#define TKV_AB_LANES_LDS_R 0
+#endif
 template <int ALIGN, int NF>
 void launch_lanes_r_nf(RowsArgs a, unsigned ncu, hipStream_t st) {
   const std::uint64_t steps = (static_cast<std::uint64_t>(a.nblocks) + 63u) / 64u;
@@ -1101,6 +1105,26 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
     const dim3 g(static_cast<unsigned>(grid)), t(kThreads);
     const std::uint32_t nw = (a.len + 3u) / 4u;  // words to read (the tail's included)
     const std::uint32_t kb = (15u + 63u * a.stride + a.len + 8u + 1023u) / 1024u;  // KiB a step copies
+    if (TKV_AB_LANES_LDS_R && nw >= 7u && nw <= 12u && kb >= 2u) {
+      // right-aligned windows: the window start's class decides the realigning reads
+      const bool ra = align == 1 || lead != 0u;
+#define TKV_LANES_LDS_R(RA, NF)                                                               \
+      if (kb == 2) hipLaunchKernelGGL((crc_lanes_lds<RA, NF, 2, NF>), g, t, 0, st, b);        \
+      else hipLaunchKernelGGL((crc_lanes_lds<RA, NF, 3, NF>), g, t, 0, st, b);
+#define TKV_LANES_LDS_R_NF(RA)                                                                \
+      switch (nw) {                                                                           \
+        case 7: TKV_LANES_LDS_R(RA, 7) break;                                                 \
+        case 8: TKV_LANES_LDS_R(RA, 8) break;                                                 \
+        case 9: TKV_LANES_LDS_R(RA, 9) break;                                                 \
+        case 10: TKV_LANES_LDS_R(RA, 10) break;                                               \
+        case 11: TKV_LANES_LDS_R(RA, 11) break;                                               \
+        default: TKV_LANES_LDS_R(RA, 12) break;                                               \
+      }
+      if (ra) { TKV_LANES_LDS_R_NF(true) } else { TKV_LANES_LDS_R_NF(false) }
+#undef TKV_LANES_LDS_R_NF
+#undef TKV_LANES_LDS_R
+      return hipGetLastError();
+    }
 #define TKV_LANES_LDS_KB(RA, NW)                                                             \
     if (kb <= 1) hipLaunchKernelGGL((crc_lanes_lds<RA, NW, 1>), g, t, 0, st, b);             \
     else if (kb == 2) hipLaunchKernelGGL((crc_lanes_lds<RA, NW, 2>), g, t, 0, st, b);        \
