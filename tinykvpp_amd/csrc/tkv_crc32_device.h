@@ -1624,13 +1624,9 @@ __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_
 // for 16 waves x 2 buffers x 3 KiB.
 constexpr std::uint32_t kLanesLdsBuf = 3072;                              // bytes per step buffer
 constexpr std::uint32_t kLanesLdsMaxStride = (kLanesLdsBuf - 16u) / 64u;  // 47
-// NF > 0: right-aligned as crc_lanes_r_body (NW = NF whole dwords ending at the block end, the lead
-// bytes in front masked, folded from register 0, the init term Shift_len(init) added at the end; RA
-// then says whether the window start, not the block, is dword-aligned).
-template <bool RA, int NW, int KB, int PRIO = 0, int NF = 0>
+template <bool RA, int NW, int KB, int PRIO = 0>
 __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(NW >= 1 && NW <= 16, "a block's dwords (ceil(len / 4) <= NW)");
-  static_assert(NF == 0 || NF == NW, "right-aligned windows read exactly NF dwords");
   static_assert(KB >= 1 && KB <= static_cast<int>(kLanesLdsBuf / 1024u), "KiB copied per step");
   constexpr std::uint32_t kTabWords = kLdsSliceWords / 2;  // the 64 KiB image
   fill_lds_slicing16(a.tabs, lds);
@@ -1648,9 +1644,6 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
   const std::uint64_t stride = a.stride;
   const std::uint32_t len = a.len;
   const std::uint32_t nf = len >> 2, tb = len & 3u;  // whole dwords, tail bytes (uniform)
-  const std::uint32_t lead = 4u * NF - len;          // (NF > 0) bytes in front of the block, masked
-  const std::uint32_t m0 = NF > 0 ? ~0u << (8u * lead) : ~0u;
-  const std::uint32_t K = NF > 0 ? multmodp(a.head_z, a.init_default, a.tabs->poly) ^ a.out_xor : 0u;
   // the batch's last byte's granule: no copy reads past it (bytes beyond the last block are never used)
   const std::uintptr_t glast = (base + (nb - 1u) * stride + (len ? len : 1u) - 1u) & ~static_cast<std::uintptr_t>(15);
   // this wave's two step buffers, byte offsets in LDS
@@ -1684,8 +1677,7 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
     }
     const std::uint64_t b0 = (s0 + j) * 64u;
     const std::uint32_t o = static_cast<std::uint32_t>((base + b0 * stride) & 15u);
-    // this lane's block in LDS; right-aligned (NF > 0): the NF dwords ending at the block's end
-    const std::uint32_t q = cur + o + lane * static_cast<std::uint32_t>(stride) - (NF > 0 ? lead : 0u);
+    const std::uint32_t q = cur + o + lane * static_cast<std::uint32_t>(stride);  // this lane's block in LDS
     const std::uint32_t qa = q & ~3u, sh = q & 3u;
     (void)qa;
     (void)sh;
@@ -1702,27 +1694,18 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
 #pragma unroll
       for (int k = 0; k < NW; ++k) w[k] = lds32(q + 4u * k);
     }
-    if constexpr (NF > 0) {
-      Reg p{0u, 0u};
-      slice4(lds, p, w[0] & m0, kc);
+    Reg p{a.init_default, 0};
 #pragma unroll
-      for (int k = 1; k < NF; ++k) slice4(lds, p, w[k], kc);
-      const std::uint64_t b = b0 + lane;
-      if (b < nb) a.out[b] = p.value() ^ K;
-    } else {
-      Reg p{a.init_default, 0};
-#pragma unroll
-      for (int k = 0; k < NW; ++k) {
-        if (static_cast<std::uint32_t>(k) < nf) {
-          slice4(lds, p, w[k], kc);
-        } else {
-          if (static_cast<std::uint32_t>(k) == nf && tb != 0u) p = Reg{sarwate_bytes(lds, kc, p.value(), w[k], tb), 0};
-          break;
-        }
+    for (int k = 0; k < NW; ++k) {
+      if (static_cast<std::uint32_t>(k) < nf) {
+        slice4(lds, p, w[k], kc);
+      } else {
+        if (static_cast<std::uint32_t>(k) == nf && tb != 0u) p = Reg{sarwate_bytes(lds, kc, p.value(), w[k], tb), 0};
+        break;
       }
-      const std::uint64_t b = b0 + lane;
-      if (b < nb) a.out[b] = p.value() ^ a.out_xor;
     }
+    const std::uint64_t b = b0 + lane;
+    if (b < nb) a.out[b] = p.value() ^ a.out_xor;
   }
 }
 

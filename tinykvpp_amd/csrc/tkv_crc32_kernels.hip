@@ -253,11 +253,10 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_r(RowsArgs a) {
 
 // Uniform lane batches staged through LDS by LDS-DMA (crc_lanes_lds_body): strides up to
 // kLanesLdsMaxStride, default initial registers. RA: blocks not dword-aligned (v_alignbyte reads).
-// NF > 0: right-aligned windows of NF = NW dwords (crc_lanes_r_body's arithmetic).
-template <bool RA, int NW, int KB, int NF = 0>
+template <bool RA, int NW, int KB>
 __global__ __launch_bounds__(kThreads) void crc_lanes_lds(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsSliceWords / 2 + kThreads / 64 * 2 * dev::kLanesLdsBuf / 4];
-  dev::crc_lanes_lds_body<RA, NW, KB, kPackedPrio, NF>(a, lds);
+  dev::crc_lanes_lds_body<RA, NW, KB, kPackedPrio>(a, lds);
 }
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
@@ -1048,11 +1047,8 @@ void launch_lanes_shape(RowsArgs a, unsigned ncu, hipStream_t st) {
   hipLaunchKernelGGL((crc_lanes_n<ALIGN, NG>), dim3(static_cast<unsigned>(grid)), dim3(S::kThreads), 0, st, a);
 }
 
-#ifndef TKV_AB_LANES_R  // (A/B builds: 0 off, 1 right-aligned windows where crc_lanes_n would run, 2 also
-#define TKV_AB_LANES_R 1  // before the LDS-staged kernel)
-#endif
-#ifndef TKV_AB_LANES_LDS_R  // (A/B builds: 1 = the LDS-staged kernel with right-aligned windows)
-#define TKV_AB_LANES_LDS_R 0
+#ifndef TKV_AB_LANES_R  // (A/B builds: 0 keeps lengths that are not whole dwords on crc_lanes_n)
+#define TKV_AB_LANES_R 1
 #endif
 template <int ALIGN, int NF>
 void launch_lanes_r_nf(RowsArgs a, unsigned ncu, hipStream_t st) {
@@ -1079,17 +1075,12 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   if (a.len > kLaneMax) return hipErrorInvalidValue;
   const std::uintptr_t m = reinterpret_cast<std::uintptr_t>(a.base) | static_cast<std::uintptr_t>(a.stride);
   const int align = (m & 15u) == 0 ? 16 : (m & 3u) == 0 ? 4 : 1;
-  const bool lanes_r = TKV_AB_LANES_R != 0 && a.init_raw == nullptr && a.len >= 1u;
+  // lengths that are not whole dwords, default register: right-aligned windows (crc_lanes_r_body, whose
+  // window start is then never dword-aligned). In one process against crc_lanes_n
+  // (profiles/r4/lanes_r/): 59 B +8.6 %, 59 B at stride 67 +5.2 %, 26 B +0.1 %; lengths of whole
+  // dwords (no Sarwate tail to save) measured 3 % slower at 16 and 48 B and keep crc_lanes_n.
   const std::uint32_t nf = (a.len + 3u) / 4u, lead = 4u * nf - a.len;
-  const int ralign = lead != 0u ? 1 : align;  // the window start's class
-  if (lanes_r && TKV_AB_LANES_R == 2) {
-    if (ralign == 16) launch_lanes_r<16>(a, nf, ncu, st);
-    else if (ralign == 4) launch_lanes_r<4>(a, nf, ncu, st);
-    else launch_lanes_r<1>(a, nf, ncu, st);
-    return hipGetLastError();
-  }
-  const std::uint32_t mis = align == 16 ? 0u : align == 4 ? 12u : 15u;  // worst start offset in a granule
-  const std::uint32_t ng = std::max<std::uint32_t>(1u, (a.len + mis + 15u) / 16u);  // granules a block can touch
+  const bool lanes_r = TKV_AB_LANES_R != 0 && a.init_raw == nullptr && lead != 0u;
   // a step's bytes fit one 3 KiB LDS buffer (the last lane's block, its alignment slack and the
   // realigning read's extra dword included) and the granule path would realign: stage through LDS.
   // In one process against crc_lanes_n (profiles/r4/lanes_lds/): 33 B +2.3 %, 36 B +0.7 %, 36 B at
@@ -1105,26 +1096,6 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
     const dim3 g(static_cast<unsigned>(grid)), t(kThreads);
     const std::uint32_t nw = (a.len + 3u) / 4u;  // words to read (the tail's included)
     const std::uint32_t kb = (15u + 63u * a.stride + a.len + 8u + 1023u) / 1024u;  // KiB a step copies
-    if (TKV_AB_LANES_LDS_R && nw >= 7u && nw <= 12u && kb >= 2u) {
-      // right-aligned windows: the window start's class decides the realigning reads
-      const bool ra = align == 1 || lead != 0u;
-#define TKV_LANES_LDS_R(RA, NF)                                                               \
-      if (kb == 2) hipLaunchKernelGGL((crc_lanes_lds<RA, NF, 2, NF>), g, t, 0, st, b);        \
-      else hipLaunchKernelGGL((crc_lanes_lds<RA, NF, 3, NF>), g, t, 0, st, b);
-#define TKV_LANES_LDS_R_NF(RA)                                                                \
-      switch (nw) {                                                                           \
-        case 7: TKV_LANES_LDS_R(RA, 7) break;                                                 \
-        case 8: TKV_LANES_LDS_R(RA, 8) break;                                                 \
-        case 9: TKV_LANES_LDS_R(RA, 9) break;                                                 \
-        case 10: TKV_LANES_LDS_R(RA, 10) break;                                               \
-        case 11: TKV_LANES_LDS_R(RA, 11) break;                                               \
-        default: TKV_LANES_LDS_R(RA, 12) break;                                               \
-      }
-      if (ra) { TKV_LANES_LDS_R_NF(true) } else { TKV_LANES_LDS_R_NF(false) }
-#undef TKV_LANES_LDS_R_NF
-#undef TKV_LANES_LDS_R
-      return hipGetLastError();
-    }
 #define TKV_LANES_LDS_KB(RA, NW)                                                             \
     if (kb <= 1) hipLaunchKernelGGL((crc_lanes_lds<RA, NW, 1>), g, t, 0, st, b);             \
     else if (kb == 2) hipLaunchKernelGGL((crc_lanes_lds<RA, NW, 2>), g, t, 0, st, b);        \
@@ -1140,9 +1111,7 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
     return hipGetLastError();
   }
   if (lanes_r) {
-    if (ralign == 16) launch_lanes_r<16>(a, nf, ncu, st);
-    else if (ralign == 4) launch_lanes_r<4>(a, nf, ncu, st);
-    else launch_lanes_r<1>(a, nf, ncu, st);
+    launch_lanes_r<1>(a, nf, ncu, st);
     return hipGetLastError();
   }
 #define TKV_LANES_N(A)                                           \

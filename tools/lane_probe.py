@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--gib", type=float, default=1.0)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--lens", default=None, help="comma-separated uniform lengths instead of the default list")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     libs = [load(p) for p in args.libs]
@@ -69,7 +70,7 @@ def main():
         return total // pitch
 
     work = []
-    for L in (16, 26, 28, 32, 33, 36, 48, 59, 64):
+    for L in ([int(x) for x in args.lens.split(",")] if args.lens else (16, 26, 28, 32, 33, 36, 48, 59, 64)):
         work.append(uniform(L))
     for L in (100, 200, 300, 500, 1000, 1500, 2000):  # 65 B - 2 KiB, not multiples of 16 (crc_packed_small_gen)
         work.append(uniform(L))
