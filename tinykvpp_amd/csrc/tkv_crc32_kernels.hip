@@ -1081,6 +1081,8 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   // dwords (no Sarwate tail to save) measured 3 % slower at 16 and 48 B and keep crc_lanes_n.
   const std::uint32_t nf = (a.len + 3u) / 4u, lead = 4u * nf - a.len;
   const bool lanes_r = TKV_AB_LANES_R != 0 && a.init_raw == nullptr && lead != 0u;
+  const std::uint32_t mis = align == 16 ? 0u : align == 4 ? 12u : 15u;  // worst start offset in a granule
+  const std::uint32_t ng = std::max<std::uint32_t>(1u, (a.len + mis + 15u) / 16u);  // granules a block can touch
   // a step's bytes fit one 3 KiB LDS buffer (the last lane's block, its alignment slack and the
   // realigning read's extra dword included) and the granule path would realign: stage through LDS.
   // In one process against crc_lanes_n (profiles/r4/lanes_lds/): 33 B +2.3 %, 36 B +0.7 %, 36 B at
