@@ -26,6 +26,15 @@ __device__ __forceinline__ uint4 gload16(std::uintptr_t p) {
   const v4u v = *reinterpret_cast<g_v4u*>(p);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// Keeps every dword of a loaded window live up to this point (call it where the window is folded). A
+// window dword that no fold reads is dead as soon as its load is issued, and the compiler then reuses
+// its register while the load is in flight, which costs a vmcnt(0) wait in front of every step and so
+// drains the whole load pipeline.
+template <int N>
+__device__ __forceinline__ void keep_live(const uint4 (&g)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" ::"v"(g[i].x), "v"(g[i].y), "v"(g[i].z), "v"(g[i].w));
+}
 __device__ __forceinline__ std::uint32_t sload32(const std::uint32_t* p, std::uint32_t i) {
   return reinterpret_cast<c_u32*>(reinterpret_cast<std::uintptr_t>(p))[i];
 }
@@ -1504,14 +1513,19 @@ __device__ __forceinline__ void crc_lanes_r_body(const RowsArgs& a, std::uint32_
     o16[slot] = static_cast<std::uint32_t>(s & 15u);
   };
   auto fold = [&](int q, std::uint32_t j) {
+    keep_live(buf[q]);
     std::uint32_t d[4 * NG];
     lane_dwords_n<ALIGN, NG>(buf[q], o16[q], d);
     Reg p{0u, 0u};
     slice4(lds, p, d[0] & m0, kc);
 #pragma unroll
     for (int k = 1; k < NF; ++k) slice4(lds, p, d[k], kc);
+    std::uint32_t v = p.value() ^ K;
+    // computed by every lane: sunk into the store's divergent branch, the fold made the compiler
+    // drain every load in flight (vmcnt(0)) in front of it
+    asm volatile("" : "+v"(v));
     const std::uint64_t b = blk0 + 64ull * j;
-    if (b < nb) a.out[b] = p.value() ^ K;
+    if (b < nb) a.out[b] = v;
   };
 
 #pragma unroll

@@ -1080,7 +1080,16 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   // (profiles/r4/lanes_r/): 59 B +8.6 %, 59 B at stride 67 +5.2 %, 26 B +0.1 %; lengths of whole
   // dwords (no Sarwate tail to save) measured 3 % slower at 16 and 48 B and keep crc_lanes_n.
   const std::uint32_t nf = (a.len + 3u) / 4u, lead = 4u * nf - a.len;
-  const bool lanes_r = TKV_AB_LANES_R != 0 && a.init_raw == nullptr && lead != 0u;
+  const bool lanes_r = TKV_AB_LANES_R != 0 && a.init_raw == nullptr && (lead != 0u || TKV_AB_LANES_R == 2);
+#if TKV_AB_LANES_R == 2  // (A/B builds: every length, ahead of the LDS-staged kernel too)
+  if (lanes_r) {
+    const int ralign = lead != 0u ? 1 : align;
+    if (ralign == 16) launch_lanes_r<16>(a, nf, ncu, st);
+    else if (ralign == 4) launch_lanes_r<4>(a, nf, ncu, st);
+    else launch_lanes_r<1>(a, nf, ncu, st);
+    return hipGetLastError();
+  }
+#endif
   const std::uint32_t mis = align == 16 ? 0u : align == 4 ? 12u : 15u;  // worst start offset in a granule
   const std::uint32_t ng = std::max<std::uint32_t>(1u, (a.len + mis + 15u) / 16u);  // granules a block can touch
   // a step's bytes fit one 3 KiB LDS buffer (the last lane's block, its alignment slack and the
