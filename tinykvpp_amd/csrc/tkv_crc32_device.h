@@ -1231,10 +1231,14 @@ __device__ __forceinline__ void crc_packed_small_gen_body(const RowsArgs& a, std
   }
 
   uint4 buf[DEPTH][kLaneGran];
-  std::uint32_t o16[DEPTH];
+  std::uint32_t o16[DEPTH], ini[INIT ? DEPTH : 1];
   auto issue = [&](std::uint32_t j, int slot) {
     const std::uint32_t jc = j < nrows ? j : nrows - 1;  // rows past the range reload the last one
     const bool live = static_cast<std::uint64_t>(r0 + jc) * kBpr + lane_blk < a.nblocks;
+    if constexpr (INIT) {  // with the granules: a load issued at the fold would drain them all (vmcnt(0))
+      const std::uint64_t blk = static_cast<std::uint64_t>(r0 + jc) * kBpr + lane_blk;
+      ini[slot] = a.init_raw[blk < a.nblocks ? blk : a.nblocks - 1u];
+    }
     const std::uintptr_t blo = blk_base + static_cast<std::uint64_t>(jc) * row_stride, bhi = blo + L;
     const std::uintptr_t p = static_cast<std::uintptr_t>(static_cast<std::int64_t>(blo) + c_lane);
     const std::uintptr_t al = p & ~static_cast<std::uintptr_t>(15);
@@ -1247,11 +1251,10 @@ __device__ __forceinline__ void crc_packed_small_gen_body(const RowsArgs& a, std
   };
   std::uint32_t keep = 0;
   const std::uint32_t keep_src = ((lane % kBpr) * G + (G - 1u)) * 4u;  // byte address for ds_bpermute
-  auto finish = [&](std::uint32_t j, std::uint32_t p) {
+  auto finish = [&](std::uint32_t j, std::uint32_t p, int bslot) {
     std::uint32_t v = lane_shift(lds, p, kc);
-    const std::uint64_t blk = static_cast<std::uint64_t>(r0 + j) * kBpr + lane_blk;
     if constexpr (INIT) {
-      const std::uint32_t init = a.init_raw[blk < a.nblocks ? blk : a.nblocks - 1u];
+      const std::uint32_t init = ini[bslot];
 #pragma unroll
       for (int i = 0; i < kBits; ++i)
         v ^= static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), gl * kBits + i, 1)) & hsr[i];
@@ -1293,7 +1296,7 @@ __device__ __forceinline__ void crc_packed_small_gen_body(const RowsArgs& a, std
       }
 #pragma unroll
       for (int i = 0; i < ILP; ++i)
-        if (jq + i < nrows) finish(jq + i, p[i].value());
+        if (jq + i < nrows) finish(jq + i, p[i].value(), q + i);
     }
   }
 }

@@ -246,7 +246,13 @@ template <int ALIGN, int NF>
 __global__ __launch_bounds__(kThreads) void crc_lanes_r(RowsArgs a) {
   constexpr int kMis = ALIGN == 16 ? 0 : ALIGN == 4 ? 12 : 15;
   constexpr int NG = (4 * NF + kMis + 15) / 16;
-  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? 5 : 4;
+#ifndef TKV_AB_R_DEPTH5  // (A/B builds only: steps of 5-granule windows in flight)
+#define TKV_AB_R_DEPTH5 4
+#endif
+#ifndef TKV_AB_R_DEPTH4
+#define TKV_AB_R_DEPTH4 5
+#endif
+  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? TKV_AB_R_DEPTH4 : TKV_AB_R_DEPTH5;
   __shared__ std::uint32_t lds[kLdsSliceWords];
   dev::crc_lanes_r_body<ALIGN, NF, NG, DEPTH, kPackedPrio>(a, lds);
 }

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--gib", type=float, default=1.0)
     ap.add_argument("--only", default=None)
     ap.add_argument("--lens", default=None, help="comma-separated uniform lengths instead of the default list")
+    ap.add_argument("--init", action="store_true", help="uniform batches with per-block initial registers")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     libs = [load(p) for p in args.libs]
@@ -53,8 +54,10 @@ def main():
     def uniform(L, stride=None, off=0):
         stride = stride or L
         n = total // stride
-        return (f"uniform {L} B stride {stride} base+{off}", n * L, n,
-                lambda lib, o: lib.tkv_crc32_batch_uniform_device(VP(D + off), stride, L, None, o, n, sp))
+        ini = torch.randint(0, 2**31 - 1, (n,), dtype=torch.int32, device="cuda") if args.init else None
+        iv = VP(ini.data_ptr()) if args.init else None
+        return (f"uniform {L} B stride {stride} base+{off}" + (" per-block init" if args.init else ""), n * L, n,
+                lambda lib, o: lib.tkv_crc32_batch_uniform_device(VP(D + off), stride, L, iv, o, n, sp))
 
     def irregular(name, lens, gaps, off=0):
         lens = np.asarray(lens, np.int64)
