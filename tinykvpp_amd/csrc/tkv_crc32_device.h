@@ -1197,7 +1197,7 @@ __device__ __forceinline__ void lane_dwords(const uint4 (&g)[kLaneGran], std::ui
 template <int G, bool INIT, int DEPTH, int ILP, int PRIO = 0>
 __device__ __forceinline__ void crc_packed_small_gen_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(G >= 2 && G <= 32 && (G & (G - 1)) == 0, "G-lane groups of a power of two, 2 to 32");
-  static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
+  static_assert(DEPTH >= ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP (DEPTH - ILP steps in flight)");
   constexpr std::uint32_t kBpr = 64u / G;   // blocks per row
   constexpr int kBits = INIT ? 32 / G : 1;  // init bits per lane
   fill_lds_group<G>(a.tabs, lds);
@@ -1546,7 +1546,7 @@ __device__ __forceinline__ void crc_lanes_r_body(const RowsArgs& a, std::uint32_
 
 template <int ALIGN, int NG, int DEPTH, int ILP, int PRIO = 0, int R = 32>
 __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_t* lds) {
-  static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
+  static_assert(DEPTH >= ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP (DEPTH - ILP steps in flight)");
   constexpr int ND = 4 * NG;
   static_assert(R == 32 || R == 16, "32- or 16-replica table image");
   if constexpr (R == 32) fill_lds_slicing(a.tabs, lds);
@@ -1739,7 +1739,7 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
 #endif
 constexpr int kWalkAhead = TKV_AB_WALK_AHEAD;
 constexpr int kListAhead = TKV_AB_LIST_AHEAD;
-static_assert(kWalkAhead >= 1 && kWalkAhead <= 3 && kListAhead >= 1 && kListAhead <= 3,
+static_assert(kWalkAhead >= 0 && kWalkAhead <= 3 && kListAhead >= 0 && kListAhead <= 3,
               "at most three steps ahead of a four-slot ring");
 
 // Lane blocks of an irregular batch (len <= kLaneMax, in a scan tile the prepass marked dense), walked

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small(RowsArgs a) {
 #ifndef TKV_GEN_ILP
 #define TKV_GEN_ILP 1
 #endif
-static_assert(TKV_GEN_ILP >= 1 && TKV_GEN_DEPTH > TKV_GEN_ILP, "crc_packed_small_gen: DEPTH - ILP rows stay in flight");
+static_assert(TKV_GEN_ILP >= 1 && TKV_GEN_DEPTH >= TKV_GEN_ILP, "crc_packed_small_gen: DEPTH - ILP rows stay in flight");
 template <int G, bool INIT>
 __global__ __launch_bounds__(kThreads) void crc_packed_small_gen(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
@@ -234,7 +234,13 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
 #ifndef TKV_AB_LANES_DEPTH3  // (A/B builds only: the 3-granule window's depth)
 #define TKV_AB_LANES_DEPTH3 6
 #endif
-  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? TKV_AB_LANES_DEPTH3 : NG == 4 ? 5 : 4;
+#ifndef TKV_AB_LANES_DEPTH4
+#define TKV_AB_LANES_DEPTH4 5
+#endif
+#ifndef TKV_AB_LANES_DEPTH5
+#define TKV_AB_LANES_DEPTH5 4
+#endif
+  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? TKV_AB_LANES_DEPTH3 : NG == 4 ? TKV_AB_LANES_DEPTH4 : TKV_AB_LANES_DEPTH5;
   __shared__ std::uint32_t lds[kLdsSliceWords];
   dev::crc_lanes_n_body<ALIGN, NG, DEPTH, 1, kPackedPrio>(a, lds);
 }
@@ -246,8 +252,11 @@ template <int ALIGN, int NF>
 __global__ __launch_bounds__(kThreads) void crc_lanes_r(RowsArgs a) {
   constexpr int kMis = ALIGN == 16 ? 0 : ALIGN == 4 ? 12 : 15;
   constexpr int NG = (4 * NF + kMis + 15) / 16;
+// 5-granule windows load no step ahead of their fold: in one process against DEPTH 4 / 3 / 2
+// (profiles/r4/lanes_r/depth_probe.jsonl) 50-59 B ran 11-13 % faster with no step in flight and the
+// same with one to three; narrow windows (5-27 B) want their steps in flight (+2 to +20 %).
 #ifndef TKV_AB_R_DEPTH5  // (A/B builds only: steps of 5-granule windows in flight)
-#define TKV_AB_R_DEPTH5 4
+#define TKV_AB_R_DEPTH5 1
 #endif
 #ifndef TKV_AB_R_DEPTH4
 #define TKV_AB_R_DEPTH4 5

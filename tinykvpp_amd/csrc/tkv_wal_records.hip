@@ -102,6 +102,9 @@ __device__ __forceinline__ std::uint32_t rec_fold(const std::uint32_t* lds, cons
 
 // NG granules per record window; AHEAD steps of granules in flight (3 for narrow windows, 2 at 6
 // granules, 1 for the wide ones, whose three slots would spill at 16 waves per CU).
+#ifndef TKV_AB_REC_AHEAD0  // (A/B builds: 1 = no granules in flight ahead of the fold)
+#define TKV_AB_REC_AHEAD0 0
+#endif
 template <int NG, int AHEAD, bool W16>
 __global__ __launch_bounds__(RecShape<W16>::kThreads)
 __attribute__((amdgpu_waves_per_eu(RecShape<W16>::kWgPerCu * RecShape<W16>::kThreads / 256))) void
@@ -110,7 +113,7 @@ wal_rec_lanes(RecArgs a, const DeviceTables* tabs) {
   constexpr int NPAY = ND - 3;        // whole payload dwords folded from the window (payload at dword 2; one spare for the tail)
   constexpr int RING = 4;             // offsets are fetched RING steps ahead of their granules
   constexpr int DRING = AHEAD == 1 ? 2 : 4;
-  static_assert(AHEAD >= 1 && AHEAD <= 3, "granules one to three steps ahead");
+  static_assert(AHEAD >= 0 && AHEAD <= 3, "granules up to three steps ahead");
   __shared__ std::uint32_t lds[W16 ? kLdsSliceWords / 2 : kLdsSliceWords];
   if constexpr (W16) dev::fill_lds_slicing16(tabs, lds);
   else dev::fill_lds_slicing(tabs, lds);
@@ -407,11 +410,11 @@ void launch_records(RecArgs a, std::uint32_t max_payload, int ncu, const DeviceT
   switch (w16 ? ng : ng + 16u) {
     case 4: hipLaunchKernelGGL((wal_rec_lanes<4, TKV_AB_REC16_AHEAD, true>), g, b, 0, st, a, tabs); break;
     case 5: hipLaunchKernelGGL((wal_rec_lanes<5, TKV_AB_REC16_AHEAD, true>), g, b, 0, st, a, tabs); break;
-    case 20: hipLaunchKernelGGL((wal_rec_lanes<4, 3, false>), g, b, 0, st, a, tabs); break;
-    case 21: hipLaunchKernelGGL((wal_rec_lanes<5, 3, false>), g, b, 0, st, a, tabs); break;
-    case 22: hipLaunchKernelGGL((wal_rec_lanes<6, 2, false>), g, b, 0, st, a, tabs); break;
-    case 23: hipLaunchKernelGGL((wal_rec_lanes<7, 1, false>), g, b, 0, st, a, tabs); break;
-    default: hipLaunchKernelGGL((wal_rec_lanes<8, 1, false>), g, b, 0, st, a, tabs); break;
+    case 20: hipLaunchKernelGGL((wal_rec_lanes<4, TKV_AB_REC_AHEAD0 ? 0 : 3, false>), g, b, 0, st, a, tabs); break;
+    case 21: hipLaunchKernelGGL((wal_rec_lanes<5, TKV_AB_REC_AHEAD0 ? 0 : 3, false>), g, b, 0, st, a, tabs); break;
+    case 22: hipLaunchKernelGGL((wal_rec_lanes<6, TKV_AB_REC_AHEAD0 ? 0 : 2, false>), g, b, 0, st, a, tabs); break;
+    case 23: hipLaunchKernelGGL((wal_rec_lanes<7, TKV_AB_REC_AHEAD0 ? 0 : 1, false>), g, b, 0, st, a, tabs); break;
+    default: hipLaunchKernelGGL((wal_rec_lanes<8, TKV_AB_REC_AHEAD0 ? 0 : 1, false>), g, b, 0, st, a, tabs); break;
   }
 }
 
