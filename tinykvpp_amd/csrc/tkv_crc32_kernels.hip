@@ -237,8 +237,10 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
 #ifndef TKV_AB_LANES_DEPTH4
 #define TKV_AB_LANES_DEPTH4 5
 #endif
+// 5-granule windows: no step in flight (+7-13 % at 52-60 B in one process against DEPTH 4,
+// profiles/r4/lanes_r/nopf_probe.jsonl; the right-aligned kernel measured the same, crc_lanes_r)
 #ifndef TKV_AB_LANES_DEPTH5
-#define TKV_AB_LANES_DEPTH5 4
+#define TKV_AB_LANES_DEPTH5 1
 #endif
   constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? TKV_AB_LANES_DEPTH3 : NG == 4 ? TKV_AB_LANES_DEPTH4 : TKV_AB_LANES_DEPTH5;
   __shared__ std::uint32_t lds[kLdsSliceWords];

@@ -105,6 +105,9 @@ __device__ __forceinline__ std::uint32_t rec_fold(const std::uint32_t* lds, cons
 #ifndef TKV_AB_REC_AHEAD0  // (A/B builds: 1 = no granules in flight ahead of the fold)
 #define TKV_AB_REC_AHEAD0 0
 #endif
+#ifndef TKV_AB_REC4_AHEAD  // (A/B builds: steps in flight for 4-granule windows)
+#define TKV_AB_REC4_AHEAD 3
+#endif
 template <int NG, int AHEAD, bool W16>
 __global__ __launch_bounds__(RecShape<W16>::kThreads)
 __attribute__((amdgpu_waves_per_eu(RecShape<W16>::kWgPerCu * RecShape<W16>::kThreads / 256))) void
@@ -410,7 +413,7 @@ void launch_records(RecArgs a, std::uint32_t max_payload, int ncu, const DeviceT
   switch (w16 ? ng : ng + 16u) {
     case 4: hipLaunchKernelGGL((wal_rec_lanes<4, TKV_AB_REC16_AHEAD, true>), g, b, 0, st, a, tabs); break;
     case 5: hipLaunchKernelGGL((wal_rec_lanes<5, TKV_AB_REC16_AHEAD, true>), g, b, 0, st, a, tabs); break;
-    case 20: hipLaunchKernelGGL((wal_rec_lanes<4, TKV_AB_REC_AHEAD0 ? 0 : 3, false>), g, b, 0, st, a, tabs); break;
+    case 20: hipLaunchKernelGGL((wal_rec_lanes<4, TKV_AB_REC_AHEAD0 ? 0 : TKV_AB_REC4_AHEAD, false>), g, b, 0, st, a, tabs); break;
     case 21: hipLaunchKernelGGL((wal_rec_lanes<5, TKV_AB_REC_AHEAD0 ? 0 : 3, false>), g, b, 0, st, a, tabs); break;
     case 22: hipLaunchKernelGGL((wal_rec_lanes<6, TKV_AB_REC_AHEAD0 ? 0 : 2, false>), g, b, 0, st, a, tabs); break;
     case 23: hipLaunchKernelGGL((wal_rec_lanes<7, TKV_AB_REC_AHEAD0 ? 0 : 1, false>), g, b, 0, st, a, tabs); break;
