@@ -1679,11 +1679,17 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
     }
   };
   auto lds32 = [&](std::uint32_t byte) { return lds_at(lds, byte); };
-  copy(0, buf0);
+#ifndef TKV_AB_LANES_LDS_NOPF  // (A/B builds: 1 = each step's copy issued and awaited at its fold)
+#define TKV_AB_LANES_LDS_NOPF 0
+#endif
+  if (!TKV_AB_LANES_LDS_NOPF) copy(0, buf0);
   for (std::uint32_t j = 0; j < ns; ++j) {
     if constexpr (PRIO != 0) set_prio_from_left<PRIO>(ns - j, ns);
     const std::uint32_t cur = buf0 + (j & 1u) * kLanesLdsBuf;
-    if (j + 1u < ns) {
+    if (TKV_AB_LANES_LDS_NOPF) {
+      copy(j, cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (j + 1u < ns) {
       copy(j + 1u, buf0 + ((j + 1u) & 1u) * kLanesLdsBuf);
       // step j's copy has landed; step j+1's KB copies stay in flight
       if constexpr (KB == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");

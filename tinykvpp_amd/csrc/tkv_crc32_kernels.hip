@@ -263,7 +263,10 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_r(RowsArgs a) {
 #ifndef TKV_AB_R_DEPTH4
 #define TKV_AB_R_DEPTH4 5
 #endif
-  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? TKV_AB_R_DEPTH4 : TKV_AB_R_DEPTH5;
+#ifndef TKV_AB_R_DEPTH3
+#define TKV_AB_R_DEPTH3 6
+#endif
+  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? TKV_AB_R_DEPTH3 : NG == 4 ? TKV_AB_R_DEPTH4 : TKV_AB_R_DEPTH5;
   __shared__ std::uint32_t lds[kLdsSliceWords];
   dev::crc_lanes_r_body<ALIGN, NF, NG, DEPTH, kPackedPrio>(a, lds);
 }

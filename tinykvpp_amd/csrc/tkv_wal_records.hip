@@ -105,8 +105,11 @@ __device__ __forceinline__ std::uint32_t rec_fold(const std::uint32_t* lds, cons
 #ifndef TKV_AB_REC_AHEAD0  // (A/B builds: 1 = no granules in flight ahead of the fold)
 #define TKV_AB_REC_AHEAD0 0
 #endif
+// 4-granule record windows load at the fold, no step ahead: in one process against 3 and 1 steps in
+// flight (profiles/r4/lanes_r/rec4_probe.jsonl) 28-byte payloads 0.2946 -> 0.2851 ms (+3.3 %; +5.5 %
+// on another box); wider windows lost with it (mixed 22-80 B -4.7 %).
 #ifndef TKV_AB_REC4_AHEAD  // (A/B builds: steps in flight for 4-granule windows)
-#define TKV_AB_REC4_AHEAD 3
+#define TKV_AB_REC4_AHEAD 0
 #endif
 template <int NG, int AHEAD, bool W16>
 __global__ __launch_bounds__(RecShape<W16>::kThreads)
