@@ -30,6 +30,10 @@ __device__ __forceinline__ uint4 gload16(std::uintptr_t p) {
 // window dword that no fold reads is dead as soon as its load is issued, and the compiler then reuses
 // its register while the load is in flight, which costs a vmcnt(0) wait in front of every step and so
 // drains the whole load pipeline.
+#ifndef TKV_AB_GROUP_SHUF  // (A/B builds: 1 = group lanes take their fifth granule from the next lane)
+#define TKV_AB_GROUP_SHUF 0
+#endif
+constexpr bool kGroupShuf = TKV_AB_GROUP_SHUF != 0;
 template <int N>
 __device__ __forceinline__ void keep_live(const uint4 (&g)[N]) {
 #pragma unroll
@@ -1243,9 +1247,16 @@ __device__ __forceinline__ void crc_packed_small_gen_body(const RowsArgs& a, std
     const std::uintptr_t p = static_cast<std::uintptr_t>(static_cast<std::int64_t>(blo) + c_lane);
     const std::uintptr_t al = p & ~static_cast<std::uintptr_t>(15);
 #pragma unroll
-    for (int i = 0; i < kLaneGran; ++i) {
+    for (int i = 0; i < (kGroupShuf ? kLaneGran - 1 : kLaneGran); ++i) {
       const std::uintptr_t q = al + 16u * i;
       buf[slot][i] = gload16(live && q + 16u > blo && q < bhi ? q : dmy);
+    }
+    if constexpr (kGroupShuf) {  // the fifth granule: the group's last lane only (group_walk)
+      buf[slot][kLaneGran - 1] = make_uint4(0u, 0u, 0u, 0u);
+      if (gl == G - 1u) {
+        const std::uintptr_t q = al + 16u * (kLaneGran - 1);
+        buf[slot][kLaneGran - 1] = gload16(live && q + 16u > blo && q < bhi ? q : dmy);
+      }
     }
     o16[slot] = static_cast<std::uint32_t>(p & 15u);
   };
@@ -1286,6 +1297,15 @@ __device__ __forceinline__ void crc_packed_small_gen_body(const RowsArgs& a, std
       Reg p[ILP];
 #pragma unroll
       for (int i = 0; i < ILP; ++i) {
+        if constexpr (kGroupShuf) {
+          const int src = static_cast<int>(((lane + 1u) & 63u) * 4u);
+          const uint4 n0 = buf[q + i][0];
+          const uint4 nb = make_uint4(static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.x))),
+                                      static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.y))),
+                                      static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.z))),
+                                      static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.w))));
+          if (gl != G - 1u) buf[q + i][kLaneGran - 1] = nb;
+        }
         lane_dwords<1>(buf[q + i], o16[q + i], d[i]);
         p[i] = Reg{0, 0};
       }
@@ -1880,10 +1900,20 @@ __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_
                                 64 * static_cast<std::int32_t>(gl);
     const std::uintptr_t p = static_cast<std::uintptr_t>(static_cast<std::int64_t>(blo) + c_lane);
     const std::uintptr_t al = p & ~static_cast<std::uintptr_t>(15);
+    // SHUF: a lane's fifth granule is the next lane's first (the group's lanes cover adjacent 64-byte
+    // ranges at the same offset), so only the group's last lane loads it and the others take it from
+    // their neighbour at the fold (ds_bpermute): 4 + 1/G granule loads per lane instead of 5
 #pragma unroll
-    for (int i = 0; i < kLaneGran; ++i) {
+    for (int i = 0; i < (kGroupShuf ? kLaneGran - 1 : kLaneGran); ++i) {
       const std::uintptr_t g = al + 16u * i;
       q[slot][i] = gload16(live && g + 16u > blo && g < bhi ? g : dmy);
+    }
+    if constexpr (kGroupShuf) {
+      q[slot][kLaneGran - 1] = make_uint4(0u, 0u, 0u, 0u);
+      if (gl == G - 1u) {
+        const std::uintptr_t g = al + 16u * (kLaneGran - 1);
+        q[slot][kLaneGran - 1] = gload16(live && g + 16u > blo && g < bhi ? g : dmy);
+      }
     }
     m_len[slot] = live ? len : 0xFFFFFFFFu;  // 0xFFFFFFFF: nothing to fold or store
     m_o[slot] = static_cast<std::uint32_t>(p & 15u);
@@ -1899,6 +1929,15 @@ __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_
     const std::uint32_t len = m_len[slot];
     const bool live = len != 0xFFFFFFFFu;
     if (__ballot(live) == 0) return;  // no group block in this step
+    if constexpr (kGroupShuf) {
+      const int src = static_cast<int>(((lane + 1u) & 63u) * 4u);
+      const uint4 n0 = q[slot][0];
+      const uint4 nb = make_uint4(static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.x))),
+                                  static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.y))),
+                                  static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.z))),
+                                  static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.w))));
+      if (gl != G - 1u) q[slot][kLaneGran - 1] = nb;
+    }
     std::uint32_t d[16];
     lane_dwords<1>(q[slot], m_o[slot], d);
     const std::int32_t lead = m_lead[slot];
