@@ -34,6 +34,12 @@ __device__ __forceinline__ uint4 gload16(std::uintptr_t p) {
 #define TKV_AB_GROUP_SHUF 0
 #endif
 constexpr bool kGroupShuf = TKV_AB_GROUP_SHUF != 0;
+// The 16-lane list walk (blocks of 513-1024 bytes) takes it from the next lane in the product: in one
+// process +2.9 % on 513-1024-byte and +3.9 % on 300-1000-byte payloads; with 4- and 8-lane groups
+// the shuffle cost more than the loads it saved (-6.5 % and -4.5 %, profiles/r4/group_shuf/).
+#ifndef TKV_AB_GROUP16_SHUF
+#define TKV_AB_GROUP16_SHUF 1
+#endif
 template <int N>
 __device__ __forceinline__ void keep_live(const uint4 (&g)[N]) {
 #pragma unroll
@@ -1855,6 +1861,7 @@ template <int G, bool LIST>
 __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_t* lds, std::uint32_t lo,
                                            std::uint32_t cnt) {
   static_assert(G == 4 || G == 8 || (LIST && G == 16), "4- or 8-lane groups (16 for listed blocks)");
+  constexpr bool kShuf = kGroupShuf || (G == 16 && TKV_AB_GROUP16_SHUF != 0);
   constexpr int RING = 4;
   constexpr int kAhead = LIST ? kListAhead : kWalkAhead;  // steps of data in flight
   constexpr std::uint32_t kSlot = 64u * G;
@@ -1904,11 +1911,11 @@ __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_
     // ranges at the same offset), so only the group's last lane loads it and the others take it from
     // their neighbour at the fold (ds_bpermute): 4 + 1/G granule loads per lane instead of 5
 #pragma unroll
-    for (int i = 0; i < (kGroupShuf ? kLaneGran - 1 : kLaneGran); ++i) {
+    for (int i = 0; i < (kShuf ? kLaneGran - 1 : kLaneGran); ++i) {
       const std::uintptr_t g = al + 16u * i;
       q[slot][i] = gload16(live && g + 16u > blo && g < bhi ? g : dmy);
     }
-    if constexpr (kGroupShuf) {
+    if constexpr (kShuf) {
       q[slot][kLaneGran - 1] = make_uint4(0u, 0u, 0u, 0u);
       if (gl == G - 1u) {
         const std::uintptr_t g = al + 16u * (kLaneGran - 1);
@@ -1929,7 +1936,7 @@ __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_
     const std::uint32_t len = m_len[slot];
     const bool live = len != 0xFFFFFFFFu;
     if (__ballot(live) == 0) return;  // no group block in this step
-    if constexpr (kGroupShuf) {
+    if constexpr (kShuf) {
       const int src = static_cast<int>(((lane + 1u) & 63u) * 4u);
       const uint4 n0 = q[slot][0];
       const uint4 nb = make_uint4(static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.x))),
