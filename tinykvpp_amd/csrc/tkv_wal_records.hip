@@ -235,6 +235,9 @@ __device__ __forceinline__ std::uint32_t wave_max_u32(std::uint32_t v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
+#ifndef TKV_AB_REC_LDS_STOREWAIT  // (A/B builds: 1 = every step also waits for the previous step's store)
+#define TKV_AB_REC_LDS_STOREWAIT 0
+#endif
 template <int NG>
 __global__ __launch_bounds__(kRecLdsThreads) void wal_rec_lds(RecArgs a, const DeviceTables* tabs) {
   constexpr int ND = 4 * NG - 4;  // realigned dwords of the window
@@ -306,7 +309,10 @@ __global__ __launch_bounds__(kRecLdsThreads) void wal_rec_lds(RecArgs a, const D
   plan(0);
   for (std::uint32_t j = 0; j < ns; ++j) {
     dev::set_prio_from_left<3>(ns - j, ns);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step j's span and step j+1's offsets have landed
+    // step j's span and step j+1's offsets have landed. With a result array, step j-1's result store
+    // is the newest memory operation and need not be waited for (vmcnt counts stores too)
+    if (TKV_AB_REC_LDS_STOREWAIT == 0 && a.crc && j > 0u) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const std::uint32_t k = j & 1u;
     const std::uint32_t off = dev::lds_at(lds, offs0 + k * 256u + 4u * lane);  // (read before its buffer is reused)
     const bool staged = k ? st_staged1 : st_staged0;
