@@ -1705,6 +1705,9 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
     }
   };
   auto lds32 = [&](std::uint32_t byte) { return lds_at(lds, byte); };
+#ifndef TKV_AB_LANES_LDS_STOREWAIT  // (A/B builds: 1 = every step also waits for the previous step's store)
+#define TKV_AB_LANES_LDS_STOREWAIT 0
+#endif
 #ifndef TKV_AB_LANES_LDS_NOPF  // (A/B builds: 1 = each step's copy issued and awaited at its fold)
 #define TKV_AB_LANES_LDS_NOPF 0
 #endif
@@ -1717,10 +1720,19 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (j + 1u < ns) {
       copy(j + 1u, buf0 + ((j + 1u) & 1u) * kLanesLdsBuf);
-      // step j's copy has landed; step j+1's KB copies stay in flight
-      if constexpr (KB == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      else if constexpr (KB == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      // step j's copy has landed; step j+1's KB copies stay in flight, and so does step j-1's result
+      // store (issued after step j's copy; vmcnt counts stores too, in issue order)
+      if (TKV_AB_LANES_LDS_STOREWAIT == 0 && j > 0u) {
+        if constexpr (KB == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if constexpr (KB == 2) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        if constexpr (KB == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        else if constexpr (KB == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      }
+    } else if (TKV_AB_LANES_LDS_STOREWAIT == 0 && j > 0u) {
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
