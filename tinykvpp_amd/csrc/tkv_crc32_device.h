@@ -1705,8 +1705,11 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
     }
   };
   auto lds32 = [&](std::uint32_t byte) { return lds_at(lds, byte); };
-#ifndef TKV_AB_LANES_LDS_STOREWAIT  // (A/B builds: 1 = every step also waits for the previous step's store)
-#define TKV_AB_LANES_LDS_STOREWAIT 0
+// Leaving the previous step's result store in flight at the step wait (vmcnt(KB + 1)) measured
+// neutral here (-2.1 to +1.0 % at 28-47 B, profiles/r4/storewait/lanes_probe.jsonl); the record check
+// kept it (+0.8 %). 0 = leave it in flight.
+#ifndef TKV_AB_LANES_LDS_STOREWAIT  // (A/B builds: 0 = the step wait leaves the previous store in flight)
+#define TKV_AB_LANES_LDS_STOREWAIT 1
 #endif
 #ifndef TKV_AB_LANES_LDS_NOPF  // (A/B builds: 1 = each step's copy issued and awaited at its fold)
 #define TKV_AB_LANES_LDS_NOPF 0
