@@ -914,10 +914,13 @@ __device__ __forceinline__ void crc_stream_body(const RowsArgs& a, std::uint32_t
 // ranges, slots 12-15 the smallest, matching the issue arbitration that favours a SIMD's older waves.
 // PRIO (0: off): set_prio_from_left<PRIO> once per DEPTH rows (the product uses 3, and SKEW 154 for
 // blocks of more than one row; tkv_crc32_kernels.hip).
+#ifndef TKV_AB_PACKED_EARLY  // (A/B builds: 0 = table fill first, then the first rows' loads)
+#define TKV_AB_PACKED_EARLY 1
+#endif
+constexpr bool kPackedEarly = TKV_AB_PACKED_EARLY != 0;
 template <int DEPTH, int ILP, bool R1, int SKEW = 0, int PRIO = 0>
 __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
-  fill_lds(a.tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
   const LaneConst kc = lane_const(lane);
   const std::uint32_t hcon = a.tabs->horner[lane & 31u];  // Shift_4096(1 << (l & 31))
@@ -927,7 +930,6 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
       lo_half ? 0u
               : static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(a.init_default),
                                                                 lane & 31u, 1)) & hcon;
-  __syncthreads();
 
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint64_t W = a.nwaves;
@@ -948,7 +950,6 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
     b0 = static_cast<std::uint32_t>(wave * static_cast<std::uint64_t>(a.nblocks) / W);
     nb = static_cast<std::uint32_t>((wave + 1) * static_cast<std::uint64_t>(a.nblocks) / W) - b0;
   }
-  if (nb == 0) return;
   const std::uint32_t nrows = nb * R;  // wave-local rows j = 0 .. nrows-1, contiguous in memory
   const std::uintptr_t lane_base =
       reinterpret_cast<std::uintptr_t>(a.base) + static_cast<std::uint64_t>(b0) * R * kRow + lane * kSeg;
@@ -995,8 +996,19 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
     }
   };
 
+  // EARLY: the first rows' loads go out before the table fill, so the fill (table loads from L2, LDS
+  // writes, the barrier) overlaps their HBM latency instead of preceding it
+  if (kPackedEarly && nb != 0) {
 #pragma unroll
-  for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
+    for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
+  }
+  fill_lds(a.tabs, lds);
+  __syncthreads();
+  if (nb == 0) return;
+  if (!kPackedEarly) {
+#pragma unroll
+    for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
+  }
   for (std::uint32_t j = 0; j < nrows; j += DEPTH) {
     if constexpr (PRIO != 0) set_prio_from_left<PRIO>(nrows - j, nrows);
 #pragma unroll
