@@ -1786,15 +1786,17 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
 }
 
 // Steps of data in flight ahead of the fold in the lane phase and the group walks (the ring holds
-// four; A/B builds: -DTKV_AB_WALK_AHEAD=3).
+// four), and in the small phase's class-list walks. One step each: in one process against two (walks)
+// and three (lists), the listed small-block batches ran 3.1-3.7 % faster (300-1000 B, 0-1024 B,
+// 100-700 B, 180-400 B), the group passes up to 1.3 % (profiles/r4/walk_depth/); two list steps
+// measured below both one and three. (Earlier in round 4 three list steps had beaten two by
+// 0.7-1.6 %, profiles/r4/s12/; the lane phase and group passes spill at three.) 0 = no step ahead
+// (10-15 % slower for every walk, profiles/r4/lanes_r/nopf_probe.jsonl).
 #ifndef TKV_AB_WALK_AHEAD
-#define TKV_AB_WALK_AHEAD 2
+#define TKV_AB_WALK_AHEAD 1
 #endif
-// The small phase's list walks (in crc_rows, which has registers to spare) keep three steps ahead:
-// +0.7-1.6 % on listed 257-1024-byte batches in one process; the lane phase and group passes (in
-// crc_stream, 128 VGPRs) would spill at three and measured 7 % slower (profiles/r4/s12/).
 #ifndef TKV_AB_LIST_AHEAD
-#define TKV_AB_LIST_AHEAD 3
+#define TKV_AB_LIST_AHEAD 1
 #endif
 constexpr int kWalkAhead = TKV_AB_WALK_AHEAD;
 constexpr int kListAhead = TKV_AB_LIST_AHEAD;
