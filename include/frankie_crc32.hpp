@@ -19,7 +19,7 @@
 // on this node, a HIP failure) the same span is recomputed on the host by tkv_crc32_update_fallback,
 // which warns once per process on stderr and counts the call. update therefore never fails, at any
 // span size, with or without a device. -DTKV_DROPIN_HOST_MAX=0 sends every span to the GPU first.
-// tkv_debug_update_counts says which path the calling thread's calls took: [0] host span, [1] GPU,
+// tkv_debug_update_counts_n says which path the calling thread's calls took: [0] host span, [1] GPU,
 // [2] host recompute after a GPU error.
 //
 // Build: add include/ to the include path and link libtkv_crc32.so.

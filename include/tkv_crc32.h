@@ -262,9 +262,13 @@ int tkv_debug_multi_combine(uint32_t poly, int ndev, const uint64_t *h_offsets, 
                             const uint32_t *h_init_raw, uint64_t n, const uint32_t *piece_final,
                             uint32_t *h_out_final);
 /* Update calls of the calling thread so far: out[0] through tkv_crc32[c]_update_host (the drop-in's
- * short-span host path), out[1] through tkv_crc32[c]_update (the GPU), out[2] through
- * tkv_crc32[c]_update_fallback (host recomputes after a failed GPU update). */
-void tkv_debug_update_counts(uint64_t out[3]);
+ * short-span host path), out[1] through tkv_crc32[c]_update (the GPU). (The round-3 entry point:
+ * two words.) */
+void tkv_debug_update_counts(uint64_t out[2]);
+/* The same counters into out[0..n) (n may be smaller or larger than the count), plus out[2] = calls
+ * through tkv_crc32[c]_update_fallback (host recomputes after a failed GPU update). Returns the number
+ * of counters (3). */
+size_t tkv_debug_update_counts_n(uint64_t *out, size_t n);
 /* What the calling thread's last tkv_wal_verify / tkv_wal_verify_device did: out[0] = device walk
  * passes, out[1] = 1 when it handed the image to the exact host-thread walk, out[2] = 1 when a
  * host image was copied to the device, out[3] = 1 when at least one device pass ran and every pass

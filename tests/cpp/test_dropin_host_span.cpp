@@ -3,7 +3,7 @@
 // and wal_entry::encode's record CRC (wal.cpp:54-57, tests/golden/wal.json) through
 // frankie::core::crc32, every length up to the threshold, and the reference's contract: update never
 // fails and touches no GPU for these spans (this runs on a machine without one; the per-thread
-// counters of tkv_debug_update_counts show every call on the host path). It also times a 36-byte put
+// counters of tkv_debug_update_counts_n show every call on the host path). It also times a 36-byte put
 // (wal_entry::encode's {put, 42, "hello", "world"}) against the reference's byte loop
 // (crc32.cpp:9-16, restated inline) on the same core.
 //
@@ -129,7 +129,7 @@ std::uint32_t byte_loop(const std::byte* p, std::size_t n) {
 // Spans longer than the threshold: the GPU, or the host recompute after its error.
 void long_spans() {
   std::uint64_t c0[3], c1[3];
-  tkv_debug_update_counts(c0);
+  tkv_debug_update_counts_n(c0, 3);
   std::vector<std::byte> big(1u << 20);
   for (std::size_t i = 0; i < big.size(); ++i) big[i] = static_cast<std::byte>((i * 2246822519u) >> 13);
   CHECK_EQ(crc32{}.update({big.data(), big.size()}).finalize(), byte_loop(big.data(), big.size()));
@@ -148,7 +148,7 @@ void long_spans() {
   crc32 chained;
   (void)chained.update({rec.data() + 8, 100}).update({rec.data() + 108, 100000}).update({rec.data() + 100108, 7});
   CHECK_EQ(chained.finalize(), byte_loop(rec.data() + 8, 100107));
-  tkv_debug_update_counts(c1);
+  tkv_debug_update_counts_n(c1, 3);
   const bool gpu = tkv_device_count() > 0;
   std::printf("long_spans: %s; GPU calls %llu, host recomputes %llu\n", gpu ? "GPU present" : "no GPU",
               (unsigned long long)(c1[1] - c0[1]), (unsigned long long)(c1[2] - c0[2]));
@@ -160,7 +160,7 @@ void long_spans() {
 
 int main() {
   std::uint64_t c0[3], c1[3];
-  tkv_debug_update_counts(c0);
+  tkv_debug_update_counts_n(c0, 3);
   known_values();
   incremental_equals_single();
   wal_record_crc();
@@ -169,7 +169,7 @@ int main() {
     std::vector<std::byte> big(TKV_DROPIN_HOST_MAX, std::byte{7});
     (void)crc32{}.update({big.data(), big.size()}).finalize();
   }
-  tkv_debug_update_counts(c1);
+  tkv_debug_update_counts_n(c1, 3);
   CHECK_EQ(c1[1] - c0[1], 0u);   // no call took the GPU path
   if (c1[0] - c0[0] < 200) {      // every update above was a host span
     std::fprintf(stderr, "only %llu host span calls counted\n", (unsigned long long)(c1[0] - c0[0]));

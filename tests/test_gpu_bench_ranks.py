@@ -71,17 +71,3 @@ def test_bench_two_ranks_share_the_gpu(gpu, config):
     assert line["n_gpus"] == 2 and line["ranks_seen"] == 2
     assert line["bit_exact"] is True
     assert line["bit_exact_scope"].startswith("every block of every rank's shard")
-
-
-@pytest.mark.gpu
-def test_bench_two_ranks_cfg5_leg(gpu):
-    """The multi-rank line carries the cfg5 leg: each rank checksums its own 32 GiB shard
-    of BASELINE configs[4] (rank 1 = global blocks [512 K, 1 M), checked only by its committed golden
-    shard aggregate), and the leg's aggregate is both shards' bytes over the max wall time."""
-    line = run_bench(2, {"TKV_BENCH_BACKEND": "gloo"}, "cfg2", more=True)
-    assert set(line["more_configs"]) == {"cfg5"}
-    m = line["more_configs"]["cfg5"]
-    assert m["n_gpus"] == 2 and m["ranks_seen"] == 2
-    assert m["bit_exact"] is True
-    assert m["bit_exact_scope"].startswith("every block of every rank's shard")
-    assert m["value"] > 0 and m["ms_per_step"] > 0

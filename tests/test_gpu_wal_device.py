@@ -2,8 +2,9 @@
 
 tkv_wal_verify copies the slurped image to HBM and tkv_wal_verify_device takes an image already
 there; both walk the record_len chain of wal_entry::decode (/root/reference/src/engine/wal.cpp:63-130)
-on the GPU by speculative parallel walks with exact stitching, check every record's CRC in one batch
-and report the first corruption. Every case is compared with a sequential decode written here
+on the GPU in one sweep over the image (per-wave chunks, exact per-region walks, device-side fix-ups
+where a chunk's speculative entry was wrong), check every record's CRC and report the first
+corruption. No image is walked on the host. Every case is compared with a sequential decode written here
 (header size, record_len, CRC via the test oracle, key/value bounds: wal.cpp:68-121), so the
 parity is against the reference's decode order, not against the library's own host walk.
 """
@@ -81,9 +82,9 @@ def make_wal(rng, n_rec, vmax=16000, giant=(), fake_headers=0.0):
 
 
 def wal_last():
-    """What this thread's last WAL verify did (tkv_debug_wal_last): device passes, whether the exact
-    host-thread walk had to finish it, whether a host image was copied, whether every pass took the
-    fast stitch (no pointer jumping)."""
+    """What this thread's last WAL verify did (tkv_debug_wal_last): device rounds (the sweep plus its
+    fix-up rounds), whether the exact host-thread walk had to finish it (only for a host image the
+    device cannot hold), whether a host image was copied, whether the sweep needed no fix-up."""
     out = (ctypes.c_uint64 * 4)()
     tk.load_library().tkv_debug_wal_last(out)
     return {"passes": out[0], "host_walk": out[1], "copied": out[2], "fast": out[3]}
@@ -107,8 +108,8 @@ def both(img, size, shift=0):
 
 
 def device_walk_only(max_passes=1, fast=None):
-    """Both verifies of the last `both` call finished on the device, in at most max_passes passes
-    (and, if `fast` is given, with or without the pointer-jumping stitch)."""
+    """Both verifies of the last `both` call finished on the device, in at most max_passes rounds
+    (and, if `fast` is given, with or without fix-up rounds)."""
     for path, r in LAST.items():
         assert r["host_walk"] == 0, (path, r)
         assert 1 <= r["passes"] <= max_passes, (path, r)
@@ -162,8 +163,8 @@ def test_corrupted_record_len_and_overrun(gpu, oracle):
         want = sequential_decode(oracle, img, n)
         assert want == ("corrupted", bad, o)
         assert both(img, n) == (want, want)
-        # the chain breaks with pieces holding records after it: the fast stitch must refuse
-        device_walk_only(max_passes=8, fast=0)
+        # the chain breaks with regions holding records after it: decided in the sweep, on the device
+        device_walk_only(max_passes=8)
         img[o:o + 4] = old
 
 
@@ -176,12 +177,14 @@ def test_fake_headers_inside_values(gpu, oracle):
     want = sequential_decode(oracle, img, n)
     assert want == ("ok", offs.size, n)
     assert both(img, n) == (want, want)
-    print("fake headers, clean image:", LAST)  # which path ran: passes, host walk
+    print("fake headers, clean image:", LAST)  # which path ran: rounds, host walk
+    device_walk_only(max_passes=10 ** 6)  # fix-up rounds, never the host walk
     o = int(offs[39000]) + 26
     img[o] ^= 0x80
     want = sequential_decode(oracle, img, n)
     assert both(img, n) == (want, want)
     print("fake headers, corrupted image:", LAST)
+    device_walk_only(max_passes=10 ** 6)
 
 
 @pytest.mark.parametrize("n", [0, 1, 25, 26, 27, 33, 34, 35, 255, 256, 257, 2047, 2048, 2049, 4096 + 17, 16383, 16384,
@@ -203,3 +206,61 @@ def test_golden_records_on_device(gpu):
     bad[len(recs[0]) + 4] ^= 0xFF  # wal_test.cpp:809-850: parked at record 1
     d = torch.frombuffer(bad, dtype=torch.uint8).cuda()
     assert tk.wal.verify_device(d) == ("corrupted", 1, len(recs[0]))
+
+
+def test_values_made_of_records(gpu, oracle):
+    """Every value is itself a run of well-formed WAL records: chunk entries land on
+    fake chains, and the device fix-ups settle the true chain without the host walk, clean and with a
+    corruption near the end."""
+    rng = np.random.default_rng(12)
+    img, offs, size = make_wal(rng, 60000, vmax=4000, fake_headers=1.0)
+    n = img.size
+    want = sequential_decode(oracle, img, n)
+    assert want == ("ok", offs.size, n)
+    assert both(img, n) == (want, want)
+    print("values made of records:", LAST)
+    device_walk_only(max_passes=10 ** 6)
+    o = int(offs[59000]) + 30
+    img[o] ^= 0x40
+    want = sequential_decode(oracle, img, n)
+    assert both(img, n) == (want, want)
+    device_walk_only(max_passes=10 ** 6)
+
+
+@pytest.mark.parametrize("plen", [0, 1, 17, 18, 239, 240, 241, 3000])
+def test_payload_length_classes(gpu, oracle, plen):
+    """Records whose payloads sit at the lane-fold limit (240 bytes) and past it (the long-payload
+    batch), next to tiny corrupt ones (record_len < 18: key and value cannot fit)."""
+    rng = np.random.default_rng(plen + 100)
+    img, offs, size = make_wal(rng, 3000, vmax=300)
+    n = img.size
+    # rewrite record 1500 with a payload of plen bytes (record_len = plen), restamped
+    recs = [img[int(offs[i]):int(offs[i]) + int(size[i])].tobytes() for i in range(offs.size)]
+    klen = min(plen - 18, 4) if plen >= 18 else 0
+    vlen = plen - 18 - klen if plen >= 18 else 0
+    body = bytearray(rng.integers(0, 256, 26 + max(plen - 18, 0), dtype=np.uint8).tobytes())
+    body[0:4] = plen.to_bytes(4, "little")
+    body[8] = 0
+    body[17] = 0
+    body[18:22] = klen.to_bytes(4, "little")
+    body[22:26] = vlen.to_bytes(4, "little")
+    rec = bytes(body[:8 + plen]) if plen < 18 else bytes(body)
+    recs[1500] = rec
+    image = np.frombuffer(b"".join(recs), np.uint8).copy()
+    offs2 = np.concatenate([[0], np.cumsum([len(r) for r in recs])[:-1]]).astype(np.uint64)
+    sz2 = np.array([len(r) for r in recs], np.uint32)
+    lib = tk.load_library()
+    tk.check(lib.tkv_wal_stamp(ctypes.c_void_p(image.ctypes.data), ctypes.c_void_p(offs2.ctypes.data),
+                               ctypes.c_void_p(sz2.ctypes.data), offs2.size))
+    m = image.size
+    want = sequential_decode(oracle, image, m)
+    assert both(image, m) == (want, want)
+    if plen >= 18:
+        assert want == ("ok", len(recs), m)
+        o = int(offs2[1500]) + len(rec) - 1  # flip the record's last byte
+        image[o] ^= 1
+        want = sequential_decode(oracle, image, m)
+        assert want[:2] == ("corrupted", 1500)
+        assert both(image, m) == (want, want)
+    else:
+        assert want[:2] == ("corrupted", 1500)

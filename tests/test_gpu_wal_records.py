@@ -232,3 +232,42 @@ def test_lds_staged_windows(gpu, oracle, layout, shift):
         for i in sorted(rng.integers(70, n - 70, 3), reverse=True):  # latest first: each becomes the first bad
             img[o[i] + 8 + int(rng.integers(0, 36))] ^= 0x10
             assert check(oracle, img, offs, 36, shift) == i
+
+
+@pytest.mark.parametrize("max_payload", [36, 64])
+def test_null_crc_output(gpu, oracle, max_payload):
+    """d_crc = NULL through the C ABI: only the first bad record is computed, on the
+    LDS-staged path (36-byte payloads, 4-granule windows) and the granule path; clean and with a CRC
+    flip, first_bad must equal the restated decode's."""
+    import ctypes
+    rng = np.random.default_rng(77 + max_payload)
+    n = 20000
+    klen = rng.integers(0, 6, n).astype(np.uint64)
+    vlen = (max_payload - 18 - klen).astype(np.uint64)
+    size = 26 + klen + vlen
+    offs = np.concatenate([[0], np.cumsum(size[:-1])]).astype(np.uint64)
+    img = rng.integers(0, 256, int(size.sum()), dtype=np.uint8)
+    hdr = np.zeros((n, 26), np.uint8)
+    hdr[:, 0:4] = (size - 8).astype("<u4").view(np.uint8).reshape(-1, 4)
+    hdr[:, 18:22] = klen.astype("<u4").view(np.uint8).reshape(-1, 4)
+    hdr[:, 22:26] = vlen.astype("<u4").view(np.uint8).reshape(-1, 4)
+    img[offs.astype(np.int64)[:, None] + np.arange(26)] = hdr
+    size32 = size.astype(np.uint32)
+    lib = tk.load_library()
+    tk.check(lib.tkv_wal_stamp(ctypes.c_void_p(img.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                               ctypes.c_void_p(size32.ctypes.data), n))
+    for flip in (None, 12345):
+        if flip is not None:
+            img[int(offs[flip]) + int(size[flip]) - 1] ^= 0x10
+        _, ok = expected(oracle, img, img.size, offs)
+        bad = np.flatnonzero(~ok)
+        want = int(bad[0]) if bad.size else n
+        d = torch.from_numpy(img).cuda()
+        o = torch.from_numpy(offs.astype(np.uint32).view(np.int32)).cuda()
+        fb = torch.empty(1, dtype=torch.int64, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        tk.check(lib.tkv_wal_check_records_device(ctypes.c_void_p(d.data_ptr()), img.size,
+                                                  ctypes.c_void_p(o.data_ptr()), n, max_payload, None,
+                                                  ctypes.c_void_p(fb.data_ptr()), ctypes.c_void_p(st)))
+        torch.cuda.synchronize()
+        assert int(fb.item()) == want, (flip, int(fb.item()), want)

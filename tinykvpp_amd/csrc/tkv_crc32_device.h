@@ -30,16 +30,6 @@ __device__ __forceinline__ uint4 gload16(std::uintptr_t p) {
 // window dword that no fold reads is dead as soon as its load is issued, and the compiler then reuses
 // its register while the load is in flight, which costs a vmcnt(0) wait in front of every step and so
 // drains the whole load pipeline.
-#ifndef TKV_AB_GROUP_SHUF  // (A/B builds: 1 = group lanes take their fifth granule from the next lane)
-#define TKV_AB_GROUP_SHUF 0
-#endif
-constexpr bool kGroupShuf = TKV_AB_GROUP_SHUF != 0;
-// The 16-lane list walk (blocks of 513-1024 bytes) takes it from the next lane in the product: in one
-// process +2.9 % on 513-1024-byte and +3.9 % on 300-1000-byte payloads; with 4- and 8-lane groups
-// the shuffle cost more than the loads it saved (-6.5 % and -4.5 %, profiles/r4/group_shuf/).
-#ifndef TKV_AB_GROUP16_SHUF
-#define TKV_AB_GROUP16_SHUF 1
-#endif
 template <int N>
 __device__ __forceinline__ void keep_live(const uint4 (&g)[N]) {
 #pragma unroll
@@ -914,10 +904,6 @@ __device__ __forceinline__ void crc_stream_body(const RowsArgs& a, std::uint32_t
 // ranges, slots 12-15 the smallest, matching the issue arbitration that favours a SIMD's older waves.
 // PRIO (0: off): set_prio_from_left<PRIO> once per DEPTH rows (the product uses 3, and SKEW 154 for
 // blocks of more than one row; tkv_crc32_kernels.hip).
-#ifndef TKV_AB_PACKED_EARLY  // (A/B builds: 0 = table fill first, then the first rows' loads)
-#define TKV_AB_PACKED_EARLY 1
-#endif
-constexpr bool kPackedEarly = TKV_AB_PACKED_EARLY != 0;
 template <int DEPTH, int ILP, bool R1, int SKEW = 0, int PRIO = 0>
 __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
@@ -996,19 +982,15 @@ __device__ __forceinline__ void crc_packed_body(const RowsArgs& a, std::uint32_t
     }
   };
 
-  // EARLY: the first rows' loads go out before the table fill, so the fill (table loads from L2, LDS
-  // writes, the barrier) overlaps their HBM latency instead of preceding it
-  if (kPackedEarly && nb != 0) {
+  // the first rows' loads go out before the table fill, so the fill (table loads from L2, LDS writes,
+  // the barrier) overlaps their HBM latency instead of preceding it (round 4, profiles/r4/packed_early/)
+  if (nb != 0) {
 #pragma unroll
     for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
   }
   fill_lds(a.tabs, lds);
   __syncthreads();
   if (nb == 0) return;
-  if (!kPackedEarly) {
-#pragma unroll
-    for (int s = 0; s < DEPTH - ILP; ++s) issue(s, buf[s]);
-  }
   for (std::uint32_t j = 0; j < nrows; j += DEPTH) {
     if constexpr (PRIO != 0) set_prio_from_left<PRIO>(nrows - j, nrows);
 #pragma unroll
@@ -1265,16 +1247,9 @@ __device__ __forceinline__ void crc_packed_small_gen_body(const RowsArgs& a, std
     const std::uintptr_t p = static_cast<std::uintptr_t>(static_cast<std::int64_t>(blo) + c_lane);
     const std::uintptr_t al = p & ~static_cast<std::uintptr_t>(15);
 #pragma unroll
-    for (int i = 0; i < (kGroupShuf ? kLaneGran - 1 : kLaneGran); ++i) {
+    for (int i = 0; i < kLaneGran; ++i) {
       const std::uintptr_t q = al + 16u * i;
       buf[slot][i] = gload16(live && q + 16u > blo && q < bhi ? q : dmy);
-    }
-    if constexpr (kGroupShuf) {  // the fifth granule: the group's last lane only (group_walk)
-      buf[slot][kLaneGran - 1] = make_uint4(0u, 0u, 0u, 0u);
-      if (gl == G - 1u) {
-        const std::uintptr_t q = al + 16u * (kLaneGran - 1);
-        buf[slot][kLaneGran - 1] = gload16(live && q + 16u > blo && q < bhi ? q : dmy);
-      }
     }
     o16[slot] = static_cast<std::uint32_t>(p & 15u);
   };
@@ -1315,15 +1290,6 @@ __device__ __forceinline__ void crc_packed_small_gen_body(const RowsArgs& a, std
       Reg p[ILP];
 #pragma unroll
       for (int i = 0; i < ILP; ++i) {
-        if constexpr (kGroupShuf) {
-          const int src = static_cast<int>(((lane + 1u) & 63u) * 4u);
-          const uint4 n0 = buf[q + i][0];
-          const uint4 nb = make_uint4(static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.x))),
-                                      static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.y))),
-                                      static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.z))),
-                                      static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(n0.w))));
-          if (gl != G - 1u) buf[q + i][kLaneGran - 1] = nb;
-        }
         lane_dwords<1>(buf[q + i], o16[q + i], d[i]);
         p[i] = Reg{0, 0};
       }
@@ -1717,37 +1683,19 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
     }
   };
   auto lds32 = [&](std::uint32_t byte) { return lds_at(lds, byte); };
-// Leaving the previous step's result store in flight at the step wait (vmcnt(KB + 1)) measured
-// neutral here (-2.1 to +1.0 % at 28-47 B, profiles/r4/storewait/lanes_probe.jsonl); the record check
-// kept it (+0.8 %). 0 = leave it in flight.
-#ifndef TKV_AB_LANES_LDS_STOREWAIT  // (A/B builds: 0 = the step wait leaves the previous store in flight)
-#define TKV_AB_LANES_LDS_STOREWAIT 1
-#endif
-#ifndef TKV_AB_LANES_LDS_NOPF  // (A/B builds: 1 = each step's copy issued and awaited at its fold)
-#define TKV_AB_LANES_LDS_NOPF 0
-#endif
-  if (!TKV_AB_LANES_LDS_NOPF) copy(0, buf0);
+  // One step's copy in flight while the previous one folds (issuing and awaiting each step's copy at
+  // its fold, or leaving the previous step's result store in flight at the wait, measured slower or
+  // neutral: profiles/r4/storewait/, profiles/r4/lanes_lds/).
+  copy(0, buf0);
   for (std::uint32_t j = 0; j < ns; ++j) {
     if constexpr (PRIO != 0) set_prio_from_left<PRIO>(ns - j, ns);
     const std::uint32_t cur = buf0 + (j & 1u) * kLanesLdsBuf;
-    if (TKV_AB_LANES_LDS_NOPF) {
-      copy(j, cur);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (j + 1u < ns) {
+    if (j + 1u < ns) {
       copy(j + 1u, buf0 + ((j + 1u) & 1u) * kLanesLdsBuf);
-      // step j's copy has landed; step j+1's KB copies stay in flight, and so does step j-1's result
-      // store (issued after step j's copy; vmcnt counts stores too, in issue order)
-      if (TKV_AB_LANES_LDS_STOREWAIT == 0 && j > 0u) {
-        if constexpr (KB == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else if constexpr (KB == 2) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        if constexpr (KB == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-        else if constexpr (KB == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      }
-    } else if (TKV_AB_LANES_LDS_STOREWAIT == 0 && j > 0u) {
-      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      // step j's copy has landed; step j+1's KB copies stay in flight (vmcnt counts in issue order)
+      if constexpr (KB == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else if constexpr (KB == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1792,14 +1740,8 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
 // measured below both one and three. (Earlier in round 4 three list steps had beaten two by
 // 0.7-1.6 %, profiles/r4/s12/; the lane phase and group passes spill at three.) 0 = no step ahead
 // (10-15 % slower for every walk, profiles/r4/lanes_r/nopf_probe.jsonl).
-#ifndef TKV_AB_WALK_AHEAD
-#define TKV_AB_WALK_AHEAD 1
-#endif
-#ifndef TKV_AB_LIST_AHEAD
-#define TKV_AB_LIST_AHEAD 1
-#endif
-constexpr int kWalkAhead = TKV_AB_WALK_AHEAD;
-constexpr int kListAhead = TKV_AB_LIST_AHEAD;
+constexpr int kWalkAhead = 1;
+constexpr int kListAhead = 1;
 static_assert(kWalkAhead >= 0 && kWalkAhead <= 3 && kListAhead >= 0 && kListAhead <= 3,
               "at most three steps ahead of a four-slot ring");
 
@@ -1890,7 +1832,10 @@ template <int G, bool LIST>
 __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_t* lds, std::uint32_t lo,
                                            std::uint32_t cnt) {
   static_assert(G == 4 || G == 8 || (LIST && G == 16), "4- or 8-lane groups (16 for listed blocks)");
-  constexpr bool kShuf = kGroupShuf || (G == 16 && TKV_AB_GROUP16_SHUF != 0);
+  // 16-lane groups take their fifth granule from the next lane: +2.9 % on 513-1024-byte and +3.9 % on
+  // 300-1000-byte payloads in one process; with 4- and 8-lane groups the shuffle cost more than the
+  // loads it saved (-6.5 %, -4.5 %; profiles/r4/group_shuf/)
+  constexpr bool kShuf = G == 16;
   constexpr int RING = 4;
   constexpr int kAhead = LIST ? kListAhead : kWalkAhead;  // steps of data in flight
   constexpr std::uint32_t kSlot = 64u * G;

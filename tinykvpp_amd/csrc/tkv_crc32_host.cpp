@@ -430,22 +430,8 @@ RowsArgs base_args(DevCtx* c, StreamScratch* s, int algo) {
   return a;
 }
 
-// Uniform batches with len <= lane_max() take crc_lanes: kLaneMax. An A/B build
-// (-DTKV_AB_LANE_MAX_ENV, tools/build_variant.sh) lets the environment variable TKV_LANE_MAX lower it
-// (-1 turns the kernel off) to measure against the kernels that served these lengths before; the
-// product library has no such knob, so its kernel choice depends on the batch alone.
-long long lane_max() {
-#ifdef TKV_AB_LANE_MAX_ENV
-  static const long long v = [] {
-    const char* e = std::getenv("TKV_LANE_MAX");
-    const long long x = e ? std::atoll(e) : static_cast<long long>(kLaneMax);
-    return std::max(-1LL, std::min<long long>(x, kLaneMax));
-  }();
-  return v;
-#else
-  return static_cast<long long>(kLaneMax);
-#endif
-}
+// Uniform batches with len <= lane_max() take crc_lanes: kLaneMax.
+long long lane_max() { return static_cast<long long>(kLaneMax); }
 
 // Uniform-length batch (also used for single spans).
 int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t stride, std::uint64_t len,

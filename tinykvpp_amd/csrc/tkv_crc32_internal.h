@@ -29,17 +29,6 @@ constexpr int kSeg = 64;                 // contiguous bytes one lane folds per 
 constexpr int kRow = 64 * kSeg;          // bytes one wave folds per row (4 KiB)
 constexpr int kWavesPerWG = 16;          // packed kernel: 1024-thread workgroups, one per CU (LDS-bound)
 constexpr int kThreads = 64 * kWavesPerWG;
-// A/B builds only (TKV_AB_LANES16=1): the uniform lane kernel's windows of up to 4 granules on the
-// 64 KiB 16-replica table image with two workgroups per CU (LaneShape in tkv_crc32_kernels.hip;
-// 1024 threads for windows of at most TKV_AB_LANES16_NARROW granules, 768 for wider ones). Measured
-// against the 128 KiB image with one 1024-thread workgroup per CU, in one process: within -5..+2 %
-// (profiles/r4/lanes16/), so the product keeps the 128 KiB image.
-#ifndef TKV_AB_LANES16
-#define TKV_AB_LANES16 0
-#endif
-#ifndef TKV_AB_LANES16_NARROW
-#define TKV_AB_LANES16_NARROW 3
-#endif
 constexpr int kRowsWavesPerWG = 12;      // generic row kernels: 768 threads (162 VGPRs at ILP 2)
 constexpr int kRowsThreads = 64 * kRowsWavesPerWG;
 
@@ -135,9 +124,6 @@ constexpr int kCountPhases = 9;
 // folds each class with groups of 4, 8 or 16 lanes.
 constexpr int kCountSmall4 = 10;
 constexpr int kCountSmall8 = 11;
-// counts[kCountTicket]: workgroups of the tile scan done so far (the last one scans the tile sums and
-// resets it to 0; zero when the scratch is allocated).
-constexpr int kCountTicket = 12;
 
 // Blocks of at most kLaneMax bytes are folded whole by one lane each, from their own initial register
 // (DESIGN.md §4.5): uniform batches by crc_lanes, irregular ones by the lane phase in crc_stream's
@@ -166,17 +152,11 @@ constexpr std::uint32_t kGroup8Max = 512;
 // group phase's own latency chain (descriptor, data, fold: ~10 us) would only add to the batch
 // (cfg4's general path: 1300 blocks of 255 bytes per tile, +1.2 % time with the group phase).
 constexpr std::uint32_t kLaneDenseTile = 256;
-#ifndef TKV_AB_GROUP_DENSE  // (A/B builds only: tools/build_at.sh -DTKV_AB_GROUP_DENSE=...)
-#define TKV_AB_GROUP_DENSE 3072
-#endif
-#ifndef TKV_AB_GROUP8_DENSE
-#define TKV_AB_GROUP8_DENSE 3968
-#endif
-constexpr std::uint32_t kGroupDenseTile = TKV_AB_GROUP_DENSE;
+constexpr std::uint32_t kGroupDenseTile = 3072;
 // A back-to-back tile with at least this many blocks of at most kSmallMax bytes and at most
 // kGroupTileRows rows of larger ones takes the general path, not stream mode (rows_tile_scan).
 constexpr std::uint32_t kStreamSmallTile = 1024;
-constexpr std::uint32_t kGroup8DenseTile = TKV_AB_GROUP8_DENSE;
+constexpr std::uint32_t kGroup8DenseTile = 3968;
 constexpr std::uint64_t kGroupTileRows = 1024;
 // Per-tile flags (tile_ok):
 constexpr std::uint32_t kTileStream = 1u;     // the tile's blocks qualify for stream mode

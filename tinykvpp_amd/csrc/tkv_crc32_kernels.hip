@@ -149,11 +149,7 @@ __global__ __launch_bounds__(kStreamThreads) void crc_stream(RowsArgs a) {
   const std::uint32_t g0 = dev::sload32(a.s_row0, wave), g1 = dev::sload32(a.s_row0, wave + 1);
   const std::uint32_t e0 = dev::sload32(a.wave_start, wave);
   const std::uint32_t e1 = wave + 1 < a.nwaves ? dev::sload32(a.wave_start, wave + 1) : a.nblocks;
-#ifdef TKV_PROBE_STREAM_SCALAR
-  const bool many = false;
-#else
   const bool many = g1 > g0 && e1 > e0 && e1 - e0 > 8u * (g1 - g0);
-#endif
   if (many) dev::crc_stream_body<3, true>(a, lds);
   else dev::crc_stream_body<3, false>(a, lds);
 }
@@ -186,17 +182,12 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small(RowsArgs a) {
 // General small uniform blocks (64 < len <= 2 KiB, any stride, alignment, initial registers):
 // DESIGN.md §4.4. G-lane groups, five granules per lane. DEPTH 4 spills here; DEPTH 2 / ILP 1 measured
 // 1-3 % faster than DEPTH 3 / ILP 1 in one process (profiles/r3/small_gen/ab_depth.jsonl).
-#ifndef TKV_GEN_DEPTH
-#define TKV_GEN_DEPTH 2
-#endif
-#ifndef TKV_GEN_ILP
-#define TKV_GEN_ILP 1
-#endif
-static_assert(TKV_GEN_ILP >= 1 && TKV_GEN_DEPTH >= TKV_GEN_ILP, "crc_packed_small_gen: DEPTH - ILP rows stay in flight");
+constexpr int kGenDepth = 2;
+constexpr int kGenIlp = 1;
 template <int G, bool INIT>
 __global__ __launch_bounds__(kThreads) void crc_packed_small_gen(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_small_gen_body<G, INIT, TKV_GEN_DEPTH, TKV_GEN_ILP, kPackedPrio>(a, lds);
+  dev::crc_packed_small_gen_body<G, INIT, kGenDepth, kGenIlp, kPackedPrio>(a, lds);
 }
 
 // Uniform batches of blocks of at most kLaneMax bytes (any stride, alignment, initial registers): one
@@ -204,49 +195,16 @@ __global__ __launch_bounds__(kThreads) void crc_packed_small_gen(RowsArgs a) {
 // NG 3, 5 at NG 4, 4 at NG 5, ILP 1. Only the slicing tables go to LDS (128 KiB).
 // In one process against the five-granule DEPTH 3-4 kernel of round 3 (profiles/r4/lanes_ab/):
 // 26 B 3544 -> 3825 GB/s, 16 B 3615 -> 3720, 28 B 3877 -> 4044, 36 B and 59 B unchanged.
-// Per window size: threads per workgroup, workgroups per CU and pipeline depth. Narrow windows fit
-// two 1024-thread workgroups per CU (8 waves per SIMD: at most 64 VGPRs), 4 granules two 768-thread
-// ones (6 waves: 80 VGPRs); 5 granules keep the 128 KiB image's shape (one 1024-thread workgroup,
-// DEPTH 4), whose window does not fit 80 registers deep enough.
-template <int NG>
-struct LaneShape {
-  static constexpr bool kW16 = TKV_AB_LANES16 && NG <= 4;
-  static constexpr unsigned kThreads = !kW16 ? 1024u : NG <= TKV_AB_LANES16_NARROW ? 1024u : 768u;
-  static constexpr unsigned kWgPerCu = kW16 ? 2u : 1u;
-  static constexpr int kDepth = !kW16 ? 4 : 3;
-};
-#if TKV_AB_LANES16
-template <int ALIGN, int NG>
-__global__ __launch_bounds__(LaneShape<NG>::kThreads)
-__attribute__((amdgpu_waves_per_eu(LaneShape<NG>::kWgPerCu * LaneShape<NG>::kThreads / 256))) void
-crc_lanes_n(RowsArgs a) {
-  if constexpr (LaneShape<NG>::kW16) {
-    __shared__ std::uint32_t lds[kLdsSliceWords / 2];
-    dev::crc_lanes_n_body<ALIGN, NG, LaneShape<NG>::kDepth, 1, kPackedPrio, 16>(a, lds);
-  } else {
-    __shared__ std::uint32_t lds[kLdsSliceWords];
-    dev::crc_lanes_n_body<ALIGN, NG, LaneShape<NG>::kDepth, 1, kPackedPrio>(a, lds);
-  }
-}
-#else
+// One 1024-thread workgroup per CU on the 128 KiB image (the 64 KiB 16-replica image with two
+// workgroups per CU measured within -5..+2 %, profiles/r4/lanes16/). 5-granule windows keep no step
+// in flight (+7-13 % at 52-60 B in one process against DEPTH 4, profiles/r4/lanes_r/nopf_probe.jsonl;
+// the right-aligned kernel measured the same, crc_lanes_r).
 template <int ALIGN, int NG>
 __global__ __launch_bounds__(kThreads) void crc_lanes_n(RowsArgs a) {
-#ifndef TKV_AB_LANES_DEPTH3  // (A/B builds only: the 3-granule window's depth)
-#define TKV_AB_LANES_DEPTH3 6
-#endif
-#ifndef TKV_AB_LANES_DEPTH4
-#define TKV_AB_LANES_DEPTH4 5
-#endif
-// 5-granule windows: no step in flight (+7-13 % at 52-60 B in one process against DEPTH 4,
-// profiles/r4/lanes_r/nopf_probe.jsonl; the right-aligned kernel measured the same, crc_lanes_r)
-#ifndef TKV_AB_LANES_DEPTH5
-#define TKV_AB_LANES_DEPTH5 1
-#endif
-  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? TKV_AB_LANES_DEPTH3 : NG == 4 ? TKV_AB_LANES_DEPTH4 : TKV_AB_LANES_DEPTH5;
+  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? 5 : 1;
   __shared__ std::uint32_t lds[kLdsSliceWords];
   dev::crc_lanes_n_body<ALIGN, NG, DEPTH, 1, kPackedPrio>(a, lds);
 }
-#endif
 
 // Uniform lane batches with the default initial register, right-aligned windows of NF whole dwords
 // (crc_lanes_r_body); ALIGN is the window start's alignment class.
@@ -257,16 +215,7 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_r(RowsArgs a) {
 // 5-granule windows load no step ahead of their fold: in one process against DEPTH 4 / 3 / 2
 // (profiles/r4/lanes_r/depth_probe.jsonl) 50-59 B ran 11-13 % faster with no step in flight and the
 // same with one to three; narrow windows (5-27 B) want their steps in flight (+2 to +20 %).
-#ifndef TKV_AB_R_DEPTH5  // (A/B builds only: steps of 5-granule windows in flight)
-#define TKV_AB_R_DEPTH5 1
-#endif
-#ifndef TKV_AB_R_DEPTH4
-#define TKV_AB_R_DEPTH4 5
-#endif
-#ifndef TKV_AB_R_DEPTH3
-#define TKV_AB_R_DEPTH3 6
-#endif
-  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? TKV_AB_R_DEPTH3 : NG == 4 ? TKV_AB_R_DEPTH4 : TKV_AB_R_DEPTH5;
+  constexpr int DEPTH = NG <= 2 ? 8 : NG == 3 ? 6 : NG == 4 ? 5 : 1;
   __shared__ std::uint32_t lds[kLdsSliceWords];
   dev::crc_lanes_r_body<ALIGN, NF, NG, DEPTH, kPackedPrio>(a, lds);
 }
@@ -340,8 +289,7 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
                                                               std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
                                                               std::uint32_t* lscan, std::uint32_t* tile_lanes,
                                                               std::uint32_t* cscan, std::uint64_t* tile_cls,
-                                                              std::uint32_t group_stream, std::uint32_t* counts,
-                                                              std::uint64_t* sinfo, std::uint32_t last_scans) {
+                                                              std::uint32_t group_stream) {
   constexpr unsigned kTileWaves = kTileThreads / 64;
   constexpr unsigned kTileBpt = kScanTile / kTileThreads;
   static_assert(kScanTile % kTileThreads == 0 && kTileWaves >= 1 && kTileBpt >= 4 && kTileBpt % 4 == 0,
@@ -500,32 +448,6 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     const std::uint32_t tc = cls_pair(ltot);
     tile_cls[blockIdx.x] = (tc & 0xFFFFu) | (static_cast<std::uint64_t>(tc >> 16) << 32);
   }
-  // last_scans (batches of at most kFusedTiles tiles): the workgroup that finishes last scans the tile
-  // sums for all (rows_scan_tiles_body), so the scatter that follows reads its tile's offsets instead
-  // of every workgroup summing all tile sums again. Each workgroup's tile records are released by a
-  // device-scope fence before its ticket; the last one acquires them by another fence.
-#if TKV_AB_LAST_SCANS
-  if constexpr (kTileThreads == 1024) {
-    if (last_scans) {  // (uniform)
-      __shared__ ScanLds L;
-      __shared__ std::uint32_t is_last;
-      __threadfence();
-      __syncthreads();
-      if (threadIdx.x == 0) is_last = atomicAdd(counts + kCountTicket, 1u) == gridDim.x - 1u ? 1u : 0u;
-      __syncthreads();
-      if (is_last) {
-        __threadfence();
-        rows_scan_tiles_body(L, tile_sums, tile_lanes, tile_cls, gridDim.x, n, counts, tile_ok, sbase, offsets,
-                             lengths, sinfo);
-        if (threadIdx.x == 0) counts[kCountTicket] = 0u;  // ready for the next batch on this stream
-      }
-    }
-  }
-#else
-  (void)counts;
-  (void)sinfo;
-  (void)last_scans;
-#endif
 }
 
 // Scan of the tile sums for batches of more than kFusedTiles tiles (one workgroup), with the
@@ -687,23 +609,15 @@ __global__ void rows_finish(const std::uint8_t* base, const std::uint64_t* offse
 // no single-workgroup tile-scan launch sits between the tile scan and the scatter. Workgroup 0
 // publishes counts for the row kernel.
 constexpr std::uint32_t kFusedTiles = 1024;
-// Batches of at most kFusedTiles tiles: every scatter workgroup sums the tile sums itself (the
-// product), or the tile scan's last workgroup scans them and the plain scatter follows
-// (TKV_AB_LAST_SCANS=1, A/B builds). The latter measured far slower in one process (300-1000 B gapped
-// 3041 -> 1934 GB/s, cfg4 -2 %, profiles/r4/s14/), most likely from the device-scope fence each
-// tile-scan workgroup needs before its ticket (on gfx950 it writes back the XCD's L2).
-#ifndef TKV_AB_LAST_SCANS
-#define TKV_AB_LAST_SCANS 0
-#endif
-// A 256-thread workgroup per 256 blocks, each re-reading all tile sums. One 1024-thread workgroup per
-// scan tile with 4 blocks per thread (TKV_AB_FINISH_PER=4) cuts those re-reads by 16 but measured
-// slower: 300-1000 B gapped 3210 -> 2929 GB/s, 257-512 B 3210 -> 2748 (profiles/r4/s7/): the scatter's
+// Batches of at most kFusedTiles tiles: every scatter workgroup sums the tile sums itself. (Letting
+// the tile scan's last workgroup scan them measured far slower in one process: 300-1000 B gapped
+// 3041 -> 1934 GB/s, cfg4 -2 %, profiles/r4/s14/, most likely from the device-scope fence each
+// tile-scan workgroup needs before its ticket.) A 256-thread workgroup per 256 blocks, each re-reading
+// all tile sums: one 1024-thread workgroup per scan tile with 4 blocks per thread cuts those re-reads
+// by 16 but measured slower (300-1000 B gapped 3210 -> 2929 GB/s, profiles/r4/s7/): the scatter's
 // latency, not the re-reads, is what the finish pays for.
-#ifndef TKV_AB_FINISH_PER  // (A/B builds only)
-#define TKV_AB_FINISH_PER 1
-#endif
-constexpr std::uint32_t kFinishPer = TKV_AB_FINISH_PER;
-constexpr std::uint32_t kFinishThreads = kFinishPer == 1 ? 256 : kScanTile / kFinishPer;
+constexpr std::uint32_t kFinishPer = 1;
+constexpr std::uint32_t kFinishThreads = 256;
 // Stream mode (every tile qualified): instead of the small/large lists, every block
 // gets its end E[b] in bytes from row 0 (the stream start rounded down to 16 bytes), and every
 // row-kernel wave the first block ending in or after its first row; counts = {0, 0, rows, 1} and
@@ -1053,23 +967,15 @@ hipError_t launch_packed_small_gen(const RowsArgs& a, unsigned grid, hipStream_t
 }
 
 // Uniform lane-block batch (a.len <= kLaneMax): ALIGN from the base pointer and the stride.
-#ifndef TKV_AB_LANES_LDS  // (A/B builds: 0 keeps every uniform lane batch on crc_lanes_n)
-#define TKV_AB_LANES_LDS 1
-#endif
 template <int ALIGN, int NG>
 void launch_lanes_shape(RowsArgs a, unsigned ncu, hipStream_t st) {
-  using S = LaneShape<NG>;
   const std::uint64_t steps = (static_cast<std::uint64_t>(a.nblocks) + 63u) / 64u;
-  const std::uint64_t waves = S::kThreads / 64u;
-  const std::uint64_t grid =
-      std::max<std::uint64_t>(1, std::min<std::uint64_t>(static_cast<std::uint64_t>(ncu) * S::kWgPerCu, (steps + waves - 1) / waves));
+  const std::uint64_t waves = kThreads / 64u;
+  const std::uint64_t grid = std::max<std::uint64_t>(1, std::min<std::uint64_t>(ncu, (steps + waves - 1) / waves));
   a.nwaves = static_cast<std::uint32_t>(grid * waves);
-  hipLaunchKernelGGL((crc_lanes_n<ALIGN, NG>), dim3(static_cast<unsigned>(grid)), dim3(S::kThreads), 0, st, a);
+  hipLaunchKernelGGL((crc_lanes_n<ALIGN, NG>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, st, a);
 }
 
-#ifndef TKV_AB_LANES_R  // (A/B builds: 0 keeps lengths that are not whole dwords on crc_lanes_n)
-#define TKV_AB_LANES_R 1
-#endif
 template <int ALIGN, int NF>
 void launch_lanes_r_nf(RowsArgs a, unsigned ncu, hipStream_t st) {
   const std::uint64_t steps = (static_cast<std::uint64_t>(a.nblocks) + 63u) / 64u;
@@ -1090,7 +996,7 @@ void launch_lanes_r(const RowsArgs& a, std::uint32_t nf, unsigned ncu, hipStream
 }
 
 // Uniform lane-block batch (a.len <= kLaneMax): ALIGN from the base pointer and the stride, the window
-// (NG granules) from the length; grid and waves from the window's LaneShape.
+// (NG granules) from the length.
 hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   if (a.len > kLaneMax) return hipErrorInvalidValue;
   const std::uintptr_t m = reinterpret_cast<std::uintptr_t>(a.base) | static_cast<std::uintptr_t>(a.stride);
@@ -1100,16 +1006,7 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   // (profiles/r4/lanes_r/): 59 B +8.6 %, 59 B at stride 67 +5.2 %, 26 B +0.1 %; lengths of whole
   // dwords (no Sarwate tail to save) measured 3 % slower at 16 and 48 B and keep crc_lanes_n.
   const std::uint32_t nf = (a.len + 3u) / 4u, lead = 4u * nf - a.len;
-  const bool lanes_r = TKV_AB_LANES_R != 0 && a.init_raw == nullptr && (lead != 0u || TKV_AB_LANES_R == 2);
-#if TKV_AB_LANES_R == 2  // (A/B builds: every length, ahead of the LDS-staged kernel too)
-  if (lanes_r) {
-    const int ralign = lead != 0u ? 1 : align;
-    if (ralign == 16) launch_lanes_r<16>(a, nf, ncu, st);
-    else if (ralign == 4) launch_lanes_r<4>(a, nf, ncu, st);
-    else launch_lanes_r<1>(a, nf, ncu, st);
-    return hipGetLastError();
-  }
-#endif
+  const bool lanes_r = a.init_raw == nullptr && lead != 0u;
   const std::uint32_t mis = align == 16 ? 0u : align == 4 ? 12u : 15u;  // worst start offset in a granule
   const std::uint32_t ng = std::max<std::uint32_t>(1u, (a.len + mis + 15u) / 16u);  // granules a block can touch
   // a step's bytes fit one 3 KiB LDS buffer (the last lane's block, its alignment slack and the
@@ -1117,7 +1014,7 @@ hipError_t launch_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   // In one process against crc_lanes_n (profiles/r4/lanes_lds/): 33 B +2.3 %, 36 B +0.7 %, 36 B at
   // base + 3 +5.3 %, 36 B stride 44 +1.3 %; 16-byte aligned blocks (no realignment to save) and blocks
   // under 28 bytes (a step copies more than it folds) measured slower and keep crc_lanes_n.
-  if (TKV_AB_LANES_LDS && a.init_raw == nullptr && align != 16 && a.len >= 28u && a.stride <= dev::kLanesLdsMaxStride &&
+  if (a.init_raw == nullptr && align != 16 && a.len >= 28u && a.stride <= dev::kLanesLdsMaxStride &&
       15u + 63u * a.stride + a.len + 8u <= dev::kLanesLdsBuf) {
     const std::uint64_t steps = (static_cast<std::uint64_t>(a.nblocks) + 63u) / 64u;
     const std::uint64_t waves = kThreads / 64u;
@@ -1176,19 +1073,15 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
   const std::uint64_t ntiles = prepass_tiles(n);
   const std::uint64_t nfused = (static_cast<std::uint64_t>(n) + kFinishThreads * kFinishPer - 1) / (kFinishThreads * kFinishPer);
   const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
-  const std::uint32_t last_scans = TKV_AB_LAST_SCANS && ntiles <= kFusedTiles ? 1u : 0u;
   if (ntiles <= kFusedTiles)
     hipLaunchKernelGGL(rows_tile_scan<1024>, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets,
                        lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
-                       group_stream, counts, sinfo, last_scans);
+                       group_stream);
   else
     hipLaunchKernelGGL(rows_tile_scan<512>, dim3(static_cast<unsigned>(ntiles)), dim3(512), 0, st, base, offsets,
                        lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
-                       group_stream, counts, sinfo, 0u);
-  if (last_scans) {
-    hipLaunchKernelGGL(rows_finish, dim3(static_cast<unsigned>(nfinish)), dim3(256), 0, st, base, offsets, lengths,
-                       n, scan, tile_sums, counts, tile_ok, o, W, out, ends, sinfo, Ws, row0);
-  } else if (ntiles <= kFusedTiles) {
+                       group_stream);
+  if (ntiles <= kFusedTiles) {
     hipLaunchKernelGGL((rows_finish_fused<kFinishThreads, kFinishPer>), dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
                        offsets, lengths, n, scan, tile_sums, tile_ok, static_cast<std::uint32_t>(ntiles), counts, o,
                        W, out, ends, sinfo, Ws, row0);

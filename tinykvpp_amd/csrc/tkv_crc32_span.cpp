@@ -105,10 +105,14 @@ int tkv_crc32c_update_fallback(int gpu_status, uint32_t raw_state, const void* d
   return update_fallback(0x82F63B78u, gpu_status, raw_state, data, len, out_raw);
 }
 
-void tkv_debug_update_counts(uint64_t out[3]) {
+void tkv_debug_update_counts(uint64_t out[2]) {
   out[0] = tkv::g_update_calls[0];
   out[1] = tkv::g_update_calls[1];
-  out[2] = tkv::g_update_calls[2];
+}
+
+size_t tkv_debug_update_counts_n(uint64_t* out, size_t n) {
+  for (size_t i = 0; i < n && i < 3; ++i) out[i] = tkv::g_update_calls[i];
+  return 3;
 }
 
 }  // extern "C"

@@ -1,40 +1,42 @@
 // WAL recovery verify on the device: the record_len chain walk of
-// wal_entry::decode (/root/reference/src/engine/wal.cpp:63-130) over a WAL image resident in HBM,
-// the CRC check of every record (wal.cpp:89-96) and the key/value bounds check (wal.cpp:118-121),
-// ending in the first corruption - without walking the chain on the host.
+// wal_entry::decode (/root/reference/src/engine/wal.cpp:63-130, driven by engine::create's recovery
+// loop, /root/reference/src/engine/engine.cpp:31-53) over a WAL image resident in HBM, the CRC check
+// of every record (wal.cpp:89-96) and the key/value bounds check (wal.cpp:118-121), ending in the first
+// corruption. The image is read from HBM once (round 5).
 //
-// The record chain is a linked list through the image (record i+1 starts 8 + record_len bytes after
-// record i), so it is walked speculatively in parallel and stitched exactly:
-//  1. wal_scan_head: the image is cut into pieces of kWalPiece bytes, and the first plausible header
-//     of every piece (one the reference encoder could have written, wal.cpp:19-61), searched from
-//     the piece's front, becomes its speculative start S_k; piece 0 starts at 0.
-//  2. wal_spec: one lane per piece walks the chain from S_k over the records that start in the
-//     piece (X_k = the first record start at or past the piece's end, or the header that broke),
-//     and checks them as it goes: key/value bounds, and the CRC of every payload of at most
-//     kWalLaneMax bytes folded by the lane itself (slicing-by-4 lookups into the engine's tables in
-//     LDS, the payload zero-padded in front to whole dwords). Larger records (at most two start in a
-//     piece) wait in the piece's slots for one CRC batch through the engine's irregular path.
-//  3. wal_jump: next(k) = the piece holding X_k. The true chain visits the pieces 0, next(0),
-//     next(next(0)), ...; pointer jumping (x4 per round) marks exactly those pieces in
-//     log4(#pieces) rounds, and wal_link hands every on-path piece its entry E = X of its predecessor.
-//  4. wal_count: an on-path piece whose entry is its speculative start keeps its speculative walk
-//     and checks; otherwise it walks again from E (and wal_recheck checks it again). Its speculative
-//     exit was right when the exact walk leaves at the same X (and breaks, or not, the same way).
-//     Entries are exact up to and including the first piece k* whose speculative exit was wrong (a
-//     corrupted record_len, or a fake header in a key or value that led the speculation astray):
-//     later pieces are dropped, and when no record up to k*'s exact exit fails, the next pass
-//     resumes there (a true record start) as a new image.
-//  5. one exclusive scan numbers the records; wal_gather turns each piece's first failing record
-//     into a record index and moves the big-record slots into a dense list for the CRC batch;
-//     wal_check_big checks those. The first bad record is an atomic minimum of record indices.
-// Every step reads the image in HBM; the host only reads back a few counters.
+// wal_sweep: every wave streams a contiguous chunk of the image, one region of kRegion bytes at a
+// time. Regions are loaded kAhead steps ahead into registers (coalesced 16-byte loads) and written
+// into the wave's LDS window together with the first kOver bytes of the next region, so a record that
+// starts in the region and has a payload of at most kLaneFold bytes lies wholly in the window. Per
+// region:
+//  1. walk: lane l owns the piece [rs + kPiece l, + kPiece). The lane holding the region's entry E
+//     (where the chain leaves the previous region) starts there; every later lane starts at the first
+//     plausible header of its piece (one the reference encoder could have written, wal.cpp:19-61),
+//     speculatively. Each lane walks the records that start in its piece (wal.cpp:63-87: at least 26
+//     bytes left, record_len + 8 within the image), all reads from LDS.
+//  2. link check: every lane with a start must be entered exactly where the previous such lane's walk
+//     left (one shuffle per lane). Where a link fails, the chain from the last good lane is followed
+//     exactly (the lane it lands in walks again from the landing point, the lanes it skips drop out),
+//     so the region's chain is exact given E. Its exit is the next region's entry.
+//  3. fold: the region's records are listed in chain order in LDS and folded one per lane from the
+//     window (slicing-by-4 into the engine's conflict-free LDS tables), compared with the stored CRC
+//     and checked for key/value bounds; the region keeps the index of its first bad record. Payloads
+//     longer than kLaneFold go to a global list that one irregular CRC batch checks afterwards.
+// The chunk's first region has no known entry: its wave takes the first plausible header it finds
+// (a region without one "searches" on). After a break the wave searches again.
+//
+// Exactness across chunks (wal_bounds, wal_sweep in fix-up mode): wherever a region's entry did not
+// come from its predecessor's exit in the same walk (chunk starts, search starts, fix-up starts),
+// the predecessor's exit must land exactly on the entry, with only searching regions (no chain)
+// between. A boundary that fails is walked again from the true exit by a fix-up wave, which stops as
+// soon as its exit meets a stored entry (the chains coincide from there) or at the next failing
+// boundary; the boundaries are checked again, and the first failing one moves forward every round.
+// Nothing leaves the device but a few result words, and no image is walked on the host.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
-#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -47,76 +49,72 @@
 namespace tkv {
 namespace {
 
-constexpr std::uint64_t kWalPiece = 2048;     // bytes of image per speculative walker
-constexpr std::uint64_t kWalMeta = 26;        // wal.hpp:21-27 kMetadataSize
-constexpr std::uint32_t kWalLaneMax = 1024;   // payloads up to this size are checked by their lane
+constexpr std::uint64_t kWalMeta = 26;          // wal.hpp:21-27 kMetadataSize
 constexpr std::uint64_t kNone = ~0ull;
-constexpr unsigned kScanThreads = 256;        // wal_scan_head: 8 lanes per piece, 8 pieces per wave
-constexpr unsigned kCheckThreads = 1024;      // wal_spec/wal_recheck
-// A/B builds only (TKV_AB_WAL16=1): wal_spec/wal_recheck on the 64 KiB 16-replica table image with two
-// workgroups per CU (32 waves, at most 64 VGPRs) where the 128 KiB image allows one: the walk is
-// latency-bound (8 or 4 waves per CU instead of 16 were 15 % and 66 % slower).
-#ifndef TKV_AB_WAL16
-#define TKV_AB_WAL16 0
+#ifndef TKV_X_REGION
+#define TKV_X_REGION 10240
 #endif
-constexpr unsigned kCheckWgPerCu = TKV_AB_WAL16 ? 2 : 1;
-constexpr unsigned kHres = 16;                // words of the pinned result block
+constexpr std::uint32_t kRegion = TKV_X_REGION;  // image bytes per region (one wave step)
+constexpr int kRows = kRegion / 1024;           // 1 KiB load rows per region
+constexpr std::uint32_t kPiece = kRegion / 64;  // bytes per lane piece
+constexpr std::uint32_t kOver = 256;            // bytes of the next region behind the window
+constexpr std::uint32_t kLaneFold = 240;        // payloads up to this long are folded by one lane from LDS
+constexpr std::uint32_t kWin = 16 + kRegion + kOver;  // window: the region's aligned start, region, overlap
+constexpr std::uint32_t kList = kRegion / 26 + 4;  // listed records per region (see the list step)
+constexpr std::uint32_t kWinBytes = (kWin + 2 * kList + 15) & ~15u;
+constexpr std::uint32_t kStore = kPiece / 26 + 2;  // starts a lane lists: its records up to the first tiny one
+constexpr std::uint32_t kSearchStep = 48;       // positions a lane tests per search step
+constexpr unsigned kSweepWaves = 8;             // waves per workgroup: the 64 KiB tables + 8 windows of LDS
+constexpr unsigned kSweepThreads = 64 * kSweepWaves;
+constexpr unsigned kHres = 16;                  // words of the pinned result block
+static_assert(kRegion % 1024 == 0 && kPiece % 16 == 0, "region = whole 1 KiB load rows");
+static_assert(kOver >= kLaneFold + 8 && kOver >= kWalMeta, "a lane-folded record ends inside the window");
+static_assert(kList * 26 >= kRegion + 26 * 2, "records of >= 26 bytes fit the list");
+static_assert(kLdsSliceWords * 2 + kSweepWaves * kWinBytes <= 163840, "LDS");
+static_assert(kStore <= 8, "list counts per lane < 16");
 
-struct WalArgs {
+// Region flags (low byte of fl[]; the region's version, bumped by every fix-up rewrite, above it).
+constexpr std::uint32_t kChain = 1;   // the region has chain state: E (entry, may lie past the region) and X
+constexpr std::uint32_t kSpec = 2;    // its entry came from a search (speculative)
+constexpr std::uint32_t kSearch = 4;  // no chain: the walk searched the region and found no header
+constexpr std::uint32_t kBroke = 8;   // the chain broke in the region, at X (wal.cpp:68-70, 80-87)
+constexpr std::uint32_t kEnd = 16;    // the chain reached the end of the image exactly (X == size)
+constexpr std::uint32_t kFix = 32;    // its entry came from a fix-up task (checked like kSpec)
+
+// Result words (device, u64): see wal_fin_*.
+enum : int { kResLongA = 0, kResIncons, kResP, kResQ, kResLidx, kResCnt, kResLongSeg, kResWords = 8 };
+
+struct SweepArgs {
   const std::uint8_t* w;
   std::uint64_t size;
-  std::uint32_t K;           // pieces
-  // per piece
-  std::uint64_t* S;          // speculative start (kNone: no plausible header)
-  std::uint64_t* X;          // exit of its speculative chain, or the start of the header that broke it
-  std::uint64_t* spec_cnt;   // records of the speculative chain: (all << 32) | (larger than kWalLaneMax)
-  std::uint32_t* next;       // piece of X (K: end of image, broken chain or no start)
-  std::uint8_t* broke;       // the speculative chain hit a header that does not fit (at X)
-  std::uint64_t* first_loc;  // first failing record of the piece's checked walk (local index, kNone)
-  std::uint64_t* first_pos;  // and its start
-  std::uint64_t* slot_off;   // two slots per piece: records larger than kWalLaneMax (payload offset,
-  std::uint32_t* slot_len;   //   length, stored CRC, local index)
-  std::uint32_t* slot_crc;
-  std::uint32_t* slot_loc;
-  std::uint32_t* Ja;         // pointer-jumping tables
-  std::uint32_t* Jb;
-  std::uint8_t* on;          // piece is on the true chain
-  std::uint8_t* recheck;     // entered off its speculative start: walked and checked again
-  std::uint64_t* entry;      // true entry point of an on-path piece
-  std::uint64_t* cnt;        // records of an on-path piece from its entry, packed as spec_cnt
-  std::uint64_t* base;       // exclusive scan of cnt: first record index (high), first big record (low)
-  std::uint64_t* Xe;         // exit of its exact walk from the entry (or the header that broke it)
-  std::uint8_t* Be;          // the exact walk broke
-  std::uint64_t* bad_at;     // index of the piece's first failing record
-  // per big record (dense, in record order)
-  std::uint64_t* big_off;
-  std::uint32_t* big_len;
-  std::uint64_t* big_idx;
-  std::uint32_t* big_crc;
-  std::uint32_t* got;        // engine CRC of each big payload (finalized)
-  const std::uint32_t* inj;  // inj[L] = Shift_L(0xFFFFFFFF), L <= kWalLaneMax: the init term
+  std::uintptr_t al0;         // w rounded down to 16 bytes
+  std::uintptr_t glast;       // the image's last 16-byte granule (loads past it are clamped there)
+  std::uint32_t o;            // w - al0
+  std::uint32_t nreg;
+  std::uint32_t nwaves;       // sweep: chunks; fix-up: tasks
+  std::uint32_t wsweep;       // the sweep's waves (segments of the long-payload list)
+  const std::uint32_t* t_begin;  // fix-up task: first region, limit (exclusive), entry
+  const std::uint32_t* t_limit;
+  const std::uint64_t* t_entry;
+  // per region
+  std::uint64_t* E;
+  std::uint64_t* X;
+  std::uint64_t* B;           // start of the region's first bad record (kNone)
+  std::uint32_t* cnt;         // chain records starting in the region
+  std::uint32_t* bidx;        // index of the first bad one among them
+  std::uint32_t* fl;
+  // records with payloads longer than kLaneFold (checked by a CRC batch)
+  std::uint64_t* l_off;
+  std::uint32_t* l_len;
+  std::uint32_t* l_crc;
+  std::uint32_t* l_reg;
+  std::uint32_t* l_meta;      // index in the region | version << 8
+  std::uint64_t l_cap;        // entries; sweep wave w owns [w * l_seg, (w + 1) * l_seg), the rest is
+  std::uint64_t l_seg;        //   taken by atomics (fix-ups, and sweep waves whose segment is full)
+  std::uint32_t* l_cnt;       // per sweep wave: entries in its segment
+  unsigned long long* res;
   const DeviceTables* tabs;
-  std::uint64_t* res;        // [0] first piece with a wrong speculative exit, [1] chain end and
-                             // [2] chain broke (from the path's last piece), [3] first bad record,
-                             // [4] its start, [5] pieces re-checked
 };
-
-// Little-endian u32 at byte p of the image, p + 4 <= size: dword loads aligned to the absolute
-// address, realigned with v_alignbyte. The second dword is read only when it starts inside the
-// image, so no load touches a dword past the image's last byte (nor a page past its allocation);
-// the first may start up to 3 bytes before w, inside the same aligned dword as w itself.
-__device__ __forceinline__ std::uint32_t ld32(const std::uint8_t* w, std::uint64_t p, std::uint64_t size) {
-  const std::uintptr_t q = reinterpret_cast<std::uintptr_t>(w) + p;
-  const std::uintptr_t a = q & ~static_cast<std::uintptr_t>(3);
-  const std::uintptr_t end = reinterpret_cast<std::uintptr_t>(w) + size;
-  const std::uint32_t lo = *reinterpret_cast<const std::uint32_t*>(a);
-  const std::uint32_t hi = (q & 3u) && a + 4 < end ? *reinterpret_cast<const std::uint32_t*>(a + 4) : 0u;
-  return __builtin_amdgcn_alignbyte(hi, lo, static_cast<std::uint32_t>(q & 3u));
-}
-
-__device__ __forceinline__ std::uint64_t gid() {
-  return blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
-}
 
 __device__ __forceinline__ std::uint32_t le1_bytes4(std::uint32_t d) {
   // 4-bit mask: bit i set iff byte i of d is 0 or 1
@@ -125,481 +123,619 @@ __device__ __forceinline__ std::uint32_t le1_bytes4(std::uint32_t d) {
   return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
 }
 
-// 1. The first plausible header of every piece, searched from the piece's front with an early exit.
-// A group of 8 lanes owns one piece and tests 224 positions per step. Lanes 0-6 each hold 32 bytes
-// (two 16-byte loads) and report their 32 positions; lane 7 only lends its bytes. A header at p has
-// its op and tombstone bytes (p+8, p+17) at 0 or 1 (wal.cpp:30-52): each lane marks which of its
-// bytes are 0 or 1 with byte-parallel arithmetic, takes its right neighbour's marks by a cross-lane
-// shift and so tests all 32 positions at once; only positions that pass get the full check
-// (record_len = 18 + klen + vlen, fitting the image; re-read through L1). The group moves on only
-// while no position of its piece passed. In a WAL of small records the first step finds the
-// header, so about 256 bytes of every 2 KiB piece are read; a piece inside a large value is scanned
-// whole. The earlier kernel scanned every position of the image in one coalesced pass: 1.11 ->
-// 0.85 ms on 1 GiB of 59-byte records, Zipf image unchanged (profiles/r2/wal_head_scan/). Each
-// piece has one owner, so the result is a plain store (S is preset to kNone; piece 0 starts at 0).
-constexpr unsigned kHeadLanes = 8;                   // lanes per piece
-constexpr unsigned kHeadChunks = 2 * (kHeadLanes - 1);  // 16-byte chunks reported per group and step
-__global__ __launch_bounds__(kScanThreads) void wal_scan_head(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
-  const std::uintptr_t w0 = reinterpret_cast<std::uintptr_t>(a.w);
-  const std::uintptr_t al = w0 & ~static_cast<std::uintptr_t>(15);
-  const std::uint64_t off0 = w0 - al;
-  const std::uintptr_t end = w0 + a.size;
-  const std::uint32_t lane = threadIdx.x & 63u, g = lane / kHeadLanes, i = lane % kHeadLanes;
-  const std::uint64_t k = k_lo + (gid() >> 6) * (64 / kHeadLanes) + g;
-  const std::uint64_t ps = k * kWalPiece;
-  // positions with a whole header inside the image and inside the piece: [ps, pe)
-  const std::uint64_t pe = a.size < kWalMeta ? 0 : std::min<std::uint64_t>(ps + kWalPiece, a.size - kWalMeta + 1);
-  bool active = k < k_hi && k != 0 && ps < pe;  // uniform within a group
-  const std::uint64_t tg = (ps + off0) / 16;   // the chunk holding ps
-  std::uint64_t found_at = kNone;
-  for (std::uint64_t step = 0; __ballot(active) != 0; ++step) {
-    const std::uint64_t t = tg + step * kHeadChunks + 2 * i;
-    const std::uintptr_t c0 = al + 16 * t;
-    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
-    if (active && c0 < end) v0 = *reinterpret_cast<const uint4*>(c0);
-    if (active && c0 + 16 < end) v1 = *reinterpret_cast<const uint4*>(c0 + 16);
-    const std::uint32_t f = le1_bytes4(v0.x) | le1_bytes4(v0.y) << 4 | le1_bytes4(v0.z) << 8 | le1_bytes4(v0.w) << 12 |
-                            le1_bytes4(v1.x) << 16 | le1_bytes4(v1.y) << 20 | le1_bytes4(v1.z) << 24 |
-                            le1_bytes4(v1.w) << 28;
-    const std::uint32_t f1 = static_cast<std::uint32_t>(__shfl_down(static_cast<int>(f), 1, 64));
-    const std::uint64_t F = f | static_cast<std::uint64_t>(f1) << 32;
-    std::uint32_t cand = static_cast<std::uint32_t>((F >> 8) & (F >> 17));  // bytes j+8, j+17 are 0/1
-    const std::int64_t p0 = static_cast<std::int64_t>(16 * t) - static_cast<std::int64_t>(off0);
-    const std::int64_t lo = static_cast<std::int64_t>(ps) - p0, hi = static_cast<std::int64_t>(pe) - 1 - p0;
-    if (!active || i + 1 == kHeadLanes || hi < 0 || lo > 31) {
-      cand = 0;
-    } else {
-      const std::uint32_t jlo = lo < 0 ? 0u : static_cast<std::uint32_t>(lo);
-      const std::uint32_t jhi = hi > 31 ? 31u : static_cast<std::uint32_t>(hi);
-      cand &= (jhi == 31u ? 0xFFFFFFFFu : (2u << jhi) - 1u) & ~((1u << jlo) - 1u);
-    }
-    std::uint64_t best = kNone;
-    while (cand) {
-      const int j = __builtin_ctz(cand);
-      const std::uint64_t p = static_cast<std::uint64_t>(p0 + j);
-      const std::uint64_t rlen = ld32(a.w, p, a.size), klen = ld32(a.w, p + 18, a.size), vlen = ld32(a.w, p + 22, a.size);
-      if (rlen == 18u + klen + vlen && rlen + 8 <= a.size - p) {
-        best = p;
-        break;
-      }
-      cand &= cand - 1;
-    }
-    // positions grow with the lane index inside a group: its first header is its lowest finder's
-    const std::uint64_t bal = __ballot(best != kNone);
-    const std::uint32_t gb = static_cast<std::uint32_t>(bal >> (g * kHeadLanes)) & ((1u << (kHeadLanes - 1)) - 1u);
-    const std::uint32_t src = g * kHeadLanes + (gb ? static_cast<std::uint32_t>(__builtin_ctz(gb)) : 0u);
-    const std::uint64_t first = __shfl(best, static_cast<int>(src), 64);
-    const std::int64_t next_p0 = static_cast<std::int64_t>(16 * (tg + (step + 1) * kHeadChunks)) - static_cast<std::int64_t>(off0);
-    if (active && gb) {
-      found_at = first;
-      active = false;
-    } else if (next_p0 >= static_cast<std::int64_t>(pe)) {
-      active = false;
-    }
-  }
-  if (i == 0 && found_at != kNone) a.S[k] = found_at;
+// Little-endian u32 at byte b of the window (dword-aligned reads, v_alignbyte).
+__device__ __forceinline__ std::uint32_t rd32(const std::uint8_t* win, std::uint32_t b) {
+  const std::uint32_t q = b & ~3u;
+  const std::uint32_t lo = *reinterpret_cast<const std::uint32_t*>(win + q);
+  const std::uint32_t hi = *reinterpret_cast<const std::uint32_t*>(win + q + 4);
+  return __builtin_amdgcn_alignbyte(hi, lo, b & 3u);
 }
 
-// One slicing-by-4 step of the lane's register over dword w (the engine's replicated LDS tables).
-__device__ __forceinline__ void wal_fold(const std::uint32_t* lds, dev::Reg& r, std::uint32_t w, const dev::LaneConst& kc) {
-  dev::slice4(lds, r, w, kc);
+__device__ __forceinline__ std::uint64_t shfl64(std::uint64_t v, std::uint32_t src) {
+  const std::uint32_t lo = static_cast<std::uint32_t>(__shfl(static_cast<int>(static_cast<std::uint32_t>(v)), static_cast<int>(src), 64));
+  const std::uint32_t hi = static_cast<std::uint32_t>(__shfl(static_cast<int>(static_cast<std::uint32_t>(v >> 32)), static_cast<int>(src), 64));
+  return (static_cast<std::uint64_t>(hi) << 32) | lo;
 }
 
-// CRC-32 (finalized) of the payload [q, q + L) in image bytes, L <= kWalLaneMax, folded by this
-// lane alone with slicing-by-4 lookups into the LDS tables; the init register enters as
-// inj[L] = Shift_L(0xFFFFFFFF) (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). The payload is read as the
-// 16-byte aligned granules that hold it, two at a time with the next two in flight: the bytes in
-// front of the payload in its first granule are zeroed (leading zeros leave an init-0 register at
-// 0), whole dwords are folded, and the last 0-3 bytes take Sarwate steps. A granule never crosses a
-// page, so reading the whole of one that holds payload bytes cannot fault. Each lane reads its own
-// part of the image, so a CU's lanes touch far more lines than its L1 holds; 16-byte reads take a
-// quarter of the requests of the dword reads they replace (profiles/r2/wal_pmc/).
-__device__ __forceinline__ std::uint32_t lane_crc(const std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
-                                                  std::uint64_t q, std::uint32_t L) {
-  if (L == 0) return 0u;  // crc32 of nothing
-  const std::uintptr_t s = reinterpret_cast<std::uintptr_t>(a.w) + q;
-  const std::uintptr_t g0 = s & ~static_cast<std::uintptr_t>(15);
-  const std::uint32_t h = static_cast<std::uint32_t>(s - g0);  // bytes in front, zeroed
-  const std::uint32_t span = h + L;
-  const std::uint32_t nd = span >> 2, tb = span & 3u;          // whole dwords, then tail bytes
-  const std::uint32_t glast = (span - 1u) >> 4;                 // last granule with payload bytes
-  auto G = [&](std::uint32_t m) { return *reinterpret_cast<const uint4*>(g0 + 16u * (m < glast ? m : glast)); };
-  auto mask = [&](std::uint32_t k) -> std::uint32_t {  // bytes of dword k at or after the payload start
-    const std::int32_t lead = static_cast<std::int32_t>(h) - static_cast<std::int32_t>(4u * k);
-    return lead <= 0 ? 0xFFFFFFFFu : (lead >= 4 ? 0u : 0xFFFFFFFFu << (8 * lead));
-  };
-  dev::Reg r{0, 0};
-  uint4 c0 = G(0), c1 = G(1);
-  // Granule pairs [m, m + 2): the first one masks the head dwords, the ones wholly inside the
-  // payload fold unguarded, the last one (<= 8 dwords left) is guarded and takes the tail bytes.
-  auto pair = [&](std::uint32_t m, const uint4& x0, const uint4& x1, bool head, bool guarded) {
-    const std::uint32_t d[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+// Exclusive prefix over the lanes of a value < 2^BITS, and its total (bit planes through ballots).
+template <int BITS>
+__device__ __forceinline__ std::uint32_t lane_prefix(std::uint32_t v, std::uint32_t* total) {
+  std::uint32_t pre = 0, tot = 0;
 #pragma unroll
-    for (std::uint32_t i = 0; i < 8; ++i) {
-      const std::uint32_t k = 4u * m + i;
-      const std::uint32_t w = head ? d[i] & mask(k) : d[i];
-      if (!guarded || k < nd) {
-        wal_fold(lds, r, w, kc);
-      } else if (k == nd && tb) {  // the last 1-3 bytes
-        std::uint32_t x = r.value(), b = w;
-        for (std::uint32_t t = 0; t < tb; ++t, b >>= 8) x = (x >> 8) ^ dev::lds_at(lds, (((x ^ b) & 0xFFu) << 8) | kc.L0);
-        r = dev::Reg{x, 0};
-      }
-    }
-  };
-  std::uint32_t m = 0;
-  for (; 4u * m + 8u <= nd; m += 2) {  // pairs whose 8 dwords are all whole payload dwords
-    const uint4 n0 = G(m + 2), n1 = G(m + 3);  // the next two granules, in flight
-    if (m == 0) pair(0, c0, c1, true, false);
-    else pair(m, c0, c1, false, false);
-    c0 = n0;
-    c1 = n1;
+  for (int bit = 0; bit < BITS; ++bit) {
+    const std::uint64_t m = __ballot((v >> bit) & 1u);
+    pre += static_cast<std::uint32_t>(__builtin_amdgcn_mbcnt_hi(static_cast<std::uint32_t>(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<std::uint32_t>(m), 0u)))
+           << bit;
+    tot += static_cast<std::uint32_t>(__builtin_popcountll(m)) << bit;
   }
-  pair(m, c0, c1, m == 0, true);  // the last 0-7 whole dwords and the tail bytes
-  return r.value() ^ a.inj[L] ^ 0xFFFFFFFFu;
+  *total = tot;
+  return pre;
 }
 
-// Slicing tables into LDS (the row kernels' lane-shift tables are not needed here).
-__device__ __forceinline__ void fill_slices(const DeviceTables* tabs, std::uint32_t* lds) {
-  if constexpr (TKV_AB_WAL16) {
-    dev::fill_lds_slicing16(tabs, lds);
-  } else {
-    for (std::uint32_t u = threadIdx.x; u < 1024u; u += blockDim.x) {
-      const std::uint32_t pair = u >> 9, e = (u >> 1) & 255u, tt = u & 1u;
-      const std::uint32_t v = tabs->slice[2 * pair + tt][e];
-      uint4* dst = reinterpret_cast<uint4*>(lds + pair * 16384u + e * 64u + tt * 32u);
+__device__ __forceinline__ std::uint32_t wave_min_u32(std::uint32_t v) {
 #pragma unroll
-      for (std::uint32_t k = 0; k < 8u; ++k) dst[(k + u) & 7u] = make_uint4(v, v, v, v);
-    }
-  }
-  __syncthreads();
+  for (int m = 32; m > 0; m >>= 1) v = std::min<std::uint32_t>(v, static_cast<std::uint32_t>(__shfl_xor(static_cast<int>(v), m, 64)));
+  return v;
 }
 
-// The header fields of the record at p (p + 26 <= size): record_len, the stored CRC, key and value
-// lengths (wal.cpp:14-18). header_load issues two dword-aligned 16-byte loads over [p & ~3, + 32),
-// so the walk can put the next record's header in flight before it folds the current payload;
-// header_fields realigns the fields in registers. Within 32 bytes of the image's end (where those
-// loads could cross into the next page) nothing is loaded and the fields are read as dwords.
-struct HdrRaw {
-  uint4 u, v;
+// The first plausible header in [ps, qe) (qe - ps <= kSearchStep; every position there has 26 bytes
+// in the image): op and tombstone bytes (p+8, p+17) 0 or 1, then record_len = 18 + klen + vlen and
+// record_len + 8 within the image. The 0/1 marks of 80 window bytes from ps + 8 are computed
+// byte-parallel from five 16-byte reads; only positions that pass them are checked in full.
+__device__ __forceinline__ std::uint64_t search_piece(const std::uint8_t* win, std::uint64_t rs, std::uint32_t o,
+                                                      std::uint64_t ps, std::uint64_t qe, std::uint64_t size) {
+  if (ps >= qe) return kNone;
+  const std::uint32_t b0 = static_cast<std::uint32_t>(ps - rs) + o + 8u;
+  const std::uint32_t a16 = b0 & ~15u, sh = b0 & 15u;
+  const uint4* g = reinterpret_cast<const uint4*>(win + a16);
+  std::uint64_t m0 = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint4 v = g[i];
+    const std::uint32_t m = le1_bytes4(v.x) | le1_bytes4(v.y) << 4 | le1_bytes4(v.z) << 8 | le1_bytes4(v.w) << 12;
+    m0 |= static_cast<std::uint64_t>(m) << (16 * i);
+  }
+  const uint4 v4 = g[4];
+  const std::uint32_t m1 = le1_bytes4(v4.x) | le1_bytes4(v4.y) << 4 | le1_bytes4(v4.z) << 8 | le1_bytes4(v4.w) << 12;
+  const std::uint64_t M = sh ? (m0 >> sh) | (static_cast<std::uint64_t>(m1) << (64u - sh)) : m0;
+  const std::uint32_t span = static_cast<std::uint32_t>(qe - ps);  // <= kSearchStep < 64
+  std::uint64_t cand = M & (M >> 9) & ((1ull << span) - 1ull);
+  while (cand) {
+    const std::uint32_t i = static_cast<std::uint32_t>(__builtin_ctzll(cand));
+    const std::uint32_t b = b0 - 8u + i;
+    const std::uint64_t rl = rd32(win, b), kl = rd32(win, b + 18u), vl = rd32(win, b + 22u);
+    const std::uint64_t q = ps + i;
+    if (rl == 18u + kl + vl && rl + 8u <= size - q) return q;
+    cand &= cand - 1ull;
+  }
+  return kNone;
+}
+
+// The records that start in [s, pe) from s (wal.cpp:63-87), read from the window. n: their count;
+// st[j]: the offsets from rs of the first kStore; x: the first record start at or past pe, or where
+// the chain broke (broke); tiny: the index of the first with record_len < 18 (bad for certain: its
+// key/value fields cannot fit, wal.cpp:118-121), kStore if none among the stored ones. The records in
+// front of a lane's first tiny one are at least 26 bytes long, so it is always among the stored.
+struct Walk {
+  std::uint32_t st[kStore];
+  std::uint32_t n, tiny;
+  std::uint64_t x;
+  bool broke;
 };
-__device__ __forceinline__ bool header_window_ok(const WalArgs& a, std::uint64_t p) {
-  const std::uintptr_t b = (reinterpret_cast<std::uintptr_t>(a.w) + p) & ~static_cast<std::uintptr_t>(3);
-  return b + 32 <= reinterpret_cast<std::uintptr_t>(a.w) + a.size;
-}
-__device__ __forceinline__ HdrRaw header_load(const WalArgs& a, std::uint64_t p) {
-  HdrRaw h{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-  if (header_window_ok(a, p)) {
-    const std::uintptr_t b = (reinterpret_cast<std::uintptr_t>(a.w) + p) & ~static_cast<std::uintptr_t>(3);
-    h.u = *reinterpret_cast<const uint4*>(b);
-    h.v = *reinterpret_cast<const uint4*>(b + 16);
+__device__ __forceinline__ void walk_piece(const std::uint8_t* win, std::uint64_t rs, std::uint32_t o, std::uint64_t s,
+                                           std::uint64_t pe, std::uint64_t size, bool go, Walk& wk) {
+  std::uint64_t p = s;
+  bool act = go && s != kNone;
+  if (go) {
+    wk.n = 0;
+    wk.tiny = kStore;
+    wk.broke = false;
   }
-  return h;
-}
-__device__ __forceinline__ void header_fields(const WalArgs& a, std::uint64_t p, const HdrRaw& h, std::uint32_t* rlen,
-                                              std::uint32_t* stored, std::uint64_t* klen, std::uint64_t* vlen) {
-  if (!header_window_ok(a, p)) {
-    *rlen = ld32(a.w, p, a.size);
-    *stored = ld32(a.w, p + 4, a.size);
-    *klen = ld32(a.w, p + 18, a.size);
-    *vlen = ld32(a.w, p + 22, a.size);
-    return;
-  }
-  const std::uint32_t t = static_cast<std::uint32_t>((reinterpret_cast<std::uintptr_t>(a.w) + p) & 3u);
-  const std::uint32_t d[8] = {h.u.x, h.u.y, h.u.z, h.u.w, h.v.x, h.v.y, h.v.z, h.v.w};
-  auto at = [&](std::uint32_t lo, std::uint32_t hi) { return t ? __builtin_amdgcn_alignbyte(hi, lo, t) : lo; };
-  *rlen = at(d[0], d[1]);
-  *stored = at(d[1], d[2]);
-  // bytes p+18.. and p+22.. start in dword (t + 18) / 4 = 4 or 5 and (t + 22) / 4 = 5 or 6 of the
-  // window, at byte (t + 2) & 3 of it
-  const bool up = t >= 2u;
-  const std::uint32_t o = (t + 2u) & 3u;
-  auto at2 = [&](std::uint32_t lo, std::uint32_t hi) { return o ? __builtin_amdgcn_alignbyte(hi, lo, o) : lo; };
-  *klen = up ? at2(d[5], d[6]) : at2(d[4], d[5]);
-  *vlen = up ? at2(d[6], d[7]) : at2(d[5], d[6]);
-}
-
-// Walk piece k from `start` over the records that start in the piece (wal.cpp:63-87: header size,
-// then record_len against what is left) and check each one: key/value bounds (wal.cpp:118-121) and,
-// for payloads up to kWalLaneMax bytes, the CRC (wal.cpp:89-96) in this lane. Larger records (at most
-// two start in a piece) are kept in the piece's two slots for the CRC batch. Writes the piece's exit,
-// break, counts, first failing record (local index) and slots.
-__device__ __forceinline__ void walk_check(const std::uint32_t* lds, const dev::LaneConst& kc, const WalArgs& a,
-                                           std::uint64_t k, std::uint64_t start, std::uint64_t* exit_out,
-                                           std::uint8_t* broke_out, std::uint64_t* cnt_out) {
-  const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
-  std::uint64_t p = start, n_all = 0, n_big = 0, first = kNone, first_pos = 0;
-  bool bad_hdr = false;
-  HdrRaw h = header_load(a, p);
-  while (p < limit) {
-    if (a.size - p < kWalMeta) {
-      bad_hdr = true;
-      break;
-    }
-    std::uint32_t rlen, stored;
-    std::uint64_t klen, vlen;
-    header_fields(a, p, h, &rlen, &stored, &klen, &vlen);
-    if (static_cast<std::uint64_t>(rlen) + 8 > a.size - p) {
-      bad_hdr = true;
-      break;
-    }
-    const std::uint64_t np = p + 8 + static_cast<std::uint64_t>(rlen);
-    if (np < limit && a.size - np >= kWalMeta) h = header_load(a, np);  // next header in flight during the fold
-    bool bad = kWalMeta + klen + vlen > 8ull + rlen;
-    if (rlen <= kWalLaneMax) {
-      bad = bad || lane_crc(lds, kc, a, p + 8, rlen) != stored;
+  auto step = [&](std::uint32_t j, bool store) {
+    if (size - p < kWalMeta) {
+      wk.broke = true;
+      act = false;
     } else {
-      const std::uint64_t sl = 2 * k + (n_big & 1u);
-      a.slot_off[sl] = p + 8;
-      a.slot_len[sl] = rlen;
-      a.slot_crc[sl] = stored;
-      a.slot_loc[sl] = static_cast<std::uint32_t>(n_all);
-      ++n_big;
+      const std::uint32_t rl = rd32(win, static_cast<std::uint32_t>(p - rs) + o);
+      if (static_cast<std::uint64_t>(rl) + 8u > size - p) {
+        wk.broke = true;
+        act = false;
+      } else {
+        if (store) {
+          wk.st[j] = static_cast<std::uint32_t>(p - rs);
+          if (rl < 18u && wk.tiny == kStore) wk.tiny = j;
+        }
+        wk.n += 1;
+        p += 8u + static_cast<std::uint64_t>(rl);
+      }
     }
-    if (bad && first == kNone) {
-      first = n_all;
-      first_pos = p;
+  };
+  bool more = true;
+#pragma unroll
+  for (std::uint32_t j = 0; j < kStore; ++j) {
+    act = act && p < pe && p < size;  // (the chain ends where the image does: wal.cpp:63)
+    if (__ballot(act) == 0) {
+      more = false;
+      break;
     }
-    ++n_all;
-    p = np;
+    if (act) step(j, true);
   }
-  *exit_out = p;
-  *broke_out = bad_hdr ? 1 : 0;
-  *cnt_out = (n_all << 32) | n_big;
-  a.first_loc[k] = first;
-  a.first_pos[k] = first_pos;
-}
-
-// 2. Speculative walk and check of pieces [k_lo, k_hi) from their first plausible header (piece 0
-// from 0).
-__global__ __launch_bounds__(kCheckThreads) __attribute__((amdgpu_waves_per_eu(kCheckWgPerCu * kCheckThreads / 256))) void
-wal_spec(WalArgs a, std::uint64_t k_lo, std::uint64_t k_hi) {
-  __shared__ std::uint32_t lds[TKV_AB_WAL16 ? kLdsSliceWords / 2 : kLdsSliceWords];
-  fill_slices(a.tabs, lds);
-  const std::uint64_t k = k_lo + gid();
-  if (k >= k_hi) return;
-  const std::uint64_t s = k == 0 ? 0 : a.S[k];
-  if (k == 0) a.S[0] = 0;
-  if (s == kNone) {
-    a.X[k] = kNone;
-    a.next[k] = a.K;
-    a.broke[k] = 0;
-    a.spec_cnt[k] = 0;
-    a.first_loc[k] = kNone;
-    return;
+  // records past the stored ones (a chain of tiny records): walked, counted, not listed
+  while (more) {
+    act = act && p < pe && p < size;
+    if (__ballot(act) == 0) break;
+    if (act) step(0, false);
   }
-  const dev::LaneConst kc = TKV_AB_WAL16 ? dev::lane_const16(threadIdx.x & 63u) : dev::lane_const(threadIdx.x & 63u);
-  std::uint64_t x, c;
-  std::uint8_t br;
-  walk_check(lds, kc, a, k, s, &x, &br, &c);
-  a.X[k] = x;
-  a.broke[k] = br;
-  a.spec_cnt[k] = c;
-  a.next[k] = (br || x >= a.size) ? a.K : static_cast<std::uint32_t>(x / kWalPiece);
+  if (go) wk.x = p;
 }
 
-__global__ void wal_jump_init(WalArgs a) {
-  const std::uint64_t k = gid();
-  if (k >= a.K) return;
-  a.Ja[k] = a.next[k];
-  a.on[k] = k == 0 ? 1 : 0;
-  a.recheck[k] = 0;
-  a.bad_at[k] = kNone;
+// CRC-32 register (init 0xFFFFFFFF, not finalized) of the L window bytes at b, folded by this lane:
+// 64-byte chunks realigned from five 16-byte reads, slicing-by-4 lookups, Sarwate steps for the
+// last 1-3 bytes (crc32.cpp:9-16).
+__device__ __forceinline__ std::uint32_t fold_win(const std::uint8_t* win, const std::uint32_t* tab, const dev::LaneConst& kc,
+                                                  std::uint32_t b, std::uint32_t L) {
+  dev::Reg r{0xFFFFFFFFu, 0u};
+  const std::uint32_t nf = L >> 2, tb = L & 3u;
+  const std::uint32_t a = b & ~15u, o = b & 15u;
+  const std::uint32_t nch = (L + 63u) >> 6;
+  for (std::uint32_t c = 0; __ballot(c < nch) != 0; ++c) {
+    if (c < nch) {
+      uint4 g[dev::kLaneGran];
+#pragma unroll
+      for (int i = 0; i < dev::kLaneGran; ++i) g[i] = *reinterpret_cast<const uint4*>(win + a + 64u * c + 16u * i);
+      std::uint32_t d[16];
+      dev::lane_dwords<1>(g, o, d);
+#pragma unroll
+      for (std::uint32_t k = 0; k < 16; ++k) {
+        const std::uint32_t idx = 16u * c + k;
+        if (idx < nf) dev::slice4(tab, r, d[k], kc);
+        else if (idx == nf && tb != 0u) r = dev::Reg{dev::sarwate_bytes(tab, kc, r.value(), d[k], tb), 0u};
+      }
+    }
+  }
+  return r.value();
 }
 
-// 3 (fast path). Takes every piece with a speculative start (S != kNone) as on the true chain and
-// entered at S, and checks that this holds: each such piece p must leave exactly into the next such
-// piece q (next(p) == q and X_p == S_q), and the last one must end the chain (next == K). Piece 0
-// is entered at 0, so by induction every such piece is then entered at S, and a piece with no
-// plausible header holds no record start of the chain (a header the encoder wrote is plausible; a
-// chain that reaches an implausible one breaks there, and next(p) == K contradicts a later piece
-// with a start). Pieces further than kFastScan pieces from the next start fail the check. When it
-// fails (res[6] = 1) the host runs the pointer-jumping stitch instead. Replaces wal_jump_init,
-// ceil(log4 K) wal_jump launches and wal_link on every image whose speculation was right.
-constexpr std::uint32_t kFastScan = 64;
-__global__ void wal_fast(WalArgs a) {
-  const std::uint64_t k = gid();
-  if (k >= a.K) return;
-  const std::uint64_t s = a.S[k];
-  const bool has = k == 0 || s != kNone;
-  a.on[k] = has ? 1 : 0;
-  a.entry[k] = k == 0 ? 0 : s;
-  a.recheck[k] = 0;
-  a.bad_at[k] = kNone;
-  if (!has) return;
-  std::uint64_t q = k + 1;
-  while (q < a.K && q - k <= kFastScan && a.S[q] == kNone) ++q;
-  bool ok;
-  if (q >= a.K) ok = a.next[k] >= a.K;
-  else ok = q - k <= kFastScan && a.next[k] == q && a.X[k] == a.S[q];
-  if (!ok) a.res[6] = 1;
-}
+#ifndef TKV_X_BODY
+#define TKV_X_BODY 4
+#endif
+#ifndef TKV_X_AHEAD
+#define TKV_X_AHEAD 2
+#endif
+constexpr int kAhead = TKV_X_BODY == 0 ? 4 : TKV_X_AHEAD;  // regions in registers: the current one and the rest in flight
 
-// Result words (res[0..6]) and the record scan's last entries into the host's pinned block.
-__global__ void wal_publish(WalArgs a, std::uint64_t* h) {
-  const unsigned i = threadIdx.x;
-  if (i < 7) h[i] = a.res[i];
-  if (i == 7) h[7] = a.base[a.K - 1];
-  if (i == 8) h[8] = a.cnt[a.K - 1];
-}
-
-// 3. One quadrupling round (J = next^(4^t)): every marked k marks J(k), J(J(k)) and J(J(J(k))), then
-// J <- J o J o J o J. After round t the marks hold next^i(0) for every i < 4^(t+1), so
-// ceil(log4 K) rounds mark the whole path: half the launches of doubling, for two more dependent
-// loads per round. Marks set during the round by other threads are pieces of the true path too,
-// so reading them early is safe. K is the end of the path.
-__global__ void wal_jump(const std::uint32_t* J, std::uint32_t* J2, std::uint8_t* on, std::uint32_t K) {
-  const std::uint64_t k = gid();
-  if (k >= K) return;
-  const std::uint32_t j1 = J[k];
-  const std::uint32_t j2 = j1 < K ? J[j1] : K;
-  const std::uint32_t j3 = j2 < K ? J[j2] : K;
-  J2[k] = j3 < K ? J[j3] : K;
-  if (on[k]) {
-    if (j1 < K) on[j1] = 1;
-    if (j2 < K) on[j2] = 1;
-    if (j3 < K) on[j3] = 1;
+// Region r's granules: 1 KiB load rows k = 0..kRows-1, lane l's 16 bytes at row offset 16 l. Rows
+// past `rows` (regions the wave will not write into its window) read the image's last granule
+// instead, one line for the whole wave: every load is issued, so the compiler counts them exactly.
+__device__ __forceinline__ void load_region(const SweepArgs& a, std::uint64_t r, std::uint32_t lane, int rows, uint4 (&g)[kRows]) {
+  const std::uintptr_t base = a.al0 + r * kRegion + 16u * lane;
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    const std::uintptr_t p = base + 1024u * k;
+    g[k] = dev::gload16(k < rows && p < a.glast ? p : a.glast);
   }
 }
 
-// Entry points: each on-path piece hands its exit to the piece that holds it (one writer each:
-// the path is a simple chain).
-__global__ void wal_link(WalArgs a) {
-  const std::uint64_t k = gid();
-  if (k >= a.K || !a.on[k]) return;
-  if (k == 0) a.entry[0] = 0;
-  const std::uint32_t n = a.next[k];
-  if (n < a.K) a.entry[n] = a.X[k];
+// One wave: regions [r0, limit) from entry e (kNone: search). Fix-up mode stops where the exit meets
+// the stored entry of the next region. No global load in the loop waits for a value except in fix-up
+// mode (a wait on a load drains every prefetch issued before it).
+template <bool FIXUP>
+__device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win, std::uint16_t* list, const std::uint32_t* tab,
+                           std::uint32_t r0, std::uint32_t limit, std::uint64_t e, std::uint32_t wave) {
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const dev::LaneConst kc = dev::lane_const16(lane);
+  const std::uint64_t size = a.size;
+  const std::uint32_t o = a.o;
+  // the last region whose granules this wave writes into its window: limit (the overlap of limit - 1)
+  const std::uint32_t rlast = limit;
+  uint4 buf[kAhead][kRows];
+  auto rows_of = [&](std::uint64_t r) -> int { return r < rlast ? kRows : r == rlast ? 1 : 0; };
+#pragma unroll
+  for (int k = 0; k < kAhead; ++k) load_region(a, static_cast<std::uint64_t>(r0) + k, lane, rows_of(static_cast<std::uint64_t>(r0) + k), buf[k]);
+  std::uint32_t spec_next = e == kNone ? kSpec : (FIXUP ? kFix : 0u);  // flags the next entry carries
+  std::uint64_t nlong = 0;  // long payloads listed in this wave's segment
+  // window <- region rr and the head of rr + 1; the buffer refilled with region rr + kAhead
+  auto put = [&](std::uint32_t rr, uint4 (&cur)[kRows], const uint4& head) {
+#pragma unroll
+    for (int j = 0; j < kRows; ++j) *reinterpret_cast<uint4*>(win + 1024u * j + 16u * lane) = cur[j];
+    if (lane < (16u + kOver) / 16u) *reinterpret_cast<uint4*>(win + kRegion + 16u * lane) = head;
+    const std::uint64_t nxt = static_cast<std::uint64_t>(rr) + kAhead;
+    load_region(a, nxt, lane, rows_of(nxt), cur);
+  };
+  // the region body: true when the wave stops (fix-up converged)
+  auto body = [&](std::uint32_t rr) -> bool {
+    {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+
+      const std::uint64_t rs = static_cast<std::uint64_t>(rr) * kRegion;
+      const std::uint64_t re = rs + kRegion;
+      std::uint32_t ver = 0;
+      if constexpr (FIXUP) ver = (a.fl[rr] >> 8) + 1u;
+      // ---- 1. starts ------------------------------------------------------------------------------
+      const std::uint64_t ps = rs + static_cast<std::uint64_t>(kPiece) * lane, pe = ps + kPiece;
+      const bool exact = e != kNone;
+      std::uint32_t flags;
+      std::uint64_t Er = e, Xout = e;
+      std::uint32_t count = 0, bad_k = 0xFFFFFFFFu;
+      std::uint64_t Bpos = kNone;
+      if (exact && (e >= re || e >= size)) {
+        flags = kChain | spec_next;  // inside a record, or past the chain's end: no starts here
+      } else {
+        const std::uint32_t le = exact ? static_cast<std::uint32_t>((e - rs) / kPiece) : 0u;
+        std::uint64_t s = kNone;
+        if (exact && lane == le) s = e;
+        // the piece's first plausible header, kSearchStep positions at a time from its front (the first
+        // step finds it in a WAL of small records; a piece inside a long payload is searched whole)
+        const std::uint64_t qend = size >= kWalMeta ? std::min<std::uint64_t>(pe, size - kWalMeta + 1u) : 0u;
+        bool hunt = (!exact || lane > le) && ps < qend;
+        for (std::uint64_t q0 = ps; __ballot(hunt) != 0; q0 += kSearchStep) {
+          if (hunt) {
+            s = search_piece(win, rs, o, q0, std::min<std::uint64_t>(q0 + kSearchStep, qend), size);
+            hunt = s == kNone && q0 + kSearchStep < qend;
+          }
+        }
+        Walk wk;
+        walk_piece(win, rs, o, s, pe, size, true, wk);
+        // ---- 2. link check ---------------------------------------------------------------------------
+        std::uint64_t C = __ballot(s != kNone);
+        const std::uint32_t f = exact ? le : (C ? static_cast<std::uint32_t>(__builtin_ctzll(C)) : 64u);
+        if (f == 64u) {
+          flags = kSearch;
+          Er = Xout = kNone;
+        } else {
+          C &= ~((1ull << f) - 1ull);
+          std::uint32_t cur = f;
+          for (;;) {
+            const std::uint64_t below = C & ((1ull << lane) - 1ull);
+            const std::uint32_t prev = below ? 63u - static_cast<std::uint32_t>(__builtin_clzll(below)) : lane;
+            const std::uint64_t xp = shfl64(wk.x, prev);
+            const bool bp = __shfl(static_cast<int>(wk.broke), static_cast<int>(prev), 64) != 0;
+            const bool mine = ((C >> lane) & 1ull) && lane > cur;
+            const std::uint64_t fails = __ballot(mine && (bp || xp != s));
+            std::uint32_t pv;  // the last lane known to be on the chain, whose exit must be followed
+            if (fails) {
+              const std::uint32_t l0 = static_cast<std::uint32_t>(__builtin_ctzll(fails));
+              pv = 63u - static_cast<std::uint32_t>(__builtin_clzll(C & ((1ull << l0) - 1ull)));
+            } else {
+              pv = 63u - static_cast<std::uint32_t>(__builtin_clzll(C));  // every link holds: the last lane
+            }
+            const std::uint64_t xv = dev::readlane64(wk.x, pv);
+            const bool bv = __builtin_amdgcn_readlane(static_cast<int>(wk.broke), static_cast<int>(pv)) != 0;
+            if (bv || xv >= re || xv >= size) {  // the chain breaks, leaves the region or ends at pv
+              C &= (2ull << pv) - 1ull;
+              break;
+            }
+            // otherwise the chain goes on inside the region, at a lane whose start is not xv
+            const std::uint32_t q = static_cast<std::uint32_t>((xv - rs) / kPiece);
+            C &= ~(((1ull << q) - 1ull) & ~((2ull << pv) - 1ull));  // lanes strictly between drop out
+            C |= 1ull << q;
+            const bool me = lane == q;
+            if (me) s = xv;
+            walk_piece(win, rs, o, s, pe, size, me, wk);
+            cur = q;
+          }
+          const std::uint32_t last = 63u - static_cast<std::uint32_t>(__builtin_clzll(C));
+          Xout = dev::readlane64(wk.x, last);
+          const bool broke = __builtin_amdgcn_readlane(static_cast<int>(wk.broke), static_cast<int>(last)) != 0;
+          Er = exact ? e : dev::readlane64(s, f);
+          flags = kChain | spec_next | (broke ? kBroke : 0u) | (!broke && Xout == size ? kEnd : 0u);
+          // ---- 3. list and fold ------------------------------------------------------------------------
+          const bool on = (C >> lane) & 1ull;
+          (void)lane_prefix<kPiece / 8 < 32 ? 5 : 6>(on ? wk.n : 0u, &count);  // every chain record
+          // listed: each lane's records up to its first tiny one (all stored), in chain order
+          const std::uint32_t nn = on ? std::min<std::uint32_t>(wk.n, wk.tiny == kStore ? kStore : wk.tiny + 1u) : 0u;
+          std::uint32_t nlist;
+          const std::uint32_t pre = lane_prefix<4>(nn, &nlist);
+          const std::uint32_t t = on && wk.tiny < nn ? pre + wk.tiny : 0xFFFFFFFFu;
+          const std::uint32_t tmin = wave_min_u32(t);
+          const std::uint32_t nl = std::min<std::uint32_t>(std::min<std::uint32_t>(nlist, tmin == 0xFFFFFFFFu ? nlist : tmin + 1u), kList);
+#pragma unroll
+          for (std::uint32_t j = 0; j < kStore; ++j)
+            if (j < nn && pre + j < nl) list[pre + j] = static_cast<std::uint16_t>(wk.st[j]);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          for (std::uint32_t base = 0; base < nl; base += 64u) {
+            const std::uint32_t kk = base + lane;
+            const bool act = kk < nl;
+            const std::uint32_t so = act ? list[kk] : 0u;
+            const std::uint32_t b = so + o;
+            const std::uint32_t rl = rd32(win, b), stored = rd32(win, b + 4u);
+            const std::uint32_t kl = rd32(win, b + 18u), vl = rd32(win, b + 22u);
+            const bool kv_ok = kWalMeta + static_cast<std::uint64_t>(kl) + vl <= 8ull + rl;  // wal.cpp:118-121
+            const bool lng = act && rl > kLaneFold;
+            const std::uint32_t L = act && !lng ? rl : 0u;
+#if TKV_X_NOFOLD
+            const std::uint32_t crc = L + stored;
+            (void)tab;
+#else
+            const std::uint32_t crc = fold_win(win, tab, kc, b + 8u, L) ^ 0xFFFFFFFFu;
+#endif
+            const bool bad = act && (!kv_ok || (!lng && crc != stored));
+            const std::uint64_t lb = __ballot(lng);
+            if (lb) {
+              const std::uint32_t nb = static_cast<std::uint32_t>(__builtin_popcountll(lb));
+              std::uint64_t at;
+              if (!FIXUP && nlong + nb <= a.l_seg) {  // the wave's own segment: no atomic, no wait
+                at = static_cast<std::uint64_t>(wave) * a.l_seg + nlong;
+                nlong += nb;
+              } else {
+                at = 0;
+                if (lane == static_cast<std::uint32_t>(__builtin_ctzll(lb)))
+                  at = atomicAdd(&a.res[kResLongA], static_cast<unsigned long long>(nb));
+                at = a.l_seg * a.wsweep + dev::readlane64(at, static_cast<std::uint32_t>(__builtin_ctzll(lb)));
+              }
+              const std::uint64_t idx = at + __builtin_amdgcn_mbcnt_hi(static_cast<std::uint32_t>(lb >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo(static_cast<std::uint32_t>(lb), 0u));
+              if (lng && idx < a.l_cap) {
+                a.l_off[idx] = rs + so + 8u;
+                a.l_len[idx] = rl;
+                a.l_crc[idx] = stored;
+                a.l_reg[idx] = rr;
+                a.l_meta[idx] = kk | (ver << 8);
+              }
+            }
+            const std::uint64_t bk = __ballot(bad);
+            if (bk && bad_k == 0xFFFFFFFFu) bad_k = base + static_cast<std::uint32_t>(__builtin_ctzll(bk));
+          }
+          if (bad_k != 0xFFFFFFFFu) Bpos = rs + list[bad_k];
+        }
+      }
+      // ---- 4. region record, next entry --------------------------------------------------------------
+      bool stop = false;
+      std::uint64_t next_e = kNone;
+      std::uint32_t next_spec = kSpec;
+      if ((flags & kChain) && !(flags & kBroke)) {  // (after kEnd: size, past every later region)
+        next_e = Xout;
+        next_spec = 0u;
+      }
+      if constexpr (FIXUP) {
+        // converged: the next region's stored chain enters where this one leaves
+        if (rr + 1u >= limit || (flags & (kBroke | kEnd)) || !(flags & kChain)) {
+          stop = true;
+        } else {
+          const std::uint32_t nf = a.fl[rr + 1u];
+          if ((nf & kChain) && a.E[rr + 1u] == next_e) stop = true;
+        }
+      }
+      switch (lane) {
+        case 0: a.E[rr] = Er; break;
+        case 1: a.X[rr] = Xout; break;
+        case 2: a.B[rr] = Bpos; break;
+        case 3: a.cnt[rr] = count; break;
+        case 4: a.bidx[rr] = bad_k; break;
+        case 5: a.fl[rr] = flags | (ver << 8); break;
+        default: break;
+      }
+      e = next_e;
+      spec_next = next_spec;
+      return stop;
+    }
+  };
+#if TKV_X_BODY == 0
+  // One copy of the region body; only the window write and the refill are switched on rr % 4.
+  for (std::uint32_t rr = r0; rr < limit; ++rr) {
+    switch ((rr - r0) & 3u) {
+      case 0: put(rr, buf[0], buf[1][0]); break;
+      case 1: put(rr, buf[1], buf[2][0]); break;
+      case 2: put(rr, buf[2], buf[3][0]); break;
+      default: put(rr, buf[3], buf[0][0]); break;
+    }
+    if (body(rr)) break;
+  }
+#else
+  bool done = false;
+  for (std::uint32_t r = r0; r < limit && !done; r += kAhead) {
+#pragma unroll
+    for (int k = 0; k < kAhead; ++k) {
+      const std::uint32_t rr = r + static_cast<std::uint32_t>(k);
+      if (done || rr >= limit) {
+        done = true;
+        break;
+      }
+      put(rr, buf[k], buf[(k + 1) % kAhead][0]);
+      done = body(rr);
+    }
+  }
+#endif
+  if (!FIXUP && lane == 0) a.l_cnt[wave] = static_cast<std::uint32_t>(nlong);
 }
 
-// 4. Records of an on-path piece from its entry: the speculative walk's when it started there;
-// otherwise an exact walk (the records are checked again by wal_recheck). res[0] = the first piece
-// whose speculative exit was wrong; res[5] counts re-checked pieces. Off-path pieces count 0.
-__global__ void wal_count(WalArgs a) {
-  const std::uint64_t k = gid();
-  if (k >= a.K) return;
-  if (!a.on[k]) {
-    a.cnt[k] = 0;
-    return;
-  }
-  const std::uint64_t e = a.entry[k];
-  std::uint64_t p, packed;
-  bool bad;
-  if (e == a.S[k]) {
-    p = a.X[k];
-    bad = a.broke[k] != 0;
-    packed = a.spec_cnt[k];
+template <bool FIXUP>
+__global__ __launch_bounds__(kSweepThreads) void wal_sweep(SweepArgs a) {
+  __shared__ __attribute__((aligned(16))) std::uint32_t tab[kLdsSliceWords / 2];
+  __shared__ __attribute__((aligned(16))) std::uint8_t wins[kSweepWaves][kWinBytes];
+  dev::fill_lds_slicing16(a.tabs, tab);
+  __syncthreads();
+  const std::uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t w = blockIdx.x * kSweepWaves + wv;
+  if (w >= a.nwaves) return;
+  std::uint8_t* win = wins[wv];
+  std::uint16_t* list = reinterpret_cast<std::uint16_t*>(win + kWin);
+  if constexpr (!FIXUP) {
+    const std::uint32_t r0 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(w) * a.nreg / a.nwaves);
+    const std::uint32_t r1 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(w + 1) * a.nreg / a.nwaves);
+    sweep_wave<false>(a, win, list, tab, r0, r1, r0 == 0 ? 0ull : kNone, w);
   } else {
-    const std::uint64_t limit = (k + 1) * kWalPiece < a.size ? (k + 1) * kWalPiece : a.size;
-    std::uint64_t n_all = 0, n_big = 0;
-    p = e;
-    bad = false;
-    while (p < limit) {  // wal.cpp:63-87
-      if (a.size - p < kWalMeta) {
-        bad = true;
-        break;
-      }
-      const std::uint64_t rlen = ld32(a.w, p, a.size);
-      if (rlen + 8 > a.size - p) {
-        bad = true;
-        break;
-      }
-      ++n_all;
-      n_big += rlen > kWalLaneMax ? 1u : 0u;
-      p += 8 + rlen;
+    sweep_wave<true>(a, win, list, tab, a.t_begin[w], a.t_limit[w], a.t_entry[w], w);
+  }
+}
+
+// Dense long-payload list for the CRC batch: the sweep waves' segments, then the atomic area.
+// One block of 1024 threads scans the per-wave counts; every block copies its waves' entries.
+__global__ void wal_long_scan(const std::uint32_t* l_cnt, std::uint32_t W, std::uint64_t* l_base, unsigned long long* res) {
+  __shared__ std::uint64_t part[1024];
+  const std::uint32_t t = threadIdx.x;
+  const std::uint32_t per = (W + 1023u) / 1024u;
+  std::uint64_t s = 0;
+  for (std::uint32_t i = 0; i < per; ++i) {
+    const std::uint32_t w = t * per + i;
+    if (w < W) s += l_cnt[w];
+  }
+  part[t] = s;
+  __syncthreads();
+  for (std::uint32_t d = 1; d < 1024u; d <<= 1) {
+    const std::uint64_t v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  std::uint64_t run = t ? part[t - 1] : 0;
+  for (std::uint32_t i = 0; i < per; ++i) {
+    const std::uint32_t w = t * per + i;
+    if (w < W) {
+      l_base[w] = run;
+      run += l_cnt[w];
     }
-    packed = (n_all << 32) | n_big;
-    a.recheck[k] = 1;
-    atomicAdd(reinterpret_cast<unsigned long long*>(&a.res[5]), 1ull);
-    if (p != a.X[k] || bad != (a.broke[k] != 0)) atomicMin(reinterpret_cast<unsigned long long*>(&a.res[0]), k);
   }
-  a.cnt[k] = packed;
-  a.Xe[k] = p;
-  a.Be[k] = bad ? 1 : 0;
-  if (a.next[k] >= a.K) {
-    a.res[1] = p;
-    a.res[2] = bad ? 1 : 0;
+  if (t == 1023u) {
+    l_base[W] = part[1023];
+    res[kResLongSeg] = part[1023];
   }
 }
-
-// Pieces entered off their speculative start: check their records from the true entry.
-__global__ __launch_bounds__(kCheckThreads) __attribute__((amdgpu_waves_per_eu(kCheckWgPerCu * kCheckThreads / 256))) void
-wal_recheck(WalArgs a) {
-  __shared__ std::uint32_t lds[TKV_AB_WAL16 ? kLdsSliceWords / 2 : kLdsSliceWords];
-  fill_slices(a.tabs, lds);
-  const std::uint64_t k = gid();
-  if (k >= a.K || !a.recheck[k]) return;
-  const dev::LaneConst kc = TKV_AB_WAL16 ? dev::lane_const16(threadIdx.x & 63u) : dev::lane_const(threadIdx.x & 63u);
-  std::uint64_t x, c;
-  std::uint8_t br;
-  walk_check(lds, kc, a, k, a.entry[k], &x, &br, &c);
-}
-
-// Records past the first piece with a wrong speculative exit are not on the true chain (or not
-// known to be): drop them.
-__global__ void wal_trim(WalArgs a, std::uint64_t kstar) {
-  const std::uint64_t k = gid();
-  if (k < a.K && k > kstar) a.cnt[k] = 0;
-}
-
-// 5. Record numbering: the first failing record of each counted piece becomes a record index, and
-// the big-record slots move to the dense list the CRC batch reads.
-__global__ void wal_gather(WalArgs a) {
-  const std::uint64_t k = gid();
-  if (k >= a.K || a.cnt[k] == 0) return;
-  const std::uint64_t b_all = a.base[k] >> 32, b_big = a.base[k] & 0xFFFFFFFFull;
-  const std::uint64_t n_big = a.cnt[k] & 0xFFFFFFFFull;
-  if (a.first_loc[k] != kNone) {
-    a.bad_at[k] = b_all + a.first_loc[k];
-    atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), b_all + a.first_loc[k]);
+// entry j of the dense list (d_*) <- wave w's segment / the atomic area
+__global__ void wal_long_gather(SweepArgs a, const std::uint64_t* l_base, std::uint32_t W, const unsigned long long* res,
+                                std::uint64_t* d_off, std::uint32_t* d_len, std::uint32_t* d_crc, std::uint32_t* d_reg,
+                                std::uint32_t* d_meta) {
+  const std::uint64_t nseg = l_base[W];
+  const std::uint64_t n_atomic = std::min<std::uint64_t>(res[kResLongA], a.l_cap - a.l_seg * W);
+  const std::uint64_t j = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+  if (j >= nseg + n_atomic) return;
+  std::uint64_t src;
+  if (j < nseg) {
+    std::uint32_t lo = 0, hi = W;  // the wave whose range holds j
+    while (hi - lo > 1) {
+      const std::uint32_t mid = (lo + hi) / 2;
+      if (l_base[mid] <= j) lo = mid;
+      else hi = mid;
+    }
+    src = static_cast<std::uint64_t>(lo) * a.l_seg + (j - l_base[lo]);
+  } else {
+    src = a.l_seg * W + (j - nseg);
   }
-  for (std::uint64_t j = 0; j < n_big; ++j) {
-    const std::uint64_t sl = 2 * k + j;
-    a.big_off[b_big + j] = a.slot_off[sl];
-    a.big_len[b_big + j] = a.slot_len[sl];
-    a.big_crc[b_big + j] = a.slot_crc[sl];
-    a.big_idx[b_big + j] = b_all + a.slot_loc[sl];
+  d_off[j] = a.l_off[src];
+  d_len[j] = a.l_len[src];
+  d_crc[j] = a.l_crc[src];
+  d_reg[j] = a.l_reg[src];
+  d_meta[j] = a.l_meta[src];
+}
+
+// Boundary checks: region p ends a chain segment when the next region's entry did not come from p
+// (it searched, or was entered by a search or a fix-up). Unless the chain ended in p, p's exit X must
+// land exactly on the entry of region q = X / kRegion, and every region between must hold no chain
+// (it searched) or be inside the same record (a chain region entered at X: a fix-up's, carried
+// through the record). A chain region whose entry lies past its own end was carried there, so the
+// rule is exact. Failing p go to the list.
+__global__ void wal_bounds(SweepArgs a, std::uint32_t* inc_p, std::uint64_t* inc_x, std::uint32_t cap) {
+  const std::uint64_t p = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+  if (p + 1 >= a.nreg) return;
+  const std::uint32_t f = a.fl[p] & 0xFFu;
+  if (!(f & kChain) || (f & (kBroke | kEnd))) return;
+  if (!(a.fl[p + 1] & (kSpec | kSearch | kFix))) return;
+  const std::uint64_t x = a.X[p];
+  const std::uint64_t q = x / kRegion;
+  bool ok = q > p && q < a.nreg;
+  for (std::uint64_t j = p + 1; ok && j < q; ++j) {
+    const std::uint32_t fj = a.fl[j];
+    ok = (fj & kSearch) || ((fj & kChain) && a.E[j] == x);
+  }
+  if (ok) ok = (a.fl[q] & kChain) && a.E[q] == x;
+  if (!ok) {
+    const unsigned long long i = atomicAdd(&a.res[kResIncons], 1ull);
+    if (i < cap) {
+      inc_p[i] = static_cast<std::uint32_t>(p);
+      inc_x[i] = x;
+    }
   }
 }
 
-__global__ void wal_check_big(WalArgs a, std::uint64_t n) {
-  const std::uint64_t i = gid();
-  if (i < n && a.got[i] != a.big_crc[i]) atomicMin(reinterpret_cast<unsigned long long*>(&a.res[3]), a.big_idx[i]);
+__global__ void wal_reset(unsigned long long* res, int lo, int hi) {
+  const int i = lo + static_cast<int>(threadIdx.x);
+  if (i < hi) res[i] = (i == kResP || i == kResQ) ? ~0ull : 0ull;
 }
 
-// Start of the first bad record (res[3]): from the piece that found it, or from the big list.
-__global__ void wal_bad_pos(WalArgs a, std::uint64_t n_big) {
-  const std::uint64_t i = gid();
-  const std::uint64_t want = a.res[3];
-  if (i < a.K && a.cnt[i] != 0 && a.bad_at[i] == want) a.res[4] = a.first_pos[i];
-  if (i < n_big && a.big_idx[i] == want) a.res[4] = a.big_off[i] - 8;
+// First bad record P (region lists and, when their versions are current, the long payloads) and the
+// chain's break Q.
+__global__ void wal_fin_min(SweepArgs a, const std::uint32_t* got, std::uint64_t nlong) {
+  const std::uint64_t i = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+  if (i < a.nreg) {
+    const std::uint32_t f = a.fl[i];
+    if (f & kChain) {
+      if (f & kBroke) atomicMin(&a.res[kResQ], static_cast<unsigned long long>(a.X[i]));
+      const std::uint64_t b = a.B[i];
+      if (b != kNone) atomicMin(&a.res[kResP], static_cast<unsigned long long>(b));
+    }
+  }
+  if (i < nlong) {
+    const std::uint32_t r = a.l_reg[i];
+    if ((a.l_meta[i] >> 8) == (a.fl[r] >> 8) && got[i] != a.l_crc[i])
+      atomicMin(&a.res[kResP], static_cast<unsigned long long>(a.l_off[i] - 8u));
+  }
+}
+
+// Records before the stop (block sums of cnt over the regions before it) and the first bad record's
+// index within its region.
+__global__ void wal_fin_count(SweepArgs a, const std::uint32_t* got, std::uint64_t nlong) {
+  __shared__ unsigned long long part[8];
+  const std::uint64_t i = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+  const std::uint64_t P = a.res[kResP], Q = a.res[kResQ];
+  const bool bad = P < Q;
+  const std::uint64_t stop = bad ? P : Q;
+  const std::uint64_t rb = stop == kNone ? a.nreg : stop / kRegion;
+  std::uint64_t c = 0;
+  if (i < a.nreg) {
+    const std::uint32_t f = a.fl[i];
+    if ((f & kChain) && (i < rb || (i == rb && !bad))) c = a.cnt[i];
+    if (bad && i == rb && a.B[i] == P) a.res[kResLidx] = a.bidx[i];
+  }
+  if (bad && i < nlong) {
+    const std::uint32_t r = a.l_reg[i];
+    if ((a.l_meta[i] >> 8) == (a.fl[r] >> 8) && got[i] != a.l_crc[i] && a.l_off[i] - 8u == P)
+      a.res[kResLidx] = a.l_meta[i] & 0xFFu;
+  }
+  // block sum
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) c += static_cast<std::uint64_t>(__shfl_xor(static_cast<long long>(c), m, 64));
+  if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long s = 0;
+    for (unsigned k = 0; k < blockDim.x / 64u; ++k) s += part[k];
+    if (s) atomicAdd(&a.res[kResCnt], s);
+  }
+}
+
+// Result words into the host's pinned block: [0] failing boundaries, [1] long payloads, [2] records
+// good, [3] stop offset, [4] corrupted, [5] entries the atomic area was asked for.
+__global__ void wal_publish(SweepArgs a, std::uint64_t* h) {
+  if (threadIdx.x != 0) return;
+  const std::uint64_t P = a.res[kResP], Q = a.res[kResQ];
+  h[0] = a.res[kResIncons];
+  h[1] = a.res[kResLongSeg] + std::min<std::uint64_t>(a.res[kResLongA], a.l_cap - a.l_seg * a.wsweep);
+  h[5] = a.res[kResLongA];
+  if (P < Q) {
+    h[2] = a.res[kResCnt] + a.res[kResLidx];
+    h[3] = P;
+    h[4] = 1;
+  } else {
+    h[2] = a.res[kResCnt];
+    h[3] = Q == kNone ? a.size : Q;
+    h[4] = Q == kNone ? 0 : 1;
+  }
 }
 
 // Per-device scratch, grown by doubling and kept between calls (guarded by mu).
 struct WalScratch {
   std::mutex mu;
-  std::uint64_t cap_pieces = 0, cap_big = 0;
-  void* pieces = nullptr;  // per piece: 13 u64, 9 u32, 4 u8 (carve)
-  void* bigs = nullptr;    // per big record: 2 u64, 3 u32
-  void* cub = nullptr;
-  std::size_t cub_bytes = 0;
-  std::uint64_t* res = nullptr;
-  std::uint64_t* h_res = nullptr;  // pinned, kHres words
-  std::uint64_t* d_hres = nullptr;  // device view of h_res (wal_publish)
-  std::uint32_t* inj = nullptr;  // Shift_L(0xFFFFFFFF), L = 0..kWalLaneMax
-  // host images: device copy, pinned staging slabs for pageable sources, own stream
+  std::uint64_t cap_reg = 0, cap_raw = 0, cap_dense = 0;
+  std::uint32_t cap_waves = 0;
+  void* regs = nullptr;   // per region: E, X, B (u64), cnt, bidx, fl (u32)
+  void* raw = nullptr;    // long payloads as the sweep lists them: off (u64), len, crc, reg, meta (u32)
+  void* dense = nullptr;  // the same, gathered for the CRC batch, and got (u32)
+  std::uint32_t* l_cnt = nullptr;   // per sweep wave, then the scan's bases (u64)
+  std::uint64_t* l_base = nullptr;
+  unsigned long long* res = nullptr;
+  std::uint64_t* h_res = nullptr;   // pinned, kHres words
+  std::uint64_t* d_hres = nullptr;  // device view of h_res
+  // failing boundaries (device) and fix-up tasks (pinned, read by the kernel in place)
+  std::uint32_t* inc_p = nullptr;
+  std::uint64_t* inc_x = nullptr;
+  std::uint32_t* h_inc_p = nullptr;  // pinned copies for the host's pruning
+  std::uint64_t* h_inc_x = nullptr;
+  std::uint32_t* h_task = nullptr;   // pinned: begin[kMaxFix], limit[kMaxFix], entry (u64)[kMaxFix]
+  std::uint32_t* d_task = nullptr;
+  // host images: device copy, pinned staging slabs for pageable sources, own streams
   std::uint8_t* d_img = nullptr;
   std::uint64_t cap_img = 0;
   std::uint8_t* slab[2] = {nullptr, nullptr};
   hipEvent_t slab_free[2] = {nullptr, nullptr};
-  hipEvent_t landed[2] = {nullptr, nullptr};  // copy of a chunk done (copy stream -> compute stream)
   hipStream_t st = nullptr;   // copies of host images
-  hipStream_t stc = nullptr;  // device work on host images (overlaps the copies)
+  hipStream_t stc = nullptr;  // device work on host images
+  int ncu = 0;
   ~WalScratch() {
     if (st) (void)hipStreamSynchronize(st);
     if (stc) (void)hipStreamSynchronize(stc);
-    for (int i = 0; i < 2; ++i)
-      if (landed[i]) (void)hipEventDestroy(landed[i]);
     if (stc) (void)hipStreamDestroy(stc);
     (void)hipFree(d_img);
     for (int i = 0; i < 2; ++i) {
@@ -607,20 +743,27 @@ struct WalScratch {
       if (slab_free[i]) (void)hipEventDestroy(slab_free[i]);
     }
     if (st) (void)hipStreamDestroy(st);
-    (void)hipFree(pieces);
-    (void)hipFree(bigs);
-    (void)hipFree(cub);
+    (void)hipFree(regs);
+    (void)hipFree(raw);
+    (void)hipFree(dense);
+    (void)hipFree(l_cnt);
+    (void)hipFree(l_base);
     (void)hipFree(res);
-    (void)hipFree(inj);
+    (void)hipFree(inc_p);
+    (void)hipFree(inc_x);
     (void)hipHostFree(h_res);
+    (void)hipHostFree(h_inc_p);
+    (void)hipHostFree(h_inc_x);
+    (void)hipHostFree(h_task);
   }
 };
+constexpr std::uint32_t kMaxFix = 1u << 16;  // failing boundaries handled per round
 
 std::mutex g_wal_mu;
 WalScratch* g_wal[64] = {};
 
 // What the calling thread's last WAL verify did (tkv_debug_wal_last).
-thread_local std::uint64_t g_last[4] = {0, 0, 0, 0};  // passes, host walk needed, image copied, fast stitch
+thread_local std::uint64_t g_last[4] = {0, 0, 0, 0};  // rounds, host walk needed, image copied, no fix-up
 
 #define WAL_HIP(call)                                                            \
   do {                                                                           \
@@ -628,199 +771,64 @@ thread_local std::uint64_t g_last[4] = {0, 0, 0, 0};  // passes, host walk neede
     if (e_ != hipSuccess) return set_error(TKV_IO_ERROR, hipGetErrorString(e_)); \
   } while (0)
 
-int grow_pieces(WalScratch& s, std::uint64_t K) {
-  if (K <= s.cap_pieces) return TKV_OK;
-  const std::uint64_t cap = std::max<std::uint64_t>(K, 2 * s.cap_pieces);
-  WAL_HIP(hipFree(s.pieces));
-  s.pieces = nullptr;
-  s.cap_pieces = 0;
-  WAL_HIP(hipMalloc(&s.pieces, cap * (13 * 8 + 9 * 4 + 4)));
-  s.cap_pieces = cap;
+unsigned blocks(std::uint64_t n, unsigned t) { return static_cast<unsigned>((n + t - 1) / t); }
+
+int grow(void** p, std::uint64_t* cap, std::uint64_t want, std::uint64_t unit) {
+  if (want <= *cap) return TKV_OK;
+  const std::uint64_t c = std::max<std::uint64_t>(want, 2 * *cap);
+  WAL_HIP(hipFree(*p));
+  *p = nullptr;
+  *cap = 0;
+  WAL_HIP(hipMalloc(p, c * unit));
+  *cap = c;
   return TKV_OK;
 }
 
-int grow_big(WalScratch& s, std::uint64_t n) {
-  if (n <= s.cap_big) return TKV_OK;
-  const std::uint64_t cap = std::max<std::uint64_t>(n, 2 * s.cap_big);
-  WAL_HIP(hipFree(s.bigs));
-  s.bigs = nullptr;
-  s.cap_big = 0;
-  WAL_HIP(hipMalloc(&s.bigs, cap * (2 * 8 + 3 * 4)));
-  s.cap_big = cap;
-  return TKV_OK;
+constexpr std::uint64_t kRawUnit = 8 + 4 * 4, kDenseUnit = 8 + 5 * 4;
+
+// Long-payload arrays of the raw (sweep) or dense (batch) layout.
+void long_view(void* base, std::uint64_t cap, SweepArgs* a, std::uint32_t** got) {
+  auto* l8 = static_cast<std::uint64_t*>(base);
+  a->l_off = l8;
+  auto* l4 = reinterpret_cast<std::uint32_t*>(l8 + cap);
+  a->l_len = l4;
+  a->l_crc = l4 + cap;
+  a->l_reg = l4 + 2 * cap;
+  a->l_meta = l4 + 3 * cap;
+  if (got) *got = l4 + 4 * cap;
 }
 
-WalArgs carve(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std::uint32_t K, const DeviceTables* tabs) {
-  WalArgs a{};
+SweepArgs carve(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std::uint32_t nreg, std::uint32_t W,
+                std::uint64_t seg, const DeviceTables* tabs) {
+  SweepArgs a{};
   a.w = w;
   a.size = size;
-  a.K = K;
-  const std::uint64_t C = s.cap_pieces;
-  auto* p8 = static_cast<std::uint64_t*>(s.pieces);
-  std::uint64_t** u64s[] = {&a.S, &a.X, &a.spec_cnt, &a.first_loc, &a.first_pos, &a.entry, &a.cnt, &a.base, &a.Xe,
-                            &a.bad_at};
-  for (std::size_t i = 0; i < sizeof(u64s) / sizeof(u64s[0]); ++i) *u64s[i] = p8 + i * C;
-  a.slot_off = p8 + 10 * C;  // 2C
-  auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 13 * C);
-  a.next = p4;
-  a.Ja = p4 + C;
-  a.Jb = p4 + 2 * C;
-  a.slot_len = p4 + 3 * C;  // 2C each
-  a.slot_crc = p4 + 5 * C;
-  a.slot_loc = p4 + 7 * C;
-  auto* p1 = reinterpret_cast<std::uint8_t*>(p4 + 9 * C);
-  a.broke = p1;
-  a.on = p1 + C;
-  a.Be = p1 + 2 * C;
-  a.recheck = p1 + 3 * C;
-  const std::uint64_t B = s.cap_big;
-  if (B) {
-    auto* b8 = static_cast<std::uint64_t*>(s.bigs);
-    a.big_off = b8;
-    a.big_idx = b8 + B;
-    auto* b4 = reinterpret_cast<std::uint32_t*>(b8 + 2 * B);
-    a.big_len = b4;
-    a.big_crc = b4 + B;
-    a.got = b4 + 2 * B;
-  }
-  a.inj = s.inj;
-  a.tabs = tabs;
+  const std::uintptr_t wp = reinterpret_cast<std::uintptr_t>(w);
+  a.al0 = wp & ~static_cast<std::uintptr_t>(15);
+  a.glast = (wp + size - 1) & ~static_cast<std::uintptr_t>(15);
+  a.o = static_cast<std::uint32_t>(wp - a.al0);
+  a.nreg = nreg;
+  a.nwaves = W;
+  a.wsweep = W;
+  const std::uint64_t C = s.cap_reg;
+  auto* p8 = static_cast<std::uint64_t*>(s.regs);
+  a.E = p8;
+  a.X = p8 + C;
+  a.B = p8 + 2 * C;
+  auto* p4 = reinterpret_cast<std::uint32_t*>(p8 + 3 * C);
+  a.cnt = p4;
+  a.bidx = p4 + C;
+  a.fl = p4 + 2 * C;
+  long_view(s.raw, s.cap_raw, &a, nullptr);
+  a.l_cap = s.cap_raw;
+  a.l_seg = seg;
+  a.l_cnt = s.l_cnt;
   a.res = s.res;
+  a.tabs = tabs;
   return a;
 }
 
-unsigned blocks(std::uint64_t n, unsigned t) { return static_cast<unsigned>((n + t - 1) / t); }
-
-// CRC batches of at most this many records (the irregular path's u32 block indices).
-constexpr std::uint64_t kWalCrcChunk = std::uint64_t(1) << 31;
-
-// A pass over the image [w, w + size), which starts with a record (or is empty), in three parts:
-// pass_begin (result words, speculative starts cleared), pass_front over ranges of pieces (scan and
-// speculative walk; each range's bytes and the next 1 KiB + 26 bytes must be resident), pass_tail.
-int pass_begin(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream_t st, WalArgs* out) {
-  const std::uint32_t K = static_cast<std::uint32_t>((size + kWalPiece - 1) / kWalPiece);
-  const DeviceTables* tabs = device_tables(kAlgoCrc32);
-  if (!tabs) return TKV_IO_ERROR;
-  if (int rc = grow_pieces(s, K)) return rc;
-  WalArgs a = carve(s, w, size, K, tabs);
-  s.h_res[0] = kNone;
-  s.h_res[1] = size;
-  s.h_res[2] = 0;
-  s.h_res[3] = kNone;
-  s.h_res[4] = 0;
-  s.h_res[5] = 0;
-  s.h_res[6] = 0;
-  WAL_HIP(hipMemcpyAsync(s.res, s.h_res, 7 * sizeof(std::uint64_t), hipMemcpyHostToDevice, st));
-  WAL_HIP(hipMemsetAsync(a.S, 0xFF, K * sizeof(std::uint64_t), st));
-  *out = a;
-  return TKV_OK;
-}
-
-void pass_front(const WalArgs& a, std::uint64_t k_lo, std::uint64_t k_hi, hipStream_t st) {
-  if (k_hi <= k_lo) return;
-  const std::uint64_t threads = (k_hi - k_lo + 64 / kHeadLanes - 1) / (64 / kHeadLanes) * 64;  // 8 pieces per wave
-  hipLaunchKernelGGL(wal_scan_head, dim3(blocks(threads, kScanThreads)), dim3(kScanThreads), 0, st, a, k_lo, k_hi);
-  hipLaunchKernelGGL(wal_spec, dim3(blocks(k_hi - k_lo, kCheckThreads)), dim3(kCheckThreads), 0, st, a, k_lo, k_hi);
-}
-
-int pass_tail(WalScratch& s, WalArgs a, hipStream_t st, PassResult* r) {
-  const std::uint8_t* w = a.w;
-  const std::uint64_t size = a.size;
-  const std::uint32_t K = a.K;
-  const DeviceTables* tabs = a.tabs;
-  // 3: the pieces on the true chain and their entries, first by the fast path (wal_fast), with
-  // record counts and their scan behind it, so one host sync reads the verdict and the totals
-  std::size_t need = 0;
-  WAL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, a.cnt, a.base, K, st));
-  if (need > s.cub_bytes) {
-    WAL_HIP(hipStreamSynchronize(st));
-    WAL_HIP(hipFree(s.cub));
-    s.cub = nullptr;
-    s.cub_bytes = 0;
-    WAL_HIP(hipMalloc(&s.cub, need));
-    s.cub_bytes = need;
-  }
-  auto count_and_publish = [&]() -> int {
-    hipLaunchKernelGGL(wal_count, dim3(blocks(K, 256)), dim3(256), 0, st, a);
-    WAL_HIP(hipcub::DeviceScan::ExclusiveSum(s.cub, need, a.cnt, a.base, K, st));
-    hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
-    WAL_HIP(hipGetLastError());
-    WAL_HIP(hipStreamSynchronize(st));
-    return TKV_OK;
-  };
-  hipLaunchKernelGGL(wal_fast, dim3(blocks(K, 256)), dim3(256), 0, st, a);
-  if (int rc = count_and_publish()) return rc;
-  if (s.h_res[6]) g_last[3] = 0;  // the pointer-jumping stitch ran
-  if (s.h_res[6]) {
-    // the speculation was wrong somewhere: pointer jumping marks the pieces on the true chain
-    // (wal_count above took the fast path's entries, which are speculative starts: it left res[0]
-    // and res[5] alone, and the exact count below rewrites res[1], res[2] from the true last piece)
-    hipLaunchKernelGGL(wal_jump_init, dim3(blocks(K, 256)), dim3(256), 0, st, a);
-    std::uint32_t* J = a.Ja;
-    std::uint32_t* J2 = a.Jb;
-    for (std::uint64_t reach = 1; reach < K; reach <<= 2) {
-      hipLaunchKernelGGL(wal_jump, dim3(blocks(K, 256)), dim3(256), 0, st, J, J2, a.on, K);
-      std::swap(J, J2);
-    }
-    hipLaunchKernelGGL(wal_link, dim3(blocks(K, 256)), dim3(256), 0, st, a);
-    // 4: record counts from the entries
-    if (int rc = count_and_publish()) return rc;
-  }
-  const std::uint64_t kstar = s.h_res[0];
-  std::uint64_t chain_end = s.h_res[1];
-  bool broke = s.h_res[2] != 0;
-  const bool partial = kstar < K;
-  std::uint64_t tot = s.h_res[7] + s.h_res[8];  // (records << 32) | big records
-  if (s.h_res[5]) hipLaunchKernelGGL(wal_recheck, dim3(blocks(K, kCheckThreads)), dim3(kCheckThreads), 0, st, a);
-  if (partial) {
-    hipLaunchKernelGGL(wal_trim, dim3(blocks(K, 256)), dim3(256), 0, st, a, kstar);
-    WAL_HIP(hipcub::DeviceScan::ExclusiveSum(s.cub, need, a.cnt, a.base, K, st));
-    hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
-    std::uint8_t be = 0;
-    WAL_HIP(hipMemcpyAsync(s.h_res + 1, a.Xe + kstar, 8, hipMemcpyDeviceToHost, st));
-    WAL_HIP(hipMemcpyAsync(&be, a.Be + kstar, 1, hipMemcpyDeviceToHost, st));
-    WAL_HIP(hipStreamSynchronize(st));
-    chain_end = s.h_res[1];
-    broke = be != 0;
-    tot = s.h_res[7] + s.h_res[8];
-  }
-  // 5: record numbering (the scan above), first failing in-lane record, the CRC batch of the big ones
-  const std::uint64_t n = tot >> 32, n_big = tot & 0xFFFFFFFFull;
-  std::uint64_t first = n;
-  if (n) {
-    if (int rc = grow_big(s, std::max<std::uint64_t>(n_big, 1))) return rc;
-    a = carve(s, w, size, K, tabs);
-    hipLaunchKernelGGL(wal_gather, dim3(blocks(K, 256)), dim3(256), 0, st, a);
-    WAL_HIP(hipGetLastError());
-    for (std::uint64_t i = 0; i < n_big; i += kWalCrcChunk) {
-      const std::uint64_t m = std::min(kWalCrcChunk, n_big - i);
-      if (int rc = batch_device_impl(kAlgoCrc32, w, a.big_off + i, a.big_len + i, nullptr, a.got + i, m, st)) return rc;
-    }
-    if (n_big) hipLaunchKernelGGL(wal_check_big, dim3(blocks(n_big, 256)), dim3(256), 0, st, a, n_big);
-    hipLaunchKernelGGL(wal_bad_pos, dim3(blocks(std::max<std::uint64_t>(K, n_big), 256)), dim3(256), 0, st, a, n_big);
-    WAL_HIP(hipGetLastError());
-    hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
-    WAL_HIP(hipGetLastError());
-    WAL_HIP(hipStreamSynchronize(st));
-    first = std::min<std::uint64_t>(s.h_res[3], n);
-  }
-  r->good = first;
-  r->corrupted = first < n || broke;
-  r->stop = first < n ? s.h_res[4] : chain_end;
-  r->resume = !r->corrupted && partial && chain_end < size;
-  return TKV_OK;
-}
-
-// A whole pass over a resident image.
-int wal_pass(WalScratch& s, const std::uint8_t* w, std::uint64_t size, hipStream_t st, PassResult* r) {
-  WalArgs a;
-  if (int rc = pass_begin(s, w, size, st, &a)) return rc;
-  pass_front(a, 0, a.K, st);
-  return pass_tail(s, a, st, r);
-}
-
-// The calling thread's device's scratch (created on first use, with its result words and the
-// init-term table).
+// The calling thread's device's scratch (created on first use).
 int scratch(WalScratch** out) {
   int dev = 0;
   WAL_HIP(hipGetDevice(&dev));
@@ -833,47 +841,132 @@ int scratch(WalScratch** out) {
   }
   std::lock_guard<std::mutex> lk(sp->mu);
   if (!sp->res) {
-    WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->res), 8 * sizeof(std::uint64_t)));
+    hipDeviceProp_t prop;
+    WAL_HIP(hipGetDeviceProperties(&prop, dev));
+    sp->ncu = prop.multiProcessorCount;
+    WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->inc_p), kMaxFix * sizeof(std::uint32_t)));
+    WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->inc_x), kMaxFix * sizeof(std::uint64_t)));
+    WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&sp->h_inc_p), kMaxFix * sizeof(std::uint32_t), hipHostMallocDefault));
+    WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&sp->h_inc_x), kMaxFix * sizeof(std::uint64_t), hipHostMallocDefault));
+    WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&sp->h_task), kMaxFix * 16, hipHostMallocDefault));
+    WAL_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&sp->d_task), sp->h_task, 0));
     WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&sp->h_res), kHres * sizeof(std::uint64_t), hipHostMallocDefault));
     WAL_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&sp->d_hres), sp->h_res, 0));
     WAL_HIP(hipStreamCreateWithFlags(&sp->st, hipStreamNonBlocking));
     WAL_HIP(hipStreamCreateWithFlags(&sp->stc, hipStreamNonBlocking));
-    for (int i = 0; i < 2; ++i) WAL_HIP(hipEventCreateWithFlags(&sp->landed[i], hipEventDisableTiming));
-    std::vector<std::uint32_t> inj(kWalLaneMax + 1);
-    for (std::uint32_t L = 0; L <= kWalLaneMax; ++L) inj[L] = shift_bytes(kInit, L, kPoly);
-    WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->inj), inj.size() * 4));
-    WAL_HIP(hipMemcpy(sp->inj, inj.data(), inj.size() * 4, hipMemcpyHostToDevice));
+    WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->res), kResWords * sizeof(unsigned long long)));
+    const std::uint32_t wmax = static_cast<std::uint32_t>(sp->ncu) * kSweepWaves;
+    WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->l_cnt), (wmax + 1) * sizeof(std::uint32_t)));
+    WAL_HIP(hipMalloc(reinterpret_cast<void**>(&sp->l_base), (wmax + 1) * sizeof(std::uint64_t)));
+    sp->cap_waves = wmax;
   }
   *out = sp;
   return TKV_OK;
 }
 
-int verify_locked(WalScratch& s, const std::uint8_t* d_wal, std::uint64_t size, std::uint64_t* n_good,
-                  std::uint64_t* stop_offset, hipStream_t st, bool* needs_host_walk,
-                  const PassResult* first_pass = nullptr) {
-  // Each pass checks the true chain at least through its first piece; a pass that stops short of
-  // the end without a verdict resumes at a true record start. Adversarial images that keep the
-  // speculation wrong go to the exact host walk after kMaxPasses.
-  constexpr int kMaxPasses = 8;
-  std::uint64_t start = 0, good = 0;
-  g_last[0] = g_last[1] = 0;
-  for (int pass = 0; pass < kMaxPasses; ++pass) {
-    PassResult r;
-    g_last[0] = static_cast<std::uint64_t>(pass) + 1;
-    if (pass == 0 && !first_pass) g_last[3] = 1;  // cleared by the first pass that needs the pointer-jumping stitch
-    if (pass == 0 && first_pass) r = *first_pass;
-    else if (int rc = wal_pass(s, d_wal + start, size - start, st, &r)) return rc;
-    good += r.good;
-    if (!r.resume) {
-      *n_good = good;
-      *stop_offset = start + r.stop;
-      return r.corrupted ? set_error(TKV_CORRUPTED, "corrupted WAL record") : TKV_OK;
+// fin_min, fin_count, publish (long payloads from the dense list when nlong > 0).
+void launch_fin(SweepArgs a, WalScratch& s, std::uint64_t nlong, hipStream_t st) {
+  std::uint32_t* got = nullptr;
+  if (nlong) long_view(s.dense, s.cap_dense, &a, &got);
+  const std::uint64_t n = std::max<std::uint64_t>(a.nreg, nlong);
+  hipLaunchKernelGGL(wal_fin_min, dim3(blocks(n, 256)), dim3(256), 0, st, a, got, nlong);
+  hipLaunchKernelGGL(wal_fin_count, dim3(blocks(n, 512)), dim3(512), 0, st, a, got, nlong);
+  hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
+}
+
+// The verify of [w, w + size) on `st` (synchronous). Caller holds s.mu.
+int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std::uint64_t* n_good,
+                  std::uint64_t* stop_offset, hipStream_t st) {
+  const DeviceTables* tabs = device_tables(kAlgoCrc32);
+  if (!tabs) return TKV_IO_ERROR;
+  const std::uint64_t nreg64 = (size + kRegion - 1) / kRegion;
+  if (nreg64 >= 0xFFFFFFF0ull) return set_error(TKV_INVALID_ARGUMENT, "WAL image too large for the device walk");
+  const std::uint32_t nreg = static_cast<std::uint32_t>(nreg64);
+  if (int rc = grow(&s.regs, &s.cap_reg, nreg, 3 * 8 + 3 * 4)) return rc;
+  const std::uint32_t W = static_cast<std::uint32_t>(std::min<std::uint64_t>(nreg, s.cap_waves));
+  // a wave's segment holds the long payloads of its chunk's chain (>= kLaneFold + 8 bytes apart);
+  // more (speculative chains) and the fix-ups' go to the atomic area behind the segments
+  const std::uint64_t seg = (static_cast<std::uint64_t>((nreg + W - 1) / W) * kRegion) / (kLaneFold + 8) + 16;
+  std::uint64_t atomic_area = nreg / 4 + 4096;
+  for (;;) {  // (once, unless the long-payload list overflows)
+    if (int rc = grow(&s.raw, &s.cap_raw, seg * W + atomic_area, kRawUnit)) return rc;
+    SweepArgs a = carve(s, w, size, nreg, W, seg, tabs);
+    hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, 0, static_cast<int>(kResWords));
+    hipLaunchKernelGGL((wal_sweep<false>), dim3(blocks(W, kSweepWaves)), dim3(kSweepThreads), 0, st, a);
+    hipLaunchKernelGGL(wal_long_scan, dim3(1), dim3(1024), 0, st, s.l_cnt, W, s.l_base, s.res);
+    hipLaunchKernelGGL(wal_bounds, dim3(blocks(nreg, 256)), dim3(256), 0, st, a, s.inc_p, s.inc_x, kMaxFix);
+    launch_fin(a, s, 0, st);
+    WAL_HIP(hipGetLastError());
+    WAL_HIP(hipStreamSynchronize(st));
+    std::uint64_t rounds = 1;
+    const bool clean = s.h_res[0] == 0;
+    // fix-up rounds: every failing boundary is walked again from its true exit (race-free ranges)
+    while (s.h_res[0] != 0) {
+      const std::uint64_t ninc = std::min<std::uint64_t>(s.h_res[0], kMaxFix);
+      WAL_HIP(hipMemcpyAsync(s.h_inc_p, s.inc_p, ninc * 4, hipMemcpyDeviceToHost, st));
+      WAL_HIP(hipMemcpyAsync(s.h_inc_x, s.inc_x, ninc * 8, hipMemcpyDeviceToHost, st));
+      WAL_HIP(hipStreamSynchronize(st));
+      std::vector<std::pair<std::uint32_t, std::uint64_t>> v(ninc);
+      for (std::uint64_t i = 0; i < ninc; ++i) v[i] = {s.h_inc_p[i], s.h_inc_x[i]};
+      std::sort(v.begin(), v.end());
+      // keep a boundary only if the previous kept one's exit lands before it (else it lies inside that
+      // record, and the earlier fix-up covers it); each task may rewrite regions up to the next kept one
+      std::vector<std::pair<std::uint32_t, std::uint64_t>> kept;
+      std::uint64_t reach = 0;
+      for (const auto& pv : v) {
+        if (!kept.empty() && static_cast<std::uint64_t>(pv.first) + 1 <= reach) continue;
+        kept.push_back(pv);
+        reach = pv.second / kRegion;
+      }
+      std::uint32_t* tb = s.h_task;
+      std::uint32_t* tl = s.h_task + kMaxFix;
+      auto* te = reinterpret_cast<std::uint64_t*>(s.h_task + 2 * kMaxFix);
+      for (std::size_t k = 0; k < kept.size(); ++k) {
+        tb[k] = kept[k].first + 1;
+        tl[k] = k + 1 < kept.size() ? kept[k + 1].first + 1 : nreg;
+        te[k] = kept[k].second;
+      }
+      SweepArgs f = a;
+      f.nwaves = static_cast<std::uint32_t>(kept.size());
+      f.t_begin = s.d_task;
+      f.t_limit = s.d_task + kMaxFix;
+      f.t_entry = reinterpret_cast<const std::uint64_t*>(s.d_task + 2 * kMaxFix);
+      hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, static_cast<int>(kResIncons), static_cast<int>(kResIncons) + 1);
+      hipLaunchKernelGGL((wal_sweep<true>), dim3(blocks(f.nwaves, kSweepWaves)), dim3(kSweepThreads), 0, st, f);
+      hipLaunchKernelGGL(wal_bounds, dim3(blocks(nreg, 256)), dim3(256), 0, st, a, s.inc_p, s.inc_x, kMaxFix);
+      hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
+      WAL_HIP(hipGetLastError());
+      WAL_HIP(hipStreamSynchronize(st));
+      ++rounds;
+      if (rounds > static_cast<std::uint64_t>(nreg) + 8) return set_error(TKV_IO_ERROR, "WAL fix-up rounds did not settle");
     }
-    start += r.stop;
+    g_last[0] = rounds;
+    g_last[3] = clean ? 1 : 0;
+    if (s.h_res[5] > atomic_area) {  // atomic area overflow: a larger one, walk again
+      atomic_area = 2 * s.h_res[5];
+      continue;
+    }
+    const std::uint64_t nlong = s.h_res[1];
+    if (nlong || !clean) {
+      if (nlong) {
+        if (int rc = grow(&s.dense, &s.cap_dense, nlong, kDenseUnit)) return rc;
+        SweepArgs d = a;
+        std::uint32_t* got = nullptr;
+        long_view(s.dense, s.cap_dense, &d, &got);
+        hipLaunchKernelGGL(wal_long_gather, dim3(blocks(nlong, 256)), dim3(256), 0, st, a, s.l_base, W, s.res, d.l_off,
+                           d.l_len, d.l_crc, d.l_reg, d.l_meta);
+        WAL_HIP(hipGetLastError());
+        if (int rc = batch_device_impl(kAlgoCrc32, w, d.l_off, d.l_len, nullptr, got, nlong, st)) return rc;
+      }
+      hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, static_cast<int>(kResP), static_cast<int>(kResCnt) + 1);
+      launch_fin(a, s, nlong, st);
+      WAL_HIP(hipGetLastError());
+      WAL_HIP(hipStreamSynchronize(st));
+    }
+    *n_good = s.h_res[2];
+    *stop_offset = s.h_res[3];
+    return s.h_res[4] ? set_error(TKV_CORRUPTED, "corrupted WAL record") : TKV_OK;
   }
-  *needs_host_walk = true;
-  g_last[1] = 1;
-  return TKV_OK;
 }
 
 // memcpy of a large range into pinned staging on several host threads.
@@ -897,7 +990,45 @@ constexpr std::uint64_t kStageSlab = std::uint64_t(64) << 20;
 constexpr std::uint64_t kKeepImg = std::uint64_t(256) << 20;
 
 int host_image_locked(WalScratch& s, const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
-                      std::uint64_t* stop_offset, bool* needs_host_walk);
+                      std::uint64_t* stop_offset, bool* needs_host_walk) {
+  if (size > s.cap_img) {
+    (void)hipStreamSynchronize(s.st);
+    (void)hipFree(s.d_img);
+    s.d_img = nullptr;
+    s.cap_img = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&s.d_img), size) != hipSuccess) {
+      (void)hipGetLastError();  // the image does not fit the device: exact host walk instead
+      *needs_host_walk = true;
+      g_last[1] = 1;
+      return TKV_OK;
+    }
+    s.cap_img = size;
+  }
+  hipPointerAttribute_t attr;
+  const bool pinned = hipPointerGetAttributes(&attr, h_wal) == hipSuccess && attr.type == hipMemoryTypeHost;
+  if (!pinned) (void)hipGetLastError();
+  if (pinned) {
+    WAL_HIP(hipMemcpyAsync(s.d_img, h_wal, size, hipMemcpyHostToDevice, s.st));
+  } else {
+    // pageable: host threads fill one pinned slab while the copy engine drains the other
+    for (int i = 0; i < 2; ++i) {
+      if (!s.slab[i]) {
+        WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.slab[i]), kStageSlab, hipHostMallocDefault));
+        WAL_HIP(hipEventCreateWithFlags(&s.slab_free[i], hipEventDisableTiming));
+      }
+    }
+    int k = 0;
+    for (std::uint64_t off = 0; off < size; off += kStageSlab, k ^= 1) {
+      const std::uint64_t m = std::min(kStageSlab, size - off);
+      WAL_HIP(hipEventSynchronize(s.slab_free[k]));
+      stage_copy(s.slab[k], h_wal + off, m);
+      WAL_HIP(hipMemcpyAsync(s.d_img + off, s.slab[k], m, hipMemcpyHostToDevice, s.st));
+      WAL_HIP(hipEventRecord(s.slab_free[k], s.st));
+    }
+  }
+  WAL_HIP(hipStreamSynchronize(s.st));
+  return verify_locked(s, s.d_img, size, n_good, stop_offset, s.stc);
+}
 
 }  // namespace
 
@@ -908,13 +1039,11 @@ int wal_verify_device_impl(const std::uint8_t* d_wal, std::uint64_t size, std::u
   *stop_offset = 0;
   g_last[0] = g_last[1] = g_last[2] = g_last[3] = 0;
   if (size == 0) return TKV_OK;
-  if ((size + kWalPiece - 1) / kWalPiece >= 0xFFFFFFFFull)
-    return set_error(TKV_INVALID_ARGUMENT, "WAL image too large for the device walk");
   WalScratch* sp = nullptr;
   if (int rc = scratch(&sp)) return rc;
   WalScratch& s = *sp;
   std::lock_guard<std::mutex> lk(s.mu);
-  return verify_locked(s, d_wal, size, n_good, stop_offset, st, needs_host_walk);
+  return verify_locked(s, d_wal, size, n_good, stop_offset, st);
 }
 
 int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
@@ -924,10 +1053,6 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
   *stop_offset = 0;
   g_last[0] = g_last[1] = g_last[2] = g_last[3] = 0;
   if (size == 0) return TKV_OK;
-  if ((size + kWalPiece - 1) / kWalPiece >= 0xFFFFFFFFull) {
-    *needs_host_walk = true;
-    return TKV_OK;
-  }
   WalScratch* sp = nullptr;
   if (int rc = scratch(&sp)) return rc;
   WalScratch& s = *sp;
@@ -946,71 +1071,6 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
   }
   return rc;
 }
-
-namespace {
-int host_image_locked(WalScratch& s, const std::uint8_t* h_wal, std::uint64_t size, std::uint64_t* n_good,
-                      std::uint64_t* stop_offset, bool* needs_host_walk) {
-  if (size > s.cap_img) {
-    (void)hipStreamSynchronize(s.st);
-    (void)hipFree(s.d_img);
-    s.d_img = nullptr;
-    s.cap_img = 0;
-    if (hipMalloc(reinterpret_cast<void**>(&s.d_img), size) != hipSuccess) {
-      (void)hipGetLastError();  // the image does not fit the device: exact host walk instead
-      *needs_host_walk = true;
-      g_last[1] = 1;
-      return TKV_OK;
-    }
-    s.cap_img = size;
-  }
-  hipPointerAttribute_t attr;
-  const bool pinned = hipPointerGetAttributes(&attr, h_wal) == hipSuccess && attr.type == hipMemoryTypeHost;
-  if (!pinned) (void)hipGetLastError();
-  if (!pinned) {
-    for (int i = 0; i < 2; ++i) {
-      if (!s.slab[i]) {
-        WAL_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.slab[i]), kStageSlab, hipHostMallocDefault));
-        WAL_HIP(hipEventCreateWithFlags(&s.slab_free[i], hipEventDisableTiming));
-      }
-    }
-  }
-  // The image goes over in chunks on the copy stream (pageable sources through two pinned slabs that
-  // host threads fill while the copy engine drains the other). As each chunk lands, the compute
-  // stream scans and speculatively walks the pieces before it whose records' bytes are all resident
-  // (pieces ending at least kFrontMargin bytes before the end of what has landed), so only the last
-  // chunk's pieces and the stitching remain once the copy is done.
-  constexpr std::uint64_t kFrontMargin = kWalPiece + kWalLaneMax + 64;
-  WalArgs a;
-  if (int rc = pass_begin(s, s.d_img, size, s.stc, &a)) return rc;
-  std::uint64_t fronted = 0;
-  int k = 0;
-  for (std::uint64_t off = 0; off < size; off += kStageSlab, k ^= 1) {
-    const std::uint64_t m = std::min(kStageSlab, size - off);
-    if (pinned) {
-      WAL_HIP(hipMemcpyAsync(s.d_img + off, h_wal + off, m, hipMemcpyHostToDevice, s.st));
-    } else {
-      WAL_HIP(hipEventSynchronize(s.slab_free[k]));
-      stage_copy(s.slab[k], h_wal + off, m);
-      WAL_HIP(hipMemcpyAsync(s.d_img + off, s.slab[k], m, hipMemcpyHostToDevice, s.st));
-      WAL_HIP(hipEventRecord(s.slab_free[k], s.st));
-    }
-    WAL_HIP(hipEventRecord(s.landed[k], s.st));
-    WAL_HIP(hipStreamWaitEvent(s.stc, s.landed[k], 0));
-    const bool last = off + m >= size;
-    const std::uint64_t k_hi = last ? a.K : (off + m > kFrontMargin ? (off + m - kFrontMargin) / kWalPiece : 0);
-    if (k_hi > fronted) {
-      pass_front(a, fronted, k_hi, s.stc);
-      fronted = k_hi;
-    }
-  }
-  WAL_HIP(hipGetLastError());
-  PassResult r;
-  g_last[0] = 1;
-  g_last[3] = 1;  // the first device pass starts here; cleared if it needs the pointer-jumping stitch
-  if (int rc = pass_tail(s, a, s.stc, &r)) return rc;
-  return verify_locked(s, s.d_img, size, n_good, stop_offset, s.stc, needs_host_walk, &r);
-}
-}  // namespace
 
 }  // namespace tkv
 

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 
 #include "tkv_crc32.h"
@@ -34,24 +35,10 @@ namespace tkv {
 namespace {
 
 constexpr std::uint32_t kRecMeta = 26;  // wal.hpp kMetadataSize: 8-byte header + op, seq, tombstone, key/value lengths
-// A/B builds only (TKV_AB_REC16=1): narrow windows (4-5 granules, payloads up to 54 bytes) on the
-// 64 KiB 16-replica table image with two 768-thread workgroups per CU (24 waves, at most 80 VGPRs).
-// Measured 3 % slower than the 128 KiB image with one 1024-thread workgroup per CU
-// (profiles/r4/lanes16/rec_probe_rec16.jsonl), which every window keeps.
-#ifndef TKV_AB_REC16
-#define TKV_AB_REC16 0
-#endif
-#ifndef TKV_AB_REC16_AHEAD
-#define TKV_AB_REC16_AHEAD 1
-#endif
-#ifndef TKV_AB_REC_LDS  // (A/B builds: 0 keeps narrow windows on wal_rec_lanes)
-#define TKV_AB_REC_LDS 1
-#endif
-template <bool W16>
-struct RecShape {
-  static constexpr unsigned kThreads = W16 ? 768 : 1024;
-  static constexpr unsigned kWgPerCu = W16 ? 2 : 1;
-};
+// The granule kernel uses the 128 KiB table image with one 1024-thread workgroup per CU (narrow
+// windows on the 64 KiB image with two 768-thread workgroups measured 3 % slower,
+// profiles/r4/lanes16/rec_probe_rec16.jsonl).
+constexpr unsigned kRecThreadsN = 1024;
 
 struct RecArgs {
   const std::uint8_t* w;
@@ -100,31 +87,21 @@ __device__ __forceinline__ std::uint32_t rec_fold(const std::uint32_t* lds, cons
   return r.value();
 }
 
-// NG granules per record window; AHEAD steps of granules in flight (3 for narrow windows, 2 at 6
-// granules, 1 for the wide ones, whose three slots would spill at 16 waves per CU).
-#ifndef TKV_AB_REC_AHEAD0  // (A/B builds: 1 = no granules in flight ahead of the fold)
-#define TKV_AB_REC_AHEAD0 0
-#endif
-// 4-granule record windows load at the fold, no step ahead: in one process against 3 and 1 steps in
-// flight (profiles/r4/lanes_r/rec4_probe.jsonl) 28-byte payloads 0.2946 -> 0.2851 ms (+3.3 %; +5.5 %
-// on another box); wider windows lost with it (mixed 22-80 B -4.7 %).
-#ifndef TKV_AB_REC4_AHEAD  // (A/B builds: steps in flight for 4-granule windows)
-#define TKV_AB_REC4_AHEAD 0
-#endif
-template <int NG, int AHEAD, bool W16>
-__global__ __launch_bounds__(RecShape<W16>::kThreads)
-__attribute__((amdgpu_waves_per_eu(RecShape<W16>::kWgPerCu * RecShape<W16>::kThreads / 256))) void
-wal_rec_lanes(RecArgs a, const DeviceTables* tabs) {
+// NG granules per record window; AHEAD steps of granules in flight: 3 at 5 granules, 2 at 6, 1 for
+// the wide ones (whose three slots would spill at 16 waves per CU), none at 4 (4-granule windows load
+// at the fold: in one process against 3 and 1 steps in flight, profiles/r4/lanes_r/rec4_probe.jsonl,
+// 28-byte payloads 0.2946 -> 0.2851 ms, +3.3 %; wider windows lost with it, mixed 22-80 B -4.7 %).
+template <int NG, int AHEAD>
+__global__ __launch_bounds__(kRecThreadsN) void wal_rec_lanes(RecArgs a, const DeviceTables* tabs) {
   constexpr int ND = 4 * NG - 4;      // realigned dwords of the window
   constexpr int NPAY = ND - 3;        // whole payload dwords folded from the window (payload at dword 2; one spare for the tail)
   constexpr int RING = 4;             // offsets are fetched RING steps ahead of their granules
   constexpr int DRING = AHEAD == 1 ? 2 : 4;
   static_assert(AHEAD >= 0 && AHEAD <= 3, "granules up to three steps ahead");
-  __shared__ std::uint32_t lds[W16 ? kLdsSliceWords / 2 : kLdsSliceWords];
-  if constexpr (W16) dev::fill_lds_slicing16(tabs, lds);
-  else dev::fill_lds_slicing(tabs, lds);
+  __shared__ std::uint32_t lds[kLdsSliceWords];
+  dev::fill_lds_slicing(tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
-  const dev::LaneConst kc = W16 ? dev::lane_const16(lane) : dev::lane_const(lane);
+  const dev::LaneConst kc = dev::lane_const(lane);
   __syncthreads();
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint64_t W = a.nwaves, n = a.n;
@@ -235,9 +212,6 @@ __device__ __forceinline__ std::uint32_t wave_max_u32(std::uint32_t v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
-#ifndef TKV_AB_REC_LDS_STOREWAIT  // (A/B builds: 1 = every step also waits for the previous step's store)
-#define TKV_AB_REC_LDS_STOREWAIT 0
-#endif
 template <int NG>
 __global__ __launch_bounds__(kRecLdsThreads) void wal_rec_lds(RecArgs a, const DeviceTables* tabs) {
   constexpr int ND = 4 * NG - 4;  // realigned dwords of the window
@@ -310,8 +284,9 @@ __global__ __launch_bounds__(kRecLdsThreads) void wal_rec_lds(RecArgs a, const D
   for (std::uint32_t j = 0; j < ns; ++j) {
     dev::set_prio_from_left<3>(ns - j, ns);
     // step j's span and step j+1's offsets have landed. With a result array, step j-1's result store
-    // is the newest memory operation and need not be waited for (vmcnt counts stores too)
-    if (TKV_AB_REC_LDS_STOREWAIT == 0 && a.crc && j > 0u) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    // is the newest memory operation and need not be waited for (vmcnt counts stores too; waiting for
+    // it measured 0.8 % slower, profiles/r4/storewait/)
+    if (a.crc && j > 0u) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const std::uint32_t k = j & 1u;
     const std::uint32_t off = dev::lds_at(lds, offs0 + k * 256u + 4u * lane);  // (read before its buffer is reused)
@@ -378,31 +353,30 @@ __global__ __launch_bounds__(kRecLdsThreads) void wal_rec_lds(RecArgs a, const D
 }
 
 int cu_count() {
-  static int cached[64] = {};
+  static std::atomic<int> cached[64] = {};  // (concurrent first calls store the same value)
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cached[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    cached[dev] = n;
+  int c = cached[dev].load(std::memory_order_relaxed);
+  if (c == 0) {
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cached[dev].store(c, std::memory_order_relaxed);
   }
-  return cached[dev];
+  return c;
 }
 
 // The record check over n records (first_bad preset to n by the caller's stream order).
 void launch_records(RecArgs a, std::uint32_t max_payload, int ncu, const DeviceTables* tabs, hipStream_t st) {
   const std::uint64_t steps = (a.n + 63) / 64;
-  // window: NG granules hold the header, the key/value lengths and a payload of up to 16 NG - 26 bytes
-  // at any alignment (36-byte payloads: 4 granules; 64: 6; 100: 8); longer ones continue 64 bytes at
-  // a time. Records are latency-bound like the lane kernel (profiles/r4/rec_check/): narrow windows keep
-  // three steps of granules in flight, 6 granules two, wider ones one (registers).
+  // window: NG granules hold the header, the key/value lengths and a first fold of 16 NG - 28 payload
+  // bytes at any alignment (36-byte payloads: 4 granules; 68: 6; 100: 8); longer ones continue 64 bytes
+  // at a time. Records are latency-bound like the lane kernel (profiles/r4/rec_check/).
   const std::uint32_t ng =
-      std::min<std::uint32_t>(8u, std::max<std::uint32_t>(4u, (std::min<std::uint32_t>(max_payload, 1024u) + 26u + 15u) / 16u));
+      std::min<std::uint32_t>(8u, std::max<std::uint32_t>(4u, (std::min<std::uint32_t>(max_payload, 1024u) + 28u + 15u) / 16u));
   // narrow windows with payloads of at least 32 bytes: staged through LDS (wal_rec_lds). One process
   // against wal_rec_lanes (profiles/r4/rec_lds/): 44-byte records (36-byte payloads) 2957 -> 3099 GB/s
   // of payload; 36-byte records (28-byte payloads) 2813 -> 2591, where the per-step cost (span
   // reduction, copy, full wait) outweighs what the copy saves, so shorter payloads keep wal_rec_lanes.
-  if (TKV_AB_REC_LDS && ng <= 5 && max_payload >= 32u) {
+  if (ng <= 5 && max_payload >= 32u) {
     constexpr std::uint64_t waves = kRecLdsThreads / 64;
     const std::uint64_t grid =
         std::max<std::uint64_t>(1, std::min<std::uint64_t>(static_cast<std::uint64_t>(ncu), (steps + waves - 1) / waves));
@@ -411,22 +385,17 @@ void launch_records(RecArgs a, std::uint32_t max_payload, int ncu, const DeviceT
     else hipLaunchKernelGGL((wal_rec_lds<5>), dim3(static_cast<unsigned>(grid)), dim3(kRecLdsThreads), 0, st, a, tabs);
     return;
   }
-  const bool w16 = TKV_AB_REC16 && ng <= 5;
-  const std::uint64_t threads = w16 ? RecShape<true>::kThreads : RecShape<false>::kThreads;
-  const std::uint64_t per_cu = w16 ? RecShape<true>::kWgPerCu : RecShape<false>::kWgPerCu;
-  const std::uint64_t waves = threads / 64;
-  const std::uint64_t grid = std::max<std::uint64_t>(
-      1, std::min<std::uint64_t>(static_cast<std::uint64_t>(ncu) * per_cu, (steps + waves - 1) / waves));
+  const std::uint64_t waves = kRecThreadsN / 64;
+  const std::uint64_t grid =
+      std::max<std::uint64_t>(1, std::min<std::uint64_t>(static_cast<std::uint64_t>(ncu), (steps + waves - 1) / waves));
   a.nwaves = static_cast<std::uint32_t>(grid * waves);
-  const dim3 g(static_cast<unsigned>(grid)), b(static_cast<unsigned>(threads));
-  switch (w16 ? ng : ng + 16u) {
-    case 4: hipLaunchKernelGGL((wal_rec_lanes<4, TKV_AB_REC16_AHEAD, true>), g, b, 0, st, a, tabs); break;
-    case 5: hipLaunchKernelGGL((wal_rec_lanes<5, TKV_AB_REC16_AHEAD, true>), g, b, 0, st, a, tabs); break;
-    case 20: hipLaunchKernelGGL((wal_rec_lanes<4, TKV_AB_REC_AHEAD0 ? 0 : TKV_AB_REC4_AHEAD, false>), g, b, 0, st, a, tabs); break;
-    case 21: hipLaunchKernelGGL((wal_rec_lanes<5, TKV_AB_REC_AHEAD0 ? 0 : 3, false>), g, b, 0, st, a, tabs); break;
-    case 22: hipLaunchKernelGGL((wal_rec_lanes<6, TKV_AB_REC_AHEAD0 ? 0 : 2, false>), g, b, 0, st, a, tabs); break;
-    case 23: hipLaunchKernelGGL((wal_rec_lanes<7, TKV_AB_REC_AHEAD0 ? 0 : 1, false>), g, b, 0, st, a, tabs); break;
-    default: hipLaunchKernelGGL((wal_rec_lanes<8, TKV_AB_REC_AHEAD0 ? 0 : 1, false>), g, b, 0, st, a, tabs); break;
+  const dim3 g(static_cast<unsigned>(grid)), b(kRecThreadsN);
+  switch (ng) {
+    case 4: hipLaunchKernelGGL((wal_rec_lanes<4, 0>), g, b, 0, st, a, tabs); break;
+    case 5: hipLaunchKernelGGL((wal_rec_lanes<5, 3>), g, b, 0, st, a, tabs); break;
+    case 6: hipLaunchKernelGGL((wal_rec_lanes<6, 2>), g, b, 0, st, a, tabs); break;
+    case 7: hipLaunchKernelGGL((wal_rec_lanes<7, 1>), g, b, 0, st, a, tabs); break;
+    default: hipLaunchKernelGGL((wal_rec_lanes<8, 1>), g, b, 0, st, a, tabs); break;
   }
 }
 

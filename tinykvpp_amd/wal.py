@@ -96,16 +96,24 @@ def check_records_device(image, rec_offsets, max_payload=64, crc_out=None, first
     torch op issued there (tkv_wal_check_records_device)."""
     import torch
     from .crc32 import _check_data, _check_vec, _launch_stream
+    if image.dtype != torch.uint8:
+        raise ValueError("image must be a uint8 tensor (its size in bytes is its numel)")
     _check_data(image)
     n = rec_offsets.numel()
     if rec_offsets.dtype not in (torch.int32,):
         raise ValueError("rec_offsets must be an int32 tensor (u32 offsets)")
     _check_vec("rec_offsets", rec_offsets, torch.int32, n, image.device)
+    # outputs allocated here are tied to a non-current stream for the caching allocator (as _out_vec)
+    other = stream is not None and stream != torch.cuda.current_stream(image.device)
     if crc_out is None:
         crc_out = torch.empty(n, dtype=torch.int32, device=image.device)
+        if other:
+            crc_out.record_stream(stream)
     _check_vec("crc_out", crc_out, torch.int32, n, image.device)
     if first_bad is None:
         first_bad = torch.empty(1, dtype=torch.int64, device=image.device)
+        if other:
+            first_bad.record_stream(stream)
     _check_vec("first_bad", first_bad, torch.int64, 1, image.device)
     check(load_library().tkv_wal_check_records_device(
         ctypes.c_void_p(image.data_ptr()), image.numel(), ctypes.c_void_p(rec_offsets.data_ptr()), n,
