@@ -4,11 +4,12 @@
 // of every record (wal.cpp:89-96) and the key/value bounds check (wal.cpp:118-121), ending in the first
 // corruption. The image is read from HBM once (round 5).
 //
-// wal_sweep: every wave streams a contiguous chunk of the image, one region of kRegion bytes at a
-// time. Regions are loaded kAhead steps ahead into registers (coalesced 16-byte loads) and written
-// into the wave's LDS window together with the first kOver bytes of the next region, so a record that
-// starts in the region and has a payload of at most kLaneFold bytes lies wholly in the window. Per
-// region:
+// wal_sweep: every wave streams a contiguous chunk of the image, one region of kRegion = 10 KiB at a
+// time. Regions are loaded a region ahead into registers (coalesced 16-byte buffer loads whose
+// descriptor ends at the image's end) and written into the wave's LDS window together with the first
+// kOver bytes of the next region, so a record that starts in the region and has a payload of at most
+// kLaneFold bytes lies wholly in the window. Eight waves share one copy of the 64 KiB slicing tables
+// (16 replicas, at LDS address 0). Positions are 32-bit for images below 4 GiB. Per region:
 //  1. walk: lane l owns the piece [rs + kPiece l, + kPiece). The lane holding the region's entry E
 //     (where the chain leaves the previous region) starts there; every later lane starts at the first
 //     plausible header of its piece (one the reference encoder could have written, wal.cpp:19-61),
@@ -51,10 +52,7 @@ namespace {
 
 constexpr std::uint64_t kWalMeta = 26;          // wal.hpp:21-27 kMetadataSize
 constexpr std::uint64_t kNone = ~0ull;
-#ifndef TKV_X_REGION
-#define TKV_X_REGION 10240
-#endif
-constexpr std::uint32_t kRegion = TKV_X_REGION;  // image bytes per region (one wave step)
+constexpr std::uint32_t kRegion = 10240;  // image bytes per region (one wave step)
 constexpr int kRows = kRegion / 1024;           // 1 KiB load rows per region
 constexpr std::uint32_t kPiece = kRegion / 64;  // bytes per lane piece
 constexpr std::uint32_t kOver = 256;            // bytes of the next region behind the window
@@ -70,7 +68,7 @@ constexpr unsigned kHres = 16;                  // words of the pinned result bl
 static_assert(kRegion % 1024 == 0 && kPiece % 16 == 0, "region = whole 1 KiB load rows");
 static_assert(kOver >= kLaneFold + 8 && kOver >= kWalMeta, "a lane-folded record ends inside the window");
 static_assert(kList * 26 >= kRegion + 26 * 2, "records of >= 26 bytes fit the list");
-static_assert(kLdsSliceWords * 2 + kSweepWaves * kWinBytes <= 163840, "LDS");
+static_assert(kLdsSliceWords * 2 + kSweepWaves * kWinBytes + 4 * (kLaneFold + 1) <= 163840, "LDS");
 static_assert(kStore <= 8, "list counts per lane < 16");
 
 // Region flags (low byte of fl[]; the region's version, bumped by every fix-up rewrite, above it).
@@ -88,7 +86,7 @@ struct SweepArgs {
   const std::uint8_t* w;
   std::uint64_t size;
   std::uintptr_t al0;         // w rounded down to 16 bytes
-  std::uintptr_t glast;       // the image's last 16-byte granule (loads past it are clamped there)
+  std::uintptr_t gend;        // the end of the image's last 16-byte granule (loads stop there)
   std::uint32_t o;            // w - al0
   std::uint32_t nreg;
   std::uint32_t nwaves;       // sweep: chunks; fix-up: tasks
@@ -116,11 +114,10 @@ struct SweepArgs {
   const DeviceTables* tabs;
 };
 
-__device__ __forceinline__ std::uint32_t le1_bytes4(std::uint32_t d) {
-  // 4-bit mask: bit i set iff byte i of d is 0 or 1
-  const std::uint32_t x = d & 0xFEFEFEFEu;
-  const std::uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu) & 0x80808080u;
-  return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
+__device__ __forceinline__ std::uint32_t le1_marks(std::uint32_t d) {
+  // bit 7 of byte i set iff byte i of d is 0 or 1 (bit 7 of (b & 0x7E) + 0x7F is clear iff no bit 1-6
+  // of b is set; no byte carries into the next)
+  return ~(((d & 0x7E7E7E7Eu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
 }
 
 // Little-endian u32 at byte b of the window (dword-aligned reads, v_alignbyte).
@@ -131,11 +128,27 @@ __device__ __forceinline__ std::uint32_t rd32(const std::uint8_t* win, std::uint
   return __builtin_amdgcn_alignbyte(hi, lo, b & 3u);
 }
 
-__device__ __forceinline__ std::uint64_t shfl64(std::uint64_t v, std::uint32_t src) {
-  const std::uint32_t lo = static_cast<std::uint32_t>(__shfl(static_cast<int>(static_cast<std::uint32_t>(v)), static_cast<int>(src), 64));
-  const std::uint32_t hi = static_cast<std::uint32_t>(__shfl(static_cast<int>(static_cast<std::uint32_t>(v >> 32)), static_cast<int>(src), 64));
+// Image positions in the sweep: u32 for images of at most kPos32Max bytes (every position, the
+// region ends and kNone fit), u64 beyond.
+constexpr std::uint64_t kPos32Max = 0xFFFF0000ull;
+template <typename P>
+constexpr P kNoneP = static_cast<P>(~0ull);
+template <typename P>
+__device__ __forceinline__ std::uint64_t widen(P v) {
+  return v == kNoneP<P> ? kNone : static_cast<std::uint64_t>(v);
+}
+__device__ __forceinline__ std::uint32_t shfl_pos(std::uint32_t v, std::uint32_t src) {
+  return static_cast<std::uint32_t>(__shfl(static_cast<int>(v), static_cast<int>(src), 64));
+}
+__device__ __forceinline__ std::uint64_t shfl_pos(std::uint64_t v, std::uint32_t src) {
+  const std::uint32_t lo = shfl_pos(static_cast<std::uint32_t>(v), src);
+  const std::uint32_t hi = shfl_pos(static_cast<std::uint32_t>(v >> 32), src);
   return (static_cast<std::uint64_t>(hi) << 32) | lo;
 }
+__device__ __forceinline__ std::uint32_t readlane_pos(std::uint32_t v, std::uint32_t l) {
+  return static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(l)));
+}
+__device__ __forceinline__ std::uint64_t readlane_pos(std::uint64_t v, std::uint32_t l) { return dev::readlane64(v, l); }
 
 // Exclusive prefix over the lanes of a value < 2^BITS, and its total (bit planes through ballots).
 template <int BITS>
@@ -161,35 +174,64 @@ __device__ __forceinline__ std::uint32_t wave_min_u32(std::uint32_t v) {
 
 // The first plausible header in [ps, qe) (qe - ps <= kSearchStep; every position there has 26 bytes
 // in the image): op and tombstone bytes (p+8, p+17) 0 or 1, then record_len = 18 + klen + vlen and
-// record_len + 8 within the image. The 0/1 marks of 80 window bytes from ps + 8 are computed
-// byte-parallel from five 16-byte reads; only positions that pass them are checked in full.
-__device__ __forceinline__ std::uint64_t search_piece(const std::uint8_t* win, std::uint64_t rs, std::uint32_t o,
-                                                      std::uint64_t ps, std::uint64_t qe, std::uint64_t size) {
-  if (ps >= qe) return kNone;
+// record_len + 8 within the image. Byte-parallel over the 76 window bytes from the 16-byte granule of
+// ps + 8 (five 16-byte reads): z marks each byte that is 0 or 1 (bit 7), c = z & (z 9 bytes on)
+// marks the positions passing both, and the c of four dwords are packed into one word per 16
+// positions, transposed (bit 8 j + i = byte j of dword i; 4 shifts and 2 ORs, no multiply). ps + 8 is
+// at the same granule offset sh in every lane (pieces and steps are multiples of 16 bytes), so the
+// mask of the positions in front of it is wave-uniform. Candidates are taken in position order and
+// checked in full.
+static_assert(kPiece % 16 == 0 && kSearchStep % 16 == 0 && kSearchStep + 15 + 9 < 80, "search granules");
+template <typename P>
+__device__ __forceinline__ P search_piece(const std::uint8_t* win, P rs, std::uint32_t o, P ps, P qe, P size) {
+  if (ps >= qe) return kNoneP<P>;
   const std::uint32_t b0 = static_cast<std::uint32_t>(ps - rs) + o + 8u;
-  const std::uint32_t a16 = b0 & ~15u, sh = b0 & 15u;
+  const std::uint32_t a16 = b0 & ~15u;
+  const std::uint32_t sh = __builtin_amdgcn_readfirstlane(b0 & 15u);
   const uint4* g = reinterpret_cast<const uint4*>(win + a16);
-  std::uint64_t m0 = 0;
+  std::uint32_t z[20];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 5; ++i) {
     const uint4 v = g[i];
-    const std::uint32_t m = le1_bytes4(v.x) | le1_bytes4(v.y) << 4 | le1_bytes4(v.z) << 8 | le1_bytes4(v.w) << 12;
-    m0 |= static_cast<std::uint64_t>(m) << (16 * i);
+    z[4 * i] = le1_marks(v.x);
+    z[4 * i + 1] = le1_marks(v.y);
+    z[4 * i + 2] = le1_marks(v.z);
+    z[4 * i + 3] = le1_marks(v.w);
   }
-  const uint4 v4 = g[4];
-  const std::uint32_t m1 = le1_bytes4(v4.x) | le1_bytes4(v4.y) << 4 | le1_bytes4(v4.z) << 8 | le1_bytes4(v4.w) << 12;
-  const std::uint64_t M = sh ? (m0 >> sh) | (static_cast<std::uint64_t>(m1) << (64u - sh)) : m0;
-  const std::uint32_t span = static_cast<std::uint32_t>(qe - ps);  // <= kSearchStep < 64
-  std::uint64_t cand = M & (M >> 9) & ((1ull << span) - 1ull);
-  while (cand) {
-    const std::uint32_t i = static_cast<std::uint32_t>(__builtin_ctzll(cand));
-    const std::uint32_t b = b0 - 8u + i;
+  std::uint32_t y[4];
+#pragma unroll
+  for (int gi = 0; gi < 4; ++gi) {
+    std::uint32_t c[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = 4 * gi + i;
+      c[i] = z[k] & __builtin_amdgcn_alignbyte(z[k + 3], z[k + 2], 1u);
+    }
+    y[gi] = (c[0] >> 7) | (c[1] >> 6) | (c[2] >> 5) | (c[3] >> 4);
+  }
+  // positions p = 4 i + j < sh of the first group (wave-uniform)
+  const std::uint32_t si = sh >> 2, sj = sh & 3u;
+  y[0] &= ((0xFu << (si + 1u)) & 0xFu) * 0x01010101u | ((0x01010101u << (8u * sj)) << si);
+  const std::uint32_t span = static_cast<std::uint32_t>(qe - ps);  // <= kSearchStep
+  std::uint64_t m0 = y[0] | static_cast<std::uint64_t>(y[1]) << 32, m1 = y[2] | static_cast<std::uint64_t>(y[3]) << 32;
+  while (m0 | m1) {
+    const bool lo = m0 != 0;
+    const std::uint64_t cur = lo ? m0 : m1;
+    const bool hw = static_cast<std::uint32_t>(cur) == 0u;
+    const std::uint32_t yv = hw ? static_cast<std::uint32_t>(cur >> 32) : static_cast<std::uint32_t>(cur);
+    const std::uint32_t gi = (lo ? 0u : 2u) + (hw ? 1u : 0u);
+    const std::uint32_t i = static_cast<std::uint32_t>(__builtin_ctz((yv | yv >> 8 | yv >> 16 | yv >> 24) & 0xFu));
+    const std::uint32_t j = static_cast<std::uint32_t>(__builtin_ctz((yv >> i) & 0x01010101u)) >> 3;
+    const std::uint32_t pos = 16u * gi + 4u * i + j - sh;  // from ps
+    if (pos >= span) return kNoneP<P>;  // (every later candidate lies further on)
+    const std::uint32_t b = b0 - 8u + pos;
     const std::uint64_t rl = rd32(win, b), kl = rd32(win, b + 18u), vl = rd32(win, b + 22u);
-    const std::uint64_t q = ps + i;
-    if (rl == 18u + kl + vl && rl + 8u <= size - q) return q;
-    cand &= cand - 1ull;
+    const P q = ps + pos;
+    if (rl == 18u + kl + vl && static_cast<P>(rl) <= size - q - 8u) return q;  // (size - q >= 26)
+    const std::uint64_t bit = 1ull << ((hw ? 32u : 0u) + 8u * j + i);
+    if (lo) m0 &= ~bit; else m1 &= ~bit;
   }
-  return kNone;
+  return kNoneP<P>;
 }
 
 // The records that start in [s, pe) from s (wal.cpp:63-87), read from the window. n: their count;
@@ -197,16 +239,18 @@ __device__ __forceinline__ std::uint64_t search_piece(const std::uint8_t* win, s
 // the chain broke (broke); tiny: the index of the first with record_len < 18 (bad for certain: its
 // key/value fields cannot fit, wal.cpp:118-121), kStore if none among the stored ones. The records in
 // front of a lane's first tiny one are at least 26 bytes long, so it is always among the stored.
+template <typename P>
 struct Walk {
   std::uint32_t st[kStore];
   std::uint32_t n, tiny;
-  std::uint64_t x;
+  P x;
   bool broke;
 };
-__device__ __forceinline__ void walk_piece(const std::uint8_t* win, std::uint64_t rs, std::uint32_t o, std::uint64_t s,
-                                           std::uint64_t pe, std::uint64_t size, bool go, Walk& wk) {
-  std::uint64_t p = s;
-  bool act = go && s != kNone;
+template <typename P>
+__device__ __forceinline__ void walk_piece(const std::uint8_t* win, P rs, std::uint32_t o, P s, P pe, P size, bool go,
+                                           Walk<P>& wk) {
+  P p = s;
+  bool act = go && s != kNoneP<P>;
   if (go) {
     wk.n = 0;
     wk.tiny = kStore;
@@ -218,7 +262,7 @@ __device__ __forceinline__ void walk_piece(const std::uint8_t* win, std::uint64_
       act = false;
     } else {
       const std::uint32_t rl = rd32(win, static_cast<std::uint32_t>(p - rs) + o);
-      if (static_cast<std::uint64_t>(rl) + 8u > size - p) {
+      if (static_cast<P>(rl) > size - p - 8u) {  // (size - p >= 26)
         wk.broke = true;
         act = false;
       } else {
@@ -227,7 +271,7 @@ __device__ __forceinline__ void walk_piece(const std::uint8_t* win, std::uint64_
           if (rl < 18u && wk.tiny == kStore) wk.tiny = j;
         }
         wk.n += 1;
-        p += 8u + static_cast<std::uint64_t>(rl);
+        p += 8u + static_cast<P>(rl);
       }
     }
   };
@@ -250,70 +294,86 @@ __device__ __forceinline__ void walk_piece(const std::uint8_t* win, std::uint64_
   if (go) wk.x = p;
 }
 
-// CRC-32 register (init 0xFFFFFFFF, not finalized) of the L window bytes at b, folded by this lane:
-// 64-byte chunks realigned from five 16-byte reads, slicing-by-4 lookups, Sarwate steps for the
-// last 1-3 bytes (crc32.cpp:9-16).
-__device__ __forceinline__ std::uint32_t fold_win(const std::uint8_t* win, const std::uint32_t* tab, const dev::LaneConst& kc,
-                                                  std::uint32_t b, std::uint32_t L) {
-  dev::Reg r{0xFFFFFFFFu, 0u};
-  const std::uint32_t nf = L >> 2, tb = L & 3u;
-  const std::uint32_t a = b & ~15u, o = b & 15u;
-  const std::uint32_t nch = (L + 63u) >> 6;
-  for (std::uint32_t c = 0; __ballot(c < nch) != 0; ++c) {
-    if (c < nch) {
-      uint4 g[dev::kLaneGran];
+__device__ __forceinline__ std::uint32_t wave_max_u32(std::uint32_t v) {
 #pragma unroll
-      for (int i = 0; i < dev::kLaneGran; ++i) g[i] = *reinterpret_cast<const uint4*>(win + a + 64u * c + 16u * i);
-      std::uint32_t d[16];
-      dev::lane_dwords<1>(g, o, d);
-#pragma unroll
-      for (std::uint32_t k = 0; k < 16; ++k) {
-        const std::uint32_t idx = 16u * c + k;
-        if (idx < nf) dev::slice4(tab, r, d[k], kc);
-        else if (idx == nf && tb != 0u) r = dev::Reg{dev::sarwate_bytes(tab, kc, r.value(), d[k], tb), 0u};
-      }
-    }
-  }
-  return r.value();
+  for (int m = 32; m > 0; m >>= 1) v = std::max<std::uint32_t>(v, static_cast<std::uint32_t>(__shfl_xor(static_cast<int>(v), m, 64)));
+  return v;
 }
 
-#ifndef TKV_X_BODY
-#define TKV_X_BODY 4
-#endif
-#ifndef TKV_X_AHEAD
-#define TKV_X_AHEAD 2
-#endif
-constexpr int kAhead = TKV_X_BODY == 0 ? 4 : TKV_X_AHEAD;  // regions in registers: the current one and the rest in flight
+// CRC-32 (finalized) of the L <= kLaneFold window bytes at s, one record per lane. The record is read
+// from s - z, z = 4 nd - L (nd = its dwords), so that it ends on a dword; the z bytes in front are
+// zeroed in its first dword (leading zeros leave a zero register at 0). Every lane steps through the
+// round's largest dword count, its register frozen after its own nd (selects, no branch: the LDS
+// waits stay countable; exec-masked steps measured slower). Dword i is v_alignbyte of two
+// dword-aligned window reads. The initial register enters as inj[L] = Shift_L(0xFFFFFFFF)
+// (crc_s(D) = Shift_|D|(s) ^ crc_0(D)); slicing-by-4 into the 64 KiB table image (crc32.cpp:9-16
+// restated). (Two or three records per lane at once, as independent chains, measured slower.)
+__device__ __forceinline__ std::uint32_t fold_lane(const std::uint8_t* win, const std::uint32_t* tab, const std::uint32_t* inj,
+                                                   const dev::LaneConst& kc, std::uint32_t s, std::uint32_t L) {
+  const std::uint32_t nd = (L + 3u) >> 2;
+  const std::uint32_t nmax = __builtin_amdgcn_readfirstlane(wave_max_u32(nd));
+  const std::uint32_t z = 4u * nd - L;
+  const std::uint32_t b0 = s - z;  // (s >= 8: b0 >= 5)
+  const std::uint32_t sh = b0 & 3u;
+  const std::uint32_t* w = reinterpret_cast<const std::uint32_t*>(win + (b0 & ~3u));
+  std::uint32_t lo = w[1];
+  dev::Reg r{0u, 0u};
+  dev::slice4(tab, r, __builtin_amdgcn_alignbyte(lo, w[0], sh) & (~0u << (8u * z)), kc);
+  if (nd == 0u) r = dev::Reg{0u, 0u};
+#pragma unroll 2
+  for (std::uint32_t i = 1; i < nmax; ++i) {
+    const std::uint32_t hi = w[i + 1u];
+    dev::Reg t = r;
+    dev::slice4(tab, t, __builtin_amdgcn_alignbyte(hi, lo, sh), kc);
+    if (i < nd) r = t;
+    lo = hi;
+  }
+  return r.value() ^ inj[L] ^ 0xFFFFFFFFu;
+}
 
-// Region r's granules: 1 KiB load rows k = 0..kRows-1, lane l's 16 bytes at row offset 16 l. Rows
-// past `rows` (regions the wave will not write into its window) read the image's last granule
-// instead, one line for the whole wave: every load is issued, so the compiler counts them exactly.
+constexpr int kAhead = 2;  // regions in registers: the current one and the next, in flight
+
+// Region r's granules: 1 KiB load rows k = 0..kRows-1, lane l's 16 bytes at row offset 16 l, as
+// buffer loads through a descriptor over the region's first `rows` rows, cut at the image's end: the
+// hardware range check returns zeros past it and fetches nothing (regions the wave will not write
+// into its window have rows = 0). Every load is issued, so the compiler counts them exactly.
 __device__ __forceinline__ void load_region(const SweepArgs& a, std::uint64_t r, std::uint32_t lane, int rows, uint4 (&g)[kRows]) {
-  const std::uintptr_t base = a.al0 + r * kRegion + 16u * lane;
+  const std::uint64_t ad = a.al0 + r * kRegion;
+  const std::uint64_t base = static_cast<std::uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<std::uint32_t>(ad))) |
+                             static_cast<std::uint64_t>(static_cast<std::uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<std::uint32_t>(ad >> 32)))) << 32;
+  const std::uint64_t left = a.gend > base ? a.gend - base : 0u;
+  const std::uint32_t nrec = __builtin_amdgcn_readfirstlane(static_cast<std::uint32_t>(std::min<std::uint64_t>(left, 1024u * static_cast<std::uint32_t>(rows))));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, nrec, 0x00020000);
 #pragma unroll
   for (int k = 0; k < kRows; ++k) {
-    const std::uintptr_t p = base + 1024u * k;
-    g[k] = dev::gload16(k < rows && p < a.glast ? p : a.glast);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16u * lane + 1024u * k, 0, 0);
+    g[k] = uint4{v[0], v[1], v[2], v[3]};
   }
 }
 
 // One wave: regions [r0, limit) from entry e (kNone: search). Fix-up mode stops where the exit meets
 // the stored entry of the next region. No global load in the loop waits for a value except in fix-up
 // mode (a wait on a load drains every prefetch issued before it).
-template <bool FIXUP>
+template <bool FIXUP, typename P>
 __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win, std::uint16_t* list, const std::uint32_t* tab,
-                           std::uint32_t r0, std::uint32_t limit, std::uint64_t e, std::uint32_t wave) {
+                                           const std::uint32_t* inj, std::uint32_t r0, std::uint32_t limit, P e,
+                                           std::uint32_t wave) {
+  constexpr P kNo = kNoneP<P>;
   const std::uint32_t lane = threadIdx.x & 63u;
   const dev::LaneConst kc = dev::lane_const16(lane);
-  const std::uint64_t size = a.size;
+  const P size = static_cast<P>(a.size);
   const std::uint32_t o = a.o;
   // the last region whose granules this wave writes into its window: limit (the overlap of limit - 1)
   const std::uint32_t rlast = limit;
   uint4 buf[kAhead][kRows];
   auto rows_of = [&](std::uint64_t r) -> int { return r < rlast ? kRows : r == rlast ? 1 : 0; };
 #pragma unroll
-  for (int k = 0; k < kAhead; ++k) load_region(a, static_cast<std::uint64_t>(r0) + k, lane, rows_of(static_cast<std::uint64_t>(r0) + k), buf[k]);
-  std::uint32_t spec_next = e == kNone ? kSpec : (FIXUP ? kFix : 0u);  // flags the next entry carries
+  for (int k = 0; k < kAhead; ++k) {
+    load_region(a, static_cast<std::uint64_t>(r0) + k, lane, rows_of(static_cast<std::uint64_t>(r0) + k), buf[k]);
+    // in order: the loop's waits count the loads issued after the ones they wait for, on entry as well
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  std::uint32_t spec_next = e == kNo ? kSpec : (FIXUP ? kFix : 0u);  // flags the next entry carries
   std::uint64_t nlong = 0;  // long payloads listed in this wave's segment
   // window <- region rr and the head of rr + 1; the buffer refilled with region rr + kAhead
   auto put = [&](std::uint32_t rr, uint4 (&cur)[kRows], const uint4& head) {
@@ -329,48 +389,48 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
 
-      const std::uint64_t rs = static_cast<std::uint64_t>(rr) * kRegion;
-      const std::uint64_t re = rs + kRegion;
+      const P rs = static_cast<P>(rr) * kRegion;
+      const P re = rs + kRegion;
       std::uint32_t ver = 0;
       if constexpr (FIXUP) ver = (a.fl[rr] >> 8) + 1u;
       // ---- 1. starts ------------------------------------------------------------------------------
-      const std::uint64_t ps = rs + static_cast<std::uint64_t>(kPiece) * lane, pe = ps + kPiece;
-      const bool exact = e != kNone;
+      const P ps = rs + static_cast<P>(kPiece) * lane, pe = ps + kPiece;
+      const bool exact = e != kNo;
       std::uint32_t flags;
-      std::uint64_t Er = e, Xout = e;
+      P Er = e, Xout = e;
       std::uint32_t count = 0, bad_k = 0xFFFFFFFFu;
-      std::uint64_t Bpos = kNone;
+      P Bpos = kNo;
       if (exact && (e >= re || e >= size)) {
         flags = kChain | spec_next;  // inside a record, or past the chain's end: no starts here
       } else {
         const std::uint32_t le = exact ? static_cast<std::uint32_t>((e - rs) / kPiece) : 0u;
-        std::uint64_t s = kNone;
+        P s = kNo;
         if (exact && lane == le) s = e;
         // the piece's first plausible header, kSearchStep positions at a time from its front (the first
         // step finds it in a WAL of small records; a piece inside a long payload is searched whole)
-        const std::uint64_t qend = size >= kWalMeta ? std::min<std::uint64_t>(pe, size - kWalMeta + 1u) : 0u;
+        const P qend = size >= kWalMeta ? std::min<P>(pe, size - static_cast<P>(kWalMeta) + 1u) : 0u;
         bool hunt = (!exact || lane > le) && ps < qend;
-        for (std::uint64_t q0 = ps; __ballot(hunt) != 0; q0 += kSearchStep) {
+        for (P q0 = ps; __ballot(hunt) != 0; q0 += kSearchStep) {
           if (hunt) {
-            s = search_piece(win, rs, o, q0, std::min<std::uint64_t>(q0 + kSearchStep, qend), size);
-            hunt = s == kNone && q0 + kSearchStep < qend;
+            s = search_piece<P>(win, rs, o, q0, std::min<P>(q0 + kSearchStep, qend), size);
+            hunt = s == kNo && q0 + kSearchStep < qend;
           }
         }
-        Walk wk;
+        Walk<P> wk;
         walk_piece(win, rs, o, s, pe, size, true, wk);
         // ---- 2. link check ---------------------------------------------------------------------------
-        std::uint64_t C = __ballot(s != kNone);
+        std::uint64_t C = __ballot(s != kNo);
         const std::uint32_t f = exact ? le : (C ? static_cast<std::uint32_t>(__builtin_ctzll(C)) : 64u);
         if (f == 64u) {
           flags = kSearch;
-          Er = Xout = kNone;
+          Er = Xout = kNo;
         } else {
           C &= ~((1ull << f) - 1ull);
           std::uint32_t cur = f;
           for (;;) {
             const std::uint64_t below = C & ((1ull << lane) - 1ull);
             const std::uint32_t prev = below ? 63u - static_cast<std::uint32_t>(__builtin_clzll(below)) : lane;
-            const std::uint64_t xp = shfl64(wk.x, prev);
+            const P xp = shfl_pos(wk.x, prev);
             const bool bp = __shfl(static_cast<int>(wk.broke), static_cast<int>(prev), 64) != 0;
             const bool mine = ((C >> lane) & 1ull) && lane > cur;
             const std::uint64_t fails = __ballot(mine && (bp || xp != s));
@@ -381,7 +441,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
             } else {
               pv = 63u - static_cast<std::uint32_t>(__builtin_clzll(C));  // every link holds: the last lane
             }
-            const std::uint64_t xv = dev::readlane64(wk.x, pv);
+            const P xv = readlane_pos(wk.x, pv);
             const bool bv = __builtin_amdgcn_readlane(static_cast<int>(wk.broke), static_cast<int>(pv)) != 0;
             if (bv || xv >= re || xv >= size) {  // the chain breaks, leaves the region or ends at pv
               C &= (2ull << pv) - 1ull;
@@ -397,9 +457,9 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
             cur = q;
           }
           const std::uint32_t last = 63u - static_cast<std::uint32_t>(__builtin_clzll(C));
-          Xout = dev::readlane64(wk.x, last);
+          Xout = readlane_pos(wk.x, last);
           const bool broke = __builtin_amdgcn_readlane(static_cast<int>(wk.broke), static_cast<int>(last)) != 0;
-          Er = exact ? e : dev::readlane64(s, f);
+          Er = exact ? e : readlane_pos(s, f);
           flags = kChain | spec_next | (broke ? kBroke : 0u) | (!broke && Xout == size ? kEnd : 0u);
           // ---- 3. list and fold ------------------------------------------------------------------------
           const bool on = (C >> lane) & 1ull;
@@ -425,13 +485,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
             const std::uint32_t kl = rd32(win, b + 18u), vl = rd32(win, b + 22u);
             const bool kv_ok = kWalMeta + static_cast<std::uint64_t>(kl) + vl <= 8ull + rl;  // wal.cpp:118-121
             const bool lng = act && rl > kLaneFold;
-            const std::uint32_t L = act && !lng ? rl : 0u;
-#if TKV_X_NOFOLD
-            const std::uint32_t crc = L + stored;
-            (void)tab;
-#else
-            const std::uint32_t crc = fold_win(win, tab, kc, b + 8u, L) ^ 0xFFFFFFFFu;
-#endif
+            const std::uint32_t crc = fold_lane(win, tab, inj, kc, b + 8u, act && !lng ? rl : 0u);
             const bool bad = act && (!kv_ok || (!lng && crc != stored));
             const std::uint64_t lb = __ballot(lng);
             if (lb) {
@@ -449,7 +503,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
               const std::uint64_t idx = at + __builtin_amdgcn_mbcnt_hi(static_cast<std::uint32_t>(lb >> 32),
                                                                        __builtin_amdgcn_mbcnt_lo(static_cast<std::uint32_t>(lb), 0u));
               if (lng && idx < a.l_cap) {
-                a.l_off[idx] = rs + so + 8u;
+                a.l_off[idx] = static_cast<std::uint64_t>(rs) + so + 8u;
                 a.l_len[idx] = rl;
                 a.l_crc[idx] = stored;
                 a.l_reg[idx] = rr;
@@ -464,7 +518,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
       }
       // ---- 4. region record, next entry --------------------------------------------------------------
       bool stop = false;
-      std::uint64_t next_e = kNone;
+      P next_e = kNo;
       std::uint32_t next_spec = kSpec;
       if ((flags & kChain) && !(flags & kBroke)) {  // (after kEnd: size, past every later region)
         next_e = Xout;
@@ -476,13 +530,13 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
           stop = true;
         } else {
           const std::uint32_t nf = a.fl[rr + 1u];
-          if ((nf & kChain) && a.E[rr + 1u] == next_e) stop = true;
+          if ((nf & kChain) && a.E[rr + 1u] == widen(next_e)) stop = true;
         }
       }
       switch (lane) {
-        case 0: a.E[rr] = Er; break;
-        case 1: a.X[rr] = Xout; break;
-        case 2: a.B[rr] = Bpos; break;
+        case 0: a.E[rr] = widen(Er); break;
+        case 1: a.X[rr] = widen(Xout); break;
+        case 2: a.B[rr] = widen(Bpos); break;
         case 3: a.cnt[rr] = count; break;
         case 4: a.bidx[rr] = bad_k; break;
         case 5: a.fl[rr] = flags | (ver << 8); break;
@@ -493,18 +547,6 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
       return stop;
     }
   };
-#if TKV_X_BODY == 0
-  // One copy of the region body; only the window write and the refill are switched on rr % 4.
-  for (std::uint32_t rr = r0; rr < limit; ++rr) {
-    switch ((rr - r0) & 3u) {
-      case 0: put(rr, buf[0], buf[1][0]); break;
-      case 1: put(rr, buf[1], buf[2][0]); break;
-      case 2: put(rr, buf[2], buf[3][0]); break;
-      default: put(rr, buf[3], buf[0][0]); break;
-    }
-    if (body(rr)) break;
-  }
-#else
   bool done = false;
   for (std::uint32_t r = r0; r < limit && !done; r += kAhead) {
 #pragma unroll
@@ -518,15 +560,18 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
       done = body(rr);
     }
   }
-#endif
   if (!FIXUP && lane == 0) a.l_cnt[wave] = static_cast<std::uint32_t>(nlong);
 }
 
-template <bool FIXUP>
+template <bool FIXUP, typename P>
 __global__ __launch_bounds__(kSweepThreads) void wal_sweep(SweepArgs a) {
-  __shared__ __attribute__((aligned(16))) std::uint32_t tab[kLdsSliceWords / 2];
-  __shared__ __attribute__((aligned(16))) std::uint8_t wins[kSweepWaves][kWinBytes];
+  // one block with the tables at LDS address 0, so a lookup's v_perm result is its address
+  __shared__ __attribute__((aligned(16))) std::uint8_t lds[kLdsSliceWords * 2 + kSweepWaves * kWinBytes + 4 * (kLaneFold + 1)];
+  std::uint32_t* tab = reinterpret_cast<std::uint32_t*>(lds);
+  std::uint8_t (*wins)[kWinBytes] = reinterpret_cast<std::uint8_t (*)[kWinBytes]>(lds + kLdsSliceWords * 2);
+  std::uint32_t* inj = reinterpret_cast<std::uint32_t*>(lds + kLdsSliceWords * 2 + kSweepWaves * kWinBytes);  // Shift_L(0xFFFFFFFF)
   dev::fill_lds_slicing16(a.tabs, tab);
+  for (std::uint32_t i = threadIdx.x; i <= kLaneFold; i += blockDim.x) inj[i] = a.tabs->init_shift[i];
   __syncthreads();
   const std::uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint32_t w = blockIdx.x * kSweepWaves + wv;
@@ -536,9 +581,9 @@ __global__ __launch_bounds__(kSweepThreads) void wal_sweep(SweepArgs a) {
   if constexpr (!FIXUP) {
     const std::uint32_t r0 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(w) * a.nreg / a.nwaves);
     const std::uint32_t r1 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(w + 1) * a.nreg / a.nwaves);
-    sweep_wave<false>(a, win, list, tab, r0, r1, r0 == 0 ? 0ull : kNone, w);
+    sweep_wave<false, P>(a, win, list, tab, inj, r0, r1, r0 == 0 ? P(0) : kNoneP<P>, w);
   } else {
-    sweep_wave<true>(a, win, list, tab, a.t_begin[w], a.t_limit[w], a.t_entry[w], w);
+    sweep_wave<true, P>(a, win, list, tab, inj, a.t_begin[w], a.t_limit[w], static_cast<P>(a.t_entry[w]), w);
   }
 }
 
@@ -805,7 +850,7 @@ SweepArgs carve(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std::u
   a.size = size;
   const std::uintptr_t wp = reinterpret_cast<std::uintptr_t>(w);
   a.al0 = wp & ~static_cast<std::uintptr_t>(15);
-  a.glast = (wp + size - 1) & ~static_cast<std::uintptr_t>(15);
+  a.gend = ((wp + size - 1) & ~static_cast<std::uintptr_t>(15)) + 16u;
   a.o = static_cast<std::uint32_t>(wp - a.al0);
   a.nreg = nreg;
   a.nwaves = W;
@@ -892,7 +937,10 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
     if (int rc = grow(&s.raw, &s.cap_raw, seg * W + atomic_area, kRawUnit)) return rc;
     SweepArgs a = carve(s, w, size, nreg, W, seg, tabs);
     hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, 0, static_cast<int>(kResWords));
-    hipLaunchKernelGGL((wal_sweep<false>), dim3(blocks(W, kSweepWaves)), dim3(kSweepThreads), 0, st, a);
+    if (size <= kPos32Max)
+      hipLaunchKernelGGL((wal_sweep<false, std::uint32_t>), dim3(blocks(W, kSweepWaves)), dim3(kSweepThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL((wal_sweep<false, std::uint64_t>), dim3(blocks(W, kSweepWaves)), dim3(kSweepThreads), 0, st, a);
     hipLaunchKernelGGL(wal_long_scan, dim3(1), dim3(1024), 0, st, s.l_cnt, W, s.l_base, s.res);
     hipLaunchKernelGGL(wal_bounds, dim3(blocks(nreg, 256)), dim3(256), 0, st, a, s.inc_p, s.inc_x, kMaxFix);
     launch_fin(a, s, 0, st);
@@ -932,7 +980,10 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
       f.t_limit = s.d_task + kMaxFix;
       f.t_entry = reinterpret_cast<const std::uint64_t*>(s.d_task + 2 * kMaxFix);
       hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, static_cast<int>(kResIncons), static_cast<int>(kResIncons) + 1);
-      hipLaunchKernelGGL((wal_sweep<true>), dim3(blocks(f.nwaves, kSweepWaves)), dim3(kSweepThreads), 0, st, f);
+      if (size <= kPos32Max)
+        hipLaunchKernelGGL((wal_sweep<true, std::uint32_t>), dim3(blocks(f.nwaves, kSweepWaves)), dim3(kSweepThreads), 0, st, f);
+      else
+        hipLaunchKernelGGL((wal_sweep<true, std::uint64_t>), dim3(blocks(f.nwaves, kSweepWaves)), dim3(kSweepThreads), 0, st, f);
       hipLaunchKernelGGL(wal_bounds, dim3(blocks(nreg, 256)), dim3(256), 0, st, a, s.inc_p, s.inc_x, kMaxFix);
       hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
       WAL_HIP(hipGetLastError());

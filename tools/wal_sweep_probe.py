@@ -48,6 +48,10 @@ def main():
         assert lib.tkv_wal_stamp(VP(w.ctypes.data), VP(offs.ctypes.data), VP(sz.ctypes.data), offs.size) == 0
         d = torch.from_numpy(w).cuda()
         torch.cuda.synchronize()
+        stamps = hasattr(lib, "tkv_debug_wal_stamps")
+        sv = np.zeros(8, np.uint64)
+        if stamps:
+            lib.tkv_debug_wal_stamps(VP(sv.ctypes.data))
         ts = []
         for r in range(args.reps + 1):
             good, stop = U64(0), U64(0)
@@ -63,6 +67,12 @@ def main():
         print(json.dumps({"image": name, "median_ms": round(med * 1e3, 3), "min_ms": round(min(ts) * 1e3, 3),
                           "GB_per_s": round(w.size / med / 1e9, 1), "rounds": int(last[0]), "fixup_free": int(last[3])}),
               flush=True)
+        if stamps:
+            lib.tkv_debug_wal_stamps(VP(sv.ctypes.data))
+            names = ["put", "search", "walk", "link", "list", "fold", "record"]
+            tot = float(sv[:7].sum())
+            print(json.dumps({"image": name, "regions": int(sv[7]), "cycles_per_region": round(tot / max(int(sv[7]), 1), 1),
+                              "share": {n: round(float(sv[i]) / tot, 3) for i, n in enumerate(names)}}), flush=True)
 
 
 if __name__ == "__main__":
