@@ -85,6 +85,37 @@ __device__ __forceinline__ void slice4(const std::uint32_t* lds, Reg& r, std::ui
   r.u = lds_at(lds, a3);
 }
 
+// The 16-replica image read without bank conflicts. ds_read_b32 banks are (a/4) mod 32 within each
+// 32-lane group, and table t of replica c sits in bank (16 t + c) mod 32, so lanes l and l + 16 of a
+// group collide whenever they look up the same table. Here the half with lane bit 4 set takes the
+// bytes of each pair in the other order (byte j = i ^ 1 in lookup i): in every lookup instruction the
+// two halves use tables of opposite parity, i.e. disjoint banks. Each lane still looks up all four
+// bytes, and the XOR of the four lookups does not depend on their order.
+struct LaneConstX {
+  std::uint32_t L[4];  // byte 0 of the address: 64 t + 4 c for the table of lookup i's byte
+  std::uint32_t S[4];  // v_perm selector dropping that byte of x into byte 1 (entry * 256)
+};
+__device__ __forceinline__ LaneConstX lane_const16x(std::uint32_t lane) {
+  const std::uint32_t c4 = (lane & 15u) << 2, h = (lane >> 4) & 1u;
+  LaneConstX k;
+#pragma unroll
+  for (std::uint32_t i = 0; i < 4u; ++i) {
+    const std::uint32_t j = i ^ h;       // byte j of x goes through T(3 - j)
+    k.L[i] = 64u * (3u - j) + c4;
+    k.S[i] = 0x0C020400u | (j << 8);
+  }
+  return k;
+}
+__device__ __forceinline__ void slice4x(const std::uint32_t* lds, Reg& r, std::uint32_t w, const LaneConstX& k) {
+  const std::uint32_t x = xor3(r.t, r.u, w);
+  const std::uint32_t a0 = __builtin_amdgcn_perm(x, k.L[0], k.S[0]);
+  const std::uint32_t a1 = __builtin_amdgcn_perm(x, k.L[1], k.S[1]);
+  const std::uint32_t a2 = __builtin_amdgcn_perm(x, k.L[2], k.S[2]);
+  const std::uint32_t a3 = __builtin_amdgcn_perm(x, k.L[3], k.S[3]);
+  r.t = xor3(lds_at(lds, a0), lds_at(lds, a1), lds_at(lds, a2));
+  r.u = lds_at(lds, a3);
+}
+
 // Shift_{(63-lane)*64}(p): 8 lookups into this lane's nibble tables.
 __device__ __forceinline__ std::uint32_t lane_shift(const std::uint32_t* lds, std::uint32_t p, const LaneConst& k) {
   std::uint32_t l[8];

@@ -4,12 +4,13 @@
 // of every record (wal.cpp:89-96) and the key/value bounds check (wal.cpp:118-121), ending in the first
 // corruption. The image is read from HBM once (round 5).
 //
-// wal_sweep: every wave streams a contiguous chunk of the image, one region of kRegion = 10 KiB at a
+// wal_sweep: every wave streams a contiguous chunk of the image, one region of kRegion = 7 KiB at a
 // time. Regions are loaded a region ahead into registers (coalesced 16-byte buffer loads whose
 // descriptor ends at the image's end) and written into the wave's LDS window together with the first
 // kOver bytes of the next region, so a record that starts in the region and has a payload of at most
-// kLaneFold bytes lies wholly in the window. Eight waves share one copy of the 64 KiB slicing tables
-// (16 replicas, at LDS address 0). Positions are 32-bit for images below 4 GiB. Per region:
+// kLaneFold bytes lies wholly in the window. Twelve waves (three per SIMD: 10 KiB regions with eight
+// waves, and 5 KiB with sixteen, measured slower) share one copy of the 64 KiB slicing tables (16
+// replicas, at LDS address 0). Positions are 32-bit for images below 4 GiB. Per region:
 //  1. walk: lane l owns the piece [rs + kPiece l, + kPiece). The lane holding the region's entry E
 //     (where the chain leaves the previous region) starts there; every later lane starts at the first
 //     plausible header of its piece (one the reference encoder could have written, wal.cpp:19-61),
@@ -52,7 +53,7 @@ namespace {
 
 constexpr std::uint64_t kWalMeta = 26;          // wal.hpp:21-27 kMetadataSize
 constexpr std::uint64_t kNone = ~0ull;
-constexpr std::uint32_t kRegion = 10240;  // image bytes per region (one wave step)
+constexpr std::uint32_t kRegion = 7168;  // image bytes per region (one wave step)
 constexpr int kRows = kRegion / 1024;           // 1 KiB load rows per region
 constexpr std::uint32_t kPiece = kRegion / 64;  // bytes per lane piece
 constexpr std::uint32_t kOver = 256;            // bytes of the next region behind the window
@@ -62,7 +63,7 @@ constexpr std::uint32_t kList = kRegion / 26 + 4;  // listed records per region 
 constexpr std::uint32_t kWinBytes = (kWin + 2 * kList + 15) & ~15u;
 constexpr std::uint32_t kStore = kPiece / 26 + 2;  // starts a lane lists: its records up to the first tiny one
 constexpr std::uint32_t kSearchStep = 48;       // positions a lane tests per search step
-constexpr unsigned kSweepWaves = 8;             // waves per workgroup: the 64 KiB tables + 8 windows of LDS
+constexpr unsigned kSweepWaves = 12;            // waves per workgroup: the 64 KiB tables + 12 windows of LDS
 constexpr unsigned kSweepThreads = 64 * kSweepWaves;
 constexpr unsigned kHres = 16;                  // words of the pinned result block
 static_assert(kRegion % 1024 == 0 && kPiece % 16 == 0, "region = whole 1 KiB load rows");
@@ -309,7 +310,7 @@ __device__ __forceinline__ std::uint32_t wave_max_u32(std::uint32_t v) {
 // (crc_s(D) = Shift_|D|(s) ^ crc_0(D)); slicing-by-4 into the 64 KiB table image (crc32.cpp:9-16
 // restated). (Two or three records per lane at once, as independent chains, measured slower.)
 __device__ __forceinline__ std::uint32_t fold_lane(const std::uint8_t* win, const std::uint32_t* tab, const std::uint32_t* inj,
-                                                   const dev::LaneConst& kc, std::uint32_t s, std::uint32_t L) {
+                                                   const dev::LaneConstX& kc, std::uint32_t s, std::uint32_t L) {
   const std::uint32_t nd = (L + 3u) >> 2;
   const std::uint32_t nmax = __builtin_amdgcn_readfirstlane(wave_max_u32(nd));
   const std::uint32_t z = 4u * nd - L;
@@ -318,13 +319,13 @@ __device__ __forceinline__ std::uint32_t fold_lane(const std::uint8_t* win, cons
   const std::uint32_t* w = reinterpret_cast<const std::uint32_t*>(win + (b0 & ~3u));
   std::uint32_t lo = w[1];
   dev::Reg r{0u, 0u};
-  dev::slice4(tab, r, __builtin_amdgcn_alignbyte(lo, w[0], sh) & (~0u << (8u * z)), kc);
+  dev::slice4x(tab, r, __builtin_amdgcn_alignbyte(lo, w[0], sh) & (~0u << (8u * z)), kc);
   if (nd == 0u) r = dev::Reg{0u, 0u};
 #pragma unroll 2
   for (std::uint32_t i = 1; i < nmax; ++i) {
     const std::uint32_t hi = w[i + 1u];
     dev::Reg t = r;
-    dev::slice4(tab, t, __builtin_amdgcn_alignbyte(hi, lo, sh), kc);
+    dev::slice4x(tab, t, __builtin_amdgcn_alignbyte(hi, lo, sh), kc);
     if (i < nd) r = t;
     lo = hi;
   }
@@ -360,7 +361,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
                                            std::uint32_t wave) {
   constexpr P kNo = kNoneP<P>;
   const std::uint32_t lane = threadIdx.x & 63u;
-  const dev::LaneConst kc = dev::lane_const16(lane);
+  const dev::LaneConstX kc = dev::lane_const16x(lane);
   const P size = static_cast<P>(a.size);
   const std::uint32_t o = a.o;
   // the last region whose granules this wave writes into its window: limit (the overlap of limit - 1)

@@ -1,17 +1,35 @@
 #!/usr/bin/env python3
-"""Probe build (not product): the library with s_memtime stamps around the sections of the WAL
-sweep's region body, summed per section over every wave, as tools/ab/libtkv_stamp.so (export
-tkv_debug_wal_stamps). The product sources are copied and patched in a temporary directory."""
+"""Probe build (not product): the library with source patches applied to a temporary copy of the
+product sources, as tools/ab/libtkv_NAME.so, for in-process A/B runs (tools/ab_wal.py).
+
+    python tools/variant.py NAME PATCH [PATCH ...]
+
+Patches:
+  stamp     s_memtime stamps around the sections of the WAL sweep's region body, summed per section
+            over every wave (export tkv_debug_wal_stamps; tools/wal_sweep_probe.py prints the shares)
+  region5k  5 KiB regions and 16 waves per sweep workgroup (4 waves per SIMD)
+  region7k  7 KiB regions and 12 waves per sweep workgroup (3 waves per SIMD)
+"""
 import os
 import shutil
 import subprocess
+import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 H = os.path.join(ROOT, "tinykvpp_amd", "csrc")
 
 
-def patch(s):
+def region5k(s):
+    def rep(x, y):
+        assert s.count(x) == 1, x
+        return s.replace(x, y)
+    s = rep("constexpr std::uint32_t kRegion = 10240;", "constexpr std::uint32_t kRegion = 5120;")
+    s = rep("constexpr unsigned kSweepWaves = 8; ", "constexpr unsigned kSweepWaves = 16; ")
+    return s
+
+
+def stamp(s):
     def rep(x, y):
         assert s.count(x) >= 1, x
         return s.replace(x, y)
@@ -25,7 +43,7 @@ def patch(s):
     s = rep("        Walk<P> wk;\n", "        ST(1);\n        Walk<P> wk;\n")
     s = rep("        walk_piece(win, rs, o, s, pe, size, true, wk);\n", "        walk_piece(win, rs, o, s, pe, size, true, wk);\n        ST(2);\n")
     s = rep("          // ---- 3. list and fold", "          ST(3);\n          // ---- 3. list and fold")
-    s = rep("          // records base + 64 c + lane", "          ST(4);\n          // records base + 64 c + lane")
+    s = rep("          for (std::uint32_t base = 0; base < nl; base += 64u) {", "          ST(4);\n          for (std::uint32_t base = 0; base < nl; base += 64u) {")
     s = rep("          if (bad_k != 0xFFFFFFFFu) Bpos", "          ST(5);\n          if (bad_k != 0xFFFFFFFFu) Bpos")
     s = rep("      e = next_e;\n", "      ST(6);\n      e = next_e;\n")
     s = rep("  if (!FIXUP && lane == 0) a.l_cnt[wave]",
@@ -37,14 +55,25 @@ def patch(s):
     return s
 
 
+def region7k(s):
+    s = s.replace("constexpr std::uint32_t kRegion = 10240;", "constexpr std::uint32_t kRegion = 7168;")
+    return s.replace("constexpr unsigned kSweepWaves = 8; ", "constexpr unsigned kSweepWaves = 12; ")
+
+
+PATCHES = {"stamp": stamp, "region5k": region5k, "region7k": region7k}
+
+
 def main():
+    name, patches = sys.argv[1], sys.argv[2:]
     t = tempfile.mkdtemp()
     try:
         src = os.path.join(t, "csrc")
         shutil.copytree(H, src, ignore=shutil.ignore_patterns("build", "*.so", "*.o"))
         p = os.path.join(src, "tkv_wal_device.hip")
         with open(p) as f:
-            s = patch(f.read())
+            s = f.read()
+            for pn in patches:
+                s = PATCHES[pn](s)
         with open(p, "w") as f:
             f.write(s)
         fl = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I" + os.path.join(ROOT, "include"), "-I" + src]
@@ -54,7 +83,7 @@ def main():
         b = os.path.join(H, "build")
         objs = [os.path.join(b, n) for n in ("tkv_crc32_host.o", "tkv_formats.o", "tkv_crc32_span.o", "tkv_wal_records.o", "tkv_build_id.o")]
         os.makedirs(os.path.join(ROOT, "tools", "ab"), exist_ok=True)
-        subprocess.check_call([hc, "-shared", "-fPIC", "--offload-arch=gfx950", "-o", os.path.join(ROOT, "tools", "ab", "libtkv_stamp.so"),
+        subprocess.check_call([hc, "-shared", "-fPIC", "--offload-arch=gfx950", "-o", os.path.join(ROOT, "tools", "ab", "libtkv_%s.so" % name),
                                os.path.join(t, "k.o"), os.path.join(t, "w.o")] + objs + ["-lpthread"])
     finally:
         shutil.rmtree(t)

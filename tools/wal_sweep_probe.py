@@ -2,7 +2,7 @@
 """Probe (not product code): the device WAL verify on the 1 GiB image of small records and the 430 MB
 Zipf image (tools/ab_wal.py's images), timed per call, for rocprofv3 kernel traces of its kernels.
 
-    python tools/wal_sweep_probe.py [lib.so] [--reps 10] [--image small|zipf|both]
+    python tools/wal_sweep_probe.py [lib.so] [--reps 10] [--image small|zipf|both|adv]
 """
 import argparse
 import ctypes
@@ -19,6 +19,35 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 from ab_wal import image  # noqa: E402
 
 VP, U64 = ctypes.c_void_p, ctypes.c_uint64
+
+
+def adversarial(rng, target=1 << 30):
+    """Zipf values (|v| = min(48 zipf(1.6), 16000)), every value a run of well-formed 40-byte records
+    (tests/test_gpu_wal_device.py::test_values_made_of_records at 1 GiB): every chunk and search start
+    inside a value lands on a fake chain."""
+    n = int(target / 300)
+    klen = rng.integers(0, 40, n).astype(np.uint32)
+    vlen = np.minimum(rng.zipf(1.6, n) * 48, 16000).astype(np.uint32)
+    size = 26 + klen.astype(np.uint64) + vlen
+    n = int(np.searchsorted(np.cumsum(size), target))
+    klen, vlen, size = klen[:n], vlen[:n], size[:n]
+    w, offs, sz = image(n, klen, vlen, rng)
+    fake = np.zeros(40, np.uint8)
+    fake[0:4] = np.frombuffer((32).to_bytes(4, "little"), np.uint8)
+    fake[18:22] = np.frombuffer((6).to_bytes(4, "little"), np.uint8)
+    fake[22:26] = np.frombuffer((8).to_bytes(4, "little"), np.uint8)
+    v0 = (offs + 26 + klen).astype(np.int64)
+    ln = (vlen // 40 * 40).astype(np.int64)
+    for a in range(0, n, 200_000):
+        b = min(n, a + 200_000)
+        L = ln[a:b]
+        tot = int(L.sum())
+        if not tot:
+            continue
+        start = np.repeat(v0[a:b], L)
+        r = np.arange(tot, dtype=np.int64) - np.repeat(np.cumsum(L) - L, L)
+        w[start + r] = fake[r % 40]
+    return w, offs, sz
 
 
 def main():
@@ -39,6 +68,8 @@ def main():
         n = 18_199_191
         imgs.append(("small records 1 GiB", image(n, rng.integers(4, 24, n).astype(np.uint32),
                                                   rng.integers(0, 40, n).astype(np.uint32), rng)))
+    if args.image == "adv":
+        imgs.append(("values made of records 1 GiB", adversarial(rng)))
     if args.image in ("zipf", "both"):
         n2 = 400_000
         imgs.append(("zipf 430 MB", image(n2, rng.integers(8, 64, n2).astype(np.uint32),
@@ -64,8 +95,9 @@ def main():
         last = np.zeros(4, np.uint64)
         lib.tkv_debug_wal_last(VP(last.ctypes.data))
         med = float(np.median(ts))
-        print(json.dumps({"image": name, "median_ms": round(med * 1e3, 3), "min_ms": round(min(ts) * 1e3, 3),
-                          "GB_per_s": round(w.size / med / 1e9, 1), "rounds": int(last[0]), "fixup_free": int(last[3])}),
+        print(json.dumps({"image": name, "bytes": int(w.size), "records": int(offs.size), "median_ms": round(med * 1e3, 3),
+                          "min_ms": round(min(ts) * 1e3, 3), "GB_per_s": round(w.size / med / 1e9, 1), "rounds": int(last[0]),
+                          "host_walk": int(last[1]), "fixup_free": int(last[3])}),
               flush=True)
         if stamps:
             lib.tkv_debug_wal_stamps(VP(sv.ctypes.data))
