@@ -269,12 +269,15 @@ void tkv_debug_update_counts(uint64_t out[2]);
  * through tkv_crc32[c]_update_fallback (host recomputes after a failed GPU update). Returns the number
  * of counters (3). */
 size_t tkv_debug_update_counts_n(uint64_t *out, size_t n);
-/* What the calling thread's last tkv_wal_verify / tkv_wal_verify_device did: out[0] = device walk
- * passes, out[1] = 1 when it handed the image to the exact host-thread walk, out[2] = 1 when a
- * host image was copied to the device, out[3] = 1 when at least one device pass ran and every pass
- * stitched its pieces by the fast path (no pointer jumping); 0 when no device pass ran. (Before
- * round 3, out[3] counted pieces; it is a flag since.) */
+/* What the calling thread's last tkv_wal_verify / tkv_wal_verify_device did: out[0] = device
+ * rounds (the sweep, then one per fix-up round), out[1] = 1 when it handed the image to the exact
+ * host-thread walk (only a host image the device cannot hold), out[2] = 1 when a host image was
+ * copied to the device, out[3] = 1 when the sweep needed no fix-up (0 when no device round ran). */
 void tkv_debug_wal_last(uint64_t out[4]);
+/* Per fix-up round of the calling thread's last device WAL verify, four words each: failing chunk
+ * boundaries found, fix-up tasks launched, the longest task's regions, all tasks' regions. Writes up
+ * to n words; returns the number available (0 when the sweep needed no fix-up). */
+size_t tkv_debug_wal_rounds(uint64_t *out, size_t n);
 /* Which path the last irregular batch on `stream` took: 1 = byte-stream row walk (blocks back to
  * back, each at least 64 bytes), 0 = general row walk; -1 on error. Synchronizes
  * the stream. */

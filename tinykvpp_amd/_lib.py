@@ -74,6 +74,7 @@ SIGNATURES = {
     "tkv_debug_set_stream_groups": (_int, [_int]),
     "tkv_debug_wal_chain": (_sz, [_u8p, _u64, _vp, _sz, ctypes.POINTER(_u64), ctypes.POINTER(_int)]),
     "tkv_debug_wal_last": (None, [_vp]),
+    "tkv_debug_wal_rounds": (ctypes.c_size_t, [_vp, ctypes.c_size_t]),
     "tkv_debug_update_counts": (None, [_vp]),
     "tkv_debug_update_counts_n": (_sz, [_vp, _sz]),
     "tkv_debug_irregular_mode": (_int, [_vp]),

@@ -55,14 +55,6 @@ __device__ __forceinline__ LaneConst lane_const(std::uint32_t lane) {
   const std::uint32_t c4 = (lane & 31u) << 2;
   return {c4, 128u + c4, 0x10000u + c4, 0x10080u + c4, kLdsLaneBase + lane * 4u};
 }
-// The 64 KiB image (fill_lds_slicing16): 16 replicas, all four tables in one 256-byte row per entry
-// (table t at bytes 64 t + 4 c), so the entry * 256 addressing of slice4 holds; lanes l and l + 16 of
-// a half-wave share a bank (2-way conflicts when their entries differ). Lane shifts are not in it.
-__device__ __forceinline__ LaneConst lane_const16(std::uint32_t lane) {
-  const std::uint32_t c4 = (lane & 15u) << 2;
-  return {c4, 64u + c4, 128u + c4, 192u + c4, 0u};
-}
-
 __device__ __forceinline__ std::uint32_t xor3(std::uint32_t a, std::uint32_t b, std::uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32 truth table 0x96 = a ^ b ^ c
 }
@@ -91,13 +83,18 @@ __device__ __forceinline__ void slice4(const std::uint32_t* lds, Reg& r, std::ui
 // bytes of each pair in the other order (byte j = i ^ 1 in lookup i): in every lookup instruction the
 // two halves use tables of opposite parity, i.e. disjoint banks. Each lane still looks up all four
 // bytes, and the XOR of the four lookups does not depend on their order.
+// The 64 KiB image (fill_lds_slicing16): 16 replicas, all four tables in one 256-byte row per entry
+// (table t at bytes 64 t + 4 c), so the entry * 256 addressing of slice4 holds. Lane shifts are not
+// in it.
 struct LaneConstX {
   std::uint32_t L[4];  // byte 0 of the address: 64 t + 4 c for the table of lookup i's byte
   std::uint32_t S[4];  // v_perm selector dropping that byte of x into byte 1 (entry * 256)
+  std::uint32_t L0;    // T0's offset for this lane (Sarwate steps)
 };
-__device__ __forceinline__ LaneConstX lane_const16x(std::uint32_t lane) {
+__device__ __forceinline__ LaneConstX lane_const16(std::uint32_t lane) {
   const std::uint32_t c4 = (lane & 15u) << 2, h = (lane >> 4) & 1u;
   LaneConstX k;
+  k.L0 = c4;
 #pragma unroll
   for (std::uint32_t i = 0; i < 4u; ++i) {
     const std::uint32_t j = i ^ h;       // byte j of x goes through T(3 - j)
@@ -106,7 +103,7 @@ __device__ __forceinline__ LaneConstX lane_const16x(std::uint32_t lane) {
   }
   return k;
 }
-__device__ __forceinline__ void slice4x(const std::uint32_t* lds, Reg& r, std::uint32_t w, const LaneConstX& k) {
+__device__ __forceinline__ void slice4(const std::uint32_t* lds, Reg& r, std::uint32_t w, const LaneConstX& k) {
   const std::uint32_t x = xor3(r.t, r.u, w);
   const std::uint32_t a0 = __builtin_amdgcn_perm(x, k.L[0], k.S[0]);
   const std::uint32_t a1 = __builtin_amdgcn_perm(x, k.L[1], k.S[1]);
@@ -1390,7 +1387,8 @@ __device__ __forceinline__ void lane_dwords(const uint4 (&g)[kLaneGran], std::ui
 }
 
 // Sarwate steps (crc32.cpp:12-14) over the low m <= 3 bytes of w, with T0 from the LDS image.
-__device__ __forceinline__ std::uint32_t sarwate_bytes(const std::uint32_t* lds, const LaneConst& kc, std::uint32_t c,
+template <typename KC>
+__device__ __forceinline__ std::uint32_t sarwate_bytes(const std::uint32_t* lds, const KC& kc, std::uint32_t c,
                                                        std::uint32_t w, std::uint32_t m) {
 #pragma unroll
   for (std::uint32_t j = 0; j < 3u; ++j)
@@ -1587,7 +1585,10 @@ __device__ __forceinline__ void crc_lanes_n_body(const RowsArgs& a, std::uint32_
   if constexpr (R == 32) fill_lds_slicing(a.tabs, lds);
   else fill_lds_slicing16(a.tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
-  const LaneConst kc = R == 32 ? lane_const(lane) : lane_const16(lane);
+  const auto kc = [lane] {
+    if constexpr (R == 32) return lane_const(lane);
+    else return lane_const16(lane);
+  }();
   __syncthreads();
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint64_t W = a.nwaves, nb = a.nblocks;
@@ -1683,7 +1684,7 @@ __device__ __forceinline__ void crc_lanes_lds_body(const RowsArgs& a, std::uint3
   constexpr std::uint32_t kTabWords = kLdsSliceWords / 2;  // the 64 KiB image
   fill_lds_slicing16(a.tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
-  const LaneConst kc = lane_const16(lane);
+  const LaneConstX kc = lane_const16(lane);
   const std::uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   __syncthreads();
   const std::uint32_t wave = blockIdx.x * (blockDim.x >> 6) + wid;

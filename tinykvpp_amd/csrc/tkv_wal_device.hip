@@ -81,7 +81,8 @@ constexpr std::uint32_t kEnd = 16;    // the chain reached the end of the image 
 constexpr std::uint32_t kFix = 32;    // its entry came from a fix-up task (checked like kSpec)
 
 // Result words (device, u64): see wal_fin_*.
-enum : int { kResLongA = 0, kResIncons, kResP, kResQ, kResLidx, kResCnt, kResLongSeg, kResWords = 8 };
+enum : int { kResLongA = 0, kResIncons, kResFirst, kResP, kResQ, kResLidx, kResCnt, kResLongSeg, kResWords = 8 };
+static_assert(kResLongSeg < kResWords, "result words");
 
 struct SweepArgs {
   const std::uint8_t* w;
@@ -319,13 +320,13 @@ __device__ __forceinline__ std::uint32_t fold_lane(const std::uint8_t* win, cons
   const std::uint32_t* w = reinterpret_cast<const std::uint32_t*>(win + (b0 & ~3u));
   std::uint32_t lo = w[1];
   dev::Reg r{0u, 0u};
-  dev::slice4x(tab, r, __builtin_amdgcn_alignbyte(lo, w[0], sh) & (~0u << (8u * z)), kc);
+  dev::slice4(tab, r, __builtin_amdgcn_alignbyte(lo, w[0], sh) & (~0u << (8u * z)), kc);
   if (nd == 0u) r = dev::Reg{0u, 0u};
 #pragma unroll 2
   for (std::uint32_t i = 1; i < nmax; ++i) {
     const std::uint32_t hi = w[i + 1u];
     dev::Reg t = r;
-    dev::slice4x(tab, t, __builtin_amdgcn_alignbyte(hi, lo, sh), kc);
+    dev::slice4(tab, t, __builtin_amdgcn_alignbyte(hi, lo, sh), kc);
     if (i < nd) r = t;
     lo = hi;
   }
@@ -361,7 +362,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
                                            std::uint32_t wave) {
   constexpr P kNo = kNoneP<P>;
   const std::uint32_t lane = threadIdx.x & 63u;
-  const dev::LaneConstX kc = dev::lane_const16x(lane);
+  const dev::LaneConstX kc = dev::lane_const16(lane);
   const P size = static_cast<P>(a.size);
   const std::uint32_t o = a.o;
   // the last region whose granules this wave writes into its window: limit (the overlap of limit - 1)
@@ -384,8 +385,22 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
     const std::uint64_t nxt = static_cast<std::uint64_t>(rr) + kAhead;
     load_region(a, nxt, lane, rows_of(nxt), cur);
   };
-  // the region body: true when the wave stops (fix-up converged)
-  auto body = [&](std::uint32_t rr) -> bool {
+  // regions [j0, j1) lie inside the record the chain is in (it leaves at x past them): stored without
+  // being loaded or walked
+  auto pass_over = [&](std::uint32_t j0, std::uint32_t j1, P x) {
+    for (std::uint32_t j = j0 + lane; j < j1; j += 64u) {
+      std::uint32_t v = 0;
+      if constexpr (FIXUP) v = (a.fl[j] >> 8) + 1u;
+      a.E[j] = widen(x);
+      a.X[j] = widen(x);
+      a.B[j] = kNone;
+      a.cnt[j] = 0;
+      a.bidx[j] = 0xFFFFFFFFu;
+      a.fl[j] = kChain | (v << 8);
+    }
+  };
+  // the region body: the next region to walk (limit: the wave stops; fix-up converged)
+  auto body = [&](std::uint32_t rr) -> std::uint32_t {
     {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -545,7 +560,20 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
       }
       e = next_e;
       spec_next = next_spec;
-      return stop;
+      std::uint32_t nx = stop ? limit : rr + 1u;
+      if (!stop && (flags & kChain) && !(flags & kBroke)) {
+        // the chain's current record covers whole regions: store them, go on where it ends
+        const std::uint32_t qr = static_cast<std::uint32_t>(next_e / kRegion);
+        const std::uint32_t q = next_e >= size || qr > limit ? limit : qr;
+        if (q > rr + 1u) {
+          pass_over(rr + 1u, q, next_e);
+          nx = q;
+          if constexpr (FIXUP) {
+            if (q < limit && (a.fl[q] & kChain) && a.E[q] == widen(next_e)) nx = limit;  // converged
+          }
+        }
+      }
+      return nx;
     }
   };
   bool done = false;
@@ -558,7 +586,14 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
         break;
       }
       put(rr, buf[k], buf[(k + 1) % kAhead][0]);
-      done = body(rr);
+      const std::uint32_t nx = body(rr);
+      if (nx >= limit) {
+        done = true;
+      } else if (nx != rr + 1u) {  // passed over regions: the pipeline restarts at nx
+        load_region(a, nx, lane, rows_of(nx), buf[(k + 1) % kAhead]);
+        load_region(a, static_cast<std::uint64_t>(nx) + 1u, lane, rows_of(static_cast<std::uint64_t>(nx) + 1u), buf[k]);
+        r = nx - static_cast<std::uint32_t>(k) - 1u;
+      }
     }
   }
   if (!FIXUP && lane == 0) a.l_cnt[wave] = static_cast<std::uint32_t>(nlong);
@@ -668,6 +703,7 @@ __global__ void wal_bounds(SweepArgs a, std::uint32_t* inc_p, std::uint64_t* inc
   }
   if (ok) ok = (a.fl[q] & kChain) && a.E[q] == x;
   if (!ok) {
+    atomicMin(&a.res[kResFirst], static_cast<unsigned long long>(p));
     const unsigned long long i = atomicAdd(&a.res[kResIncons], 1ull);
     if (i < cap) {
       inc_p[i] = static_cast<std::uint32_t>(p);
@@ -678,7 +714,7 @@ __global__ void wal_bounds(SweepArgs a, std::uint32_t* inc_p, std::uint64_t* inc
 
 __global__ void wal_reset(unsigned long long* res, int lo, int hi) {
   const int i = lo + static_cast<int>(threadIdx.x);
-  if (i < hi) res[i] = (i == kResP || i == kResQ) ? ~0ull : 0ull;
+  if (i < hi) res[i] = (i == kResP || i == kResQ || i == kResFirst) ? ~0ull : 0ull;
 }
 
 // First bad record P (region lists and, when their versions are current, the long payloads) and the
@@ -740,6 +776,7 @@ __global__ void wal_publish(SweepArgs a, std::uint64_t* h) {
   h[0] = a.res[kResIncons];
   h[1] = a.res[kResLongSeg] + std::min<std::uint64_t>(a.res[kResLongA], a.l_cap - a.l_seg * a.wsweep);
   h[5] = a.res[kResLongA];
+  h[6] = a.res[kResFirst];
   if (P < Q) {
     h[2] = a.res[kResCnt] + a.res[kResLidx];
     h[3] = P;
@@ -810,6 +847,9 @@ WalScratch* g_wal[64] = {};
 
 // What the calling thread's last WAL verify did (tkv_debug_wal_last).
 thread_local std::uint64_t g_last[4] = {0, 0, 0, 0};  // rounds, host walk needed, image copied, no fix-up
+// per fix-up round of the calling thread's last verify: failing boundaries, tasks, longest task and
+// all tasks' regions (tkv_debug_wal_rounds)
+thread_local std::vector<std::uint64_t> g_rounds;
 
 #define WAL_HIP(call)                                                            \
   do {                                                                           \
@@ -949,6 +989,7 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
     WAL_HIP(hipStreamSynchronize(st));
     std::uint64_t rounds = 1;
     const bool clean = s.h_res[0] == 0;
+    g_rounds.clear();
     // fix-up rounds: every failing boundary is walked again from its true exit (race-free ranges)
     while (s.h_res[0] != 0) {
       const std::uint64_t ninc = std::min<std::uint64_t>(s.h_res[0], kMaxFix);
@@ -958,29 +999,52 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
       std::vector<std::pair<std::uint32_t, std::uint64_t>> v(ninc);
       for (std::uint64_t i = 0; i < ninc; ++i) v[i] = {s.h_inc_p[i], s.h_inc_x[i]};
       std::sort(v.begin(), v.end());
-      // keep a boundary only if the previous kept one's exit lands before it (else it lies inside that
-      // record, and the earlier fix-up covers it); each task may rewrite regions up to the next kept one
+      if (v[0].first != s.h_res[6]) {  // (more than kMaxFix failed: the list holds an arbitrary part) the first
+        const std::uint32_t p0 = static_cast<std::uint32_t>(s.h_res[6]);
+        std::uint64_t x0 = 0;
+        WAL_HIP(hipMemcpy(&x0, a.X + p0, 8, hipMemcpyDeviceToHost));
+        v.insert(v.begin(), {p0, x0});
+        v.resize(std::min<std::size_t>(v.size(), kMaxFix));
+      }
+      // Tasks. The first failing boundary's exit is on the true chain (every boundary before it holds,
+      // back to region 0): its task runs up to the first boundary past the record it lands in (the
+      // ones inside that jump are covered by it). Every later boundary gets a task up to the next one
+      // (disjoint ranges: no two tasks write one region) unless its exit lies past that range: such an
+      // exit is most likely a fake chain's long jump, and its task would only pass a stretch of
+      // regions over, round after round; it waits until it is the first failing boundary.
+      std::vector<std::pair<std::uint32_t, std::uint64_t>> bnd;  // boundaries whose ranges are taken
+      const std::uint64_t reach0 = v[0].second / kRegion;
+      bnd.push_back(v[0]);
+      for (std::size_t k = 1; k < v.size(); ++k)
+        if (static_cast<std::uint64_t>(v[k].first) + 1 > reach0) bnd.push_back(v[k]);
       std::vector<std::pair<std::uint32_t, std::uint64_t>> kept;
-      std::uint64_t reach = 0;
-      for (const auto& pv : v) {
-        if (!kept.empty() && static_cast<std::uint64_t>(pv.first) + 1 <= reach) continue;
-        kept.push_back(pv);
-        reach = pv.second / kRegion;
+      std::vector<std::uint32_t> kept_lim;
+      for (std::size_t k = 0; k < bnd.size(); ++k) {
+        const std::uint32_t lim = k + 1 < bnd.size() ? bnd[k + 1].first + 1 : nreg;
+        if (k > 0 && bnd[k].second / kRegion >= lim) continue;
+        kept.push_back(bnd[k]);
+        kept_lim.push_back(lim);
       }
       std::uint32_t* tb = s.h_task;
       std::uint32_t* tl = s.h_task + kMaxFix;
       auto* te = reinterpret_cast<std::uint64_t*>(s.h_task + 2 * kMaxFix);
       for (std::size_t k = 0; k < kept.size(); ++k) {
         tb[k] = kept[k].first + 1;
-        tl[k] = k + 1 < kept.size() ? kept[k + 1].first + 1 : nreg;
+        tl[k] = kept_lim[k];
         te[k] = kept[k].second;
       }
+      std::uint64_t span_max = 0, span_sum = 0;
+      for (std::size_t k = 0; k < kept.size(); ++k) {
+        span_max = std::max<std::uint64_t>(span_max, tl[k] - tb[k]);
+        span_sum += tl[k] - tb[k];
+      }
+      g_rounds.insert(g_rounds.end(), {s.h_res[0], kept.size(), span_max, span_sum});
       SweepArgs f = a;
       f.nwaves = static_cast<std::uint32_t>(kept.size());
       f.t_begin = s.d_task;
       f.t_limit = s.d_task + kMaxFix;
       f.t_entry = reinterpret_cast<const std::uint64_t*>(s.d_task + 2 * kMaxFix);
-      hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, static_cast<int>(kResIncons), static_cast<int>(kResIncons) + 1);
+      hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, static_cast<int>(kResIncons), static_cast<int>(kResFirst) + 1);
       if (size <= kPos32Max)
         hipLaunchKernelGGL((wal_sweep<true, std::uint32_t>), dim3(blocks(f.nwaves, kSweepWaves)), dim3(kSweepThreads), 0, st, f);
       else
@@ -1128,4 +1192,10 @@ int wal_verify_host_image_impl(const std::uint8_t* h_wal, std::uint64_t size, st
 
 extern "C" void tkv_debug_wal_last(uint64_t out[4]) {
   for (int i = 0; i < 4; ++i) out[i] = tkv::g_last[i];
+}
+
+extern "C" size_t tkv_debug_wal_rounds(uint64_t* out, size_t n) {
+  const std::size_t k = std::min(n, tkv::g_rounds.size());
+  for (std::size_t i = 0; i < k; ++i) out[i] = tkv::g_rounds[i];
+  return tkv::g_rounds.size();
 }

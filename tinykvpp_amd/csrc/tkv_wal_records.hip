@@ -73,8 +73,8 @@ __device__ __forceinline__ void rec_dwords(const uint4 (&g)[NG], std::uint32_t o
 }
 
 // Folds the payload bytes [0, n) of d (n <= 4 * ND) into register c (whole dwords, then Sarwate steps).
-template <int ND>
-__device__ __forceinline__ std::uint32_t rec_fold(const std::uint32_t* lds, const dev::LaneConst& kc, const std::uint32_t* d,
+template <int ND, typename KC>
+__device__ __forceinline__ std::uint32_t rec_fold(const std::uint32_t* lds, const KC& kc, const std::uint32_t* d,
                                                   std::uint32_t n, std::uint32_t c) {
   dev::Reg r{c, 0};
   const std::uint32_t nf = n >> 2, tb = n & 3u;
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kRecLdsThreads) void wal_rec_lds(RecArgs a, const D
   __shared__ std::uint32_t lds[(kTabBytes + kWaves * (2 * kRecLdsBuf + 2 * 256)) / 4];
   dev::fill_lds_slicing16(tabs, lds);
   const std::uint32_t lane = threadIdx.x & 63u;
-  const dev::LaneConst kc = dev::lane_const16(lane);
+  const dev::LaneConstX kc = dev::lane_const16(lane);
   const std::uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   __syncthreads();
   const std::uint32_t wave = blockIdx.x * kWaves + wid;

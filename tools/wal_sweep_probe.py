@@ -81,6 +81,14 @@ def main():
         torch.cuda.synchronize()
         stamps = hasattr(lib, "tkv_debug_wal_stamps")
         sv = np.zeros(8, np.uint64)
+        if hasattr(lib, "tkv_debug_wal_rounds"):
+            lib.tkv_debug_wal_rounds.restype = ctypes.c_size_t
+            lib.tkv_debug_wal_rounds.argtypes = [VP, ctypes.c_size_t]
+            rw = np.zeros(256, np.uint64)
+            k = lib.tkv_debug_wal_rounds(VP(rw.ctypes.data), 256)
+            rounds = [dict(zip(("failing", "tasks", "longest", "regions"), map(int, rw[i:i + 4]))) for i in range(0, min(k, 256), 4)]
+            if rounds:
+                print(json.dumps({"image": name, "fixup_rounds": rounds}), flush=True)
         if stamps:
             lib.tkv_debug_wal_stamps(VP(sv.ctypes.data))
         ts = []
@@ -89,6 +97,7 @@ def main():
             t0 = time.perf_counter()
             rc = lib.tkv_wal_verify_device(VP(d.data_ptr()), w.size, ctypes.byref(good), ctypes.byref(stop), st)
             dt = time.perf_counter() - t0
+            print(json.dumps({"image": name, "rep": r, "ms": round(dt * 1e3, 3)}), flush=True)
             assert rc == 0 and good.value == offs.size and stop.value == w.size, (rc, good.value, stop.value)
             if r:
                 ts.append(dt)
@@ -99,6 +108,14 @@ def main():
                           "min_ms": round(min(ts) * 1e3, 3), "GB_per_s": round(w.size / med / 1e9, 1), "rounds": int(last[0]),
                           "host_walk": int(last[1]), "fixup_free": int(last[3])}),
               flush=True)
+        if hasattr(lib, "tkv_debug_wal_rounds"):
+            lib.tkv_debug_wal_rounds.restype = ctypes.c_size_t
+            lib.tkv_debug_wal_rounds.argtypes = [VP, ctypes.c_size_t]
+            rw = np.zeros(256, np.uint64)
+            k = lib.tkv_debug_wal_rounds(VP(rw.ctypes.data), 256)
+            rounds = [dict(zip(("failing", "tasks", "longest", "regions"), map(int, rw[i:i + 4]))) for i in range(0, min(k, 256), 4)]
+            if rounds:
+                print(json.dumps({"image": name, "fixup_rounds": rounds}), flush=True)
         if stamps:
             lib.tkv_debug_wal_stamps(VP(sv.ctypes.data))
             names = ["put", "search", "walk", "link", "list", "fold", "record"]
