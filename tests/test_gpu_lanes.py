@@ -122,6 +122,55 @@ def test_irregular_wal_payloads(gpu, oracle, buf, sizes, base):
     assert np.array_equal(got, oracle.batch(host, offs, lens, init))
 
 
+@pytest.mark.parametrize("shape", ["shuffled", "late_shuffle", "late_long", "spread", "tiny_batch", "zero_lengths",
+                                   "at_allocation_end", "crc32c"])
+def test_irregular_one_pass_lanes(gpu, oracle, buf, shape):
+    """crc_list_lanes, the one-pass kernel in front of the general path for irregular batches with the
+    default register: steps of 64 blocks staged through an LDS window when they lie in
+    4 KiB, per-lane granule loads for a later step that does not (blocks out of order, spread out), the
+    general path for the whole batch when a first step does not fit or a block is over 64 bytes (near
+    the start or the end), every length 0-64, batches ending inside a step, empty blocks, blocks ending
+    at the last byte of their allocation, and CRC-32C on the same kernel. Batches of at least 1 M blocks
+    (the kernel's threshold) except the tiny one."""
+    host, d = buf
+    rng = np.random.default_rng(sum(map(ord, shape)))
+    offs, lens = wal_payloads(rng, 1_100_003, tuple(range(0, 65)), 3)  # (>= 1 M blocks: the one-pass kernel runs)
+    if shape == "shuffled":
+        p = rng.permutation(offs.size)
+        offs, lens = offs[p], lens[p]
+    elif shape == "late_shuffle":  # the first steps fit; later 64-block steps are out of order
+        p = np.arange(offs.size)
+        p[600_000:] = 600_000 + rng.permutation(offs.size - 600_000)
+        offs, lens = offs[p], lens[p]
+    elif shape == "late_long":
+        lens[-5] = 65
+    elif shape == "spread":  # every 97th step's blocks far apart
+        for s0 in range(640, offs.size - 64, 64 * 97):
+            offs[s0:s0 + 64] = rng.integers(0, host.size - 64, 64)
+    elif shape == "tiny_batch":  # (below the one-pass kernel's threshold: the general path)
+        offs, lens = offs[:37], lens[:37]
+    elif shape == "zero_lengths":
+        lens[rng.random(lens.size) < 0.3] = 0
+    elif shape == "at_allocation_end":
+        n = 1 << 20
+        lens = rng.integers(0, 65, n).astype(np.int32)
+        offs = (host.size - 64 * n + 64 * np.arange(n) + (64 - lens)).astype(np.int64)  # each ends a 64-byte slot
+    o, ln = torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu)
+    if shape == "crc32c":
+        got = u32(tk.crc32_batch(d, o, ln, algo="crc32c"))
+        sample = rng.choice(offs.size, 20_000, replace=False)
+        assert np.array_equal(got[sample], oracle_c(oracle, host, offs[sample], lens[sample]))
+        return
+    got = u32(tk.crc32_batch(d, o, ln))
+    want = oracle.batch(host, offs, lens)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, (shape, bad[:5])
+    if shape == "at_allocation_end":  # a copy whose last byte is the allocation's last byte
+        tail = d[host.size - 64 * n:].clone()
+        got = u32(tk.crc32_batch(tail, torch.from_numpy(offs - (host.size - 64 * n)).to(gpu), ln))
+        assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("mix", ["lane_small_large", "lane_then_large", "random_offsets", "lane_at_buffer_end"])
 def test_irregular_mixed_classes(gpu, oracle, mix):
     """Lane blocks (<= 64 B), small blocks (<= 1 KiB) and large ones in one batch: each class goes to

@@ -1399,8 +1399,8 @@ __device__ __forceinline__ std::uint32_t sarwate_bytes(const std::uint32_t* lds,
 // Folds NB blocks (dwords d[i], lengths n[i] <= 64, registers r[i] holding their initial values on
 // entry and their final raw registers on return) with their chains interleaved. UNI: every block has
 // the same length (uniform batches), so the bounds are wave-uniform and the branches scalar.
-template <int NB, bool UNI>
-__device__ __forceinline__ void lane_fold(const std::uint32_t* lds, const LaneConst& kc, const std::uint32_t (*d)[16],
+template <int NB, bool UNI, typename KC>
+__device__ __forceinline__ void lane_fold(const std::uint32_t* lds, const KC& kc, const std::uint32_t (*d)[16],
                                           const std::uint32_t* n, std::uint32_t* r) {
   Reg p[NB];
 #pragma unroll

@@ -37,8 +37,10 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
                           std::uint32_t n, std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* tile_ok,
                           std::uint32_t* counts, std::uint64_t* sinfo, std::uint64_t* ends, const PrepassOut& o,
                           std::uint32_t W, std::uint32_t ncu, std::uint32_t* out, std::uint32_t* row0,
-                          std::uint32_t group_stream, hipStream_t st);
+                          std::uint32_t group_stream, const std::uint32_t* gate, std::uint32_t seq,
+                          const std::uint32_t* gate_flags, hipStream_t st);
 hipError_t launch_stream_rows(const RowsArgs& a, hipStream_t st, unsigned grid);
+hipError_t launch_list_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st);
 std::uint64_t prepass_tiles(std::uint64_t n);
 hipError_t launch_span(const std::uint8_t* stage, const SpanDesc& one, const SpanDesc* desc, std::uint32_t n,
                        std::uint32_t out_xor, std::uint32_t* out, std::uint32_t* count, std::uint32_t base,
@@ -181,6 +183,7 @@ struct StreamScratch {
   std::uint32_t* tile_ok = nullptr;  // per scan tile: its blocks qualify for stream mode
   PrepassOut po{};
   std::uint64_t cap_blocks = 0;
+  std::uint32_t gate_seq = 0;  // irregular calls on this stream (crc_list_lanes' gate, counts[kCountGate])
 };
 
 // Spans up to this size take update()'s latency path (mapped pinned memory, one crc_span launch,
@@ -374,8 +377,9 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->seams), sizeof(Seam) * 2 * c->W));
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->wave_start), sizeof(std::uint32_t) * c->W));
     // counts[0..3], then (u64) the stream-mode info at counts + 4
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->counts), sizeof(std::uint32_t) * 16));
-    TKV_HIP(hipMemset(slot->counts, 0, sizeof(std::uint32_t) * 16));  // (the tile scan's ticket starts at 0)
+    // (crc_list_lanes' per-workgroup flags from word kListFlags on)
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->counts), sizeof(std::uint32_t) * (kListFlags + kListMaxGroups)));
+    TKV_HIP(hipMemset(slot->counts, 0, sizeof(std::uint32_t) * (kListFlags + kListMaxGroups)));
   }
   StreamScratch* s = slot.get();
   if (nblocks > s->cap_blocks) {
@@ -506,6 +510,7 @@ int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t s
 // those blocks faster than the stream walk's many-ends rows).
 std::atomic<int> g_stream_groups{0};
 
+constexpr std::uint64_t kListMinBlocks = std::uint64_t(1) << 20;
 int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::uint64_t* d_off, const std::uint32_t* d_len,
                   const std::uint32_t* d_init, std::uint32_t* d_out, std::uint64_t n, hipStream_t st) {
   if (n == 0) return TKV_OK;
@@ -544,9 +549,26 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   a.l_off = d_off;  // the lane phase walks the caller's own arrays
   a.l_len = d_len;
   a.l_tile = s->tile_ok;
+  // Default registers, at least kListMinBlocks blocks: one pass of crc_list_lanes first, which folds
+  // every block when none is longer than kLaneMax bytes (WAL payload lists); the general path's launches
+  // then return at once. When it meets a longer block it flags its workgroup and the general path folds
+  // the whole batch. Smaller batches skip it: the pass costs a batch it hands on ~10 us (2-4 % of a
+  // 1 GiB batch of larger blocks, profiles/r5/list_lanes/), more than it saves a short lane-only one.
+  // 
+  if (d_init == nullptr && n >= kListMinBlocks) {
+    s->gate_seq = s->gate_seq + 1u == 0u ? 1u : s->gate_seq + 1u;
+    a.gate = s->counts + kCountGate;
+    a.gate_seq = s->gate_seq;
+    a.gate_flags = s->counts + kListFlags;
+    RowsArgs l = a;
+    l.offsets = d_off;
+    l.lengths = d_len;
+    TKV_HIP(launch_list_lanes(l, static_cast<unsigned>(c->ncu), st));
+  }
   TKV_HIP(launch_prepass(d_base, d_off, d_len, a.nblocks, s->scan, s->tiles, s->tile_ok, s->counts, sinfo, s->po.big_off,
                          s->po, a.nwaves, static_cast<std::uint32_t>(c->ncu), d_out, row0,
-                         static_cast<std::uint32_t>(g_stream_groups.load(std::memory_order_relaxed)), st));
+                         static_cast<std::uint32_t>(g_stream_groups.load(std::memory_order_relaxed)), a.gate, a.gate_seq,
+                         a.gate_flags, st));
   // stream mode: crc_stream walks the rows and crc_rows finishes the block CRCs; general path:
   // crc_stream returns at once and crc_rows walks the rows (and combines its own seams)
   TKV_HIP(launch_stream_rows(a, st, static_cast<unsigned>(c->ncu)));

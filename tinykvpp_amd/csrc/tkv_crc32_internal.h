@@ -109,7 +109,22 @@ struct RowsArgs {
   const std::uint64_t* l_off;
   const std::uint32_t* l_len;
   const std::uint32_t* l_tile;  // per scan tile of 4096 blocks: kTileLanes when its lane blocks are ours
+  // irregular batches after crc_list_lanes (nullable): the kernels of the general path run only when
+  // gate[0] == gate_seq, i.e. the one-pass lane kernel found a block it does not take
+  const std::uint32_t* gate;
+  std::uint32_t gate_seq;
+  const std::uint32_t* gate_flags;  // crc_list_lanes: per workgroup, the call's number when it met such a block
 };
+// counts[kCountGate]: the call's sequence number when the general path must run (a block over
+// kLaneMax bytes): rows_tile_scan's workgroup 0 writes it from crc_list_lanes' per-workgroup flags
+// (counts[kListFlags + g]; one writer per address: a single word written by every wave that met such
+// a block took ~0.4 ms of same-address stores)
+constexpr int kCountGate = 12;
+constexpr int kListFlags = 64;
+constexpr unsigned kListMaxGroups = 1024;
+__device__ __forceinline__ bool gate_closed(const std::uint32_t* gate, std::uint32_t seq) {
+  return gate != nullptr && *gate != seq;
+}
 constexpr std::uint32_t kModeStream = 1;
 // counts[] of an irregular batch: [0] large blocks, [1] small blocks, [2] rows of the large blocks,
 // [3] mode, [4..7] stream-mode info (two u64), [8] lane and group blocks (len <= kGroupMax) of dense tiles

@@ -105,6 +105,7 @@ template <bool ALIGNED, bool UNIFORM>
 __global__ __launch_bounds__(kRowsThreads) void crc_rows(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
   if constexpr (!UNIFORM) {
+    if (gate_closed(a.gate, a.gate_seq)) return;  // crc_list_lanes folded every block
     // irregular batch whose blocks lie back to back: the prepass chose the byte-stream row walk,
     // crc_stream (launched just before) has walked it, and this launch turns its registers into
     // block CRCs
@@ -124,6 +125,7 @@ constexpr unsigned kStreamThreads = kThreads;
 constexpr int kStreamSkew = 154;
 __global__ __launch_bounds__(kStreamThreads) void crc_stream(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
+  if (gate_closed(a.gate, a.gate_seq)) return;  // crc_list_lanes folded every block
   if (dev::sload32(a.counts, 3) != kModeStream) {
     // General path: this launch folds the batch's lane and group blocks (len <= kGroup8Max, DESIGN.md
     // §4.5), each phase only if the prepass found its blocks; crc_rows follows with the rest. The
@@ -230,6 +232,206 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_lds(RowsArgs a) {
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 
+// ---- irregular batches of lane blocks in one pass -----------------------------------------------------
+// crc_list_lanes folds an irregular batch (default initial register) straight from the caller's
+// (offset, length) arrays, every block of at most kLaneMax bytes by one lane, with no prepass: the
+// general path's launches that follow it return at once unless it met a longer block (gate). Wave w
+// takes 64-block steps [w TS / W, (w + 1) TS / W). A step's blocks usually lie in a few KiB (WAL
+// payloads); then its bytes [lo, hi) are loaded by coalesced 16-byte buffer loads (a descriptor that
+// ends at hi, so nothing past the last block is read), kListRows rows per lane, kListRing steps ahead
+// in registers, written into the wave's LDS window just before the fold, and every lane folds its block
+// from the window (the WAL sweep's fold, tkv_wal_device.hip). The metadata is loaded kListRing steps
+// ahead of the data. A later step whose blocks do not fit one window, or are not in ascending order
+// from its first block, loads each block's granules per lane instead (the lane phase's loads; correct
+// for any batch); when a wave's first step does not fit, the batch goes to the general path.
+// A block over kLaneMax bytes stops the kernel: the first wave of a workgroup to meet one writes the
+// call's sequence number into the workgroup's flag, every wave polls the flags every 4 step groups and
+// leaves, and the general path then folds the whole batch (rows_tile_scan opens the gate from the
+// flags).
+constexpr std::uint32_t kListSpan = 4096;          // bytes of one step's window
+constexpr int kListRows = kListSpan / 1024;        // 1 KiB load rows per step
+constexpr int kListRing = 3;                       // steps of data in registers (R - 1 ahead of the fold)
+constexpr unsigned kListThreads = 1024;
+constexpr unsigned kListWaves = kListThreads / 64;
+constexpr std::uint32_t kListSlot = 32 + kListSpan + 96;  // a window slot: slack for reads before and after
+__device__ __forceinline__ std::uint32_t wave_max32(std::uint32_t v) {
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) v = std::max<std::uint32_t>(v, static_cast<std::uint32_t>(__shfl_xor(static_cast<int>(v), m, 64)));
+  return v;
+}
+__global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
+  constexpr std::uint32_t kTabBytes = kLdsSliceWords * 2;  // the 64 KiB 16-replica image
+  __shared__ __attribute__((aligned(16))) std::uint8_t lds[kTabBytes + kListWaves * kListSlot + 4 * (kLaneMax + 1)];
+  __shared__ std::uint32_t wg_hit_word;
+  std::uint32_t* wg_hit = &wg_hit_word;
+  if (threadIdx.x == 0) wg_hit_word = 0;  // (ordered before any use by the barrier below)
+  std::uint32_t* tab = reinterpret_cast<std::uint32_t*>(lds);
+  std::uint32_t* inj = reinterpret_cast<std::uint32_t*>(lds + kTabBytes + kListWaves * kListSlot);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // the batch's counts as the general path's debug entry points report them when it does not run
+    // (tkv_debug_irregular_*); the prepass rewrites them when it does
+    std::uint32_t* c = const_cast<std::uint32_t*>(a.counts);
+    c[0] = c[1] = c[2] = c[3] = 0;
+    c[kCountLanes] = c[kCountPhases] = c[kCountSmall4] = c[kCountSmall8] = 0;
+  }
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t wave = blockIdx.x * kListWaves + wv;
+  const std::uint64_t W = a.nwaves, n = a.nblocks;
+  const std::uint64_t TS = (n + 63u) / 64u;
+  const std::uint64_t s0 = wave * TS / W;
+  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
+  std::uint32_t* flags = const_cast<std::uint32_t*>(a.gate_flags);
+  const std::uint32_t seq = a.gate_seq;
+  // the first step's lengths before anything else: a workgroup that meets a longer block there leaves
+  // before its table fill (a batch of longer blocks costs this launch little more than its dispatch)
+  const std::uint64_t b00 = s0 * 64u + lane;
+  const std::uint32_t len00 = ns != 0 ? a.lengths[b00 < n ? b00 : n - 1u] : 0u;
+  if (__syncthreads_or(ns != 0 && b00 < n && len00 > kLaneMax ? 1 : 0) != 0) {
+    if (threadIdx.x == 0) __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  dev::fill_lds_slicing16(a.tabs, tab);
+  for (std::uint32_t i = threadIdx.x; i <= kLaneMax; i += blockDim.x) inj[i] = a.tabs->init_shift[i];
+  __syncthreads();
+  if (ns == 0) return;
+  const dev::LaneConstX kc = dev::lane_const16(lane);
+  std::uint8_t* win = lds + kTabBytes + wv * kListSlot + 32;  // the step's bytes from its granule start
+  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
+  constexpr int R = kListRing;
+  std::uint64_t m_off[R];
+  std::uint32_t m_len[R];
+  auto fetch = [&](std::uint32_t j, int k) {  // step j's descriptors
+    const std::uint64_t b = (s0 + j) * 64u + lane;
+    const std::uint64_t bc = b < n ? b : n - 1u;
+    m_off[k] = a.offsets[bc];
+    m_len[k] = a.lengths[bc];
+  };
+  uint4 d[R][kListRows];
+  std::uint32_t f_rel[R], f_len[R];  // the block's byte in the window (or its offset's low word), its length
+  std::uint32_t f_hi[R];             // gathered steps: the offset's high word
+  bool staged[R];
+  std::uint32_t quit = 0;  // wave-uniform (readfirstlane): the wave stops
+  auto issue = [&](std::uint32_t j, int k) {  // step j's bytes, from its descriptors in slot k
+    const std::uint64_t b = (s0 + j) * 64u + lane;
+    const bool live = j < ns && b < n;
+    const std::uint64_t off = m_off[k];
+    const std::uint32_t len = m_len[k];
+    const std::uint64_t lb = __ballot(live && len > kLaneMax);
+    // one store per workgroup (the first wave to meet a long block: an LDS exchange elects it)
+    if (lb != 0 && lane == 0 && atomicExch(wg_hit, 1u) == 0u)
+      __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    quit = __builtin_amdgcn_readfirstlane(quit | (lb != 0 ? 1u : 0u));
+    const std::uint64_t lo = dev::readlane64(off, 0);  // (lane 0 is live whenever any lane is)
+    const std::uint64_t al = (base + lo) & ~static_cast<std::uint64_t>(15);
+    const std::uint64_t rel = base + off - al;
+    const bool fit = !live || (off >= lo && rel + len <= kListSpan);
+    const bool all = __ballot(!fit) == 0 && __ballot(live) != 0;
+    const std::uint32_t hi = wave_max32(live ? static_cast<std::uint32_t>(rel < kListSpan ? rel + len : 0u) : 0u);
+    const std::uint32_t nrec = all ? ((hi + 15u) & ~15u) : 0u;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(static_cast<std::uintptr_t>(
+            static_cast<std::uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<std::uint32_t>(al))) |
+            static_cast<std::uint64_t>(static_cast<std::uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<std::uint32_t>(al >> 32)))) << 32)),
+        0, __builtin_amdgcn_readfirstlane(nrec), 0x00020000);
+#pragma unroll
+    for (int r = 0; r < kListRows; ++r) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16u * lane + 1024u * r, 0, 0);
+      d[k][r] = uint4{v[0], v[1], v[2], v[3]};
+    }
+    staged[k] = all;
+    f_rel[k] = all ? static_cast<std::uint32_t>(rel) : static_cast<std::uint32_t>(off);
+    f_hi[k] = static_cast<std::uint32_t>(off >> 32);
+    f_len[k] = live ? len : 0xFFFFFFFFu;
+  };
+  auto fold = [&](std::uint32_t j, int k) {
+    const std::uint32_t len = f_len[k];
+    const bool live = len != 0xFFFFFFFFu;
+    const std::uint32_t L = live ? len : 0u;
+    std::uint32_t crc;
+    if (staged[k]) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < kListRows; ++r) *reinterpret_cast<uint4*>(win + 1024u * r + 16u * lane) = d[k][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // the payload read as dwords ending on its last byte, the z bytes in front zeroed, every lane
+      // through the step's longest block with its register frozen after its own (tkv_wal_device.hip)
+      const std::uint32_t nd = (L + 3u) >> 2;
+      const std::uint32_t nmax = __builtin_amdgcn_readfirstlane(wave_max32(nd));
+      const std::uint32_t z = 4u * nd - L;
+      const std::uint32_t b0 = 32u + f_rel[k] - z;  // from the slot's start (32 bytes of slack in front)
+      const std::uint32_t* w = reinterpret_cast<const std::uint32_t*>(win - 32 + (b0 & ~3u));
+      const std::uint32_t sh = b0 & 3u;
+      std::uint32_t lo = w[1];
+      dev::Reg r{0u, 0u};
+      dev::slice4(tab, r, __builtin_amdgcn_alignbyte(lo, w[0], sh) & (~0u << (8u * z)), kc);
+      if (nd == 0u) r = dev::Reg{0u, 0u};
+      for (std::uint32_t i = 1; i < nmax; ++i) {
+        const std::uint32_t hw = w[i + 1u];
+        dev::Reg t = r;
+        dev::slice4(tab, t, __builtin_amdgcn_alignbyte(hw, lo, sh), kc);
+        if (i < nd) r = t;
+        lo = hw;
+      }
+      crc = r.value() ^ inj[L];
+    } else {
+      // a step that is not one window: each lane loads its own block's granules (lane_phase's loads)
+      const std::uintptr_t blk = base + (static_cast<std::uint64_t>(f_hi[k]) << 32 | f_rel[k]);
+      uint4 q[dev::kLaneGran];
+      dev::lane_issue<1>(blk, L, reinterpret_cast<std::uintptr_t>(a.dummy), q);
+      std::uint32_t dd[1][16], nn[1] = {L}, rr[1] = {a.init_default};
+      dev::lane_dwords<1>(q, static_cast<std::uint32_t>(blk & 15u), dd[0]);
+      dev::lane_fold<1, false>(tab, kc, dd, nn, rr);
+      crc = rr[0];
+    }
+    const std::uint64_t b = (s0 + j) * 64u + lane;
+    if (live) a.out[b] = crc ^ a.out_xor;
+  };
+  // prologue: descriptors of steps 0 .. R-1, their data, then the descriptors of steps R .. 2R-1
+#pragma unroll
+  for (int k = 0; k < R; ++k) fetch(static_cast<std::uint32_t>(k), k);
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    issue(static_cast<std::uint32_t>(k), k);
+    fetch(static_cast<std::uint32_t>(k + R), k);
+    __builtin_amdgcn_sched_barrier(0);  // in order: the loop's waits count the loads issued after these
+  }
+  // a first step that is not one window (blocks spread out, or 64-byte blocks back to back): the batch
+  // goes to the general path, whose lane phase takes such layouts faster than per-lane granule loads
+  if (!staged[0] && quit == 0u) {
+    if (lane == 0 && atomicExch(wg_hit, 1u) == 0u)
+      __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    quit = 1u;
+  }
+  // every fourth group of steps, the other workgroups' flags (16 per lane), checked one group later
+  std::uint32_t g = 0, nchk = 0;
+  const std::uint32_t ngroups = gridDim.x;
+  for (std::uint32_t t = 0; t < ns && quit == 0u; t += R) {
+    if (nchk++ % 4u == 0u) {
+      g = 0;
+#pragma unroll
+      for (std::uint32_t i = 0; i < kListMaxGroups / 64u; ++i) {
+        const std::uint32_t f = lane + 64u * i;
+        if (i * 64u < ngroups && f < ngroups) g |= __hip_atomic_load(flags + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == seq ? 1u : 0u;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const std::uint32_t j = t + static_cast<std::uint32_t>(k);
+      if (j >= ns || quit != 0u) break;
+      fold(j, k);
+      issue(j + R, k);
+      fetch(j + 2u * R, k);
+    }
+    // another workgroup met a long block: the general path folds the batch
+    quit = __builtin_amdgcn_readfirstlane(quit | (__ballot(g != 0u) != 0 ? 1u : 0u));
+  }
+}
+
+
+
 }  // namespace
 
 // ---- irregular-batch prepass -----------------------------------------------------------------------
@@ -289,7 +491,17 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
                                                               std::uint32_t* tile_ok, std::uint32_t* row0, std::uint32_t Ws,
                                                               std::uint32_t* lscan, std::uint32_t* tile_lanes,
                                                               std::uint32_t* cscan, std::uint64_t* tile_cls,
-                                                              std::uint32_t group_stream) {
+                                                              std::uint32_t group_stream, const std::uint32_t* gate,
+                                                              std::uint32_t seq, const std::uint32_t* gate_flags) {
+  if (gate != nullptr) {
+    // after crc_list_lanes: the general path runs only if one of its workgroups met a long block;
+    // workgroup 0 publishes the verdict for the launches that follow
+    bool hit = false;
+    for (unsigned i = threadIdx.x; i < kListMaxGroups; i += kTileThreads) hit = hit || gate_flags[i] == seq;
+    const bool open = __syncthreads_or(hit ? 1 : 0) != 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *const_cast<std::uint32_t*>(gate) = open ? seq : 0u;
+    if (!open) return;
+  }
   constexpr unsigned kTileWaves = kTileThreads / 64;
   constexpr unsigned kTileBpt = kScanTile / kTileThreads;
   static_assert(kScanTile % kTileThreads == 0 && kTileWaves >= 1 && kTileBpt >= 4 && kTileBpt % 4 == 0,
@@ -535,7 +747,8 @@ __global__ __launch_bounds__(1024) void rows_scan_tiles(std::uint64_t* tile_sums
                                                        std::uint64_t* tile_cls, std::uint32_t ntiles, std::uint32_t n, std::uint32_t* counts,
                                                        const std::uint32_t* tile_ok, const std::uint8_t* base,
                                                        const std::uint64_t* offsets, const std::uint32_t* lengths,
-                                                       std::uint64_t* sinfo) {
+                                                       std::uint64_t* sinfo, const std::uint32_t* gate, std::uint32_t seq) {
+  if (gate_closed(gate, seq)) return;
   __shared__ ScanLds L;
   rows_scan_tiles_body(L, tile_sums, tile_lanes, tile_cls, ntiles, n, counts, tile_ok, base, offsets, lengths, sinfo);
 }
@@ -584,7 +797,8 @@ __global__ void rows_finish(const std::uint8_t* base, const std::uint64_t* offse
                             std::uint32_t n, const std::uint64_t* scan, const std::uint64_t* tile_offs,
                             std::uint32_t* counts, const std::uint32_t* tile_ok, PrepassOut o, std::uint32_t W,
                             std::uint32_t* out, std::uint64_t* ends, std::uint64_t* sinfo, std::uint32_t Ws,
-                            const std::uint32_t* row0) {
+                            const std::uint32_t* row0, const std::uint32_t* gate, std::uint32_t seq) {
+  if (gate_closed(gate, seq)) return;
   const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
   if (b >= n) return;
   const bool stream = dev::sload32(counts, 3) == kModeStream;  // rows_scan_tiles found every tile back to back
@@ -653,7 +867,8 @@ __global__ __launch_bounds__(T) void rows_finish_fused(
     const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths, std::uint32_t n,
     const std::uint64_t* scan, const std::uint64_t* tile_sums, const std::uint32_t* tile_ok, std::uint32_t ntiles,
     std::uint32_t* counts, PrepassOut o, std::uint32_t W, std::uint32_t* out, std::uint64_t* ends,
-    std::uint64_t* sinfo, std::uint32_t Ws, const std::uint32_t* row0) {
+    std::uint64_t* sinfo, std::uint32_t Ws, const std::uint32_t* row0, const std::uint32_t* gate, std::uint32_t seq) {
+  if (gate_closed(gate, seq)) return;
   static_assert(kScanTile % (T * PER) == 0 && T % 64 == 0, "a workgroup lies in one scan tile");
   constexpr std::uint32_t kWaves = T / 64;
   __shared__ std::uint64_t red[8][kWaves];
@@ -1063,11 +1278,23 @@ hipError_t launch_fixup(const RowsArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// One-pass lane kernel of an irregular batch (default initial register): see crc_list_lanes.
+hipError_t launch_list_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
+  const std::uint64_t steps = (static_cast<std::uint64_t>(a.nblocks) + 63u) / 64u;
+  const std::uint64_t grid = std::max<std::uint64_t>(
+      1, std::min<std::uint64_t>(std::min<std::uint64_t>(ncu, kListMaxGroups), (steps + kListWaves - 1) / kListWaves));
+  RowsArgs b = a;
+  b.nwaves = static_cast<std::uint32_t>(grid * kListWaves);
+  hipLaunchKernelGGL(crc_list_lanes, dim3(static_cast<unsigned>(grid)), dim3(kListThreads), 0, st, b);
+  return hipGetLastError();
+}
+
 hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets, const std::uint32_t* lengths,
                           std::uint32_t n, std::uint64_t* scan, std::uint64_t* tile_sums, std::uint32_t* tile_ok,
                           std::uint32_t* counts, std::uint64_t* sinfo, std::uint64_t* ends, const PrepassOut& o,
                           std::uint32_t W, std::uint32_t ncu, std::uint32_t* out, std::uint32_t* row0,
-                          std::uint32_t group_stream, hipStream_t st) {
+                          std::uint32_t group_stream, const std::uint32_t* gate, std::uint32_t seq,
+                          const std::uint32_t* gate_flags, hipStream_t st) {
   const std::uint32_t Ws = ncu * (kStreamThreads / 64);  // crc_stream's waves
   // Grid sizes in 64-bit arithmetic: n may be close to 2^32 (the host caps it at kMaxIrregularBlocks).
   const std::uint64_t ntiles = prepass_tiles(n);
@@ -1076,20 +1303,20 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
   if (ntiles <= kFusedTiles)
     hipLaunchKernelGGL(rows_tile_scan<1024>, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets,
                        lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
-                       group_stream);
+                       group_stream, gate, seq, gate_flags);
   else
     hipLaunchKernelGGL(rows_tile_scan<512>, dim3(static_cast<unsigned>(ntiles)), dim3(512), 0, st, base, offsets,
                        lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
-                       group_stream);
+                       group_stream, gate, seq, gate_flags);
   if (ntiles <= kFusedTiles) {
     hipLaunchKernelGGL((rows_finish_fused<kFinishThreads, kFinishPer>), dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
                        offsets, lengths, n, scan, tile_sums, tile_ok, static_cast<std::uint32_t>(ntiles), counts, o,
-                       W, out, ends, sinfo, Ws, row0);
+                       W, out, ends, sinfo, Ws, row0, gate, seq);
   } else {
     hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, o.tile_lanes, o.tile_cls,
-                       static_cast<std::uint32_t>(ntiles), n, counts, tile_ok, base, offsets, lengths, sinfo);
+                       static_cast<std::uint32_t>(ntiles), n, counts, tile_ok, base, offsets, lengths, sinfo, gate, seq);
     hipLaunchKernelGGL(rows_finish, dim3(static_cast<unsigned>(nfinish)), dim3(256), 0, st, base, offsets, lengths,
-                       n, scan, tile_sums, counts, tile_ok, o, W, out, ends, sinfo, Ws, row0);
+                       n, scan, tile_sums, counts, tile_ok, o, W, out, ends, sinfo, Ws, row0, gate, seq);
   }
   return hipGetLastError();
 }
