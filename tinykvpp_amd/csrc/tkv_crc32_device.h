@@ -133,6 +133,29 @@ __device__ __forceinline__ std::uint32_t wave_xor_to_lane63(std::uint32_t v) {
   return v;
 }
 
+// Maximum of v over the 64 lanes, wave-uniform (the DPP pattern of wave_xor_to_lane63, then lane 63):
+// VALU only, no LDS round trips (a shuffle-based reduction costs six dependent ds_bpermute).
+__device__ __forceinline__ std::uint32_t wave_max(std::uint32_t v) {
+  v = std::max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xF, 0xF, false)));
+  v = std::max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4E, 0xF, 0xF, false)));
+  v = std::max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x141, 0xF, 0xF, false)));
+  v = std::max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x140, 0xF, 0xF, false)));
+  v = std::max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xA, 0xF, false)));
+  v = std::max(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xC, 0xF, false)));
+  return static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+
+// Minimum of v over the 64 lanes, wave-uniform (as wave_max; lanes past a row's edge read ~0).
+__device__ __forceinline__ std::uint32_t wave_min(std::uint32_t v) {
+  v = std::min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(v), 0xB1, 0xF, 0xF, false)));
+  v = std::min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(v), 0x4E, 0xF, 0xF, false)));
+  v = std::min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(v), 0x141, 0xF, 0xF, false)));
+  v = std::min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(v), 0x140, 0xF, 0xF, false)));
+  v = std::min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(v), 0x142, 0xA, 0xF, false)));
+  v = std::min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(v), 0x143, 0xC, 0xF, false)));
+  return static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+
 // a*b mod P in the reflected representation (x^0 = 0x80000000).
 __device__ __forceinline__ std::uint32_t multmodp(std::uint32_t a, std::uint32_t b, std::uint32_t poly) {
   std::uint32_t p = 0;

@@ -254,11 +254,6 @@ constexpr int kListRing = 3;                       // steps of data in registers
 constexpr unsigned kListThreads = 1024;
 constexpr unsigned kListWaves = kListThreads / 64;
 constexpr std::uint32_t kListSlot = 32 + kListSpan + 96;  // a window slot: slack for reads before and after
-__device__ __forceinline__ std::uint32_t wave_max32(std::uint32_t v) {
-#pragma unroll
-  for (int m = 32; m > 0; m >>= 1) v = std::max<std::uint32_t>(v, static_cast<std::uint32_t>(__shfl_xor(static_cast<int>(v), m, 64)));
-  return v;
-}
 __global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
   constexpr std::uint32_t kTabBytes = kLdsSliceWords * 2;  // the 64 KiB 16-replica image
   __shared__ __attribute__((aligned(16))) std::uint8_t lds[kTabBytes + kListWaves * kListSlot + 4 * (kLaneMax + 1)];
@@ -327,7 +322,7 @@ __global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
     const std::uint64_t rel = base + off - al;
     const bool fit = !live || (off >= lo && rel + len <= kListSpan);
     const bool all = __ballot(!fit) == 0 && __ballot(live) != 0;
-    const std::uint32_t hi = wave_max32(live ? static_cast<std::uint32_t>(rel < kListSpan ? rel + len : 0u) : 0u);
+    const std::uint32_t hi = dev::wave_max(live ? static_cast<std::uint32_t>(rel < kListSpan ? rel + len : 0u) : 0u);
     const std::uint32_t nrec = all ? ((hi + 15u) & ~15u) : 0u;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(static_cast<std::uintptr_t>(
@@ -359,7 +354,7 @@ __global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
       // the payload read as dwords ending on its last byte, the z bytes in front zeroed, every lane
       // through the step's longest block with its register frozen after its own (tkv_wal_device.hip)
       const std::uint32_t nd = (L + 3u) >> 2;
-      const std::uint32_t nmax = __builtin_amdgcn_readfirstlane(wave_max32(nd));
+      const std::uint32_t nmax = dev::wave_max(nd);
       const std::uint32_t z = 4u * nd - L;
       const std::uint32_t b0 = 32u + f_rel[k] - z;  // from the slot's start (32 bytes of slack in front)
       const std::uint32_t* w = reinterpret_cast<const std::uint32_t*>(win - 32 + (b0 & ~3u));

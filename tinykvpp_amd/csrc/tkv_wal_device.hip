@@ -168,11 +168,6 @@ __device__ __forceinline__ std::uint32_t lane_prefix(std::uint32_t v, std::uint3
   return pre;
 }
 
-__device__ __forceinline__ std::uint32_t wave_min_u32(std::uint32_t v) {
-#pragma unroll
-  for (int m = 32; m > 0; m >>= 1) v = std::min<std::uint32_t>(v, static_cast<std::uint32_t>(__shfl_xor(static_cast<int>(v), m, 64)));
-  return v;
-}
 
 // The first plausible header in [ps, qe) (qe - ps <= kSearchStep; every position there has 26 bytes
 // in the image): op and tombstone bytes (p+8, p+17) 0 or 1, then record_len = 18 + klen + vlen and
@@ -296,11 +291,6 @@ __device__ __forceinline__ void walk_piece(const std::uint8_t* win, P rs, std::u
   if (go) wk.x = p;
 }
 
-__device__ __forceinline__ std::uint32_t wave_max_u32(std::uint32_t v) {
-#pragma unroll
-  for (int m = 32; m > 0; m >>= 1) v = std::max<std::uint32_t>(v, static_cast<std::uint32_t>(__shfl_xor(static_cast<int>(v), m, 64)));
-  return v;
-}
 
 // CRC-32 (finalized) of the L <= kLaneFold window bytes at s, one record per lane. The record is read
 // from s - z, z = 4 nd - L (nd = its dwords), so that it ends on a dword; the z bytes in front are
@@ -313,7 +303,7 @@ __device__ __forceinline__ std::uint32_t wave_max_u32(std::uint32_t v) {
 __device__ __forceinline__ std::uint32_t fold_lane(const std::uint8_t* win, const std::uint32_t* tab, const std::uint32_t* inj,
                                                    const dev::LaneConstX& kc, std::uint32_t s, std::uint32_t L) {
   const std::uint32_t nd = (L + 3u) >> 2;
-  const std::uint32_t nmax = __builtin_amdgcn_readfirstlane(wave_max_u32(nd));
+  const std::uint32_t nmax = dev::wave_max(nd);
   const std::uint32_t z = 4u * nd - L;
   const std::uint32_t b0 = s - z;  // (s >= 8: b0 >= 5)
   const std::uint32_t sh = b0 & 3u;
@@ -485,7 +475,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
           std::uint32_t nlist;
           const std::uint32_t pre = lane_prefix<4>(nn, &nlist);
           const std::uint32_t t = on && wk.tiny < nn ? pre + wk.tiny : 0xFFFFFFFFu;
-          const std::uint32_t tmin = wave_min_u32(t);
+          const std::uint32_t tmin = dev::wave_min(t);
           const std::uint32_t nl = std::min<std::uint32_t>(std::min<std::uint32_t>(nlist, tmin == 0xFFFFFFFFu ? nlist : tmin + 1u), kList);
 #pragma unroll
           for (std::uint32_t j = 0; j < kStore; ++j)

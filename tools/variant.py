@@ -9,6 +9,7 @@ Patches:
             over every wave (export tkv_debug_wal_stamps; tools/wal_sweep_probe.py prints the shares)
   region5k  5 KiB regions and 16 waves per sweep workgroup (4 waves per SIMD)
   region7k  7 KiB regions and 12 waves per sweep workgroup (3 waves per SIMD)
+  listpoll64  crc_list_lanes polls the other workgroups' flags every 64 step groups instead of 4
 """
 import os
 import shutil
@@ -60,7 +61,13 @@ def region7k(s):
     return s.replace("constexpr unsigned kSweepWaves = 8; ", "constexpr unsigned kSweepWaves = 12; ")
 
 
-PATCHES = {"stamp": stamp, "region5k": region5k, "region7k": region7k}
+def listpoll64(s):
+    x = "if (nchk++ % 4u == 0u) {"
+    assert s.count(x) == 1
+    return s.replace(x, "if (nchk++ % 64u == 0u) {")
+
+
+PATCHES = {"stamp": stamp, "region5k": region5k, "region7k": region7k, "listpoll64": listpoll64}
 
 
 def main():
@@ -69,13 +76,16 @@ def main():
     try:
         src = os.path.join(t, "csrc")
         shutil.copytree(H, src, ignore=shutil.ignore_patterns("build", "*.so", "*.o"))
-        p = os.path.join(src, "tkv_wal_device.hip")
-        with open(p) as f:
-            s = f.read()
+        for fn in ("tkv_wal_device.hip", "tkv_crc32_kernels.hip"):
+            p = os.path.join(src, fn)
+            with open(p) as f:
+                s = f.read()
             for pn in patches:
-                s = PATCHES[pn](s)
-        with open(p, "w") as f:
-            f.write(s)
+                if (pn.startswith("list")) == (fn == "tkv_crc32_kernels.hip"):
+                    s = PATCHES[pn](s)
+            with open(p, "w") as f:
+                f.write(s)
+        p = os.path.join(src, "tkv_wal_device.hip")
         fl = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I" + os.path.join(ROOT, "include"), "-I" + src]
         hc = "/opt/rocm/bin/hipcc"
         subprocess.check_call([hc] + fl + ["-c", os.path.join(src, "tkv_crc32_kernels.hip"), "-o", os.path.join(t, "k.o")])
