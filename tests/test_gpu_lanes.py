@@ -244,15 +244,17 @@ def test_lane_blocks_then_stream_batch_same_scratch(gpu, oracle, buf):
 
 @pytest.mark.parametrize("shape", ["wal_payloads", "mixed_gaps", "back_to_back_128", "back_to_back_128_stream",
                                    "back_to_back_300"])
-def test_irregular_more_than_1024_tiles(gpu, oracle, shape):
-    """Batches of more than 4 M blocks (over 1024 prepass tiles of 4096 blocks) take the 512-thread
-    tile scan and the unfused scatter: lane-dense tiles (WAL payloads), tiles mixing lane, small and
+@pytest.mark.parametrize("tiles", [129, 1025])
+def test_irregular_more_than_1024_tiles(gpu, oracle, shape, tiles):
+    """Batches of more than 128 prepass tiles of 4096 blocks take the one-workgroup tile-sum scan and
+    the looping scatter (rows_finish), and above 1024 tiles (4 M blocks) also the 512-thread tile scan:
+    lane-dense tiles (WAL payloads), tiles mixing lane, small and
     large blocks with random gaps, and 128-byte blocks back to back, which take stream mode through
     rows_scan_tiles' verdict with tkv_debug_set_stream_groups(1), the general path by default;
     per-block initial registers on the mixed batch."""
     rng = np.random.default_rng({"wal_payloads": 1, "mixed_gaps": 2, "back_to_back_128": 3, "back_to_back_128_stream": 3,
                                  "back_to_back_300": 4}[shape])
-    n = 4096 * 1025 + 777
+    n = 4096 * tiles - 4096 + 777
     if shape == "wal_payloads":
         offs, lens = wal_payloads(rng, n, WAL_SIZES, 3)
     elif shape == "mixed_gaps":

@@ -436,7 +436,8 @@ __global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
 //   * compacts large blocks into big_off/big_len/big_idx with their row offsets (row_scan) for the
 //     row kernel, and records the first large block of every row-kernel wave (wave_start),
 //   * leaves counts = {large blocks, small blocks, rows of large blocks}.
-constexpr int kScanTile = 4096;  // blocks per scan workgroup (rows_tile_scan)
+constexpr int kScanTile = 4096;  // blocks per scan tile (rows_tile_scan)
+constexpr std::uint32_t kScanGroupsPerCu = 2;
 
 __device__ __forceinline__ std::uint64_t scan_item(std::uint32_t len) {
   return len <= kSmallMax ? 1ull : static_cast<std::uint64_t>(rows_for_len(len)) << 32;
@@ -462,8 +463,8 @@ __device__ __forceinline__ StreamGeom stream_geometry(const std::uint8_t* base, 
   return {zoff, s0rel, end >= off0 ? (end - off0 + s0rel + kRow - 1) / kRow : 0};
 }
 
-// One workgroup per scan tile of kScanTile blocks, T threads with kScanTile / T consecutive blocks
-// each. Batches of more than kFusedTiles tiles (over 4 M blocks: WAL-record-sized batches) take
+// Scan tiles of kScanTile blocks, looped over by at most kScanGroupsPerCu workgroups per CU, T
+// threads with kScanTile / T consecutive blocks each. Batches of more than kFusedTiles tiles (over 4 M blocks: WAL-record-sized batches) take
 // 512-thread tiles, which keep more tiles in flight per CU; fewer tiles keep 1024 threads (in one
 // process, 1 GiB batches, profiles/r3/scan_tiles/: WAL payloads of 36 B with 8-byte gaps 1820 ->
 // 1957 GB/s, back-to-back 36 B 1991 -> 2212, 64 B 2687 -> 2818, 128 B 730 -> 697 GB/s; cfg4 and
@@ -508,152 +509,156 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     const std::uint64_t TR = stream_geometry(sbase, offsets, lengths, n).rows;
     row0[w] = static_cast<std::uint32_t>(dev::stream_row0<kStreamSkew>(w, TR, Ws));
   }
-  const std::uint64_t base = static_cast<std::uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * kTileBpt;
-  const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  // Every block first counts as a small or large one (v); lane blocks, the two group classes and the
-  // small blocks over kGroup8Max bytes are also counted in one packed u64 (16 bits each, lane blocks
-  // lowest, then 4- and 8-lane group blocks, then the rest up to kSmallMax: a tile has at most 4096 of
-  // each), so the one scan below yields all of them, and the tile's verdict on them (below) only
-  // subtracts. The last two fields also place listed small blocks in their class's list (cscan).
-  std::uint64_t pk[kTileBpt];
-  std::uint64_t v[kTileBpt], s = 0;
-  std::uint64_t ls = 0;
-  // Loads at clamped indices, all issued before any is used (n >= 1 here): one round trip for the
-  // lengths, one more for the offsets, which only a thread whose blocks are all long enough for stream
-  // mode reads (a lane-block batch never touches them).
-  std::uint32_t len[kTileBpt];
-  bool ok = true;
-#pragma unroll
-  for (unsigned i = 0; i < kTileBpt; ++i) {
-    const std::uint64_t b = base + i;
-    len[i] = lengths[b < n ? b : n - 1];
-  }
-#pragma unroll
-  for (unsigned i = 0; i < kTileBpt; ++i) {
-    const bool in = base + i < n;
-    len[i] = in ? len[i] : 0u;
-    pk[i] = !in                    ? 0ull
-            : len[i] <= kLaneMax    ? 1ull
-            : len[i] <= kGroupMax   ? 1ull << 16
-            : len[i] <= kGroup8Max  ? 1ull << 32
-            : len[i] <= kSmallMax   ? 1ull << 48
-                                    : 0ull;
-    v[i] = in ? scan_item(len[i]) : 0ull;
-    s += v[i];
-    ls += pk[i];
-    ok = ok && (!in || len[i] >= kStreamMinLen);
-  }
-  if (ok && base < n) {
-    std::uint64_t o[kTileBpt + 1];
-#pragma unroll
-    for (unsigned i = 0; i <= kTileBpt; ++i) o[i] = offsets[base + i < n ? base + i : n - 1];
-#pragma unroll
-    for (unsigned i = 0; i < kTileBpt; ++i) ok = ok && (base + i + 1 >= n || o[i] + len[i] == o[i + 1]);
-  }
-  // Inclusive scans of the thread sums inside the wave (cross-lane shifts, no barriers), then the
-  // wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
-  std::uint64_t inc = s;
-  std::uint64_t linc = ls;
-#pragma unroll
-  for (unsigned off = 1; off < 64; off <<= 1) {
-    const std::uint64_t y = __shfl_up(inc, off, 64);
-    const std::uint64_t ly = __shfl_up(linc, off, 64);
-    inc += lane >= off ? y : 0ull;
-    linc += lane >= off ? ly : 0ull;
-  }
-  const bool wave_ok = __ballot(!ok) == 0;
-  if (lane == 63u) {
-    wsum[wid] = inc;
-    lsum[wid] = linc;
-    wok[wid] = wave_ok ? 1u : 0u;
-  }
-  __syncthreads();
-  std::uint64_t wpre = 0, tot = 0, lpre = 0, ltot = 0;
-  std::uint32_t all_ok = 1;
-#pragma unroll
-  for (unsigned w = 0; w < kTileWaves; ++w) {
-    const std::uint64_t t = wsum[w];
-    const std::uint64_t lt = lsum[w];
-    wpre += w < wid ? t : 0ull;
-    tot += t;
-    lpre += w < wid ? lt : 0ull;
-    ltot += lt;
-    all_ok &= wok[w];
-  }
-  // A tile with at least kLaneDenseTile lane blocks leaves them to the lane phase (in no list); one
-  // with at most kGroupTileRows rows of large blocks leaves each group class of which it holds at
-  // least that class's threshold to that class's group pass; in other tiles they are listed as small
-  // blocks, so a batch with a few of them scattered about pays no phase walk over its metadata.
-  const bool few_rows = (tot >> 32) <= kGroupTileRows;
-  auto cls = [&](int c) { return static_cast<std::uint32_t>((ltot >> (16 * c)) & 0xFFFFu); };
-  const std::uint32_t tph = (cls(0) >= kLaneDenseTile ? kTileLanes : 0u) |
-                            (few_rows && cls(1) >= kGroupDenseTile ? kTileGroups : 0u) |
-                            (few_rows && cls(2) >= kGroup8DenseTile ? kTileGroups8 : 0u);
-  const std::uint64_t tmask = ((tph & kTileLanes) ? 0xFFFFull : 0ull) | ((tph & kTileGroups) ? 0xFFFFull << 16 : 0ull) |
-                              ((tph & kTileGroups8) ? 0xFFFFull << 32 : 0ull);
-  auto taken = [&](std::uint64_t x) {  // the phase blocks among packed counts x
-    x &= tmask;
-    return static_cast<std::uint32_t>((x & 0xFFFFu) + ((x >> 16) & 0xFFFFu) + ((x >> 32) & 0xFFFFu));
-  };
-  // listed blocks of kGroupMax + 1 .. kGroup8Max bytes (none when the 8-lane pass takes them) and of
-  // kGroup8Max + 1 .. kSmallMax bytes among packed counts x, as the low and high half of a u32
-  const std::uint64_t c8mask = (tph & kTileGroups8) ? 0ull : 0xFFFFull << 32;
-  auto cls_pair = [&](std::uint64_t x) {
-    return static_cast<std::uint32_t>(((x & c8mask) >> 32) | ((x >> 48) << 16));
-  };
-  // A tile whose bytes are mostly in small blocks (at least kStreamSmallTile blocks of at most
-  // kSmallMax bytes and at most kGroupTileRows rows of larger ones) does not qualify for stream mode
-  // (unless group_stream, a debug setting): the group passes and the small phase fold such blocks at
-  // the rate of gapped ones, where the stream walk's rows of many block ends ran slower (back-to-back
-  // 128 B: 1404 against 2351 GB/s, profiles/r3/group_phase/; 300-1000 B: 2893 against 3206,
-  // profiles/r4/s5/). Tiles whose bytes are in larger blocks keep stream mode, where it wins (cfg4,
-  // 64 KiB blocks, and short batches of any blocks).
-  const bool small_tile = few_rows && static_cast<std::uint32_t>(tot) >= kStreamSmallTile;
-  const bool stream_ok = all_ok && (group_stream != 0u || !small_tile);
-  const std::uint64_t tile_n = n - static_cast<std::uint64_t>(blockIdx.x) * kScanTile;  // blocks in the tile
-  const bool all_taken = taken(ltot) == (tile_n < kScanTile ? tile_n : kScanTile);
-  if (threadIdx.x == 0) tile_ok[blockIdx.x] = (stream_ok ? kTileStream : 0u) | tph | (all_taken ? kTileAllTaken : 0u);
-  std::uint64_t run = wpre + inc - s;  // exclusive, lane and group blocks counted as small
-  std::uint64_t lrun = lpre + linc - ls;
-  if (tph == 0 && base + kTileBpt <= n) {
-    // every block of such a tile is listed: this thread's entries as whole 16-byte stores
-    // (scan, lscan and cscan are 16-byte aligned scratch, base a multiple of kTileBpt >= 4)
-    std::uint64_t sc[kTileBpt];
-    std::uint32_t cs[kTileBpt];
-#pragma unroll
+  const std::uint32_t ntiles = static_cast<std::uint32_t>((static_cast<std::uint64_t>(n) + kScanTile - 1) / kScanTile);
+  for (std::uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const std::uint64_t base = static_cast<std::uint64_t>(tile) * kScanTile + threadIdx.x * kTileBpt;
+    const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    // Every block first counts as a small or large one (v); lane blocks, the two group classes and the
+    // small blocks over kGroup8Max bytes are also counted in one packed u64 (16 bits each, lane blocks
+    // lowest, then 4- and 8-lane group blocks, then the rest up to kSmallMax: a tile has at most 4096 of
+    // each), so the one scan below yields all of them, and the tile's verdict on them (below) only
+    // subtracts. The last two fields also place listed small blocks in their class's list (cscan).
+    std::uint64_t pk[kTileBpt];
+    std::uint64_t v[kTileBpt], s = 0;
+    std::uint64_t ls = 0;
+    // Loads at clamped indices, all issued before any is used (n >= 1 here): one round trip for the
+    // lengths, one more for the offsets, which only a thread whose blocks are all long enough for stream
+    // mode reads (a lane-block batch never touches them).
+    std::uint32_t len[kTileBpt];
+    bool ok = true;
+  #pragma unroll
     for (unsigned i = 0; i < kTileBpt; ++i) {
-      sc[i] = run;
-      cs[i] = cls_pair(lrun);
-      run += v[i];
-      lrun += pk[i];
+      const std::uint64_t b = base + i;
+      len[i] = lengths[b < n ? b : n - 1];
     }
-#pragma unroll
-    for (unsigned i = 0; i < kTileBpt; i += 2)
-      *reinterpret_cast<ulonglong2*>(scan + base + i) = make_ulonglong2(sc[i], sc[i + 1]);
-#pragma unroll
-    for (unsigned i = 0; i < kTileBpt; i += 4) {
-      *reinterpret_cast<uint4*>(lscan + base + i) = make_uint4(0, 0, 0, 0);
-      *reinterpret_cast<uint4*>(cscan + base + i) = make_uint4(cs[i], cs[i + 1], cs[i + 2], cs[i + 3]);
-    }
-  } else {
-#pragma unroll
+  #pragma unroll
     for (unsigned i = 0; i < kTileBpt; ++i) {
-      if (base + i < n && !taken(pk[i])) {  // the scatter reads these for listed blocks only
-        const std::uint32_t t = taken(lrun);
-        scan[base + i] = run - t;  // (t <= the small count in run's low half: no borrow)
-        lscan[base + i] = t;
-        cscan[base + i] = cls_pair(lrun);
+      const bool in = base + i < n;
+      len[i] = in ? len[i] : 0u;
+      pk[i] = !in                    ? 0ull
+              : len[i] <= kLaneMax    ? 1ull
+              : len[i] <= kGroupMax   ? 1ull << 16
+              : len[i] <= kGroup8Max  ? 1ull << 32
+              : len[i] <= kSmallMax   ? 1ull << 48
+                                      : 0ull;
+      v[i] = in ? scan_item(len[i]) : 0ull;
+      s += v[i];
+      ls += pk[i];
+      ok = ok && (!in || len[i] >= kStreamMinLen);
+    }
+    if (ok && base < n) {
+      std::uint64_t o[kTileBpt + 1];
+  #pragma unroll
+      for (unsigned i = 0; i <= kTileBpt; ++i) o[i] = offsets[base + i < n ? base + i : n - 1];
+  #pragma unroll
+      for (unsigned i = 0; i < kTileBpt; ++i) ok = ok && (base + i + 1 >= n || o[i] + len[i] == o[i + 1]);
+    }
+    // Inclusive scans of the thread sums inside the wave (cross-lane shifts, no barriers), then the
+    // wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
+    std::uint64_t inc = s;
+    std::uint64_t linc = ls;
+  #pragma unroll
+    for (unsigned off = 1; off < 64; off <<= 1) {
+      const std::uint64_t y = __shfl_up(inc, off, 64);
+      const std::uint64_t ly = __shfl_up(linc, off, 64);
+      inc += lane >= off ? y : 0ull;
+      linc += lane >= off ? ly : 0ull;
+    }
+    const bool wave_ok = __ballot(!ok) == 0;
+    if (lane == 63u) {
+      wsum[wid] = inc;
+      lsum[wid] = linc;
+      wok[wid] = wave_ok ? 1u : 0u;
+    }
+    __syncthreads();
+    std::uint64_t wpre = 0, tot = 0, lpre = 0, ltot = 0;
+    std::uint32_t all_ok = 1;
+  #pragma unroll
+    for (unsigned w = 0; w < kTileWaves; ++w) {
+      const std::uint64_t t = wsum[w];
+      const std::uint64_t lt = lsum[w];
+      wpre += w < wid ? t : 0ull;
+      tot += t;
+      lpre += w < wid ? lt : 0ull;
+      ltot += lt;
+      all_ok &= wok[w];
+    }
+    // A tile with at least kLaneDenseTile lane blocks leaves them to the lane phase (in no list); one
+    // with at most kGroupTileRows rows of large blocks leaves each group class of which it holds at
+    // least that class's threshold to that class's group pass; in other tiles they are listed as small
+    // blocks, so a batch with a few of them scattered about pays no phase walk over its metadata.
+    const bool few_rows = (tot >> 32) <= kGroupTileRows;
+    auto cls = [&](int c) { return static_cast<std::uint32_t>((ltot >> (16 * c)) & 0xFFFFu); };
+    const std::uint32_t tph = (cls(0) >= kLaneDenseTile ? kTileLanes : 0u) |
+                              (few_rows && cls(1) >= kGroupDenseTile ? kTileGroups : 0u) |
+                              (few_rows && cls(2) >= kGroup8DenseTile ? kTileGroups8 : 0u);
+    const std::uint64_t tmask = ((tph & kTileLanes) ? 0xFFFFull : 0ull) | ((tph & kTileGroups) ? 0xFFFFull << 16 : 0ull) |
+                                ((tph & kTileGroups8) ? 0xFFFFull << 32 : 0ull);
+    auto taken = [&](std::uint64_t x) {  // the phase blocks among packed counts x
+      x &= tmask;
+      return static_cast<std::uint32_t>((x & 0xFFFFu) + ((x >> 16) & 0xFFFFu) + ((x >> 32) & 0xFFFFu));
+    };
+    // listed blocks of kGroupMax + 1 .. kGroup8Max bytes (none when the 8-lane pass takes them) and of
+    // kGroup8Max + 1 .. kSmallMax bytes among packed counts x, as the low and high half of a u32
+    const std::uint64_t c8mask = (tph & kTileGroups8) ? 0ull : 0xFFFFull << 32;
+    auto cls_pair = [&](std::uint64_t x) {
+      return static_cast<std::uint32_t>(((x & c8mask) >> 32) | ((x >> 48) << 16));
+    };
+    // A tile whose bytes are mostly in small blocks (at least kStreamSmallTile blocks of at most
+    // kSmallMax bytes and at most kGroupTileRows rows of larger ones) does not qualify for stream mode
+    // (unless group_stream, a debug setting): the group passes and the small phase fold such blocks at
+    // the rate of gapped ones, where the stream walk's rows of many block ends ran slower (back-to-back
+    // 128 B: 1404 against 2351 GB/s, profiles/r3/group_phase/; 300-1000 B: 2893 against 3206,
+    // profiles/r4/s5/). Tiles whose bytes are in larger blocks keep stream mode, where it wins (cfg4,
+    // 64 KiB blocks, and short batches of any blocks).
+    const bool small_tile = few_rows && static_cast<std::uint32_t>(tot) >= kStreamSmallTile;
+    const bool stream_ok = all_ok && (group_stream != 0u || !small_tile);
+    const std::uint64_t tile_n = n - static_cast<std::uint64_t>(tile) * kScanTile;  // blocks in the tile
+    const bool all_taken = taken(ltot) == (tile_n < kScanTile ? tile_n : kScanTile);
+    if (threadIdx.x == 0) tile_ok[tile] = (stream_ok ? kTileStream : 0u) | tph | (all_taken ? kTileAllTaken : 0u);
+    std::uint64_t run = wpre + inc - s;  // exclusive, lane and group blocks counted as small
+    std::uint64_t lrun = lpre + linc - ls;
+    if (tph == 0 && base + kTileBpt <= n) {
+      // every block of such a tile is listed: this thread's entries as whole 16-byte stores
+      // (scan, lscan and cscan are 16-byte aligned scratch, base a multiple of kTileBpt >= 4)
+      std::uint64_t sc[kTileBpt];
+      std::uint32_t cs[kTileBpt];
+  #pragma unroll
+      for (unsigned i = 0; i < kTileBpt; ++i) {
+        sc[i] = run;
+        cs[i] = cls_pair(lrun);
+        run += v[i];
+        lrun += pk[i];
       }
-      run += v[i];
-      lrun += pk[i];
+  #pragma unroll
+      for (unsigned i = 0; i < kTileBpt; i += 2)
+        *reinterpret_cast<ulonglong2*>(scan + base + i) = make_ulonglong2(sc[i], sc[i + 1]);
+  #pragma unroll
+      for (unsigned i = 0; i < kTileBpt; i += 4) {
+        *reinterpret_cast<uint4*>(lscan + base + i) = make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(cscan + base + i) = make_uint4(cs[i], cs[i + 1], cs[i + 2], cs[i + 3]);
+      }
+    } else {
+  #pragma unroll
+      for (unsigned i = 0; i < kTileBpt; ++i) {
+        if (base + i < n && !taken(pk[i])) {  // the scatter reads these for listed blocks only
+          const std::uint32_t t = taken(lrun);
+          scan[base + i] = run - t;  // (t <= the small count in run's low half: no borrow)
+          lscan[base + i] = t;
+          cscan[base + i] = cls_pair(lrun);
+        }
+        run += v[i];
+        lrun += pk[i];
+      }
     }
-  }
-  if (threadIdx.x == kTileThreads - 1) {
-    const std::uint32_t tl = taken(ltot);
-    tile_sums[blockIdx.x] = tot - tl;
-    tile_lanes[blockIdx.x] = tl;
-    const std::uint32_t tc = cls_pair(ltot);
-    tile_cls[blockIdx.x] = (tc & 0xFFFFu) | (static_cast<std::uint64_t>(tc >> 16) << 32);
+    if (threadIdx.x == kTileThreads - 1) {
+      const std::uint32_t tl = taken(ltot);
+      tile_sums[tile] = tot - tl;
+      tile_lanes[tile] = tl;
+      const std::uint32_t tc = cls_pair(ltot);
+      tile_cls[tile] = (tc & 0xFFFFu) | (static_cast<std::uint64_t>(tc >> 16) << 32);
+    }
+    __syncthreads();  // wsum, lsum and wok are rewritten by the next tile
   }
 }
 
@@ -794,30 +799,38 @@ __global__ void rows_finish(const std::uint8_t* base, const std::uint64_t* offse
                             std::uint32_t* out, std::uint64_t* ends, std::uint64_t* sinfo, std::uint32_t Ws,
                             const std::uint32_t* row0, const std::uint32_t* gate, std::uint32_t seq) {
   if (gate_closed(gate, seq)) return;
-  const std::uint64_t b = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
-  if (b >= n) return;
   const bool stream = dev::sload32(counts, 3) == kModeStream;  // rows_scan_tiles found every tile back to back
-  // (launched with 256 threads: a workgroup lies in one scan tile, so its flags are one scalar load)
-  const std::uint64_t t = b / kScanTile;
-  const std::uint32_t tk = stream ? 0u : dev::sload32(tile_ok, static_cast<std::uint32_t>(blockIdx.x / (kScanTile / 256u)));
-  if (tk & kTileAllTaken) return;  // every block of the tile is the lane or a group phase's: nothing to list
-  const std::uint32_t len = lengths[b];
-  if (stream) {
-    stream_block(base, offsets, lengths, n, b, offsets[b], len, Ws, row0, counts, ends, sinfo, o.wave_start);
-    return;
+  const std::uint32_t nchunks = static_cast<std::uint32_t>((static_cast<std::uint64_t>(n) + 255u) / 256u);
+  for (std::uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const std::uint64_t b = c * static_cast<std::uint64_t>(256) + threadIdx.x;
+    if (b >= n) continue;
+    // (256-block chunks: a chunk lies in one scan tile, so its flags are one scalar load)
+    const std::uint64_t t = b / kScanTile;
+    const std::uint32_t tk = stream ? 0u : dev::sload32(tile_ok, static_cast<std::uint32_t>(c / (kScanTile / 256u)));
+    if (tk & kTileAllTaken) continue;  // every block of the tile is the lane or a group phase's: nothing to list
+    const std::uint32_t len = lengths[b];
+    if (stream) {
+      stream_block(base, offsets, lengths, n, b, offsets[b], len, Ws, row0, counts, ends, sinfo, o.wave_start);
+      continue;
+    }
+    if (phase_block(len, tk)) continue;  // the lane or group phase's
+    const std::uint32_t cs = o.cscan[b];
+    const std::uint64_t cpre = o.tile_cls[t] + (cs & 0xFFFFu) + (static_cast<std::uint64_t>(cs >> 16) << 32);
+    finish_block(offsets[b], len, b, scan[b] + tile_offs[t], o.lscan[b] + o.tile_lanes[t], cpre,
+                 dev::sload32(counts, kCountSmall4), dev::sload32(counts, kCountSmall8), counts[2], o, W, out, tk);
   }
-  if (phase_block(len, tk)) return;  // the lane or group phase's
-  const std::uint32_t cs = o.cscan[b];
-  const std::uint64_t cpre = o.tile_cls[t] + (cs & 0xFFFFu) + (static_cast<std::uint64_t>(cs >> 16) << 32);
-  finish_block(offsets[b], len, b, scan[b] + tile_offs[t], o.lscan[b] + o.tile_lanes[t], cpre,
-               dev::sload32(counts, kCountSmall4), dev::sload32(counts, kCountSmall8), counts[2], o, W, out, tk);
 }
 
-// rows_finish with the scan of the tile sums folded in (ntiles <= kFusedTiles): every workgroup sums
+// rows_finish with the scan of the tile sums folded in (ntiles <= kFusedFinishTiles): every workgroup sums
 // the tile sums in front of its own tile and over all tiles itself (at most 4 loads per thread), so
 // no single-workgroup tile-scan launch sits between the tile scan and the scatter. Workgroup 0
 // publishes counts for the row kernel.
 constexpr std::uint32_t kFusedTiles = 1024;
+// The fused scatter re-reads every tile sum in each of its workgroups, so its cost grows with the
+// tile count: above kFusedFinishTiles tiles the one-workgroup scan (rows_scan_tiles) and the plain
+// scatter measured faster (one process, profiles/r5/scatter/: 300-1000 B gapped 3116 -> 3224-3334
+// GB/s, 180-400 B 2549 -> 2650, 257-512 B 2879 -> 3480; cfg4's 32 tiles keep the fused kernel).
+constexpr std::uint32_t kFusedFinishTiles = 128;
 // Batches of at most kFusedTiles tiles: every scatter workgroup sums the tile sums itself. (Letting
 // the tile scan's last workgroup scan them measured far slower in one process: 300-1000 B gapped
 // 3041 -> 1934 GB/s, cfg4 -2 %, profiles/r4/s14/, most likely from the device-scope fence each
@@ -827,6 +840,7 @@ constexpr std::uint32_t kFusedTiles = 1024;
 // latency, not the re-reads, is what the finish pays for.
 constexpr std::uint32_t kFinishPer = 1;
 constexpr std::uint32_t kFinishThreads = 256;
+constexpr std::uint32_t kFinishGroupsPerCu = 16;  // rows_finish
 // Stream mode (every tile qualified): instead of the small/large lists, every block
 // gets its end E[b] in bytes from row 0 (the stream start rounded down to 16 bytes), and every
 // row-kernel wave the first block ending in or after its first row; counts = {0, 0, rows, 1} and
@@ -1295,22 +1309,32 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
   const std::uint64_t ntiles = prepass_tiles(n);
   const std::uint64_t nfused = (static_cast<std::uint64_t>(n) + kFinishThreads * kFinishPer - 1) / (kFinishThreads * kFinishPer);
   const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
+  // at most kScanGroupsPerCu tile-scan workgroups per CU, each looping over tiles: against one
+  // workgroup per tile, gapped 36-byte WAL payloads 2567 -> 2625 GB/s, back-to-back 36 B 2933 -> 3018,
+  // the rest within noise (4 or 8 per CU measured the same or lower; profiles/r5/scatter/)
+  const std::uint64_t scap = std::uint64_t(ncu) * kScanGroupsPerCu;
+  const unsigned gscan = static_cast<unsigned>(ntiles < scap ? ntiles : scap);
   if (ntiles <= kFusedTiles)
-    hipLaunchKernelGGL(rows_tile_scan<1024>, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets,
+    hipLaunchKernelGGL(rows_tile_scan<1024>, dim3(gscan), dim3(1024), 0, st, base, offsets,
                        lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
                        group_stream, gate, seq, gate_flags);
   else
-    hipLaunchKernelGGL(rows_tile_scan<512>, dim3(static_cast<unsigned>(ntiles)), dim3(512), 0, st, base, offsets,
+    hipLaunchKernelGGL(rows_tile_scan<512>, dim3(gscan), dim3(512), 0, st, base, offsets,
                        lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
                        group_stream, gate, seq, gate_flags);
-  if (ntiles <= kFusedTiles) {
+  if (ntiles <= kFusedFinishTiles) {
     hipLaunchKernelGGL((rows_finish_fused<kFinishThreads, kFinishPer>), dim3(static_cast<unsigned>(nfused)), dim3(kFinishThreads), 0, st, base,
                        offsets, lengths, n, scan, tile_sums, tile_ok, static_cast<std::uint32_t>(ntiles), counts, o,
                        W, out, ends, sinfo, Ws, row0, gate, seq);
   } else {
     hipLaunchKernelGGL(rows_scan_tiles, dim3(1), dim3(1024), 0, st, tile_sums, o.tile_lanes, o.tile_cls,
                        static_cast<std::uint32_t>(ntiles), n, counts, tile_ok, base, offsets, lengths, sinfo, gate, seq);
-    hipLaunchKernelGGL(rows_finish, dim3(static_cast<unsigned>(nfinish)), dim3(256), 0, st, base, offsets, lengths,
+    // at most kFinishGroupsPerCu workgroups per CU, each looping over 256-block chunks: a batch whose
+    // gate stays closed (crc_list_lanes folded it) no longer dispatches one workgroup per 256 blocks
+    // (gapped 36-byte WAL payloads 2441 -> 2555 GB/s, back-to-back 36 B 2755 -> 2973;
+    // profiles/r5/scatter/)
+    const std::uint64_t gcap = std::uint64_t(ncu) * kFinishGroupsPerCu;
+    hipLaunchKernelGGL(rows_finish, dim3(static_cast<unsigned>(nfinish < gcap ? nfinish : gcap)), dim3(256), 0, st, base, offsets, lengths,
                        n, scan, tile_sums, counts, tile_ok, o, W, out, ends, sinfo, Ws, row0, gate, seq);
   }
   return hipGetLastError();
