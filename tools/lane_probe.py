@@ -115,6 +115,9 @@ def main():
     work.append(irregular("irregular 100-700 B, 8 B gaps", rng.integers(100, 701, ng), np.full(ng, 8), 8))
     ng = count(290, 298)  # 65-256 B ~40 %, 257-512 B ~60 %
     work.append(irregular("irregular 180-400 B, 8 B gaps", rng.integers(180, 401, ng), np.full(ng, 8), 8))
+    ng = count(300, 308)  # listed 257-384 B (the 8-lane pass needs 3968 of 4096 per tile)
+    lm = np.where(rng.random(ng) < 0.1, rng.integers(100, 201, ng), rng.integers(257, 385, ng))
+    work.append(irregular("irregular 257-384 B + 10 % 100-200 B, 8 B gaps", lm, np.full(ng, 8), 8))
     ng = count(545, 553)
     work.append(irregular("irregular 65-1024 B, 8 B gaps", rng.integers(65, 1025, ng), np.full(ng, 8), 8))
     n = count(2048, 2056)

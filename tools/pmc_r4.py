@@ -5,6 +5,7 @@ bound is read from (MI355X_MICROARCH.md: SQ_* cycle counters count quad-cycles, 
 the chip; FETCH_SIZE x 1024 x 2 = HBM bytes on gfx950).
 
     python tools/pmc_r4.py gpurun_out/r4_s2/lanepmc > profiles/r4/lanes_pmc/summary.txt
+    python tools/pmc_r4.py gpurun_out/r5_lanepmc r5   (round 5's workloads, tools/gpu_r5_lanepmc.sh)
 """
 import csv
 import os
@@ -16,6 +17,12 @@ from statistics import median
 WORK = {"w1": "uniform 26 B", "w2": "uniform 36 B", "w3": "uniform 59 B", "w4": "irregular WAL payloads 36 B (8-byte gaps)"}
 PAYLOAD = {"w1": (1 << 30) // 26 * 26, "w2": (1 << 30) // 36 * 36, "w3": (1 << 30) // 59 * 59,
            "w4": (1 << 30) // 44 * 36}
+LEN = {"w1": 26, "w2": 36, "w3": 59, "w4": 36}
+WORK5 = {"w1": "uniform 26 B", "w2": "uniform 36 B", "w3": "uniform 36 B at stride 44 from base + 8",
+         "w4": "irregular WAL payloads 36 B (8-byte gaps)"}
+PAYLOAD5 = {"w1": (1 << 30) // 26 * 26, "w2": (1 << 30) // 36 * 36, "w3": ((1 << 30) - 8) // 44 * 36,
+            "w4": (1 << 30) // 44 * 36}
+LEN5 = {"w1": 26, "w2": 36, "w3": 36, "w4": 36}
 
 
 def short(name):
@@ -54,7 +61,7 @@ def main(root):
                 pass
             n = PAYLOAD.get(w)
             if n and "SQ_INSTS_VALU" in med:
-                blocks = n / {"w1": 26, "w2": 36, "w3": 59, "w4": 36}[w]
+                blocks = n / LEN[w]
                 for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SMEM"):
                     if c in med:
                         print(f"    {c} per 64 blocks (one wave step) = {med[c] / (blocks / 64):.1f}")
@@ -65,4 +72,6 @@ def main(root):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[2] == "r5":
+        WORK, PAYLOAD, LEN = WORK5, PAYLOAD5, LEN5
     main(sys.argv[1])
