@@ -1129,22 +1129,6 @@ __device__ __forceinline__ std::uint32_t group_xor(std::uint32_t v) {
   return v;
 }
 
-// XOR over each G-lane group, valid in the group's last lane: group_xor for a power of two, else the
-// group's other G - 1 values pulled into the last lane (ds_bpermute; groups at lanes [G k, G k + G)).
-template <int G>
-__device__ __forceinline__ std::uint32_t group_sum_last(std::uint32_t v) {
-  if constexpr ((G & (G - 1)) == 0) {
-    return group_xor<G>(v);
-  } else {
-    const std::uint32_t lane = threadIdx.x & 63u;
-    std::uint32_t s = v;
-#pragma unroll
-    for (std::uint32_t k = 1; k < static_cast<std::uint32_t>(G); ++k)
-      s ^= static_cast<std::uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(((lane - k) & 63u) * 4u), static_cast<int>(v)));
-    return s;
-  }
-}
-
 // Batch rows (4 KiB each, 64/G blocks) are split over the waves in contiguous ranges, with the
 // packed kernel's pipeline and issue priority. Every block starts from init_default (per-block
 // initial registers take the generic kernel): raw = Shift_len(init) ^ crc_0(block), with
@@ -1902,7 +1886,7 @@ __device__ __forceinline__ void lane_phase(const RowsArgs& a, const std::uint32_
 template <int G, bool LIST>
 __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_t* lds, std::uint32_t lo,
                                            std::uint32_t cnt) {
-  static_assert(G == 4 || G == 8 || (LIST && (G == 16 || G == 6)), "4- or 8-lane groups (6 and 16 for listed blocks)");
+  static_assert(G == 4 || G == 8 || (LIST && G == 16), "4- or 8-lane groups (16 for listed blocks)");
   // 16-lane groups take their fifth granule from the next lane: +2.9 % on 513-1024-byte and +3.9 % on
   // 300-1000-byte payloads in one process; with 4- and 8-lane groups the shuffle cost more than the
   // loads it saved (-6.5 %, -4.5 %; profiles/r4/group_shuf/)
@@ -1920,7 +1904,6 @@ __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_
   const std::uint64_t b0 = first + wave * n / W, b1 = first + (wave + 1) * n / W;
   if (b0 >= b1) return;
   constexpr std::uint32_t kPer = 64u / G;  // blocks per step
-  const bool lane_in = grp < kPer;         // (6-lane groups: lanes 60-63 hold no block)
   const std::uint32_t ns = static_cast<std::uint32_t>((b1 - b0 + kPer - 1u) / kPer);
   const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
   const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
@@ -1946,7 +1929,7 @@ __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_
   auto issue = [&](int slot, std::uint32_t j) {
     const std::uint64_t b = b0 + kPer * static_cast<std::uint64_t>(j) + grp;
     const std::uint32_t len0 = d_len[slot];
-    const bool live = lane_in && j < ns && b < b1 && len0 <= kSlot && (LIST || (len0 > kLo && (a.l_tile[b / 4096u] & kFlag)));
+    const bool live = j < ns && b < b1 && len0 <= kSlot && (LIST || (len0 > kLo && (a.l_tile[b / 4096u] & kFlag)));
     const std::uint32_t len = live ? len0 : 0u;
     const std::uintptr_t blo = base + d_off[slot], bhi = blo + len;
     const std::int32_t c_lane = static_cast<std::int32_t>(len) - static_cast<std::int32_t>(kSlot) +
@@ -2006,18 +1989,16 @@ __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_
     if (a.init_raw) {
       // per-block registers (a rare path): loaded here rather than carried through the ring
       const std::uint32_t init = a.init_raw[live || LIST ? out_idx(slot, j) : b0];
-      constexpr std::uint32_t kBits = (32u + G - 1u) / G;
 #pragma unroll
-      for (std::uint32_t i = 0; i < kBits; ++i) {
-        const std::uint32_t bit = gl * kBits + i;
-        if (bit < 32u)
-          v ^= static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), bit, 1)) &
-               a.tabs->head_shift[L][bit];
+      for (std::uint32_t i = 0; i < 32u / G; ++i) {
+        const std::uint32_t bit = gl * (32u / G) + i;
+        v ^= static_cast<std::uint32_t>(__builtin_amdgcn_sbfe(static_cast<std::int32_t>(init), bit, 1)) &
+             a.tabs->head_shift[L][bit];
       }
     } else if (gl == 0u) {
       v ^= m_ishift[slot];
     }
-    v = group_sum_last<G>(v);  // the group's last lane holds the group's sum
+    v = group_xor<G>(v);  // every lane of the group holds the group's sum
     if (live && gl == G - 1u) a.out[out_idx(slot, j)] = v ^ a.out_xor;
   };
 
@@ -2052,11 +2033,7 @@ __device__ __forceinline__ void small_phase(const RowsArgs& a, const std::uint32
   const std::uint32_t ns = sload32(a.counts, 1), n4 = sload32(a.counts, kCountSmall4);
   const std::uint32_t n8 = sload32(a.counts, kCountSmall8);
   if (n4) group_walk<4, true>(a, lds, 0u, n4);
-#if TKV_PROBE_G6
-  if (n8) group_walk<6, true>(a, lds, n4, n8);  // probe: 6-lane groups for the 257-512 list (blocks <= 384 only)
-#else
   if (n8) group_walk<8, true>(a, lds, n4, n8);
-#endif
   if (ns - n4 - n8) group_walk<16, true>(a, lds, n4 + n8, ns - n4 - n8);
 }
 

@@ -526,12 +526,12 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     // mode reads (a lane-block batch never touches them).
     std::uint32_t len[kTileBpt];
     bool ok = true;
-  #pragma unroll
+#pragma unroll
     for (unsigned i = 0; i < kTileBpt; ++i) {
       const std::uint64_t b = base + i;
       len[i] = lengths[b < n ? b : n - 1];
     }
-  #pragma unroll
+#pragma unroll
     for (unsigned i = 0; i < kTileBpt; ++i) {
       const bool in = base + i < n;
       len[i] = in ? len[i] : 0u;
@@ -548,16 +548,16 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     }
     if (ok && base < n) {
       std::uint64_t o[kTileBpt + 1];
-  #pragma unroll
+#pragma unroll
       for (unsigned i = 0; i <= kTileBpt; ++i) o[i] = offsets[base + i < n ? base + i : n - 1];
-  #pragma unroll
+#pragma unroll
       for (unsigned i = 0; i < kTileBpt; ++i) ok = ok && (base + i + 1 >= n || o[i] + len[i] == o[i + 1]);
     }
     // Inclusive scans of the thread sums inside the wave (cross-lane shifts, no barriers), then the
     // wave totals through LDS: one barrier instead of the 20 of a workgroup-wide Hillis-Steele.
     std::uint64_t inc = s;
     std::uint64_t linc = ls;
-  #pragma unroll
+#pragma unroll
     for (unsigned off = 1; off < 64; off <<= 1) {
       const std::uint64_t y = __shfl_up(inc, off, 64);
       const std::uint64_t ly = __shfl_up(linc, off, 64);
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     __syncthreads();
     std::uint64_t wpre = 0, tot = 0, lpre = 0, ltot = 0;
     std::uint32_t all_ok = 1;
-  #pragma unroll
+#pragma unroll
     for (unsigned w = 0; w < kTileWaves; ++w) {
       const std::uint64_t t = wsum[w];
       const std::uint64_t lt = lsum[w];
@@ -623,23 +623,23 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
       // (scan, lscan and cscan are 16-byte aligned scratch, base a multiple of kTileBpt >= 4)
       std::uint64_t sc[kTileBpt];
       std::uint32_t cs[kTileBpt];
-  #pragma unroll
+#pragma unroll
       for (unsigned i = 0; i < kTileBpt; ++i) {
         sc[i] = run;
         cs[i] = cls_pair(lrun);
         run += v[i];
         lrun += pk[i];
       }
-  #pragma unroll
+#pragma unroll
       for (unsigned i = 0; i < kTileBpt; i += 2)
         *reinterpret_cast<ulonglong2*>(scan + base + i) = make_ulonglong2(sc[i], sc[i + 1]);
-  #pragma unroll
+#pragma unroll
       for (unsigned i = 0; i < kTileBpt; i += 4) {
         *reinterpret_cast<uint4*>(lscan + base + i) = make_uint4(0, 0, 0, 0);
         *reinterpret_cast<uint4*>(cscan + base + i) = make_uint4(cs[i], cs[i + 1], cs[i + 2], cs[i + 3]);
       }
     } else {
-  #pragma unroll
+#pragma unroll
       for (unsigned i = 0; i < kTileBpt; ++i) {
         if (base + i < n && !taken(pk[i])) {  // the scatter reads these for listed blocks only
           const std::uint32_t t = taken(lrun);

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 5, step 37: listed 257-384-byte blocks in 6-lane groups (prepass class, small-phase walk):
+# lanes/stream/fuzz tests, then the irregular probe against the build before (one process).
+set -u
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r5s37
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest tests/test_gpu_lanes.py tests/test_gpu_stream.py tests/test_gpu_fuzz.py tests/test_gpu_parity.py -m gpu -q --maxfail=10 --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest.log; grep -E "^FAILED|^ERROR" $O/pytest.log | head -20
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 500 python -u tools/lane_probe.py tools/ab/libtkv_base.so tinykvpp_amd/libtkv_crc32.so --rounds 4 --only "irregular" > $O/lane_probe.jsonl 2>&1
+echo "lane rc=$?"
+timeout -k 10 200 python -u tools/ab_multi.py tools/ab/libtkv_base.so tinykvpp_amd/libtkv_crc32.so --rounds 6 > $O/ab_multi.jsonl 2>&1
+echo "multi rc=$?"
+echo done
