@@ -509,8 +509,9 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
     const std::uint64_t TR = stream_geometry(sbase, offsets, lengths, n).rows;
     row0[w] = static_cast<std::uint32_t>(dev::stream_row0<kStreamSkew>(w, TR, Ws));
   }
-  const std::uint32_t ntiles = static_cast<std::uint32_t>((static_cast<std::uint64_t>(n) + kScanTile - 1) / kScanTile);
-  for (std::uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // one tile per workgroup (1024 threads), or tiles looped over by a bounded grid (512 threads, batches
+  // of more than kFusedTiles tiles): the loop costs the 1024-thread shape a spill (125 VGPRs)
+  auto tile_body = [&](const std::uint32_t tile) {
     const std::uint64_t base = static_cast<std::uint64_t>(tile) * kScanTile + threadIdx.x * kTileBpt;
     const unsigned lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
     // Every block first counts as a small or large one (v); lane blocks, the two group classes and the
@@ -658,7 +659,15 @@ __global__ __launch_bounds__(kTileThreads) void rows_tile_scan(const std::uint8_
       const std::uint32_t tc = cls_pair(ltot);
       tile_cls[tile] = (tc & 0xFFFFu) | (static_cast<std::uint64_t>(tc >> 16) << 32);
     }
-    __syncthreads();  // wsum, lsum and wok are rewritten by the next tile
+  };
+  if constexpr (kTileThreads == 512) {
+    const std::uint32_t ntiles = static_cast<std::uint32_t>((static_cast<std::uint64_t>(n) + kScanTile - 1) / kScanTile);
+    for (std::uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+      tile_body(tile);
+      __syncthreads();  // wsum, lsum and wok are rewritten by the next tile
+    }
+  } else {
+    tile_body(blockIdx.x);
   }
 }
 
@@ -1309,13 +1318,14 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
   const std::uint64_t ntiles = prepass_tiles(n);
   const std::uint64_t nfused = (static_cast<std::uint64_t>(n) + kFinishThreads * kFinishPer - 1) / (kFinishThreads * kFinishPer);
   const std::uint64_t nfinish = (static_cast<std::uint64_t>(n) + 255) / 256;
-  // at most kScanGroupsPerCu tile-scan workgroups per CU, each looping over tiles: against one
-  // workgroup per tile, gapped 36-byte WAL payloads 2567 -> 2625 GB/s, back-to-back 36 B 2933 -> 3018,
-  // the rest within noise (4 or 8 per CU measured the same or lower; profiles/r5/scatter/)
+  // batches of more than kFusedTiles tiles: at most kScanGroupsPerCu tile-scan workgroups per CU, each
+  // looping over tiles: against one workgroup per tile, gapped 36-byte WAL payloads 2567 -> 2625 GB/s,
+  // back-to-back 36 B 2933 -> 3018, the rest within noise (4 or 8 per CU measured the same or lower;
+  // profiles/r5/scatter/)
   const std::uint64_t scap = std::uint64_t(ncu) * kScanGroupsPerCu;
   const unsigned gscan = static_cast<unsigned>(ntiles < scap ? ntiles : scap);
   if (ntiles <= kFusedTiles)
-    hipLaunchKernelGGL(rows_tile_scan<1024>, dim3(gscan), dim3(1024), 0, st, base, offsets,
+    hipLaunchKernelGGL(rows_tile_scan<1024>, dim3(static_cast<unsigned>(ntiles)), dim3(1024), 0, st, base, offsets,
                        lengths, n, scan, tile_sums, tile_ok, row0, Ws, o.lscan, o.tile_lanes, o.cscan, o.tile_cls,
                        group_stream, gate, seq, gate_flags);
   else
