@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-5 evidence on the tree: the GPU suite, smoke(), the default bench line, kernel traces of cfg2
-# (one stream: the stats average is the per-launch duration), cfg4 and the device WAL verify, one
-# FETCH_SIZE pass each for cfg2-cfg5 and the WAL verify, SQ passes of the WAL sweep, and the probes.
-# Output: gpurun_out/r5final/.
+# Round-5 evidence on the tree, part 1: the GPU suite, smoke(), the default bench line, kernel traces of
+# cfg2 (one stream: the stats average is the per-launch duration), cfg4 and the device WAL verify, one
+# FETCH_SIZE pass each for cfg2-cfg5 and the WAL verify, SQ passes of the WAL sweep. Part 2 (the probes
+# against the round-4 library, lane PMC): tools/gpu_r5_final2.sh. Output: gpurun_out/r5final/.
 set -u
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r5final
@@ -15,14 +15,6 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('s
 rc=$?; echo "smoke rc=$rc"; tail -1 $O/smoke.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err
 rc=$?; echo "bench rc=$rc"; tail -c 400 $O/bench.json; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u tools/ab_wal.py tools/ab/libtkv_r4.so tinykvpp_amd/libtkv_crc32.so --rounds 4 > $O/ab_wal.jsonl 2>&1
-rc=$?; echo "ab_wal rc=$rc"; grep image $O/ab_wal.jsonl; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 240 python -u tools/wal_sweep_probe.py --reps 3 --image adv > $O/wal_adv.jsonl 2>&1
-rc=$?; echo "wal_adv rc=$rc"; tail -2 $O/wal_adv.jsonl; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python -u tools/lane_probe.py tinykvpp_amd/libtkv_crc32.so --rounds 3 --reps 5 > $O/lane_probe.jsonl 2>&1
-rc=$?; echo "lane_probe rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u tools/rec_probe.py tinykvpp_amd/libtkv_crc32.so --rounds 3 --reps 5 > $O/rec_probe.jsonl 2>&1
-rc=$?; echo "rec_probe rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp
 run() {  # name limit command...
   local name=$1 t=$2
