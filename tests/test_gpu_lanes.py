@@ -135,18 +135,23 @@ def test_irregular_one_pass_lanes(gpu, oracle, buf, shape):
     host, d = buf
     rng = np.random.default_rng(sum(map(ord, shape)))
     offs, lens = wal_payloads(rng, 1_100_003, tuple(range(0, 65)), 3)  # (>= 1 M blocks: the one-pass kernel runs)
+    # the kernel's 64-block steps that start no wave's range (a wave whose first step does not fit one
+    # window sends the whole batch to the general path): launch_list_lanes' partition restated
+    ts = (offs.size + 63) // 64
+    nw = min(torch.cuda.get_device_properties(0).multi_processor_count, (ts + 15) // 16) * 16
+    later = np.setdiff1d(np.arange(ts - 1), np.arange(nw, dtype=np.int64) * ts // nw)
     if shape == "shuffled":
         p = rng.permutation(offs.size)
         offs, lens = offs[p], lens[p]
-    elif shape == "late_shuffle":  # the first steps fit; later 64-block steps are out of order
-        p = np.arange(offs.size)
-        p[600_000:] = 600_000 + rng.permutation(offs.size - 600_000)
-        offs, lens = offs[p], lens[p]
+    elif shape == "late_shuffle":  # every wave's first step fits; a third of the later steps are out of order
+        for st in later[rng.random(later.size) < 0.33]:
+            p = st * 64 + rng.permutation(64)
+            offs[st * 64:st * 64 + 64], lens[st * 64:st * 64 + 64] = offs[p], lens[p]
     elif shape == "late_long":
         lens[-5] = 65
-    elif shape == "spread":  # every 97th step's blocks far apart
-        for s0 in range(640, offs.size - 64, 64 * 97):
-            offs[s0:s0 + 64] = rng.integers(0, host.size - 64, 64)
+    elif shape == "spread":  # every 97th later step's blocks far apart
+        for st in later[::97]:
+            offs[st * 64:st * 64 + 64] = rng.integers(0, host.size - 64, 64)
     elif shape == "tiny_batch":  # (below the one-pass kernel's threshold: the general path)
         offs, lens = offs[:37], lens[:37]
     elif shape == "zero_lengths":
@@ -162,6 +167,10 @@ def test_irregular_one_pass_lanes(gpu, oracle, buf, shape):
         assert np.array_equal(got[sample], oracle_c(oracle, host, offs[sample], lens[sample]))
         return
     got = u32(tk.crc32_batch(d, o, ln))
+    if shape in ("shuffled", "late_long", "late_shuffle", "spread", "zero_lengths"):
+        # which path ran: the one-pass kernel leaves the general path's phase word at 0; the general
+        # path publishes the lane phase for these lane-dense tiles (a first step out of order, a long block)
+        assert phases() == (1 if shape in ("shuffled", "late_long") else 0), shape
     want = oracle.batch(host, offs, lens)
     bad = np.flatnonzero(got != want)
     assert bad.size == 0, (shape, bad[:5])
