@@ -12,8 +12,11 @@ Prints one JSON line (rank 0). Extra fields: roofline (dominant kernel: algorith
 launch / HIP-event launch time vs 8 TB/s HBM peak), cpu_baseline (the reference's own crc32.cpp
 compiled from /root/reference into oracle/_ref, or the oracle port, on host cores over the same
 buffers; plus a slicing-by-8 row that is not the reference), bit_exact (this run's CRCs vs the
-oracle / golden aggregates), pipelined_two_streams (the same steps alternating two HIP streams, as a
-caller checksumming a stream of batches may run them; never `value`).
+oracle / golden aggregates), bit_exact_paths (post-timing parity of every other path: the one-pass
+lane kernel and its fall-through, CRC-32C, device/host WAL verify on small, Zipf and adversarial images
+clean and corrupted, the record check, WAL and SSTable stamps, the chained update),
+pipelined_two_streams (the same steps alternating two HIP streams, as a caller checksumming a stream of
+batches may run them; never `value`).
 """
 import argparse
 import ctypes
@@ -330,6 +333,156 @@ def host_legs(cfg_ctx, crcs):
     return legs
 
 
+def bit_exact_paths(dev, ora, quick=False):
+    """Post-timing parity checks of the paths the headline batch never reaches,
+    each against the oracle (oracle/liboracle.so: Sarwate CRC, the sequential WAL decode of
+    wal.cpp:63-130, the WAL stamp of wal.cpp:54-58, the SSTable stamp) on seeded synthetic inputs:
+      list_lanes_one_pass   >= 1 M gapped 26-59 B WAL payloads through tkv_crc32_batch_device (the
+                            one-pass crc_list_lanes kernel: the general path publishes no phase)
+      list_lanes_fall_through  the same batch with one 65 B block near its end (the general path)
+      crc32c_list_lanes     the one-pass batch under CRC-32C (sampled against the oracle)
+      wal_verify_device_*   tkv_wal_verify_device on small-record, Zipf and values-made-of-records
+                            images, clean and with one flipped payload byte: same (status, records
+                            decoded, stop offset) as the sequential decode
+      wal_verify_host       tkv_wal_verify (host image, copied to HBM), clean and corrupted
+      wal_check_records     tkv_wal_check_records_device (record starts known), clean and corrupted
+      wal_stamp             tkv_wal_stamp (group commit) byte-identical to the oracle's stamps
+      sst_stamp             tkv_sst_stamp_blocks vs oracle_sst_stamp; verify finds one flipped byte
+      update_chain          tkv_crc32_update_device chained over odd spans of a device buffer
+    Nothing here is inside a timed region. quick: smaller inputs (smoke())."""
+    import torch
+    import tinykvpp_amd as tk
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_images
+    wo = wal_images.load(os.path.join(ROOT, "oracle", "liboracle.so"))
+    lib = tk.load_library()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ora.oracle_crc_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p]
+    ora.oracle_update_c.restype = ctypes.c_uint32
+    ora.oracle_update_c.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+    ora.oracle_sst_stamp.restype = ctypes.c_uint32
+    ora.oracle_sst_stamp.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    ora.oracle_crc32.restype = ctypes.c_uint32
+    ora.oracle_crc32.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    res = {}
+    rng = np.random.default_rng(2026)
+
+    def u32(t):
+        return t.cpu().numpy().view(np.uint32)
+
+    # ---- irregular batches of WAL-payload-sized blocks -------------------------------------------
+    nb = 1_100_003  # (>= 1 M blocks: the one-pass kernel's threshold)
+    lens = rng.integers(26, 60, nb).astype(np.int64)
+    offs = 3 + 8 + np.concatenate([[0], np.cumsum(lens[:-1] + 8)])  # an 8-byte record prefix before each
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    for name, tweak in (("list_lanes_one_pass", None), ("list_lanes_fall_through", nb - 5)):
+        ln = lens.copy()
+        if tweak is not None:
+            ln[tweak] = 65
+        o, l32 = torch.from_numpy(offs).to(dev), torch.from_numpy(ln.astype(np.int32)).to(dev)
+        got = u32(tk.crc32_batch(d, o, l32))
+        ph = lib.tkv_debug_irregular_phases(st)
+        want = np.zeros(nb, np.uint32)
+        ora.oracle_crc_batch(host.ctypes.data, offs.astype(np.uint64).ctypes.data,
+                             ln.astype(np.uint32).ctypes.data, None, nb, want.ctypes.data)
+        path_ok = ph == (0 if tweak is None else 1)
+        res[name] = {"ok": bool(np.array_equal(got, want)) and path_ok, "blocks": nb, "mismatches":
+                     int((got != want).sum()), "general_path_phases": int(ph), "path_as_expected": path_ok}
+        if tweak is None:
+            gc = u32(tk.crc32_batch(d, o, l32, algo="crc32c"))
+            smp = rng.choice(nb, 4000 if quick else 20000, replace=False)
+            wc = np.array([ora.oracle_update_c(0xFFFFFFFF, host.ctypes.data + int(offs[i]), int(ln[i])) ^ 0xFFFFFFFF
+                           for i in smp], np.uint32)
+            res["crc32c_list_lanes"] = {"ok": bool(np.array_equal(gc[smp], wc)), "sampled": int(smp.size)}
+    del d
+
+    # ---- WAL recovery verify on the device ---------------------------------------------------------
+    sizes = {"small": 150_000 if quick else 1_500_000, "zipf": 10_000 if quick else 100_000,
+             "values_of_records": 6_000 if quick else 60_000}
+    U64 = ctypes.c_uint64
+    for shape, n in sizes.items():
+        img, roffs, rsize = wal_images.image(wo, shape, n, seed=len(shape))
+        want_clean = wal_images.decode(wo, img)
+        entry = {"records": n, "bytes": int(img.size), "oracle_clean": list(want_clean)}
+        ok = want_clean == ("ok", n, img.size)
+        dimg = torch.from_numpy(img).to(dev)
+        bad = n - 777
+        flip = int(roffs[bad] + rsize[bad] - 1)  # the record's last payload byte
+        for tag in ("clean", "corrupted"):
+            if tag == "corrupted":
+                img[flip] ^= 0x01
+                dimg[flip] ^= 0x01
+            want = wal_images.decode(wo, img)
+            if tag == "corrupted":
+                ok = ok and want == ("corrupted", bad, int(roffs[bad]))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            got = tk.wal.verify_device(dimg)
+            ms = (time.perf_counter() - t0) * 1e3
+            rounds = (U64 * 4)()
+            lib.tkv_debug_wal_last(rounds)
+            entry[tag] = {"device": list(got), "oracle": list(want), "ms": round(ms, 3), "device_rounds": rounds[0]}
+            ok = ok and tuple(got) == want
+            if shape == "small":  # the host-image entry point and the record check on the same image
+                hv = tk.wal.verify(img)
+                res.setdefault("wal_verify_host", {"ok": True})
+                res["wal_verify_host"][tag] = list(hv)
+                res["wal_verify_host"]["ok"] &= tuple(hv) == want
+                ro = torch.from_numpy(roffs.astype(np.int32)).to(dev)
+                fb, crc = tk.wal.check_records_device(dimg, ro)
+                fbv = int(fb.item())
+                stored = img[(roffs + 4)[:, None].astype(np.int64) + np.arange(4)].copy().view("<u4").ravel()
+                want_fb = bad if tag == "corrupted" else n
+                crc_ok = bool(np.array_equal(np.delete(u32(crc), bad), np.delete(stored, bad)))
+                res.setdefault("wal_check_records", {"ok": True})
+                res["wal_check_records"][tag] = {"first_bad": fbv, "want": want_fb}
+                res["wal_check_records"]["ok"] &= fbv == want_fb and crc_ok
+        entry["ok"] = bool(ok)
+        res[f"wal_verify_device_{shape}"] = entry
+        if shape == "small":  # group-commit stamp of the same records, against the oracle's bytes
+            img[flip] ^= 0x01
+            m = min(n, 200_000)
+            end = int(roffs[m - 1] + rsize[m - 1])
+            un = img[:end].copy()
+            for b in range(4, 8):
+                un[roffs[:m].astype(np.int64) + b] = 0
+            check_rc = lib.tkv_wal_stamp(ctypes.c_void_p(un.ctypes.data), ctypes.c_void_p(roffs.ctypes.data),
+                                         ctypes.c_void_p(rsize[:m].astype(np.uint32).ctypes.data), ctypes.c_uint64(m))
+            res["wal_stamp"] = {"ok": check_rc == 0 and bool(np.array_equal(un, img[:end])), "records": m}
+        del dimg, img
+
+    # ---- SSTable data-block stamps ------------------------------------------------------------------
+    nimg = 2000
+    isz = rng.integers(22, 9000, nimg).astype(np.uint64)
+    ioff = np.concatenate([[0], np.cumsum(isz[:-1])]).astype(np.uint64)
+    f = rng.integers(0, 256, int(isz.sum()), dtype=np.uint8)
+    tk.sst.stamp_blocks(f, ioff, isz)
+    stamped = f[(ioff + 17)[:, None].astype(np.int64) + np.arange(4)].copy().view("<u4").ravel()
+    want = np.array([ora.oracle_sst_stamp(f.ctypes.data + int(o), int(s)) for o, s in zip(ioff, isz)], np.uint32)
+    v_ok = tk.sst.verify_blocks(f, ioff, isz) == ("ok", 0, nimg)
+    f[int(ioff[1234] + isz[1234] // 2)] ^= 0x10
+    v_bad = tk.sst.verify_blocks(f, ioff, isz)
+    res["sst_stamp"] = {"ok": bool(np.array_equal(stamped, want)) and v_ok and v_bad == ("corrupted", 1, 1234),
+                        "images": nimg, "verify_corrupted": list(v_bad)}
+
+    # ---- the drop-in update, chained over device spans ---------------------------------------------
+    buf = rng.integers(0, 256, 5_000_003, dtype=np.uint8)
+    dbuf = torch.from_numpy(buf).to(dev)
+    cuts = np.sort(rng.choice(buf.size, 9, replace=False))
+    c = tk.crc32()
+    prev = 0
+    for cut in list(cuts) + [buf.size]:
+        c.update(dbuf[prev:cut])
+        prev = int(cut)
+    res["update_chain"] = {"ok": c.finalize() == ora.oracle_crc32(buf.ctypes.data, buf.size), "spans": int(cuts.size + 1)}
+    torch.cuda.synchronize()
+    for k in res:
+        res[k]["ok"] = bool(res[k]["ok"])
+    res["all_ok"] = all(v["ok"] for v in res.values())
+    return res
+
+
 def build_identity():
     """The build id baked into the loaded library against the hash of this tree's sources."""
     from tinykvpp_amd import build_id
@@ -355,6 +508,8 @@ def main():
     ap.add_argument("--no-pipelined", action="store_true", help="skip the two-stream pipelined rate (extra field)")
     ap.add_argument("--no-more-configs", action="store_true",
                     help="cfg2: skip timing cfg3, cfg4 and cfg5 (N=1) or cfg5 (N>1) in the same run (more_configs)")
+    ap.add_argument("--no-paths", action="store_true",
+                    help="skip the post-timing parity checks of the other paths (bit_exact_paths)")
     ap.add_argument("--traffic-csv", default=None,
                     help="rocprofv3 --pmc counter_collection.csv (FETCH_SIZE) of this command, for roofline.traffic")
     args = ap.parse_args()
@@ -521,6 +676,17 @@ def main():
             del c, o
             torch.cuda.empty_cache()
         line["more_configs"] = more
+    if not args.no_paths:
+        # after every timed region: parity of the paths the timed batches never reach (every rank checks
+        # on its own GPU; the line carries rank 0's details and the AND over ranks)
+        torch.cuda.empty_cache()
+        paths = bit_exact_paths(dev, ora)
+        if use_dist:
+            ok = torch.tensor([1 if paths["all_ok"] else 0], dtype=torch.int32,
+                              device=dev if backend == "nccl" else None)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            paths["all_ranks_ok"] = bool(ok.item())
+        line["bit_exact_paths"] = paths
     if rank == 0:
         print(json.dumps(line), flush=True)
     if use_dist:

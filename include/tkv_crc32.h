@@ -82,7 +82,7 @@ int tkv_crc32c_update_host(uint32_t raw_state, const void *data, size_t len, uin
  * span recomputed on the host (the slicing-by-8 code of tkv_crc32_update_host), so crc32::update
  * keeps the reference's never-fail contract (crc32.cpp:9-16) for spans of any size on a node without
  * a usable GPU. Prints one warning per process on stderr (with gpu_status and tkv_last_error()) and
- * counts the call in tkv_debug_update_counts slot 2. Fails only on null pointers. */
+ * counts the call in tkv_debug_update_counts_n out[2]. Fails only on null pointers. */
 int tkv_crc32_update_fallback(int gpu_status, uint32_t raw_state, const void *data, size_t len, uint32_t *out_raw);
 int tkv_crc32c_update_fallback(int gpu_status, uint32_t raw_state, const void *data, size_t len,
                                uint32_t *out_raw);
@@ -150,7 +150,7 @@ int tkv_wal_verify_device(const uint8_t *d_wal, uint64_t size, uint64_t *n_good,
  * check, n when every record passes. d_crc (nullable, device): the computed finalized CRC of every
  * payload (0 for a record whose length check failed). max_payload is a dispatch hint (the longest
  * record_len the caller expects: one lane reads each record in a window of 4-8 16-byte granules sized
- * for it, 36-byte payloads in 4, up to 102 bytes in 8); longer payloads are still checked exactly,
+ * for it, 36-byte payloads in 4, up to 100 bytes in 8); longer payloads are still checked exactly,
  * 64 bytes at a time. Asynchronous on `stream`. */
 int tkv_wal_check_records_device(const uint8_t *d_img, uint64_t size, const uint32_t *d_rec_off, uint64_t n,
                                  uint32_t max_payload, uint32_t *d_crc, uint64_t *d_first_bad, void *stream);

@@ -167,6 +167,54 @@ uint32_t oracle_sst_stamp(const uint8_t *img, size_t size) {
   return raw ^ ORACLE_INIT;
 }
 
+/* ---- WAL records (wal.cpp:19-130; layout wal.hpp:21-27) ----
+ * Record = u32 record_len | u32 crc32 | u8 op | u64 seq | u8 tombstone | u32 key_len | u32 value_len |
+ * key | value, little-endian and packed (26-byte header); record_len = size - 8; the CRC covers
+ * [8, 8 + record_len). */
+#define ORACLE_WAL_META 26u /* wal.hpp kMetadataSize */
+
+static uint32_t rd_le32(const uint8_t *p) {
+  return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+/* wal.cpp:54-58 (wal_entry::encode's stamp): for each record at offs[i], crc32 of its record_len bytes
+ * after the 8-byte prefix, stored little-endian at offs[i] + 4. */
+void oracle_wal_stamp(uint8_t *img, const uint64_t *offs, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) {
+    uint8_t *r = img + offs[i];
+    uint32_t c = oracle_crc32(r + 8, rd_le32(r));
+    r[4] = (uint8_t)c;
+    r[5] = (uint8_t)(c >> 8);
+    r[6] = (uint8_t)(c >> 16);
+    r[7] = (uint8_t)(c >> 24);
+  }
+}
+
+/* engine::create's recovery loop (engine.cpp:31-53) over a slurped image (wal.cpp:204-240): decode
+ * (wal.cpp:63-130) record after record until eof or the first failure. Checks in the reference's
+ * order: eof on an empty view (:64-66); corrupted when fewer than 26 bytes remain (:68-70), when
+ * record_len + 8 exceeds the view (:80-84; computed in 64 bits here, where the reference's u32 sum can
+ * wrap into undefined behaviour), on a CRC mismatch (:86-93) and when key_len + value_len overrun the
+ * record (:115-119). Returns 0 at a clean eof, 1 when corrupted; *n_good = records decoded, *stop =
+ * the offset the view is parked on (the failing record's start, or size). */
+int oracle_wal_decode(const uint8_t *img, uint64_t size, uint64_t *n_good, uint64_t *stop) {
+  uint64_t p = 0, n = 0;
+  int bad = 0;
+  while (p < size) {
+    if (size - p < ORACLE_WAL_META) { bad = 1; break; }
+    const uint64_t rl = rd_le32(img + p);
+    if (rl + 8u > size - p) { bad = 1; break; }
+    if (oracle_crc32(img + p + 8, (size_t)rl) != rd_le32(img + p + 4)) { bad = 1; break; }
+    const uint64_t kl = rd_le32(img + p + 18), vl = rd_le32(img + p + 22);
+    if (ORACLE_WAL_META + kl + vl > 8u + rl) { bad = 1; break; }
+    p += 8u + rl;
+    ++n;
+  }
+  *n_good = n;
+  *stop = p;
+  return bad;
+}
+
 /* ---- Slicing-by-8 (NOT the reference algorithm; CPU comparison row only) ----
  * SURVEY.md §8d's optional "slicing-by-8 CPU row, clearly labelled 'not reference'": the same
  * CRC-32/ISO-HDLC eight bytes per step with tables T_k[i] = Shift_k o T (Intel's slicing-by-8).

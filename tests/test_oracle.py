@@ -5,13 +5,15 @@ prefixes of a synthetic block, and the SURVEY §8c/§8d synthetic-batch goldens 
 reference's compiled crc32.cpp (tests/golden/make_golden.py) and cross-checked with zlib.
 """
 import ctypes
+import os
 import struct
+import sys
 import zlib
 
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import ROOT, golden
 
 
 def test_table_matches_reference_generator(oracle):
@@ -240,3 +242,85 @@ def test_reference_wal_loops(ref_lib):
     buf = ctypes.create_string_buffer(bytes(zeroed), len(zeroed))
     ref_lib.ref_wal_stamp(buf, offs.ctypes.data, sizes.ctypes.data, len(recs))
     assert buf.raw[:len(img)] == bytes(img)
+
+
+def _wal_oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_images
+    return wal_images, wal_images.load()
+
+
+def _py_decode(img):
+    """wal.cpp:63-130 applied record after record, in Python (the tests' sequential decode)."""
+    import zlib
+    u32 = lambda p: int.from_bytes(bytes(img[p:p + 4]), "little")  # noqa: E731
+    p, n, size = 0, 0, len(img)
+    while p < size:
+        if size - p < 26 or u32(p) + 8 > size - p:
+            return "corrupted", n, p
+        rl = u32(p)
+        if zlib.crc32(bytes(img[p + 8:p + 8 + rl])) != u32(p + 4) or 26 + u32(p + 18) + u32(p + 22) > 8 + rl:
+            return "corrupted", n, p
+        p += 8 + rl
+        n += 1
+    return "ok", n, p
+
+
+def test_oracle_wal_decode_golden():
+    """oracle_wal_decode / oracle_wal_stamp (the checker bench.py's bit_exact_paths and smoke() use)
+    on the reference's golden records (tests/golden/wal.json, written from the compiled reference):
+    clean, a flipped CRC-covered byte, a torn tail, a key_len past the record, restamping."""
+    wi, wo = _wal_oracle()
+    recs = [bytes.fromhex(r["hex"]) for r in golden("wal.json")["records"]]
+    img = np.frombuffer(b"".join(recs), np.uint8).copy()
+    starts = np.cumsum([0] + [len(r) for r in recs]).astype(np.uint64)
+    assert wi.decode(wo, img) == ("ok", len(recs), img.size)
+    bad = img.copy()
+    bad[int(starts[3]) + 20] ^= 0x40
+    assert wi.decode(wo, bad) == ("corrupted", 3, int(starts[3]))
+    assert wi.decode(wo, img, img.size - 1) == ("corrupted", len(recs) - 1, int(starts[-2]))
+    assert wi.decode(wo, img, 0) == ("ok", 0, 0)
+    un = img.copy()
+    for s in starts[:-1]:
+        un[int(s) + 4:int(s) + 8] = 0
+    wo.oracle_wal_stamp(un.ctypes.data, starts[:-1].copy().ctypes.data, len(recs))
+    assert np.array_equal(un, img)
+    # key_len + value_len past the record (restamped so only the bounds check fails, wal.cpp:115-119)
+    kv = img.copy()
+    kv[int(starts[2]) + 18:int(starts[2]) + 22] = np.frombuffer((10 ** 6).to_bytes(4, "little"), np.uint8)
+    wo.oracle_wal_stamp(kv.ctypes.data, starts[2:3].copy().ctypes.data, 1)
+    assert wi.decode(wo, kv) == ("corrupted", 2, int(starts[2])) == _py_decode(kv)
+
+
+@pytest.mark.parametrize("shape", ["small", "zipf", "values_of_records"])
+def test_oracle_wal_images(shape):
+    """The synthetic images (oracle/wal_images.py) decode clean; one flipped payload byte, a lying
+    record_len and a truncation stop where the Python decode (zlib CRC) stops."""
+    wi, wo = _wal_oracle()
+    img, offs, size = wi.image(wo, shape, 3000, seed=7)
+    assert wi.decode(wo, img) == ("ok", 3000, img.size) == _py_decode(img)
+    for victim in (0, 1500, 2999):
+        b = img.copy()
+        b[int(offs[victim] + size[victim] - 1)] ^= 1
+        assert wi.decode(wo, b) == ("corrupted", victim, int(offs[victim])) == _py_decode(b)
+        b = img.copy()
+        b[int(offs[victim]):int(offs[victim]) + 4] = np.frombuffer((int(size[victim]) - 8 + 3).to_bytes(4, "little"),
+                                                                   np.uint8)
+        assert wi.decode(wo, b) == _py_decode(b)
+    assert wi.decode(wo, img, img.size - 3) == _py_decode(img[:-3])
+
+
+def test_oracle_wal_decode_matches_reference(ref_lib):
+    """oracle_wal_decode against oracle/_ref's ref_wal_verify (the reference's own crc32.cpp) on the
+    synthetic images, clean and corrupted."""
+    wi, wo = _wal_oracle()
+    ref_lib.ref_wal_verify.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    for shape in ("small", "zipf", "values_of_records"):
+        img, offs, size = wi.image(wo, shape, 20000, seed=11)
+        for flip in (None, int(offs[12345]) + 30):
+            b = img.copy()
+            if flip is not None:
+                b[flip] ^= 0x20
+            good, stop = ctypes.c_uint64(), ctypes.c_uint64()
+            rc = ref_lib.ref_wal_verify(b.ctypes.data, b.size, ctypes.byref(good), ctypes.byref(stop))
+            assert wi.decode(wo, b) == ("corrupted" if rc else "ok", good.value, stop.value)
