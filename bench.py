@@ -384,8 +384,8 @@ def bit_exact_paths(dev, ora, quick=False):
         got = u32(tk.crc32_batch(d, o, l32))
         ph = lib.tkv_debug_irregular_phases(st)
         want = np.zeros(nb, np.uint32)
-        ora.oracle_crc_batch(host.ctypes.data, offs.astype(np.uint64).ctypes.data,
-                             ln.astype(np.uint32).ctypes.data, None, nb, want.ctypes.data)
+        o64, l32h = offs.astype(np.uint64), ln.astype(np.uint32)  # (named: alive across the call)
+        ora.oracle_crc_batch(host.ctypes.data, o64.ctypes.data, l32h.ctypes.data, None, nb, want.ctypes.data)
         path_ok = ph == (0 if tweak is None else 1)
         res[name] = {"ok": bool(np.array_equal(got, want)) and path_ok, "blocks": nb, "mismatches":
                      int((got != want).sum()), "general_path_phases": int(ph), "path_as_expected": path_ok}
@@ -447,8 +447,9 @@ def bit_exact_paths(dev, ora, quick=False):
             un = img[:end].copy()
             for b in range(4, 8):
                 un[roffs[:m].astype(np.int64) + b] = 0
+            sz32 = rsize[:m].astype(np.uint32)
             check_rc = lib.tkv_wal_stamp(ctypes.c_void_p(un.ctypes.data), ctypes.c_void_p(roffs.ctypes.data),
-                                         ctypes.c_void_p(rsize[:m].astype(np.uint32).ctypes.data), ctypes.c_uint64(m))
+                                         ctypes.c_void_p(sz32.ctypes.data), ctypes.c_uint64(m))
             res["wal_stamp"] = {"ok": check_rc == 0 and bool(np.array_equal(un, img[:end])), "records": m}
         del dimg, img
 

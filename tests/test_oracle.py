@@ -283,12 +283,14 @@ def test_oracle_wal_decode_golden():
     un = img.copy()
     for s in starts[:-1]:
         un[int(s) + 4:int(s) + 8] = 0
-    wo.oracle_wal_stamp(un.ctypes.data, starts[:-1].copy().ctypes.data, len(recs))
+    st0 = starts[:-1].copy()
+    wo.oracle_wal_stamp(un.ctypes.data, st0.ctypes.data, len(recs))
     assert np.array_equal(un, img)
     # key_len + value_len past the record (restamped so only the bounds check fails, wal.cpp:115-119)
     kv = img.copy()
     kv[int(starts[2]) + 18:int(starts[2]) + 22] = np.frombuffer((10 ** 6).to_bytes(4, "little"), np.uint8)
-    wo.oracle_wal_stamp(kv.ctypes.data, starts[2:3].copy().ctypes.data, 1)
+    st2 = starts[2:3].copy()
+    wo.oracle_wal_stamp(kv.ctypes.data, st2.ctypes.data, 1)
     assert wi.decode(wo, kv) == ("corrupted", 2, int(starts[2])) == _py_decode(kv)
 
 
