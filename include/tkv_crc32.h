@@ -274,9 +274,10 @@ size_t tkv_debug_update_counts_n(uint64_t *out, size_t n);
  * host-thread walk (only a host image the device cannot hold), out[2] = 1 when a host image was
  * copied to the device, out[3] = 1 when the sweep needed no fix-up (0 when no device round ran). */
 void tkv_debug_wal_last(uint64_t out[4]);
-/* Per fix-up round of the calling thread's last device WAL verify, four words each: failing chunk
- * boundaries found, fix-up tasks launched, the longest task's regions, all tasks' regions. Writes up
- * to n words; returns the number available (0 when the sweep needed no fix-up). */
+/* Per fix-up round of the calling thread's last device WAL verify, six words each: failing chunk
+ * boundaries found, fix-up tasks launched, the longest task's range and all tasks' ranges (regions a
+ * task may walk), the most regions one task walked and all regions walked. Writes up to n words;
+ * returns the number available (0 when the sweep needed no fix-up). */
 size_t tkv_debug_wal_rounds(uint64_t *out, size_t n);
 /* Which path the last irregular batch on `stream` took: 1 = byte-stream row walk (blocks back to
  * back, each at least 64 bytes), 0 = general row walk; -1 on error. Synchronizes

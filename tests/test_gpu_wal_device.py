@@ -90,6 +90,15 @@ def wal_last():
     return {"passes": out[0], "host_walk": out[1], "copied": out[2], "fast": out[3]}
 
 
+def wal_rounds():
+    """Per fix-up round of this thread's last verify (tkv_debug_wal_rounds): failing boundaries, tasks,
+    the longest task's range, all ranges, the most regions a task walked, all regions walked."""
+    out = np.zeros(6 * 256, np.uint64)
+    k = tk.load_library().tkv_debug_wal_rounds(ctypes.c_void_p(out.ctypes.data), out.size)
+    keys = ("failing", "tasks", "longest", "regions", "walk_max", "walked")
+    return [dict(zip(keys, map(int, out[i:i + 6]))) for i in range(0, min(k, out.size), 6)]
+
+
 LAST = {}
 
 
@@ -218,8 +227,13 @@ def test_values_made_of_records(gpu, oracle):
     want = sequential_decode(oracle, img, n)
     assert want == ("ok", offs.size, n)
     assert both(img, n) == (want, want)
-    print("values made of records:", LAST)
+    rounds = wal_rounds()
+    print("values made of records:", LAST, rounds)
     device_walk_only(max_passes=10 ** 6)
+    # bounded recovery: a fake chain that breaks where its value ends is walked again
+    # from the next plausible header, so chunk entries settle within a few regions: a handful of fix-up
+    # rounds, no fix-up task walks thousands of regions in sequence
+    assert len(rounds) <= 4 and max(r["walk_max"] for r in rounds) <= 64, rounds
     o = int(offs[59000]) + 30
     img[o] ^= 0x40
     want = sequential_decode(oracle, img, n)
@@ -227,7 +241,7 @@ def test_values_made_of_records(gpu, oracle):
     device_walk_only(max_passes=10 ** 6)
 
 
-@pytest.mark.parametrize("plen", [0, 1, 17, 18, 239, 240, 241, 3000])
+@pytest.mark.parametrize("plen", [0, 1, 17, 18, 239, 240, 241, 3000, 7168, 7200, 20000, 65536, 65537, 100000])
 def test_payload_length_classes(gpu, oracle, plen):
     """Records whose payloads sit at the lane-fold limit (240 bytes) and past it (the long-payload
     batch), next to tiny corrupt ones (record_len < 18: key and value cannot fit)."""
@@ -264,3 +278,80 @@ def test_payload_length_classes(gpu, oracle, plen):
         assert both(image, m) == (want, want)
     else:
         assert want[:2] == ("corrupted", 1500)
+
+
+REGION = 7168  # the sweep's region (tkv_wal_device.hip kRegion)
+
+
+def record(rng, plen, klen=4):
+    """One unstamped record with a payload of plen >= 18 bytes (wal.cpp:19-61 layout)."""
+    vlen = plen - 18 - klen
+    body = bytearray(rng.integers(0, 256, 26 + klen + vlen, dtype=np.uint8).tobytes())
+    body[0:4] = plen.to_bytes(4, "little")
+    body[4:8] = b"\0\0\0\0"
+    body[8] = 0
+    body[17] = 0
+    body[18:22] = klen.to_bytes(4, "little")
+    body[22:26] = vlen.to_bytes(4, "little")
+    return bytes(body)
+
+
+def region_end_records(rng):
+    """Records (unstamped) placed so that long payloads sit at region ends: (records, [(index, start,
+    payload length)] of the placed ones)."""
+    lens = [241, 500, 4000, REGION - 8, REGION, REGION + 1, 15000, 30000, 65536]
+    recs, pos, targets = [], 0, []
+    for i, d in enumerate(list(range(0, 12)) + [26, 27, 100, 3000]):
+        t = REGION * (4 + 12 * i) - d
+        while t - pos > 3000:
+            r = record(rng, int(rng.integers(22, 2000)))
+            recs.append(r)
+            pos += len(r)
+        if t - pos < 30:
+            t += REGION
+            while t - pos > 3000:
+                r = record(rng, int(rng.integers(22, 2000)))
+                recs.append(r)
+                pos += len(r)
+        filler = record(rng, t - pos - 8)
+        recs.append(filler)
+        pos += len(filler)
+        assert pos == t
+        L = lens[i % len(lens)]
+        if i % 3 == 2:  # the payload ends exactly on a region end
+            L = (-(t + 8)) % REGION + REGION * (i % 4)
+            L = max(L, 241) if L <= 65536 else 60000
+        r = record(rng, L)
+        targets.append((len(recs), pos, L))
+        recs.append(r)
+        pos += len(r)
+    recs.append(record(rng, 100))
+    return recs, targets
+
+
+def test_long_payloads_at_region_ends(gpu, oracle):
+    """Payloads of kLaneFold < record_len <= kMedMax are folded in the sweep's one read of the image:
+    whole in a region, or carried across region ends (the register after the head, crc0 carries of the
+    regions after, combined in wal_fin_*). Records placed so that their 8-byte prefix is cut by a region
+    end (d = 1..8 bytes before it), their payload starts or ends exactly on one, and they span 1-10
+    regions; clean, then each of a sample corrupted (first byte, last byte, a byte on a region end)."""
+    rng = np.random.default_rng(77)
+    recs, targets = region_end_records(rng)
+    img = np.frombuffer(b"".join(recs), np.uint8).copy()
+    offs = np.concatenate([[0], np.cumsum([len(r) for r in recs])[:-1]]).astype(np.uint64)
+    sz = np.array([len(r) for r in recs], np.uint32)
+    tk.check(tk.load_library().tkv_wal_stamp(ctypes.c_void_p(img.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                                             ctypes.c_void_p(sz.ctypes.data), offs.size))
+    n = img.size
+    want = sequential_decode(oracle, img, n)
+    assert want == ("ok", len(recs), n)
+    assert both(img, n) == (want, want)
+    device_walk_only(max_passes=8)
+    for idx, t, L in targets[::2]:
+        a = t + 8
+        for o in (a, a + L - 1, (a // REGION + 1) * REGION if (a // REGION + 1) * REGION < a + L else a + 1):
+            img[o] ^= 0x10
+            want = sequential_decode(oracle, img, n)
+            assert want == ("corrupted", idx, t), (idx, t, L, o)
+            assert both(img, n) == (want, want), (idx, t, L, o)
+            img[o] ^= 0x10

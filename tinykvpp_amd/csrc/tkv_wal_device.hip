@@ -59,8 +59,14 @@ constexpr std::uint32_t kPiece = kRegion / 64;  // bytes per lane piece
 constexpr std::uint32_t kOver = 256;            // bytes of the next region behind the window
 constexpr std::uint32_t kLaneFold = 240;        // payloads up to this long are folded by one lane from LDS
 constexpr std::uint32_t kWin = 16 + kRegion + kOver;  // window: the region's aligned start, region, overlap
-constexpr std::uint32_t kList = kRegion / 26 + 4;  // listed records per region (see the list step)
+// listed records per region (see the list step), and behind them the region's fold ranges (12 bytes
+// each: the carry range always fits behind the most records a region can hold)
+constexpr std::uint32_t kList = kRegion / 26 + 16;
 constexpr std::uint32_t kWinBytes = (kWin + 2 * kList + 15) & ~15u;
+constexpr std::uint32_t kMedMax = 65536;  // payloads longer than kLaneFold and up to this: folded in the sweep
+constexpr std::uint32_t kChunk = 112;     // bytes per lane of a range fold
+static_assert(kRegion <= 64 * kChunk && kChunk <= kLaneFold, "a whole region is one round of chunks");
+static_assert(2 * kList >= 2 * ((kRegion / 26 + 2) & ~1u) + 12, "the carry range fits behind a full list");
 constexpr std::uint32_t kStore = kPiece / 26 + 2;  // starts a lane lists: its records up to the first tiny one
 constexpr std::uint32_t kSearchStep = 48;       // positions a lane tests per search step
 constexpr unsigned kSweepWaves = 12;            // waves per workgroup: the 64 KiB tables + 12 windows of LDS
@@ -69,8 +75,9 @@ constexpr unsigned kHres = 16;                  // words of the pinned result bl
 static_assert(kRegion % 1024 == 0 && kPiece % 16 == 0, "region = whole 1 KiB load rows");
 static_assert(kOver >= kLaneFold + 8 && kOver >= kWalMeta, "a lane-folded record ends inside the window");
 static_assert(kList * 26 >= kRegion + 26 * 2, "records of >= 26 bytes fit the list");
-static_assert(kLdsSliceWords * 2 + kSweepWaves * kWinBytes + 4 * (kLaneFold + 1) <= 163840, "LDS");
+static_assert(kLdsSliceWords * 2 + kSweepWaves * kWinBytes + 4 * (kLaneFold + 1) + 4 * 64 <= 163840, "LDS");
 static_assert(kStore <= 8, "list counts per lane < 16");
+static_assert(kList <= 512, "list indices fit 9 bits (range words, long-payload metadata)");
 
 // Region flags (low byte of fl[]; the region's version, bumped by every fix-up rewrite, above it).
 constexpr std::uint32_t kChain = 1;   // the region has chain state: E (entry, may lie past the region) and X
@@ -79,10 +86,16 @@ constexpr std::uint32_t kSearch = 4;  // no chain: the walk searched the region 
 constexpr std::uint32_t kBroke = 8;   // the chain broke in the region, at X (wal.cpp:68-70, 80-87)
 constexpr std::uint32_t kEnd = 16;    // the chain reached the end of the image exactly (X == size)
 constexpr std::uint32_t kFix = 32;    // its entry came from a fix-up task (checked like kSpec)
+constexpr std::uint32_t kGiantHop = 64;  // the chain leaves it in a record longer than kMedMax (passed over)
+// kinds of fold range: the bytes in front of the region's entry (part of the record the chain is in
+// when it enters; crc0), a payload wholly inside the region (initial register injected, checked here),
+// the head of a payload that goes on past the region (initial register injected; finished by wal_fin_*)
+constexpr std::uint32_t kRangeCarry = 0, kRangeWhole = 1, kRangeHead = 2;
 
 // Result words (device, u64): see wal_fin_*.
-enum : int { kResLongA = 0, kResIncons, kResFirst, kResP, kResQ, kResLidx, kResCnt, kResLongSeg, kResWords = 8 };
-static_assert(kResLongSeg < kResWords, "result words");
+enum : int { kResLongA = 0, kResIncons, kResFirst, kResP, kResQ, kResLidx, kResCnt, kResLongSeg, kResWalkMax,
+             kResWalkSum, kResWords = 10 };
+static_assert(kResWalkSum < kResWords, "result words");
 
 struct SweepArgs {
   const std::uint8_t* w;
@@ -103,12 +116,18 @@ struct SweepArgs {
   std::uint32_t* cnt;         // chain records starting in the region
   std::uint32_t* bidx;        // index of the first bad one among them
   std::uint32_t* fl;
-  // records with payloads longer than kLaneFold (checked by a CRC batch)
+  // per region, the payloads folded in the sweep across region ends (kLaneFold < record_len <= kMedMax)
+  std::uint32_t* carry;       // crc0 of [rs, min(E, re)): the record the chain is in when it enters
+  std::uint32_t* cm_len;      // the region's crossing payload (its last record's, when it goes on past
+  std::uint32_t* cm_crc;      //   re): record_len (0: none), stored CRC, the register after its bytes in
+  std::uint32_t* cm_part;     //   the region (initial register included; ~0 when there are none), and
+  std::uint32_t* cm_pos;      //   its start - rs | its list index << 16
+  // records with payloads longer than kMedMax (checked by a CRC batch)
   std::uint64_t* l_off;
   std::uint32_t* l_len;
   std::uint32_t* l_crc;
   std::uint32_t* l_reg;
-  std::uint32_t* l_meta;      // index in the region | version << 8
+  std::uint32_t* l_meta;      // index in the region | version << 9
   std::uint64_t l_cap;        // entries; sweep wave w owns [w * l_seg, (w + 1) * l_seg), the rest is
   std::uint64_t l_seg;        //   taken by atomics (fix-ups, and sweep waves whose segment is full)
   std::uint32_t* l_cnt;       // per sweep wave: entries in its segment
@@ -177,10 +196,10 @@ __device__ __forceinline__ std::uint32_t lane_prefix(std::uint32_t v, std::uint3
 // positions, transposed (bit 8 j + i = byte j of dword i; 4 shifts and 2 ORs, no multiply). ps + 8 is
 // at the same granule offset sh in every lane (pieces and steps are multiples of 16 bytes), so the
 // mask of the positions in front of it is wave-uniform. Candidates are taken in position order and
-// checked in full.
+// checked in full; candidates in front of qmin are passed (a search again after a break).
 static_assert(kPiece % 16 == 0 && kSearchStep % 16 == 0 && kSearchStep + 15 + 9 < 80, "search granules");
 template <typename P>
-__device__ __forceinline__ P search_piece(const std::uint8_t* win, P rs, std::uint32_t o, P ps, P qe, P size) {
+__device__ __forceinline__ P search_piece(const std::uint8_t* win, P rs, std::uint32_t o, P ps, P qe, P size, P qmin) {
   if (ps >= qe) return kNoneP<P>;
   const std::uint32_t b0 = static_cast<std::uint32_t>(ps - rs) + o + 8u;
   const std::uint32_t a16 = b0 & ~15u;
@@ -224,7 +243,7 @@ __device__ __forceinline__ P search_piece(const std::uint8_t* win, P rs, std::ui
     const std::uint32_t b = b0 - 8u + pos;
     const std::uint64_t rl = rd32(win, b), kl = rd32(win, b + 18u), vl = rd32(win, b + 22u);
     const P q = ps + pos;
-    if (rl == 18u + kl + vl && static_cast<P>(rl) <= size - q - 8u) return q;  // (size - q >= 26)
+    if (q >= qmin && rl == 18u + kl + vl && static_cast<P>(rl) <= size - q - 8u) return q;  // (size - q >= 26)
     const std::uint64_t bit = 1ull << ((hw ? 32u : 0u) + 8u * j + i);
     if (lo) m0 &= ~bit; else m1 &= ~bit;
   }
@@ -241,6 +260,7 @@ struct Walk {
   std::uint32_t st[kStore];
   std::uint32_t n, tiny;
   P x;
+  P lr;  // the start of the last record walked
   bool broke;
 };
 template <typename P>
@@ -252,6 +272,7 @@ __device__ __forceinline__ void walk_piece(const std::uint8_t* win, P rs, std::u
     wk.n = 0;
     wk.tiny = kStore;
     wk.broke = false;
+    wk.lr = kNoneP<P>;
   }
   auto step = [&](std::uint32_t j, bool store) {
     if (size - p < kWalMeta) {
@@ -268,6 +289,7 @@ __device__ __forceinline__ void walk_piece(const std::uint8_t* win, P rs, std::u
           if (rl < 18u && wk.tiny == kStore) wk.tiny = j;
         }
         wk.n += 1;
+        wk.lr = p;
         p += 8u + static_cast<P>(rl);
       }
     }
@@ -300,8 +322,9 @@ __device__ __forceinline__ void walk_piece(const std::uint8_t* win, P rs, std::u
 // dword-aligned window reads. The initial register enters as inj[L] = Shift_L(0xFFFFFFFF)
 // (crc_s(D) = Shift_|D|(s) ^ crc_0(D)); slicing-by-4 into the 64 KiB table image (crc32.cpp:9-16
 // restated). (Two or three records per lane at once, as independent chains, measured slower.)
-__device__ __forceinline__ std::uint32_t fold_lane(const std::uint8_t* win, const std::uint32_t* tab, const std::uint32_t* inj,
-                                                   const dev::LaneConstX& kc, std::uint32_t s, std::uint32_t L) {
+// fold_raw is that fold from a zero register (crc0 of the bytes); callers add inj[L] ^ 0xFFFFFFFF.
+__device__ __forceinline__ std::uint32_t fold_raw(const std::uint8_t* win, const std::uint32_t* tab, const dev::LaneConstX& kc,
+                                                  std::uint32_t s, std::uint32_t L) {
   const std::uint32_t nd = (L + 3u) >> 2;
   const std::uint32_t nmax = dev::wave_max(nd);
   const std::uint32_t z = 4u * nd - L;
@@ -320,10 +343,89 @@ __device__ __forceinline__ std::uint32_t fold_lane(const std::uint8_t* win, cons
     if (i < nd) r = t;
     lo = hi;
   }
-  return r.value() ^ inj[L] ^ 0xFFFFFFFFu;
+  return r.value();
+}
+
+// a*b mod P (reflected, x^0 = bit 31) in few registers: the loop is kept rolled (fully unrolled, the
+// shift chain of b is computed ahead and held, which spills the sweep).
+__device__ __forceinline__ std::uint32_t mul_lean(std::uint32_t a, std::uint32_t b, std::uint32_t poly) {
+  std::uint32_t p = 0;
+#pragma unroll 4
+  for (int i = 0; i < 32; ++i) {
+    p ^= b & (0u - (a >> 31));
+    a <<= 1;
+    b = (b >> 1) ^ (poly & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+// x^(8n) mod P for n <= 2 kRow (head_shift[h][31] = Shift_h(x^0)), and reg moved past n zero bytes.
+__device__ __forceinline__ std::uint32_t x8n(const DeviceTables* t, std::uint32_t n) {
+  return n <= static_cast<std::uint32_t>(kRow)
+             ? t->head_shift[n][31]
+             : dev::multmodp(t->head_shift[n - kRow][31], t->head_shift[kRow][31], t->poly);
+}
+__device__ __forceinline__ std::uint32_t shift_n(const DeviceTables* t, std::uint32_t reg, std::uint32_t n) {
+  return dev::multmodp(x8n(t, n), reg, t->poly);
+}
+
+// Fold ranges R[0, nr) of the window (3 words each: x | y << 16 window offsets, kk | kind << 9 |
+// record offset << 16, and the result): every range cut into kChunk-byte chunks aligned to its end
+// (the front chunk shorter), one chunk per lane (fold_raw from LDS), the chunk j from the end moved past
+// the j kChunk bytes behind it by one multiply with K[j] = x^(8 kChunk j), and the chunks of a range
+// XORed into its result word (LDS atomics). A range of kind kRangeWhole / kRangeHead starts from the
+// initial register (the front chunk adds Shift_L(0xFFFFFFFF)), so its result is the CRC register after
+// its bytes; a kRangeCarry range gives crc0. Whole wave; nr <= 64.
+__device__ __forceinline__ void fold_ranges(const std::uint8_t* win, const std::uint32_t* tab, const std::uint32_t* inj,
+                                            const std::uint32_t* K, std::uint32_t poly, const dev::LaneConstX& kc,
+                                            std::uint32_t lane, std::uint32_t* R, std::uint32_t nr) {
+  std::uint32_t xi = 0, yi = 0, ci = 0, ki = 0;
+  if (lane < nr) {
+    const std::uint32_t w0 = R[3 * lane];
+    xi = w0 & 0xFFFFu;
+    yi = w0 >> 16;
+    ci = (yi - xi + kChunk - 1u) / kChunk;
+    ki = (R[3 * lane + 1] >> 9) & 3u;
+    R[3 * lane + 2] = 0u;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  std::uint32_t total;
+  const std::uint32_t pre = lane_prefix<7>(ci, &total);  // (ci <= 64)
+  for (std::uint32_t base = 0; base < total; base += 64u) {
+    const std::uint32_t g = base + lane;
+    const bool act = g < total;
+    std::uint32_t r = 0;  // the range of chunk g: the last one whose first chunk is at most g
+    for (std::uint32_t i = 1; i < nr; ++i) r = g >= static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(pre), static_cast<int>(i))) ? i : r;
+    const std::uint32_t x = shfl_pos(xi, r), y = shfl_pos(yi, r), c = shfl_pos(ci, r), p = shfl_pos(pre, r);
+    const std::uint32_t kd = shfl_pos(ki, r);
+    const std::uint32_t k = g - p;                 // chunk from the range's front
+    const std::uint32_t j = act ? c - 1u - k : 0u;  // chunk from its end
+    const std::uint32_t ce = y - j * kChunk;
+    const std::uint32_t cs = ce > x + kChunk ? ce - kChunk : x;
+    const std::uint32_t L = act ? ce - cs : 0u;
+    std::uint32_t v = fold_raw(win, tab, kc, cs, L);
+    if (k == 0u && kd != kRangeCarry) v ^= inj[L];
+    v = mul_lean(K[j], v, poly);
+    if (act) atomicXor(&R[3 * r + 2], v);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
 }
 
 constexpr int kAhead = 2;  // regions in registers: the current one and the next, in flight
+constexpr std::uint32_t kBreakRetries = 3;  // walks again from past a break, per region (sweep only)
+constexpr std::uint32_t kTrustHop = 2;      // whole regions a hop from an implausible header may pass over
+
+// The record at window offset (r - rs) + o has a header the encoder could have written (wal.cpp:19-61):
+// op and tombstone bytes 0 or 1, record_len = 18 + key_len + value_len. Wave-uniform r.
+template <typename P>
+__device__ __forceinline__ bool plausible_at(const std::uint8_t* win, P rs, std::uint32_t o, P r) {
+  if (r == kNoneP<P>) return false;
+  const std::uint32_t b = static_cast<std::uint32_t>(r - rs) + o;
+  const std::uint64_t rl = rd32(win, b), kl = rd32(win, b + 18u), vl = rd32(win, b + 22u);
+  return (rd32(win, b + 8u) & 0xFFu) <= 1u && (rd32(win, b + 17u) & 0xFFu) <= 1u && rl == 18u + kl + vl;
+}
 
 // Region r's granules: 1 KiB load rows k = 0..kRows-1, lane l's 16 bytes at row offset 16 l, as
 // buffer loads through a descriptor over the region's first `rows` rows, cut at the image's end: the
@@ -348,13 +450,14 @@ __device__ __forceinline__ void load_region(const SweepArgs& a, std::uint64_t r,
 // mode (a wait on a load drains every prefetch issued before it).
 template <bool FIXUP, typename P>
 __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win, std::uint16_t* list, const std::uint32_t* tab,
-                                           const std::uint32_t* inj, std::uint32_t r0, std::uint32_t limit, P e,
-                                           std::uint32_t wave) {
+                                           const std::uint32_t* inj, const std::uint32_t* K, std::uint32_t r0, std::uint32_t limit,
+                                           P e, std::uint32_t wave, bool hop_giant) {
   constexpr P kNo = kNoneP<P>;
   const std::uint32_t lane = threadIdx.x & 63u;
   const dev::LaneConstX kc = dev::lane_const16(lane);
   const P size = static_cast<P>(a.size);
   const std::uint32_t o = a.o;
+  const std::uint32_t poly = a.tabs->poly;
   // the last region whose granules this wave writes into its window: limit (the overlap of limit - 1)
   const std::uint32_t rlast = limit;
   uint4 buf[kAhead][kRows];
@@ -387,6 +490,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
       a.cnt[j] = 0;
       a.bidx[j] = 0xFFFFFFFFu;
       a.fl[j] = kChain | (v << 8);
+      a.cm_len[j] = 0;
     }
   };
   // the region body: the next region to walk (limit: the wave stops; fix-up converged)
@@ -401,24 +505,39 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
       if constexpr (FIXUP) ver = (a.fl[rr] >> 8) + 1u;
       // ---- 1. starts ------------------------------------------------------------------------------
       const P ps = rs + static_cast<P>(kPiece) * lane, pe = ps + kPiece;
-      const bool exact = e != kNo;
+      bool exact = e != kNo;
       std::uint32_t flags;
-      P Er = e, Xout = e;
+      P Er = e, Xout = e, Lr = kNo;
       std::uint32_t count = 0, bad_k = 0xFFFFFFFFu;
       P Bpos = kNo;
+      std::uint32_t carry_v = 0, cm_len = 0, cm_crc = 0, cm_part = 0, cm_pos = 0;
+      // the whole region (up to the image's end) as one carry range: a region inside a record
+      auto carry_whole = [&]() {
+        const std::uint32_t n = size - rs < static_cast<P>(kRegion) ? static_cast<std::uint32_t>(size - rs) : kRegion;
+        std::uint32_t* R = reinterpret_cast<std::uint32_t*>(list);
+        if (lane == 0) {
+          R[0] = o | (o + n) << 16;
+          R[1] = kRangeCarry << 9;
+        }
+        fold_ranges(win, tab, inj, K, poly, kc, lane, R, 1u);
+        carry_v = R[2];
+      };
       if (exact && (e >= re || e >= size)) {
         flags = kChain | spec_next;  // inside a record, or past the chain's end: no starts here
+        if (e >= re && e < size) carry_whole();
       } else {
+       P floor = rs;  // the first position a search may take (past a break, when the region is walked again)
+       for (std::uint32_t attempt = 0;; ++attempt) {
         const std::uint32_t le = exact ? static_cast<std::uint32_t>((e - rs) / kPiece) : 0u;
         P s = kNo;
         if (exact && lane == le) s = e;
         // the piece's first plausible header, kSearchStep positions at a time from its front (the first
         // step finds it in a WAL of small records; a piece inside a long payload is searched whole)
         const P qend = size >= kWalMeta ? std::min<P>(pe, size - static_cast<P>(kWalMeta) + 1u) : 0u;
-        bool hunt = (!exact || lane > le) && ps < qend;
+        bool hunt = (!exact || lane > le) && ps < qend && pe > floor;
         for (P q0 = ps; __ballot(hunt) != 0; q0 += kSearchStep) {
           if (hunt) {
-            s = search_piece<P>(win, rs, o, q0, std::min<P>(q0 + kSearchStep, qend), size);
+            s = search_piece<P>(win, rs, o, q0, std::min<P>(q0 + kSearchStep, qend), size, floor);
             hunt = s == kNo && q0 + kSearchStep < qend;
           }
         }
@@ -430,7 +549,10 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
         if (f == 64u) {
           flags = kSearch;
           Er = Xout = kNo;
-        } else {
+          carry_whole();  // (on the true chain, a region without a start lies inside a record)
+          break;
+        }
+        {
           C &= ~((1ull << f) - 1ull);
           std::uint32_t cur = f;
           for (;;) {
@@ -467,6 +589,21 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
           const bool broke = __builtin_amdgcn_readlane(static_cast<int>(wk.broke), static_cast<int>(last)) != 0;
           Er = exact ? e : readlane_pos(s, f);
           flags = kChain | spec_next | (broke ? kBroke : 0u) | (!broke && Xout == size ? kEnd : 0u);
+          if constexpr (!FIXUP) {
+            // A chain that breaks in the sweep may have entered on a guess: a chunk's search start, or a
+            // chain descended from one, such as a run of well-formed records inside a value, which breaks
+            // where the value ends. The region is walked again from the first plausible header past the
+            // break (the next true record, most likely), and its entry counts as a search start, so
+            // wal_bounds checks it against its predecessor's exit and a true break (a corruption) is
+            // found again by the fix-up walk from that exit. Region 0 enters exactly and keeps its break.
+            if (broke && rr != 0u && attempt < kBreakRetries) {
+              floor = Xout + 1u;
+              exact = false;
+              spec_next = kSpec;
+              continue;
+            }
+          }
+          Lr = readlane_pos(wk.lr, last);
           // ---- 3. list and fold ------------------------------------------------------------------------
           const bool on = (C >> lane) & 1ull;
           (void)lane_prefix<kPiece / 8 < 32 ? 5 : 6>(on ? wk.n : 0u, &count);  // every chain record
@@ -480,20 +617,61 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
 #pragma unroll
           for (std::uint32_t j = 0; j < kStore; ++j)
             if (j < nn && pre + j < nl) list[pre + j] = static_cast<std::uint16_t>(wk.st[j]);
+          // fold ranges behind the list: the bytes in front of the entry first (the record the chain is
+          // in when it enters the region), then the payloads longer than kLaneFold, in chain order
+          std::uint32_t* R = reinterpret_cast<std::uint32_t*>(list + ((nl + 1u) & ~1u));
+          const std::uint32_t rcap = (2u * kList - 2u * ((nl + 1u) & ~1u)) / 12u;
+          std::uint32_t nr = 0;
+          const std::uint32_t eo = static_cast<std::uint32_t>(Er - rs) + o;  // the entry's window offset
+          // a carry of at most kLaneFold bytes (the tail of a short record, usually) is one more lane job of
+          // the record fold below; a longer one is range 0 of the range fold
+          const bool carry_lane = Er > rs && eo - o <= kLaneFold;
+          if (Er > rs && !carry_lane) {
+            if (lane == 0) {
+              R[0] = o | eo << 16;
+              R[1] = kRangeCarry << 9;
+            }
+            nr = 1;
+          }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
-          for (std::uint32_t base = 0; base < nl; base += 64u) {
+          const std::uint32_t njobs = nl + (carry_lane ? 1u : 0u);
+          for (std::uint32_t base = 0; base < njobs; base += 64u) {
             const std::uint32_t kk = base + lane;
             const bool act = kk < nl;
+            const bool cj = carry_lane && kk == nl;  // this lane folds the carry
             const std::uint32_t so = act ? list[kk] : 0u;
             const std::uint32_t b = so + o;
             const std::uint32_t rl = rd32(win, b), stored = rd32(win, b + 4u);
             const std::uint32_t kl = rd32(win, b + 18u), vl = rd32(win, b + 22u);
             const bool kv_ok = kWalMeta + static_cast<std::uint64_t>(kl) + vl <= 8ull + rl;  // wal.cpp:118-121
             const bool lng = act && rl > kLaneFold;
-            const std::uint32_t crc = fold_lane(win, tab, inj, kc, b + 8u, act && !lng ? rl : 0u);
+            const std::uint32_t fn = cj ? eo - o : act && !lng ? rl : 0u;
+            const std::uint32_t raw = fold_raw(win, tab, kc, cj ? o : b + 8u, fn);
+            const std::uint32_t crc = raw ^ inj[fn] ^ 0xFFFFFFFFu;
+            if (carry_lane && base + 64u > nl)
+              carry_v = static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(raw), static_cast<int>(nl - base)));
             const bool bad = act && (!kv_ok || (!lng && crc != stored));
-            const std::uint64_t lb = __ballot(lng);
+            // payloads up to kMedMax: a fold range of their bytes in the region (wholly inside it, or the
+            // head of one that goes on); longer ones, or ones the ranges have no room for: the batch
+            bool gnt = lng && rl > kMedMax;
+            const bool med = lng && !gnt;
+            const std::uint64_t mb = __ballot(med);
+            if (mb) {
+              const std::uint32_t at = nr + __builtin_amdgcn_mbcnt_hi(static_cast<std::uint32_t>(mb >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo(static_cast<std::uint32_t>(mb), 0u));
+              if (med) {
+                if (at < rcap) {
+                  const std::uint32_t rend = o + kRegion, pa = b + 8u, pz = b + 8u + rl;
+                  R[3 * at] = std::min(pa, rend) | std::min(pz, rend) << 16;
+                  R[3 * at + 1] = kk | (pz <= rend ? kRangeWhole : kRangeHead) << 9 | b << 16;
+                } else {
+                  gnt = true;
+                }
+              }
+              nr = std::min<std::uint32_t>(nr + static_cast<std::uint32_t>(__builtin_popcountll(mb)), rcap);
+            }
+            const std::uint64_t lb = __ballot(gnt);
             if (lb) {
               const std::uint32_t nb = static_cast<std::uint32_t>(__builtin_popcountll(lb));
               std::uint64_t at;
@@ -508,19 +686,48 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
               }
               const std::uint64_t idx = at + __builtin_amdgcn_mbcnt_hi(static_cast<std::uint32_t>(lb >> 32),
                                                                        __builtin_amdgcn_mbcnt_lo(static_cast<std::uint32_t>(lb), 0u));
-              if (lng && idx < a.l_cap) {
+              if (gnt && idx < a.l_cap) {
                 a.l_off[idx] = static_cast<std::uint64_t>(rs) + so + 8u;
                 a.l_len[idx] = rl;
                 a.l_crc[idx] = stored;
                 a.l_reg[idx] = rr;
-                a.l_meta[idx] = kk | (ver << 8);
+                a.l_meta[idx] = kk | (ver << 9);  // (kk < 512)
               }
             }
             const std::uint64_t bk = __ballot(bad);
             if (bk && bad_k == 0xFFFFFFFFu) bad_k = base + static_cast<std::uint32_t>(__builtin_ctzll(bk));
           }
+          if (nr) {
+            fold_ranges(win, tab, inj, K, poly, kc, lane, R, nr);
+            // results, one range per lane: the carry, whole payloads checked here, the crossing one kept
+            std::uint32_t kd = 0, kki = 0, bo = 0, acc = 0, x = 0, y = 0;
+            if (lane < nr) {
+              x = R[3 * lane] & 0xFFFFu;
+              y = R[3 * lane] >> 16;
+              const std::uint32_t w1 = R[3 * lane + 1];
+              kki = w1 & 0x1FFu;
+              kd = (w1 >> 9) & 3u;
+              bo = w1 >> 16;
+              acc = R[3 * lane + 2];
+            }
+            if (Er > rs && !carry_lane) carry_v = static_cast<std::uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(acc)));
+            const std::uint32_t st = lane < nr && kd != kRangeCarry ? rd32(win, bo + 4u) : 0u;
+            const bool mbad = lane < nr && kd == kRangeWhole && (acc ^ 0xFFFFFFFFu) != st;
+            const std::uint32_t mk = dev::wave_min(mbad ? kki : 0xFFFFFFFFu);
+            bad_k = std::min(bad_k, mk);
+            const std::uint64_t hb = __ballot(lane < nr && kd == kRangeHead);
+            if (hb) {  // (at most one: the region's last record)
+              const std::uint32_t h = static_cast<std::uint32_t>(__builtin_ctzll(hb));
+              cm_len = static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rd32(win, bo)), static_cast<int>(h)));
+              cm_crc = static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(st), static_cast<int>(h)));
+              cm_part = static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x == y ? 0xFFFFFFFFu : acc), static_cast<int>(h)));
+              cm_pos = static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>((bo - o) | kki << 16), static_cast<int>(h)));
+            }
+          }
           if (bad_k != 0xFFFFFFFFu) Bpos = rs + list[bad_k];
         }
+        break;
+       }
       }
       // ---- 4. region record, next entry --------------------------------------------------------------
       bool stop = false;
@@ -530,6 +737,15 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
         next_e = Xout;
         next_spec = 0u;
       }
+      // A record that covers whole regions: longer than kMedMax, they are passed over (the batch checks
+      // it); up to kMedMax, walked one by one (their bytes are folded as carries). A region inside one
+      // (no record walked) continues the hop that led there.
+      bool ghop = false;
+      if ((flags & kChain) && !(flags & kBroke) && Xout < size && Xout / kRegion > static_cast<P>(rr) + 1u) {
+        if (Lr != kNo) hop_giant = Xout - Lr - 8u > static_cast<P>(kMedMax);
+        ghop = hop_giant;
+      }
+      if (ghop) flags |= kGiantHop;
       if constexpr (FIXUP) {
         // converged: the next region's stored chain enters where this one leaves
         if (rr + 1u >= limit || (flags & (kBroke | kEnd)) || !(flags & kChain)) {
@@ -546,6 +762,11 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
         case 3: a.cnt[rr] = count; break;
         case 4: a.bidx[rr] = bad_k; break;
         case 5: a.fl[rr] = flags | (ver << 8); break;
+        case 6: a.carry[rr] = carry_v; break;
+        case 7: a.cm_len[rr] = cm_len; break;
+        case 8: a.cm_crc[rr] = cm_crc; break;
+        case 9: a.cm_part[rr] = cm_part; break;
+        case 10: a.cm_pos[rr] = cm_pos; break;
         default: break;
       }
       e = next_e;
@@ -555,7 +776,18 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
         // the chain's current record covers whole regions: store them, go on where it ends
         const std::uint32_t qr = static_cast<std::uint32_t>(next_e / kRegion);
         const std::uint32_t q = next_e >= size || qr > limit ? limit : qr;
-        if (q > rr + 1u) {
+        if (q > rr + 1u && (next_e >= size || ghop)) {
+          // A hop over more than kTrustHop regions from a header the encoder could not have written (a
+          // fake chain reading a random record_len) is not passed over: the regions behind it are walked
+          // from their own searches, and wal_bounds checks the hop's landing like a chunk's (a fix-up from
+          // there, whose entry lies past its first region, passes over). In a fix-up task too: one that
+          // started from a fake exit would otherwise store its landing in every region it jumps, and the
+          // true chain's task could not meet a stored entry again before its limit.
+          if (Lr != kNo && next_e < size && qr > rr + 1u + kTrustHop && !plausible_at(win, rs, o, Lr)) {
+            e = kNo;
+            spec_next = kSpec;
+            return rr + 1u;
+          }
           pass_over(rr + 1u, q, next_e);
           nx = q;
           if constexpr (FIXUP) {
@@ -567,6 +799,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
     }
   };
   bool done = false;
+  std::uint32_t walked = 0;  // regions this wave walked (fix-up statistics)
   for (std::uint32_t r = r0; r < limit && !done; r += kAhead) {
 #pragma unroll
     for (int k = 0; k < kAhead; ++k) {
@@ -577,6 +810,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
       }
       put(rr, buf[k], buf[(k + 1) % kAhead][0]);
       const std::uint32_t nx = body(rr);
+      ++walked;
       if (nx >= limit) {
         done = true;
       } else if (nx != rr + 1u) {  // passed over regions: the pipeline restarts at nx
@@ -587,17 +821,23 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
     }
   }
   if (!FIXUP && lane == 0) a.l_cnt[wave] = static_cast<std::uint32_t>(nlong);
+  if (FIXUP && lane == 0) {
+    atomicMax(&a.res[kResWalkMax], static_cast<unsigned long long>(walked));
+    atomicAdd(&a.res[kResWalkSum], static_cast<unsigned long long>(walked));
+  }
 }
 
 template <bool FIXUP, typename P>
 __global__ __launch_bounds__(kSweepThreads) void wal_sweep(SweepArgs a) {
   // one block with the tables at LDS address 0, so a lookup's v_perm result is its address
-  __shared__ __attribute__((aligned(16))) std::uint8_t lds[kLdsSliceWords * 2 + kSweepWaves * kWinBytes + 4 * (kLaneFold + 1)];
+  __shared__ __attribute__((aligned(16))) std::uint8_t lds[kLdsSliceWords * 2 + kSweepWaves * kWinBytes + 4 * (kLaneFold + 1) + 4 * 64];
   std::uint32_t* tab = reinterpret_cast<std::uint32_t*>(lds);
   std::uint8_t (*wins)[kWinBytes] = reinterpret_cast<std::uint8_t (*)[kWinBytes]>(lds + kLdsSliceWords * 2);
   std::uint32_t* inj = reinterpret_cast<std::uint32_t*>(lds + kLdsSliceWords * 2 + kSweepWaves * kWinBytes);  // Shift_L(0xFFFFFFFF)
+  std::uint32_t* K = inj + kLaneFold + 1;  // x^(8 kChunk j), j < 64
   dev::fill_lds_slicing16(a.tabs, tab);
   for (std::uint32_t i = threadIdx.x; i <= kLaneFold; i += blockDim.x) inj[i] = a.tabs->init_shift[i];
+  if (threadIdx.x < 64u) K[threadIdx.x] = x8n(a.tabs, kChunk * threadIdx.x);
   __syncthreads();
   const std::uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const std::uint32_t w = blockIdx.x * kSweepWaves + wv;
@@ -607,9 +847,12 @@ __global__ __launch_bounds__(kSweepThreads) void wal_sweep(SweepArgs a) {
   if constexpr (!FIXUP) {
     const std::uint32_t r0 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(w) * a.nreg / a.nwaves);
     const std::uint32_t r1 = static_cast<std::uint32_t>(static_cast<std::uint64_t>(w + 1) * a.nreg / a.nwaves);
-    sweep_wave<false, P>(a, win, list, tab, inj, r0, r1, r0 == 0 ? P(0) : kNoneP<P>, w);
+    sweep_wave<false, P>(a, win, list, tab, inj, K, r0, r1, r0 == 0 ? P(0) : kNoneP<P>, w, false);
   } else {
-    sweep_wave<true, P>(a, win, list, tab, inj, a.t_begin[w], a.t_limit[w], static_cast<P>(a.t_entry[w]), w);
+    const std::uint32_t b = a.t_begin[w];
+    // a task whose entry lies past its first region continues its predecessor's hop
+    const bool giant = b > 0u && (a.fl[b - 1u] & kGiantHop) != 0u;
+    sweep_wave<true, P>(a, win, list, tab, inj, K, b, a.t_limit[w], static_cast<P>(a.t_entry[w]), w, giant);
   }
 }
 
@@ -665,11 +908,17 @@ __global__ void wal_long_gather(SweepArgs a, const std::uint64_t* l_base, std::u
   } else {
     src = a.l_seg * W + (j - nseg);
   }
-  d_off[j] = a.l_off[src];
-  d_len[j] = a.l_len[src];
+  // Entries of superseded walks (a stale version) or at or past the settled chain's first bad short
+  // record / break (res P, Q of a fin pass without long payloads) are not folded: speculative chains
+  // list records of any length, hundreds of MB each. They go to the batch empty and marked stale.
+  const std::uint64_t off = a.l_off[src];
+  const std::uint32_t reg = a.l_reg[src], meta = a.l_meta[src];
+  const bool live = (meta >> 9) == (a.fl[reg] >> 8) && off - 8u < std::min<std::uint64_t>(res[kResP], res[kResQ]);
+  d_off[j] = off;
+  d_len[j] = live ? a.l_len[src] : 0u;
   d_crc[j] = a.l_crc[src];
-  d_reg[j] = a.l_reg[src];
-  d_meta[j] = a.l_meta[src];
+  d_reg[j] = reg;
+  d_meta[j] = live ? meta : 0xFFFFFFFFu;
 }
 
 // Boundary checks: region p ends a chain segment when the next region's entry did not come from p
@@ -707,8 +956,41 @@ __global__ void wal_reset(unsigned long long* res, int lo, int hi) {
   if (i < hi) res[i] = (i == kResP || i == kResQ || i == kResFirst) ? ~0ull : 0ull;
 }
 
-// First bad record P (region lists and, when their versions are current, the long payloads) and the
-// chain's break Q.
+// The payload of region r's crossing record (kLaneFold < record_len <= kMedMax, going on past the
+// region's end): its register after the region (cm_part) carried through the regions it covers,
+// r' = Shift_n(r) ^ carry[q] for the n payload bytes of region q (carry[q] = crc0 of [rs_q, min(E_q, re_q)),
+// and E_q = its end in the last one). A payload that starts past rs_q (the record's 8-byte prefix cut
+// by the region end) has those prefix bytes h in front of it in carry[q]: crc0(h || p) =
+// Shift_|p|(crc0(h)) ^ crc0(p), so r' = Shift_|p|(r ^ crc0(h)) ^ carry[q]. True when it fails its stored
+// CRC (wal.cpp:86-93); *pos = the record's start, *idx = its index in the region's list.
+__device__ bool crossing_bad(const SweepArgs& a, std::uint64_t r, std::uint64_t* pos, std::uint32_t* idx) {
+  const std::uint32_t len = a.cm_len[r];
+  if (len == 0u) return false;
+  const std::uint32_t f = a.fl[r];
+  if (!(f & kChain) || (f & kBroke)) return false;
+  const DeviceTables* t = a.tabs;
+  const std::uint32_t cp = a.cm_pos[r];
+  const std::uint64_t s = r * kRegion + (cp & 0xFFFFu), A = s + 8u, B = A + len;
+  std::uint32_t reg = a.cm_part[r];
+  for (std::uint64_t q = r + 1u; q < a.nreg; ++q) {
+    const std::uint64_t rsq = q * kRegion, req = rsq + kRegion, y = std::min(B, req);
+    const std::uint32_t c = a.carry[q];
+    if (A > rsq) {
+      std::uint32_t h = 0;
+      for (std::uint64_t i = rsq; i < A; ++i) h = (h >> 8) ^ t->slice[0][(h ^ a.w[i]) & 0xFFu];
+      reg = shift_n(t, reg ^ h, static_cast<std::uint32_t>(y - A)) ^ c;
+    } else {
+      reg = shift_n(t, reg, static_cast<std::uint32_t>(y - rsq)) ^ c;
+    }
+    if (B <= req) break;
+  }
+  *pos = s;
+  *idx = cp >> 16;
+  return (reg ^ 0xFFFFFFFFu) != a.cm_crc[r];
+}
+
+// First bad record P (region lists, crossing payloads and, when their versions are current, the long
+// payloads) and the chain's break Q.
 __global__ void wal_fin_min(SweepArgs a, const std::uint32_t* got, std::uint64_t nlong) {
   const std::uint64_t i = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
   if (i < a.nreg) {
@@ -717,11 +999,14 @@ __global__ void wal_fin_min(SweepArgs a, const std::uint32_t* got, std::uint64_t
       if (f & kBroke) atomicMin(&a.res[kResQ], static_cast<unsigned long long>(a.X[i]));
       const std::uint64_t b = a.B[i];
       if (b != kNone) atomicMin(&a.res[kResP], static_cast<unsigned long long>(b));
+      std::uint64_t cpos;
+      std::uint32_t cidx;
+      if (crossing_bad(a, i, &cpos, &cidx)) atomicMin(&a.res[kResP], static_cast<unsigned long long>(cpos));
     }
   }
   if (i < nlong) {
     const std::uint32_t r = a.l_reg[i];
-    if ((a.l_meta[i] >> 8) == (a.fl[r] >> 8) && got[i] != a.l_crc[i])
+    if ((a.l_meta[i] >> 9) == (a.fl[r] >> 8) && got[i] != a.l_crc[i])
       atomicMin(&a.res[kResP], static_cast<unsigned long long>(a.l_off[i] - 8u));
   }
 }
@@ -739,12 +1024,17 @@ __global__ void wal_fin_count(SweepArgs a, const std::uint32_t* got, std::uint64
   if (i < a.nreg) {
     const std::uint32_t f = a.fl[i];
     if ((f & kChain) && (i < rb || (i == rb && !bad))) c = a.cnt[i];
-    if (bad && i == rb && a.B[i] == P) a.res[kResLidx] = a.bidx[i];
+    if (bad && i == rb) {
+      std::uint64_t cpos;
+      std::uint32_t cidx;
+      if (a.B[i] == P) a.res[kResLidx] = a.bidx[i];
+      else if (crossing_bad(a, i, &cpos, &cidx) && cpos == P) a.res[kResLidx] = cidx;
+    }
   }
   if (bad && i < nlong) {
     const std::uint32_t r = a.l_reg[i];
-    if ((a.l_meta[i] >> 8) == (a.fl[r] >> 8) && got[i] != a.l_crc[i] && a.l_off[i] - 8u == P)
-      a.res[kResLidx] = a.l_meta[i] & 0xFFu;
+    if ((a.l_meta[i] >> 9) == (a.fl[r] >> 8) && got[i] != a.l_crc[i] && a.l_off[i] - 8u == P)
+      a.res[kResLidx] = a.l_meta[i] & 0x1FFu;
   }
   // block sum
 #pragma unroll
@@ -767,6 +1057,8 @@ __global__ void wal_publish(SweepArgs a, std::uint64_t* h) {
   h[1] = a.res[kResLongSeg] + std::min<std::uint64_t>(a.res[kResLongA], a.l_cap - a.l_seg * a.wsweep);
   h[5] = a.res[kResLongA];
   h[6] = a.res[kResFirst];
+  h[7] = a.res[kResWalkMax];
+  h[8] = a.res[kResWalkSum];
   if (P < Q) {
     h[2] = a.res[kResCnt] + a.res[kResLidx];
     h[3] = P;
@@ -783,7 +1075,7 @@ struct WalScratch {
   std::mutex mu;
   std::uint64_t cap_reg = 0, cap_raw = 0, cap_dense = 0;
   std::uint32_t cap_waves = 0;
-  void* regs = nullptr;   // per region: E, X, B (u64), cnt, bidx, fl (u32)
+  void* regs = nullptr;   // per region: E, X, B (u64), cnt, bidx, fl, carry, cm_len, cm_crc, cm_part, cm_pos (u32)
   void* raw = nullptr;    // long payloads as the sweep lists them: off (u64), len, crc, reg, meta (u32)
   void* dense = nullptr;  // the same, gathered for the CRC batch, and got (u32)
   std::uint32_t* l_cnt = nullptr;   // per sweep wave, then the scan's bases (u64)
@@ -841,8 +1133,9 @@ WalScratch* g_wal[64] = {};
 
 // What the calling thread's last WAL verify did (tkv_debug_wal_last).
 thread_local std::uint64_t g_last[4] = {0, 0, 0, 0};  // rounds, host walk needed, image copied, no fix-up
-// per fix-up round of the calling thread's last verify: failing boundaries, tasks, longest task and
-// all tasks' regions (tkv_debug_wal_rounds)
+// per fix-up round of the calling thread's last verify: failing boundaries, tasks, the longest task's
+// range and all tasks' ranges in regions, the most regions one task walked and all walked regions
+// (tkv_debug_wal_rounds)
 thread_local std::vector<std::uint64_t> g_rounds;
 
 #define WAL_HIP(call)                                                            \
@@ -899,6 +1192,11 @@ SweepArgs carve(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std::u
   a.cnt = p4;
   a.bidx = p4 + C;
   a.fl = p4 + 2 * C;
+  a.carry = p4 + 3 * C;
+  a.cm_len = p4 + 4 * C;
+  a.cm_crc = p4 + 5 * C;
+  a.cm_part = p4 + 6 * C;
+  a.cm_pos = p4 + 7 * C;
   long_view(s.raw, s.cap_raw, &a, nullptr);
   a.l_cap = s.cap_raw;
   a.l_seg = seg;
@@ -962,7 +1260,7 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
   const std::uint64_t nreg64 = (size + kRegion - 1) / kRegion;
   if (nreg64 >= 0xFFFFFFF0ull) return set_error(TKV_INVALID_ARGUMENT, "WAL image too large for the device walk");
   const std::uint32_t nreg = static_cast<std::uint32_t>(nreg64);
-  if (int rc = grow(&s.regs, &s.cap_reg, nreg, 3 * 8 + 3 * 4)) return rc;
+  if (int rc = grow(&s.regs, &s.cap_reg, nreg, 3 * 8 + 8 * 4)) return rc;
   const std::uint32_t W = static_cast<std::uint32_t>(std::min<std::uint64_t>(nreg, s.cap_waves));
   // a wave's segment holds the long payloads of its chunk's chain (>= kLaneFold + 8 bytes apart);
   // more (speculative chains) and the fix-ups' go to the atomic area behind the segments
@@ -1032,13 +1330,15 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
         span_max = std::max<std::uint64_t>(span_max, tl[k] - tb[k]);
         span_sum += tl[k] - tb[k];
       }
-      g_rounds.insert(g_rounds.end(), {s.h_res[0], kept.size(), span_max, span_sum});
+      const std::size_t at = g_rounds.size();
+      g_rounds.insert(g_rounds.end(), {s.h_res[0], kept.size(), span_max, span_sum, 0, 0});
       SweepArgs f = a;
       f.nwaves = static_cast<std::uint32_t>(kept.size());
       f.t_begin = s.d_task;
       f.t_limit = s.d_task + kMaxFix;
       f.t_entry = reinterpret_cast<const std::uint64_t*>(s.d_task + 2 * kMaxFix);
       hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, static_cast<int>(kResIncons), static_cast<int>(kResFirst) + 1);
+      hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, static_cast<int>(kResWalkMax), static_cast<int>(kResWalkSum) + 1);
       if (size <= kPos32Max)
         hipLaunchKernelGGL((wal_sweep<true, std::uint32_t>), dim3(blocks(f.nwaves, kSweepWaves)), dim3(kSweepThreads), 0, st, f);
       else
@@ -1047,6 +1347,8 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
       hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
       WAL_HIP(hipGetLastError());
       WAL_HIP(hipStreamSynchronize(st));
+      g_rounds[at + 4] = s.h_res[7];
+      g_rounds[at + 5] = s.h_res[8];
       ++rounds;
       if (rounds > kRoundBudget) {  // (never seen) the exact host walk decides instead
         *needs_host_walk = true;
@@ -1068,6 +1370,9 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
         SweepArgs d = a;
         std::uint32_t* got = nullptr;
         long_view(s.dense, s.cap_dense, &d, &got);
+        // P and Q without the long payloads, on the settled chain: the gather folds only live entries
+        hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, static_cast<int>(kResP), static_cast<int>(kResCnt) + 1);
+        hipLaunchKernelGGL(wal_fin_min, dim3(blocks(nreg, 256)), dim3(256), 0, st, a, nullptr, 0ull);
         hipLaunchKernelGGL(wal_long_gather, dim3(blocks(nlong, 256)), dim3(256), 0, st, a, s.l_base, W, s.res, d.l_off,
                            d.l_len, d.l_crc, d.l_reg, d.l_meta);
         WAL_HIP(hipGetLastError());

@@ -84,9 +84,10 @@ def main():
         if hasattr(lib, "tkv_debug_wal_rounds"):
             lib.tkv_debug_wal_rounds.restype = ctypes.c_size_t
             lib.tkv_debug_wal_rounds.argtypes = [VP, ctypes.c_size_t]
-            rw = np.zeros(256, np.uint64)
-            k = lib.tkv_debug_wal_rounds(VP(rw.ctypes.data), 256)
-            rounds = [dict(zip(("failing", "tasks", "longest", "regions"), map(int, rw[i:i + 4]))) for i in range(0, min(k, 256), 4)]
+            rw = np.zeros(6 * 256, np.uint64)
+            k = lib.tkv_debug_wal_rounds(VP(rw.ctypes.data), rw.size)
+            rounds = [dict(zip(("failing", "tasks", "longest", "regions", "walk_max", "walked"), map(int, rw[i:i + 6])))
+                      for i in range(0, min(k, rw.size), 6)]
             if rounds:
                 print(json.dumps({"image": name, "fixup_rounds": rounds}), flush=True)
         if stamps:
@@ -111,9 +112,10 @@ def main():
         if hasattr(lib, "tkv_debug_wal_rounds"):
             lib.tkv_debug_wal_rounds.restype = ctypes.c_size_t
             lib.tkv_debug_wal_rounds.argtypes = [VP, ctypes.c_size_t]
-            rw = np.zeros(256, np.uint64)
-            k = lib.tkv_debug_wal_rounds(VP(rw.ctypes.data), 256)
-            rounds = [dict(zip(("failing", "tasks", "longest", "regions"), map(int, rw[i:i + 4]))) for i in range(0, min(k, 256), 4)]
+            rw = np.zeros(6 * 256, np.uint64)
+            k = lib.tkv_debug_wal_rounds(VP(rw.ctypes.data), rw.size)
+            rounds = [dict(zip(("failing", "tasks", "longest", "regions", "walk_max", "walked"), map(int, rw[i:i + 6])))
+                      for i in range(0, min(k, rw.size), 6)]
             if rounds:
                 print(json.dumps({"image": name, "fixup_rounds": rounds}), flush=True)
         if stamps:
