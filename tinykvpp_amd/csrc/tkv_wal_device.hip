@@ -27,7 +27,7 @@
 // The chunk's first region has no known entry: its wave takes the first plausible header it finds
 // (a region without one "searches" on). After a break the wave searches again.
 //
-// Exactness across chunks (wal_bounds, wal_sweep in fix-up mode): wherever a region's entry did not
+// Exactness across chunks (bounds_one in wal_after, wal_sweep in fix-up mode): wherever a region's entry did not
 // come from its predecessor's exit in the same walk (chunk starts, search starts, fix-up starts),
 // the predecessor's exit must land exactly on the entry, with only searching regions (no chain)
 // between. A boundary that fails is walked again from the true exit by a fix-up wave, which stops as
@@ -72,6 +72,7 @@ constexpr std::uint32_t kSearchStep = 48;       // positions a lane tests per se
 constexpr unsigned kSweepWaves = 12;            // waves per workgroup: the 64 KiB tables + 12 windows of LDS
 constexpr unsigned kSweepThreads = 64 * kSweepWaves;
 constexpr unsigned kHres = 16;                  // words of the pinned result block
+constexpr std::uint32_t kMaxFix = 1u << 16;     // failing boundaries handled per fix-up round
 static_assert(kRegion % 1024 == 0 && kPiece % 16 == 0, "region = whole 1 KiB load rows");
 static_assert(kOver >= kLaneFold + 8 && kOver >= kWalMeta, "a lane-folded record ends inside the window");
 static_assert(kList * 26 >= kRegion + 26 * 2, "records of >= 26 bytes fit the list");
@@ -94,8 +95,8 @@ constexpr std::uint32_t kRangeCarry = 0, kRangeWhole = 1, kRangeHead = 2;
 
 // Result words (device, u64): see wal_fin_*.
 enum : int { kResLongA = 0, kResIncons, kResFirst, kResP, kResQ, kResLidx, kResCnt, kResLongSeg, kResWalkMax,
-             kResWalkSum, kResWords = 10 };
-static_assert(kResWalkSum < kResWords, "result words");
+             kResWalkSum, kResDone, kResWords = 11 };
+static_assert(kResDone < kResWords, "result words");
 
 struct SweepArgs {
   const std::uint8_t* w;
@@ -196,10 +197,10 @@ __device__ __forceinline__ std::uint32_t lane_prefix(std::uint32_t v, std::uint3
 // positions, transposed (bit 8 j + i = byte j of dword i; 4 shifts and 2 ORs, no multiply). ps + 8 is
 // at the same granule offset sh in every lane (pieces and steps are multiples of 16 bytes), so the
 // mask of the positions in front of it is wave-uniform. Candidates are taken in position order and
-// checked in full; candidates in front of qmin are passed (a search again after a break).
+// checked in full.
 static_assert(kPiece % 16 == 0 && kSearchStep % 16 == 0 && kSearchStep + 15 + 9 < 80, "search granules");
 template <typename P>
-__device__ __forceinline__ P search_piece(const std::uint8_t* win, P rs, std::uint32_t o, P ps, P qe, P size, P qmin) {
+__device__ __forceinline__ P search_piece(const std::uint8_t* win, P rs, std::uint32_t o, P ps, P qe, P size) {
   if (ps >= qe) return kNoneP<P>;
   const std::uint32_t b0 = static_cast<std::uint32_t>(ps - rs) + o + 8u;
   const std::uint32_t a16 = b0 & ~15u;
@@ -243,7 +244,7 @@ __device__ __forceinline__ P search_piece(const std::uint8_t* win, P rs, std::ui
     const std::uint32_t b = b0 - 8u + pos;
     const std::uint64_t rl = rd32(win, b), kl = rd32(win, b + 18u), vl = rd32(win, b + 22u);
     const P q = ps + pos;
-    if (q >= qmin && rl == 18u + kl + vl && static_cast<P>(rl) <= size - q - 8u) return q;  // (size - q >= 26)
+    if (rl == 18u + kl + vl && static_cast<P>(rl) <= size - q - 8u) return q;  // (size - q >= 26)
     const std::uint64_t bit = 1ull << ((hw ? 32u : 0u) + 8u * j + i);
     if (lo) m0 &= ~bit; else m1 &= ~bit;
   }
@@ -414,7 +415,6 @@ __device__ __forceinline__ void fold_ranges(const std::uint8_t* win, const std::
 }
 
 constexpr int kAhead = 2;  // regions in registers: the current one and the next, in flight
-constexpr std::uint32_t kBreakRetries = 3;  // walks again from past a break, per region (sweep only)
 constexpr std::uint32_t kTrustHop = 2;      // whole regions a hop from an implausible header may pass over
 
 // The record at window offset (r - rs) + o has a header the encoder could have written (wal.cpp:19-61):
@@ -505,7 +505,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
       if constexpr (FIXUP) ver = (a.fl[rr] >> 8) + 1u;
       // ---- 1. starts ------------------------------------------------------------------------------
       const P ps = rs + static_cast<P>(kPiece) * lane, pe = ps + kPiece;
-      bool exact = e != kNo;
+      const bool exact = e != kNo;
       std::uint32_t flags;
       P Er = e, Xout = e, Lr = kNo;
       std::uint32_t count = 0, bad_k = 0xFFFFFFFFu;
@@ -526,18 +526,17 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
         flags = kChain | spec_next;  // inside a record, or past the chain's end: no starts here
         if (e >= re && e < size) carry_whole();
       } else {
-       P floor = rs;  // the first position a search may take (past a break, when the region is walked again)
-       for (std::uint32_t attempt = 0;; ++attempt) {
+       do {  // (breaks out to the region record)
         const std::uint32_t le = exact ? static_cast<std::uint32_t>((e - rs) / kPiece) : 0u;
         P s = kNo;
         if (exact && lane == le) s = e;
         // the piece's first plausible header, kSearchStep positions at a time from its front (the first
         // step finds it in a WAL of small records; a piece inside a long payload is searched whole)
         const P qend = size >= kWalMeta ? std::min<P>(pe, size - static_cast<P>(kWalMeta) + 1u) : 0u;
-        bool hunt = (!exact || lane > le) && ps < qend && pe > floor;
+        bool hunt = (!exact || lane > le) && ps < qend;
         for (P q0 = ps; __ballot(hunt) != 0; q0 += kSearchStep) {
           if (hunt) {
-            s = search_piece<P>(win, rs, o, q0, std::min<P>(q0 + kSearchStep, qend), size, floor);
+            s = search_piece<P>(win, rs, o, q0, std::min<P>(q0 + kSearchStep, qend), size);
             hunt = s == kNo && q0 + kSearchStep < qend;
           }
         }
@@ -589,20 +588,6 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
           const bool broke = __builtin_amdgcn_readlane(static_cast<int>(wk.broke), static_cast<int>(last)) != 0;
           Er = exact ? e : readlane_pos(s, f);
           flags = kChain | spec_next | (broke ? kBroke : 0u) | (!broke && Xout == size ? kEnd : 0u);
-          if constexpr (!FIXUP) {
-            // A chain that breaks in the sweep may have entered on a guess: a chunk's search start, or a
-            // chain descended from one, such as a run of well-formed records inside a value, which breaks
-            // where the value ends. The region is walked again from the first plausible header past the
-            // break (the next true record, most likely), and its entry counts as a search start, so
-            // wal_bounds checks it against its predecessor's exit and a true break (a corruption) is
-            // found again by the fix-up walk from that exit. Region 0 enters exactly and keeps its break.
-            if (broke && rr != 0u && attempt < kBreakRetries) {
-              floor = Xout + 1u;
-              exact = false;
-              spec_next = kSpec;
-              continue;
-            }
-          }
           Lr = readlane_pos(wk.lr, last);
           // ---- 3. list and fold ------------------------------------------------------------------------
           const bool on = (C >> lane) & 1ull;
@@ -726,8 +711,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
           }
           if (bad_k != 0xFFFFFFFFu) Bpos = rs + list[bad_k];
         }
-        break;
-       }
+       } while (false);
       }
       // ---- 4. region record, next entry --------------------------------------------------------------
       bool stop = false;
@@ -779,7 +763,7 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
         if (q > rr + 1u && (next_e >= size || ghop)) {
           // A hop over more than kTrustHop regions from a header the encoder could not have written (a
           // fake chain reading a random record_len) is not passed over: the regions behind it are walked
-          // from their own searches, and wal_bounds checks the hop's landing like a chunk's (a fix-up from
+          // from their own searches, and the boundary check takes the hop's landing like a chunk's (a fix-up from
           // there, whose entry lies past its first region, passes over). In a fix-up task too: one that
           // started from a fake exit would otherwise store its landing in every region it jumps, and the
           // true chain's task could not meet a stored entry again before its limit.
@@ -857,11 +841,13 @@ __global__ __launch_bounds__(kSweepThreads) void wal_sweep(SweepArgs a) {
 }
 
 // Dense long-payload list for the CRC batch: the sweep waves' segments, then the atomic area.
-// One block of 1024 threads scans the per-wave counts; every block copies its waves' entries.
-__global__ void wal_long_scan(const std::uint32_t* l_cnt, std::uint32_t W, std::uint64_t* l_base, unsigned long long* res) {
-  __shared__ std::uint64_t part[1024];
+// One block of kFinThreads threads scans the per-wave counts (block 0 of wal_after); every block of
+// wal_long_gather copies its entries.
+constexpr unsigned kFinThreads = 256;
+__device__ void long_scan_block(const std::uint32_t* l_cnt, std::uint32_t W, std::uint64_t* l_base, unsigned long long* res) {
+  __shared__ std::uint64_t part[kFinThreads];
   const std::uint32_t t = threadIdx.x;
-  const std::uint32_t per = (W + 1023u) / 1024u;
+  const std::uint32_t per = (W + kFinThreads - 1u) / kFinThreads;
   std::uint64_t s = 0;
   for (std::uint32_t i = 0; i < per; ++i) {
     const std::uint32_t w = t * per + i;
@@ -869,7 +855,7 @@ __global__ void wal_long_scan(const std::uint32_t* l_cnt, std::uint32_t W, std::
   }
   part[t] = s;
   __syncthreads();
-  for (std::uint32_t d = 1; d < 1024u; d <<= 1) {
+  for (std::uint32_t d = 1; d < kFinThreads; d <<= 1) {
     const std::uint64_t v = t >= d ? part[t - d] : 0;
     __syncthreads();
     part[t] += v;
@@ -883,9 +869,9 @@ __global__ void wal_long_scan(const std::uint32_t* l_cnt, std::uint32_t W, std::
       run += l_cnt[w];
     }
   }
-  if (t == 1023u) {
-    l_base[W] = part[1023];
-    res[kResLongSeg] = part[1023];
+  if (t == kFinThreads - 1u) {
+    l_base[W] = part[kFinThreads - 1u];
+    res[kResLongSeg] = part[kFinThreads - 1u];
   }
 }
 // entry j of the dense list (d_*) <- wave w's segment / the atomic area
@@ -927,8 +913,7 @@ __global__ void wal_long_gather(SweepArgs a, const std::uint64_t* l_base, std::u
 // (it searched) or be inside the same record (a chain region entered at X: a fix-up's, carried
 // through the record). A chain region whose entry lies past its own end was carried there, so the
 // rule is exact. Failing p go to the list.
-__global__ void wal_bounds(SweepArgs a, std::uint32_t* inc_p, std::uint64_t* inc_x, std::uint32_t cap) {
-  const std::uint64_t p = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+__device__ void bounds_one(const SweepArgs& a, std::uint64_t p, std::uint32_t* inc_p, std::uint64_t* inc_x, std::uint32_t cap) {
   if (p + 1 >= a.nreg) return;
   const std::uint32_t f = a.fl[p] & 0xFFu;
   if (!(f & kChain) || (f & (kBroke | kEnd))) return;
@@ -991,8 +976,7 @@ __device__ bool crossing_bad(const SweepArgs& a, std::uint64_t r, std::uint64_t*
 
 // First bad record P (region lists, crossing payloads and, when their versions are current, the long
 // payloads) and the chain's break Q.
-__global__ void wal_fin_min(SweepArgs a, const std::uint32_t* got, std::uint64_t nlong) {
-  const std::uint64_t i = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
+__device__ void fin_min_one(const SweepArgs& a, std::uint64_t i, const std::uint32_t* got, std::uint64_t nlong) {
   if (i < a.nreg) {
     const std::uint32_t f = a.fl[i];
     if (f & kChain) {
@@ -1011,10 +995,63 @@ __global__ void wal_fin_min(SweepArgs a, const std::uint32_t* got, std::uint64_t
   }
 }
 
+// After a sweep (one launch, kFinThreads per block): the long-payload scan (block 0, when scan), the
+// boundary check of every region (bounds) and its share of P and Q (fmin).
+struct AfterArgs {
+  const std::uint32_t* l_cnt;
+  std::uint32_t W;
+  std::uint64_t* l_base;
+  std::uint32_t* inc_p;
+  std::uint64_t* inc_x;
+  const std::uint32_t* got;
+  std::uint64_t nlong;
+  bool scan, bounds, fmin;
+};
+__global__ __launch_bounds__(kFinThreads) void wal_after(SweepArgs a, AfterArgs f) {
+  std::uint32_t b = blockIdx.x;
+  if (f.scan) {
+    if (b == 0) {
+      long_scan_block(f.l_cnt, f.W, f.l_base, a.res);
+      return;
+    }
+    --b;
+  }
+  const std::uint64_t i = b * static_cast<std::uint64_t>(kFinThreads) + threadIdx.x;
+  if (f.bounds) bounds_one(a, i, f.inc_p, f.inc_x, kMaxFix);
+  if (f.fmin) fin_min_one(a, i, f.got, f.nlong);
+}
+
+__device__ __forceinline__ std::uint64_t res_load(const unsigned long long* r) {
+  return __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Result words into the host's pinned block: [0] failing boundaries, [1] long payloads, [2] records
+// good, [3] stop offset, [4] corrupted, [5] entries the atomic area was asked for, [6] the first failing
+// boundary, [7]/[8] the fix-up walk statistics.
+__device__ void publish_one(const SweepArgs& a, std::uint64_t* h) {
+  const std::uint64_t P = res_load(&a.res[kResP]), Q = res_load(&a.res[kResQ]);
+  h[0] = res_load(&a.res[kResIncons]);
+  h[1] = res_load(&a.res[kResLongSeg]) + std::min<std::uint64_t>(res_load(&a.res[kResLongA]), a.l_cap - a.l_seg * a.wsweep);
+  h[5] = res_load(&a.res[kResLongA]);
+  h[6] = res_load(&a.res[kResFirst]);
+  h[7] = res_load(&a.res[kResWalkMax]);
+  h[8] = res_load(&a.res[kResWalkSum]);
+  if (P < Q) {
+    h[2] = res_load(&a.res[kResCnt]) + res_load(&a.res[kResLidx]);
+    h[3] = P;
+    h[4] = 1;
+  } else {
+    h[2] = res_load(&a.res[kResCnt]);
+    h[3] = Q == kNone ? a.size : Q;
+    h[4] = Q == kNone ? 0 : 1;
+  }
+}
+
 // Records before the stop (block sums of cnt over the regions before it) and the first bad record's
-// index within its region.
-__global__ void wal_fin_count(SweepArgs a, const std::uint32_t* got, std::uint64_t nlong) {
+// index within its region; the last block to finish publishes the result words.
+__global__ __launch_bounds__(512) void wal_finish(SweepArgs a, const std::uint32_t* got, std::uint64_t nlong, std::uint64_t* h) {
   __shared__ unsigned long long part[8];
+  __shared__ bool last;
   const std::uint64_t i = blockIdx.x * static_cast<std::uint64_t>(blockDim.x) + threadIdx.x;
   const std::uint64_t P = a.res[kResP], Q = a.res[kResQ];
   const bool bad = P < Q;
@@ -1027,14 +1064,14 @@ __global__ void wal_fin_count(SweepArgs a, const std::uint32_t* got, std::uint64
     if (bad && i == rb) {
       std::uint64_t cpos;
       std::uint32_t cidx;
-      if (a.B[i] == P) a.res[kResLidx] = a.bidx[i];
-      else if (crossing_bad(a, i, &cpos, &cidx) && cpos == P) a.res[kResLidx] = cidx;
+      if (a.B[i] == P) atomicExch(&a.res[kResLidx], static_cast<unsigned long long>(a.bidx[i]));
+      else if (crossing_bad(a, i, &cpos, &cidx) && cpos == P) atomicExch(&a.res[kResLidx], static_cast<unsigned long long>(cidx));
     }
   }
   if (bad && i < nlong) {
     const std::uint32_t r = a.l_reg[i];
     if ((a.l_meta[i] >> 9) == (a.fl[r] >> 8) && got[i] != a.l_crc[i] && a.l_off[i] - 8u == P)
-      a.res[kResLidx] = a.l_meta[i] & 0x1FFu;
+      atomicExch(&a.res[kResLidx], static_cast<unsigned long long>(a.l_meta[i] & 0x1FFu));
   }
   // block sum
 #pragma unroll
@@ -1045,29 +1082,20 @@ __global__ void wal_fin_count(SweepArgs a, const std::uint32_t* got, std::uint64
     unsigned long long s = 0;
     for (unsigned k = 0; k < blockDim.x / 64u; ++k) s += part[k];
     if (s) atomicAdd(&a.res[kResCnt], s);
+    __threadfence();  // (this block's words, the Lidx exchanges included, before its count)
+    last = atomicAdd(&a.res[kResDone], 1ull) == gridDim.x - 1u;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __threadfence();
+    publish_one(a, h);
+    a.res[kResDone] = 0;
   }
 }
 
-// Result words into the host's pinned block: [0] failing boundaries, [1] long payloads, [2] records
-// good, [3] stop offset, [4] corrupted, [5] entries the atomic area was asked for.
+// The result words alone (fix-up rounds).
 __global__ void wal_publish(SweepArgs a, std::uint64_t* h) {
-  if (threadIdx.x != 0) return;
-  const std::uint64_t P = a.res[kResP], Q = a.res[kResQ];
-  h[0] = a.res[kResIncons];
-  h[1] = a.res[kResLongSeg] + std::min<std::uint64_t>(a.res[kResLongA], a.l_cap - a.l_seg * a.wsweep);
-  h[5] = a.res[kResLongA];
-  h[6] = a.res[kResFirst];
-  h[7] = a.res[kResWalkMax];
-  h[8] = a.res[kResWalkSum];
-  if (P < Q) {
-    h[2] = a.res[kResCnt] + a.res[kResLidx];
-    h[3] = P;
-    h[4] = 1;
-  } else {
-    h[2] = a.res[kResCnt];
-    h[3] = Q == kNone ? a.size : Q;
-    h[4] = Q == kNone ? 0 : 1;
-  }
+  if (threadIdx.x == 0) publish_one(a, h);
 }
 
 // Per-device scratch, grown by doubling and kept between calls (guarded by mu).
@@ -1122,7 +1150,6 @@ struct WalScratch {
     (void)hipHostFree(h_task);
   }
 };
-constexpr std::uint32_t kMaxFix = 1u << 16;  // failing boundaries handled per round
 // Fix-up rounds before the exact host walk takes over. The first failing boundary moves forward every
 // round, so the rounds are bounded by the boundaries; none of the adversarial images needs more than a
 // handful, and each round costs two host syncs.
@@ -1243,13 +1270,16 @@ int scratch(WalScratch** out) {
 }
 
 // fin_min, fin_count, publish (long payloads from the dense list when nlong > 0).
-void launch_fin(SweepArgs a, WalScratch& s, std::uint64_t nlong, hipStream_t st) {
+// wal_after (scan: the long-payload scan; bounds: the boundary checks; P and Q always, with the long
+// payloads from the dense list when nlong > 0), then, when finish, wal_finish (counts and the result words).
+void launch_after(SweepArgs a, WalScratch& s, std::uint32_t W, std::uint64_t nlong, bool scan, bool bounds, bool finish,
+                  hipStream_t st) {
   std::uint32_t* got = nullptr;
   if (nlong) long_view(s.dense, s.cap_dense, &a, &got);
   const std::uint64_t n = std::max<std::uint64_t>(a.nreg, nlong);
-  hipLaunchKernelGGL(wal_fin_min, dim3(blocks(n, 256)), dim3(256), 0, st, a, got, nlong);
-  hipLaunchKernelGGL(wal_fin_count, dim3(blocks(n, 512)), dim3(512), 0, st, a, got, nlong);
-  hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
+  const AfterArgs f{s.l_cnt, W, s.l_base, s.inc_p, s.inc_x, got, nlong, scan, bounds, true};
+  hipLaunchKernelGGL(wal_after, dim3(blocks(n, kFinThreads) + (scan ? 1u : 0u)), dim3(kFinThreads), 0, st, a, f);
+  if (finish) hipLaunchKernelGGL(wal_finish, dim3(blocks(n, 512)), dim3(512), 0, st, a, got, nlong, s.d_hres);
 }
 
 // The verify of [w, w + size) on `st` (synchronous). Caller holds s.mu.
@@ -1274,9 +1304,7 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
       hipLaunchKernelGGL((wal_sweep<false, std::uint32_t>), dim3(blocks(W, kSweepWaves)), dim3(kSweepThreads), 0, st, a);
     else
       hipLaunchKernelGGL((wal_sweep<false, std::uint64_t>), dim3(blocks(W, kSweepWaves)), dim3(kSweepThreads), 0, st, a);
-    hipLaunchKernelGGL(wal_long_scan, dim3(1), dim3(1024), 0, st, s.l_cnt, W, s.l_base, s.res);
-    hipLaunchKernelGGL(wal_bounds, dim3(blocks(nreg, 256)), dim3(256), 0, st, a, s.inc_p, s.inc_x, kMaxFix);
-    launch_fin(a, s, 0, st);
+    launch_after(a, s, W, 0, true, true, true, st);
     WAL_HIP(hipGetLastError());
     WAL_HIP(hipStreamSynchronize(st));
     std::uint64_t rounds = 1;
@@ -1313,7 +1341,7 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
       std::vector<std::uint32_t> kept_lim;
       for (std::size_t k = 0; k < bnd.size(); ++k) {
         const std::uint32_t lim = k + 1 < bnd.size() ? bnd[k + 1].first + 1 : nreg;
-        if (k > 0 && bnd[k].second / kRegion >= lim) continue;
+        if (k > 0 && (bnd[k].second / kRegion >= lim || bnd[k].second / kRegion > bnd[k].first + 1u + kTrustHop)) continue;
         kept.push_back(bnd[k]);
         kept_lim.push_back(lim);
       }
@@ -1343,7 +1371,8 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
         hipLaunchKernelGGL((wal_sweep<true, std::uint32_t>), dim3(blocks(f.nwaves, kSweepWaves)), dim3(kSweepThreads), 0, st, f);
       else
         hipLaunchKernelGGL((wal_sweep<true, std::uint64_t>), dim3(blocks(f.nwaves, kSweepWaves)), dim3(kSweepThreads), 0, st, f);
-      hipLaunchKernelGGL(wal_bounds, dim3(blocks(nreg, 256)), dim3(256), 0, st, a, s.inc_p, s.inc_x, kMaxFix);
+      const AfterArgs fb{s.l_cnt, W, s.l_base, s.inc_p, s.inc_x, nullptr, 0, false, true, false};
+      hipLaunchKernelGGL(wal_after, dim3(blocks(nreg, kFinThreads)), dim3(kFinThreads), 0, st, a, fb);
       hipLaunchKernelGGL(wal_publish, dim3(1), dim3(64), 0, st, a, s.d_hres);
       WAL_HIP(hipGetLastError());
       WAL_HIP(hipStreamSynchronize(st));
@@ -1372,14 +1401,14 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
         long_view(s.dense, s.cap_dense, &d, &got);
         // P and Q without the long payloads, on the settled chain: the gather folds only live entries
         hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, static_cast<int>(kResP), static_cast<int>(kResCnt) + 1);
-        hipLaunchKernelGGL(wal_fin_min, dim3(blocks(nreg, 256)), dim3(256), 0, st, a, nullptr, 0ull);
+        launch_after(a, s, W, 0, false, false, false, st);
         hipLaunchKernelGGL(wal_long_gather, dim3(blocks(nlong, 256)), dim3(256), 0, st, a, s.l_base, W, s.res, d.l_off,
                            d.l_len, d.l_crc, d.l_reg, d.l_meta);
         WAL_HIP(hipGetLastError());
         if (int rc = batch_device_impl(kAlgoCrc32, w, d.l_off, d.l_len, nullptr, got, nlong, st)) return rc;
       }
       hipLaunchKernelGGL(wal_reset, dim3(1), dim3(64), 0, st, s.res, static_cast<int>(kResP), static_cast<int>(kResCnt) + 1);
-      launch_fin(a, s, nlong, st);
+      launch_after(a, s, W, nlong, false, false, true, st);
       WAL_HIP(hipGetLastError());
       WAL_HIP(hipStreamSynchronize(st));
     }
