@@ -305,7 +305,8 @@ def test_model_small_block_groups(model, oracle):
 
 
 def packed_small_group(n):
-    """crc_packed_small's G: the smallest power of two with 64 G >= n (n <= 2048, a multiple of 16)."""
+    """The slot kernels' G (crc_packed_small at n = 64 G, crc_packed_small_gen for other n): the smallest
+    power of two with 64 G >= n (n <= 2048)."""
     g = 1
     while 64 * g < n:
         g *= 2
@@ -314,7 +315,7 @@ def packed_small_group(n):
 
 @pytest.mark.parametrize("n", [16, 48, 64, 80, 96, 128, 144, 256, 512, 1024, 1040, 2048])
 def test_model_packed_small_slots(model, oracle, n):
-    """crc_packed_small's arithmetic on a wave row of 64/G uniform blocks of n bytes packed back to
+    """The slot kernels' arithmetic on a wave row of 64/G uniform blocks of n bytes packed back to
     back (DESIGN.md §4.4): lane l of block l // G reads the 64 bytes at n - 64 G + 64 (l % G) of its
     block (pieces in front of the block read zeros), folds them, and moves the partial with the
     lane-shift column the workgroup copies into column l (device column 64 - G + l % G); the group's

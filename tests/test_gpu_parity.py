@@ -695,7 +695,7 @@ def test_rank_shards_full_size(gpu, oracle, cfg):
         assert aggregates(got) == (sh["xor"], sh["sum32"]), f"{cfg} shard at block {first}"
 
 
-@pytest.mark.parametrize("blen", [16, 48, 64, 80, 128, 144, 256, 512, 1024, 1040, 2048, 2064, 3008, 4080])
+@pytest.mark.parametrize("blen", [16, 48, 64, 80, 128, 144, 256, 512, 1024, 1040, 2000, 2048, 2064, 3008, 4080])
 def test_packed_small_blocks(gpu, oracle, blen):
     """Uniform batches of small blocks packed back to back (G-lane groups, each block right-aligned
     in a 64*G-byte slot, 64/G blocks per wave row): batches ending in a partial row,

@@ -1133,7 +1133,7 @@ __device__ __forceinline__ std::uint32_t group_xor(std::uint32_t v) {
 // packed kernel's pipeline and issue priority. Every block starts from init_default (per-block
 // initial registers take the generic kernel): raw = Shift_len(init) ^ crc_0(block), with
 // Shift_len(init) = head_z * init (head_z = x^(8 len)) added by the lane that stores the block.
-template <int G, bool EXACT, int DEPTH, int ILP, int PRIO = 0>
+template <int G, int DEPTH, int ILP, int PRIO = 0>
 __device__ __forceinline__ void crc_packed_small_body(const RowsArgs& a, std::uint32_t* lds) {
   static_assert(G >= 1 && G <= 32 && (G & (G - 1)) == 0, "G-lane groups of a power of two up to 32");
   static_assert(DEPTH > ILP && DEPTH % ILP == 0, "DEPTH must be a multiple of ILP and exceed it");
@@ -1149,35 +1149,21 @@ __device__ __forceinline__ void crc_packed_small_body(const RowsArgs& a, std::ui
   const std::uint32_t r0 = static_cast<std::uint32_t>(wave * TR / W);
   const std::uint32_t nrows = static_cast<std::uint32_t>((wave + 1) * TR / W) - r0;
   if (nrows == 0) return;
-  // Block b (len L <= 64 G, a multiple of 16) sits right-aligned in a slot of 64 G bytes: lane g
-  // of its group reads [b L + L - 64 G + 64 g, + 64). Pieces of that range in front of the block
-  // read the zero buffer (leading zeros leave an init-0 register at 0), so every load lies inside
-  // the batch. Row r holds blocks [r kBpr, (r + 1) kBpr): the lane's address is a per-lane constant
-  // plus r kBpr L. EXACT (L = 64 G): rows are the batch's 4 KiB rows and no piece lies in front of
-  // a block, so the addressing is the packed kernel's (the per-piece selects cost 8-15 % there); in
-  // the batch's last row the lanes past its last block read that row's first segment instead.
-  // Lanes past the batch's last block store nothing.
-  const std::uint32_t L = a.len;
-  const std::int64_t c_lane = static_cast<std::int64_t>(L) - 64 * G + 64 * static_cast<std::int64_t>(lane % G);
-  const std::int64_t lane_off = static_cast<std::int64_t>(lane / G) * L + c_lane;
-  const std::uint64_t row_stride = EXACT ? static_cast<std::uint64_t>(kRow) : static_cast<std::uint64_t>(kBpr) * L;
-  const std::uintptr_t row_base = reinterpret_cast<std::uintptr_t>(a.base) + static_cast<std::uint64_t>(r0) * row_stride;
-  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
+  // Blocks of exactly 64 G bytes: row r is the batch's 4 KiB row r and holds blocks [r kBpr,
+  // (r + 1) kBpr), lane g of a block's group reads its bytes [64 g, + 64), so the addressing is the
+  // packed kernel's; in the batch's last row the lanes past its last block read that row's first
+  // segment instead and store nothing. (Other multiples of 16 take crc_packed_small_gen's slots: the
+  // zero-filled slot tails cost 6-10 % here, profiles/r6/small_uniform/lens.jsonl.)
+  const std::uintptr_t row_base = reinterpret_cast<std::uintptr_t>(a.base) + static_cast<std::uint64_t>(r0) * kRow;
   const std::uint32_t lane_blk = lane / G;
 
   uint4 buf[DEPTH][4];
   auto issue = [&](std::uint32_t j, uint4 (&q)[4]) {
     const std::uint32_t jc = j < nrows ? j : nrows - 1;  // rows past the range reload the last one
     const bool live = static_cast<std::uint64_t>(r0 + jc) * kBpr + lane_blk < a.nblocks;
-    if constexpr (EXACT) {
-      const std::uintptr_t p = row_base + static_cast<std::uint64_t>(jc) * kRow + (live ? lane * kSeg : 0u);
+    const std::uintptr_t p = row_base + static_cast<std::uint64_t>(jc) * kRow + (live ? lane * kSeg : 0u);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i);
-    } else {
-      const std::uintptr_t p = row_base + static_cast<std::uint64_t>(jc) * row_stride + lane_off;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) q[i] = gload16(live && c_lane + 16 * i >= 0 ? p + 16u * i : dmy);
-    }
+    for (int i = 0; i < 4; ++i) q[i] = gload16(p + 16u * i);
   };
   // G >= 2: the kBpr results of a row move into keep lanes ((j % G) * kBpr + block of the row), so
   // G rows fill all 64 and leave in one coalesced store; a store per row would sit in the same vmcnt

@@ -173,12 +173,12 @@ __global__ __launch_bounds__(kThreads) void crc_packed(RowsArgs a) {
   dev::crc_packed_body<kPackedDepth, kPackedIlp, R1, R1 ? 0 : kPackedSkew, kPackedPrio>(a, lds);
 }
 
-// Packed small blocks (len <= 2 KiB a multiple of 16, stride == len, 16-byte aligned, default init):
-// DESIGN.md §4.4. EXACT: len = 64 G.
-template <int G, bool EXACT>
+// Packed small blocks (len = 64 G <= 2 KiB for a power of two G, stride == len, 16-byte aligned,
+// default init): DESIGN.md §4.4.
+template <int G>
 __global__ __launch_bounds__(kThreads) void crc_packed_small(RowsArgs a) {
   __shared__ std::uint32_t lds[kLdsWords];
-  dev::crc_packed_small_body<G, EXACT, kPackedDepth, kPackedIlp, kPackedPrio>(a, lds);
+  dev::crc_packed_small_body<G, kPackedDepth, kPackedIlp, kPackedPrio>(a, lds);
 }
 
 // General small uniform blocks (64 < len <= 2 KiB, any stride, alignment, initial registers):
@@ -1143,20 +1143,20 @@ hipError_t launch_packed(const RowsArgs& a, unsigned grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Lanes per block of crc_packed_small: the smallest power of two G with 64 G >= len, for len <= 2 KiB
-// a multiple of 16 (0: not this kernel's batch; between 2 and 4 KiB a slot is a whole 4 KiB row, and
-// the generic kernel measured faster, profiles/r2/packed_small/ab_slots.jsonl).
+// Lanes per block of crc_packed_small: G with len = 64 G, a power of two up to 32 (0: not this
+// kernel's batch. Other multiples of 16 up to 2 KiB, right-aligned in 64 G-byte slots with zeros in
+// front, measured 6-10 % faster through crc_packed_small_gen, profiles/r6/small_uniform/lens.jsonl;
+// between 2 and 4 KiB a slot is a whole 4 KiB row and the generic kernel measured faster,
+// profiles/r2/packed_small/ab_slots.jsonl).
 std::uint32_t packed_small_group(std::uint32_t len) {
-  if (len == 0 || len > 2048u || len % 16u != 0) return 0;
-  std::uint32_t g = 1;
-  while (64u * g < len) g <<= 1;
-  return g;
+  for (std::uint32_t g = 1; g <= 32u; g <<= 1)
+    if (len == 64u * g) return g;
+  return 0;
 }
 
 template <int G>
 void launch_small_g(const RowsArgs& a, unsigned grid, hipStream_t st) {
-  if (a.len == 64u * G) hipLaunchKernelGGL((crc_packed_small<G, true>), dim3(grid), dim3(kThreads), 0, st, a);
-  else hipLaunchKernelGGL((crc_packed_small<G, false>), dim3(grid), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL((crc_packed_small<G>), dim3(grid), dim3(kThreads), 0, st, a);
 }
 
 hipError_t launch_packed_small(const RowsArgs& a, unsigned grid, hipStream_t st) {
