@@ -287,6 +287,10 @@ int tkv_debug_irregular_mode(void *stream);
  * mode): bit 0 the lane phase (blocks <= 64 B), bits 1 / 2 the 4- / 8-lane group passes (65-256 /
  * 257-512 B); -1 on error. Synchronizes the stream. */
 int tkv_debug_irregular_phases(void *stream);
+/* Waves of the one-pass lane kernel (crc_list_lanes) for an irregular batch of nblocks on the current
+ * device: wave w takes its 64-block steps [w TS / W, (w + 1) TS / W), TS = ceil(nblocks / 64). 0 when
+ * no device is usable. */
+uint32_t tkv_debug_list_lanes_waves(uint64_t nblocks);
 /* The small-block lists of the last irregular batch on `stream` (all 0 in stream mode): out[0] =
  * blocks of at most 1 KiB the small-block phase folds (those no lane or group pass took), out[1] =
  * how many of them are at most 256 bytes (4-lane groups), out[2] = 257-512 bytes (8-lane groups; the

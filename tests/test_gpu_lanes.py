@@ -136,9 +136,10 @@ def test_irregular_one_pass_lanes(gpu, oracle, buf, shape):
     rng = np.random.default_rng(sum(map(ord, shape)))
     offs, lens = wal_payloads(rng, 1_100_003, tuple(range(0, 65)), 3)  # (>= 1 M blocks: the one-pass kernel runs)
     # the kernel's 64-block steps that start no wave's range (a wave whose first step does not fit one
-    # window sends the whole batch to the general path): launch_list_lanes' partition restated
+    # window sends the whole batch to the general path), from the kernel's own wave count
     ts = (offs.size + 63) // 64
-    nw = min(torch.cuda.get_device_properties(0).multi_processor_count, (ts + 15) // 16) * 16
+    nw = int(tk.load_library().tkv_debug_list_lanes_waves(offs.size))
+    assert nw > 0
     later = np.setdiff1d(np.arange(ts - 1), np.arange(nw, dtype=np.int64) * ts // nw)
     if shape == "shuffled":
         p = rng.permutation(offs.size)

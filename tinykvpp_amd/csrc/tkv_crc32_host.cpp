@@ -41,6 +41,7 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
                           const std::uint32_t* gate_flags, hipStream_t st);
 hipError_t launch_stream_rows(const RowsArgs& a, hipStream_t st, unsigned grid);
 hipError_t launch_list_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st);
+std::uint32_t list_lanes_waves(std::uint64_t nblocks, unsigned ncu);
 std::uint64_t prepass_tiles(std::uint64_t n);
 hipError_t launch_span(const std::uint8_t* stage, const SpanDesc& one, const SpanDesc* desc, std::uint32_t n,
                        std::uint32_t out_xor, std::uint32_t* out, std::uint32_t* count, std::uint32_t base,
@@ -1374,6 +1375,12 @@ int read_count_word(void* stream, int word) {
 int tkv_debug_irregular_mode(void* stream) { return read_count_word(stream, 3); }
 
 int tkv_debug_irregular_phases(void* stream) { return read_count_word(stream, kCountPhases); }
+
+uint32_t tkv_debug_list_lanes_waves(uint64_t nblocks) {
+  DevCtx* c = nullptr;
+  if (get_ctx(&c)) return 0;
+  return tkv::list_lanes_waves(nblocks, static_cast<unsigned>(c->ncu));
+}
 
 int tkv_debug_irregular_lists(void* stream, std::uint32_t out[3]) {
   const int w[3] = {1, kCountSmall4, kCountSmall8};

@@ -1296,13 +1296,20 @@ hipError_t launch_fixup(const RowsArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// One-pass lane kernel of an irregular batch (default initial register): see crc_list_lanes.
-hipError_t launch_list_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
-  const std::uint64_t steps = (static_cast<std::uint64_t>(a.nblocks) + 63u) / 64u;
+// Waves of crc_list_lanes for a batch of nblocks: one workgroup per CU (at most kListMaxGroups) or
+// fewer when the 64-block steps run out (tkv_debug_list_lanes_waves reports it to the tests).
+std::uint32_t list_lanes_waves(std::uint64_t nblocks, unsigned ncu) {
+  const std::uint64_t steps = (nblocks + 63u) / 64u;
   const std::uint64_t grid = std::max<std::uint64_t>(
       1, std::min<std::uint64_t>(std::min<std::uint64_t>(ncu, kListMaxGroups), (steps + kListWaves - 1) / kListWaves));
+  return static_cast<std::uint32_t>(grid * kListWaves);
+}
+
+// One-pass lane kernel of an irregular batch (default initial register): see crc_list_lanes.
+hipError_t launch_list_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   RowsArgs b = a;
-  b.nwaves = static_cast<std::uint32_t>(grid * kListWaves);
+  b.nwaves = list_lanes_waves(a.nblocks, ncu);
+  const std::uint64_t grid = b.nwaves / kListWaves;
   hipLaunchKernelGGL(crc_list_lanes, dim3(static_cast<unsigned>(grid)), dim3(kListThreads), 0, st, b);
   return hipGetLastError();
 }
