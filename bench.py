@@ -123,15 +123,16 @@ def pmc_traffic(csv_path, config):
     separate run: counters are never collected inside the timed run): per kernel of the step, the
     median over its dispatches, summed. FETCH_SIZE is in KiB and counts half the bytes of a wide
     streaming read on gfx950, so bytes = FETCH_SIZE*1024*2 (MI355X_MICROARCH.md §HBM). Default
-    source: the committed profile of this config, newest round first (profiles/r5/final/ holds cfg2-cfg5
-    on the round-5 tree)."""
+    source: the committed profile of this config, newest round first (profiles/r6/final/ holds cfg2-cfg5
+    on the round-6 tree, tools/gpu_evidence.sh)."""
     import csv
     from collections import defaultdict
     step_kernels = (("crc_rows", "crc_stream", "rows_tile_scan", "rows_scan_tiles",
                      "rows_finish", "crc_fixup") if config == "cfg4" else ("crc_packed",))
     path = csv_path
     if path is None:
-        for cand in (os.path.join(ROOT, "profiles", "r5", "final", f"pmc_{config}_FETCH_SIZE.csv"),
+        for cand in (os.path.join(ROOT, "profiles", "r6", "final", f"pmc_{config}_FETCH_SIZE.csv"),
+                     os.path.join(ROOT, "profiles", "r5", "final", f"pmc_{config}_FETCH_SIZE.csv"),
                      os.path.join(ROOT, "profiles", "r4", "final", f"pmc_{config}_FETCH_SIZE.csv"),
                      os.path.join(ROOT, "profiles", "r3", "pmc", f"pmc_{config}_FETCH_SIZE.csv"),
                      os.path.join(ROOT, "profiles", "r2", f"pmc_{config}", "FETCH_SIZE_counters.csv"),
