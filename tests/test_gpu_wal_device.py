@@ -355,3 +355,50 @@ def test_long_payloads_at_region_ends(gpu, oracle):
             assert want == ("corrupted", idx, t), (idx, t, L, o)
             assert both(img, n) == (want, want), (idx, t, L, o)
             img[o] ^= 0x10
+
+
+def test_image_over_4_gib(gpu, oracle):
+    """An image past 4 GiB (kPos32Max) takes the sweep's 64-bit positions (wal_sweep<*, uint64_t>):
+    257 records of exactly 16 MiB (zero values: passed over and checked by the long-payload batch at
+    offsets past 4 GiB), then 60 K Zipf records with 3-9 MiB values among them, all past 4 GiB. Clean,
+    then a payload byte flipped in a small record past 4 GiB, in a giant record's value below it, and
+    a torn tail: the verdict, good-record count and stop offset of wal.cpp:63-130 (the first bad
+    record is the flipped one; every other record is stamped)."""
+    rng = np.random.default_rng(44)
+    big, nbig = 16 << 20, 257
+    tail, toffs, tsize = make_wal(rng, 60_000, vmax=4000, giant=(100, 30_000))
+    head = big * nbig
+    size = head + tail.size
+    assert size > 0xFFFF0000
+    img = np.zeros(size, np.uint8)
+    img[head:] = tail
+    offs = np.arange(nbig, dtype=np.uint64) * big
+    hdr = np.zeros((nbig, 26), np.uint8)
+    hdr[:, 0:4] = np.full(nbig, big - 8, "<u4").view(np.uint8).reshape(-1, 4)
+    hdr[:, 9:17] = np.arange(nbig, dtype="<u8").view(np.uint8).reshape(-1, 8)
+    hdr[:, 22:26] = np.full(nbig, big - 26, "<u4").view(np.uint8).reshape(-1, 4)
+    img[offs.astype(np.int64)[:, None] + np.arange(26)] = hdr
+    lib = tk.load_library()
+    size32 = np.full(nbig, big, np.uint32)
+    tk.check(lib.tkv_wal_stamp(ctypes.c_void_p(img.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                               ctypes.c_void_p(size32.ctypes.data), nbig))
+    for k in (0, nbig - 1):  # the stamp of two giant records against the oracle
+        o = int(offs[k])
+        assert oracle.crc(img[o + 8:o + big].tobytes()) == int.from_bytes(img[o + 4:o + 8].tobytes(), "little")
+    nrec = nbig + toffs.size
+    d = torch.from_numpy(img).cuda()
+    del img
+    assert tk.wal.verify_device(d, size) == ("ok", nrec, size)
+    device_state = wal_last()
+    assert device_state["host_walk"] == 0, device_state
+    # a payload byte of tail record k (past 4 GiB), then of giant record 200's value (below 4 GiB)
+    for pos, idx in ((head + int(toffs[777]) + 26 + 3, nbig + 777), (int(offs[200]) + 5000, 200)):
+        d[pos] ^= 0x5A
+        start = head + int(toffs[777]) if idx >= nbig else int(offs[200])
+        assert tk.wal.verify_device(d, size) == ("corrupted", idx, start), pos
+        d[pos] ^= 0x5A
+    # a torn tail inside the last record
+    cut = head + int(toffs[-1]) + 10
+    assert tk.wal.verify_device(d, cut) == ("corrupted", nrec - 1, head + int(toffs[-1]))
+    del d
+    torch.cuda.empty_cache()

@@ -88,6 +88,8 @@ constexpr std::uint32_t kBroke = 8;   // the chain broke in the region, at X (wa
 constexpr std::uint32_t kEnd = 16;    // the chain reached the end of the image exactly (X == size)
 constexpr std::uint32_t kFix = 32;    // its entry came from a fix-up task (checked like kSpec)
 constexpr std::uint32_t kGiantHop = 64;  // the chain leaves it in a record longer than kMedMax (passed over)
+constexpr std::uint32_t kFakeHop = 128;  // ... over more than kTrustHop regions from an implausible header
+constexpr std::uint64_t kFakeHopBit = 1ull << 63;  // a failing boundary's exit (inc_x) from such a region
 // kinds of fold range: the bytes in front of the region's entry (part of the record the chain is in
 // when it enters; crc0), a payload wholly inside the region (initial register injected, checked here),
 // the head of a payload that goes on past the region (initial register injected; finished by wal_fin_*)
@@ -730,6 +732,11 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
         ghop = hop_giant;
       }
       if (ghop) flags |= kGiantHop;
+      // A hop over more than kTrustHop regions from a header the encoder could not have written (a fake
+      // chain reading a random record_len): see the pass-over below.
+      const bool fake_hop = ghop && Lr != kNo && Xout / kRegion > static_cast<P>(rr) + 1u + kTrustHop &&
+                            !plausible_at(win, rs, o, Lr);
+      if (fake_hop) flags |= kFakeHop;
       if constexpr (FIXUP) {
         // converged: the next region's stored chain enters where this one leaves
         if (rr + 1u >= limit || (flags & (kBroke | kEnd)) || !(flags & kChain)) {
@@ -761,13 +768,13 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
         const std::uint32_t qr = static_cast<std::uint32_t>(next_e / kRegion);
         const std::uint32_t q = next_e >= size || qr > limit ? limit : qr;
         if (q > rr + 1u && (next_e >= size || ghop)) {
-          // A hop over more than kTrustHop regions from a header the encoder could not have written (a
-          // fake chain reading a random record_len) is not passed over: the regions behind it are walked
-          // from their own searches, and the boundary check takes the hop's landing like a chunk's (a fix-up from
-          // there, whose entry lies past its first region, passes over). In a fix-up task too: one that
-          // started from a fake exit would otherwise store its landing in every region it jumps, and the
-          // true chain's task could not meet a stored entry again before its limit.
-          if (Lr != kNo && next_e < size && qr > rr + 1u + kTrustHop && !plausible_at(win, rs, o, Lr)) {
+          // A fake hop (kFakeHop) is not passed over: the regions behind it are walked from their own
+          // searches, and the boundary check takes the hop's landing like a chunk's (its fix-up task waits
+          // until it is the first failing boundary, whose exit is on the true chain; that task, whose entry
+          // lies past its first region, passes over). In a fix-up task too: one that started from a fake
+          // exit would otherwise store its landing in every region it jumps, and the true chain's task
+          // could not meet a stored entry again before its limit.
+          if (fake_hop && next_e < size) {
             e = kNo;
             spec_next = kSpec;
             return rr + 1u;
@@ -931,7 +938,7 @@ __device__ void bounds_one(const SweepArgs& a, std::uint64_t p, std::uint32_t* i
     const unsigned long long i = atomicAdd(&a.res[kResIncons], 1ull);
     if (i < cap) {
       inc_p[i] = static_cast<std::uint32_t>(p);
-      inc_x[i] = x;
+      inc_x[i] = x | ((f & kFakeHop) ? kFakeHopBit : 0ull);
     }
   }
 }
@@ -1316,6 +1323,7 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
       WAL_HIP(hipMemcpyAsync(s.h_inc_p, s.inc_p, ninc * 4, hipMemcpyDeviceToHost, st));
       WAL_HIP(hipMemcpyAsync(s.h_inc_x, s.inc_x, ninc * 8, hipMemcpyDeviceToHost, st));
       WAL_HIP(hipStreamSynchronize(st));
+      // failing boundaries (p, exit X; bit 63 of X: p's exit is a fake hop), in region order
       std::vector<std::pair<std::uint32_t, std::uint64_t>> v(ninc);
       for (std::uint64_t i = 0; i < ninc; ++i) v[i] = {s.h_inc_p[i], s.h_inc_x[i]};
       std::sort(v.begin(), v.end());
@@ -1326,22 +1334,34 @@ int verify_locked(WalScratch& s, const std::uint8_t* w, std::uint64_t size, std:
         v.insert(v.begin(), {p0, x0});
         v.resize(std::min<std::size_t>(v.size(), kMaxFix));
       }
+      std::vector<bool> fake(v.size());
+      for (std::size_t k = 0; k < v.size(); ++k) {
+        fake[k] = (v[k].second & kFakeHopBit) != 0;
+        v[k].second &= ~kFakeHopBit;
+      }
       // Tasks. The first failing boundary's exit is on the true chain (every boundary before it holds,
       // back to region 0): its task runs up to the first boundary past the record it lands in (the
       // ones inside that jump are covered by it). Every later boundary gets a task up to the next one
-      // (disjoint ranges: no two tasks write one region) unless its exit lies past that range: such an
-      // exit is most likely a fake chain's long jump, and its task would only pass a stretch of
-      // regions over, round after round; it waits until it is the first failing boundary.
+      // (disjoint ranges: no two tasks write one region) unless its exit lies past that range, or is a
+      // fake hop (a random record_len read from an implausible header): such a task would pass a stretch
+      // of regions over and store its landing in each, which the true chain's task must then walk again
+      // region by region (1 GiB of record-valued records: 137 ms against 3.3); it waits until it is the
+      // first failing boundary.
       std::vector<std::pair<std::uint32_t, std::uint64_t>> bnd;  // boundaries whose ranges are taken
+      std::vector<bool> bfake;
       const std::uint64_t reach0 = v[0].second / kRegion;
       bnd.push_back(v[0]);
+      bfake.push_back(fake[0]);
       for (std::size_t k = 1; k < v.size(); ++k)
-        if (static_cast<std::uint64_t>(v[k].first) + 1 > reach0) bnd.push_back(v[k]);
+        if (static_cast<std::uint64_t>(v[k].first) + 1 > reach0) {
+          bnd.push_back(v[k]);
+          bfake.push_back(fake[k]);
+        }
       std::vector<std::pair<std::uint32_t, std::uint64_t>> kept;
       std::vector<std::uint32_t> kept_lim;
       for (std::size_t k = 0; k < bnd.size(); ++k) {
         const std::uint32_t lim = k + 1 < bnd.size() ? bnd[k + 1].first + 1 : nreg;
-        if (k > 0 && (bnd[k].second / kRegion >= lim || bnd[k].second / kRegion > bnd[k].first + 1u + kTrustHop)) continue;
+        if (k > 0 && (bnd[k].second / kRegion >= lim || bfake[k])) continue;
         kept.push_back(bnd[k]);
         kept_lim.push_back(lim);
       }

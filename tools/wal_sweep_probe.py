@@ -2,7 +2,7 @@
 """Probe (not product code): the device WAL verify on the 1 GiB image of small records and the 430 MB
 Zipf image (tools/ab_wal.py's images), timed per call, for rocprofv3 kernel traces of its kernels.
 
-    python tools/wal_sweep_probe.py [lib.so] [--reps 10] [--image small|zipf|both|adv]
+    python tools/wal_sweep_probe.py [lib.so] [--reps 10] [--image small|zipf|both|adv|advgiant]
 """
 import argparse
 import ctypes
@@ -21,13 +21,17 @@ from ab_wal import image  # noqa: E402
 VP, U64 = ctypes.c_void_p, ctypes.c_uint64
 
 
-def adversarial(rng, target=1 << 30):
+def adversarial(rng, target=1 << 30, giant=0.0):
     """Zipf values (|v| = min(48 zipf(1.6), 16000)), every value a run of well-formed 40-byte records
     (tests/test_gpu_wal_device.py::test_values_made_of_records at 1 GiB): every chunk and search start
-    inside a value lands on a fake chain."""
+    inside a value lands on a fake chain. giant: the share of values given 1-4 MiB (also runs of fake
+    records), so that most chunk boundaries fall inside a giant record."""
     n = int(target / 300)
     klen = rng.integers(0, 40, n).astype(np.uint32)
     vlen = np.minimum(rng.zipf(1.6, n) * 48, 16000).astype(np.uint32)
+    if giant:
+        g = rng.random(n) < giant
+        vlen[g] = rng.integers(1 << 20, 4 << 20, int(g.sum())).astype(np.uint32)
     size = 26 + klen.astype(np.uint64) + vlen
     n = int(np.searchsorted(np.cumsum(size), target))
     klen, vlen, size = klen[:n], vlen[:n], size[:n]
@@ -70,6 +74,8 @@ def main():
                                                   rng.integers(0, 40, n).astype(np.uint32), rng)))
     if args.image == "adv":
         imgs.append(("values made of records 1 GiB", adversarial(rng)))
+    if args.image == "advgiant":
+        imgs.append(("values made of records, 0.1 % of 1-4 MiB, 1 GiB", adversarial(rng, giant=0.001)))
     if args.image in ("zipf", "both"):
         n2 = 400_000
         imgs.append(("zipf 430 MB", image(n2, rng.integers(8, 64, n2).astype(np.uint32),
