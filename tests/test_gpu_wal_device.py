@@ -230,15 +230,39 @@ def test_values_made_of_records(gpu, oracle):
     rounds = wal_rounds()
     print("values made of records:", LAST, rounds)
     device_walk_only(max_passes=10 ** 6)
-    # bounded recovery: a fake chain that breaks where its value ends is walked again
-    # from the next plausible header, so chunk entries settle within a few regions: a handful of fix-up
-    # rounds, no fix-up task walks thousands of regions in sequence
+    # bounded recovery: chunk entries settle within a few regions, a handful of
+    # fix-up rounds, no fix-up task walks thousands of regions in sequence
     assert len(rounds) <= 4 and max(r["walk_max"] for r in rounds) <= 64, rounds
     o = int(offs[59000]) + 30
     img[o] ^= 0x40
     want = sequential_decode(oracle, img, n)
     assert both(img, n) == (want, want)
     device_walk_only(max_passes=10 ** 6)
+
+
+def test_giant_values_made_of_records(gpu, oracle):
+    """Forty 3-9 MiB values that are runs of well-formed records among 20 K record-valued records: chunk
+    boundaries fall inside giant records whose hops are true, while the fake chains inside them hop on
+    random record_len fields. Only a fake hop's fix-up task waits for its turn (kFakeHop): the device
+    settles in a few rounds with no host walk and no task walking thousands of regions, clean and with a
+    corruption past the giant records."""
+    rng = np.random.default_rng(13)
+    giant = tuple(int(g) for g in np.sort(rng.choice(np.arange(100, 19000), 40, replace=False)))
+    img, offs, size = make_wal(rng, 20000, vmax=4000, giant=giant, fake_headers=1.0)
+    n = img.size
+    want = sequential_decode(oracle, img, n)
+    assert want == ("ok", offs.size, n)
+    assert both(img, n) == (want, want)
+    rounds = wal_rounds()
+    print("giant values made of records:", LAST, rounds)
+    device_walk_only(max_passes=16)
+    assert max(r["walk_max"] for r in rounds) <= 4096, rounds
+    o = int(offs[19500]) + 30
+    img[o] ^= 0x40
+    want = sequential_decode(oracle, img, n)
+    assert want[0] == "corrupted"
+    assert both(img, n) == (want, want)
+    device_walk_only(max_passes=16)
 
 
 @pytest.mark.parametrize("plen", [0, 1, 17, 18, 239, 240, 241, 3000, 7168, 7200, 20000, 65536, 65537, 100000])
