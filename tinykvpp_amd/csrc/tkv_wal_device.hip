@@ -68,7 +68,6 @@ constexpr std::uint32_t kChunk = 112;     // bytes per lane of a range fold
 static_assert(kRegion <= 64 * kChunk && kChunk <= kLaneFold, "a whole region is one round of chunks");
 static_assert(2 * kList >= 2 * ((kRegion / 26 + 2) & ~1u) + 12, "the carry range fits behind a full list");
 constexpr std::uint32_t kStore = kPiece / 26 + 2;  // starts a lane lists: its records up to the first tiny one
-constexpr std::uint32_t kSearchStep = 48;       // positions a lane tests per search step
 constexpr unsigned kSweepWaves = 12;            // waves per workgroup: the 64 KiB tables + 12 windows of LDS
 constexpr unsigned kSweepThreads = 64 * kSweepWaves;
 constexpr unsigned kHres = 16;                  // words of the pinned result block
@@ -191,35 +190,38 @@ __device__ __forceinline__ std::uint32_t lane_prefix(std::uint32_t v, std::uint3
 }
 
 
-// The first plausible header in [ps, qe) (qe - ps <= kSearchStep; every position there has 26 bytes
-// in the image): op and tombstone bytes (p+8, p+17) 0 or 1, then record_len = 18 + klen + vlen and
-// record_len + 8 within the image. Byte-parallel over the 76 window bytes from the 16-byte granule of
-// ps + 8 (five 16-byte reads): z marks each byte that is 0 or 1 (bit 7), c = z & (z 9 bytes on)
-// marks the positions passing both, and the c of four dwords are packed into one word per 16
-// positions, transposed (bit 8 j + i = byte j of dword i; 4 shifts and 2 ORs, no multiply). ps + 8 is
-// at the same granule offset sh in every lane (pieces and steps are multiples of 16 bytes), so the
-// mask of the positions in front of it is wave-uniform. Candidates are taken in position order and
-// checked in full.
-static_assert(kPiece % 16 == 0 && kSearchStep % 16 == 0 && kSearchStep + 15 + 9 < 80, "search granules");
-template <typename P>
+// The first plausible header in [ps, qe) (qe - ps <= 16 NG - 16: a whole piece at NG = 8; every
+// position there has 26 bytes in the image): op and tombstone bytes (p+8, p+17) 0 or 1, then
+// record_len = 18 + klen + vlen and record_len + 8 within the image. Byte-parallel over the window
+// bytes from the 16-byte granule of ps + 8 (NG + 1 16-byte reads): z marks each byte that is 0 or 1
+// (bit 7), c = z & (z 9 bytes on) marks the positions passing both, and the c of four dwords are packed
+// into one word per 16 positions, transposed (bit 8 j + i = byte j of dword i; 4 shifts and 2 ORs, no
+// multiply). ps + 8 is at the same granule offset sh in every lane (pieces are multiples of 16 bytes),
+// so the mask of the positions in front of it is wave-uniform. Candidates are taken in position order
+// and checked in full. One call covers a whole piece: searching it 48 positions at a time cost the
+// wave a second step whenever any lane's first header lay further in (almost every region of small
+// records) and three in every region inside a long payload.
+static_assert(kPiece % 16 == 0 && kPiece + 15 + 9 < 16 * 9, "a piece's search fits nine granules");
+template <typename P, int NG>
 __device__ __forceinline__ P search_piece(const std::uint8_t* win, P rs, std::uint32_t o, P ps, P qe, P size) {
+  static_assert(NG % 2 == 0, "groups of 16 positions in pairs (64-bit masks)");
   if (ps >= qe) return kNoneP<P>;
   const std::uint32_t b0 = static_cast<std::uint32_t>(ps - rs) + o + 8u;
   const std::uint32_t a16 = b0 & ~15u;
   const std::uint32_t sh = __builtin_amdgcn_readfirstlane(b0 & 15u);
   const uint4* g = reinterpret_cast<const uint4*>(win + a16);
-  std::uint32_t z[20];
+  std::uint32_t z[4 * (NG + 1)];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
+  for (int i = 0; i <= NG; ++i) {
     const uint4 v = g[i];
     z[4 * i] = le1_marks(v.x);
     z[4 * i + 1] = le1_marks(v.y);
     z[4 * i + 2] = le1_marks(v.z);
     z[4 * i + 3] = le1_marks(v.w);
   }
-  std::uint32_t y[4];
+  std::uint32_t y[NG];
 #pragma unroll
-  for (int gi = 0; gi < 4; ++gi) {
+  for (int gi = 0; gi < NG; ++gi) {
     std::uint32_t c[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -231,14 +233,24 @@ __device__ __forceinline__ P search_piece(const std::uint8_t* win, P rs, std::ui
   // positions p = 4 i + j < sh of the first group (wave-uniform)
   const std::uint32_t si = sh >> 2, sj = sh & 3u;
   y[0] &= ((0xFu << (si + 1u)) & 0xFu) * 0x01010101u | ((0x01010101u << (8u * sj)) << si);
-  const std::uint32_t span = static_cast<std::uint32_t>(qe - ps);  // <= kSearchStep
-  std::uint64_t m0 = y[0] | static_cast<std::uint64_t>(y[1]) << 32, m1 = y[2] | static_cast<std::uint64_t>(y[3]) << 32;
-  while (m0 | m1) {
-    const bool lo = m0 != 0;
-    const std::uint64_t cur = lo ? m0 : m1;
+  const std::uint32_t span = static_cast<std::uint32_t>(qe - ps);
+  std::uint64_t m[NG / 2];
+#pragma unroll
+  for (int k = 0; k < NG / 2; ++k) m[k] = y[2 * k] | static_cast<std::uint64_t>(y[2 * k + 1]) << 32;
+  for (;;) {
+    std::uint64_t cur = 0;
+    std::uint32_t sel = 0;
+#pragma unroll
+    for (int k = NG / 2 - 1; k >= 0; --k) {  // the first non-empty pair
+      if (m[k] != 0) {
+        cur = m[k];
+        sel = static_cast<std::uint32_t>(k);
+      }
+    }
+    if (cur == 0) break;
     const bool hw = static_cast<std::uint32_t>(cur) == 0u;
     const std::uint32_t yv = hw ? static_cast<std::uint32_t>(cur >> 32) : static_cast<std::uint32_t>(cur);
-    const std::uint32_t gi = (lo ? 0u : 2u) + (hw ? 1u : 0u);
+    const std::uint32_t gi = 2u * sel + (hw ? 1u : 0u);
     const std::uint32_t i = static_cast<std::uint32_t>(__builtin_ctz((yv | yv >> 8 | yv >> 16 | yv >> 24) & 0xFu));
     const std::uint32_t j = static_cast<std::uint32_t>(__builtin_ctz((yv >> i) & 0x01010101u)) >> 3;
     const std::uint32_t pos = 16u * gi + 4u * i + j - sh;  // from ps
@@ -248,7 +260,9 @@ __device__ __forceinline__ P search_piece(const std::uint8_t* win, P rs, std::ui
     const P q = ps + pos;
     if (rl == 18u + kl + vl && static_cast<P>(rl) <= size - q - 8u) return q;  // (size - q >= 26)
     const std::uint64_t bit = 1ull << ((hw ? 32u : 0u) + 8u * j + i);
-    if (lo) m0 &= ~bit; else m1 &= ~bit;
+#pragma unroll
+    for (int k = 0; k < NG / 2; ++k)
+      if (static_cast<std::uint32_t>(k) == sel) m[k] &= ~bit;
   }
   return kNoneP<P>;
 }
@@ -532,16 +546,9 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
         const std::uint32_t le = exact ? static_cast<std::uint32_t>((e - rs) / kPiece) : 0u;
         P s = kNo;
         if (exact && lane == le) s = e;
-        // the piece's first plausible header, kSearchStep positions at a time from its front (the first
-        // step finds it in a WAL of small records; a piece inside a long payload is searched whole)
+        // the piece's first plausible header (the whole piece in one search)
         const P qend = size >= kWalMeta ? std::min<P>(pe, size - static_cast<P>(kWalMeta) + 1u) : 0u;
-        bool hunt = (!exact || lane > le) && ps < qend;
-        for (P q0 = ps; __ballot(hunt) != 0; q0 += kSearchStep) {
-          if (hunt) {
-            s = search_piece<P>(win, rs, o, q0, std::min<P>(q0 + kSearchStep, qend), size);
-            hunt = s == kNo && q0 + kSearchStep < qend;
-          }
-        }
+        if ((!exact || lane > le) && ps < qend) s = search_piece<P, 8>(win, rs, o, ps, qend, size);
         Walk<P> wk;
         walk_piece(win, rs, o, s, pe, size, true, wk);
         // ---- 2. link check ---------------------------------------------------------------------------
