@@ -173,20 +173,22 @@ __device__ __forceinline__ std::uint32_t readlane_pos(std::uint32_t v, std::uint
 }
 __device__ __forceinline__ std::uint64_t readlane_pos(std::uint64_t v, std::uint32_t l) { return dev::readlane64(v, l); }
 
-// Exclusive prefix over the lanes of a value < 2^BITS, and its total (bit planes through ballots).
-template <int BITS>
+// Exclusive prefix sum over the 64 lanes (all active), and its total: an inclusive scan by DPP row
+// shifts within rows of 16, then the row totals broadcast into the rows above (row_bcast:15 / :31).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ std::uint32_t dpp_add(std::uint32_t x) {
+  return x + static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), CTRL, ROW_MASK, 0xF, false));
+}
 __device__ __forceinline__ std::uint32_t lane_prefix(std::uint32_t v, std::uint32_t* total) {
-  std::uint32_t pre = 0, tot = 0;
-#pragma unroll
-  for (int bit = 0; bit < BITS; ++bit) {
-    const std::uint64_t m = __ballot((v >> bit) & 1u);
-    pre += static_cast<std::uint32_t>(__builtin_amdgcn_mbcnt_hi(static_cast<std::uint32_t>(m >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<std::uint32_t>(m), 0u)))
-           << bit;
-    tot += static_cast<std::uint32_t>(__builtin_popcountll(m)) << bit;
-  }
-  *total = tot;
-  return pre;
+  std::uint32_t x = v;
+  x = dpp_add<0x111, 0xF>(x);  // row_shr:1
+  x = dpp_add<0x112, 0xF>(x);  // row_shr:2
+  x = dpp_add<0x114, 0xF>(x);  // row_shr:4
+  x = dpp_add<0x118, 0xF>(x);  // row_shr:8
+  x = dpp_add<0x142, 0xA>(x);  // row_bcast:15 into rows 1 and 3
+  x = dpp_add<0x143, 0xC>(x);  // row_bcast:31 into rows 2 and 3
+  *total = static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
+  return x - v;
 }
 
 
@@ -408,7 +410,7 @@ __device__ __forceinline__ void fold_ranges(const std::uint8_t* win, const std::
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   std::uint32_t total;
-  const std::uint32_t pre = lane_prefix<7>(ci, &total);  // (ci <= 64)
+  const std::uint32_t pre = lane_prefix(ci, &total);
   for (std::uint32_t base = 0; base < total; base += 64u) {
     const std::uint32_t g = base + lane;
     const bool act = g < total;
@@ -600,11 +602,11 @@ __device__ __forceinline__ void sweep_wave(const SweepArgs& a, std::uint8_t* win
           Lr = readlane_pos(wk.lr, last);
           // ---- 3. list and fold ------------------------------------------------------------------------
           const bool on = (C >> lane) & 1ull;
-          (void)lane_prefix<kPiece / 8 < 32 ? 5 : 6>(on ? wk.n : 0u, &count);  // every chain record
+          (void)lane_prefix(on ? wk.n : 0u, &count);  // every chain record
           // listed: each lane's records up to its first tiny one (all stored), in chain order
           const std::uint32_t nn = on ? std::min<std::uint32_t>(wk.n, wk.tiny == kStore ? kStore : wk.tiny + 1u) : 0u;
           std::uint32_t nlist;
-          const std::uint32_t pre = lane_prefix<4>(nn, &nlist);
+          const std::uint32_t pre = lane_prefix(nn, &nlist);
           const std::uint32_t t = on && wk.tiny < nn ? pre + wk.tiny : 0xFFFFFFFFu;
           const std::uint32_t tmin = dev::wave_min(t);
           const std::uint32_t nl = std::min<std::uint32_t>(std::min<std::uint32_t>(nlist, tmin == 0xFFFFFFFFu ? nlist : tmin + 1u), kList);
