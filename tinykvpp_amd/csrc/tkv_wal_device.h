@@ -8,19 +8,12 @@
 
 namespace tkv {
 
-// One pass of the device verify over an image that starts with a record (tkv_wal_device.hip).
-struct PassResult {
-  std::uint64_t good = 0;  // records verified good from the pass's start
-  std::uint64_t stop = 0;  // where decoding stopped (relative to the pass's start)
-  bool corrupted = false;
-  bool resume = false;     // the chain continues at `stop` (a true record start) beyond what was checked
-};
-
-
-// Verify the WAL image [d_wal, d_wal + size) in device memory on `st` (synchronous): the record
-// chain walked on the device, one CRC batch, the first bad record. Same results as tkv_wal_verify.
-// *needs_host_walk is set (and nothing else is decided) when the speculative walk could not settle
-// the chain within its pass budget; the caller then runs the exact host walk.
+// Verify the WAL image [d_wal, d_wal + size) in device memory on `st` (synchronous): one sweep that
+// walks the record chain and folds every payload of at most 64 KiB, device fix-up rounds where a
+// chunk's speculative entry was wrong, one CRC batch for longer payloads, the first bad record. Same
+// results as tkv_wal_verify. *needs_host_walk is set (and nothing else is decided) when the fix-up
+// rounds have not settled the chain within their budget (kRoundBudget); the caller then runs the
+// exact host walk.
 int wal_verify_device_impl(const std::uint8_t* d_wal, std::uint64_t size, std::uint64_t* n_good,
                            std::uint64_t* stop_offset, hipStream_t st, bool* needs_host_walk);
 
