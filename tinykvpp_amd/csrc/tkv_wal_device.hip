@@ -1093,12 +1093,13 @@ __global__ __launch_bounds__(512) void wal_finish(SweepArgs a, const std::uint32
 #pragma unroll
   for (int m = 32; m > 0; m >>= 1) c += static_cast<std::uint64_t>(__shfl_xor(static_cast<long long>(c), m, 64));
   if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = c;
+  __threadfence();  // every wave's Lidx exchange done and visible before the block counts itself in
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long s = 0;
     for (unsigned k = 0; k < blockDim.x / 64u; ++k) s += part[k];
     if (s) atomicAdd(&a.res[kResCnt], s);
-    __threadfence();  // (this block's words, the Lidx exchanges included, before its count)
+    __threadfence();
     last = atomicAdd(&a.res[kResDone], 1ull) == gridDim.x - 1u;
   }
   __syncthreads();
