@@ -339,8 +339,10 @@ def bit_exact_paths(dev, ora, quick=False):
     each against the oracle (oracle/liboracle.so: Sarwate CRC, the sequential WAL decode of
     wal.cpp:63-130, the WAL stamp of wal.cpp:54-58, the SSTable stamp) on seeded synthetic inputs:
       list_lanes_one_pass   >= 1 M gapped 26-59 B WAL payloads through tkv_crc32_batch_device (the
-                            one-pass crc_list_lanes kernel: the general path publishes no phase)
-      list_lanes_fall_through  the same batch with one 65 B block near its end (the general path)
+                            one-pass crc_list_lanes kernel; tkv_debug_irregular_path 0)
+      list_pack_one_pass    the same batch with one 65 B block near its end (crc_list_lanes hands it
+                            on, the one-pass crc_list_pack kernel folds it: path 1)
+      list_lanes_fall_through  the same batch with one 1025 B block (the general path: path 2)
       crc32c_list_lanes     the one-pass batch under CRC-32C (sampled against the oracle)
       wal_verify_device_*   tkv_wal_verify_device on small-record, Zipf and values-made-of-records
                             images, clean and with one flipped payload byte: same (status, records
@@ -377,19 +379,22 @@ def bit_exact_paths(dev, ora, quick=False):
     offs = 3 + 8 + np.concatenate([[0], np.cumsum(lens[:-1] + 8)])  # an 8-byte record prefix before each
     host = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
     d = torch.from_numpy(host).to(dev)
-    for name, tweak in (("list_lanes_one_pass", None), ("list_lanes_fall_through", nb - 5)):
+    for name, tweak, want_path in (("list_lanes_one_pass", None, 0), ("list_pack_one_pass", (nb - 5, 65), 1),
+                                   ("list_lanes_fall_through", (nb - 40, 1025), 2)):
         ln = lens.copy()
         if tweak is not None:
-            ln[tweak] = 65
+            ln[tweak[0]] = tweak[1]
         o, l32 = torch.from_numpy(offs).to(dev), torch.from_numpy(ln.astype(np.int32)).to(dev)
         got = u32(tk.crc32_batch(d, o, l32))
+        kp = lib.tkv_debug_irregular_path(st)
         ph = lib.tkv_debug_irregular_phases(st)
         want = np.zeros(nb, np.uint32)
         o64, l32h = offs.astype(np.uint64), ln.astype(np.uint32)  # (named: alive across the call)
         ora.oracle_crc_batch(host.ctypes.data, o64.ctypes.data, l32h.ctypes.data, None, nb, want.ctypes.data)
-        path_ok = ph == (0 if tweak is None else 1)
+        path_ok = kp == want_path and (ph == 0) == (want_path != 2)
         res[name] = {"ok": bool(np.array_equal(got, want)) and path_ok, "blocks": nb, "mismatches":
-                     int((got != want).sum()), "general_path_phases": int(ph), "path_as_expected": path_ok}
+                     int((got != want).sum()), "kernel_path": int(kp), "general_path_phases": int(ph),
+                     "path_as_expected": path_ok}
         if tweak is None:
             gc = u32(tk.crc32_batch(d, o, l32, algo="crc32c"))
             smp = rng.choice(nb, 4000 if quick else 20000, replace=False)

@@ -287,6 +287,11 @@ int tkv_debug_irregular_mode(void *stream);
  * mode): bit 0 the lane phase (blocks <= 64 B), bits 1 / 2 the 4- / 8-lane group passes (65-256 /
  * 257-512 B); -1 on error. Synchronizes the stream. */
 int tkv_debug_irregular_phases(void *stream);
+/* Which kernel folded the last irregular batch on `stream`: 0 = the one-pass lane kernel
+ * (crc_list_lanes: every block <= 64 B), 1 = the one-pass packed kernel (crc_list_pack: every block
+ * <= 1 KiB), 2 = the general path after both handed it on, 3 = the general path alone (fewer than
+ * 1 M blocks, or per-block initial registers); -1 on error. Synchronizes the stream. */
+int tkv_debug_irregular_path(void *stream);
 /* Waves of the one-pass lane kernel (crc_list_lanes) for an irregular batch of nblocks on the current
  * device: wave w takes its 64-block steps [w TS / W, (w + 1) TS / W), TS = ceil(nblocks / 64). 0 when
  * no device is usable. */

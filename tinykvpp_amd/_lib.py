@@ -79,6 +79,7 @@ SIGNATURES = {
     "tkv_debug_update_counts_n": (_sz, [_vp, _sz]),
     "tkv_debug_irregular_mode": (_int, [_vp]),
     "tkv_debug_irregular_phases": (_int, [_vp]),
+    "tkv_debug_irregular_path": (_int, [_vp]),
     "tkv_debug_list_lanes_waves": (ctypes.c_uint32, [ctypes.c_uint64]),
     "tkv_debug_irregular_lists": (_int, [_vp, _vp]),
     "tkv_debug_multi_plan": (_sz, [_int, _vp, _vp, _vp, _u64, _vp, _sz]),

@@ -145,6 +145,24 @@ __device__ __forceinline__ std::uint32_t wave_max(std::uint32_t v) {
   return static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
 }
 
+// Exclusive prefix sum over the 64 lanes (all active), and its total: an inclusive scan by DPP row
+// shifts within rows of 16, then the row totals broadcast into the rows above (row_bcast:15 / :31).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ std::uint32_t dpp_add(std::uint32_t x) {
+  return x + static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), CTRL, ROW_MASK, 0xF, false));
+}
+__device__ __forceinline__ std::uint32_t lane_prefix(std::uint32_t v, std::uint32_t* total) {
+  std::uint32_t x = v;
+  x = dpp_add<0x111, 0xF>(x);  // row_shr:1
+  x = dpp_add<0x112, 0xF>(x);  // row_shr:2
+  x = dpp_add<0x114, 0xF>(x);  // row_shr:4
+  x = dpp_add<0x118, 0xF>(x);  // row_shr:8
+  x = dpp_add<0x142, 0xA>(x);  // row_bcast:15 into rows 1 and 3
+  x = dpp_add<0x143, 0xC>(x);  // row_bcast:31 into rows 2 and 3
+  *total = static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
+  return x - v;
+}
+
 // Minimum of v over the 64 lanes, wave-uniform (as wave_max; lanes past a row's edge read ~0).
 __device__ __forceinline__ std::uint32_t wave_min(std::uint32_t v) {
   v = std::min(v, static_cast<std::uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(v), 0xB1, 0xF, 0xF, false)));

@@ -41,6 +41,7 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
                           const std::uint32_t* gate_flags, hipStream_t st);
 hipError_t launch_stream_rows(const RowsArgs& a, hipStream_t st, unsigned grid);
 hipError_t launch_list_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st);
+hipError_t launch_list_pack(const RowsArgs& a, unsigned ncu, hipStream_t st);
 std::uint32_t list_lanes_waves(std::uint64_t nblocks, unsigned ncu);
 std::uint64_t prepass_tiles(std::uint64_t n);
 hipError_t launch_span(const std::uint8_t* stage, const SpanDesc& one, const SpanDesc* desc, std::uint32_t n,
@@ -185,6 +186,8 @@ struct StreamScratch {
   PrepassOut po{};
   std::uint64_t cap_blocks = 0;
   std::uint32_t gate_seq = 0;  // irregular calls on this stream (crc_list_lanes' gate, counts[kCountGate])
+  bool one_pass = false;       // the last irregular call launched crc_list_lanes
+  bool pack = false;           // ... and crc_list_pack
 };
 
 // Spans up to this size take update()'s latency path (mapped pinned memory, one crc_span launch,
@@ -378,9 +381,9 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->seams), sizeof(Seam) * 2 * c->W));
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->wave_start), sizeof(std::uint32_t) * c->W));
     // counts[0..3], then (u64) the stream-mode info at counts + 4
-    // (crc_list_lanes' per-workgroup flags from word kListFlags on)
-    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->counts), sizeof(std::uint32_t) * (kListFlags + kListMaxGroups)));
-    TKV_HIP(hipMemset(slot->counts, 0, sizeof(std::uint32_t) * (kListFlags + kListMaxGroups)));
+    // (crc_list_lanes' per-workgroup flags from word kListFlags on, crc_list_pack's from kPackFlags)
+    TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->counts), sizeof(std::uint32_t) * kCountWords));
+    TKV_HIP(hipMemset(slot->counts, 0, sizeof(std::uint32_t) * kCountWords));
   }
   StreamScratch* s = slot.get();
   if (nblocks > s->cap_blocks) {
@@ -556,7 +559,9 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   // the whole batch. Smaller batches skip it: the pass costs a batch it hands on ~10 us (2-4 % of a
   // 1 GiB batch of larger blocks, profiles/r5/list_lanes/), more than it saves a short lane-only one.
   // 
-  if (d_init == nullptr && n >= kListMinBlocks) {
+  s->one_pass = d_init == nullptr && n >= kListMinBlocks;
+  s->pack = false;
+  if (s->one_pass) {
     s->gate_seq = s->gate_seq + 1u == 0u ? 1u : s->gate_seq + 1u;
     a.gate = s->counts + kCountGate;
     a.gate_seq = s->gate_seq;
@@ -565,6 +570,14 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
     l.offsets = d_off;
     l.lengths = d_len;
     TKV_HIP(launch_list_lanes(l, static_cast<unsigned>(c->ncu), st));
+    // then crc_list_pack, which folds a batch handed on whose blocks are at most kPackMax bytes; the
+    // general path runs only when it hands the batch on too (its flags open the gate). Not under
+    // tkv_debug_set_stream_groups(1), which keeps the byte-stream walk of such batches under test.
+    if (g_stream_groups.load(std::memory_order_relaxed) == 0) {
+      TKV_HIP(launch_list_pack(l, static_cast<unsigned>(c->ncu), st));
+      a.gate_flags = s->counts + kPackFlags;
+      s->pack = true;
+    }
   }
   TKV_HIP(launch_prepass(d_base, d_off, d_len, a.nblocks, s->scan, s->tiles, s->tile_ok, s->counts, sinfo, s->po.big_off,
                          s->po, a.nwaves, static_cast<std::uint32_t>(c->ncu), d_out, row0,
@@ -1375,6 +1388,24 @@ int read_count_word(void* stream, int word) {
 int tkv_debug_irregular_mode(void* stream) { return read_count_word(stream, 3); }
 
 int tkv_debug_irregular_phases(void* stream) { return read_count_word(stream, kCountPhases); }
+
+int tkv_debug_irregular_path(void* stream) {
+  DevCtx* c = nullptr;
+  if (get_ctx(&c)) return -1;
+  StreamScratch* s = nullptr;
+  if (get_scratch(c, stream, 0, &s)) return -1;
+  if (!s->one_pass) return 3;
+  std::vector<std::uint32_t> f(2 * kListMaxGroups);
+  if (hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess ||
+      hipMemcpy(f.data(), s->counts + kListFlags, 4 * f.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  bool list_on = false, pack_on = false;
+  for (unsigned i = 0; i < kListMaxGroups; ++i) {
+    list_on = list_on || f[i] == s->gate_seq;
+    pack_on = pack_on || f[kListMaxGroups + i] == s->gate_seq;
+  }
+  return !list_on ? 0 : s->pack && !pack_on ? 1 : 2;
+}
 
 uint32_t tkv_debug_list_lanes_waves(uint64_t nblocks) {
   DevCtx* c = nullptr;

@@ -122,6 +122,10 @@ struct RowsArgs {
 constexpr int kCountGate = 12;
 constexpr int kListFlags = 64;
 constexpr unsigned kListMaxGroups = 1024;
+// counts[kPackFlags + g]: crc_list_pack's flags (the same protocol, a block over kPackMax bytes); the
+// tile scan reads these when crc_list_pack ran after crc_list_lanes
+constexpr int kPackFlags = kListFlags + static_cast<int>(kListMaxGroups);
+constexpr int kCountWords = kPackFlags + static_cast<int>(kListMaxGroups);
 __device__ __forceinline__ bool gate_closed(const std::uint32_t* gate, std::uint32_t seq) {
   return gate != nullptr && *gate != seq;
 }

@@ -425,6 +425,227 @@ __global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
   }
 }
 
+// ---- irregular batches of blocks up to 1 KiB in one pass ----------------------------------------------
+// crc_list_pack takes an irregular batch (default initial register) that crc_list_lanes handed on (one
+// of its workgroups met a block over kLaneMax bytes; otherwise every workgroup returns at once) and
+// folds it straight from the caller's (offset, length) arrays when no block is over kPackMax bytes: no
+// prepass, no classes. Wave w takes 64-block chunks [w TS / W, (w + 1) TS / W). A block of len bytes
+// gets k = ceil(len / 64) lanes, packed back to back: the chunk's k are scanned (DPP) into each block's
+// first lane, the block-lanes write their descriptor and a lane -> block map into the wave's LDS, and
+// the chunk's ceil(sum k / 64) substeps each give every lane one 64-byte piece: lane g of k folds the
+// block's bytes [len - 64 (k - g), len - 64 (k - g - 1)) from zero (the bytes in front of the block
+// masked), moves the result to the block's end by Shift_{64 (k - 1 - g)} (nibble tables, one column per
+// shift), and XORs it into the block's LDS accumulator, which the chunk's block-lanes seeded with
+// Shift_len(0xFFFFFFFF) ^ xorout (crc_s(D) = Shift_|D|(s) ^ crc_0(D)); after the chunk's last substep the
+// accumulators are the block CRCs. Against the 4-lane groups of the general path, a substep fills its
+// 64 lanes with pieces whatever the length mix (a 128-byte block takes two lanes, not four) and nothing
+// is read twice: descriptors once, payload granules once per piece (5 granules for 64 bytes), no scan,
+// scatter or class lists.
+// Pipeline: a substep's granules are issued AHEAD substeps before its fold; a chunk is prepared (map,
+// descriptors, accumulators) when its first substep is issued, its descriptors loaded two chunks ahead;
+// four accumulator buffers, so a chunk's fold never meets the seeds of a later one.
+// A block over kPackMax bytes, as in crc_list_lanes: the workgroup stores the call's number in its own
+// flag (counts[kPackFlags + g]), every wave polls the flags and leaves, and the general path (whose
+// tile scan reads these flags) folds the batch.
+constexpr std::uint32_t kPackMax = kSmallMax;         // 16 lanes at most per block
+constexpr unsigned kPackThreads = 1024;
+constexpr unsigned kPackWaves = kPackThreads / 64;
+constexpr std::uint32_t kPackLsp = kLdsSliceWords * 2;    // after the 64 KiB image: shift tables
+constexpr std::uint32_t kPackInj = kPackLsp + 16 * 8 * 32 * 4;  // [16 shifts][8 nibbles][32 slots] words
+constexpr std::uint32_t kPackScratch = kPackInj + 4 * (kPackMax + 4);  // Shift_len(init) ^ xorout
+constexpr std::uint32_t kPackWaveBytes = 3072;        // per wave: desc[64] (16 B), acc[4][64], map[1024]
+constexpr std::uint32_t kPackLdsBytes = kPackScratch + kPackWaves * kPackWaveBytes;
+static_assert(kPackLdsBytes <= 163840, "LDS");
+static_assert(kPackFlags == kListFlags + static_cast<int>(kListMaxGroups), "pack flags follow the list flags");
+
+template <int AHEAD>
+__global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
+  constexpr int R = AHEAD + 1;  // substeps of data in registers
+  __shared__ __attribute__((aligned(16))) std::uint8_t lds[kPackLdsBytes];
+  __shared__ std::uint32_t wg_hit_word;
+  const std::uint32_t seq = a.gate_seq;
+  std::uint32_t* pflags = const_cast<std::uint32_t*>(a.gate_flags) + kListMaxGroups;
+  {
+    // crc_list_lanes (the launch before, same stream) folded the batch unless one of its flags holds seq
+    bool hit = false;
+    for (std::uint32_t i = threadIdx.x; i < kListMaxGroups; i += blockDim.x) hit = hit || a.gate_flags[i] == seq;
+    if (__syncthreads_or(hit ? 1 : 0) == 0) return;
+  }
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t wave = blockIdx.x * kPackWaves + wv;
+  const std::uint64_t W = a.nwaves, n = a.nblocks;
+  const std::uint64_t TS = (n + 63u) / 64u;
+  const std::uint64_t s0 = wave * TS / W;
+  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
+  {
+    // the first chunk's lengths before the table fill: a workgroup that meets a longer block leaves
+    const std::uint64_t b = s0 * 64u + lane;
+    const std::uint32_t len = ns != 0 ? a.lengths[b < n ? b : n - 1u] : 0u;
+    if (__syncthreads_or(ns != 0 && b < n && len > kPackMax ? 1 : 0) != 0) {
+      if (threadIdx.x == 0) __hip_atomic_store(pflags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+  std::uint32_t* tab = reinterpret_cast<std::uint32_t*>(lds);
+  dev::fill_lds_slicing16(a.tabs, tab);
+  // shift tables: word (sh * 8 + j) * 32 + (v | 16 (sh & 1)) = Shift_{64 sh}(v << 4 j) (lane_shift column
+  // 63 - sh); odd shifts in the upper 16 banks, so pieces of one block (consecutive sh) split the banks
+  std::uint32_t* lsp = reinterpret_cast<std::uint32_t*>(lds + kPackLsp);
+  for (std::uint32_t i = threadIdx.x; i < 16u * 8u * 32u; i += blockDim.x) {
+    const std::uint32_t sh = i >> 8, j = (i >> 5) & 7u, s = i & 31u;
+    lsp[i] = (s >> 4) == (sh & 1u) ? a.tabs->lane_shift[j][s & 15u][63u - sh] : 0u;
+  }
+  std::uint32_t* inj = reinterpret_cast<std::uint32_t*>(lds + kPackInj);
+  for (std::uint32_t i = threadIdx.x; i <= kPackMax; i += blockDim.x) inj[i] = a.tabs->init_shift[i] ^ a.out_xor;
+  if (threadIdx.x == 0) wg_hit_word = 0;
+  __syncthreads();
+  if (ns == 0) return;
+
+  std::uint8_t* ws = lds + kPackScratch + wv * kPackWaveBytes;
+  uint4* desc = reinterpret_cast<uint4*>(ws);
+  std::uint32_t* acc = reinterpret_cast<std::uint32_t*>(ws + 1024);
+  std::uint8_t* map = ws + 2048;
+  const dev::LaneConstX kc = dev::lane_const16(lane);
+  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
+  const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
+
+  // descriptors of the next two chunks to prepare (c0: the next one)
+  std::uint64_t c0_off, c1_off;
+  std::uint32_t c0_len, c1_len;
+  auto fetch = [&](std::uint32_t q, std::uint64_t& off, std::uint32_t& len) {
+    const std::uint64_t b = (s0 + q) * 64u + lane;
+    const std::uint64_t bc = b < n ? b : n - 1u;  // clamped: every load stays inside the arrays
+    off = a.offsets[bc];
+    len = a.lengths[bc];
+  };
+  fetch(0, c0_off, c0_len);
+  fetch(1, c1_off, c1_len);
+
+  // wave-uniform cursor: chunk iq, its substep is of nsub, its T lanes of pieces
+  std::uint32_t iq = ~0u, is = 0, nsub = 0, T = 0, quit = 0;
+  std::uint32_t poll = 0;  // polled flags, checked at the next chunk
+  auto wave_fence = [] {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto leave = [&] {
+    if (lane == 0 && atomicExch(&wg_hit_word, 1u) == 0u)
+      __hip_atomic_store(pflags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    quit = 1u;
+  };
+  auto prepare = [&](std::uint32_t q) {
+    const std::uint64_t b = (s0 + q) * 64u + lane;
+    const bool live = b < n;
+    const std::uint32_t len = live ? c0_len : 0u;
+    const std::uint64_t off = c0_off;
+    c0_off = c1_off;
+    c0_len = c1_len;
+    fetch(q + 2u, c1_off, c1_len);
+    // other workgroups' flags: loaded at every eighth chunk, looked at one chunk later
+    if ((q & 7u) == 1u) quit = __builtin_amdgcn_readfirstlane(quit | (__ballot(poll != 0u) != 0 ? 1u : 0u));
+    if ((q & 7u) == 0u) {
+      poll = 0;
+#pragma unroll
+      for (std::uint32_t i = 0; i < kListMaxGroups / 64u; ++i) {
+        const std::uint32_t f = lane + 64u * i;
+        if (i * 64u < gridDim.x && f < gridDim.x)
+          poll |= __hip_atomic_load(pflags + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == seq ? 1u : 0u;
+      }
+    }
+    if (__ballot(len > kPackMax) != 0) leave();
+    if (quit != 0u) return;
+    const std::uint32_t k = (len + 63u) >> 6;
+    std::uint32_t total;
+    const std::uint32_t ex = dev::lane_prefix(k, &total);
+    wave_fence();  // the previous chunk's map and descriptor reads are done
+    desc[lane] = make_uint4(static_cast<std::uint32_t>(off), static_cast<std::uint32_t>(off >> 32), len, ex);
+    for (std::uint32_t r = 0; __ballot(r < k) != 0; ++r)
+      if (r < k) map[ex + r] = static_cast<std::uint8_t>(lane);
+    acc[(q & 3u) * 64u + lane] = inj[len];
+    wave_fence();
+    T = total;
+    nsub = total == 0u ? 1u : (total + 63u) >> 6;
+  };
+
+  uint4 qv[R][dev::kLaneGran];
+  std::uint32_t m_o[R], m_sh[R], m_acc[R];
+  std::int32_t m_lead[R];
+  std::uint32_t m_last[R];  // wave-uniform: 1 + the chunk whose last substep this is, else 0
+  bool m_dead[R];           // wave-uniform: past the wave's last substep
+  auto issue = [&](int slot) {
+    if (is == nsub && quit == 0u) {
+      ++iq;
+      is = 0;
+      if (iq < ns) prepare(iq);
+    }
+    m_dead[slot] = iq >= ns || quit != 0u;
+    if (m_dead[slot]) return;
+    const std::uint32_t v = 64u * is + lane;
+    const bool live = v < T;
+    const std::uint32_t blk = live ? map[v] : 0u;
+    const uint4 d = desc[blk];
+    const std::uint32_t len = live ? d.z : 0u;
+    const std::uint32_t g = v - d.w;  // this lane's piece of the block
+    const std::uint32_t k = (len + 63u) >> 6;
+    const std::int32_t c_lane = static_cast<std::int32_t>(len) - 64 * static_cast<std::int32_t>(k - g);
+    const std::uintptr_t blo = base + (static_cast<std::uint64_t>(d.y) << 32 | d.x), bhi = blo + len;
+    const std::uintptr_t p = static_cast<std::uintptr_t>(static_cast<std::int64_t>(blo) + c_lane);
+    const std::uintptr_t al = p & ~static_cast<std::uintptr_t>(15);
+#pragma unroll
+    for (int i = 0; i < dev::kLaneGran; ++i) {
+      const std::uintptr_t gp = al + 16u * i;
+      qv[slot][i] = dev::gload16(live && gp + 16u > blo && gp < bhi ? gp : dmy);
+    }
+    m_o[slot] = static_cast<std::uint32_t>(p & 15u);
+    m_lead[slot] = live ? -c_lane : 64;  // bytes of the piece in front of the block (64: none of it)
+    m_sh[slot] = live ? k - 1u - g : 0u;
+    m_acc[slot] = live ? (iq & 3u) * 64u + blk : ~0u;
+    m_last[slot] = is + 1u == nsub ? iq + 1u : 0u;
+    ++is;
+  };
+  auto fold = [&](int slot) {
+    std::uint32_t d[16];
+    dev::lane_dwords<1>(qv[slot], m_o[slot], d);
+    const std::int32_t lead = m_lead[slot];
+    dev::Reg r{0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const std::int32_t before = lead - 4 * k;
+      const std::uint32_t shb = static_cast<std::uint32_t>(before < 0 ? 0 : (before > 4 ? 4 : before)) * 8u;
+      dev::slice4(tab, r, d[k] & static_cast<std::uint32_t>(0xFFFFFFFFull << shb), kc);
+    }
+    const std::uint32_t p = r.value();
+    const std::uint32_t sh = m_sh[slot];
+    const std::uint32_t lb = kPackLsp + sh * 1024u + ((sh & 1u) << 6);
+    std::uint32_t l[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) l[j] = dev::lds_at(tab, lb + 128u * j + (((p >> (4 * j)) & 15u) << 2));
+    const std::uint32_t v = dev::xor3(dev::xor3(l[0], l[1], l[2]), dev::xor3(l[3], l[4], l[5]), l[6] ^ l[7]);
+    if (m_acc[slot] != ~0u) __hip_atomic_fetch_xor(acc + m_acc[slot], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (m_last[slot] != 0u) {
+      const std::uint32_t q = m_last[slot] - 1u;
+      wave_fence();
+      const std::uint64_t b = (s0 + q) * 64u + lane;
+      const std::uint32_t crc = acc[(q & 3u) * 64u + lane];
+      if (b < n) a.out[b] = crc;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < AHEAD; ++k) issue(k);
+  for (bool done = false; !done;) {
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      issue((k + AHEAD) % R);
+      if (m_dead[k]) {
+        done = true;
+        break;
+      }
+      fold(k);
+    }
+  }
+}
+
 
 
 }  // namespace
@@ -1311,6 +1532,21 @@ hipError_t launch_list_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   b.nwaves = list_lanes_waves(a.nblocks, ncu);
   const std::uint64_t grid = b.nwaves / kListWaves;
   hipLaunchKernelGGL(crc_list_lanes, dim3(static_cast<unsigned>(grid)), dim3(kListThreads), 0, st, b);
+  return hipGetLastError();
+}
+
+// One-pass packed kernel of an irregular batch that crc_list_lanes handed on: see crc_list_pack. Its
+// workgroups return at once when crc_list_lanes folded the batch.
+#ifndef TKV_PACK_AHEAD
+#define TKV_PACK_AHEAD 1
+#endif
+hipError_t launch_list_pack(const RowsArgs& a, unsigned ncu, hipStream_t st) {
+  RowsArgs b = a;
+  const std::uint64_t chunks = (a.nblocks + 63u) / 64u;
+  const std::uint64_t grid = std::max<std::uint64_t>(
+      1, std::min<std::uint64_t>(std::min<std::uint64_t>(ncu, kListMaxGroups), (chunks + kPackWaves - 1) / kPackWaves));
+  b.nwaves = static_cast<std::uint32_t>(grid * kPackWaves);
+  hipLaunchKernelGGL(crc_list_pack<TKV_PACK_AHEAD>, dim3(static_cast<unsigned>(grid)), dim3(kPackThreads), 0, st, b);
   return hipGetLastError();
 }
 
