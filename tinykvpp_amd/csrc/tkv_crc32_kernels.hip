@@ -248,6 +248,23 @@ __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 // call's sequence number into the workgroup's flag, every wave polls the flags every 4 step groups and
 // leaves, and the general path then folds the whole batch (rows_tile_scan opens the gate from the
 // flags).
+// The per-workgroup flags of a one-pass kernel, polled by every wave: next() issues this lane's load of
+// flag lane + 64 g (g taking the ceil(groups / 64) groups in turn, clamped to the last flag) and returns
+// whether the load issued at the previous call found the call's number (seq is never 0).
+struct FlagPoll {
+  const std::uint32_t* flags;
+  std::uint32_t last, ngrp, lane, grp = 0, v = 0;
+  __device__ FlagPoll(const std::uint32_t* f, std::uint32_t groups, std::uint32_t l)
+      : flags(f), last(groups - 1u), ngrp((groups + 63u) / 64u), lane(l) {}
+  __device__ __forceinline__ bool next(std::uint32_t seq) {
+    const bool hit = v == seq;
+    const std::uint32_t f = lane + 64u * grp;
+    v = __hip_atomic_load(flags + (f < last ? f : last), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    grp = grp + 1u == ngrp ? 0u : grp + 1u;
+    return hit;
+  }
+};
+
 constexpr std::uint32_t kListSpan = 4096;          // bytes of one step's window
 constexpr int kListRows = kListSpan / 1024;        // 1 KiB load rows per step
 constexpr int kListRing = 3;                       // steps of data in registers (R - 1 ahead of the fold)
@@ -400,18 +417,12 @@ __global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
       __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     quit = 1u;
   }
-  // every fourth group of steps, the other workgroups' flags (16 per lane), checked one group later
-  std::uint32_t g = 0, nchk = 0;
-  const std::uint32_t ngroups = gridDim.x;
+  // the other workgroups' flags: one load per lane per group of steps, 64 flags at a time in turn, each
+  // looked at one group later (an unconditional load whose value waits a group: a conditional one, or
+  // one compared at once, made every check wait for all loads in flight)
+  FlagPoll poll(flags, gridDim.x, lane);
   for (std::uint32_t t = 0; t < ns && quit == 0u; t += R) {
-    if (nchk++ % 4u == 0u) {
-      g = 0;
-#pragma unroll
-      for (std::uint32_t i = 0; i < kListMaxGroups / 64u; ++i) {
-        const std::uint32_t f = lane + 64u * i;
-        if (i * 64u < ngroups && f < ngroups) g |= __hip_atomic_load(flags + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == seq ? 1u : 0u;
-      }
-    }
+    const bool hit = poll.next(seq);
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const std::uint32_t j = t + static_cast<std::uint32_t>(k);
@@ -421,7 +432,7 @@ __global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
       fetch(j + 2u * R, k);
     }
     // another workgroup met a long block: the general path folds the batch
-    quit = __builtin_amdgcn_readfirstlane(quit | (__ballot(g != 0u) != 0 ? 1u : 0u));
+    quit = __builtin_amdgcn_readfirstlane(quit | (__ballot(hit) != 0 ? 1u : 0u));
   }
 }
 
@@ -524,7 +535,7 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
 
   // wave-uniform cursor: chunk iq, its substep is of nsub, its T lanes of pieces
   std::uint32_t iq = ~0u, is = 0, nsub = 0, T = 0, quit = 0;
-  std::uint32_t poll = 0;  // polled flags, checked at the next chunk
+  FlagPoll poll(pflags, gridDim.x, lane);  // other workgroups' flags, one load per chunk
   auto wave_fence = [] {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -542,17 +553,7 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
     c0_off = c1_off;
     c0_len = c1_len;
     fetch(q + 2u, c1_off, c1_len);
-    // other workgroups' flags: loaded at every eighth chunk, looked at one chunk later
-    if ((q & 7u) == 1u) quit = __builtin_amdgcn_readfirstlane(quit | (__ballot(poll != 0u) != 0 ? 1u : 0u));
-    if ((q & 7u) == 0u) {
-      poll = 0;
-#pragma unroll
-      for (std::uint32_t i = 0; i < kListMaxGroups / 64u; ++i) {
-        const std::uint32_t f = lane + 64u * i;
-        if (i * 64u < gridDim.x && f < gridDim.x)
-          poll |= __hip_atomic_load(pflags + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == seq ? 1u : 0u;
-      }
-    }
+    quit = __builtin_amdgcn_readfirstlane(quit | (__ballot(poll.next(seq)) != 0 ? 1u : 0u));
     if (__ballot(len > kPackMax) != 0) leave();
     if (quit != 0u) return;
     const std::uint32_t k = (len + 63u) >> 6;
@@ -564,8 +565,8 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
       if (r < k) map[ex + r] = static_cast<std::uint8_t>(lane);
     acc[(q & 3u) * 64u + lane] = inj[len];
     wave_fence();
-    T = total;
-    nsub = total == 0u ? 1u : (total + 63u) >> 6;
+    T = __builtin_amdgcn_readfirstlane(total);
+    nsub = T == 0u ? 1u : (T + 63u) >> 6;
   };
 
   uint4 qv[R][dev::kLaneGran];
@@ -579,11 +580,12 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
       is = 0;
       if (iq < ns) prepare(iq);
     }
-    m_dead[slot] = iq >= ns || quit != 0u;
+    m_dead[slot] = __builtin_amdgcn_readfirstlane(iq >= ns || quit != 0u ? 1u : 0u) != 0u;
     if (m_dead[slot]) return;
-    const std::uint32_t v = 64u * is + lane;
+    const std::uint32_t v = 64u * is + lane;  // < 64 nsub <= 1024
     const bool live = v < T;
-    const std::uint32_t blk = live ? map[v] : 0u;
+    const std::uint32_t mv = map[v];
+    const std::uint32_t blk = live ? mv : 0u;
     const uint4 d = desc[blk];
     const std::uint32_t len = live ? d.z : 0u;
     const std::uint32_t g = v - d.w;  // this lane's piece of the block
@@ -601,7 +603,7 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
     m_lead[slot] = live ? -c_lane : 64;  // bytes of the piece in front of the block (64: none of it)
     m_sh[slot] = live ? k - 1u - g : 0u;
     m_acc[slot] = live ? (iq & 3u) * 64u + blk : ~0u;
-    m_last[slot] = is + 1u == nsub ? iq + 1u : 0u;
+    m_last[slot] = __builtin_amdgcn_readfirstlane(is + 1u == nsub ? iq + 1u : 0u);
     ++is;
   };
   auto fold = [&](int slot) {

@@ -87,6 +87,9 @@ def main():
     nm = count(42, 50)
     lm = rng.choice([26, 28, 33, 36, 59], nm)
     work.append(irregular("irregular WAL payloads 26-59 B, 8 B gaps", lm, np.full(nm, 8), 8))
+    nm = count(45, 53)  # mostly lane blocks, 2 % longer values (one-pass packed kernel)
+    lm = np.where(rng.random(nm) < 0.02, rng.integers(65, 401, nm), rng.choice([26, 28, 33, 36, 59], nm))
+    work.append(irregular("irregular WAL payloads 26-59 B + 2 % 65-400 B, 8 B gaps", lm, np.full(nm, 8), 8))
     ng = count(150, 158)
     work.append(irregular("irregular WAL payloads 100-200 B, 8 B gaps", rng.integers(100, 201, ng), np.full(ng, 8), 8))
     ng = count(160, 168)
