@@ -441,37 +441,41 @@ __global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
 // of its workgroups met a block over kLaneMax bytes; otherwise every workgroup returns at once) and
 // folds it straight from the caller's (offset, length) arrays when no block is over kPackMax bytes: no
 // prepass, no classes. Wave w takes 64-block chunks [w TS / W, (w + 1) TS / W). A block of len bytes
-// gets k = ceil(len / 64) lanes, packed back to back: the chunk's k are scanned (DPP) into each block's
-// first lane, the block-lanes write their descriptor and a lane -> block map into the wave's LDS, and
-// the chunk's ceil(sum k / 64) substeps each give every lane one 64-byte piece: lane g of k folds the
-// block's bytes [len - 64 (k - g), len - 64 (k - g - 1)) from zero (the bytes in front of the block
-// masked), moves the result to the block's end by Shift_{64 (k - 1 - g)} (nibble tables, one column per
-// shift), and XORs it into the block's LDS accumulator, which the chunk's block-lanes seeded with
-// Shift_len(0xFFFFFFFF) ^ xorout (crc_s(D) = Shift_|D|(s) ^ crc_0(D)); after the chunk's last substep the
+// gets k = ceil(len / 64) lanes of a per-wave lane stream: a chunk's k are scanned (DPP) into each
+// block's first lane, and its block-lanes write their descriptor and a lane -> block map into the
+// wave's LDS. Substeps take the stream 64 lanes at a time, running from one chunk into the next (never
+// further), so no substep is padded at a chunk's end: lane g of k folds the block's bytes
+// [len - 64 (k - g), len - 64 (k - g - 1)) from zero (the bytes in front of the block masked), moves the
+// result to the block's end by Shift_{64 (k - 1 - g)} (nibble tables, one column per shift), and XORs
+// it into the block's LDS accumulator, which the block-lane seeded with Shift_len(0xFFFFFFFF) ^ xorout
+// (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). After the substep that holds a chunk's last lane, its
 // accumulators are the block CRCs. Against the 4-lane groups of the general path, a substep fills its
-// 64 lanes with pieces whatever the length mix (a 128-byte block takes two lanes, not four) and nothing
-// is read twice: descriptors once, payload granules once per piece (5 granules for 64 bytes), no scan,
-// scatter or class lists.
-// Pipeline: a substep's granules are issued AHEAD substeps before its fold; a chunk is prepared (map,
-// descriptors, accumulators) when its first substep is issued, its descriptors loaded two chunks ahead;
-// four accumulator buffers, so a chunk's fold never meets the seeds of a later one.
+// 64 lanes with pieces whatever the length mix (a 128-byte block takes two lanes, not four, a 40-byte
+// one one) and nothing is read twice: descriptors once, payload granules once per piece (5 granules for
+// 64 bytes), no scan, scatter or class lists. A chunk with no lane (every block empty) is written when
+// it is prepared.
+// Pipeline: a substep's granules are issued one substep before its fold; a chunk is prepared (map,
+// descriptors, accumulator seeds) when the stream first needs it as the chunk after the current one,
+// its descriptors loaded two chunks earlier. Two descriptor buffers and a 2048-entry map ring (two
+// chunks: at most 2 x 16 x 64 lanes), four accumulator buffers: a chunk's seeds never meet an unfolded
+// substep of the chunk four before it (each substep spans two chunks at most).
 // A block over kPackMax bytes, as in crc_list_lanes: the workgroup stores the call's number in its own
 // flag (counts[kPackFlags + g]), every wave polls the flags and leaves, and the general path (whose
 // tile scan reads these flags) folds the batch.
 constexpr std::uint32_t kPackMax = kSmallMax;         // 16 lanes at most per block
 constexpr unsigned kPackThreads = 1024;
 constexpr unsigned kPackWaves = kPackThreads / 64;
-constexpr std::uint32_t kPackLsp = kLdsSliceWords * 2;    // after the 64 KiB image: shift tables
-constexpr std::uint32_t kPackInj = kPackLsp + 16 * 8 * 32 * 4;  // [16 shifts][8 nibbles][32 slots] words
+constexpr std::uint32_t kPackLsp = kLdsSliceWords * 2;  // after the 64 KiB image: shift tables
+constexpr std::uint32_t kPackInj = kPackLsp + 8 * 8 * 32 * 4;  // [8 shift pairs][8 nibbles][32] words
 constexpr std::uint32_t kPackScratch = kPackInj + 4 * (kPackMax + 4);  // Shift_len(init) ^ xorout
-constexpr std::uint32_t kPackWaveBytes = 3072;        // per wave: desc[64] (16 B), acc[4][64], map[1024]
+// per wave: desc[2][64] (16 B), map[2048] (u8: acc buffer << 6 | block), acc[4][64], acc_chunk[4]
+constexpr std::uint32_t kPackDesc = 0, kPackMap = 2048, kPackAcc = 4096, kPackAccQ = 5120;
+constexpr std::uint32_t kPackWaveBytes = 5136;
 constexpr std::uint32_t kPackLdsBytes = kPackScratch + kPackWaves * kPackWaveBytes;
-static_assert(kPackLdsBytes <= 163840, "LDS");
+static_assert(kPackLdsBytes + 4 <= 163840, "LDS");
 static_assert(kPackFlags == kListFlags + static_cast<int>(kListMaxGroups), "pack flags follow the list flags");
 
-template <int AHEAD>
 __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
-  constexpr int R = AHEAD + 1;  // substeps of data in registers
   __shared__ __attribute__((aligned(16))) std::uint8_t lds[kPackLdsBytes];
   __shared__ std::uint32_t wg_hit_word;
   const std::uint32_t seq = a.gate_seq;
@@ -500,12 +504,13 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
   }
   std::uint32_t* tab = reinterpret_cast<std::uint32_t*>(lds);
   dev::fill_lds_slicing16(a.tabs, tab);
-  // shift tables: word (sh * 8 + j) * 32 + (v | 16 (sh & 1)) = Shift_{64 sh}(v << 4 j) (lane_shift column
-  // 63 - sh); odd shifts in the upper 16 banks, so pieces of one block (consecutive sh) split the banks
+  // shift tables: word ((sh >> 1) * 8 + j) * 32 + (v | 16 (sh & 1)) = Shift_{64 sh}(v << 4 j) (lane_shift
+  // column 63 - sh): even shifts in the lower 16 banks, odd ones in the upper, so the pieces of one
+  // block (consecutive sh) split the banks
   std::uint32_t* lsp = reinterpret_cast<std::uint32_t*>(lds + kPackLsp);
-  for (std::uint32_t i = threadIdx.x; i < 16u * 8u * 32u; i += blockDim.x) {
-    const std::uint32_t sh = i >> 8, j = (i >> 5) & 7u, s = i & 31u;
-    lsp[i] = (s >> 4) == (sh & 1u) ? a.tabs->lane_shift[j][s & 15u][63u - sh] : 0u;
+  for (std::uint32_t i = threadIdx.x; i < 8u * 8u * 32u; i += blockDim.x) {
+    const std::uint32_t sh = ((i >> 8) << 1) | ((i >> 4) & 1u), j = (i >> 5) & 7u;
+    lsp[i] = a.tabs->lane_shift[j][i & 15u][63u - sh];
   }
   std::uint32_t* inj = reinterpret_cast<std::uint32_t*>(lds + kPackInj);
   for (std::uint32_t i = threadIdx.x; i <= kPackMax; i += blockDim.x) inj[i] = a.tabs->init_shift[i] ^ a.out_xor;
@@ -514,9 +519,10 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
   if (ns == 0) return;
 
   std::uint8_t* ws = lds + kPackScratch + wv * kPackWaveBytes;
-  uint4* desc = reinterpret_cast<uint4*>(ws);
-  std::uint32_t* acc = reinterpret_cast<std::uint32_t*>(ws + 1024);
-  std::uint8_t* map = ws + 2048;
+  uint4* desc = reinterpret_cast<uint4*>(ws + kPackDesc);
+  std::uint8_t* map = ws + kPackMap;
+  std::uint32_t* acc = reinterpret_cast<std::uint32_t*>(ws + kPackAcc);
+  std::uint32_t* accq = reinterpret_cast<std::uint32_t*>(ws + kPackAccQ);
   const dev::LaneConstX kc = dev::lane_const16(lane);
   const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
   const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
@@ -533,8 +539,10 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
   fetch(0, c0_off, c0_len);
   fetch(1, c1_off, c1_len);
 
-  // wave-uniform cursor: chunk iq, its substep is of nsub, its T lanes of pieces
-  std::uint32_t iq = ~0u, is = 0, nsub = 0, T = 0, quit = 0;
+  // wave-uniform stream state: the next lane to issue s, the end of the current chunk A (the one
+  // holding s) and of the prepared chunk after it, B (eb == ea: none); their accumulator buffers sa, sb
+  std::uint32_t s = 0, ea = 0, eb = 0, sa = 0, sb = 0;
+  std::uint32_t iq = 0, np = 0, quit = 0;  // next chunk to look at, chunks prepared
   FlagPoll poll(pflags, gridDim.x, lane);  // other workgroups' flags, one load per chunk
   auto wave_fence = [] {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -545,48 +553,68 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
       __hip_atomic_store(pflags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     quit = 1u;
   };
-  auto prepare = [&](std::uint32_t q) {
-    const std::uint64_t b = (s0 + q) * 64u + lane;
-    const bool live = b < n;
-    const std::uint32_t len = live ? c0_len : 0u;
-    const std::uint64_t off = c0_off;
-    c0_off = c1_off;
-    c0_len = c1_len;
-    fetch(q + 2u, c1_off, c1_len);
-    quit = __builtin_amdgcn_readfirstlane(quit | (__ballot(poll.next(seq)) != 0 ? 1u : 0u));
-    if (__ballot(len > kPackMax) != 0) leave();
-    if (quit != 0u) return;
-    const std::uint32_t k = (len + 63u) >> 6;
-    std::uint32_t total;
-    const std::uint32_t ex = dev::lane_prefix(k, &total);
-    wave_fence();  // the previous chunk's map and descriptor reads are done
-    desc[lane] = make_uint4(static_cast<std::uint32_t>(off), static_cast<std::uint32_t>(off >> 32), len, ex);
-    for (std::uint32_t r = 0; __ballot(r < k) != 0; ++r)
-      if (r < k) map[ex + r] = static_cast<std::uint8_t>(lane);
-    acc[(q & 3u) * 64u + lane] = inj[len];
-    wave_fence();
-    T = __builtin_amdgcn_readfirstlane(total);
-    nsub = T == 0u ? 1u : (T + 63u) >> 6;
+  // prepares the next chunk with lanes as B, its lanes from eb on; false when none is left (or on quit)
+  auto prepare = [&]() -> bool {
+    while (iq < ns && quit == 0u) {
+      const std::uint32_t q = iq++;
+      const std::uint64_t b = (s0 + q) * 64u + lane;
+      const bool live = b < n;
+      const std::uint32_t len = live ? c0_len : 0u;
+      const std::uint64_t off = c0_off;
+      c0_off = c1_off;
+      c0_len = c1_len;
+      fetch(q + 2u, c1_off, c1_len);
+      quit = __builtin_amdgcn_readfirstlane(quit | (__ballot(poll.next(seq)) != 0 ? 1u : 0u));
+      if (__ballot(len > kPackMax) != 0) leave();
+      if (quit != 0u) return false;
+      const std::uint32_t k = (len + 63u) >> 6;
+      std::uint32_t total;
+      const std::uint32_t ex = dev::lane_prefix(k, &total);
+      const std::uint32_t T = __builtin_amdgcn_readfirstlane(total);
+      if (T == 0u) {  // every block empty: the CRCs are the seeds
+        if (live) a.out[b] = inj[0];
+        continue;
+      }
+      const std::uint32_t slot = np++ & 3u, v0 = eb + ex;  // the block's first lane in the stream
+      wave_fence();  // reads of the chunk two before (descriptors, map) and of this buffer are done
+      desc[(slot & 1u) * 64u + lane] = make_uint4(static_cast<std::uint32_t>(off), static_cast<std::uint32_t>(off >> 32), len, v0);
+      for (std::uint32_t r = 0; __ballot(r < k) != 0; ++r)
+        if (r < k) map[(v0 + r) & 2047u] = static_cast<std::uint8_t>(slot << 6 | lane);
+      acc[slot * 64u + lane] = inj[len];
+      accq[slot] = q;
+      wave_fence();
+      eb += T;
+      sb = slot;
+      return true;
+    }
+    return false;
   };
 
-  uint4 qv[R][dev::kLaneGran];
-  std::uint32_t m_o[R], m_sh[R], m_acc[R];
-  std::int32_t m_lead[R];
-  std::uint32_t m_last[R];  // wave-uniform: 1 + the chunk whose last substep this is, else 0
-  bool m_dead[R];           // wave-uniform: past the wave's last substep
-  auto issue = [&](int slot) {
-    if (is == nsub && quit == 0u) {
-      ++iq;
-      is = 0;
-      if (iq < ns) prepare(iq);
+  uint4 qv[2][dev::kLaneGran];
+  std::uint32_t m_o[2], m_sh[2], m_acc[2];
+  std::int32_t m_lead[2];
+  std::uint32_t m_done[2];  // wave-uniform: 1 + the buffers of the chunks this substep completes, 3 bits each
+  bool m_dead[2];           // wave-uniform: past the wave's last lane
+  auto issue = [&](int r) {
+    if (quit == 0u) {
+      if (s >= ea && eb > ea) {  // A is done (the last substep may have run into B): B becomes A
+        ea = eb;
+        sa = sb;
+      }
+      if (s >= ea && prepare()) {  // none prepared (s == ea == eb): the next chunk becomes A
+        ea = eb;
+        sa = sb;
+      }
+      if (s < ea && eb == ea) prepare();  // a chunk B for the substep to run into
     }
-    m_dead[slot] = __builtin_amdgcn_readfirstlane(iq >= ns || quit != 0u ? 1u : 0u) != 0u;
-    if (m_dead[slot]) return;
-    const std::uint32_t v = 64u * is + lane;  // < 64 nsub <= 1024
-    const bool live = v < T;
-    const std::uint32_t mv = map[v];
-    const std::uint32_t blk = live ? mv : 0u;
-    const uint4 d = desc[blk];
+    m_dead[r] = __builtin_amdgcn_readfirstlane(s >= ea || quit != 0u ? 1u : 0u) != 0u;
+    if (m_dead[r]) return;
+    const std::uint32_t e = eb - s < 64u ? eb : s + 64u;  // never past B
+    const std::uint32_t v = s + lane;
+    const bool live = v < e;
+    const std::uint32_t mv = map[v & 2047u];
+    const std::uint32_t bslot = mv >> 6, blk = mv & 63u;
+    const uint4 d = desc[(bslot & 1u) * 64u + blk];
     const std::uint32_t len = live ? d.z : 0u;
     const std::uint32_t g = v - d.w;  // this lane's piece of the block
     const std::uint32_t k = (len + 63u) >> 6;
@@ -597,50 +625,56 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
 #pragma unroll
     for (int i = 0; i < dev::kLaneGran; ++i) {
       const std::uintptr_t gp = al + 16u * i;
-      qv[slot][i] = dev::gload16(live && gp + 16u > blo && gp < bhi ? gp : dmy);
+      qv[r][i] = dev::gload16(live && gp + 16u > blo && gp < bhi ? gp : dmy);
     }
-    m_o[slot] = static_cast<std::uint32_t>(p & 15u);
-    m_lead[slot] = live ? -c_lane : 64;  // bytes of the piece in front of the block (64: none of it)
-    m_sh[slot] = live ? k - 1u - g : 0u;
-    m_acc[slot] = live ? (iq & 3u) * 64u + blk : ~0u;
-    m_last[slot] = __builtin_amdgcn_readfirstlane(is + 1u == nsub ? iq + 1u : 0u);
-    ++is;
+    m_o[r] = static_cast<std::uint32_t>(p & 15u);
+    m_lead[r] = live ? -c_lane : 64;  // bytes of the piece in front of the block (64: none of it)
+    m_sh[r] = live ? k - 1u - g : 0u;
+    m_acc[r] = live ? bslot * 64u + blk : ~0u;
+    // the chunks whose last lane lies in [s, e): A when e reaches its end, B too when e is its end
+    const std::uint32_t done = (ea <= e ? sa + 1u : 0u) | (eb > ea && eb <= e ? (sb + 1u) << 3 : 0u);
+    m_done[r] = __builtin_amdgcn_readfirstlane(done);
+    s = e;
   };
-  auto fold = [&](int slot) {
+  auto readout = [&](std::uint32_t slot) {
+    const std::uint32_t q = __builtin_amdgcn_readfirstlane(accq[slot]);
+    const std::uint64_t b = (s0 + q) * 64u + lane;
+    const std::uint32_t crc = acc[slot * 64u + lane];
+    if (b < n) a.out[b] = crc;
+  };
+  auto fold = [&](int r) {
     std::uint32_t d[16];
-    dev::lane_dwords<1>(qv[slot], m_o[slot], d);
-    const std::int32_t lead = m_lead[slot];
-    dev::Reg r{0u, 0u};
+    dev::lane_dwords<1>(qv[r], m_o[r], d);
+    const std::int32_t lead = m_lead[r];
+    dev::Reg reg{0u, 0u};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const std::int32_t before = lead - 4 * k;
       const std::uint32_t shb = static_cast<std::uint32_t>(before < 0 ? 0 : (before > 4 ? 4 : before)) * 8u;
-      dev::slice4(tab, r, d[k] & static_cast<std::uint32_t>(0xFFFFFFFFull << shb), kc);
+      dev::slice4(tab, reg, d[k] & static_cast<std::uint32_t>(0xFFFFFFFFull << shb), kc);
     }
-    const std::uint32_t p = r.value();
-    const std::uint32_t sh = m_sh[slot];
-    const std::uint32_t lb = kPackLsp + sh * 1024u + ((sh & 1u) << 6);
+    const std::uint32_t p = reg.value();
+    const std::uint32_t sh = m_sh[r];
+    const std::uint32_t lb = kPackLsp + (sh >> 1) * 1024u + ((sh & 1u) << 6);
     std::uint32_t l[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) l[j] = dev::lds_at(tab, lb + 128u * j + (((p >> (4 * j)) & 15u) << 2));
     const std::uint32_t v = dev::xor3(dev::xor3(l[0], l[1], l[2]), dev::xor3(l[3], l[4], l[5]), l[6] ^ l[7]);
-    if (m_acc[slot] != ~0u) __hip_atomic_fetch_xor(acc + m_acc[slot], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    if (m_last[slot] != 0u) {
-      const std::uint32_t q = m_last[slot] - 1u;
+    if (m_acc[r] != ~0u) __hip_atomic_fetch_xor(acc + m_acc[r], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    const std::uint32_t done = m_done[r];
+    if (done != 0u) {
       wave_fence();
-      const std::uint64_t b = (s0 + q) * 64u + lane;
-      const std::uint32_t crc = acc[(q & 3u) * 64u + lane];
-      if (b < n) a.out[b] = crc;
+      if (done & 7u) readout((done & 7u) - 1u);
+      if (done >> 3) readout((done >> 3) - 1u);
     }
   };
+  issue(0);
+  for (bool fin = false; !fin;) {
 #pragma unroll
-  for (int k = 0; k < AHEAD; ++k) issue(k);
-  for (bool done = false; !done;) {
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      issue((k + AHEAD) % R);
+    for (int k = 0; k < 2; ++k) {
+      issue(k ^ 1);
       if (m_dead[k]) {
-        done = true;
+        fin = true;
         break;
       }
       fold(k);
@@ -1539,16 +1573,13 @@ hipError_t launch_list_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
 
 // One-pass packed kernel of an irregular batch that crc_list_lanes handed on: see crc_list_pack. Its
 // workgroups return at once when crc_list_lanes folded the batch.
-#ifndef TKV_PACK_AHEAD
-#define TKV_PACK_AHEAD 1
-#endif
 hipError_t launch_list_pack(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   RowsArgs b = a;
   const std::uint64_t chunks = (a.nblocks + 63u) / 64u;
   const std::uint64_t grid = std::max<std::uint64_t>(
       1, std::min<std::uint64_t>(std::min<std::uint64_t>(ncu, kListMaxGroups), (chunks + kPackWaves - 1) / kPackWaves));
   b.nwaves = static_cast<std::uint32_t>(grid * kPackWaves);
-  hipLaunchKernelGGL(crc_list_pack<TKV_PACK_AHEAD>, dim3(static_cast<unsigned>(grid)), dim3(kPackThreads), 0, st, b);
+  hipLaunchKernelGGL(crc_list_pack, dim3(static_cast<unsigned>(grid)), dim3(kPackThreads), 0, st, b);
   return hipGetLastError();
 }
 
