@@ -59,7 +59,7 @@ def oracle_c(oracle, host, offs, lens):
 
 SHAPES = ["wal_65_256", "wal_100_200", "mix_0_1024", "all_1024", "back_to_back_128", "shuffled", "overlapping",
           "zero_heavy", "lanes_then_pack", "spread_lanes", "late_huge", "early_huge", "mid_huge", "at_allocation_end",
-          "crc32c"]
+          "at_allocation_start", "crc32c"]
 
 
 @pytest.mark.parametrize("shape", SHAPES)
@@ -109,6 +109,9 @@ def test_pack_one_pass(gpu, oracle, buf, shape):
     elif shape == "at_allocation_end":  # every block ends on a 1 KiB slot's last byte, the last on the tensor's
         lens = rng.integers(0, 1025, n)
         offs = (host.size - 1024 * 64 + 1024 * (np.arange(n) % 64) + (1024 - lens)).astype(np.int64)
+    elif shape == "at_allocation_start":  # every block starts a 1 KiB slot, the first at the tensor's first byte
+        lens = rng.integers(0, 1025, n)
+        offs = (1024 * (np.arange(n) % 64)).astype(np.int64)
     offs = np.asarray(offs, np.int64)
     lens = np.asarray(lens, np.int32)
     assert int((offs + lens).max()) <= host.size
@@ -130,6 +133,12 @@ def test_pack_one_pass(gpu, oracle, buf, shape):
         cut = host.size - 1024 * 64
         tail = d[cut:].clone()
         got = u32(tk.crc32_batch(tail, torch.from_numpy(offs - cut).to(gpu), ln))
+        assert path() == 1
+        assert np.array_equal(got, want)
+    if shape == "at_allocation_start":  # a fresh copy of the first 64 KiB: no load may reach in front of it
+        head = torch.empty(64 << 10, dtype=torch.uint8, device=gpu)
+        head.copy_(d[:64 << 10])
+        got = u32(tk.crc32_batch(head, o, ln))
         assert path() == 1
         assert np.array_equal(got, want)
 

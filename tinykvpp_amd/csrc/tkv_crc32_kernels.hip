@@ -592,7 +592,7 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
 
   uint4 qv[2][dev::kLaneGran];
   std::uint32_t m_o[2], m_sh[2], m_acc[2];
-  std::int32_t m_lead[2];
+  std::int32_t m_lead[2];   // 8 x the bytes of the piece in front of the block
   std::uint32_t m_done[2];  // wave-uniform: 1 + the buffers of the chunks this substep completes, 3 bits each
   bool m_dead[2];           // wave-uniform: past the wave's last lane
   auto issue = [&](int r) {
@@ -619,16 +619,21 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
     const std::uint32_t g = v - d.w;  // this lane's piece of the block
     const std::uint32_t k = (len + 63u) >> 6;
     const std::int32_t c_lane = static_cast<std::int32_t>(len) - 64 * static_cast<std::int32_t>(k - g);
-    const std::uintptr_t blo = base + (static_cast<std::uint64_t>(d.y) << 32 | d.x), bhi = blo + len;
+    const std::uintptr_t blo = base + (static_cast<std::uint64_t>(d.y) << 32 | d.x);
     const std::uintptr_t p = static_cast<std::uintptr_t>(static_cast<std::int64_t>(blo) + c_lane);
     const std::uintptr_t al = p & ~static_cast<std::uintptr_t>(15);
+    const std::uint32_t o = static_cast<std::uint32_t>(p & 15u);
+    // granule i holds a byte of the block iff al + 16 i - blo lies in (-16, len), i.e. al + 16 i - blo +
+    // 15 in [0, len + 15) (32-bit arithmetic: -80 < al - blo < len); the others read `dummy`, so no load
+    // leaves the 16-byte granules the block touches
+    const std::int32_t rel = c_lane - static_cast<std::int32_t>(o) + 15;
 #pragma unroll
     for (int i = 0; i < dev::kLaneGran; ++i) {
-      const std::uintptr_t gp = al + 16u * i;
-      qv[r][i] = dev::gload16(live && gp + 16u > blo && gp < bhi ? gp : dmy);
+      const bool in = live && static_cast<std::uint32_t>(rel + 16 * i) < len + 15u;
+      qv[r][i] = dev::gload16(in ? al + 16u * i : dmy);
     }
-    m_o[r] = static_cast<std::uint32_t>(p & 15u);
-    m_lead[r] = live ? -c_lane : 64;  // bytes of the piece in front of the block (64: none of it)
+    m_o[r] = o;
+    m_lead[r] = live ? (c_lane < 0 ? -8 * c_lane : 0) : 512;  // bits in front of the block (512: all)
     m_sh[r] = live ? k - 1u - g : 0u;
     m_acc[r] = live ? bslot * 64u + blk : ~0u;
     // the chunks whose last lane lies in [s, e): A when e reaches its end, B too when e is its end
@@ -645,12 +650,13 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
   auto fold = [&](int r) {
     std::uint32_t d[16];
     dev::lane_dwords<1>(qv[r], m_o[r], d);
-    const std::int32_t lead = m_lead[r];
+    const std::uint32_t lead8 = static_cast<std::uint32_t>(m_lead[r]);
     dev::Reg reg{0u, 0u};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const std::int32_t before = lead - 4 * k;
-      const std::uint32_t shb = static_cast<std::uint32_t>(before < 0 ? 0 : (before > 4 ? 4 : before)) * 8u;
+      // the bits of dword k in front of the block: min(lead8 -sat 32 k, 32) (saturating subtract)
+      const std::uint32_t x = __builtin_elementwise_sub_sat(lead8, static_cast<std::uint32_t>(32 * k));
+      const std::uint32_t shb = x < 32u ? x : 32u;
       dev::slice4(tab, reg, d[k] & static_cast<std::uint32_t>(0xFFFFFFFFull << shb), kc);
     }
     const std::uint32_t p = reg.value();
