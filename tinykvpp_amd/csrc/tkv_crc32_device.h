@@ -145,6 +145,13 @@ __device__ __forceinline__ std::uint32_t wave_max(std::uint32_t v) {
   return static_cast<std::uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
 }
 
+// Dword k of a window with its bytes in front of window byte `lead` zeroed, lead8 = 8 max(lead, 0):
+// min(lead8 -sat 32 k, 32) bits from the bottom (a saturating subtract, a min, a shift and an AND).
+__device__ __forceinline__ std::uint32_t mask_front(std::uint32_t d, std::uint32_t lead8, int k) {
+  const std::uint32_t x = __builtin_elementwise_sub_sat(lead8, static_cast<std::uint32_t>(32 * k));
+  return d & static_cast<std::uint32_t>(0xFFFFFFFFull << (x < 32u ? x : 32u));
+}
+
 // Exclusive prefix sum over the 64 lanes (all active), and its total: an inclusive scan by DPP row
 // shifts within rows of 16, then the row totals broadcast into the rows above (row_bcast:15 / :31).
 template <int CTRL, int ROW_MASK>
@@ -1957,7 +1964,7 @@ __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_
     }
     m_len[slot] = live ? len : 0xFFFFFFFFu;  // 0xFFFFFFFF: nothing to fold or store
     m_o[slot] = static_cast<std::uint32_t>(p & 15u);
-    m_lead[slot] = -c_lane;     // bytes of the lane's window in front of the block
+    m_lead[slot] = c_lane < 0 ? -8 * c_lane : 0;  // bits of the lane's window in front of the block
     if constexpr (LIST) m_idx[slot] = d_idx[slot];  // (a valid batch index even in a dead slot)
     m_ishift[slot] = a.tabs->init_shift[len];  // Shift_len(0xFFFFFFFF), the reference's init (crc32.hpp:39)
   };
@@ -1980,14 +1987,10 @@ __device__ __forceinline__ void group_walk(const RowsArgs& a, const std::uint32_
     }
     std::uint32_t d[16];
     lane_dwords<1>(q[slot], m_o[slot], d);
-    const std::int32_t lead = m_lead[slot];
+    const std::uint32_t lead8 = static_cast<std::uint32_t>(m_lead[slot]);
     Reg p{0, 0};
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const std::int32_t before = lead - 4 * k;
-      const std::uint32_t sh = static_cast<std::uint32_t>(before < 0 ? 0 : (before > 4 ? 4 : before)) * 8u;
-      slice4(lds, p, d[k] & static_cast<std::uint32_t>(0xFFFFFFFFull << sh), kc);
-    }
+    for (int k = 0; k < 16; ++k) slice4(lds, p, mask_front(d[k], lead8, k), kc);
     std::uint32_t v = lane_shift(lds, p.value(), kc);
     const std::uint32_t L = live ? len : 0u;
     if (a.init_raw) {

@@ -653,12 +653,7 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
     const std::uint32_t lead8 = static_cast<std::uint32_t>(m_lead[r]);
     dev::Reg reg{0u, 0u};
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      // the bits of dword k in front of the block: min(lead8 -sat 32 k, 32) (saturating subtract)
-      const std::uint32_t x = __builtin_elementwise_sub_sat(lead8, static_cast<std::uint32_t>(32 * k));
-      const std::uint32_t shb = x < 32u ? x : 32u;
-      dev::slice4(tab, reg, d[k] & static_cast<std::uint32_t>(0xFFFFFFFFull << shb), kc);
-    }
+    for (int k = 0; k < 16; ++k) dev::slice4(tab, reg, dev::mask_front(d[k], lead8, k), kc);
     const std::uint32_t p = reg.value();
     const std::uint32_t sh = m_sh[r];
     const std::uint32_t lb = kPackLsp + (sh >> 1) * 1024u + ((sh & 1u) << 6);
