@@ -290,7 +290,8 @@ int tkv_debug_irregular_phases(void *stream);
 /* Which kernel folded the last irregular batch on `stream`: 0 = the one-pass lane kernel
  * (crc_list_lanes: every block <= 64 B), 1 = the one-pass packed kernel (crc_list_pack: every block
  * <= 1 KiB), 2 = the general path after both handed it on, 3 = the general path alone (fewer than
- * 1 M blocks, or per-block initial registers); -1 on error. Synchronizes the stream. */
+ * 256 K blocks, per-block initial registers, or tkv_debug_set_one_pass(0)); -1 on error.
+ * Synchronizes the stream. */
 int tkv_debug_irregular_path(void *stream);
 /* Waves of the one-pass lane kernel (crc_list_lanes) for an irregular batch of nblocks on the current
  * device: wave w takes its 64-block steps [w TS / W, (w + 1) TS / W), TS = ceil(nblocks / 64). 0 when
@@ -311,6 +312,11 @@ int tkv_debug_set_host_mapped(int enable);
  * walk as before round 4 (kept so its many-ends-per-row shapes stay under test). Returns the previous
  * setting. Default 0. */
 int tkv_debug_set_stream_groups(int enable);
+/* Irregular batches of at least 256 K blocks with the default register start with the one-pass
+ * kernels (crc_list_lanes, crc_list_pack) unless this is 0: then they take the general path alone, as
+ * smaller batches do (kept so the general path's large-batch shapes stay under test). Returns the
+ * previous setting. Default 1. */
+int tkv_debug_set_one_pass(int enable);
 
 
 #ifdef __cplusplus

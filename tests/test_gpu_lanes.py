@@ -169,7 +169,7 @@ def test_irregular_one_pass_lanes(gpu, oracle, buf, shape):
         return
     got = u32(tk.crc32_batch(d, o, ln))
     # which kernel folded the batch: crc_list_lanes (0), or crc_list_pack (1) after crc_list_lanes handed
-    # it on (a first step out of order, a block over 64 bytes); the general path alone below 1 M blocks (3)
+    # it on (a first step out of order, a block over 64 bytes); the general path alone below 256 K blocks (3)
     want_path = {"shuffled": 1, "late_long": 1, "tiny_batch": 3}.get(shape, 0)
     assert path() == want_path, shape
     assert phases() == 0, shape
@@ -284,11 +284,14 @@ def test_irregular_more_than_1024_tiles(gpu, oracle, shape, tiles):
     ln = torch.from_numpy(lens).to(gpu)
     lib = tk.load_library()
     prev = lib.tkv_debug_set_stream_groups(1 if shape == "back_to_back_128_stream" else 0)
+    prev_one = lib.tkv_debug_set_one_pass(0)  # the general path's prepass at these sizes, not the one-pass kernels
     try:
         assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), oracle.batch(host, offs, lens))
         got_mode = mode()
+        assert path() == 3
     finally:
         lib.tkv_debug_set_stream_groups(prev)
+        lib.tkv_debug_set_one_pass(prev_one)
     # back-to-back blocks longer than kLaneMax take stream mode at any batch size, through
     # rows_scan_tiles' verdict, unless their tiles' bytes are mostly in blocks of at most 1 KiB (128 and
     # 300 B, by default: the group passes and the small phase)

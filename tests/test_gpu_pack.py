@@ -1,5 +1,5 @@
 """GPU parity of crc_list_pack, the one-pass kernel that folds an irregular batch of
-blocks of at most 1 KiB (default initial register, at least 1 M blocks) after crc_list_lanes hands it
+blocks of at most 1 KiB (default initial register, at least 256 K blocks) after crc_list_lanes hands it
 on: each block gets ceil(len / 64) lanes packed back to back over 64-block chunks, every lane folds one
 64-byte piece, moves it to the block end and XORs it into the block's LDS accumulator.
 
@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-N = 1_100_003  # >= 1 M blocks (the one-pass kernels' threshold), not a multiple of 64
+N = 1_100_003  # >= 256 K blocks (the one-pass kernels' threshold), not a multiple of 64
 
 
 def u32(t):
@@ -175,3 +175,25 @@ def test_pack_not_with_per_block_registers(gpu, oracle, buf):
                              init_raw=torch.from_numpy(init.view(np.int32)).to(gpu)))
     assert path() == 3
     assert np.array_equal(got, oracle.batch(host, offs, lens, init))
+
+
+@pytest.mark.parametrize("n,want_path", [(262_144, 1), (262_143, 3)])
+def test_pack_threshold(gpu, oracle, buf, n, want_path):
+    """The one-pass kernels take batches of at least 256 K blocks (kListMinBlocks); one block fewer
+    takes the general path alone. Same results either way; tkv_debug_set_one_pass(0) sends the larger
+    batch to the general path too."""
+    host, d = buf
+    rng = np.random.default_rng(n)
+    lens = rng.integers(65, 257, n).astype(np.int32)
+    offs = (3 + 8 + np.concatenate([[0], np.cumsum(lens[:-1] + 8)])).astype(np.int64)
+    o, ln = torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu)
+    want = oracle.batch(host, offs, lens)
+    assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), want)
+    assert path() == want_path
+    lib = tk.load_library()
+    prev = lib.tkv_debug_set_one_pass(0)
+    try:
+        assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), want)
+        assert path() == 3
+    finally:
+        lib.tkv_debug_set_one_pass(prev)

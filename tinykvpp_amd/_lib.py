@@ -72,6 +72,7 @@ SIGNATURES = {
     "tkv_debug_x8nmodp": (_u32, [_u64]),
     "tkv_debug_set_host_mapped": (_int, [_int]),
     "tkv_debug_set_stream_groups": (_int, [_int]),
+    "tkv_debug_set_one_pass": (_int, [_int]),
     "tkv_debug_wal_chain": (_sz, [_u8p, _u64, _vp, _sz, ctypes.POINTER(_u64), ctypes.POINTER(_int)]),
     "tkv_debug_wal_last": (None, [_vp]),
     "tkv_debug_wal_rounds": (ctypes.c_size_t, [_vp, ctypes.c_size_t]),

@@ -514,7 +514,19 @@ int run_uniform(DevCtx* c, int algo, const std::uint8_t* d_base, std::uint64_t s
 // those blocks faster than the stream walk's many-ends rows).
 std::atomic<int> g_stream_groups{0};
 
-constexpr std::uint64_t kListMinBlocks = std::uint64_t(1) << 20;
+// Whether irregular batches may take the one-pass kernels (tkv_debug_set_one_pass; default 1).
+std::atomic<int> g_one_pass{1};
+
+// Irregular batches of at least kListMinBlocks blocks with the default register start with the
+// one-pass kernels. Below it the general path alone: a batch the one-pass kernels hand on pays their
+// two short launches (~10 us), which cfg4's 131072 blocks of 256 B-1 MiB must not (one process,
+// 32 MiB gapped batches against the round-5 threshold of 1 M blocks: 36-byte payloads (732 K blocks)
+// 749 -> 1011 GB/s, 26-59 B 648 -> 945, back-to-back 64 B 871 -> 1245, the rest within 1 %;
+// profiles/r6/pack/threshold.jsonl).
+#ifndef TKV_LIST_MIN_SHIFT
+#define TKV_LIST_MIN_SHIFT 18
+#endif
+constexpr std::uint64_t kListMinBlocks = std::uint64_t(1) << TKV_LIST_MIN_SHIFT;
 int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::uint64_t* d_off, const std::uint32_t* d_len,
                   const std::uint32_t* d_init, std::uint32_t* d_out, std::uint64_t n, hipStream_t st) {
   if (n == 0) return TKV_OK;
@@ -555,11 +567,9 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   a.l_tile = s->tile_ok;
   // Default registers, at least kListMinBlocks blocks: one pass of crc_list_lanes first, which folds
   // every block when none is longer than kLaneMax bytes (WAL payload lists); the general path's launches
-  // then return at once. When it meets a longer block it flags its workgroup and the general path folds
-  // the whole batch. Smaller batches skip it: the pass costs a batch it hands on ~10 us (2-4 % of a
-  // 1 GiB batch of larger blocks, profiles/r5/list_lanes/), more than it saves a short lane-only one.
-  // 
-  s->one_pass = d_init == nullptr && n >= kListMinBlocks;
+  // then return at once. When it meets a longer block it flags its workgroup and crc_list_pack (below)
+  // takes the batch.
+  s->one_pass = d_init == nullptr && n >= kListMinBlocks && g_one_pass.load(std::memory_order_relaxed) != 0;
   s->pack = false;
   if (s->one_pass) {
     s->gate_seq = s->gate_seq + 1u == 0u ? 1u : s->gate_seq + 1u;
@@ -1426,5 +1436,7 @@ int tkv_debug_irregular_lists(void* stream, std::uint32_t out[3]) {
 int tkv_debug_set_host_mapped(int enable) { return tkv::g_host_mapped.exchange(enable ? 1 : 0); }
 
 int tkv_debug_set_stream_groups(int enable) { return tkv::g_stream_groups.exchange(enable ? 1 : 0); }
+
+int tkv_debug_set_one_pass(int enable) { return tkv::g_one_pass.exchange(enable ? 1 : 0); }
 
 }  // extern "C"
