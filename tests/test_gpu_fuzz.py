@@ -364,3 +364,58 @@ def stream_many_case(oracle, gpu, seed, group_stream):
     want = oracle_batch(oracle, algo, host, offs, lens, init)
     bad = np.flatnonzero(got != want)
     assert bad.size == 0, f"n={n} start={start} shift={shift} algo={algo}: {bad.size} differ, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_one_pass_random(gpu, oracle, seed):
+    """Batches of at least 256 K blocks with the default register: the one-pass kernels
+    (crc_list_lanes, crc_list_pack). Length mixes of lane blocks only, up to 256 B,
+    up to 1 KiB and the class edges, sometimes one block over 1 KiB (the general path then folds the
+    batch); gapped, back-to-back, shuffled and overlapping layouts; base shifts; both polynomials.
+    Every block against the oracle (CRC-32C sampled), and which kernel folded the batch."""
+    rng = np.random.default_rng(9000 + seed + OFFSET)
+    algo = ALGOS[seed % 2]
+    n = int(rng.choice([262_144, 300_001, 400_003]))
+    mix = ("lanes", "small", "mid", "edges")[seed // 2 % 4]
+    if mix == "lanes":
+        lens = rng.integers(0, 65, n)
+    elif mix == "small":
+        lens = rng.integers(0, 257, n)
+    elif mix == "mid":
+        lens = rng.integers(0, 1025, n)
+    else:
+        lens = rng.choice(np.array([0, 1, 3, 4, 63, 64, 65, 127, 128, 129, 255, 256, 257, 1023, 1024]), n)
+    big = rng.random() < 0.25
+    if big:
+        lens[int(rng.integers(0, n))] = int(rng.integers(1025, 5000))
+    layout = ("gapped", "back_to_back", "shuffled", "overlapping")[seed % 4]
+    start = int(rng.integers(0, 64))
+    if layout == "overlapping":
+        offs = rng.integers(0, max(1, int(lens.sum()) // 3), n) + start
+    else:
+        gaps = rng.integers(0, 20, n) if layout != "back_to_back" else np.zeros(n, np.int64)
+        offs = start + np.concatenate([[0], np.cumsum(lens + gaps)[:-1]])
+        if layout == "shuffled":
+            p = rng.permutation(n)
+            offs, lens = offs[p], lens[p]
+    host = rng.integers(0, 256, int((offs + lens).max()) + 64, dtype=np.uint8)
+    shift = int(rng.integers(0, 16))
+    d = on_device(host, gpu, shift)
+    got = u32(tk.crc32_batch(d, torch.from_numpy(offs.astype(np.int64)).to(gpu),
+                             torch.from_numpy(lens.astype(np.int32)).to(gpu), algo=algo))
+    kp = tk.load_library().tkv_debug_irregular_path(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    if big:
+        assert kp == 2, (mix, layout)
+    elif int(lens.max()) > 64:
+        assert kp == 1, (mix, layout)
+    else:
+        assert kp in (0, 1), (mix, layout)  # (lane blocks whose first steps are no window go to crc_list_pack)
+    if algo == "crc32c":
+        smp = rng.choice(n, 4000, replace=False)
+        want = oracle_batch(oracle, algo, host, offs[smp], lens[smp], None)
+        assert np.array_equal(got[smp], want), (mix, layout, shift)
+        return
+    want = oracle_batch(oracle, algo, host, offs, lens, None)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, (f"{mix} {layout} n={n} shift={shift} path={kp}: {bad.size} differ, first {bad[:5]} "
+                           f"(lens {lens[bad[:5]]})")
