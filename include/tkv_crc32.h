@@ -287,10 +287,11 @@ int tkv_debug_irregular_mode(void *stream);
  * mode): bit 0 the lane phase (blocks <= 64 B), bits 1 / 2 the 4- / 8-lane group passes (65-256 /
  * 257-512 B); -1 on error. Synchronizes the stream. */
 int tkv_debug_irregular_phases(void *stream);
-/* Which kernel folded the last irregular batch on `stream`: 0 = the one-pass lane kernel
- * (crc_list_lanes: every block <= 64 B), 1 = the one-pass packed kernel (crc_list_pack: every block
- * <= 1 KiB), 2 = the general path after both handed it on, 3 = the general path alone (fewer than
- * 256 K blocks, per-block initial registers, or tkv_debug_set_one_pass(0)); -1 on error.
+/* Which path folded the last irregular batch on `stream`: 0 = the one-pass kernel with one lane per
+ * block only (crc_list_lanes: every block <= 64 B), 1 = the one-pass kernel with its packed mode in
+ * at least one wave (every block <= 1 KiB), 2 = the general path after the one-pass kernel handed the
+ * batch on (a block over 1 KiB), 3 = the general path alone (fewer than 256 K blocks, per-block
+ * initial registers, tkv_debug_set_one_pass(0) or tkv_debug_set_stream_groups(1)); -1 on error.
  * Synchronizes the stream. */
 int tkv_debug_irregular_path(void *stream);
 /* Waves of the one-pass lane kernel (crc_list_lanes) for an irregular batch of nblocks on the current
@@ -313,7 +314,7 @@ int tkv_debug_set_host_mapped(int enable);
  * setting. Default 0. */
 int tkv_debug_set_stream_groups(int enable);
 /* Irregular batches of at least 256 K blocks with the default register start with the one-pass
- * kernels (crc_list_lanes, crc_list_pack) unless this is 0: then they take the general path alone, as
+ * kernel (crc_list_lanes and its packed mode) unless this is 0: then they take the general path alone, as
  * smaller batches do (kept so the general path's large-batch shapes stay under test). Returns the
  * previous setting. Default 1. */
 int tkv_debug_set_one_pass(int enable);

@@ -41,7 +41,6 @@ hipError_t launch_prepass(const std::uint8_t* base, const std::uint64_t* offsets
                           const std::uint32_t* gate_flags, hipStream_t st);
 hipError_t launch_stream_rows(const RowsArgs& a, hipStream_t st, unsigned grid);
 hipError_t launch_list_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st);
-hipError_t launch_list_pack(const RowsArgs& a, unsigned ncu, hipStream_t st);
 std::uint32_t list_lanes_waves(std::uint64_t nblocks, unsigned ncu);
 std::uint64_t prepass_tiles(std::uint64_t n);
 hipError_t launch_span(const std::uint8_t* stage, const SpanDesc& one, const SpanDesc* desc, std::uint32_t n,
@@ -187,7 +186,6 @@ struct StreamScratch {
   std::uint64_t cap_blocks = 0;
   std::uint32_t gate_seq = 0;  // irregular calls on this stream (crc_list_lanes' gate, counts[kCountGate])
   bool one_pass = false;       // the last irregular call launched crc_list_lanes
-  bool pack = false;           // ... and crc_list_pack
 };
 
 // Spans up to this size take update()'s latency path (mapped pinned memory, one crc_span launch,
@@ -381,7 +379,8 @@ int get_scratch(DevCtx* c, void* stream, std::uint64_t nblocks, StreamScratch** 
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->seams), sizeof(Seam) * 2 * c->W));
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->wave_start), sizeof(std::uint32_t) * c->W));
     // counts[0..3], then (u64) the stream-mode info at counts + 4
-    // (crc_list_lanes' per-workgroup flags from word kListFlags on, crc_list_pack's from kPackFlags)
+    // (crc_list_lanes' per-workgroup flags from word kListFlags on: general path; from kPackFlags:
+    // packed mode taken)
     TKV_HIP(hipMalloc(reinterpret_cast<void**>(&slot->counts), sizeof(std::uint32_t) * kCountWords));
     TKV_HIP(hipMemset(slot->counts, 0, sizeof(std::uint32_t) * kCountWords));
   }
@@ -566,11 +565,12 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
   a.l_len = d_len;
   a.l_tile = s->tile_ok;
   // Default registers, at least kListMinBlocks blocks: one pass of crc_list_lanes first, which folds
-  // every block when none is longer than kLaneMax bytes (WAL payload lists); the general path's launches
-  // then return at once. When it meets a longer block it flags its workgroup and crc_list_pack (below)
-  // takes the batch.
-  s->one_pass = d_init == nullptr && n >= kListMinBlocks && g_one_pass.load(std::memory_order_relaxed) != 0;
-  s->pack = false;
+  // every block when none is longer than kPackMax = 1 KiB (lane blocks one per lane, longer ones in its
+  // packed mode); the general path's launches then return at once. When it meets a longer block it flags
+  // its workgroup and the general path folds the whole batch. Not under tkv_debug_set_stream_groups(1),
+  // which keeps the byte-stream walk of back-to-back small blocks under test.
+  s->one_pass = d_init == nullptr && n >= kListMinBlocks && g_one_pass.load(std::memory_order_relaxed) != 0 &&
+                g_stream_groups.load(std::memory_order_relaxed) == 0;
   if (s->one_pass) {
     s->gate_seq = s->gate_seq + 1u == 0u ? 1u : s->gate_seq + 1u;
     a.gate = s->counts + kCountGate;
@@ -580,14 +580,6 @@ int run_irregular(DevCtx* c, int algo, const std::uint8_t* d_base, const std::ui
     l.offsets = d_off;
     l.lengths = d_len;
     TKV_HIP(launch_list_lanes(l, static_cast<unsigned>(c->ncu), st));
-    // then crc_list_pack, which folds a batch handed on whose blocks are at most kPackMax bytes; the
-    // general path runs only when it hands the batch on too (its flags open the gate). Not under
-    // tkv_debug_set_stream_groups(1), which keeps the byte-stream walk of such batches under test.
-    if (g_stream_groups.load(std::memory_order_relaxed) == 0) {
-      TKV_HIP(launch_list_pack(l, static_cast<unsigned>(c->ncu), st));
-      a.gate_flags = s->counts + kPackFlags;
-      s->pack = true;
-    }
   }
   TKV_HIP(launch_prepass(d_base, d_off, d_len, a.nblocks, s->scan, s->tiles, s->tile_ok, s->counts, sinfo, s->po.big_off,
                          s->po, a.nwaves, static_cast<std::uint32_t>(c->ncu), d_out, row0,
@@ -1409,12 +1401,12 @@ int tkv_debug_irregular_path(void* stream) {
   if (hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess ||
       hipMemcpy(f.data(), s->counts + kListFlags, 4 * f.size(), hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
-  bool list_on = false, pack_on = false;
+  bool general = false, packed = false;
   for (unsigned i = 0; i < kListMaxGroups; ++i) {
-    list_on = list_on || f[i] == s->gate_seq;
-    pack_on = pack_on || f[kListMaxGroups + i] == s->gate_seq;
+    general = general || f[i] == s->gate_seq;
+    packed = packed || f[kListMaxGroups + i] == s->gate_seq;
   }
-  return !list_on ? 0 : s->pack && !pack_on ? 1 : 2;
+  return general ? 2 : packed ? 1 : 0;
 }
 
 uint32_t tkv_debug_list_lanes_waves(uint64_t nblocks) {

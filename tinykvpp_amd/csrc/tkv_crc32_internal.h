@@ -110,20 +110,20 @@ struct RowsArgs {
   const std::uint32_t* l_len;
   const std::uint32_t* l_tile;  // per scan tile of 4096 blocks: kTileLanes when its lane blocks are ours
   // irregular batches after crc_list_lanes (nullable): the kernels of the general path run only when
-  // gate[0] == gate_seq, i.e. the one-pass lane kernel found a block it does not take
+  // gate[0] == gate_seq, i.e. the one-pass kernel found a block it does not take
   const std::uint32_t* gate;
   std::uint32_t gate_seq;
   const std::uint32_t* gate_flags;  // crc_list_lanes: per workgroup, the call's number when it met such a block
 };
 // counts[kCountGate]: the call's sequence number when the general path must run (a block over
-// kLaneMax bytes): rows_tile_scan's workgroup 0 writes it from crc_list_lanes' per-workgroup flags
+// kPackMax = 1 KiB): rows_tile_scan's workgroup 0 writes it from crc_list_lanes' per-workgroup flags
 // (counts[kListFlags + g]; one writer per address: a single word written by every wave that met such
 // a block took ~0.4 ms of same-address stores)
 constexpr int kCountGate = 12;
 constexpr int kListFlags = 64;
 constexpr unsigned kListMaxGroups = 1024;
-// counts[kPackFlags + g]: crc_list_pack's flags (the same protocol, a block over kPackMax bytes); the
-// tile scan reads these when crc_list_pack ran after crc_list_lanes
+// counts[kPackFlags + g]: the call's sequence number when a wave of crc_list_lanes' workgroup g took its
+// packed mode (blocks over kLaneMax bytes; tkv_debug_irregular_path)
 constexpr int kPackFlags = kListFlags + static_cast<int>(kListMaxGroups);
 constexpr int kCountWords = kPackFlags + static_cast<int>(kListMaxGroups);
 __device__ __forceinline__ bool gate_closed(const std::uint32_t* gate, std::uint32_t seq) {

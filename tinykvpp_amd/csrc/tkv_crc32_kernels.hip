@@ -232,25 +232,31 @@ __global__ __launch_bounds__(kThreads) void crc_lanes_lds(RowsArgs a) {
 
 __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 
-// ---- irregular batches of lane blocks in one pass -----------------------------------------------------
+// ---- irregular batches of blocks up to 1 KiB in one pass ----------------------------------------------
 // crc_list_lanes folds an irregular batch (default initial register) straight from the caller's
-// (offset, length) arrays, every block of at most kLaneMax bytes by one lane, with no prepass: the
-// general path's launches that follow it return at once unless it met a longer block (gate). Wave w
-// takes 64-block steps [w TS / W, (w + 1) TS / W). A step's blocks usually lie in a few KiB (WAL
-// payloads); then its bytes [lo, hi) are loaded by coalesced 16-byte buffer loads (a descriptor that
-// ends at hi, so nothing past the last block is read), kListRows rows per lane, kListRing steps ahead
-// in registers, written into the wave's LDS window just before the fold, and every lane folds its block
-// from the window (the WAL sweep's fold, tkv_wal_device.hip). The metadata is loaded kListRing steps
-// ahead of the data. A later step whose blocks do not fit one window, or are not in ascending order
-// from its first block, loads each block's granules per lane instead (the lane phase's loads; correct
-// for any batch); when a wave's first step does not fit, the batch goes to the general path.
-// A block over kLaneMax bytes stops the kernel: the first wave of a workgroup to meet one writes the
-// call's sequence number into the workgroup's flag, every wave polls the flags every 4 step groups and
-// leaves, and the general path then folds the whole batch (rows_tile_scan opens the gate from the
-// flags).
-// The per-workgroup flags of a one-pass kernel, polled by every wave: next() issues this lane's load of
-// flag lane + 64 g (g taking the ceil(groups / 64) groups in turn, clamped to the last flag) and returns
-// whether the load issued at the previous call found the call's number (seq is never 0).
+// (offset, length) arrays when no block is over kPackMax = 1 KiB bytes, with no prepass: the general
+// path's launches that follow it return at once unless it met a longer block (gate). Wave w takes
+// 64-block steps [w TS / W, (w + 1) TS / W), in one of two modes:
+//  * lanes (every block of the step at most kLaneMax bytes): one lane per block. A step's blocks
+//    usually lie in a few KiB (WAL payloads); then its bytes [lo, hi) are loaded by coalesced 16-byte
+//    buffer loads (a descriptor that ends at hi, so nothing past the last block is read), kListRows
+//    rows per lane, kListRing steps ahead in registers, written into the wave's LDS window just before
+//    the fold, and every lane folds its block from the window (the WAL sweep's fold,
+//    tkv_wal_device.hip). A later step whose blocks do not fit one window, or are not in ascending
+//    order from its first block, loads each block's granules per lane instead (correct for any batch).
+//  * packed (pack_walk): from the first step that holds a longer block, or that is no window when it
+//    is the wave's first, to the end of the wave's range (the steps before it are done): a block gets
+//    ceil(len / 64) lanes of a per-wave lane stream, one 64-byte piece per lane (see pack_walk).
+// A block over kPackMax bytes stops the kernel: the first wave of a workgroup to meet one writes the
+// call's sequence number into the workgroup's flag, every wave polls the flags and leaves, and the
+// general path then folds the whole batch (rows_tile_scan opens the gate from the flags). A workgroup
+// any of whose waves took the packed mode says so in a second flag array (counts[kPackFlags + g],
+// tkv_debug_irregular_path).
+// The per-workgroup flags, polled by every wave: next() issues this lane's load of flag lane + 64 g
+// (g taking the ceil(groups / 64) groups in turn, clamped to the last flag) and returns whether the
+// load issued at the previous call found the call's number (seq is never 0). (An unconditional load
+// whose value waits a step group: a conditional one, or one compared at once, made every check wait
+// for all loads in flight.)
 struct FlagPoll {
   const std::uint32_t* flags;
   std::uint32_t last, ngrp, lane, grp = 0, v = 0;
@@ -271,259 +277,53 @@ constexpr int kListRing = 3;                       // steps of data in registers
 constexpr unsigned kListThreads = 1024;
 constexpr unsigned kListWaves = kListThreads / 64;
 constexpr std::uint32_t kListSlot = 32 + kListSpan + 96;  // a window slot: slack for reads before and after
-__global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
-  constexpr std::uint32_t kTabBytes = kLdsSliceWords * 2;  // the 64 KiB 16-replica image
-  __shared__ __attribute__((aligned(16))) std::uint8_t lds[kTabBytes + kListWaves * kListSlot + 4 * (kLaneMax + 1)];
-  __shared__ std::uint32_t wg_hit_word;
-  std::uint32_t* wg_hit = &wg_hit_word;
-  if (threadIdx.x == 0) wg_hit_word = 0;  // (ordered before any use by the barrier below)
-  std::uint32_t* tab = reinterpret_cast<std::uint32_t*>(lds);
-  std::uint32_t* inj = reinterpret_cast<std::uint32_t*>(lds + kTabBytes + kListWaves * kListSlot);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    // the batch's counts as the general path's debug entry points report them when it does not run
-    // (tkv_debug_irregular_*); the prepass rewrites them when it does
-    std::uint32_t* c = const_cast<std::uint32_t*>(a.counts);
-    c[0] = c[1] = c[2] = c[3] = 0;
-    c[kCountLanes] = c[kCountPhases] = c[kCountSmall4] = c[kCountSmall8] = 0;
-  }
-  const std::uint32_t lane = threadIdx.x & 63u;
-  const std::uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const std::uint32_t wave = blockIdx.x * kListWaves + wv;
-  const std::uint64_t W = a.nwaves, n = a.nblocks;
-  const std::uint64_t TS = (n + 63u) / 64u;
-  const std::uint64_t s0 = wave * TS / W;
-  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
-  std::uint32_t* flags = const_cast<std::uint32_t*>(a.gate_flags);
-  const std::uint32_t seq = a.gate_seq;
-  // the first step's lengths before anything else: a workgroup that meets a longer block there leaves
-  // before its table fill (a batch of longer blocks costs this launch little more than its dispatch)
-  const std::uint64_t b00 = s0 * 64u + lane;
-  const std::uint32_t len00 = ns != 0 ? a.lengths[b00 < n ? b00 : n - 1u] : 0u;
-  if (__syncthreads_or(ns != 0 && b00 < n && len00 > kLaneMax ? 1 : 0) != 0) {
-    if (threadIdx.x == 0) __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  dev::fill_lds_slicing16(a.tabs, tab);
-  for (std::uint32_t i = threadIdx.x; i <= kLaneMax; i += blockDim.x) inj[i] = a.tabs->init_shift[i];
-  __syncthreads();
-  if (ns == 0) return;
-  const dev::LaneConstX kc = dev::lane_const16(lane);
-  std::uint8_t* win = lds + kTabBytes + wv * kListSlot + 32;  // the step's bytes from its granule start
-  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
-  constexpr int R = kListRing;
-  std::uint64_t m_off[R];
-  std::uint32_t m_len[R];
-  auto fetch = [&](std::uint32_t j, int k) {  // step j's descriptors
-    const std::uint64_t b = (s0 + j) * 64u + lane;
-    const std::uint64_t bc = b < n ? b : n - 1u;
-    m_off[k] = a.offsets[bc];
-    m_len[k] = a.lengths[bc];
-  };
-  uint4 d[R][kListRows];
-  std::uint32_t f_rel[R], f_len[R];  // the block's byte in the window (or its offset's low word), its length
-  std::uint32_t f_hi[R];             // gathered steps: the offset's high word
-  bool staged[R];
-  std::uint32_t quit = 0;  // wave-uniform (readfirstlane): the wave stops
-  auto issue = [&](std::uint32_t j, int k) {  // step j's bytes, from its descriptors in slot k
-    const std::uint64_t b = (s0 + j) * 64u + lane;
-    const bool live = j < ns && b < n;
-    const std::uint64_t off = m_off[k];
-    const std::uint32_t len = m_len[k];
-    const std::uint64_t lb = __ballot(live && len > kLaneMax);
-    // one store per workgroup (the first wave to meet a long block: an LDS exchange elects it)
-    if (lb != 0 && lane == 0 && atomicExch(wg_hit, 1u) == 0u)
-      __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    quit = __builtin_amdgcn_readfirstlane(quit | (lb != 0 ? 1u : 0u));
-    const std::uint64_t lo = dev::readlane64(off, 0);  // (lane 0 is live whenever any lane is)
-    const std::uint64_t al = (base + lo) & ~static_cast<std::uint64_t>(15);
-    const std::uint64_t rel = base + off - al;
-    const bool fit = !live || (off >= lo && rel + len <= kListSpan);
-    const bool all = __ballot(!fit) == 0 && __ballot(live) != 0;
-    const std::uint32_t hi = dev::wave_max(live ? static_cast<std::uint32_t>(rel < kListSpan ? rel + len : 0u) : 0u);
-    const std::uint32_t nrec = all ? ((hi + 15u) & ~15u) : 0u;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(static_cast<std::uintptr_t>(
-            static_cast<std::uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<std::uint32_t>(al))) |
-            static_cast<std::uint64_t>(static_cast<std::uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<std::uint32_t>(al >> 32)))) << 32)),
-        0, __builtin_amdgcn_readfirstlane(nrec), 0x00020000);
-#pragma unroll
-    for (int r = 0; r < kListRows; ++r) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16u * lane + 1024u * r, 0, 0);
-      d[k][r] = uint4{v[0], v[1], v[2], v[3]};
-    }
-    staged[k] = all;
-    f_rel[k] = all ? static_cast<std::uint32_t>(rel) : static_cast<std::uint32_t>(off);
-    f_hi[k] = static_cast<std::uint32_t>(off >> 32);
-    f_len[k] = live ? len : 0xFFFFFFFFu;
-  };
-  auto fold = [&](std::uint32_t j, int k) {
-    const std::uint32_t len = f_len[k];
-    const bool live = len != 0xFFFFFFFFu;
-    const std::uint32_t L = live ? len : 0u;
-    std::uint32_t crc;
-    if (staged[k]) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int r = 0; r < kListRows; ++r) *reinterpret_cast<uint4*>(win + 1024u * r + 16u * lane) = d[k][r];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      // the payload read as dwords ending on its last byte, the z bytes in front zeroed, every lane
-      // through the step's longest block with its register frozen after its own (tkv_wal_device.hip)
-      const std::uint32_t nd = (L + 3u) >> 2;
-      const std::uint32_t nmax = dev::wave_max(nd);
-      const std::uint32_t z = 4u * nd - L;
-      const std::uint32_t b0 = 32u + f_rel[k] - z;  // from the slot's start (32 bytes of slack in front)
-      const std::uint32_t* w = reinterpret_cast<const std::uint32_t*>(win - 32 + (b0 & ~3u));
-      const std::uint32_t sh = b0 & 3u;
-      std::uint32_t lo = w[1];
-      dev::Reg r{0u, 0u};
-      dev::slice4(tab, r, __builtin_amdgcn_alignbyte(lo, w[0], sh) & (~0u << (8u * z)), kc);
-      if (nd == 0u) r = dev::Reg{0u, 0u};
-      for (std::uint32_t i = 1; i < nmax; ++i) {
-        const std::uint32_t hw = w[i + 1u];
-        dev::Reg t = r;
-        dev::slice4(tab, t, __builtin_amdgcn_alignbyte(hw, lo, sh), kc);
-        if (i < nd) r = t;
-        lo = hw;
-      }
-      crc = r.value() ^ inj[L];
-    } else {
-      // a step that is not one window: each lane loads its own block's granules (lane_phase's loads)
-      const std::uintptr_t blk = base + (static_cast<std::uint64_t>(f_hi[k]) << 32 | f_rel[k]);
-      uint4 q[dev::kLaneGran];
-      dev::lane_issue<1>(blk, L, reinterpret_cast<std::uintptr_t>(a.dummy), q);
-      std::uint32_t dd[1][16], nn[1] = {L}, rr[1] = {a.init_default};
-      dev::lane_dwords<1>(q, static_cast<std::uint32_t>(blk & 15u), dd[0]);
-      dev::lane_fold<1, false>(tab, kc, dd, nn, rr);
-      crc = rr[0];
-    }
-    const std::uint64_t b = (s0 + j) * 64u + lane;
-    if (live) a.out[b] = crc ^ a.out_xor;
-  };
-  // prologue: descriptors of steps 0 .. R-1, their data, then the descriptors of steps R .. 2R-1
-#pragma unroll
-  for (int k = 0; k < R; ++k) fetch(static_cast<std::uint32_t>(k), k);
-#pragma unroll
-  for (int k = 0; k < R; ++k) {
-    issue(static_cast<std::uint32_t>(k), k);
-    fetch(static_cast<std::uint32_t>(k + R), k);
-    __builtin_amdgcn_sched_barrier(0);  // in order: the loop's waits count the loads issued after these
-  }
-  // a first step that is not one window (blocks spread out, or 64-byte blocks back to back): the batch
-  // goes to the general path, whose lane phase takes such layouts faster than per-lane granule loads
-  if (!staged[0] && quit == 0u) {
-    if (lane == 0 && atomicExch(wg_hit, 1u) == 0u)
-      __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    quit = 1u;
-  }
-  // the other workgroups' flags: one load per lane per group of steps, 64 flags at a time in turn, each
-  // looked at one group later (an unconditional load whose value waits a group: a conditional one, or
-  // one compared at once, made every check wait for all loads in flight)
-  FlagPoll poll(flags, gridDim.x, lane);
-  for (std::uint32_t t = 0; t < ns && quit == 0u; t += R) {
-    const bool hit = poll.next(seq);
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      const std::uint32_t j = t + static_cast<std::uint32_t>(k);
-      if (j >= ns || quit != 0u) break;
-      fold(j, k);
-      issue(j + R, k);
-      fetch(j + 2u * R, k);
-    }
-    // another workgroup met a long block: the general path folds the batch
-    quit = __builtin_amdgcn_readfirstlane(quit | (__ballot(hit) != 0 ? 1u : 0u));
-  }
-}
+constexpr std::uint32_t kPackMax = kSmallMax;             // 16 lanes at most per block
+// LDS (one workgroup per CU): the 64 KiB 16-replica image, the packed mode's shift tables (8 KiB:
+// word ((sh >> 1) * 8 + j) * 32 + (v | 16 (sh & 1)) = Shift_{64 sh}(v << 4 j), even shifts in the
+// lower 16 banks, odd ones in the upper, so the pieces of one block split the banks),
+// Shift_len(0xFFFFFFFF) ^ xorout for len <= kPackMax, then per wave its window slot or, in the packed
+// mode, desc[2][64] (16 B), map[2048] (u8: accumulator buffer << 6 | block), acc[4][64], acc_chunk[4]
+constexpr std::uint32_t kListLsp = kLdsSliceWords * 2;
+constexpr std::uint32_t kListInj = kListLsp + 8 * 8 * 32 * 4;
+constexpr std::uint32_t kListWaveArea = kListInj + 4 * (kPackMax + 4);
+constexpr std::uint32_t kPackDesc = 0, kPackMap = 2048, kPackAcc = 4096, kPackAccQ = 5120;
+constexpr std::uint32_t kListWaveBytes = 5136;
+static_assert(kListWaveBytes >= kListSlot && kListWaveBytes >= kPackAccQ + 16, "wave area");
+constexpr std::uint32_t kListLdsBytes = kListWaveArea + kListWaves * kListWaveBytes;
+static_assert(kListLdsBytes + 8 <= 163840, "LDS");
+static_assert(kPackFlags == kListFlags + static_cast<int>(kListMaxGroups), "pack flags follow the list flags");
 
-// ---- irregular batches of blocks up to 1 KiB in one pass ----------------------------------------------
-// crc_list_pack takes an irregular batch (default initial register) that crc_list_lanes handed on (one
-// of its workgroups met a block over kLaneMax bytes; otherwise every workgroup returns at once) and
-// folds it straight from the caller's (offset, length) arrays when no block is over kPackMax bytes: no
-// prepass, no classes. Wave w takes 64-block chunks [w TS / W, (w + 1) TS / W). A block of len bytes
+// The packed mode of crc_list_lanes over steps (chunks) [s0, s0 + ns) of a wave: a block of len bytes
 // gets k = ceil(len / 64) lanes of a per-wave lane stream: a chunk's k are scanned (DPP) into each
 // block's first lane, and its block-lanes write their descriptor and a lane -> block map into the
-// wave's LDS. Substeps take the stream 64 lanes at a time, running from one chunk into the next (never
-// further), so no substep is padded at a chunk's end: lane g of k folds the block's bytes
-// [len - 64 (k - g), len - 64 (k - g - 1)) from zero (the bytes in front of the block masked), moves the
-// result to the block's end by Shift_{64 (k - 1 - g)} (nibble tables, one column per shift), and XORs
-// it into the block's LDS accumulator, which the block-lane seeded with Shift_len(0xFFFFFFFF) ^ xorout
-// (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). After the substep that holds a chunk's last lane, its
-// accumulators are the block CRCs. Against the 4-lane groups of the general path, a substep fills its
-// 64 lanes with pieces whatever the length mix (a 128-byte block takes two lanes, not four, a 40-byte
-// one one) and nothing is read twice: descriptors once, payload granules once per piece (5 granules for
-// 64 bytes), no scan, scatter or class lists. A chunk with no lane (every block empty) is written when
-// it is prepared.
+// wave's LDS area. Substeps take the stream 64 lanes at a time, running from one chunk into the next
+// (never further), so no substep is padded at a chunk's end: lane g of k folds the block's bytes
+// [len - 64 (k - g), len - 64 (k - g - 1)) from zero (the bytes in front of the block masked: leading
+// zeros leave an init-0 register at 0), moves the result to the block's end by Shift_{64 (k - 1 - g)}
+// (nibble tables, one column per shift), and XORs it into the block's LDS accumulator, which the
+// block-lane seeded with Shift_len(0xFFFFFFFF) ^ xorout (crc_s(D) = Shift_|D|(s) ^ crc_0(D)). After the
+// substep that holds a chunk's last lane, its accumulators are the block CRCs. Against the 4-lane
+// groups of the general path, a substep fills its 64 lanes with pieces whatever the length mix (a
+// 128-byte block takes two lanes, not four, a 40-byte one one) and nothing is read twice:
+// descriptors once, payload granules once per piece (5 granules for 64 bytes). A chunk with no lane
+// (every block empty) is written when it is prepared.
 // Pipeline: a substep's granules are issued one substep before its fold; a chunk is prepared (map,
 // descriptors, accumulator seeds) when the stream first needs it as the chunk after the current one,
 // its descriptors loaded two chunks earlier. Two descriptor buffers and a 2048-entry map ring (two
 // chunks: at most 2 x 16 x 64 lanes), four accumulator buffers: a chunk's seeds never meet an unfolded
 // substep of the chunk four before it (each substep spans two chunks at most).
-// A block over kPackMax bytes, as in crc_list_lanes: the workgroup stores the call's number in its own
-// flag (counts[kPackFlags + g]), every wave polls the flags and leaves, and the general path (whose
-// tile scan reads these flags) folds the batch.
-constexpr std::uint32_t kPackMax = kSmallMax;         // 16 lanes at most per block
-constexpr unsigned kPackThreads = 1024;
-constexpr unsigned kPackWaves = kPackThreads / 64;
-constexpr std::uint32_t kPackLsp = kLdsSliceWords * 2;  // after the 64 KiB image: shift tables
-constexpr std::uint32_t kPackInj = kPackLsp + 8 * 8 * 32 * 4;  // [8 shift pairs][8 nibbles][32] words
-constexpr std::uint32_t kPackScratch = kPackInj + 4 * (kPackMax + 4);  // Shift_len(init) ^ xorout
-// per wave: desc[2][64] (16 B), map[2048] (u8: acc buffer << 6 | block), acc[4][64], acc_chunk[4]
-constexpr std::uint32_t kPackDesc = 0, kPackMap = 2048, kPackAcc = 4096, kPackAccQ = 5120;
-constexpr std::uint32_t kPackWaveBytes = 5136;
-constexpr std::uint32_t kPackLdsBytes = kPackScratch + kPackWaves * kPackWaveBytes;
-static_assert(kPackLdsBytes + 4 <= 163840, "LDS");
-static_assert(kPackFlags == kListFlags + static_cast<int>(kListMaxGroups), "pack flags follow the list flags");
-
-__global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
-  __shared__ __attribute__((aligned(16))) std::uint8_t lds[kPackLdsBytes];
-  __shared__ std::uint32_t wg_hit_word;
+__device__ __forceinline__ void pack_walk(const RowsArgs& a, std::uint8_t* lds, std::uint8_t* ws, std::uint64_t s0,
+                                          std::uint32_t ns, std::uint32_t lane, const dev::LaneConstX& kc,
+                                          FlagPoll& poll, std::uint32_t* wg_hit) {
+  const std::uint64_t n = a.nblocks;
   const std::uint32_t seq = a.gate_seq;
-  std::uint32_t* pflags = const_cast<std::uint32_t*>(a.gate_flags) + kListMaxGroups;
-  {
-    // crc_list_lanes (the launch before, same stream) folded the batch unless one of its flags holds seq
-    bool hit = false;
-    for (std::uint32_t i = threadIdx.x; i < kListMaxGroups; i += blockDim.x) hit = hit || a.gate_flags[i] == seq;
-    if (__syncthreads_or(hit ? 1 : 0) == 0) return;
-  }
-  const std::uint32_t lane = threadIdx.x & 63u;
-  const std::uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const std::uint32_t wave = blockIdx.x * kPackWaves + wv;
-  const std::uint64_t W = a.nwaves, n = a.nblocks;
-  const std::uint64_t TS = (n + 63u) / 64u;
-  const std::uint64_t s0 = wave * TS / W;
-  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
-  {
-    // the first chunk's lengths before the table fill: a workgroup that meets a longer block leaves
-    const std::uint64_t b = s0 * 64u + lane;
-    const std::uint32_t len = ns != 0 ? a.lengths[b < n ? b : n - 1u] : 0u;
-    if (__syncthreads_or(ns != 0 && b < n && len > kPackMax ? 1 : 0) != 0) {
-      if (threadIdx.x == 0) __hip_atomic_store(pflags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-  }
-  std::uint32_t* tab = reinterpret_cast<std::uint32_t*>(lds);
-  dev::fill_lds_slicing16(a.tabs, tab);
-  // shift tables: word ((sh >> 1) * 8 + j) * 32 + (v | 16 (sh & 1)) = Shift_{64 sh}(v << 4 j) (lane_shift
-  // column 63 - sh): even shifts in the lower 16 banks, odd ones in the upper, so the pieces of one
-  // block (consecutive sh) split the banks
-  std::uint32_t* lsp = reinterpret_cast<std::uint32_t*>(lds + kPackLsp);
-  for (std::uint32_t i = threadIdx.x; i < 8u * 8u * 32u; i += blockDim.x) {
-    const std::uint32_t sh = ((i >> 8) << 1) | ((i >> 4) & 1u), j = (i >> 5) & 7u;
-    lsp[i] = a.tabs->lane_shift[j][i & 15u][63u - sh];
-  }
-  std::uint32_t* inj = reinterpret_cast<std::uint32_t*>(lds + kPackInj);
-  for (std::uint32_t i = threadIdx.x; i <= kPackMax; i += blockDim.x) inj[i] = a.tabs->init_shift[i] ^ a.out_xor;
-  if (threadIdx.x == 0) wg_hit_word = 0;
-  __syncthreads();
-  if (ns == 0) return;
-
-  std::uint8_t* ws = lds + kPackScratch + wv * kPackWaveBytes;
+  std::uint32_t* flags = const_cast<std::uint32_t*>(a.gate_flags);
+  const std::uint32_t* tab = reinterpret_cast<const std::uint32_t*>(lds);
+  const std::uint32_t* inj = reinterpret_cast<const std::uint32_t*>(lds + kListInj);
   uint4* desc = reinterpret_cast<uint4*>(ws + kPackDesc);
   std::uint8_t* map = ws + kPackMap;
   std::uint32_t* acc = reinterpret_cast<std::uint32_t*>(ws + kPackAcc);
   std::uint32_t* accq = reinterpret_cast<std::uint32_t*>(ws + kPackAccQ);
-  const dev::LaneConstX kc = dev::lane_const16(lane);
   const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
   const std::uintptr_t dmy = reinterpret_cast<std::uintptr_t>(a.dummy);
 
@@ -543,14 +343,13 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
   // holding s) and of the prepared chunk after it, B (eb == ea: none); their accumulator buffers sa, sb
   std::uint32_t s = 0, ea = 0, eb = 0, sa = 0, sb = 0;
   std::uint32_t iq = 0, np = 0, quit = 0;  // next chunk to look at, chunks prepared
-  FlagPoll poll(pflags, gridDim.x, lane);  // other workgroups' flags, one load per chunk
   auto wave_fence = [] {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
   };
   auto leave = [&] {
-    if (lane == 0 && atomicExch(&wg_hit_word, 1u) == 0u)
-      __hip_atomic_store(pflags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0 && atomicExch(wg_hit, 1u) == 0u)
+      __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     quit = 1u;
   };
   // prepares the next chunk with lanes as B, its lanes from eb on; false when none is left (or on quit)
@@ -656,7 +455,7 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
     for (int k = 0; k < 16; ++k) dev::slice4(tab, reg, dev::mask_front(d[k], lead8, k), kc);
     const std::uint32_t p = reg.value();
     const std::uint32_t sh = m_sh[r];
-    const std::uint32_t lb = kPackLsp + (sh >> 1) * 1024u + ((sh & 1u) << 6);
+    const std::uint32_t lb = kListLsp + (sh >> 1) * 1024u + ((sh & 1u) << 6);
     std::uint32_t l[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) l[j] = dev::lds_at(tab, lb + 128u * j + (((p >> (4 * j)) & 15u) << 2));
@@ -681,6 +480,184 @@ __global__ __launch_bounds__(kPackThreads) void crc_list_pack(RowsArgs a) {
       fold(k);
     }
   }
+}
+
+__global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
+  __shared__ __attribute__((aligned(16))) std::uint8_t lds[kListLdsBytes];
+  __shared__ std::uint32_t wg_words[2];  // this workgroup flagged the batch / took the packed mode
+  std::uint32_t* wg_hit = &wg_words[0];
+  if (threadIdx.x == 0) wg_words[0] = wg_words[1] = 0;  // (ordered before any use by the barrier below)
+  std::uint32_t* tab = reinterpret_cast<std::uint32_t*>(lds);
+  std::uint32_t* inj = reinterpret_cast<std::uint32_t*>(lds + kListInj);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // the batch's counts as the general path's debug entry points report them when it does not run
+    // (tkv_debug_irregular_*); the prepass rewrites them when it does
+    std::uint32_t* c = const_cast<std::uint32_t*>(a.counts);
+    c[0] = c[1] = c[2] = c[3] = 0;
+    c[kCountLanes] = c[kCountPhases] = c[kCountSmall4] = c[kCountSmall8] = 0;
+  }
+  const std::uint32_t lane = threadIdx.x & 63u;
+  const std::uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const std::uint32_t wave = blockIdx.x * kListWaves + wv;
+  const std::uint64_t W = a.nwaves, n = a.nblocks;
+  const std::uint64_t TS = (n + 63u) / 64u;
+  const std::uint64_t s0 = wave * TS / W;
+  const std::uint32_t ns = static_cast<std::uint32_t>((wave + 1) * TS / W - s0);
+  std::uint32_t* flags = const_cast<std::uint32_t*>(a.gate_flags);
+  const std::uint32_t seq = a.gate_seq;
+  // the first step's lengths before anything else: a workgroup that meets a block over kPackMax there
+  // leaves before its table fill (a batch of long blocks costs this launch little more than its dispatch)
+  const std::uint64_t b00 = s0 * 64u + lane;
+  const std::uint32_t len00 = ns != 0 ? a.lengths[b00 < n ? b00 : n - 1u] : 0u;
+  // a wave whose first step holds a longer block starts in the packed mode (no lane-mode prologue)
+  const bool long0 = __ballot(ns != 0 && b00 < n && len00 > kLaneMax) != 0;
+  if (__syncthreads_or(ns != 0 && b00 < n && len00 > kPackMax ? 1 : 0) != 0) {
+    if (threadIdx.x == 0) __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  dev::fill_lds_slicing16(a.tabs, tab);
+  std::uint32_t* lsp = reinterpret_cast<std::uint32_t*>(lds + kListLsp);
+  for (std::uint32_t i = threadIdx.x; i < 8u * 8u * 32u; i += blockDim.x) {
+    const std::uint32_t sh = ((i >> 8) << 1) | ((i >> 4) & 1u), j = (i >> 5) & 7u;
+    lsp[i] = a.tabs->lane_shift[j][i & 15u][63u - sh];
+  }
+  for (std::uint32_t i = threadIdx.x; i <= kPackMax; i += blockDim.x) inj[i] = a.tabs->init_shift[i] ^ a.out_xor;
+  __syncthreads();
+  if (ns == 0) return;
+  const dev::LaneConstX kc = dev::lane_const16(lane);
+  std::uint8_t* ws = lds + kListWaveArea + wv * kListWaveBytes;
+  std::uint8_t* win = ws + 32;  // the step's bytes from its granule start
+  const std::uintptr_t base = reinterpret_cast<std::uintptr_t>(a.base);
+  constexpr int R = kListRing;
+  std::uint64_t m_off[R];
+  std::uint32_t m_len[R];
+  auto fetch = [&](std::uint32_t j, int k) {  // step j's descriptors
+    const std::uint64_t b = (s0 + j) * 64u + lane;
+    const std::uint64_t bc = b < n ? b : n - 1u;
+    m_off[k] = a.offsets[bc];
+    m_len[k] = a.lengths[bc];
+  };
+  uint4 d[R][kListRows];
+  std::uint32_t f_rel[R], f_len[R];  // the block's byte in the window (or its offset's low word), its length
+  std::uint32_t f_hi[R];             // gathered steps: the offset's high word
+  bool staged[R];
+  std::uint32_t quit = 0;           // wave-uniform (readfirstlane): the wave stops
+  std::uint32_t sw = long0 ? 0 : ns;  // wave-uniform: the first step of the packed mode (ns: none)
+  auto issue = [&](std::uint32_t j, int k) {  // step j's bytes, from its descriptors in slot k
+    const std::uint64_t b = (s0 + j) * 64u + lane;
+    const bool live = j < ns && b < n;
+    const std::uint64_t off = m_off[k];
+    const std::uint32_t len = m_len[k];
+    const std::uint64_t lb = __ballot(live && len > kPackMax);
+    // one store per workgroup (the first wave to meet a block over kPackMax: an LDS exchange elects it)
+    if (lb != 0 && lane == 0 && atomicExch(wg_hit, 1u) == 0u)
+      __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    quit = __builtin_amdgcn_readfirstlane(quit | (lb != 0 ? 1u : 0u));
+    if (__ballot(live && len > kLaneMax) != 0 && j < sw) sw = j;  // the packed mode from here
+    const std::uint64_t lo = dev::readlane64(off, 0);  // (lane 0 is live whenever any lane is)
+    const std::uint64_t al = (base + lo) & ~static_cast<std::uint64_t>(15);
+    const std::uint64_t rel = base + off - al;
+    const bool fit = !live || (off >= lo && rel + len <= kListSpan);
+    // (a step of the packed mode loads nothing here: a descriptor of 0 records reads no memory)
+    const bool all = __ballot(!fit) == 0 && __ballot(live) != 0 && j < sw;
+    const std::uint32_t hi = dev::wave_max(live ? static_cast<std::uint32_t>(rel < kListSpan ? rel + len : 0u) : 0u);
+    const std::uint32_t nrec = all ? ((hi + 15u) & ~15u) : 0u;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(static_cast<std::uintptr_t>(
+            static_cast<std::uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<std::uint32_t>(al))) |
+            static_cast<std::uint64_t>(static_cast<std::uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<std::uint32_t>(al >> 32)))) << 32)),
+        0, __builtin_amdgcn_readfirstlane(nrec), 0x00020000);
+#pragma unroll
+    for (int r = 0; r < kListRows; ++r) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16u * lane + 1024u * r, 0, 0);
+      d[k][r] = uint4{v[0], v[1], v[2], v[3]};
+    }
+    staged[k] = all;
+    f_rel[k] = all ? static_cast<std::uint32_t>(rel) : static_cast<std::uint32_t>(off);
+    f_hi[k] = static_cast<std::uint32_t>(off >> 32);
+    f_len[k] = live ? len : 0xFFFFFFFFu;
+  };
+  auto fold = [&](std::uint32_t j, int k) {
+    const std::uint32_t len = f_len[k];
+    const bool live = len != 0xFFFFFFFFu;
+    const std::uint32_t L = live ? len : 0u;
+    std::uint32_t crc;
+    if (staged[k]) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < kListRows; ++r) *reinterpret_cast<uint4*>(win + 1024u * r + 16u * lane) = d[k][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // the payload read as dwords ending on its last byte, the z bytes in front zeroed, every lane
+      // through the step's longest block with its register frozen after its own (tkv_wal_device.hip)
+      const std::uint32_t nd = (L + 3u) >> 2;
+      const std::uint32_t nmax = dev::wave_max(nd);
+      const std::uint32_t z = 4u * nd - L;
+      const std::uint32_t b0 = 32u + f_rel[k] - z;  // from the slot's start (32 bytes of slack in front)
+      const std::uint32_t* w = reinterpret_cast<const std::uint32_t*>(win - 32 + (b0 & ~3u));
+      const std::uint32_t sh = b0 & 3u;
+      std::uint32_t lo = w[1];
+      dev::Reg r{0u, 0u};
+      dev::slice4(tab, r, __builtin_amdgcn_alignbyte(lo, w[0], sh) & (~0u << (8u * z)), kc);
+      if (nd == 0u) r = dev::Reg{0u, 0u};
+      for (std::uint32_t i = 1; i < nmax; ++i) {
+        const std::uint32_t hw = w[i + 1u];
+        dev::Reg t = r;
+        dev::slice4(tab, t, __builtin_amdgcn_alignbyte(hw, lo, sh), kc);
+        if (i < nd) r = t;
+        lo = hw;
+      }
+      crc = r.value() ^ inj[L];  // (inj holds Shift_L(0xFFFFFFFF) ^ xorout)
+    } else {
+      // a step that is not one window: each lane loads its own block's granules (lane_phase's loads)
+      const std::uintptr_t blk = base + (static_cast<std::uint64_t>(f_hi[k]) << 32 | f_rel[k]);
+      uint4 q[dev::kLaneGran];
+      dev::lane_issue<1>(blk, L, reinterpret_cast<std::uintptr_t>(a.dummy), q);
+      std::uint32_t dd[1][16], nn[1] = {L}, rr[1] = {a.init_default};
+      dev::lane_dwords<1>(q, static_cast<std::uint32_t>(blk & 15u), dd[0]);
+      dev::lane_fold<1, false>(tab, kc, dd, nn, rr);
+      crc = rr[0] ^ a.out_xor;
+    }
+    const std::uint64_t b = (s0 + j) * 64u + lane;
+    if (live) a.out[b] = crc;
+  };
+  FlagPoll poll(flags, gridDim.x, lane);
+  if (sw != 0) {
+    // prologue: descriptors of steps 0 .. R-1, their data, then the descriptors of steps R .. 2R-1
+#pragma unroll
+    for (int k = 0; k < R; ++k) fetch(static_cast<std::uint32_t>(k), k);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      issue(static_cast<std::uint32_t>(k), k);
+      fetch(static_cast<std::uint32_t>(k + R), k);
+      __builtin_amdgcn_sched_barrier(0);  // in order: the loop's waits count the loads issued after these
+    }
+    // a first step that is not one window (blocks spread out, or 64-byte blocks back to back): the
+    // packed mode, whose per-lane pieces take such layouts faster than per-lane granule loads
+    if (!staged[0]) sw = 0;
+  }
+  for (std::uint32_t t = 0; t < sw && quit == 0u; t += R) {
+    const bool hit = poll.next(seq);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const std::uint32_t j = t + static_cast<std::uint32_t>(k);
+      if (j >= sw || quit != 0u) break;
+      fold(j, k);
+      issue(j + R, k);
+      fetch(j + 2u * R, k);
+    }
+    // another workgroup met a block over kPackMax: the general path folds the batch
+    quit = __builtin_amdgcn_readfirstlane(quit | (__ballot(hit) != 0 ? 1u : 0u));
+  }
+  if (quit != 0u || sw >= ns) return;
+  // the packed mode for steps [sw, ns): its LDS area is this wave's window slot (the wave's own LDS
+  // reads of the window are done: in order); one store per workgroup says it ran
+  if (lane == 0 && atomicExch(&wg_words[1], 1u) == 0u)
+    __hip_atomic_store(flags + kListMaxGroups + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  pack_walk(a, lds, ws, s0 + sw, ns - sw, lane, kc, poll, wg_hit);
 }
 
 
@@ -1569,18 +1546,6 @@ hipError_t launch_list_lanes(const RowsArgs& a, unsigned ncu, hipStream_t st) {
   b.nwaves = list_lanes_waves(a.nblocks, ncu);
   const std::uint64_t grid = b.nwaves / kListWaves;
   hipLaunchKernelGGL(crc_list_lanes, dim3(static_cast<unsigned>(grid)), dim3(kListThreads), 0, st, b);
-  return hipGetLastError();
-}
-
-// One-pass packed kernel of an irregular batch that crc_list_lanes handed on: see crc_list_pack. Its
-// workgroups return at once when crc_list_lanes folded the batch.
-hipError_t launch_list_pack(const RowsArgs& a, unsigned ncu, hipStream_t st) {
-  RowsArgs b = a;
-  const std::uint64_t chunks = (a.nblocks + 63u) / 64u;
-  const std::uint64_t grid = std::max<std::uint64_t>(
-      1, std::min<std::uint64_t>(std::min<std::uint64_t>(ncu, kListMaxGroups), (chunks + kPackWaves - 1) / kPackWaves));
-  b.nwaves = static_cast<std::uint32_t>(grid * kPackWaves);
-  hipLaunchKernelGGL(crc_list_pack, dim3(static_cast<unsigned>(grid)), dim3(kPackThreads), 0, st, b);
   return hipGetLastError();
 }
 
