@@ -340,8 +340,8 @@ def bit_exact_paths(dev, ora, quick=False):
     wal.cpp:63-130, the WAL stamp of wal.cpp:54-58, the SSTable stamp) on seeded synthetic inputs:
       list_lanes_one_pass   >= 1 M gapped 26-59 B WAL payloads through tkv_crc32_batch_device (the
                             one-pass crc_list_lanes kernel; tkv_debug_irregular_path 0)
-      list_pack_one_pass    the same batch with one 65 B block near its end (crc_list_lanes hands it
-                            on, the one-pass crc_list_pack kernel folds it: path 1)
+      list_pack_one_pass    the same batch with one 65 B block near its end (the wave that meets it
+                            switches to crc_list_lanes' packed mode: path 1)
       list_lanes_fall_through  the same batch with one 1025 B block (the general path: path 2)
       crc32c_list_lanes     the one-pass batch under CRC-32C (sampled against the oracle)
       wal_verify_device_*   tkv_wal_verify_device on small-record, Zipf and values-made-of-records

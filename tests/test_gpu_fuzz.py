@@ -369,7 +369,7 @@ def stream_many_case(oracle, gpu, seed, group_stream):
 @pytest.mark.parametrize("seed", range(24))
 def test_one_pass_random(gpu, oracle, seed):
     """Batches of at least 256 K blocks with the default register: the one-pass kernels
-    (crc_list_lanes, crc_list_pack). Length mixes of lane blocks only, up to 256 B,
+    (crc_list_lanes and its packed mode). Length mixes of lane blocks only, up to 256 B,
     up to 1 KiB and the class edges, sometimes one block over 1 KiB (the general path then folds the
     batch); gapped, back-to-back, shuffled and overlapping layouts; base shifts; both polynomials.
     Every block against the oracle (CRC-32C sampled), and which kernel folded the batch."""
@@ -409,7 +409,7 @@ def test_one_pass_random(gpu, oracle, seed):
     elif int(lens.max()) > 64:
         assert kp == 1, (mix, layout)
     else:
-        assert kp in (0, 1), (mix, layout)  # (lane blocks whose first steps are no window go to crc_list_pack)
+        assert kp in (0, 1), (mix, layout)  # (lane blocks whose first steps are no window take the packed mode)
     if algo == "crc32c":
         smp = rng.choice(n, 4000, replace=False)
         want = oracle_batch(oracle, algo, host, offs[smp], lens[smp], None)

@@ -128,7 +128,7 @@ def test_irregular_one_pass_lanes(gpu, oracle, buf, shape):
     """crc_list_lanes, the one-pass kernel in front of the general path for irregular batches with the
     default register: steps of 64 blocks staged through an LDS window when they lie in
     4 KiB, per-lane granule loads for a later step that does not (blocks out of order, spread out),
-    crc_list_pack for the whole batch when a first step does not fit or a block is over 64 bytes (near
+    its packed mode from the step where a first step does not fit or a block is over 64 bytes (near
     the start or the end), every length 0-64, batches ending inside a step, empty blocks, blocks ending
     at the last byte of their allocation, and CRC-32C on the same kernel. Batches of at least 1 M blocks
     (the kernel's threshold) except the tiny one."""
@@ -168,8 +168,8 @@ def test_irregular_one_pass_lanes(gpu, oracle, buf, shape):
         assert np.array_equal(got[sample], oracle_c(oracle, host, offs[sample], lens[sample]))
         return
     got = u32(tk.crc32_batch(d, o, ln))
-    # which kernel folded the batch: crc_list_lanes (0), or crc_list_pack (1) after crc_list_lanes handed
-    # it on (a first step out of order, a block over 64 bytes); the general path alone below 256 K blocks (3)
+    # which path folded the batch: crc_list_lanes one lane per block (0), or with its packed mode in some
+    # wave (1: a first step out of order, a block over 64 bytes); the general path alone below 256 K blocks (3)
     want_path = {"shuffled": 1, "late_long": 1, "tiny_batch": 3}.get(shape, 0)
     assert path() == want_path, shape
     assert phases() == 0, shape
@@ -308,7 +308,7 @@ def phases():
 
 
 def path():
-    """Which kernel folded the last irregular batch: 0 crc_list_lanes, 1 crc_list_pack, 2 the general
+    """Which path folded the last irregular batch: 0 crc_list_lanes, 1 its packed mode, 2 the general
     path after both, 3 the general path alone (tkv_debug_irregular_path)."""
     return tk.load_library().tkv_debug_irregular_path(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
 

@@ -1,7 +1,8 @@
-"""GPU parity of crc_list_pack, the one-pass kernel that folds an irregular batch of
-blocks of at most 1 KiB (default initial register, at least 256 K blocks) after crc_list_lanes hands it
-on: each block gets ceil(len / 64) lanes packed back to back over 64-block chunks, every lane folds one
-64-byte piece, moves it to the block end and XORs it into the block's LDS accumulator.
+"""GPU parity of crc_list_lanes' packed mode: the one-pass kernel folds an irregular
+batch of blocks of at most 1 KiB (default initial register, at least 256 K blocks); a wave switches to
+the packed mode at its first step with a block over 64 B, where each block gets ceil(len / 64) lanes
+packed back to back over 64-block chunks, every lane folds one 64-byte piece, moves it to the block
+end and XORs it into the block's LDS accumulator.
 
 The shapes are the reference's WAL payloads with short and mid-size values (record_len = 18 + |k| +
 |v|, /root/reference/src/engine/wal.cpp:25, 8 header bytes before each payload, wal.cpp:54-58) and
@@ -103,7 +104,7 @@ def test_pack_one_pass(gpu, oracle, buf, shape):
     elif shape == "lanes_then_pack":  # crc_list_lanes folds its first waves' steps, then hands on
         lens = np.concatenate([rng.integers(0, 65, n // 2), rng.integers(0, 700, n - n // 2)])
         offs = gapped(rng, lens, 6)
-    elif shape == "spread_lanes":  # lane blocks whose first steps fit no window: crc_list_pack, one lane each
+    elif shape == "spread_lanes":  # lane blocks whose first steps fit no window: the packed mode, one lane each
         lens = rng.integers(0, 65, n)
         offs = rng.integers(0, host.size - 64, n)
     elif shape == "at_allocation_end":  # every block ends on a 1 KiB slot's last byte, the last on the tensor's
@@ -145,7 +146,7 @@ def test_pack_one_pass(gpu, oracle, buf, shape):
 
 def test_pack_paths_one_after_another(gpu, oracle, buf):
     """Batches on one stream whose verdicts alternate: lane blocks only (crc_list_lanes), blocks up to
-    1 KiB (crc_list_pack), one block over 1 KiB (the general path), and again; a stale flag of one call
+    1 KiB (the packed mode), one block over 1 KiB (the general path), and again; a stale flag of one call
     never steers the next (each call's flags carry its own sequence number)."""
     host, d = buf
     rng = np.random.default_rng(5)
