@@ -517,9 +517,10 @@ __global__ __launch_bounds__(kListThreads) void crc_list_lanes(RowsArgs a) {
   }
   dev::fill_lds_slicing16(a.tabs, tab);
   std::uint32_t* lsp = reinterpret_cast<std::uint32_t*>(lds + kListLsp);
-  for (std::uint32_t i = threadIdx.x; i < 8u * 8u * 32u; i += blockDim.x) {
-    const std::uint32_t sh = ((i >> 8) << 1) | ((i >> 4) & 1u), j = (i >> 5) & 7u;
-    lsp[i] = a.tabs->lane_shift[j][i & 15u][63u - sh];
+  for (std::uint32_t i = threadIdx.x; i < 8u * 16u * 16u; i += blockDim.x) {
+    // source order (columns 48-63 of each (j, v) row: coalesced), scattered into the shift tables
+    const std::uint32_t j = i >> 8, v = (i >> 4) & 15u, sh = 15u - (i & 15u);
+    lsp[((sh >> 1) * 8u + j) * 32u + (v | ((sh & 1u) << 4))] = a.tabs->lane_shift[j][v][63u - sh];
   }
   for (std::uint32_t i = threadIdx.x; i <= kPackMax; i += blockDim.x) inj[i] = a.tabs->init_shift[i] ^ a.out_xor;
   __syncthreads();
