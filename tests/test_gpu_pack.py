@@ -60,7 +60,7 @@ def oracle_c(oracle, host, offs, lens):
 
 SHAPES = ["wal_65_256", "wal_100_200", "mix_0_1024", "all_1024", "back_to_back_128", "shuffled", "overlapping",
           "zero_heavy", "lanes_then_pack", "spread_lanes", "late_huge", "early_huge", "mid_huge", "at_allocation_end",
-          "at_allocation_start", "crc32c"]
+          "at_allocation_start", "page_edges", "crc32c"]
 
 
 @pytest.mark.parametrize("shape", SHAPES)
@@ -110,6 +110,9 @@ def test_pack_one_pass(gpu, oracle, buf, shape):
     elif shape == "at_allocation_end":  # every block ends on a 1 KiB slot's last byte, the last on the tensor's
         lens = rng.integers(0, 1025, n)
         offs = (host.size - 1024 * 64 + 1024 * (np.arange(n) % 64) + (1024 - lens)).astype(np.int64)
+    elif shape == "page_edges":  # blocks starting 0-31 bytes into a 4 KiB page (the 16-byte-granule loads)
+        lens = rng.integers(0, 1025, n)
+        offs = 4096 * rng.integers(0, (host.size >> 12) - 1, n) + rng.integers(0, 32, n)
     elif shape == "at_allocation_start":  # every block starts a 1 KiB slot, the first at the tensor's first byte
         lens = rng.integers(0, 1025, n)
         offs = (1024 * (np.arange(n) % 64)).astype(np.int64)

@@ -394,6 +394,7 @@ __device__ __forceinline__ void pack_walk(const RowsArgs& a, std::uint8_t* lds, 
   std::int32_t m_lead[2];   // 8 x the bytes of the piece in front of the block
   std::uint32_t m_done[2];  // wave-uniform: 1 + the buffers of the chunks this substep completes, 3 bits each
   bool m_dead[2];           // wave-uniform: past the wave's last lane
+  bool m_fast[2];           // wave-uniform: dword-aligned loads (else 16-byte granules)
   auto issue = [&](int r) {
     if (quit == 0u) {
       if (s >= ea && eb > ea) {  // A is done (the last substep may have run into B): B becomes A
@@ -420,18 +421,36 @@ __device__ __forceinline__ void pack_walk(const RowsArgs& a, std::uint8_t* lds, 
     const std::int32_t c_lane = static_cast<std::int32_t>(len) - 64 * static_cast<std::int32_t>(k - g);
     const std::uintptr_t blo = base + (static_cast<std::uint64_t>(d.y) << 32 | d.x);
     const std::uintptr_t p = static_cast<std::uintptr_t>(static_cast<std::int64_t>(blo) + c_lane);
-    const std::uintptr_t al = p & ~static_cast<std::uintptr_t>(15);
-    const std::uint32_t o = static_cast<std::uint32_t>(p & 15u);
-    // granule i holds a byte of the block iff al + 16 i - blo lies in (-16, len), i.e. al + 16 i - blo +
-    // 15 in [0, len + 15) (32-bit arithmetic: -80 < al - blo < len); the others read `dummy`, so no load
-    // leaves the 16-byte granules the block touches
-    const std::int32_t rel = c_lane - static_cast<std::int32_t>(o) + 15;
+    // Four dword-aligned 16-byte loads and one dword (as the row kernel's interior rows: one
+    // v_alignbyte per dword realigns them) unless a piece in front of its block could reach into the
+    // page before the block's first byte (the block starts within 16 bytes of a page): then the wave
+    // takes the 16-byte granules the block touches (realigned by two selects and a v_alignbyte).
+    const bool fast = __ballot(live && c_lane < 0 && (blo & 4095u) < 16u) == 0;
+    m_fast[r] = fast;
+    if (fast) {
+      const std::uintptr_t pd = p & ~static_cast<std::uintptr_t>(3);
+      const std::uint32_t o3 = static_cast<std::uint32_t>(p & 3u);
+      // load i covers [pd + 16 i, + 16), never past the piece's end (at most the block's): it holds a
+      // byte of the block iff pd + 16 i + 16 > blo; the dword at pd + 64 holds the piece's last o3 bytes
+      const std::int32_t rel = c_lane - static_cast<std::int32_t>(o3) + 16;
 #pragma unroll
-    for (int i = 0; i < dev::kLaneGran; ++i) {
-      const bool in = live && static_cast<std::uint32_t>(rel + 16 * i) < len + 15u;
-      qv[r][i] = dev::gload16(in ? al + 16u * i : dmy);
+      for (int i = 0; i < 4; ++i) qv[r][i] = dev::gload16(live && rel + 16 * i > 0 ? pd + 16u * i : dmy);
+      qv[r][4] = make_uint4(*reinterpret_cast<dev::g_u32*>(live && o3 != 0u ? pd + 64u : dmy), 0u, 0u, 0u);
+      m_o[r] = o3;
+    } else {
+      const std::uintptr_t al = p & ~static_cast<std::uintptr_t>(15);
+      const std::uint32_t o = static_cast<std::uint32_t>(p & 15u);
+      // granule i holds a byte of the block iff al + 16 i - blo lies in (-16, len), i.e. al + 16 i - blo
+      // + 15 in [0, len + 15) (32-bit arithmetic: -80 < al - blo < len); the others read `dummy`, so no
+      // load leaves the 16-byte granules the block touches
+      const std::int32_t rel = c_lane - static_cast<std::int32_t>(o) + 15;
+#pragma unroll
+      for (int i = 0; i < dev::kLaneGran; ++i) {
+        const bool in = live && static_cast<std::uint32_t>(rel + 16 * i) < len + 15u;
+        qv[r][i] = dev::gload16(in ? al + 16u * i : dmy);
+      }
+      m_o[r] = o;
     }
-    m_o[r] = o;
     m_lead[r] = live ? (c_lane < 0 ? -8 * c_lane : 0) : 512;  // bits in front of the block (512: all)
     m_sh[r] = live ? k - 1u - g : 0u;
     m_acc[r] = live ? bslot * 64u + blk : ~0u;
@@ -448,7 +467,15 @@ __device__ __forceinline__ void pack_walk(const RowsArgs& a, std::uint8_t* lds, 
   };
   auto fold = [&](int r) {
     std::uint32_t d[16];
-    dev::lane_dwords<1>(qv[r], m_o[r], d);
+    if (m_fast[r]) {
+      const std::uint32_t raw[17] = {qv[r][0].x, qv[r][0].y, qv[r][0].z, qv[r][0].w, qv[r][1].x, qv[r][1].y,
+                                     qv[r][1].z, qv[r][1].w, qv[r][2].x, qv[r][2].y, qv[r][2].z, qv[r][2].w,
+                                     qv[r][3].x, qv[r][3].y, qv[r][3].z, qv[r][3].w, qv[r][4].x};
+#pragma unroll
+      for (int k = 0; k < 16; ++k) d[k] = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], m_o[r]);
+    } else {
+      dev::lane_dwords<1>(qv[r], m_o[r], d);
+    }
     const std::uint32_t lead8 = static_cast<std::uint32_t>(m_lead[r]);
     dev::Reg reg{0u, 0u};
 #pragma unroll
