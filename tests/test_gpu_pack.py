@@ -201,3 +201,27 @@ def test_pack_threshold(gpu, oracle, buf, n, want_path):
         assert path() == 3
     finally:
         lib.tkv_debug_set_one_pass(prev)
+
+
+@pytest.mark.parametrize("mix", ["lanes", "packed"])
+def test_one_pass_offsets_past_4_gib(gpu, oracle, mix):
+    """Block offsets on both sides of 4 GiB (u64 offsets; 32-bit arithmetic only relative to a block):
+    gapped WAL payloads of 26-59 B (lane mode) or 0-1024 B (packed mode) running across byte 2^32 of a
+    4.5 GiB device buffer. Only the bytes the blocks touch are written; the oracle sees the same bytes
+    at offsets relative to that window."""
+    rng = np.random.default_rng(4 << 30 if mix == "lanes" else 5 << 30)
+    n = 600_000 if mix == "lanes" else 300_000
+    lens = (rng.integers(26, 60, n) if mix == "lanes" else rng.integers(0, 1025, n)).astype(np.int64)
+    rel = np.concatenate([[0], np.cumsum(lens[:-1] + 8)])
+    span = int(rel[-1] + lens[-1])
+    lo = (1 << 32) - span // 2 - 8  # the window straddles 2^32
+    host = rng.integers(0, 256, span + 64, dtype=np.uint8)
+    d = torch.empty((9 << 29), dtype=torch.uint8, device=gpu)  # 4.5 GiB
+    d[lo:lo + host.size] = torch.from_numpy(host).to(gpu)
+    offs = (lo + rel).astype(np.int64)
+    got = u32(tk.crc32_batch(d, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu)))
+    assert path() == (0 if mix == "lanes" else 1)
+    want = oracle.batch(host, rel, lens.astype(np.int32))
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, (mix, bad.size, bad[:5], offs[bad[:5]])
+    del d
