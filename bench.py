@@ -490,6 +490,66 @@ def bit_exact_paths(dev, ora, quick=False):
     return res
 
 
+def wal_payload_batches(dev, ora, quick=False):
+    """Irregular batches of WAL payloads through tkv_crc32_batch_device (the reference's records are
+    record_len = 18 + |k| + |v| bytes, wal.cpp:25, each payload 8 header bytes after the previous one,
+    wal.cpp:54-58): the one-pass kernel's lane and packed modes. 1 GiB of payload
+    per batch (32 MiB with quick) in a random device buffer, 5 untimed then 20 timed launches between
+    one event pair on the launch stream; GB/s of payload; which path folded the batch
+    (tkv_debug_irregular_path: 0 lanes, 1 packed); 20 000 sampled blocks against the oracle. Never
+    `value`."""
+    import torch
+    import tinykvpp_amd as tk
+    lib = tk.load_library()
+    st = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    ora.oracle_crc_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p]
+    rng = np.random.default_rng(2606)
+    target = (32 << 20) if quick else (1 << 30)
+    data = torch.randint(0, 256, (target * 2 + 4096,), dtype=torch.uint8, device=dev)
+    host = data.cpu().numpy()
+    wal = np.array([26, 28, 33, 36, 59])
+    shapes = (("36 B", 36, lambda n: np.full(n, 36)),
+              ("26-59 B", 36, lambda n: rng.choice(wal, n)),
+              ("26-59 B + 2 % of 65-400 B", 40,
+               lambda n: np.where(rng.random(n) < 0.02, rng.integers(65, 401, n), rng.choice(wal, n))),
+              ("65-256 B", 160, lambda n: rng.integers(65, 257, n)),
+              ("180-400 B", 290, lambda n: rng.integers(180, 401, n)),
+              ("300-1000 B", 650, lambda n: rng.integers(300, 1001, n)))
+    res = {"source": "8-byte gaps (WAL headers), 5 untimed + 20 timed launches, GB/s of payload"}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for name, mean, draw in shapes:
+        n = target // (mean + 8)
+        lens = draw(n).astype(np.int64)
+        offs = 8 + np.concatenate([[0], np.cumsum(lens[:-1] + 8)])
+        o = torch.from_numpy(offs).to(dev)
+        ln = torch.from_numpy(lens.astype(np.int32)).to(dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        args = (ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(o.data_ptr()), ctypes.c_void_p(ln.data_ptr()), None,
+                ctypes.c_void_p(out.data_ptr()), n, sp)
+        for _ in range(5):
+            assert lib.tkv_crc32_batch_device(*args) == 0
+        e0.record(st)
+        for _ in range(20):
+            lib.tkv_crc32_batch_device(*args)
+        e1.record(st)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 20
+        kp = lib.tkv_debug_irregular_path(sp)
+        got = out.cpu().numpy().view(np.uint32)
+        smp = np.sort(rng.choice(n, min(n, 20_000), replace=False))
+        so, sl = offs[smp].astype(np.uint64), lens[smp].astype(np.uint32)
+        want = np.zeros(smp.size, np.uint32)
+        ora.oracle_crc_batch(host.ctypes.data, so.ctypes.data, sl.ctypes.data, None, smp.size, want.ctypes.data)
+        res[name] = {"blocks": int(n), "payload_bytes": int(lens.sum()), "ms": round(ms, 4),
+                     "GB_per_s": round(int(lens.sum()) / ms / 1e6, 1), "kernel_path": int(kp),
+                     "bit_exact_sampled": bool(np.array_equal(got[smp], want))}
+        del o, ln, out
+    del data
+    torch.cuda.empty_cache()
+    return res
+
+
 def build_identity():
     """The build id baked into the loaded library against the hash of this tree's sources."""
     from tinykvpp_amd import build_id
@@ -517,6 +577,8 @@ def main():
                     help="cfg2: skip timing cfg3, cfg4 and cfg5 (N=1) or cfg5 (N>1) in the same run (more_configs)")
     ap.add_argument("--no-paths", action="store_true",
                     help="skip the post-timing parity checks of the other paths (bit_exact_paths)")
+    ap.add_argument("--no-wal-payloads", action="store_true",
+                    help="skip the irregular WAL-payload batches (wal_payload_batches; N=1 only)")
     ap.add_argument("--traffic-csv", default=None,
                     help="rocprofv3 --pmc counter_collection.csv (FETCH_SIZE) of this command, for roofline.traffic")
     args = ap.parse_args()
@@ -683,6 +745,9 @@ def main():
             del c, o
             torch.cuda.empty_cache()
         line["more_configs"] = more
+    if world == 1 and args.config == "cfg2" and not args.no_wal_payloads:
+        torch.cuda.empty_cache()
+        line["wal_payload_batches"] = wal_payload_batches(dev, ora)
     if not args.no_paths:
         # after every timed region: parity of the paths the timed batches never reach (every rank checks
         # on its own GPU; the line carries rank 0's details and the AND over ranks)

@@ -48,6 +48,11 @@ def test_bench_one_rank_over_rccl(gpu):
     assert line["n_gpus"] == 1 and line["ranks_seen"] == 1
     assert line["bit_exact"] is True
     assert line["bit_exact_scope"].startswith("every block of every rank's shard")
+    # the WAL-payload batches: lane mode for lane blocks only, the packed mode once longer values appear
+    w = line["wal_payload_batches"]
+    for name, want in (("36 B", 0), ("26-59 B", 0), ("26-59 B + 2 % of 65-400 B", 1), ("65-256 B", 1),
+                       ("180-400 B", 1), ("300-1000 B", 1)):
+        assert w[name]["bit_exact_sampled"] is True and w[name]["kernel_path"] == want, (name, w[name])
 
 
 @pytest.mark.gpu

@@ -10,7 +10,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-evidence}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --no-pipelined --no-more-configs --no-paths --no-cpu-baseline --no-e2e"
+B="$R/bench.py --no-pipelined --no-more-configs --no-paths --no-cpu-baseline --no-e2e --no-wal-payloads"
 for C in cfg2 cfg4; do
   timeout -k 10 -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/trace_$C -o run --output-format csv -- python3 $B --config $C > $O/trace_$C.log 2>&1
   rc=$?; echo "trace $C rc=$rc"; if [ $rc -ne 0 ]; then tail -5 $O/trace_$C.log; exit $rc; fi
