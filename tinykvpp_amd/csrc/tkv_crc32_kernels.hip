@@ -234,7 +234,7 @@ __global__ void crc_fixup(RowsArgs a) { dev::crc_fixup_body(a); }
 
 // ---- irregular batches of blocks up to 1 KiB in one pass ----------------------------------------------
 // crc_list_lanes folds an irregular batch (default initial register) straight from the caller's
-// (offset, length) arrays when no block is over kPackMax = 1 KiB bytes, with no prepass: the general
+// (offset, length) arrays when no block is over kPackMax = 1 KiB, with no prepass: the general
 // path's launches that follow it return at once unless it met a longer block (gate). Wave w takes
 // 64-block steps [w TS / W, (w + 1) TS / W), in one of two modes:
 //  * lanes (every block of the step at most kLaneMax bytes): one lane per block. A step's blocks
