@@ -368,7 +368,7 @@ def stream_many_case(oracle, gpu, seed, group_stream):
 
 @pytest.mark.parametrize("seed", range(24))
 def test_one_pass_random(gpu, oracle, seed):
-    """Batches of at least 256 K blocks with the default register: the one-pass kernels
+    """Batches of at least 256 K blocks with the default register: the one-pass kernel
     (crc_list_lanes and its packed mode). Length mixes of lane blocks only, up to 256 B,
     up to 1 KiB and the class edges, sometimes one block over 1 KiB (the general path then folds the
     batch); gapped, back-to-back, shuffled and overlapping layouts; base shifts; both polynomials.

@@ -134,7 +134,7 @@ def test_irregular_one_pass_lanes(gpu, oracle, buf, shape):
     (the kernel's threshold) except the tiny one."""
     host, d = buf
     rng = np.random.default_rng(sum(map(ord, shape)))
-    offs, lens = wal_payloads(rng, 1_100_003, tuple(range(0, 65)), 3)  # (>= 1 M blocks: the one-pass kernel runs)
+    offs, lens = wal_payloads(rng, 1_100_003, tuple(range(0, 65)), 3)  # (>= 256 K blocks: the one-pass kernel runs)
     # the kernel's 64-block steps that start no wave's range (a wave whose first step does not fit one
     # window sends the whole batch to the general path), from the kernel's own wave count
     ts = (offs.size + 63) // 64
@@ -284,7 +284,7 @@ def test_irregular_more_than_1024_tiles(gpu, oracle, shape, tiles):
     ln = torch.from_numpy(lens).to(gpu)
     lib = tk.load_library()
     prev = lib.tkv_debug_set_stream_groups(1 if shape == "back_to_back_128_stream" else 0)
-    prev_one = lib.tkv_debug_set_one_pass(0)  # the general path's prepass at these sizes, not the one-pass kernels
+    prev_one = lib.tkv_debug_set_one_pass(0)  # the general path's prepass at these sizes, not the one-pass kernel
     try:
         assert np.array_equal(u32(tk.crc32_batch(d, o, ln)), oracle.batch(host, offs, lens))
         got_mode = mode()

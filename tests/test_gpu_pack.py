@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-N = 1_100_003  # >= 256 K blocks (the one-pass kernels' threshold), not a multiple of 64
+N = 1_100_003  # >= 256 K blocks (the one-pass kernel's threshold), not a multiple of 64
 
 
 def u32(t):
@@ -168,7 +168,7 @@ def test_pack_paths_one_after_another(gpu, oracle, buf):
 
 
 def test_pack_not_with_per_block_registers(gpu, oracle, buf):
-    """Per-block initial registers keep the general path (the one-pass kernels fold from the default
+    """Per-block initial registers keep the general path (the one-pass kernel folds from the default
     register only): same results as the oracle, path 3."""
     host, d = buf
     rng = np.random.default_rng(9)
@@ -183,7 +183,7 @@ def test_pack_not_with_per_block_registers(gpu, oracle, buf):
 
 @pytest.mark.parametrize("n,want_path", [(262_144, 1), (262_143, 3)])
 def test_pack_threshold(gpu, oracle, buf, n, want_path):
-    """The one-pass kernels take batches of at least 256 K blocks (kListMinBlocks); one block fewer
+    """The one-pass kernel takes batches of at least 256 K blocks (kListMinBlocks); one block fewer
     takes the general path alone. Same results either way; tkv_debug_set_one_pass(0) sends the larger
     batch to the general path too."""
     host, d = buf
